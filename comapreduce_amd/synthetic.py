@@ -1,0 +1,214 @@
+"""Deterministic synthetic COMAP Level-1 observations (host, NumPy).
+
+Implements the input spec of SURVEY.md §8(d): f32 spectrometer TOD of shape
+[feed, 4 sidebands, 1024 channels, T] at 50 Hz with a vane event on [500, 1500),
+Lissajous scans of >= 14,000 samples separated by 1,000-sample gaps, an airmass
+atmosphere 8 K (A - 1.4), a common 1/f gain drift and radiometer white noise.
+
+Every feed is drawn from ``np.random.default_rng(SeedSequence([obs_id, feed]))``
+so a feed's data do not depend on which other feeds are generated (sharding
+does not change the data).  The Level-1 layout mirrors what
+``COMAPLevel1`` reads (reference ``comancpipeline/Analysis/DataHandling.py``):
+
+* ``spectrometer/tod``            f32 [F, 4, 1024, T]
+* ``spectrometer/band_average``   f32 [F, 4, T]   (channel nanmean)
+* ``spectrometer/features``       f64 [T]         (2**bit, 0 = none)
+* ``spectrometer/MJD``            f64 [T]
+* ``spectrometer/feeds``          i64 [F]
+* ``spectrometer/bands``/``frequency``  f64 [4, 1024]
+* ``spectrometer/pixel_pointing/pixel_{ra,dec,az,el}`` f64 [F, T]
+* ``hk/antenna0/deTracker/{lissajous_status,utc}``
+* ``hk/antenna0/vane/Tvane``
+* attrs ``comap`` : obsid, source, comment
+
+This module is data generation only; the reduction itself lives in the HIP
+kernels (``comapreduce_amd/csrc``).
+"""
+from __future__ import annotations
+
+import hashlib
+from dataclasses import dataclass
+
+import numpy as np
+
+SAMPLE_RATE = 50.0
+N_BANDS = 4
+N_CHANNELS = 1024
+VANE_START, VANE_END = 500, 1500
+HOT_START, HOT_END = 600, 1000
+RAMP = 100
+SCAN_START = 1500
+SCAN_LEN = 14_000
+SCAN_GAP = 1_000
+T_VANE_K = 290.0
+WHITE_SIGMA = 1.0 / np.sqrt(2e9 / 1024 * (1.0 / SAMPLE_RATE))   # ~5.06e-3
+FIELD_RA, FIELD_DEC = 170.0, 52.0
+
+
+@dataclass
+class SyntheticConfig:
+    n_feeds: int = 1
+    n_samples: int = 30_000
+    obs_id: int = 1
+    feed_numbers: tuple | None = None     # default 1..n_feeds
+    source: str = 'Field00'
+    comment: str = 'synthetic lissajous'
+    scan_len: int = SCAN_LEN
+    scan_gap: int = SCAN_GAP
+
+    def feeds(self):
+        if self.feed_numbers is not None:
+            return np.asarray(self.feed_numbers, dtype=np.int64)
+        return np.arange(1, self.n_feeds + 1, dtype=np.int64)
+
+
+def scan_status(n_samples: int, scan_len: int = SCAN_LEN, scan_gap: int = SCAN_GAP,
+                min_last: int = 12_500) -> np.ndarray:
+    """Lissajous status (1 inside a scan) per spectrometer sample."""
+    status = np.zeros(n_samples, dtype=np.int64)
+    s = SCAN_START
+    while s < n_samples - 100:
+        e = min(s + scan_len, n_samples - 100)
+        if e - s < min_last and s != SCAN_START:
+            break
+        status[s:e] = 1
+        s = e + scan_gap
+    return status
+
+
+def features_vector(n_samples: int) -> np.ndarray:
+    f = np.full(n_samples, 2.0 ** 5)
+    f[:VANE_START] = 0.0
+    f[VANE_START:VANE_END] = 2.0 ** 13
+    return f
+
+
+def hot_fraction(n_samples: int) -> np.ndarray:
+    """Fraction of the hot load in the beam: ramps in/out around [600,1000)."""
+    h = np.zeros(n_samples)
+    t = np.arange(n_samples)
+    up = (t >= VANE_START) & (t < HOT_START)
+    h[up] = (t[up] - VANE_START) / float(HOT_START - VANE_START)
+    h[(t >= HOT_START) & (t < HOT_END)] = 1.0
+    dn = (t >= HOT_END) & (t < HOT_END + RAMP)
+    h[dn] = 1.0 - (t[dn] - HOT_END) / float(RAMP)
+    return h
+
+
+def pointing(n_samples: int, feed: int):
+    t = np.arange(n_samples) / SAMPLE_RATE
+    fo = 0.02 * (feed - 10)
+    el = 47.5 + 7.5 * np.sin(2 * np.pi * t / 300.0 + 0.1 * feed)
+    az = 180.0 + 20.0 * np.sin(2 * np.pi * t / 600.0) + fo
+    dec = FIELD_DEC + 1.0 * np.sin(2 * np.pi * t / 29.0 + 0.3) + fo
+    ra = FIELD_RA + 1.0 * np.sin(2 * np.pi * t / 37.0) / np.cos(np.radians(FIELD_DEC)) + fo
+    return ra, dec, az, el
+
+
+def gain_drift(rng, n_samples: int, sigma: float = 2e-4) -> np.ndarray:
+    w = rng.standard_normal(n_samples)
+    f = np.fft.rfftfreq(n_samples, d=1.0 / SAMPLE_RATE)
+    f[0] = f[1]
+    ps = (1.0 / f) ** 1.5
+    g = np.fft.irfft(np.fft.rfft(w) * np.sqrt(ps), n=n_samples)
+    return g / np.std(g) * sigma
+
+
+def generate_feed(cfg: SyntheticConfig, feed: int):
+    """Returns (tod f32[4,1024,T], tsys, gain, ra, dec, az, el) for one feed."""
+    T = cfg.n_samples
+    rng = np.random.default_rng(np.random.SeedSequence([cfg.obs_id, int(feed)]))
+    tsys = rng.uniform(35.0, 45.0, (N_BANDS, N_CHANNELS))
+    gain = 1e6 * rng.uniform(0.9, 1.1, (N_BANDS, N_CHANNELS))
+    dg = gain_drift(rng, T)
+    ra, dec, az, el = pointing(T, int(feed))
+    A = 1.0 / np.sin(np.radians(el))
+    atm = 8.0 * (A - 1.4)
+    hf = hot_fraction(T)
+    vane = (np.arange(T) >= VANE_START) & (np.arange(T) < VANE_END)
+    # sky level (K) and multiplicative gain drift per sample; the vane region
+    # sees the load, no atmosphere/drift
+    level = np.where(vane, 0.0, atm)
+    mult = np.where(vane, 1.0, 1.0 + dg)
+    hot_add = hf * (T_VANE_K - 2.73)
+    tod = np.empty((N_BANDS, N_CHANNELS, T), dtype=np.float32)
+    for b in range(N_BANDS):
+        noise = rng.standard_normal((N_CHANNELS, T), dtype=np.float32) * np.float32(WHITE_SIGMA)
+        sig = (tsys[b, :, None] + level[None, :] + hot_add[None, :]) * mult[None, :]
+        tod[b] = (gain[b, :, None] * sig * (1.0 + noise)).astype(np.float32)
+    return tod, tsys, gain, ra, dec, az, el
+
+
+def generate_level1(cfg: SyntheticConfig) -> dict:
+    """Returns {'data': {path: array}, 'attrs': {path: {k: v}}, 'truth': {...}}."""
+    T = cfg.n_samples
+    feeds = cfg.feeds()
+    F = feeds.size
+    tod = np.empty((F, N_BANDS, N_CHANNELS, T), dtype=np.float32)
+    pix = {k: np.empty((F, T)) for k in ('ra', 'dec', 'az', 'el')}
+    tsys_t = np.empty((F, N_BANDS, N_CHANNELS))
+    gain_t = np.empty((F, N_BANDS, N_CHANNELS))
+    for i, feed in enumerate(feeds):
+        tod[i], tsys_t[i], gain_t[i], pix['ra'][i], pix['dec'][i], pix['az'][i], pix['el'][i] = \
+            generate_feed(cfg, int(feed))
+    band_average = np.nanmean(tod, axis=2).astype(np.float32)
+    mjd = 59000.0 + cfg.obs_id * 0.1 + np.arange(T) / SAMPLE_RATE / 86400.0
+    status = scan_status(T, cfg.scan_len, cfg.scan_gap)
+    # housekeeping sampled half a sample earlier than the spectrometer
+    hk_utc = mjd - 0.5 / SAMPLE_RATE / 86400.0
+    freq = np.linspace(26.0, 34.0, N_BANDS * N_CHANNELS).reshape(N_BANDS, N_CHANNELS)
+    data = {
+        'spectrometer/tod': tod,
+        'spectrometer/band_average': band_average,
+        'spectrometer/features': features_vector(T),
+        'spectrometer/MJD': mjd,
+        'spectrometer/feeds': feeds,
+        'spectrometer/bands': freq.copy(),
+        'spectrometer/frequency': freq.copy(),
+        'spectrometer/pixel_pointing/pixel_ra': pix['ra'],
+        'spectrometer/pixel_pointing/pixel_dec': pix['dec'],
+        'spectrometer/pixel_pointing/pixel_az': pix['az'],
+        'spectrometer/pixel_pointing/pixel_el': pix['el'],
+        'hk/antenna0/deTracker/lissajous_status': status,
+        'hk/antenna0/deTracker/utc': hk_utc,
+        'hk/antenna0/vane/Tvane': np.full(64, (T_VANE_K - 273.15) * 100.0),
+    }
+    attrs = {'comap': {'obsid': str(cfg.obs_id), 'source': cfg.source, 'comment': cfg.comment}}
+    return {'data': data, 'attrs': attrs, 'truth': {'tsys': tsys_t, 'gain': gain_t}}
+
+
+def sha256(arr: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(arr).tobytes()).hexdigest()
+
+
+# ---------------------------------------------------------------- destriper
+def destriper_inputs(n_feeds: int = 2, n_samples: int = 20_000, npix_side: int = 60,
+                     offset_length: int = 50, seed: int = 7, offmap_fraction: float = 0.01):
+    """Small synthetic destriper problem (pointing int64, tod f64, weights f64).
+
+    1/f offsets + sky + white noise per feed, Lissajous pointing on an
+    npix_side x npix_side grid; a fraction of samples is off-map (pixel -1) to
+    exercise the m[-1] quirk of op_Z (reference Destriper.py:206-213).
+    """
+    rng = np.random.default_rng(seed)
+    N = n_feeds * n_samples
+    t = np.arange(n_samples) / SAMPLE_RATE
+    sky = rng.standard_normal((npix_side, npix_side)).cumsum(0).cumsum(1) * 1e-2
+    pointing = np.empty(N, dtype=np.int64)
+    tod = np.empty(N)
+    for f in range(n_feeds):
+        x = 0.5 + 0.45 * np.sin(2 * np.pi * t / 23.0 + f)
+        y = 0.5 + 0.45 * np.sin(2 * np.pi * t / 31.0 + 2 * f)
+        ix = np.clip((x * npix_side).astype(int), 0, npix_side - 1)
+        iy = np.clip((y * npix_side).astype(int), 0, npix_side - 1)
+        p = iy * npix_side + ix
+        s = slice(f * n_samples, (f + 1) * n_samples)
+        white = rng.standard_normal(n_samples) * 0.1
+        drift = np.cumsum(rng.standard_normal(n_samples)) * 0.01
+        tod[s] = sky[iy, ix] + drift + white
+        pointing[s] = p
+    off = rng.random(N) < offmap_fraction
+    pointing[off] = -1
+    weights = np.full(N, 1.0 / 0.1 ** 2)
+    weights[rng.random(N) < 0.02] = 0.0
+    return pointing, tod, weights
