@@ -1,0 +1,7 @@
+"""Reference-compatible namespace: ``from comapreduce_amd import Analysis`` then
+``getattr(Analysis, name)`` for the TOML ``processes`` list exactly as
+run_average.py:46-48 does with ``comancpipeline.Analysis``."""
+from ..pipeline.running import Runner, PipelineFunction, set_logging  # noqa: F401
+from ..pipeline.datahandling import HDF5Data, COMAPLevel1, COMAPLevel2, RepointEdges  # noqa: F401
+from ..stages.level1 import (MeasureSystemTemperature, AtmosphereRemoval,  # noqa: F401
+                             Level1AveragingGainCorrection, CheckLevel1File, AssignLevel1Data)

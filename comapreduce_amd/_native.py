@@ -1,0 +1,133 @@
+"""ctypes binding of libcomap_hip.so (the C ABI in include/comap_hip.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` /
+``make -C comapreduce_amd/csrc`` into ``comapreduce_amd/_lib/``.  There is no
+CPU fallback: if the library or a GPU is missing, every op raises.
+"""
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, '_lib', 'libcomap_hip.so')
+
+_lib = None
+_lock = threading.Lock()
+_ctx = {}
+
+c_int, c_int32, c_int64, c_double, c_void_p = ctypes.c_int, ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
+P_double = ctypes.POINTER(ctypes.c_double)
+P_int32 = ctypes.POINTER(ctypes.c_int32)
+P_int64 = ctypes.POINTER(ctypes.c_int64)
+
+
+class ObsDesc(ctypes.Structure):
+    """comap_obs_desc (include/comap_hip.h)."""
+    _fields_ = [('n_feeds', c_int32), ('n_bands', c_int32), ('n_channels', c_int32),
+                ('n_scans', c_int32), ('n_samples', c_int64), ('tod', c_void_p), ('el', c_void_p),
+                ('n_units', c_int32), ('units_host', P_int32)]
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    'comap_ctx_create': (c_int, [c_int, ctypes.POINTER(c_void_p)]),
+    'comap_ctx_destroy': (c_int, [c_void_p]),
+    'comap_last_error': (ctypes.c_char_p, [c_void_p]),
+    'comap_set_stream': (c_int, [c_void_p, c_void_p]),
+    'comap_synchronize': (c_int, [c_void_p]),
+    'comap_version': (ctypes.c_char_p, []),
+    'comap_medfilt_f64': (c_int, [c_void_p, P_double, c_int64, c_int32]),
+    'comap_bin_values_f64': (c_int, [c_void_p, P_double, c_int64, P_int64, P_double, P_int64, c_int64]),
+    'comap_l1_plan_create': (c_int, [c_void_p, ctypes.POINTER(ObsDesc), ctypes.POINTER(c_void_p)]),
+    'comap_l1_plan_destroy': (c_int, [c_void_p]),
+    'comap_l1_vane': (c_int, [c_void_p, c_int64, c_int64, P_int32, P_int64, P_int32, P_int64, c_double,
+                              c_void_p, c_void_p]),
+    'comap_l1_atmosphere': (c_int, [c_void_p, c_void_p]),
+    'comap_l1_average': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
+    'comap_l1_debug_fetch': (c_int, [c_void_p, c_int32, P_double, c_int64]),
+    'comap_l1_profile': (c_int, [c_void_p, c_int32]),
+    'comap_l1_profile_collect': (c_int, [c_void_p, P_double, P_int64, c_int32]),
+    'comap_synth_tod': (c_int, [c_void_p, c_int32, c_int64, ctypes.c_uint64, c_void_p, c_void_p, c_void_p,
+                                c_void_p, c_void_p]),
+    'comap_destripe_create': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int64,
+                                      ctypes.POINTER(c_void_p)]),
+    'comap_destripe_destroy': (c_int, [c_void_p]),
+    'comap_destripe_n_offsets': (c_int64, [c_void_p]),
+    'comap_destripe_nnz': (c_int, [c_void_p, P_int64, P_int64]),
+    'comap_destripe_local_maps': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    'comap_destripe_bin': (c_int, [c_void_p, c_void_p, c_int32, c_void_p]),
+    'comap_destripe_project': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    'comap_destripe_dot': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    'comap_destripe_cg_update': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                         c_void_p]),
+    'comap_destripe_cg_direction': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    'comap_destripe_div_map': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    'comap_destripe_solve': (c_int, [c_void_p, c_double, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                     c_void_p, P_int32]),
+}
+
+EXPORTED = tuple(_SIGS)
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libcomap_hip.so (raises if absent -- there is no fallback)."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise ImportError(f'{LIB_PATH} is missing: build it with '
+                                      '`python -c "import __graft_entry__ as g; g.build()"` '
+                                      'or `make -C comapreduce_amd/csrc`')
+                # torch-ROCm bundles its own libamdhip64.so.7 / libhsa-runtime64: load it first so
+                # our NEEDED libamdhip64.so.7 binds to the same (single) HIP runtime in the process;
+                # loading /opt/rocm's copy first leaves torch without a device.
+                import torch  # noqa: F401
+                L = ctypes.CDLL(LIB_PATH)
+                for name, (res, args) in _SIGS.items():
+                    fn = getattr(L, name)
+                    fn.restype = res
+                    fn.argtypes = args
+                _lib = L
+    return _lib
+
+
+def ctx(device=0):
+    """Per-process context for ``device`` (created on first use)."""
+    c = _ctx.get(device)
+    if c is None:
+        out = c_void_p()
+        rc = lib().comap_ctx_create(device, ctypes.byref(out))
+        if rc != 0:
+            raise NativeError(f'comap_ctx_create(device={device}) failed rc={rc}: no usable HIP device')
+        c = out
+        _ctx[device] = c
+    return c
+
+
+def check(rc, c=None, what=''):
+    if rc != 0:
+        msg = lib().comap_last_error(c).decode() if c is not None else ''
+        raise NativeError(f'{what} failed rc={rc}: {msg}')
+    return rc
+
+
+def bind_stream(c, torch_device=None):
+    """Route the context's work onto torch's current stream (so torch events time it)."""
+    import torch
+    s = torch.cuda.current_stream(torch_device)
+    check(lib().comap_set_stream(c, c_void_p(s.cuda_stream)), c, 'comap_set_stream')
+
+
+def dptr(t):
+    """Device pointer of a contiguous torch CUDA tensor."""
+    assert t.is_cuda and t.is_contiguous(), 'expected a contiguous CUDA tensor'
+    return c_void_p(t.data_ptr())
+
+
+def hptr(a, ctype):
+    return a.ctypes.data_as(ctypes.POINTER(ctype))

@@ -1,0 +1,187 @@
+// capi.hip -- context management and the host-array drop-ins of the C ABI.
+//
+//   comap_medfilt_f64     replaces medfilt.medfilt   (Tools/median_filter/medfilt.pyx:26-33)
+//   comap_bin_values_f64  replaces binFuncs.binValues (Tools/binFuncs.pyx:7-32)
+//
+// binValues is reproduced bit-exactly: samples are stably radix-sorted by
+// pixel (hipcub, keeps sample order inside a pixel) and each pixel's weights
+// are then added to image[p] in sample order, exactly the sequence of the
+// reference's serial loop.
+#include "comap_internal.h"
+
+#include <hipcub/hipcub.hpp>
+
+#include <cmath>
+#include <cstring>
+
+int comap_fail(comap_ctx *ctx, int code, const std::string &msg)
+{
+    if (ctx) ctx->err = msg;
+    return code;
+}
+
+int comap_scratch(comap_ctx *ctx, size_t bytes, void **out)
+{
+    if (bytes > ctx->scratch_bytes) {
+        if (ctx->scratch) {
+            COMAP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+            COMAP_CHECK(ctx, hipFree(ctx->scratch));
+            ctx->scratch = nullptr;
+            ctx->scratch_bytes = 0;
+        }
+        size_t nb = bytes + bytes / 4 + 4096;
+        COMAP_CHECK(ctx, hipMalloc(&ctx->scratch, nb));
+        ctx->scratch_bytes = nb;
+    }
+    *out = ctx->scratch;
+    return 0;
+}
+
+extern "C" const char *comap_version(void) { return "comap_hip gfx950 " __DATE__; }
+
+extern "C" int comap_ctx_create(int device, comap_ctx **out)
+{
+    if (!out) return -1;
+    *out = nullptr;
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev <= device || device < 0) return -6;
+    if (hipSetDevice(device) != hipSuccess) return -6;
+    auto *c = new comap_ctx();
+    c->device = device;
+    *out = c;
+    return 0;
+}
+
+extern "C" int comap_ctx_destroy(comap_ctx *ctx)
+{
+    if (!ctx) return 0;
+    if (ctx->scratch) {
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipFree(ctx->scratch);
+    }
+    delete ctx;
+    return 0;
+}
+
+extern "C" const char *comap_last_error(const comap_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+extern "C" int comap_set_stream(comap_ctx *ctx, void *stream)
+{
+    if (!ctx) return -1;
+    ctx->stream = (hipStream_t)stream;
+    return 0;
+}
+
+extern "C" int comap_synchronize(comap_ctx *ctx)
+{
+    if (!ctx) return -1;
+    COMAP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+// ------------------------------------------------------------------ medfilt drop-in
+extern "C" int comap_medfilt_f64(comap_ctx *ctx, double *x, int64_t n, int32_t w)
+{
+    if (!ctx || !x) return -1;
+    if (w < 1 || n < w) return comap_fail(ctx, -1, "medfilt requires 1 <= w <= n");
+    for (int64_t i = 0; i < n; ++i)
+        if (std::isnan(x[i])) return comap_fail(ctx, -3, "medfilt input contains NaN");
+    if (n + w >= (1ll << 31)) return comap_fail(ctx, -1, "medfilt series too long");
+    char *s = nullptr;
+    int rc = comap_scratch(ctx, 16 * (size_t)n + 64, (void **)&s);
+    if (rc) return rc;
+    double *dsrc = (double *)s;
+    double *ddst = dsrc + n;
+    MedJob job;
+    job.src = dsrc; job.dst = ddst; job.n = n; job.out_lo = 0; job.out_hi = n; job.mode = 0; job.pad_ = 0;
+    job.gate = nullptr;
+    hipStream_t st = ctx->stream;
+    COMAP_CHECK(ctx, hipMemcpyAsync(dsrc, x, 8 * n, hipMemcpyHostToDevice, st));
+    MedPlan mp;
+    rc = comap_median_plan(ctx, &mp, std::vector<MedJob>{job}, w);
+    if (!rc) rc = comap_median_run(ctx, &mp);
+    if (!rc) {
+        hipError_t e = hipMemcpyAsync(x, ddst, 8 * n, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) rc = comap_fail(ctx, -2, hipGetErrorString(e));
+    }
+    comap_median_plan_free(&mp);
+    return rc;
+}
+
+// ------------------------------------------------------------------ binValues drop-in
+__global__ void k_bin_keys(const int64_t *__restrict__ pix, const int64_t *__restrict__ mask, int64_t n,
+                           int64_t npix, int32_t *__restrict__ keys, int32_t *__restrict__ vals)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t p = pix[i];
+        const bool ok = (p >= 0) && (p < npix) && (!mask || mask[i] != 0);
+        keys[i] = ok ? (int32_t)p : (int32_t)npix;
+        vals[i] = (int32_t)i;
+    }
+}
+
+__device__ __forceinline__ int64_t lb32(const int32_t *a, int64_t n, int32_t v)
+{
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t m = (lo + hi) >> 1;
+        if (a[m] < v) lo = m + 1; else hi = m;
+    }
+    return lo;
+}
+
+// image[p] += w[i] in sample order (the reference's serial sequence).
+__global__ void k_bin_ordered(const int32_t *__restrict__ keys, const int32_t *__restrict__ vals, int64_t n,
+                              const double *__restrict__ w, int64_t npix, double *__restrict__ image)
+{
+    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t lo = lb32(keys, n, (int32_t)p), hi = lb32(keys, n, (int32_t)(p + 1));
+        if (lo == hi) continue;
+        double acc = image[p];
+        if (w) for (int64_t j = lo; j < hi; ++j) acc += w[vals[j]];
+        else for (int64_t j = lo; j < hi; ++j) acc += 1.0;
+        image[p] = acc;
+    }
+}
+
+extern "C" int comap_bin_values_f64(comap_ctx *ctx, double *image, int64_t npix, const int64_t *pixels,
+                                    const double *weights, const int64_t *mask, int64_t n)
+{
+    if (!ctx || !image || (!pixels && n > 0)) return -1;
+    if (npix <= 0 || n <= 0) return 0;
+    if (npix >= (1ll << 31) - 1 || n >= (1ll << 31)) return comap_fail(ctx, -1, "binValues size limit exceeded");
+    int end_bit = 1;
+    while ((1ll << end_bit) <= npix) ++end_bit;
+    size_t tmp_bytes = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (int32_t *)nullptr, (int32_t *)nullptr,
+                                       (int32_t *)nullptr, (int32_t *)nullptr, (int)n, 0, end_bit, ctx->stream);
+    const size_t bytes = 8 * (size_t)n * 3 + 8 * (size_t)npix + 16 * (size_t)n + tmp_bytes + 4096;
+    char *s = nullptr;
+    int rc = comap_scratch(ctx, bytes, (void **)&s);
+    if (rc) return rc;
+    auto align = [](char *p) { return (char *)(((uintptr_t)p + 255) & ~(uintptr_t)255); };
+    int64_t *dpix = (int64_t *)align(s);
+    double *dw = (double *)align((char *)(dpix + n));
+    int64_t *dmask = (int64_t *)align((char *)(dw + n));
+    double *dimg = (double *)align((char *)(dmask + n));
+    int32_t *k0 = (int32_t *)align((char *)(dimg + npix));
+    int32_t *k1 = (int32_t *)align((char *)(k0 + n));
+    int32_t *v0 = (int32_t *)align((char *)(k1 + n));
+    int32_t *v1 = (int32_t *)align((char *)(v0 + n));
+    void *tmp = (void *)align((char *)(v1 + n));
+    hipStream_t st = ctx->stream;
+    COMAP_CHECK(ctx, hipMemcpyAsync(dpix, pixels, 8 * n, hipMemcpyHostToDevice, st));
+    if (weights) COMAP_CHECK(ctx, hipMemcpyAsync(dw, weights, 8 * n, hipMemcpyHostToDevice, st));
+    if (mask) COMAP_CHECK(ctx, hipMemcpyAsync(dmask, mask, 8 * n, hipMemcpyHostToDevice, st));
+    COMAP_CHECK(ctx, hipMemcpyAsync(dimg, image, 8 * npix, hipMemcpyHostToDevice, st));
+    k_bin_keys<<<1024, 256, 0, st>>>(dpix, mask ? dmask : nullptr, n, npix, k0, v0);
+    COMAP_LAUNCH_CHECK(ctx);
+    COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, k0, k1, v0, v1, (int)n, 0, end_bit, st));
+    k_bin_ordered<<<1024, 256, 0, st>>>(k1, v1, n, weights ? dw : nullptr, npix, dimg);
+    COMAP_LAUNCH_CHECK(ctx);
+    COMAP_CHECK(ctx, hipMemcpyAsync(image, dimg, 8 * npix, hipMemcpyDeviceToHost, st));
+    COMAP_CHECK(ctx, hipStreamSynchronize(st));
+    return 0;
+}

@@ -1,0 +1,120 @@
+// Internal declarations shared by the HIP translation units of libcomap_hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/comap_hip.h"
+
+struct comap_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // scratch reused by the host-array drop-ins
+    void *scratch = nullptr;
+    size_t scratch_bytes = 0;
+};
+
+#define COMAP_CHECK(ctx, expr)                                                         \
+    do {                                                                               \
+        hipError_t _e = (expr);                                                        \
+        if (_e != hipSuccess) {                                                        \
+            (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(_e);            \
+            return -2;                                                                 \
+        }                                                                              \
+    } while (0)
+
+#define COMAP_LAUNCH_CHECK(ctx) COMAP_CHECK(ctx, hipGetLastError())
+
+int comap_fail(comap_ctx *ctx, int code, const std::string &msg);
+int comap_scratch(comap_ctx *ctx, size_t bytes, void **out);
+
+// ------------------------------------------------------------------ constants
+namespace comap {
+constexpr int kBands = 4;
+constexpr int kChannels = 1024;
+constexpr int kBC = kBands * kChannels;
+constexpr int kMedfiltWindow = 6000;           // int(50*120), Level1Averaging.py:833
+constexpr int kTile = 256;                     // samples per pass-B/D workgroup
+constexpr double kDnuTau = (2e9 / 1024.0) * (1.0 / 50.0);   // Level1Averaging.py:671-672
+}  // namespace comap
+
+// ------------------------------------------------------------------ sliding median
+// One job = one series with a virtual accessor; outputs [out_lo, out_hi) of the
+// (virtual) series are written to dst[i - out_lo].
+struct MedJob {
+    const double *src;
+    double *dst;
+    int64_t n;          // source length
+    int64_t out_lo;
+    int64_t out_hi;
+    int32_t mode;       // 0: medfilt head/tail semantics on src; 1: reflect3 [rev, x, rev]
+    int32_t pad_;
+    const double *gate; // optional: skip the job when *gate <= 0 (band count N_b)
+};
+
+// Sliding-median plan: jobs, per-job sorted-key segments, chunk table, buffers.
+struct MedPlan {
+    int32_t w = 0, lc = 0, P = 0, njobs = 0;
+    int32_t nitems = 0;
+    int64_t nchunks = 0;
+    MedJob *jobs = nullptr;      // dev [njobs]
+    int32_t *seg = nullptr;      // dev [njobs+1] segment offsets
+    int64_t *chunks = nullptr;   // dev [nchunks][2] (job, i0)
+    uint64_t *k0 = nullptr, *k1 = nullptr;
+    int32_t *v0 = nullptr, *v1 = nullptr;
+    void *temp = nullptr;
+    size_t temp_bytes = 0;
+};
+
+void comap_median_geometry(int32_t w, int32_t *lc, int32_t *P);
+int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jobs, int32_t w);
+void comap_median_plan_free(MedPlan *mp);
+int comap_median_run(comap_ctx *ctx, MedPlan *mp);
+
+// ------------------------------------------------------------------ L1 plan
+struct comap_l1_plan {
+    comap_ctx *ctx = nullptr;
+    int32_t F = 0, S = 0, U = 0;
+    int64_t T = 0;
+    const float *tod = nullptr;
+    const double *el = nullptr;
+    std::vector<int32_t> units_h;      // [U][4]
+    int32_t *units = nullptr;          // dev [U][4]
+    int32_t *tiles = nullptr;          // dev [NT][2] (unit, t_off)
+    int64_t n_tiles = 0;
+    // sliding median: one job per (unit, band)
+    MedPlan med;
+    // device workspaces
+    double *airmass = nullptr;         // [F][T]
+    double *unit_sums = nullptr;       // [U][8]: n, SA, SAA, Sv, Svv, N4
+    double *mom = nullptr;             // [5][U*4096]: Sd, SAd, Su, Suu, Suv
+    int32_t *nan_count = nullptr;      // [1]
+    bool moments_valid = false;
+    double *alpha = nullptr;           // [U*4096] 1/rms on median channels (0 off-set, NaN bad)
+    double *nf = nullptr;              // [U*4096] rms (normalisation factor)
+    double *bsum = nullptr;            // [U*4][4]: beta, gamma, N, skip
+    double *mb = nullptr;              // [F][4][T] band mean
+    double *mf = nullptr;              // [F][4][T] median-filtered band mean
+    double *ssum = nullptr;            // [U*4][4]: Smf, Smm, SAm
+    double *sdm = nullptr;             // [U*4096] sum_t d mf
+    double *gw = nullptr;              // [F][4096] gain weights w
+    int32_t *gmode = nullptr;          // [F]
+    double *kap = nullptr;             // [3][U*4096] kappa_g, kappa_r, kappa_o
+    double *dsum = nullptr;            // [U*4][16] per-band constants for pass D
+    double *xreg = nullptr;            // [U*4096][2] regression x0,x1 (debug)
+    double *dG = nullptr;              // [F][T]
+    // per-kernel HIP-event timing (comap_l1_profile)
+    bool prof_on = false;
+    std::vector<hipEvent_t> prof_pool;
+    std::vector<std::pair<int, int>> prof_rec;   // (kernel id, index of start event)
+    double prof_ms[32] = {0};
+    int64_t prof_n[32] = {0};
+};
+
+// kernel ids for comap_l1_profile_collect
+enum L1Kernel {
+    KV_VANE = 0, KV_MOMENTS, KV_ATMOS_FIT, KV_COEF_B, KV_BAND_MEAN, KV_MEDIAN, KV_SERIES_SUMS,
+    KV_REGRESS, KV_GAIN_WEIGHTS, KV_COEF_D, KV_GAIN_AVG, KV_SCAN_WEIGHTS, KV_COUNT
+};

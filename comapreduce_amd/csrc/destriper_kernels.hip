@@ -1,0 +1,524 @@
+// destriper_kernels.hip -- destriping map-maker (reference MapMaking/Destriper.py:85-263, 402-503).
+//
+// The reference's matvec A x = F^T W Z F x (op_Ax) bins every sample twice
+// per call (binFuncs.binValues, 97% of its time) and its BiCG calls it three
+// times per iteration with bit-identical arguments (p == pb, r == rb).
+//
+// Pointing and weights are constant during CG, so the operator is rebuilt
+// here once as a sparse offset<->pixel structure:
+//   entry (o, p, s) with s = sum of w_i over the samples i of offset o that
+//   fall in pixel p.  Then, with ws_o = sum_{i in o} w_i and h = weight map,
+//     num = W x               num_p = sum_{e in pixel row p} s_e x_{o(e)}
+//     m   = num / h           (m_p = num_p where h_p == 0, as share_map)
+//     y_o = ws_o x_o - sum_{e in offset row o} s_e m_{p(e)}      (op_Z + F^T W)
+// Off-map samples (pixel -1) are never binned but gather m[npix-1], the
+// reference's m[-1] wrap (Destriper.py:211).  One CG iteration streams
+// 2 nnz entries instead of 6 N samples; all reductions are fixed-order
+// (deterministic).  The sample-level maps (weight map h, hits, naive
+// numerator sum w tod) are summed per pixel in sample order after a stable
+// radix sort, i.e. in exactly binValues' order (bit-exact on one rank).
+#include "comap_internal.h"
+
+#include <hipcub/hipcub.hpp>
+
+#include <cmath>
+
+struct comap_destriper {
+    comap_ctx *ctx = nullptr;
+    int64_t N = 0, NO = 0, npix = 0;
+    int32_t L = 0;
+    int64_t nnz = 0;       // offset-major entries (incl. off-map gathers)
+    int64_t nnzp = 0;      // pixel-major entries (binned only)
+    // offset-major
+    int64_t *orow = nullptr;   // [NO+1]
+    int32_t *opix = nullptr;   // [nnz]  pixel (-1 = off-map)
+    double *ow = nullptr;      // [nnz]
+    double *ws = nullptr;      // [NO] sum w
+    double *tw = nullptr;      // [NO] sum w tod
+    // pixel-major
+    int64_t *prow = nullptr;   // [npix+1]
+    int32_t *poff = nullptr;   // [nnzp]
+    double *pw = nullptr;      // [nnzp]
+    // sample-level maps (local)
+    double *h = nullptr, *hits = nullptr, *nnum = nullptr;   // [npix]
+    // reduction scratch
+    double *part = nullptr;    // [kRedBlocks]
+    double *scal = nullptr;    // [16] device scalars
+};
+
+namespace {
+
+constexpr int kRedBlocks = 256;
+
+__device__ __forceinline__ double wave_sum(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// One wave per offset (L <= 64): unique pixels in first-occurrence order,
+// weights summed in sample order.  pass 0 counts, pass 1 fills.
+__global__ void __launch_bounds__(256) k_ds_entries(const int32_t *__restrict__ pix, const double *__restrict__ w,
+                                                    const double *__restrict__ tod, int64_t NO, int L, int pass,
+                                                    int64_t *__restrict__ cnt, const int64_t *__restrict__ orow,
+                                                    int32_t *__restrict__ opix, double *__restrict__ ow,
+                                                    double *__restrict__ ws, double *__restrict__ tw)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (o >= NO) return;
+    const int64_t i = o * L + lane;
+    const bool in = lane < L;
+    const int32_t p = in ? pix[i] : -2;
+    const double wi = in ? w[i] : 0.0;
+    // first occurrence of p among lanes < lane, and the in-order group sum
+    bool first = in;
+    double gsum = 0.0;
+    for (int j = 0; j < L; ++j) {
+        const int32_t pj = __shfl(p, j, 64);
+        const double wj = __shfl(wi, j, 64);
+        if (pj == p) {
+            if (j < lane) first = false;
+            gsum += wj;
+        }
+    }
+    const bool keep = first && gsum != 0.0;
+    const unsigned long long m = __ballot(keep);
+    if (pass == 0) {
+        if (lane == 0) cnt[o] = __popcll(m);
+        const double s = wave_sum(wi);
+        const double st = wave_sum(in ? wi * tod[i] : 0.0);
+        if (lane == 0) { ws[o] = s; tw[o] = st; }
+        return;
+    }
+    if (keep) {
+        const int rank = __popcll(m & ((1ull << lane) - 1ull));
+        const int64_t e = orow[o] + rank;
+        opix[e] = p;
+        ow[e] = gsum;
+    }
+}
+
+// keys for the pixel-major transpose: pixel of each offset-major entry (npix for off-map)
+__global__ void k_entry_keys(const int64_t *__restrict__ orow, int64_t NO, const int32_t *__restrict__ opix,
+                             int64_t npix, int32_t *__restrict__ key, int32_t *__restrict__ val,
+                             int32_t *__restrict__ eoff)
+{
+    for (int64_t o = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; o < NO; o += (int64_t)gridDim.x * blockDim.x) {
+        for (int64_t e = orow[o]; e < orow[o + 1]; ++e) {
+            const int32_t p = opix[e];
+            key[e] = (p >= 0 && p < npix) ? p : (int32_t)npix;
+            val[e] = (int32_t)e;
+            eoff[e] = (int32_t)o;
+        }
+    }
+}
+
+__device__ __forceinline__ int64_t lb32(const int32_t *a, int64_t n, int64_t v)
+{
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t m = (lo + hi) >> 1;
+        if (a[m] < v) lo = m + 1; else hi = m;
+    }
+    return lo;
+}
+
+__global__ void k_rowptr(const int32_t *__restrict__ skey, int64_t n, int64_t npix, int64_t *__restrict__ row)
+{
+    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p <= npix; p += (int64_t)gridDim.x * blockDim.x)
+        row[p] = lb32(skey, n, p);
+}
+
+__global__ void k_pixel_entries(const int32_t *__restrict__ sval, int64_t nnzp, const int32_t *__restrict__ eoff,
+                                const double *__restrict__ ow, int32_t *__restrict__ poff, double *__restrict__ pw)
+{
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < nnzp; k += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t e = sval[k];
+        poff[k] = eoff[e];
+        pw[k] = ow[e];
+    }
+}
+
+// sample-level maps in binValues order (stable pixel sort keeps sample order)
+__global__ void k_sample_keys(const int32_t *__restrict__ pix, int64_t N, int64_t npix, int32_t *__restrict__ key,
+                              int32_t *__restrict__ val)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t p = pix[i];
+        key[i] = (p >= 0 && p < npix) ? p : (int32_t)npix;
+        val[i] = (int32_t)i;
+    }
+}
+
+__global__ void k_sample_maps(const int32_t *__restrict__ skey, const int32_t *__restrict__ sval, int64_t N,
+                              int64_t npix, const double *__restrict__ w, const double *__restrict__ tod,
+                              double *__restrict__ h, double *__restrict__ hits, double *__restrict__ nnum)
+{
+    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t lo = lb32(skey, N, p), hi = lb32(skey, N, p + 1);
+        double sh = 0.0, sc = 0.0, sn = 0.0;
+        for (int64_t k = lo; k < hi; ++k) {
+            const int32_t i = sval[k];
+            const double wi = w[i];
+            sh += wi;
+            sn += tod[i] * wi;
+            sc += 1.0;
+        }
+        h[p] = sh;
+        hits[p] = sc;
+        nnum[p] = sn;
+    }
+}
+
+// num_p = sum_e s_e x_o(e)   (mode 0); mode 1: num = nnum - W x (final destriped numerator)
+__global__ void __launch_bounds__(256) k_ds_bin(const int64_t *__restrict__ prow, const int32_t *__restrict__ poff,
+                                                const double *__restrict__ pw, const double *__restrict__ x,
+                                                int64_t npix, const double *__restrict__ base, double *__restrict__ num)
+{
+    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x) {
+        double s = 0.0;
+        for (int64_t k = prow[p]; k < prow[p + 1]; ++k) s = fma(pw[k], x[poff[k]], s);
+        num[p] = base ? base[p] - s : s;
+    }
+}
+
+__device__ __forceinline__ double map_value(const double *num, const double *h, int64_t q)
+{
+    const double hv = h[q];
+    return hv != 0.0 ? num[q] / hv : num[q];
+}
+
+// y_o = ws_o x_o - sum_e s_e m_p(e)  (x == NULL: y_o = tw_o - ..., the b vector)
+// block partials of y.x (when dot_part != NULL)
+__global__ void __launch_bounds__(256) k_ds_project(const int64_t *__restrict__ orow, const int32_t *__restrict__ opix,
+                                                    const double *__restrict__ ow, const double *__restrict__ ws,
+                                                    const double *__restrict__ tw, const double *__restrict__ x,
+                                                    const double *__restrict__ num, const double *__restrict__ h,
+                                                    int64_t NO, int64_t npix, double *__restrict__ y,
+                                                    double *__restrict__ dot_part)
+{
+    __shared__ double red[4];
+    double acc = 0.0;
+    for (int64_t o = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; o < NO; o += (int64_t)gridDim.x * blockDim.x) {
+        double g = 0.0;
+        for (int64_t e = orow[o]; e < orow[o + 1]; ++e) {
+            const int32_t p = opix[e];
+            const int64_t q = (p >= 0) ? p : npix - 1;   // m[-1]
+            g = fma(ow[e], map_value(num, h, q), g);
+        }
+        const double v = (x ? ws[o] * x[o] : tw[o]) - g;
+        y[o] = v;
+        if (dot_part) acc = fma(v, x[o], acc);
+    }
+    if (dot_part) {
+        acc = wave_sum(acc);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+        __syncthreads();
+        if (threadIdx.x == 0) dot_part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_dot_part(const double *__restrict__ a, const double *__restrict__ b, int64_t n,
+                                                  double *__restrict__ part)
+{
+    __shared__ double red[4];
+    double acc = 0.0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        acc = fma(a[i], b[i], acc);
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ void __launch_bounds__(256) k_dot_final(const double *__restrict__ part, int n, double *__restrict__ out)
+{
+    __shared__ double red[4];
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) acc += part[i];
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) out[0] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// x += a p ; r -= a q ; a = rr / pq ; partials of r.r
+__global__ void __launch_bounds__(256) k_cg_update(const double *__restrict__ rr, const double *__restrict__ pq,
+                                                   double *__restrict__ x, double *__restrict__ r,
+                                                   const double *__restrict__ p, const double *__restrict__ q,
+                                                   int64_t n, double *__restrict__ part)
+{
+    __shared__ double red[4];
+    const double a = rr[0] / pq[0];
+    double acc = 0.0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        x[i] += a * p[i];
+        const double ri = r[i] - a * q[i];
+        r[i] = ri;
+        acc = fma(ri, ri, acc);
+    }
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ void k_cg_direction(const double *__restrict__ rr_new, const double *__restrict__ rr, double *__restrict__ p,
+                               const double *__restrict__ r, int64_t n)
+{
+    const double beta = rr_new[0] / rr[0];
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        p[i] = r[i] + beta * p[i];
+}
+
+__global__ void k_div_map(const double *__restrict__ num, const double *__restrict__ h, int64_t npix,
+                          double *__restrict__ out)
+{
+    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x)
+        out[p] = map_value(num, h, p);
+}
+
+inline unsigned grid_for(int64_t n, int64_t cap = 4096) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, cap)); }
+
+template <typename T>
+int dalloc(comap_ctx *ctx, T **p, size_t n)
+{
+    COMAP_CHECK(ctx, hipMalloc((void **)p, sizeof(T) * (n ? n : 1)));
+    return 0;
+}
+
+int dot(comap_destriper *d, const double *a, const double *b, double *out)
+{
+    comap_ctx *ctx = d->ctx;
+    k_dot_part<<<kRedBlocks, 256, 0, ctx->stream>>>(a, b, d->NO, d->part);
+    COMAP_LAUNCH_CHECK(ctx);
+    k_dot_final<<<1, 256, 0, ctx->stream>>>(d->part, kRedBlocks, out);
+    COMAP_LAUNCH_CHECK(ctx);
+    return 0;
+}
+
+}  // namespace
+
+extern "C" int comap_destripe_create(comap_ctx *ctx, const int32_t *pix, const double *tod, const double *w,
+                                     int64_t N, int32_t L, int64_t npix, comap_destriper **out)
+{
+    if (!ctx || !pix || !tod || !w || !out) return -1;
+    if (L < 1 || L > 64) return comap_fail(ctx, -1, "offset_length must be in [1, 64]");
+    if (N <= 0 || N % L) return comap_fail(ctx, -1, "n_samples must be a positive multiple of offset_length");
+    if (npix <= 0 || npix >= (1ll << 31) - 1 || N >= (1ll << 31)) return comap_fail(ctx, -1, "size limits exceeded");
+    hipStream_t st = ctx->stream;
+    auto *d = new comap_destriper();
+    d->ctx = ctx; d->N = N; d->L = L; d->NO = N / L; d->npix = npix;
+    int rc = 0;
+    rc |= dalloc(ctx, &d->orow, d->NO + 1);
+    rc |= dalloc(ctx, &d->ws, d->NO);
+    rc |= dalloc(ctx, &d->tw, d->NO);
+    rc |= dalloc(ctx, &d->prow, npix + 1);
+    rc |= dalloc(ctx, &d->h, npix);
+    rc |= dalloc(ctx, &d->hits, npix);
+    rc |= dalloc(ctx, &d->nnum, npix);
+    rc |= dalloc(ctx, &d->part, kRedBlocks);
+    rc |= dalloc(ctx, &d->scal, 16);
+    if (rc) { comap_destripe_destroy(d); return -2; }
+    // ---- offset-major entries
+    int64_t *cnt = nullptr;
+    if (dalloc(ctx, &cnt, d->NO + 1)) { comap_destripe_destroy(d); return -2; }
+    const unsigned gblocks = (unsigned)((d->NO + 3) / 4);
+    k_ds_entries<<<gblocks, 256, 0, st>>>(pix, w, tod, d->NO, L, 0, cnt, nullptr, nullptr, nullptr, d->ws, d->tw);
+    COMAP_LAUNCH_CHECK(ctx);
+    size_t tb = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, d->orow, (int)(d->NO + 1), st);
+    void *tmp = nullptr;
+    COMAP_CHECK(ctx, hipMalloc(&tmp, tb));
+    COMAP_CHECK(ctx, hipMemsetAsync(cnt + d->NO, 0, 8, st));
+    COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, d->orow, (int)(d->NO + 1), st));
+    COMAP_CHECK(ctx, hipMemcpyAsync(&d->nnz, d->orow + d->NO, 8, hipMemcpyDeviceToHost, st));
+    COMAP_CHECK(ctx, hipStreamSynchronize(st));
+    (void)hipFree(tmp);
+    (void)hipFree(cnt);
+    rc |= dalloc(ctx, &d->opix, d->nnz);
+    rc |= dalloc(ctx, &d->ow, d->nnz);
+    if (rc) { comap_destripe_destroy(d); return -2; }
+    k_ds_entries<<<gblocks, 256, 0, st>>>(pix, w, tod, d->NO, L, 1, nullptr, d->orow, d->opix, d->ow, nullptr, nullptr);
+    COMAP_LAUNCH_CHECK(ctx);
+    // ---- pixel-major transpose (stable radix sort keeps offset order within a pixel)
+    const int64_t sortn = std::max<int64_t>(d->nnz, N);
+    int32_t *k0 = nullptr, *k1 = nullptr, *v0 = nullptr, *v1 = nullptr, *eoff = nullptr;
+    rc |= dalloc(ctx, &k0, sortn); rc |= dalloc(ctx, &k1, sortn);
+    rc |= dalloc(ctx, &v0, sortn); rc |= dalloc(ctx, &v1, sortn);
+    rc |= dalloc(ctx, &eoff, d->nnz);
+    if (rc) { comap_destripe_destroy(d); return -2; }
+    int end_bit = 1;
+    while ((1ll << end_bit) <= npix) ++end_bit;
+    k_entry_keys<<<grid_for(d->NO), 256, 0, st>>>(d->orow, d->NO, d->opix, npix, k0, v0, eoff);
+    COMAP_LAUNCH_CHECK(ctx);
+    tb = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k0, k1, v0, v1, (int)sortn, 0, end_bit, st);
+    COMAP_CHECK(ctx, hipMalloc(&tmp, tb));
+    COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(tmp, tb, k0, k1, v0, v1, (int)d->nnz, 0, end_bit, st));
+    k_rowptr<<<grid_for(npix + 1), 256, 0, st>>>(k1, d->nnz, npix, d->prow);
+    COMAP_LAUNCH_CHECK(ctx);
+    COMAP_CHECK(ctx, hipMemcpyAsync(&d->nnzp, d->prow + npix, 8, hipMemcpyDeviceToHost, st));
+    COMAP_CHECK(ctx, hipStreamSynchronize(st));
+    rc |= dalloc(ctx, &d->poff, d->nnzp);
+    rc |= dalloc(ctx, &d->pw, d->nnzp);
+    if (rc) { comap_destripe_destroy(d); return -2; }
+    k_pixel_entries<<<grid_for(d->nnzp), 256, 0, st>>>(v1, d->nnzp, eoff, d->ow, d->poff, d->pw);
+    COMAP_LAUNCH_CHECK(ctx);
+    // ---- sample-level maps (binValues order)
+    k_sample_keys<<<grid_for(N), 256, 0, st>>>(pix, N, npix, k0, v0);
+    COMAP_LAUNCH_CHECK(ctx);
+    COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(tmp, tb, k0, k1, v0, v1, (int)N, 0, end_bit, st));
+    k_sample_maps<<<grid_for(npix), 256, 0, st>>>(k1, v1, N, npix, w, tod, d->h, d->hits, d->nnum);
+    COMAP_LAUNCH_CHECK(ctx);
+    COMAP_CHECK(ctx, hipStreamSynchronize(st));
+    (void)hipFree(tmp); (void)hipFree(k0); (void)hipFree(k1); (void)hipFree(v0); (void)hipFree(v1); (void)hipFree(eoff);
+    *out = d;
+    return 0;
+}
+
+extern "C" int comap_destripe_destroy(comap_destriper *d)
+{
+    if (!d) return 0;
+    void *b[] = {d->orow, d->opix, d->ow, d->ws, d->tw, d->prow, d->poff, d->pw, d->h, d->hits, d->nnum, d->part, d->scal};
+    for (void *p : b)
+        if (p) (void)hipFree(p);
+    delete d;
+    return 0;
+}
+
+extern "C" int64_t comap_destripe_n_offsets(const comap_destriper *d) { return d ? d->NO : -1; }
+
+extern "C" int comap_destripe_nnz(const comap_destriper *d, int64_t *nnz_offset_major, int64_t *nnz_pixel_major)
+{
+    if (!d) return -1;
+    if (nnz_offset_major) *nnz_offset_major = d->nnz;
+    if (nnz_pixel_major) *nnz_pixel_major = d->nnzp;
+    return 0;
+}
+
+extern "C" int comap_destripe_local_maps(comap_destriper *d, double *h, double *hits, double *naive_num)
+{
+    if (!d) return -1;
+    comap_ctx *ctx = d->ctx;
+    const size_t b = 8 * (size_t)d->npix;
+    if (h) COMAP_CHECK(ctx, hipMemcpyAsync(h, d->h, b, hipMemcpyDeviceToDevice, ctx->stream));
+    if (hits) COMAP_CHECK(ctx, hipMemcpyAsync(hits, d->hits, b, hipMemcpyDeviceToDevice, ctx->stream));
+    if (naive_num) COMAP_CHECK(ctx, hipMemcpyAsync(naive_num, d->nnum, b, hipMemcpyDeviceToDevice, ctx->stream));
+    return 0;
+}
+
+extern "C" int comap_destripe_bin(comap_destriper *d, const double *x, int32_t mode, double *num)
+{
+    if (!d || !x || !num) return -1;
+    comap_ctx *ctx = d->ctx;
+    k_ds_bin<<<grid_for(d->npix), 256, 0, ctx->stream>>>(d->prow, d->poff, d->pw, x, d->npix,
+                                                          mode == 1 ? d->nnum : nullptr, num);
+    COMAP_LAUNCH_CHECK(ctx);
+    return 0;
+}
+
+extern "C" int comap_destripe_project(comap_destriper *d, const double *x, const double *num, const double *h,
+                                      double *y, double *dot_out)
+{
+    if (!d || !num || !y) return -1;
+    comap_ctx *ctx = d->ctx;
+    const double *hh = h ? h : d->h;
+    const bool want = dot_out && x;
+    k_ds_project<<<kRedBlocks, 256, 0, ctx->stream>>>(d->orow, d->opix, d->ow, d->ws, d->tw, x, num, hh, d->NO,
+                                                      d->npix, y, want ? d->part : nullptr);
+    COMAP_LAUNCH_CHECK(ctx);
+    if (want) {
+        k_dot_final<<<1, 256, 0, ctx->stream>>>(d->part, kRedBlocks, dot_out);
+        COMAP_LAUNCH_CHECK(ctx);
+    }
+    return 0;
+}
+
+extern "C" int comap_destripe_dot(comap_destriper *d, const double *a, const double *b, double *out)
+{
+    if (!d || !a || !b || !out) return -1;
+    return dot(d, a, b, out);
+}
+
+extern "C" int comap_destripe_cg_update(comap_destriper *d, const double *rr, const double *pq, double *x, double *r,
+                                        const double *p, const double *q, double *rr_new)
+{
+    if (!d) return -1;
+    comap_ctx *ctx = d->ctx;
+    k_cg_update<<<kRedBlocks, 256, 0, ctx->stream>>>(rr, pq, x, r, p, q, d->NO, d->part);
+    COMAP_LAUNCH_CHECK(ctx);
+    k_dot_final<<<1, 256, 0, ctx->stream>>>(d->part, kRedBlocks, rr_new);
+    COMAP_LAUNCH_CHECK(ctx);
+    return 0;
+}
+
+extern "C" int comap_destripe_cg_direction(comap_destriper *d, const double *rr_new, const double *rr, double *p,
+                                           const double *r)
+{
+    if (!d) return -1;
+    comap_ctx *ctx = d->ctx;
+    k_cg_direction<<<grid_for(d->NO), 256, 0, ctx->stream>>>(rr_new, rr, p, r, d->NO);
+    COMAP_LAUNCH_CHECK(ctx);
+    return 0;
+}
+
+extern "C" int comap_destripe_div_map(comap_destriper *d, const double *num, const double *h, double *out)
+{
+    if (!d || !num || !out) return -1;
+    comap_ctx *ctx = d->ctx;
+    k_div_map<<<grid_for(d->npix), 256, 0, ctx->stream>>>(num, h ? h : d->h, d->npix, out);
+    COMAP_LAUNCH_CHECK(ctx);
+    return 0;
+}
+
+// Single-rank CG (Destriper.py:85-152 with p == pb, r == rb: one matvec per
+// iteration) followed by the final maps of destriper_iteration (:419-451).
+extern "C" int comap_destripe_solve(comap_destriper *d, double threshold, int32_t niter, double *x, double *map,
+                                    double *naive, double *weight, double *hits, int32_t *iters_out)
+{
+    if (!d || !x || niter < 0) return -1;
+    comap_ctx *ctx = d->ctx;
+    hipStream_t st = ctx->stream;
+    const int64_t NO = d->NO, np = d->npix;
+    double *buf = nullptr;
+    if (dalloc(ctx, &buf, 3 * (size_t)NO + (size_t)np)) return -2;
+    double *r = buf, *p = buf + NO, *q = buf + 2 * NO, *num = buf + 3 * NO;
+    double *rr0 = d->scal, *rr = d->scal + 1, *pq = d->scal + 2, *rrn = d->scal + 3;
+    int rc = 0;
+    COMAP_CHECK(ctx, hipMemsetAsync(x, 0, 8 * NO, st));
+    // b = op_Ax(tod, extend=False); r = p = b (x0 = 0)
+    rc |= comap_destripe_project(d, nullptr, d->nnum, d->h, r, nullptr);
+    COMAP_CHECK(ctx, hipMemcpyAsync(p, r, 8 * NO, hipMemcpyDeviceToDevice, st));
+    rc |= dot(d, r, r, rr0);
+    COMAP_CHECK(ctx, hipMemcpyAsync(rr, rr0, 8, hipMemcpyDeviceToDevice, st));
+    double h_rr0 = 0, h_rrn = 0;
+    COMAP_CHECK(ctx, hipMemcpyAsync(&h_rr0, rr0, 8, hipMemcpyDeviceToHost, st));
+    int it = 0;
+    for (int i = 0; i < niter && !rc; ++i) {
+        rc |= comap_destripe_bin(d, p, 0, num);
+        rc |= comap_destripe_project(d, p, num, d->h, q, pq);
+        rc |= comap_destripe_cg_update(d, rr, pq, x, r, p, q, rrn);
+        rc |= comap_destripe_cg_direction(d, rrn, rr, p, r);
+        COMAP_CHECK(ctx, hipMemcpyAsync(rr, rrn, 8, hipMemcpyDeviceToDevice, st));
+        COMAP_CHECK(ctx, hipMemcpyAsync(&h_rrn, rrn, 8, hipMemcpyDeviceToHost, st));
+        COMAP_CHECK(ctx, hipStreamSynchronize(st));
+        it = i + 1;
+        const double delta = h_rrn / h_rr0;
+        if (std::isnan(delta) || delta < threshold) break;
+    }
+    if (iters_out) *iters_out = it;
+    // final maps: map = (sum w tod - W x) / h ; naive = sum w tod / h
+    if (map) {
+        rc |= comap_destripe_bin(d, x, 1, num);
+        rc |= comap_destripe_div_map(d, num, d->h, map);
+    }
+    if (naive) rc |= comap_destripe_div_map(d, d->nnum, d->h, naive);
+    if (weight) COMAP_CHECK(ctx, hipMemcpyAsync(weight, d->h, 8 * np, hipMemcpyDeviceToDevice, st));
+    if (hits) COMAP_CHECK(ctx, hipMemcpyAsync(hits, d->hits, 8 * np, hipMemcpyDeviceToDevice, st));
+    COMAP_CHECK(ctx, hipStreamSynchronize(st));
+    (void)hipFree(buf);
+    return rc;
+}

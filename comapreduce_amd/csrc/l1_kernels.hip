@@ -1,0 +1,992 @@
+// l1_kernels.hip -- Level-1 -> Level-2 reduction on MI355X (gfx950).
+//
+// The reference reduces each (feed, scan) with NumPy/SciPy
+// (comancpipeline/Analysis/Level1Averaging.py:792-872).  Here every step is a
+// weighted sum of the raw f32 cube d[f][b][c][t] with per-channel f64
+// coefficients, so the whole observation is four streaming passes over HBM:
+//
+//   pass A  k_moments      per channel, over t: sum d, sum A d, and the
+//                          stride-4 difference moments (atmosphere fit +
+//                          normalise_data rms)                  -> 4 B/samp·ch
+//   pass B  k_band_mean    per t, over the 993 median channels: band mean of
+//                          y = (d - o - a A)/rms                -> 4 B/samp·ch
+//           k_sliding_median (median_kernels.hip) on the band means
+//   pass C  k_regress      per channel, over t: sum d mf        -> 4 B/samp·ch
+//   pass D  k_gain_avg     per t, over all 4096 channels: gain template sum
+//                          dG and both band averages            -> 4 B/samp·ch
+//
+// Layout: time is contiguous (the reference's [F][B][C][T]); a wave reads
+// 64 lanes x 16 B of one channel row per instruction (coalesced).  Pass A/C
+// waves own 4 channel rows and share the airmass / median loads; pass B/D
+// workgroups own a 256-sample tile with one wave per band.  All arithmetic
+// is f64 (the reference upcasts to f64 at subtract_fitted_atmosphere).
+#include "comap_internal.h"
+
+#include <cmath>
+
+using namespace comap;
+
+typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
+
+__device__ __forceinline__ double wave_sum(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Block-wide sum for 256-thread blocks (4 waves); every thread gets the total.
+__device__ __forceinline__ double block_sum256(double v, double *lds4)
+{
+    v = wave_sum(v);
+    const int wid = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) lds4[wid] = v;
+    __syncthreads();
+    double t = lds4[0] + lds4[1] + lds4[2] + lds4[3];
+    return t;
+}
+
+__device__ __forceinline__ bool atmos_channel(int c)
+{   // fit_atmosphere channel set: arange(10,1014) minus 510..514 (Level1Averaging.py:201-202)
+    return c >= 10 && c < 1014 && !(c >= 510 && c < 515);
+}
+
+__device__ __forceinline__ bool median_channel(int c)
+{   // median_filter index: 10..1013 minus 507..517 (Level1Averaging.py:688-690)
+    return c >= 10 && c < 1014 && !(c >= 507 && c <= 517);
+}
+
+__device__ __forceinline__ bool gain_masked(int c)
+{   // gain_subtraction_fit: [:20], [-20:], 512-5:512+5 (GainSubtraction.py:190-196)
+    return c < 20 || c >= 1004 || (c >= 507 && c < 517);
+}
+
+// ------------------------------------------------------------------ airmass
+// COMAPLevel1.airmass: 1/sin(el*pi/180) (DataHandling.py:398-401)
+__global__ void k_airmass(const double *__restrict__ el, double *__restrict__ A, int64_t n)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        A[i] = 1.0 / sin(el[i] * M_PI / 180.0);
+}
+
+// ------------------------------------------------------------------ per-unit airmass sums
+// us[u] = {n, sum A, sum A^2, sum v, sum v^2, N4}, v_k = A[4k] - A[4k+2]
+__global__ void __launch_bounds__(256) k_unit_sums(const int32_t *__restrict__ units,
+                                                   const double *__restrict__ A, int64_t T,
+                                                   double *__restrict__ us)
+{
+    __shared__ double red[4];
+    const int u = blockIdx.x;
+    const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
+    const double *a = A + (int64_t)f * T + t0;
+    double sa = 0, saa = 0, sv = 0, svv = 0;
+    for (int t = threadIdx.x; t < n; t += blockDim.x) {
+        double x = a[t];
+        sa += x;
+        saa += x * x;
+    }
+    const int n4 = n / 4;
+    for (int k = threadIdx.x; k < n4; k += blockDim.x) {
+        double v = a[4 * k] - a[4 * k + 2];
+        sv += v;
+        svv += v * v;
+    }
+    sa = block_sum256(sa, red);
+    saa = block_sum256(saa, red);
+    sv = block_sum256(sv, red);
+    svv = block_sum256(svv, red);
+    if (threadIdx.x == 0) {
+        double *o = us + 8 * (int64_t)u;
+        o[0] = n; o[1] = sa; o[2] = saa; o[3] = sv; o[4] = svv; o[5] = n4;
+    }
+}
+
+// ------------------------------------------------------------------ pass A
+// Per (unit, band, channel): Sd = sum d, SAd = sum A d over the scan, and over
+// the stride-4 pairs u_k = d[4k]-d[4k+2]: Su, Suu, Suv (v_k = A[4k]-A[4k+2]).
+// normalise_data's rms for ANY atmosphere slope a follows in closed form:
+//   diff_k = u_k - a v_k  (the offset cancels).
+constexpr int kCPW = 4;   // channel rows per wave
+__global__ void __launch_bounds__(256) k_moments(const float *__restrict__ tod, const double *__restrict__ A,
+                                                 const int32_t *__restrict__ units, int64_t T,
+                                                 double *__restrict__ mom, int64_t UC, int32_t *nan_count)
+{
+    const int wid = uniform(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int groups_per_band = kChannels / (4 * kCPW);
+    int bid = blockIdx.x;
+    const int g = bid % groups_per_band; bid /= groups_per_band;
+    const int b = bid % kBands;
+    const int u = bid / kBands;
+    const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
+    const int c0 = g * 4 * kCPW + wid * kCPW;
+    const float *row0 = tod + ((int64_t)(f * kBands + b) * kChannels + c0) * T + t0;
+    const double *a = A + (int64_t)f * T + t0;
+
+    double sd[kCPW], sad[kCPW], su[kCPW], suu[kCPW], suv[kCPW];
+#pragma unroll
+    for (int r = 0; r < kCPW; ++r) sd[r] = sad[r] = su[r] = suu[r] = suv[r] = 0.0;
+    int bad = 0;
+    const int n4 = n >> 2;
+    for (int k = lane; k < n4; k += 64) {
+        const double a0 = a[4 * k], a1 = a[4 * k + 1], a2 = a[4 * k + 2], a3 = a[4 * k + 3];
+        const double v = a0 - a2;
+#pragma unroll
+        for (int r = 0; r < kCPW; ++r) {
+            const f32x4u x = *reinterpret_cast<const f32x4u *>(row0 + (int64_t)r * T + 4 * k);
+            const double x0 = x.x, x1 = x.y, x2 = x.z, x3 = x.w;
+            bad += !isfinite(x.x) + !isfinite(x.y) + !isfinite(x.z) + !isfinite(x.w);
+            sd[r] += (x0 + x1) + (x2 + x3);
+            sad[r] = fma(a0, x0, sad[r]);
+            sad[r] = fma(a1, x1, sad[r]);
+            sad[r] = fma(a2, x2, sad[r]);
+            sad[r] = fma(a3, x3, sad[r]);
+            const double uu = x0 - x2;
+            su[r] += uu;
+            suu[r] = fma(uu, uu, suu[r]);
+            suv[r] = fma(uu, v, suv[r]);
+        }
+    }
+    // tail samples n4*4 .. n-1 (at most 3)
+    const int tt = 4 * n4 + lane;
+    if (lane < 4 && tt < n) {
+        const double at = a[tt];
+#pragma unroll
+        for (int r = 0; r < kCPW; ++r) {
+            const float xf = row0[(int64_t)r * T + tt];
+            bad += !isfinite(xf);
+            sd[r] += (double)xf;
+            sad[r] = fma(at, (double)xf, sad[r]);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < kCPW; ++r) {
+        const double s0 = wave_sum(sd[r]), s1 = wave_sum(sad[r]), s2 = wave_sum(su[r]);
+        const double s3 = wave_sum(suu[r]), s4 = wave_sum(suv[r]);
+        if (lane == 0) {
+            const int64_t idx = (int64_t)u * kBC + b * kChannels + c0 + r;
+            mom[idx] = s0;
+            mom[UC + idx] = s1;
+            mom[2 * UC + idx] = s2;
+            mom[3 * UC + idx] = s3;
+            mom[4 * UC + idx] = s4;
+        }
+    }
+    if (bad) atomicAdd(nan_count, bad);
+}
+
+// ------------------------------------------------------------------ atmosphere fit
+// AtmosphereRemoval.fit_atmosphere (Level1Averaging.py:197-227): the
+// block-diagonal spsolve is an independent 2x2 normal-equation solve per
+// channel: [[n, SA],[SA, SAA]] [o, a]^T = [Sd, SAd]^T.
+__global__ void k_atmos_fit(const int32_t *__restrict__ units, const double *__restrict__ us,
+                            const double *__restrict__ mom, int64_t UC, int F, int U,
+                            double *__restrict__ fit)
+{
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= (int64_t)U * kBC) return;
+    const int u = (int)(i / kBC);
+    const int bc = (int)(i % kBC);
+    const int b = bc / kChannels, c = bc % kChannels;
+    const int f = units[4 * u], s = units[4 * u + 1];
+    const double *q = us + 8 * (int64_t)u;
+    const double n = q[0], sa = q[1], saa = q[2];
+    double o = NAN, a = NAN;
+    if (atmos_channel(c) && n >= 100.0) {
+        const double sd = mom[i], sad = mom[UC + i];
+        const double det = n * saa - sa * sa;
+        o = (saa * sd - sa * sad) / det;
+        a = (n * sad - sa * sd) / det;
+    }
+    double *out = fit + (((int64_t)s * F + f) * kBands + b) * 2 * kChannels;
+    out[c] = o;
+    out[kChannels + c] = a;
+}
+
+// ------------------------------------------------------------------ L1AGC coefficients I
+// normalise_data (Level1Averaging.py:667-679): rms from the pass-A moments for
+// the fit slope a; pass-B coefficients alpha_c = 1/rms on the median
+// channels; per (unit, band): beta = sum alpha o, gamma = sum alpha a, N.
+__global__ void __launch_bounds__(256) k_coef_b(const int32_t *__restrict__ units, const double *__restrict__ us,
+                                                const double *__restrict__ mom, int64_t UC,
+                                                const double *__restrict__ fit, int F,
+                                                double *__restrict__ alpha, double *__restrict__ nf,
+                                                double *__restrict__ bsum)
+{
+    __shared__ double red[4];
+    const int ub = blockIdx.x;
+    const int u = ub / kBands, b = ub % kBands;
+    const int f = units[4 * u], s = units[4 * u + 1], n = units[4 * u + 3];
+    const double *q = us + 8 * (int64_t)u;
+    const double sv = q[3], svv = q[4], n4 = q[5];
+    const double *fo = fit + (((int64_t)s * F + f) * kBands + b) * 2 * kChannels;
+    double beta = 0, gamma = 0, cnt = 0;
+    for (int c = threadIdx.x; c < kChannels; c += blockDim.x) {
+        const int64_t i = (int64_t)u * kBC + b * kChannels + c;
+        const double o = fo[c], a = fo[kChannels + c];
+        double rms = NAN;
+        if (n4 > 0 && isfinite(o) && isfinite(a)) {
+            const double su = mom[2 * UC + i], suu = mom[3 * UC + i], suv = mom[4 * UC + i];
+            const double mean = (su - a * sv) / n4;
+            double var = (suu - 2.0 * a * suv + a * a * svv) / n4 - mean * mean;
+            var = var < 0.0 ? 0.0 : var;
+            rms = sqrt(var) / sqrt(2.0) * sqrt(kDnuTau);
+        }
+        nf[i] = rms;
+        double al = 0.0;
+        if (median_channel(c)) {
+            al = 1.0 / rms;
+            if (isfinite(al) && isfinite(o) && isfinite(a)) {
+                beta += al * o;
+                gamma += al * a;
+                cnt += 1.0;
+            } else {
+                al = 0.0;
+            }
+        }
+        alpha[i] = al;
+    }
+    beta = block_sum256(beta, red);
+    gamma = block_sum256(gamma, red);
+    cnt = block_sum256(cnt, red);
+    if (threadIdx.x == 0) {
+        double *o = bsum + 4 * (int64_t)ub;
+        o[0] = beta; o[1] = gamma; o[2] = cnt;
+        // median_filter skips the band when fewer than 2w finite band-mean samples
+        o[3] = (cnt > 0 && n >= 2 * kMedfiltWindow) ? 1.0 : 0.0;
+    }
+}
+
+// ------------------------------------------------------------------ pass B
+// Band mean over the median channels (nanmean, Level1Averaging.py:691-692):
+//   m_t = (sum_c alpha_c d_ct - beta - gamma A_t) / N
+__global__ void __launch_bounds__(256) k_band_mean(const float *__restrict__ tod, const double *__restrict__ A,
+                                                   const int32_t *__restrict__ units, const int32_t *__restrict__ tiles,
+                                                   int64_t T, const double *__restrict__ alpha,
+                                                   const double *__restrict__ bsum, double *__restrict__ mb)
+{
+    const int b = uniform(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int u = tiles[2 * blockIdx.x], toff = tiles[2 * blockIdx.x + 1];
+    const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
+    const int r0 = toff + 4 * lane;                 // first sample (relative) of this lane
+    const int64_t rowstride = T;
+    const float *base = tod + (int64_t)(f * kBands + b) * kChannels * T + t0 + r0;
+    const double *al = alpha + (int64_t)u * kBC + b * kChannels;
+    double acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0;
+    const bool full = (r0 + 3 < n);
+    const int nv = n - r0;   // valid samples for this lane (may be <= 0)
+    auto body = [&](int c) {
+        const double w = al[c];
+        const float *p = base + (int64_t)c * rowstride;
+        if (full) {
+            const f32x4u x = *reinterpret_cast<const f32x4u *>(p);
+            acc0 = fma(w, (double)x.x, acc0);
+            acc1 = fma(w, (double)x.y, acc1);
+            acc2 = fma(w, (double)x.z, acc2);
+            acc3 = fma(w, (double)x.w, acc3);
+        } else {
+            if (nv > 0) acc0 = fma(w, (double)p[0], acc0);
+            if (nv > 1) acc1 = fma(w, (double)p[1], acc1);
+            if (nv > 2) acc2 = fma(w, (double)p[2], acc2);
+        }
+    };
+#pragma unroll 8
+    for (int c = 10; c < 507; ++c) body(c);
+#pragma unroll 8
+    for (int c = 518; c < 1014; ++c) body(c);
+    const double *bs = bsum + 4 * ((int64_t)u * kBands + b);
+    const double beta = bs[0], gamma = bs[1], cnt = bs[2];
+    double *out = mb + (int64_t)(f * kBands + b) * T + t0 + r0;
+    const double *a = A + (int64_t)f * T + t0 + r0;
+    const double accs[4] = {acc0, acc1, acc2, acc3};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (j < nv) out[j] = cnt > 0 ? (accs[j] - beta - gamma * a[j]) / cnt : NAN;
+}
+
+// ------------------------------------------------------------------ series sums for pass C
+// ss[ub] = {sum mf, sum mf^2, sum A mf}; zeroes mf of skipped bands.
+__global__ void __launch_bounds__(256) k_series_sums(const int32_t *__restrict__ units, const double *__restrict__ A,
+                                                     int64_t T, const double *__restrict__ bsum,
+                                                     double *__restrict__ mf, double *__restrict__ ss)
+{
+    __shared__ double red[4];
+    const int ub = blockIdx.x;
+    const int u = ub / kBands, b = ub % kBands;
+    const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
+    const bool run = bsum[4 * (int64_t)ub + 3] > 0;
+    double *m = mf + (int64_t)(f * kBands + b) * T + t0;
+    const double *a = A + (int64_t)f * T + t0;
+    double s0 = 0, s1 = 0, s2 = 0;
+    for (int t = threadIdx.x; t < n; t += blockDim.x) {
+        if (!run) { m[t] = 0.0; continue; }
+        const double x = m[t];
+        s0 += x;
+        s1 = fma(x, x, s1);
+        s2 = fma(a[t], x, s2);
+    }
+    s0 = block_sum256(s0, red);
+    s1 = block_sum256(s1, red);
+    s2 = block_sum256(s2, red);
+    if (threadIdx.x == 0) {
+        double *o = ss + 4 * (int64_t)ub;
+        o[0] = s0; o[1] = s1; o[2] = s2;
+    }
+}
+
+// ------------------------------------------------------------------ pass C
+// Regression of each median channel on [1, mf] (Level1Averaging.py:701-705):
+// only sum_t d mf is new (sum d came from pass A).
+__global__ void __launch_bounds__(256) k_regress(const float *__restrict__ tod, const double *__restrict__ mf,
+                                                 const int32_t *__restrict__ units, int64_t T,
+                                                 const double *__restrict__ bsum, double *__restrict__ sdm)
+{
+    const int wid = uniform(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int groups_per_band = kChannels / (4 * kCPW);
+    int bid = blockIdx.x;
+    const int g = bid % groups_per_band; bid /= groups_per_band;
+    const int b = bid % kBands;
+    const int u = bid / kBands;
+    const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
+    const int c0 = g * 4 * kCPW + wid * kCPW;
+    const int64_t ob = (int64_t)u * kBC + b * kChannels + c0;
+    if (bsum[4 * ((int64_t)u * kBands + b) + 3] <= 0) {   // band skipped by the median filter
+        if (lane < kCPW) sdm[ob + lane] = 0.0;
+        return;
+    }
+    const float *row0 = tod + ((int64_t)(f * kBands + b) * kChannels + c0) * T + t0;
+    const double *m = mf + (int64_t)(f * kBands + b) * T + t0;
+    double acc[kCPW];
+#pragma unroll
+    for (int r = 0; r < kCPW; ++r) acc[r] = 0.0;
+    const int n4 = n >> 2;
+    for (int k = lane; k < n4; k += 64) {
+        const double m0 = m[4 * k], m1 = m[4 * k + 1], m2 = m[4 * k + 2], m3 = m[4 * k + 3];
+#pragma unroll
+        for (int r = 0; r < kCPW; ++r) {
+            const f32x4u x = *reinterpret_cast<const f32x4u *>(row0 + (int64_t)r * T + 4 * k);
+            double s = acc[r];
+            s = fma(m0, (double)x.x, s);
+            s = fma(m1, (double)x.y, s);
+            s = fma(m2, (double)x.z, s);
+            s = fma(m3, (double)x.w, s);
+            acc[r] = s;
+        }
+    }
+    const int tt = 4 * n4 + lane;
+    if (lane < 4 && tt < n) {
+#pragma unroll
+        for (int r = 0; r < kCPW; ++r) acc[r] = fma(m[tt], (double)row0[(int64_t)r * T + tt], acc[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < kCPW; ++r) {
+        const double s = wave_sum(acc[r]);
+        if (lane == 0) sdm[ob + r] = s;
+    }
+}
+
+// ------------------------------------------------------------------ gain template weights
+// gain_subtraction_fit + AMatrix + cg (GainSubtraction.py:17-209) in closed
+// form: A = P^T Z P = c I, so dG_t = sum_nu w_nu y_nu,t with w = ZP / c.
+// mode: 0 solve, 1 all Tsys NaN (dG = 0), 2 C not finite (ValueError -> dG None).
+__global__ void __launch_bounds__(1024) k_gain_weights(const double *__restrict__ tsys0,
+                                                       double *__restrict__ gw, int32_t *__restrict__ gmode)
+{
+    __shared__ double red[16][7];
+    const int f = blockIdx.x;
+    const double *ts = tsys0 + (int64_t)f * kBC;
+    double c00 = 0, c01 = 0, c11 = 0, b0 = 0, b1 = 0, nbad = 0, pp = 0;
+    double t0v[4], t1v[4], pv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = threadIdx.x + r * 1024;
+        const int c = i % kChannels;
+        const double tsv = ts[i];
+        const double v = -1.0 + 2.0 * (double)i / (double)(kBC - 1);   // linspace(-1,1,4096)
+        double T0 = 1.0 / tsv, T1 = v / tsv, P = 1.0;
+        const bool bad = isnan(tsv);
+        if (bad) nbad += 1.0;
+        if (gain_masked(c) || bad) { T0 = 0.0; T1 = 0.0; P = 0.0; }
+        t0v[r] = T0; t1v[r] = T1; pv[r] = P;
+        c00 += T0 * T0; c01 += T0 * T1; c11 += T1 * T1;
+        b0 += T0 * P; b1 += T1 * P; pp += P;
+    }
+    double vals[7] = {c00, c01, c11, b0, b1, nbad, pp};
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        double s = wave_sum(vals[k]);
+        if (lane == 0) red[wid][k] = s;
+    }
+    __syncthreads();
+    double tot[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        double s = 0;
+        for (int w = 0; w < 16; ++w) s += red[w][k];
+        tot[k] = s;
+    }
+    c00 = tot[0]; c01 = tot[1]; c11 = tot[2]; b0 = tot[3]; b1 = tot[4]; nbad = tot[5];
+    int mode = 0;
+    if (nbad == (double)kBC) mode = 1;
+    else if (!isfinite(c00 + c01 + c01 + c11)) mode = 2;
+    // inv(C) applied to T01^T P
+    const double det = c00 * c11 - c01 * c01;
+    const double g0 = (c11 * b0 - c01 * b1) / det;
+    const double g1 = (-c01 * b0 + c00 * b1) / det;
+    // c = P^T Z P = sum P (P - T0 g0 - T1 g1)
+    double cz = 0;
+    double zp[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        zp[r] = pv[r] - (t0v[r] * g0 + t1v[r] * g1);
+        cz += pv[r] * zp[r];
+    }
+    __syncthreads();
+    double s = wave_sum(cz);
+    if (lane == 0) red[wid][0] = s;
+    __syncthreads();
+    double ctot = 0;
+    for (int w = 0; w < 16; ++w) ctot += red[w][0];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = threadIdx.x + r * 1024;
+        gw[(int64_t)f * kBC + i] = (mode == 0) ? zp[r] / ctot : 0.0;
+    }
+    if (threadIdx.x == 0) gmode[f] = mode;
+}
+
+// ------------------------------------------------------------------ L1AGC coefficients II
+// Regression solve + the filtered-TOD coefficients f_ct = fa d + fb + fg A_t + fd mf_t
+// and the three channel weightings pass D sums:
+//   Kg   gain template weights (dG), zero unless the gain fit ran
+//   Kres weighted_average_over_band weights * nf / g      (residual)
+//   Korig the same weights * Tsys                          (tod_original)
+// Level1Averaging.py:701-705, 710-725, 841-867; GainSubtraction.py:190-201.
+// dsum[ub][..] = {Sg_b, Gg_b, Dg_b, Sr_b, Gr_b, Dr_b, So_b, Go_b, Do_b, SKr, SW, SWo}
+__global__ void __launch_bounds__(256) k_coef_d(const int32_t *__restrict__ units, const double *__restrict__ us,
+                                                const double *__restrict__ mom, int64_t UC,
+                                                const double *__restrict__ fit, int F,
+                                                const double *__restrict__ alpha, const double *__restrict__ nf,
+                                                const double *__restrict__ bsum, const double *__restrict__ ss,
+                                                const double *__restrict__ sdm, const double *__restrict__ tsys0,
+                                                const double *__restrict__ gain0, const double *__restrict__ gw,
+                                                const int32_t *__restrict__ gmode, int calibrator,
+                                                double *__restrict__ kap, double *__restrict__ dsum,
+                                                double *__restrict__ xreg)
+{
+    __shared__ double red[4];
+    const int ub = blockIdx.x;
+    const int u = ub / kBands, b = ub % kBands;
+    const int f = units[4 * u], s = units[4 * u + 1];
+    const double *q = us + 8 * (int64_t)u;
+    const double n = q[0], SA = q[1];
+    const double *bs = bsum + 4 * (int64_t)ub;
+    const bool band_on = bs[3] > 0;
+    const double *sq = ss + 4 * (int64_t)ub;
+    const double Smf = sq[0], Smm = sq[1], SAm = sq[2];
+    const double *fo = fit + (((int64_t)s * F + f) * kBands + b) * 2 * kChannels;
+    const int gm = gmode[f];
+    // gain path (Level1Averaging.py:710-725, 834-838):
+    //   zero: y zeroed on the gain mask (gain function was called)
+    //   use_dg: dG enters the residual
+    const bool gain_called = !calibrator;
+    const bool zero = gain_called;
+    const bool use_dg = gain_called && gm == 0;
+    const double det = n * Smm - Smf * Smf;
+    double acc[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) acc[k] = 0.0;
+    for (int c = threadIdx.x; c < kChannels; c += blockDim.x) {
+        const int64_t i = (int64_t)u * kBC + b * kChannels + c;
+        const double o = fo[c], a = fo[kChannels + c];
+        const double al = alpha[i];
+        const double tsv = tsys0[(int64_t)f * kBC + b * kChannels + c];
+        // ---- filtered TOD coefficients
+        double fa = 0, fb = 0, fg = 0, fd = 0, x0 = 0, x1 = 0;
+        if (band_on && median_channel(c)) {
+            if (al != 0.0) {
+                const double sy = al * (mom[i] - n * o - a * SA);
+                const double sym = al * (sdm[i] - o * Smf - a * SAm);
+                x0 = (Smm * sy - Smf * sym) / det;
+                x1 = (n * sym - Smf * sy) / det;
+                fa = al; fb = -(al * o + x0); fg = -al * a; fd = -x1;
+            } else {                      // NaN channel inside the regression set
+                fa = NAN; fb = NAN; fg = NAN; fd = NAN; x0 = NAN; x1 = NAN;
+            }
+        }
+        xreg[2 * i] = x0;
+        xreg[2 * i + 1] = x1;
+        if (zero && (gain_masked(c) || isnan(tsv))) { fa = fb = fg = fd = 0.0; }
+        const bool fnan = isnan(fa) || isnan(fb) || isnan(fg) || isnan(fd);
+        // ---- gain template weight
+        const double kg = use_dg ? gw[(int64_t)f * kBC + b * kChannels + c] : 0.0;
+        // ---- band-average weights (Level1Averaging.py:841-845, 593-596)
+        double W = 1.0 / (tsv * tsv);
+        if (tsv == 0.0) W = 0.0;
+        if (c < 50 || c >= 974 || c == 512 || (c >= 510 && c < 515)) W = 0.0;
+        const double nfg = nf[i] / gain0[(int64_t)f * kBC + b * kChannels + c];
+        if (isnan(nfg) || fnan) W = 0.0;                       // residual[...,0] NaN
+        const double kr = W * nfg;
+        double Wo = W;
+        if (isnan(tsv) || fnan) Wo = 0.0;                      // (clean*Tsys)[...,0] NaN
+        const double ko = Wo * tsv;
+        // ---- kappa (zero weights contribute exactly nothing, as NaN->0 does)
+        const double kgfa = (kg == 0.0) ? 0.0 : kg * fa;
+        const double krfa = (kr == 0.0) ? 0.0 : kr * fa;
+        const double kofa = (ko == 0.0) ? 0.0 : ko * fa;
+        kap[i] = kgfa;
+        kap[UC + i] = krfa;
+        kap[2 * UC + i] = kofa;
+        if (kg != 0.0) { acc[0] += kg * fb; acc[1] += kg * fg; acc[2] += kg * fd; }
+        if (kr != 0.0) { acc[3] += kr * fb; acc[4] += kr * fg; acc[5] += kr * fd; acc[9] += kr; }
+        if (ko != 0.0) { acc[6] += ko * fb; acc[7] += ko * fg; acc[8] += ko * fd; }
+        acc[10] += W;
+        acc[11] += Wo;
+    }
+#pragma unroll
+    for (int k = 0; k < 12; ++k) acc[k] = block_sum256(acc[k], red);
+    if (threadIdx.x == 0) {
+        double *o = dsum + 16 * (int64_t)ub;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) o[k] = acc[k];
+    }
+}
+
+// ------------------------------------------------------------------ pass D
+// Per 256-sample tile: wave b sums its band's 1024 channels with kappa_g,
+// kappa_r, kappa_o; dG_t = sum over the 4 bands; then
+//   tod_b  = (Sr_b - dG SKr_b) / SW_b           (residual band average)
+//   orig_b = So_b / SWo_b                        (tod_original)
+__global__ void __launch_bounds__(256) k_gain_avg(const float *__restrict__ tod, const double *__restrict__ A,
+                                                  const int32_t *__restrict__ units, const int32_t *__restrict__ tiles,
+                                                  int64_t T, int64_t UC, const double *__restrict__ kap,
+                                                  const double *__restrict__ dsum, const double *__restrict__ mf,
+                                                  double *__restrict__ tod_out, double *__restrict__ orig_out,
+                                                  double *__restrict__ dG_out)
+{
+    __shared__ double sg[kBands][kTile];
+    const int b = uniform(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int u = tiles[2 * blockIdx.x], toff = tiles[2 * blockIdx.x + 1];
+    const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
+    const int r0 = toff + 4 * lane;
+    const float *base = tod + (int64_t)(f * kBands + b) * kChannels * T + t0 + r0;
+    const int64_t kb = (int64_t)u * kBC + b * kChannels;
+    const double *kg = kap + kb, *kr = kap + UC + kb, *ko = kap + 2 * UC + kb;
+    double g0 = 0, g1 = 0, g2 = 0, g3 = 0, rr0 = 0, rr1 = 0, rr2 = 0, rr3 = 0, o0 = 0, o1 = 0, o2 = 0, o3 = 0;
+    const bool full = (r0 + 3 < n);
+    const int nv = n - r0;
+#pragma unroll 4
+    for (int c = 0; c < kChannels; ++c) {
+        const double wg = kg[c], wr = kr[c], wo = ko[c];
+        const float *p = base + (int64_t)c * T;
+        double x0, x1, x2, x3;
+        if (full) {
+            const f32x4u x = *reinterpret_cast<const f32x4u *>(p);
+            x0 = x.x; x1 = x.y; x2 = x.z; x3 = x.w;
+        } else {
+            x0 = nv > 0 ? (double)p[0] : 0.0;
+            x1 = nv > 1 ? (double)p[1] : 0.0;
+            x2 = nv > 2 ? (double)p[2] : 0.0;
+            x3 = 0.0;
+        }
+        g0 = fma(wg, x0, g0); g1 = fma(wg, x1, g1); g2 = fma(wg, x2, g2); g3 = fma(wg, x3, g3);
+        rr0 = fma(wr, x0, rr0); rr1 = fma(wr, x1, rr1); rr2 = fma(wr, x2, rr2); rr3 = fma(wr, x3, rr3);
+        o0 = fma(wo, x0, o0); o1 = fma(wo, x1, o1); o2 = fma(wo, x2, o2); o3 = fma(wo, x3, o3);
+    }
+    const double *ds = dsum + 16 * ((int64_t)u * kBands + b);
+    const double *a = A + (int64_t)f * T + t0;
+    const double *m = mf + (int64_t)(f * kBands + b) * T + t0;
+    const double gs[4] = {g0, g1, g2, g3}, rs[4] = {rr0, rr1, rr2, rr3}, os[4] = {o0, o1, o2, o3};
+    double at[4], mt[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const bool ok = j < nv;
+        at[j] = ok ? a[r0 + j] : 0.0;
+        mt[j] = ok ? m[r0 + j] : 0.0;
+        sg[b][4 * lane + j] = gs[j] + ds[0] + at[j] * ds[1] + mt[j] * ds[2];
+    }
+    __syncthreads();
+    double *to = tod_out + (int64_t)(f * kBands + b) * T + t0 + r0;
+    double *oo = orig_out + (int64_t)(f * kBands + b) * T + t0 + r0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (j >= nv) break;
+        const int tl = 4 * lane + j;
+        const double dG = sg[0][tl] + sg[1][tl] + sg[2][tl] + sg[3][tl];
+        const double sr = rs[j] + ds[3] + at[j] * ds[4] + mt[j] * ds[5];
+        const double so = os[j] + ds[6] + at[j] * ds[7] + mt[j] * ds[8];
+        to[j] = (sr - dG * ds[9]) / ds[10];
+        oo[j] = so / ds[11];
+        if (b == 0) dG_out[(int64_t)f * T + t0 + r0 + j] = dG;
+    }
+}
+
+// ------------------------------------------------------------------ scan weights
+// averaged_tod/weights = 1/auto_rms(residual)^2 per (band, scan)
+// (Level1Averaging.py:512-518, 867): nanstd of odd-even differences, ddof 0.
+__global__ void __launch_bounds__(256) k_scan_weights(const int32_t *__restrict__ units, int64_t T,
+                                                      const double *__restrict__ tod_out, double *__restrict__ w_out)
+{
+    __shared__ double red[4];
+    const int ub = blockIdx.x;
+    const int u = ub / kBands, b = ub % kBands;
+    const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
+    const double *r = tod_out + (int64_t)(f * kBands + b) * T + t0;
+    const int np = n / 2;
+    double s = 0, cnt = 0;
+    for (int k = threadIdx.x; k < np; k += blockDim.x) {
+        const double d = r[2 * k + 1] - r[2 * k];
+        if (!isnan(d)) { s += d; cnt += 1.0; }
+    }
+    s = block_sum256(s, red);
+    cnt = block_sum256(cnt, red);
+    const double mean = s / cnt;
+    double v = 0;
+    for (int k = threadIdx.x; k < np; k += blockDim.x) {
+        const double d = r[2 * k + 1] - r[2 * k];
+        if (!isnan(d)) v += (d - mean) * (d - mean);
+    }
+    v = block_sum256(v, red);
+    const double rms = sqrt(v / cnt) / sqrt(2.0);
+    const double wt = 1.0 / (rms * rms);
+    double *wo = w_out + (int64_t)(f * kBands + b) * T + t0;
+    for (int t = threadIdx.x; t < n; t += blockDim.x) wo[t] = wt;
+}
+
+// ------------------------------------------------------------------ vane
+// system_temperature_from_tod (VaneCalibration.py:67-82): per channel nanmean
+// over the hot and cold samples of the vane event; one wave per channel row.
+__global__ void __launch_bounds__(256) k_vane(const float *__restrict__ tod, int64_t T, int F,
+                                              int64_t vstart, const int32_t *__restrict__ hot,
+                                              const int64_t *__restrict__ hoff, const int32_t *__restrict__ cold,
+                                              const int64_t *__restrict__ coff, double t_hot,
+                                              double *__restrict__ tsys, double *__restrict__ gain)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);   // (f*4+b)*1024 + c
+    if (row >= (int64_t)F * kBC) return;
+    const int fb = (int)(row / kChannels);
+    const float *p = tod + row * T + vstart;
+    const int64_t h0 = hoff[fb], h1 = hoff[fb + 1], k0 = coff[fb], k1 = coff[fb + 1];
+    if (h1 == h0) return;   // no hot/cold found (RuntimeError path): leave zeros
+    // an empty cold list (all cold samples before the last hot one) gives NaN, as nanmean([]) does
+    double sh = 0, nh = 0, sc = 0, nc = 0;
+    for (int64_t j = h0 + lane; j < h1; j += 64) {
+        const float x = p[hot[j]];
+        if (!isnan(x)) { sh += x; nh += 1.0; }
+    }
+    for (int64_t j = k0 + lane; j < k1; j += 64) {
+        const float x = p[cold[j]];
+        if (!isnan(x)) { sc += x; nc += 1.0; }
+    }
+    sh = wave_sum(sh); nh = wave_sum(nh); sc = wave_sum(sc); nc = wave_sum(nc);
+    if (lane == 0) {
+        const double th = sh / nh, tc = sc / nc;
+        const double g = (th - tc) / (t_hot - 2.73);
+        gain[row] = g;
+        tsys[row] = tc / g;
+    }
+}
+
+// ================================================================== host side
+// HIP events around each launch on the plan's stream (comap_l1_profile)
+static int prof_begin(comap_l1_plan *p)
+{
+    if (!p->prof_on) return -1;
+    const int idx = (int)p->prof_rec.size() * 2;
+    while ((int)p->prof_pool.size() < idx + 2) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return -1;
+        p->prof_pool.push_back(e);
+    }
+    (void)hipEventRecord(p->prof_pool[idx], p->ctx->stream);
+    return idx;
+}
+
+static void prof_end(comap_l1_plan *p, int id, int idx)
+{
+    if (idx < 0) return;
+    (void)hipEventRecord(p->prof_pool[idx + 1], p->ctx->stream);
+    p->prof_rec.push_back({id, idx});
+}
+
+#define PROF(p, id, ...)                     \
+    do {                                     \
+        const int _pi = prof_begin(p);       \
+        __VA_ARGS__;                         \
+        prof_end(p, id, _pi);                \
+    } while (0)
+
+extern "C" int comap_l1_profile(comap_l1_plan *p, int32_t enable)
+{
+    if (!p) return -1;
+    p->prof_on = enable != 0;
+    return 0;
+}
+
+extern "C" int comap_l1_profile_collect(comap_l1_plan *p, double *ms, int64_t *counts, int32_t n)
+{
+    if (!p || !ms || !counts) return -1;
+    comap_ctx *ctx = p->ctx;
+    COMAP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    for (auto &r : p->prof_rec) {
+        float t = 0.f;
+        COMAP_CHECK(ctx, hipEventElapsedTime(&t, p->prof_pool[r.second], p->prof_pool[r.second + 1]));
+        p->prof_ms[r.first] += t;
+        p->prof_n[r.first] += 1;
+    }
+    p->prof_rec.clear();
+    for (int i = 0; i < n && i < 32; ++i) {
+        ms[i] = p->prof_ms[i];
+        counts[i] = p->prof_n[i];
+        p->prof_ms[i] = 0;
+        p->prof_n[i] = 0;
+    }
+    return 0;
+}
+
+static int upload(comap_ctx *ctx, void **dst, const void *src, size_t bytes)
+{
+    COMAP_CHECK(ctx, hipMalloc(dst, bytes ? bytes : 8));
+    if (bytes) COMAP_CHECK(ctx, hipMemcpyAsync(*dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    return 0;
+}
+
+template <typename T>
+static int dalloc(comap_ctx *ctx, T **p, size_t count)
+{
+    COMAP_CHECK(ctx, hipMalloc((void **)p, sizeof(T) * (count ? count : 1)));
+    return 0;
+}
+
+extern "C" int comap_l1_plan_create(comap_ctx *ctx, const comap_obs_desc *d, comap_l1_plan **out)
+{
+    if (!ctx || !d || !out) return -1;
+    if (d->n_bands != kBands || d->n_channels != kChannels)
+        return comap_fail(ctx, -1, "only 4 bands x 1024 channels are supported");
+    if (d->n_units <= 0 || d->n_samples <= 0 || d->n_feeds <= 0)
+        return comap_fail(ctx, -1, "empty observation");
+    COMAP_CHECK(ctx, hipSetDevice(ctx->device));
+    auto *p = new comap_l1_plan();
+    p->ctx = ctx;
+    p->F = d->n_feeds; p->S = d->n_scans; p->U = d->n_units; p->T = d->n_samples;
+    p->tod = d->tod; p->el = d->el;
+    p->units_h.assign(d->units_host, d->units_host + 4 * (size_t)d->n_units);
+    for (int u = 0; u < p->U; ++u) {
+        const int32_t *q = &p->units_h[4 * u];
+        if (q[0] < 0 || q[0] >= p->F || q[1] < 0 || q[1] >= p->S || q[2] < 0 || q[3] < 1 ||
+            (int64_t)q[2] + q[3] > p->T) {
+            delete p;
+            return comap_fail(ctx, -1, "unit out of range");
+        }
+    }
+    std::vector<int32_t> tiles;
+    for (int u = 0; u < p->U; ++u)
+        for (int t = 0; t < p->units_h[4 * u + 3]; t += kTile) { tiles.push_back(u); tiles.push_back(t); }
+    p->n_tiles = (int64_t)tiles.size() / 2;
+    const int64_t UC = (int64_t)p->U * kBC;
+    int rc = 0;
+    rc |= upload(ctx, (void **)&p->units, p->units_h.data(), p->units_h.size() * 4);
+    rc |= upload(ctx, (void **)&p->tiles, tiles.data(), tiles.size() * 4);
+    rc |= dalloc(ctx, &p->airmass, (size_t)p->F * p->T);
+    rc |= dalloc(ctx, &p->unit_sums, 8 * (size_t)p->U);
+    rc |= dalloc(ctx, &p->mom, 5 * (size_t)UC);
+    rc |= dalloc(ctx, &p->nan_count, 1);
+    rc |= dalloc(ctx, &p->alpha, UC);
+    rc |= dalloc(ctx, &p->nf, UC);
+    rc |= dalloc(ctx, &p->bsum, 4 * (size_t)p->U * kBands);
+    rc |= dalloc(ctx, &p->mb, (size_t)p->F * kBands * p->T);
+    rc |= dalloc(ctx, &p->mf, (size_t)p->F * kBands * p->T);
+    rc |= dalloc(ctx, &p->ssum, 4 * (size_t)p->U * kBands);
+    rc |= dalloc(ctx, &p->sdm, UC);
+    rc |= dalloc(ctx, &p->gw, (size_t)p->F * kBC);
+    rc |= dalloc(ctx, &p->gmode, p->F);
+    rc |= dalloc(ctx, &p->kap, 3 * (size_t)UC);
+    rc |= dalloc(ctx, &p->dsum, 16 * (size_t)p->U * kBands);
+    rc |= dalloc(ctx, &p->xreg, 2 * (size_t)UC);
+    rc |= dalloc(ctx, &p->dG, (size_t)p->F * p->T);
+    if (rc) { delete p; return -2; }
+    // median jobs: (unit, band) series, reflect-3 padded [rev, x, rev], outputs [n, 2n)
+    // (bands of scans shorter than 2w are skipped by median_filter: no outputs)
+    std::vector<MedJob> jobs((size_t)p->U * kBands);
+    for (int u = 0; u < p->U; ++u) {
+        const int32_t f = p->units_h[4 * u], t0 = p->units_h[4 * u + 2], n = p->units_h[4 * u + 3];
+        for (int b = 0; b < kBands; ++b) {
+            MedJob &j = jobs[(size_t)u * kBands + b];
+            const int64_t off = (int64_t)(f * kBands + b) * p->T + t0;
+            j.src = p->mb + off;
+            j.dst = p->mf + off;
+            j.n = n;
+            j.out_lo = n;
+            j.out_hi = (n >= 2 * kMedfiltWindow) ? 2 * (int64_t)n : (int64_t)n;
+            j.mode = 1;
+            j.pad_ = 0;
+            j.gate = p->bsum + 4 * ((int64_t)u * kBands + b) + 3;
+        }
+    }
+    rc = comap_median_plan(ctx, &p->med, jobs, kMedfiltWindow);
+    if (rc) { comap_l1_plan_destroy(p); return rc; }
+    // airmass and per-unit airmass sums depend only on the pointing
+    k_airmass<<<2048, 256, 0, ctx->stream>>>(p->el, p->airmass, (int64_t)p->F * p->T);
+    COMAP_LAUNCH_CHECK(ctx);
+    k_unit_sums<<<p->U, 256, 0, ctx->stream>>>(p->units, p->airmass, p->T, p->unit_sums);
+    COMAP_LAUNCH_CHECK(ctx);
+    *out = p;
+    return 0;
+}
+
+extern "C" int comap_l1_plan_destroy(comap_l1_plan *p)
+{
+    if (!p) return 0;
+    void *bufs[] = {p->units, p->tiles, p->airmass, p->unit_sums, p->mom,
+                    p->nan_count, p->alpha, p->nf, p->bsum, p->mb, p->mf, p->ssum, p->sdm, p->gw,
+                    p->gmode, p->kap, p->dsum, p->xreg, p->dG};
+    for (void *b : bufs)
+        if (b) (void)hipFree(b);
+    comap_median_plan_free(&p->med);
+    for (hipEvent_t e : p->prof_pool) (void)hipEventDestroy(e);
+    delete p;
+    return 0;
+}
+
+static int run_moments(comap_l1_plan *p)
+{
+    comap_ctx *ctx = p->ctx;
+    const int64_t UC = (int64_t)p->U * kBC;
+    COMAP_CHECK(ctx, hipMemsetAsync(p->nan_count, 0, 4, ctx->stream));
+    const int64_t grid = (int64_t)p->U * kBands * (kChannels / (4 * kCPW));
+    PROF(p, KV_MOMENTS, k_moments<<<grid, 256, 0, ctx->stream>>>(p->tod, p->airmass, p->units, p->T, p->mom, UC,
+                                                                 p->nan_count));
+    COMAP_LAUNCH_CHECK(ctx);
+    int32_t nanc = 0;
+    COMAP_CHECK(ctx, hipMemcpyAsync(&nanc, p->nan_count, 4, hipMemcpyDeviceToHost, ctx->stream));
+    COMAP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    if (nanc)
+        return comap_fail(ctx, -5, "non-finite samples in the Level-1 TOD: the NaN fill/"
+                                   "select_time path (fill_bad_data) is not implemented on the device");
+    p->moments_valid = true;
+    return 0;
+}
+
+extern "C" int comap_l1_atmosphere(comap_l1_plan *p, double *fit)
+{
+    if (!p || !fit) return -1;
+    comap_ctx *ctx = p->ctx;
+    int rc = run_moments(p);
+    if (rc) return rc;
+    const int64_t UC = (int64_t)p->U * kBC;
+    const int64_t n = UC;
+    PROF(p, KV_ATMOS_FIT, k_atmos_fit<<<(n + 255) / 256, 256, 0, ctx->stream>>>(p->units, p->unit_sums, p->mom, UC,
+                                                                                p->F, p->U, fit));
+    COMAP_LAUNCH_CHECK(ctx);
+    return 0;
+}
+
+extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const double *tsys0, const double *gain0,
+                                int32_t calibrator, double *tod_out, double *orig_out, double *w_out)
+{
+    if (!p || !fit || !tsys0 || !gain0 || !tod_out || !orig_out || !w_out) return -1;
+    comap_ctx *ctx = p->ctx;
+    if (calibrator)
+        return comap_fail(ctx, -4, "calibrator sources (per-channel median atmosphere) are not "
+                                   "implemented on the device");
+    if (!p->moments_valid) {
+        int rc = run_moments(p);
+        if (rc) return rc;
+    }
+    const int64_t UC = (int64_t)p->U * kBC;
+    const int UB = p->U * kBands;
+    hipStream_t st = ctx->stream;
+    PROF(p, KV_COEF_B, k_coef_b<<<UB, 256, 0, st>>>(p->units, p->unit_sums, p->mom, UC, fit, p->F, p->alpha,
+                                                    p->nf, p->bsum));
+    COMAP_LAUNCH_CHECK(ctx);
+    PROF(p, KV_BAND_MEAN, k_band_mean<<<p->n_tiles, 256, 0, st>>>(p->tod, p->airmass, p->units, p->tiles, p->T,
+                                                                  p->alpha, p->bsum, p->mb));
+    COMAP_LAUNCH_CHECK(ctx);
+    int rc = 0;
+    PROF(p, KV_MEDIAN, rc = comap_median_run(ctx, &p->med));
+    if (rc) return rc;
+    PROF(p, KV_SERIES_SUMS, k_series_sums<<<UB, 256, 0, st>>>(p->units, p->airmass, p->T, p->bsum, p->mf, p->ssum));
+    COMAP_LAUNCH_CHECK(ctx);
+    const int64_t grid = (int64_t)p->U * kBands * (kChannels / (4 * kCPW));
+    PROF(p, KV_REGRESS, k_regress<<<grid, 256, 0, st>>>(p->tod, p->mf, p->units, p->T, p->bsum, p->sdm));
+    COMAP_LAUNCH_CHECK(ctx);
+    PROF(p, KV_GAIN_WEIGHTS, k_gain_weights<<<p->F, 1024, 0, st>>>(tsys0, p->gw, p->gmode));
+    COMAP_LAUNCH_CHECK(ctx);
+    PROF(p, KV_COEF_D, k_coef_d<<<UB, 256, 0, st>>>(p->units, p->unit_sums, p->mom, UC, fit, p->F, p->alpha, p->nf,
+                                                    p->bsum, p->ssum, p->sdm, tsys0, gain0, p->gw, p->gmode,
+                                                    calibrator, p->kap, p->dsum, p->xreg));
+    COMAP_LAUNCH_CHECK(ctx);
+    PROF(p, KV_GAIN_AVG, k_gain_avg<<<p->n_tiles, 256, 0, st>>>(p->tod, p->airmass, p->units, p->tiles, p->T, UC,
+                                                                p->kap, p->dsum, p->mf, tod_out, orig_out, p->dG));
+    COMAP_LAUNCH_CHECK(ctx);
+    PROF(p, KV_SCAN_WEIGHTS, k_scan_weights<<<UB, 256, 0, st>>>(p->units, p->T, tod_out, w_out));
+    COMAP_LAUNCH_CHECK(ctx);
+    return 0;
+}
+
+extern "C" int comap_l1_vane(comap_l1_plan *p, int64_t vstart, int64_t vlen, const int32_t *hot_h,
+                             const int64_t *hoff_h, const int32_t *cold_h, const int64_t *coff_h,
+                             double t_hot, double *tsys, double *gain)
+{
+    if (!p || !hoff_h || !coff_h || !tsys || !gain) return -1;
+    comap_ctx *ctx = p->ctx;
+    const int FB = p->F * kBands;
+    if (vstart < 0 || vstart + vlen > p->T) return comap_fail(ctx, -1, "vane event out of range");
+    const int64_t nh = hoff_h[FB], nc = coff_h[FB];
+    for (int64_t i = 0; i < nh; ++i)
+        if (hot_h[i] < 0 || hot_h[i] >= vlen) return comap_fail(ctx, -1, "hot index out of range");
+    for (int64_t i = 0; i < nc; ++i)
+        if (cold_h[i] < 0 || cold_h[i] >= vlen) return comap_fail(ctx, -1, "cold index out of range");
+    size_t bytes = (size_t)(nh + nc) * 4 + (size_t)(FB + 1) * 16 + 64;
+    char *s = nullptr;
+    int rc = comap_scratch(ctx, bytes, (void **)&s);
+    if (rc) return rc;
+    int32_t *dh = (int32_t *)s;
+    int32_t *dc = dh + nh;
+    int64_t *dho = (int64_t *)(((uintptr_t)(dc + nc) + 15) & ~(uintptr_t)15);
+    int64_t *dco = dho + FB + 1;
+    hipStream_t st = ctx->stream;
+    if (nh) COMAP_CHECK(ctx, hipMemcpyAsync(dh, hot_h, nh * 4, hipMemcpyHostToDevice, st));
+    if (nc) COMAP_CHECK(ctx, hipMemcpyAsync(dc, cold_h, nc * 4, hipMemcpyHostToDevice, st));
+    COMAP_CHECK(ctx, hipMemcpyAsync(dho, hoff_h, (FB + 1) * 8, hipMemcpyHostToDevice, st));
+    COMAP_CHECK(ctx, hipMemcpyAsync(dco, coff_h, (FB + 1) * 8, hipMemcpyHostToDevice, st));
+    COMAP_CHECK(ctx, hipMemsetAsync(tsys, 0, (size_t)FB * kChannels * 8, st));
+    COMAP_CHECK(ctx, hipMemsetAsync(gain, 0, (size_t)FB * kChannels * 8, st));
+    const int64_t rows = (int64_t)FB * kChannels;
+    PROF(p, KV_VANE, k_vane<<<(rows + 3) / 4, 256, 0, st>>>(p->tod, p->T, p->F, vstart, dh, dho, dc, dco, t_hot,
+                                                            tsys, gain));
+    COMAP_LAUNCH_CHECK(ctx);
+    // the host arrays may be freed by the caller after return
+    COMAP_CHECK(ctx, hipStreamSynchronize(st));
+    return 0;
+}
+
+extern "C" int comap_l1_debug_fetch(comap_l1_plan *p, int32_t what, double *out, int64_t n)
+{
+    if (!p || !out) return -1;
+    comap_ctx *ctx = p->ctx;
+    const int64_t UC = (int64_t)p->U * kBC;
+    const double *src = nullptr;
+    int64_t cnt = 0;
+    switch (what) {
+    case 0: src = p->nf; cnt = UC; break;
+    case 1: src = p->mf; cnt = (int64_t)p->F * kBands * p->T; break;
+    case 2: src = p->dG; cnt = (int64_t)p->F * p->T; break;
+    case 3: src = p->xreg; cnt = 2 * UC; break;
+    case 4: src = p->mb; cnt = (int64_t)p->F * kBands * p->T; break;
+    default: return comap_fail(ctx, -1, "unknown debug array");
+    }
+    if (n < cnt) return comap_fail(ctx, -1, "debug buffer too small");
+    COMAP_CHECK(ctx, hipMemcpyAsync(out, src, cnt * 8, hipMemcpyDeviceToHost, ctx->stream));
+    COMAP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    return 0;
+}

@@ -1,0 +1,283 @@
+// median_kernels.hip -- exact sliding median (window w) on gfx950.
+//
+// Replaces the reference's serial two-heap filter (Tools/median_filter/
+// Mediator.h:9-197, medianFilter.cpp:4-30) with an order-statistics
+// formulation that is bit-exact for NaN-free input: the median of a window is
+// a pure function of its multiset; even w averages s[w/2-1] and s[w/2] as
+// (hi + lo) / 2 in f64, the order Mediator::getMedian uses (Mediator.h:91-99).
+//
+// 1. k_med_keys: every series (job) contributes the Ns = n_out + w - 1 values
+//    its windows touch, as order-preserving u64 keys + positions.
+// 2. hipcub segmented radix sort: each series sorted ONCE (stable).
+// 3. k_med_walk, one workgroup per chunk of Lc consecutive outputs:
+//    a. the chunk's union U = positions [c, c+w+L-1) is extracted from the
+//       sorted series in sorted order (stream compaction) into LDS;
+//    b. output k's window excludes exactly the offsets < k (head zone) and
+//       >= k+w (tail zone); the 2(L-1) zone entries are compacted in rank
+//       order (list E);
+//    c. lane k walks E (wave-uniform LDS reads): from q = r, every excluded
+//       zone entry with rank <= q pushes q up by one -> q = rank in U of the
+//       r-th smallest window element.
+#include "comap_internal.h"
+
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+
+namespace {
+
+constexpr int kWalkThreads = 512;
+
+__device__ __forceinline__ uint64_t key_of(double v)
+{
+    const uint64_t b = __double_as_longlong(v);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+__device__ __forceinline__ double val_of(uint64_t k)
+{
+    const uint64_t b = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+    return __longlong_as_double(b);
+}
+
+// virtual series x'(pos), pos relative to the start of the (virtual) series
+__device__ __forceinline__ double xprime(const MedJob &j, int64_t pos, int h)
+{
+    const int64_t n = j.n;
+    if (j.mode == 0) {   // medfilt: x'[j<h] = x[0] (head inserts + overwritten head), x'[j>=n] = x[n-1]
+        if (pos < h) return j.src[0];
+        if (pos >= n) return j.src[n - 1];
+        return j.src[pos];
+    }
+    // reflect-3: [x[::-1], x, x[::-1]] of length 3n
+    if (pos < 0) pos = 0;
+    if (pos < n) return j.src[n - 1 - pos];
+    if (pos < 2 * n) return j.src[pos - n];
+    int64_t q = 3 * n - 1 - pos;
+    return j.src[q < 0 ? 0 : q];
+}
+
+__global__ void __launch_bounds__(256) k_med_keys(const MedJob *__restrict__ jobs, const int32_t *__restrict__ seg,
+                                                  int32_t njobs, int32_t w, uint64_t *__restrict__ keys,
+                                                  int32_t *__restrict__ vals)
+{
+    const int jb = blockIdx.y;
+    if (jb >= njobs) return;
+    const MedJob job = jobs[jb];
+    const int32_t s0 = seg[jb], ns = seg[jb + 1] - s0;
+    const int h = w / 2;
+    const int64_t base = job.out_lo - h;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += gridDim.x * blockDim.x) {
+        keys[s0 + i] = key_of(xprime(job, base + i, h));
+        vals[s0 + i] = i;
+    }
+}
+
+template <int P>
+__global__ void __launch_bounds__(kWalkThreads) k_med_walk(const MedJob *__restrict__ jobs,
+                                                           const int64_t *__restrict__ chunks,
+                                                           const int32_t *__restrict__ seg,
+                                                           const uint64_t *__restrict__ skeys,
+                                                           const int32_t *__restrict__ svals, int32_t w, int32_t lc)
+{
+    extern __shared__ __align__(16) unsigned char smem[];
+    uint64_t *keys = reinterpret_cast<uint64_t *>(smem);
+    uint16_t *pos = reinterpret_cast<uint16_t *>(smem + sizeof(uint64_t) * P);
+    uint32_t *E = reinterpret_cast<uint32_t *>(smem + (sizeof(uint64_t) + sizeof(uint16_t)) * P);
+    int *scan = reinterpret_cast<int *>(E + 2 * lc + 8);
+    __shared__ int s_tot;
+
+    const int tid = threadIdx.x;
+    const int jb = (int)chunks[2 * blockIdx.x];
+    const MedJob job = jobs[jb];
+    if (job.gate && *job.gate <= 0.0) return;
+    const int64_t i0 = chunks[2 * blockIdx.x + 1];
+    const int L = (int)min((int64_t)lc, job.out_hi - i0);
+    const int M = w + L - 1;
+    const int c0 = (int)(i0 - job.out_lo);          // chunk offset inside the series' position space
+    const int32_t s0 = seg[jb], ns = seg[jb + 1] - s0;
+
+    // ---- a. extract U in sorted order: entries of the sorted series with position in [c0, c0+M)
+    const int per = (ns + kWalkThreads - 1) / kWalkThreads;
+    const int b0 = tid * per, b1 = min(ns, b0 + per);
+    int cnt = 0;
+    for (int s = b0; s < b1; ++s) {
+        const int p = svals[s0 + s] - c0;
+        cnt += (p >= 0) & (p < M);
+    }
+    scan[tid] = cnt;
+    __syncthreads();
+    for (int off = 1; off < kWalkThreads; off <<= 1) {
+        const int v = (tid >= off) ? scan[tid - off] : 0;
+        __syncthreads();
+        scan[tid] += v;
+        __syncthreads();
+    }
+    int wr = scan[tid] - cnt;
+    for (int s = b0; s < b1; ++s) {
+        const int p = svals[s0 + s] - c0;
+        if ((p >= 0) & (p < M)) {
+            keys[wr] = skeys[s0 + s];
+            pos[wr] = (uint16_t)p;
+            ++wr;
+        }
+    }
+    __syncthreads();
+
+    // ---- b. zone entries (head [0, L-1), tail [w, M)) in rank order
+    const int per2 = (M + kWalkThreads - 1) / kWalkThreads;
+    const int e0 = tid * per2, e1 = min(M, e0 + per2);
+    int zc = 0;
+    for (int s = e0; s < e1; ++s) {
+        const int p = pos[s];
+        zc += (p < L - 1) | (p >= w);
+    }
+    __syncthreads();
+    scan[tid] = zc;
+    __syncthreads();
+    for (int off = 1; off < kWalkThreads; off <<= 1) {
+        const int v = (tid >= off) ? scan[tid - off] : 0;
+        __syncthreads();
+        scan[tid] += v;
+        __syncthreads();
+    }
+    int ew = scan[tid] - zc;
+    if (tid == kWalkThreads - 1) s_tot = scan[tid];
+    for (int s = e0; s < e1; ++s) {
+        const int p = pos[s];
+        if ((p < L - 1) | (p >= w)) E[ew++] = ((uint32_t)s << 16) | (uint32_t)p;
+    }
+    __syncthreads();
+    const int ne = s_tot;
+    if (tid < 8) E[ne + tid] = 0xffffffffu;   // sentinel rank 0xffff > any q
+    __syncthreads();
+
+    // ---- c. walk (E reads are wave-uniform: j advances in lockstep)
+    if (tid < L) {
+        const int k = tid;
+        const int r_lo = (w % 2 == 0) ? (w / 2 - 1) : (w / 2);
+        int q = r_lo;
+        int j = 0;
+        for (;;) {
+            const uint32_t e = E[j];
+            if ((int)(e >> 16) > q) break;
+            const int pp = (int)(e & 0xffff);
+            q += (pp < k) | (pp >= k + w);
+            ++j;
+        }
+        const int q1 = q;
+        double out;
+        if (w % 2 == 0) {
+            q = q1 + 1;
+            for (;;) {
+                const uint32_t e = E[j];
+                if ((int)(e >> 16) > q) break;
+                const int pp = (int)(e & 0xffff);
+                q += (pp < k) | (pp >= k + w);
+                ++j;
+            }
+            out = (val_of(keys[q]) + val_of(keys[q1])) / 2.0;
+        } else {
+            out = val_of(keys[q1]);
+        }
+        job.dst[i0 + k - job.out_lo] = out;
+    }
+}
+
+template <int P>
+size_t walk_smem(int lc) { return (sizeof(uint64_t) + sizeof(uint16_t)) * P + 4 * (2 * lc + 8) + 4 * kWalkThreads + 64; }
+
+}  // namespace
+
+void comap_median_geometry(int32_t w, int32_t *lc, int32_t *P)
+{
+    int p = 1024;
+    while (p < w + 511) p <<= 1;
+    *P = p;
+    *lc = 512;
+}
+
+// ------------------------------------------------------------------ plan
+int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jobs, int32_t w)
+{
+    mp->w = w;
+    comap_median_geometry(w, &mp->lc, &mp->P);
+    if (mp->P > 8192) return comap_fail(ctx, -1, "median window too large (w <= 7681)");
+    std::vector<int32_t> seg(jobs.size() + 1, 0);
+    std::vector<int64_t> chunks;
+    for (size_t j = 0; j < jobs.size(); ++j) {
+        const int64_t nout = jobs[j].out_hi - jobs[j].out_lo;
+        const int64_t ns = nout > 0 ? nout + w - 1 : 0;
+        if ((int64_t)seg[j] + ns >= (1ll << 31)) return comap_fail(ctx, -1, "median plan too large");
+        seg[j + 1] = seg[j] + (int32_t)ns;
+        for (int64_t i0 = jobs[j].out_lo; i0 < jobs[j].out_hi; i0 += mp->lc) {
+            chunks.push_back((int64_t)j);
+            chunks.push_back(i0);
+        }
+    }
+    mp->njobs = (int32_t)jobs.size();
+    mp->nitems = seg.back();
+    mp->nchunks = (int64_t)chunks.size() / 2;
+    hipStream_t st = ctx->stream;
+    auto alloc = [&](void **p, size_t b) { return hipMalloc(p, b ? b : 8); };
+    COMAP_CHECK(ctx, alloc((void **)&mp->jobs, sizeof(MedJob) * jobs.size()));
+    COMAP_CHECK(ctx, alloc((void **)&mp->seg, 4 * seg.size()));
+    COMAP_CHECK(ctx, alloc((void **)&mp->chunks, 8 * chunks.size()));
+    COMAP_CHECK(ctx, alloc((void **)&mp->k0, 8 * (size_t)mp->nitems));
+    COMAP_CHECK(ctx, alloc((void **)&mp->k1, 8 * (size_t)mp->nitems));
+    COMAP_CHECK(ctx, alloc((void **)&mp->v0, 4 * (size_t)mp->nitems));
+    COMAP_CHECK(ctx, alloc((void **)&mp->v1, 4 * (size_t)mp->nitems));
+    COMAP_CHECK(ctx, hipMemcpyAsync(mp->jobs, jobs.data(), sizeof(MedJob) * jobs.size(), hipMemcpyHostToDevice, st));
+    COMAP_CHECK(ctx, hipMemcpyAsync(mp->seg, seg.data(), 4 * seg.size(), hipMemcpyHostToDevice, st));
+    if (!chunks.empty())
+        COMAP_CHECK(ctx, hipMemcpyAsync(mp->chunks, chunks.data(), 8 * chunks.size(), hipMemcpyHostToDevice, st));
+    size_t tb = 0;
+    COMAP_CHECK(ctx, hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb, mp->k0, mp->k1, mp->v0, mp->v1,
+                                                                 (int)mp->nitems, mp->njobs, mp->seg, mp->seg + 1,
+                                                                 0, 64, st));
+    mp->temp_bytes = tb;
+    COMAP_CHECK(ctx, alloc(&mp->temp, tb));
+    COMAP_CHECK(ctx, hipStreamSynchronize(st));   // host vectors go out of scope
+    return 0;
+}
+
+void comap_median_plan_free(MedPlan *mp)
+{
+    void *b[] = {mp->jobs, mp->seg, mp->chunks, mp->k0, mp->k1, mp->v0, mp->v1, mp->temp};
+    for (void *p : b)
+        if (p) (void)hipFree(p);
+    *mp = MedPlan();
+}
+
+int comap_median_run(comap_ctx *ctx, MedPlan *mp)
+{
+    if (mp->nchunks == 0) return 0;
+    hipStream_t st = ctx->stream;
+    dim3 g1(64, (unsigned)mp->njobs);
+    k_med_keys<<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, mp->k0, mp->v0);
+    COMAP_LAUNCH_CHECK(ctx);
+    size_t tb = mp->temp_bytes;
+    COMAP_CHECK(ctx, hipcub::DeviceSegmentedRadixSort::SortPairs(mp->temp, tb, mp->k0, mp->k1, mp->v0, mp->v1,
+                                                                 (int)mp->nitems, mp->njobs, mp->seg, mp->seg + 1,
+                                                                 0, 64, st));
+    switch (mp->P) {
+#define CASE(PP)                                                                                         \
+    case PP: {                                                                                           \
+        const size_t sm = walk_smem<PP>(mp->lc);                                                          \
+        COMAP_CHECK(ctx, hipFuncSetAttribute((const void *)k_med_walk<PP>,                               \
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));      \
+        k_med_walk<PP><<<mp->nchunks, kWalkThreads, sm, st>>>(mp->jobs, mp->chunks, mp->seg, mp->k1,     \
+                                                              mp->v1, mp->w, mp->lc);                    \
+        break;                                                                                           \
+    }
+        CASE(1024)
+        CASE(2048)
+        CASE(4096)
+        CASE(8192)
+#undef CASE
+    default:
+        return comap_fail(ctx, -1, "median window too large");
+    }
+    COMAP_LAUNCH_CHECK(ctx);
+    return 0;
+}

@@ -1,0 +1,231 @@
+"""Device-resident observation: the L1 -> L2 hot path on MI355X.
+
+``GPUObservation`` owns the device copy of one Level-1 observation (the f32
+cube stays resident in HBM across the three stages) and its
+``comap_l1_plan`` (include/comap_hip.h).  The stage classes in
+``comapreduce_amd.stages`` are thin wrappers around it; bench.py drives it
+directly with device-resident synthetic inputs.
+
+Host work is limited to O(T) control logic the reference also runs on the
+host: feature decoding, scan edges, vane sample selection on the 1-D band
+average.  Every O(F x 4 x 1024 x T) operation is a HIP kernel; there is no
+CPU fallback (missing library or GPU -> exception).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+from .pipeline.datahandling import to_host
+
+N_BANDS, N_CHANNELS = 4, 1024
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        raise N.NativeError('no HIP device visible to torch: the COMAP hot path has no CPU fallback')
+    return torch
+
+
+def to_device(x, dtype, device):
+    """Contiguous CUDA tensor of ``dtype`` (copies host arrays)."""
+    torch = _torch()
+    if isinstance(x, torch.Tensor):
+        t = x.to(device=device, dtype=dtype)
+        return t.contiguous()
+    a = np.ascontiguousarray(to_host(x))
+    return torch.from_numpy(a).to(device=device, dtype=dtype).contiguous()
+
+
+# ---------------------------------------------------------------- vane sample selection (host)
+def auto_rms_2d(tod):
+    """Tools/stats.py:59-72, 2-D branch (rows = samples)."""
+    N2 = (tod.shape[0] // 2) * 2
+    return np.nanstd(tod[1:N2:2, :] - tod[:N2:2, :], axis=0) / np.sqrt(2)
+
+
+def find_hot_cold_from_tod(tod):
+    """Hot/cold sample offsets of a vane event from the 1-D band average
+    (VaneCalibration.py:86-141); same NumPy operation sequence and dtypes as
+    the reference so the selected indices are identical."""
+    def find_indices(x, _rms, greater):
+        v = x * 1.0
+        rng = np.nanmax(v) - np.nanmin(v)
+        v /= rng
+        rms = _rms / rng
+        mid = (np.nanmax(v) + np.nanmin(v)) / 2.0
+        cmp = np.greater if greater else np.less
+        group = cmp(v - mid, 15 * rms) & (np.abs(np.gradient(v)) < 2e-3)
+        return np.arange(v.size, dtype=int)[group]
+
+    rms = auto_rms_2d(tod[:, None]).flatten()
+    hot = find_indices(tod, rms, True)
+    cold = find_indices(tod, rms, False)
+    if len(hot) == 0 or len(cold) == 0:
+        return None, None
+    hot = np.sort(hot)
+    cold = np.sort(cold)
+    return hot, cold[cold > hot[-1]]
+
+
+def vane_events(features):
+    """find_vane_samples (VaneCalibration.py:56-65): [[start, end], ...]."""
+    flag = features == 13
+    idx = np.nonzero(np.diff(flag))[0] + 1
+    return idx.reshape((idx.size // 2, 2))
+
+
+class GPUObservation:
+    """One observation resident on one GPU, with its reduction plan."""
+
+    def __init__(self, data, device: int = 0):
+        torch = _torch()
+        self.device = device
+        self.tdev = torch.device('cuda', device)
+        self.ctx = N.ctx(device)
+        with torch.cuda.device(device):
+            self.tod = to_device(data['spectrometer/tod'], torch.float32, self.tdev)
+            self.el = to_device(data['spectrometer/pixel_pointing/pixel_el'], torch.float64, self.tdev)
+        F, B, C, T = self.tod.shape
+        if (B, C) != (N_BANDS, N_CHANNELS):
+            raise ValueError(f'unsupported TOD shape {tuple(self.tod.shape)}')
+        self.F, self.T = F, T
+        self.features = data.features
+        self.edges = np.asarray(to_host(data.scan_edges), dtype=np.int64).reshape(-1, 2)
+        self.S = len(self.edges)
+        self.feeds = np.asarray(to_host(data['spectrometer/feeds'])).reshape(-1)
+        for s, e in self.edges:
+            if e > s and np.all(self.features[s:e] == 9):
+                raise NotImplementedError('constant-elevation scan (features == 9): the per-channel '
+                                          'median atmosphere of filter_atmosphere is not implemented '
+                                          'on the device')
+        units = [(f, s, int(a), int(b - a)) for f in range(F) for s, (a, b) in enumerate(self.edges) if b > a]
+        self.units = np.ascontiguousarray(np.array(units, dtype=np.int32).reshape(-1, 4))
+        desc = N.ObsDesc(F, B, C, self.S, T, self.tod.data_ptr(), self.el.data_ptr(), len(units),
+                         N.hptr(self.units, ctypes.c_int32))
+        plan = ctypes.c_void_p()
+        self._bind()
+        N.check(N.lib().comap_l1_plan_create(self.ctx, ctypes.byref(desc), ctypes.byref(plan)), self.ctx,
+                'comap_l1_plan_create')
+        self.plan = plan
+
+    def _bind(self):
+        N.bind_stream(self.ctx, self.tdev)
+
+    def close(self):
+        if getattr(self, 'plan', None) is not None:
+            _torch().cuda.synchronize(self.tdev)
+            N.lib().comap_l1_plan_destroy(self.plan)
+            self.plan = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # pragma: no cover
+            pass
+
+    # ------------------------------------------------------------ stages
+    def vane(self, band_average, t_hot: float, features=None):
+        """MeasureSystemTemperature: returns (tsys, gain) CUDA f64 [nV, F, 4, 1024]
+        or (None, None) when there is no vane event."""
+        torch = _torch()
+        feats = self.features if features is None else features
+        ev = vane_events(feats)
+        nV = ev.shape[0]
+        if nV == 0:
+            return None, None
+        tsys = torch.zeros((nV, self.F, N_BANDS, N_CHANNELS), dtype=torch.float64, device=self.tdev)
+        gain = torch.zeros_like(tsys)
+        self._bind()
+        for iv, (s, e) in enumerate(ev):
+            ba = to_host(band_average[:, :, s:e])
+            hot_l, cold_l = [], []
+            hoff, coff = [0], [0]
+            for f in range(self.F):
+                for b in range(N_BANDS):
+                    h, c = find_hot_cold_from_tod(ba[f, b])
+                    if h is None or c is None:      # RuntimeError path: (feed, band) stays 0
+                        h = c = np.zeros(0, dtype=int)
+                    hot_l.append(h)
+                    cold_l.append(c)
+                    hoff.append(hoff[-1] + len(h))
+                    coff.append(coff[-1] + len(c))
+            hot = np.ascontiguousarray(np.concatenate(hot_l).astype(np.int32))
+            cold = np.ascontiguousarray(np.concatenate(cold_l).astype(np.int32))
+            hoff = np.asarray(hoff, dtype=np.int64)
+            coff = np.asarray(coff, dtype=np.int64)
+            N.check(N.lib().comap_l1_vane(self.plan, int(s), int(e - s), N.hptr(hot, ctypes.c_int32),
+                                          N.hptr(hoff, ctypes.c_int64), N.hptr(cold, ctypes.c_int32),
+                                          N.hptr(coff, ctypes.c_int64), float(t_hot),
+                                          N.dptr(tsys[iv]), N.dptr(gain[iv])), self.ctx, 'comap_l1_vane')
+        return tsys, gain
+
+    def atmosphere(self):
+        """AtmosphereRemoval: CUDA f64 [S, F, 4, 2, 1024]."""
+        torch = _torch()
+        fit = torch.full((self.S, self.F, N_BANDS, 2, N_CHANNELS), float('nan'), dtype=torch.float64,
+                         device=self.tdev)
+        self._bind()
+        N.check(N.lib().comap_l1_atmosphere(self.plan, N.dptr(fit)), self.ctx, 'comap_l1_atmosphere')
+        return fit
+
+    def average(self, fit_values, tsys0, gain0, calibrator: bool = False):
+        """Level1AveragingGainCorrection: (tod, tod_original, weights) CUDA f64 [F, 4, T]."""
+        torch = _torch()
+        fit = to_device(fit_values, torch.float64, self.tdev)
+        ts = to_device(tsys0, torch.float64, self.tdev)
+        gn = to_device(gain0, torch.float64, self.tdev)
+        out = torch.zeros((3, self.F, N_BANDS, self.T), dtype=torch.float64, device=self.tdev)
+        self._bind()
+        N.check(N.lib().comap_l1_average(self.plan, N.dptr(fit), N.dptr(ts), N.dptr(gn), int(bool(calibrator)),
+                                         N.dptr(out[0]), N.dptr(out[1]), N.dptr(out[2])), self.ctx,
+                'comap_l1_average')
+        self._keep = (fit, ts, gn)   # inputs must outlive the enqueued kernels
+        big = self.feeds > 19        # Level1Averaging.py:817-818
+        if big.any():
+            out[:, torch.as_tensor(np.flatnonzero(big), device=self.tdev)] = 0
+        return out[0], out[1], out[2]
+
+    KERNELS = ('vane', 'moments', 'atmos_fit', 'coef_b', 'band_mean', 'median', 'series_sums', 'regress',
+               'gain_weights', 'coef_d', 'gain_avg', 'scan_weights')
+    STREAMING = ('moments', 'band_mean', 'regress', 'gain_avg')   # the four HBM passes (A, B, C, D)
+
+    def profile(self, enable: bool = True):
+        """Record HIP events around every kernel launch of this plan."""
+        N.check(N.lib().comap_l1_profile(self.plan, int(enable)), self.ctx, 'comap_l1_profile')
+
+    def profile_collect(self):
+        """{kernel: (total_ms, launches)} since the last collect (synchronises)."""
+        ms = np.zeros(32)
+        cnt = np.zeros(32, dtype=np.int64)
+        N.check(N.lib().comap_l1_profile_collect(self.plan, N.hptr(ms, ctypes.c_double),
+                                                 N.hptr(cnt, ctypes.c_int64), 32), self.ctx,
+                'comap_l1_profile_collect')
+        return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(self.KERNELS)}
+
+    def scan_samples(self) -> int:
+        """Sum over units of the scan lengths (samples each streaming pass visits per channel)."""
+        return int(self.units[:, 3].sum())
+
+    def debug(self, what: int):
+        """Internal arrays (host f64): 0 rms [U,4,1024]; 1 mf [F,4,T]; 2 dG [F,T]; 3 x [U,4,1024,2]; 4 mb."""
+        U = self.units.shape[0]
+        shapes = {0: (U, 4, 1024), 1: (self.F, 4, self.T), 2: (self.F, self.T), 3: (U, 4, 1024, 2),
+                  4: (self.F, 4, self.T)}
+        out = np.empty(shapes[what])
+        self._bind()
+        N.check(N.lib().comap_l1_debug_fetch(self.plan, what, N.hptr(out, ctypes.c_double), out.size), self.ctx,
+                'comap_l1_debug_fetch')
+        return out
+
+
+def gpu_observation(data, device: int = 0) -> GPUObservation:
+    """The GPUObservation cached on a Level-1 data object (created on first use)."""
+    obs = getattr(data, '_gpu_observation', None)
+    if obs is None or obs.device != device:
+        obs = GPUObservation(data, device)
+        data._gpu_observation = obs
+    return obs

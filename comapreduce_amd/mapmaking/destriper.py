@@ -1,0 +1,289 @@
+"""Destriping map-maker on MI355X (drop-in for comancpipeline/MapMaking/Destriper.py).
+
+``run_destriper`` keeps the reference signature and return value
+(Destriper.py:456-503): ``{'All': {'map', 'naive', 'weight', 'map2', 'hits'}}``
+on rank 0 and ``None`` maps on other ranks.  Internally:
+
+* ``DeviceOps`` -- one rank's samples as the constant offset<->pixel sparse
+  operator built by ``comap_destripe_create`` (destriper_kernels.hip);
+* ``cg_solve`` -- the reference BiCG (Destriper.py:85-152) with its two
+  duplicate matvecs folded (p == pb, r == rb), run on device vectors; per
+  iteration the only exchange is a SUM all-reduce of the map numerator
+  (npix f64) and of two scalars (p.q, r.r) -- RCCL over xGMI when
+  torch.distributed is initialised with the nccl backend.  ``cg_solve`` is
+  backend-agnostic (the gloo CPU tests drive it with the oracle's NumPy ops).
+
+Samples are sharded by whole offsets (the reference shards files,
+run_destriper.py:131-138); the map is replicated.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from .. import _native as N
+
+
+def _dist():
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            return dist
+    except ImportError:  # pragma: no cover
+        pass
+    return None
+
+
+def torch_allreduce(t):
+    """SUM all-reduce in place (no-op on one rank)."""
+    d = _dist()
+    if d is not None and d.get_world_size() > 1:
+        d.all_reduce(t, op=d.ReduceOp.SUM)
+    return t
+
+
+def cg_solve(ops, allreduce, threshold=1e-6, niter=100, h=None, nnum=None):
+    """Distributed CG for the destriper offsets.
+
+    ops: operator object (DeviceOps or oracle.destriper.ShardOps) for this
+    rank's samples; allreduce(array) sums in place across ranks.  h / nnum
+    are the global weight map and naive numerator (computed when None).
+    Returns (x, iterations, h, nnum)."""
+    if h is None or nnum is None:
+        h0, _, n0 = ops.local_maps()
+        h = allreduce(h0)
+        nnum = allreduce(n0)
+    NO = ops.n_offsets
+    x = ops.zeros(NO)
+    r = ops.zeros(NO)
+    ops.project(None, nnum, h, r)                # b = op_Ax(tod, extend=False); r0 = b - A 0
+    p = ops.copy(r)
+    rr0 = ops.scalar()
+    ops.dot(r, r, rr0)
+    allreduce(rr0)
+    rr = ops.copy(rr0)
+    thresh0 = ops.host_scalar(rr0)
+    num = ops.zeros(ops.npix)
+    q = ops.zeros(NO)
+    pq = ops.scalar()
+    rrn = ops.scalar()
+    it = 0
+    for i in range(niter):
+        ops.bin(p, 0, num)
+        allreduce(num)
+        ops.project(p, num, h, q, pq)
+        allreduce(pq)
+        ops.cg_update(rr, pq, x, r, p, q, rrn)
+        allreduce(rrn)
+        ops.cg_direction(rrn, rr, p, r)
+        ops.set_scalar(rr, rrn)
+        it = i + 1
+        delta = ops.host_scalar(rrn) / thresh0
+        if np.isnan(delta) or delta < threshold:
+            break
+    return x, it, h, nnum
+
+
+class DeviceOps:
+    """One rank's destriper operator on the GPU (comap_destripe_* C ABI)."""
+
+    def __init__(self, pixels, tod, weights, offset_length, npix, device=0):
+        import torch
+        self.torch = torch
+        self.dev = torch.device('cuda', device)
+        self.ctx = N.ctx(device)
+        self.pix = self._t(pixels, torch.int32)
+        self.tod = self._t(tod, torch.float64)
+        self.w = self._t(weights, torch.float64)
+        n = self.tod.numel()
+        if self.pix.numel() != n or self.w.numel() != n:
+            raise ValueError('pointing, tod and weights must have the same length')
+        if n % offset_length:
+            raise ValueError('number of samples must be a multiple of offset_length')
+        pmax = int(self.pix.max().item()) if n else -1
+        if pmax >= npix:
+            raise IndexError(f'pixel index {pmax} out of range for a map of {npix} pixels')
+        self.L, self.npix = int(offset_length), int(npix)
+        h = ctypes.c_void_p()
+        N.bind_stream(self.ctx, self.dev)
+        N.check(N.lib().comap_destripe_create(self.ctx, N.dptr(self.pix), N.dptr(self.tod), N.dptr(self.w), n,
+                                              self.L, self.npix, ctypes.byref(h)), self.ctx,
+                'comap_destripe_create')
+        self.h = h
+        self.n_offsets = int(N.lib().comap_destripe_n_offsets(h))
+
+    def _t(self, a, dt):
+        torch = self.torch
+        if isinstance(a, torch.Tensor):
+            return a.to(device=self.dev, dtype=dt).contiguous().reshape(-1)
+        return torch.from_numpy(np.ascontiguousarray(a)).to(device=self.dev, dtype=dt).reshape(-1)
+
+    def __del__(self):
+        try:
+            if getattr(self, 'h', None) is not None:
+                self.torch.cuda.synchronize(self.dev)
+                N.lib().comap_destripe_destroy(self.h)
+                self.h = None
+        except Exception:  # pragma: no cover
+            pass
+
+    def nnz(self):
+        a = ctypes.c_int64()
+        b = ctypes.c_int64()
+        N.lib().comap_destripe_nnz(self.h, ctypes.byref(a), ctypes.byref(b))
+        return int(a.value), int(b.value)
+
+    # ---- vector helpers
+    def zeros(self, n):
+        return self.torch.zeros(n, dtype=self.torch.float64, device=self.dev)
+
+    def scalar(self):
+        return self.zeros(1)
+
+    def copy(self, a):
+        return a.clone()
+
+    def host_scalar(self, s):
+        return float(s.item())
+
+    def set_scalar(self, dst, src):
+        dst.copy_(src)
+
+    def _c(self, fn, *args):
+        N.bind_stream(self.ctx, self.dev)
+        N.check(getattr(N.lib(), fn)(*args), self.ctx, fn)
+
+    # ---- operator pieces
+    def local_maps(self):
+        h, hits, nn = self.zeros(self.npix), self.zeros(self.npix), self.zeros(self.npix)
+        self._c('comap_destripe_local_maps', self.h, N.dptr(h), N.dptr(hits), N.dptr(nn))
+        return h, hits, nn
+
+    def bin(self, x, mode, out):
+        self._c('comap_destripe_bin', self.h, N.dptr(x), int(mode), N.dptr(out))
+
+    def project(self, x, num, h, y, dot=None):
+        self._c('comap_destripe_project', self.h, None if x is None else N.dptr(x), N.dptr(num), N.dptr(h),
+                N.dptr(y), None if dot is None else N.dptr(dot))
+
+    def dot(self, a, b, out):
+        self._c('comap_destripe_dot', self.h, N.dptr(a), N.dptr(b), N.dptr(out))
+
+    def cg_update(self, rr, pq, x, r, p, q, rr_new):
+        self._c('comap_destripe_cg_update', self.h, N.dptr(rr), N.dptr(pq), N.dptr(x), N.dptr(r), N.dptr(p),
+                N.dptr(q), N.dptr(rr_new))
+
+    def cg_direction(self, rr_new, rr, p, r):
+        self._c('comap_destripe_cg_direction', self.h, N.dptr(rr_new), N.dptr(rr), N.dptr(p), N.dptr(r))
+
+    def div_map(self, num, h, out):
+        self._c('comap_destripe_div_map', self.h, N.dptr(num), N.dptr(h), N.dptr(out))
+
+    # ---- single-rank native solve (no Python per iteration)
+    def solve_native(self, threshold, niter):
+        x = self.zeros(self.n_offsets)
+        maps = {k: self.zeros(self.npix) for k in ('map', 'naive', 'weight', 'hits')}
+        it = ctypes.c_int32(0)
+        self._c('comap_destripe_solve', self.h, float(threshold), int(niter), N.dptr(x), N.dptr(maps['map']),
+                N.dptr(maps['naive']), N.dptr(maps['weight']), N.dptr(maps['hits']), ctypes.byref(it))
+        return x, int(it.value), maps
+
+
+class DeviceDestriper:
+    """Convenience wrapper: the whole destriper_iteration on device tensors."""
+
+    def __init__(self, pixels, tod, weights, offset_length, npix, device=0):
+        self.ops = DeviceOps(pixels, tod, weights, offset_length, npix, device)
+
+    def nnz(self):
+        return self.ops.nnz()
+
+    def solve(self, threshold=1e-6, niter=100):
+        d = _dist()
+        ops = self.ops
+        if d is None or d.get_world_size() == 1:
+            x, it, maps = ops.solve_native(threshold, niter)
+            maps['map2'] = maps['weight']
+            return {'x': x, 'iters': it, 'maps': maps}
+        x, it, h, nnum = cg_solve(ops, torch_allreduce, threshold, niter)
+        _, hits, _ = ops.local_maps()
+        torch_allreduce(hits)
+        num = ops.zeros(ops.npix)
+        ops.bin(x, 1, num)
+        torch_allreduce(num)
+        maps = {'map': ops.zeros(ops.npix), 'naive': ops.zeros(ops.npix), 'weight': h, 'hits': hits}
+        ops.div_map(num, h, maps['map'])
+        ops.div_map(nnum, h, maps['naive'])
+        maps['map2'] = h
+        return {'x': x, 'iters': it, 'maps': maps}
+
+
+def run_destriper(_pointing, _tod, _weights, offset_length, pixel_edges, az=None, el=None, ra=None, dec=None,
+                  feedid=None, obsids=None, obsid_cuts=None, threshold=1e-6, niter=100, chi2_cutoff=100,
+                  special_weight=None, healpix=False, device=None):
+    """Destriper.run_destriper (Destriper.py:456-503) on the GPU.
+
+    ``pixel_edges[-1] + 1`` is the map size (bin_offset_map, :169).  Returns
+    {'All': maps} with host NumPy maps on rank 0; other ranks get None maps."""
+    if special_weight is not None:
+        raise NotImplementedError('special_weight is unused by run_destriper in the reference (:482)')
+    import torch
+    if device is None:
+        device = torch.cuda.current_device()
+    npix = int(pixel_edges[-1]) + 1
+    dd = DeviceDestriper(np.asarray(_pointing), np.asarray(_tod, dtype=np.float64),
+                         np.asarray(_weights, dtype=np.float64), int(offset_length), npix, device)
+    res = dd.solve(threshold, niter)
+    d = _dist()
+    rank = d.get_rank() if d is not None else 0
+    if rank != 0:
+        return {'All': {'map': None, 'naive': None, 'weight': None, 'map2': None}}
+    maps = {k: v.cpu().numpy() for k, v in res['maps'].items()}
+    return {'All': maps}
+
+
+# ---------------------------------------------------------------- bench helper
+def car_pixels(ra, dec, nx=480, ny=480, cdelt=1.0 / 60.0, ra0=None, dec0=None):
+    """Plate-carree pixel index (floor(x + 0.5) convention of transform_to_1d,
+    COMAPData.py:83-117) of (ra, dec) on an nx x ny grid centred on (ra0, dec0);
+    off-map -> -1.  A fp64 restatement of CAR without wcslib (WCS parity is
+    SURVEY §8f row 1)."""
+    import torch
+    ra0 = float(torch.median(ra)) if ra0 is None else ra0
+    dec0 = float(torch.median(dec)) if dec0 is None else dec0
+    px = torch.floor(-(ra - ra0) / cdelt + (nx / 2 - 1) + 0.5)
+    py = torch.floor((dec - dec0) / cdelt + (ny / 2 - 1) + 0.5)
+    ok = (px >= 0) & (px <= nx - 1) & (py >= 0) & (py <= ny - 1)
+    return torch.where(ok, py * nx + px, torch.full_like(px, -1)).to(torch.int32)
+
+
+def level2_to_destriper_inputs(level2, data, band=0, offset_length=50):
+    """Flat (tod, weights, pixels) device tensors from a Level-2 result: per
+    feed and scan the first floor(n/L)*L samples (countDataSize,
+    COMAPData.py:163-187), weights = averaged_tod/weights.  The cuts and the
+    w=400 median filter of get_tod are SURVEY §8f row 1 (not applied here)."""
+    import torch
+    tod = level2['averaged_tod/tod']
+    w = level2['averaged_tod/weights']
+    dev = tod.device
+    ra = torch.as_tensor(np.asarray(data['spectrometer/pixel_pointing/pixel_ra']), device=dev)
+    dec = torch.as_tensor(np.asarray(data['spectrometer/pixel_pointing/pixel_dec']), device=dev)
+    edges = np.asarray(level2['averaged_tod/scan_edges'])
+    segs_t, segs_w, segs_p = [], [], []
+    ra0, dec0 = float(torch.median(ra)), float(torch.median(dec))
+    for f in range(tod.shape[0]):
+        for s, e in edges:
+            n = int((e - s) // offset_length * offset_length)
+            if n <= 0:
+                continue
+            segs_t.append(tod[f, band, s:s + n])
+            segs_w.append(w[f, band, s:s + n])
+            segs_p.append(car_pixels(ra[f, s:s + n], dec[f, s:s + n], ra0=ra0, dec0=dec0))
+    t = torch.cat(segs_t)
+    ww = torch.cat(segs_w)
+    pp = torch.cat(segs_p)
+    bad = ~torch.isfinite(t)
+    t = torch.where(bad, torch.zeros_like(t), t)
+    ww = torch.where(bad | ~torch.isfinite(ww), torch.zeros_like(ww), ww)
+    return t, ww, pp

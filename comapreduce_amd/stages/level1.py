@@ -1,0 +1,207 @@
+"""Level-1 -> Level-2 stages (drop-in for comancpipeline/Analysis/{VaneCalibration,Level1Averaging}.py).
+
+Same class names, dataclass fields, Level-2 dataset paths/shapes and STATE
+semantics as the reference; the numerical work runs on the GPU through
+``comapreduce_amd.gpu.GPUObservation``:
+
+  MeasureSystemTemperature        VaneCalibration.py:21-198
+  AtmosphereRemoval               Level1Averaging.py:156-246
+  Level1AveragingGainCorrection   Level1Averaging.py:473-872
+  CheckLevel1File                 Level1Averaging.py:323-356
+  AssignLevel1Data                Level2Data.py:25-68
+
+Outputs are host NumPy arrays (as the reference writes them) unless
+``device_outputs=True``, which keeps torch CUDA tensors (bench.py).  The
+reference's diagnostic PNGs are not produced (plotting is out of scope).
+"""
+from __future__ import annotations
+
+import logging
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from ..gpu import gpu_observation
+from ..pipeline.datahandling import CALIBRATOR_LIST, COMAPLevel1, COMAPLevel2, to_host
+from ..pipeline.running import PipelineFunction
+
+
+def _out(x, device_outputs):
+    if x is None or device_outputs:
+        return x
+    return to_host(x)
+
+
+@dataclass
+class MeasureSystemTemperature(PipelineFunction):
+    """Vane hot/cold Tsys and gain per (vane event, feed, band, channel)."""
+    name: str = 'MeasureSystemTemperature'
+    system_temperature: object = field(default_factory=lambda: np.zeros(1))
+    system_gain: object = field(default_factory=lambda: np.zeros(1))
+    OBSID_MINIMUM: int = 7_000
+    OBSID_MAXIMUM: int = 1_000_000
+    VANE_COLD_TEMP: float = 2.73
+    groups: list = field(default_factory=lambda: ['vane'])
+    overwrite: bool = False
+    STATE: bool = True
+    figure_directory: str = 'figures'
+    device: int = 0
+    device_outputs: bool = False
+
+    def __call__(self, data, level2_data=None):
+        if isinstance(data, COMAPLevel2):
+            return self.STATE
+        self.measure_system_temperature(data)
+        return self.STATE
+
+    @property
+    def save_data(self):
+        return {'vane/system_temperature': self.system_temperature,
+                'vane/system_gain': self.system_gain}, {}
+
+    def measure_system_temperature(self, data: COMAPLevel1):
+        obs = gpu_observation(data, self.device)
+        tsys, gain = obs.vane(data['spectrometer/band_average'], data.vane_temperature)
+        if tsys is None:
+            logging.info(f'{self.name}: NO VANE FEATURES FOUND... SKIPPING OBSERVATION')
+            self.STATE = False
+            return
+        self.system_temperature = _out(tsys, self.device_outputs)
+        self.system_gain = _out(gain, self.device_outputs)
+
+
+@dataclass
+class AtmosphereRemoval(PipelineFunction):
+    """Per-channel airmass (1/sin el) least-squares fit, per scan."""
+    name: str = 'AtmosphereRemoval'
+    groups: list = field(default_factory=lambda: ['atmosphere'])
+    figure_directory: str = 'figures'
+    overwrite: bool = False
+    STATE: bool = True
+    fit_values: object = None
+    device: int = 0
+    device_outputs: bool = False
+
+    @property
+    def save_data(self):
+        return {'atmosphere/fit_values': self.fit_values}, {}
+
+    def __call__(self, data, level2_data=None):
+        if isinstance(data, COMAPLevel2):
+            self.fit_values = data['atmosphere/fit_values'][...]
+            return self.STATE
+        self.filter_atmosphere(data)
+        return self.STATE
+
+    def filter_atmosphere(self, data: COMAPLevel1):
+        obs = gpu_observation(data, self.device)
+        logging.info(f'{self.name}: Total number of scans {obs.S:03d}')
+        self.fit_values = _out(obs.atmosphere(), self.device_outputs)
+
+
+@dataclass
+class Level1AveragingGainCorrection(PipelineFunction):
+    """L1 -> L2 reduction: de-atmosphere, normalise, median high-pass,
+    gain-fluctuation subtraction and 1/Tsys^2-weighted band averages."""
+    name: str = 'Level1AveragingGainCorrection'
+    groups: list = field(default_factory=lambda: ['averaged_tod'])
+    figure_directory: str = 'figures'
+    overwrite: bool = False
+    STATE: bool = True
+    gain_subtraction_name: str = 'gain_subtraction_fit'
+    gain_subtracted_tod_name: str = 'tod'
+    frequency_bin_size: int = 512
+    N_CHANNELS: int = 1024
+    device: int = 0
+    device_outputs: bool = False
+    tod_cleaned: object = None
+    tod_original: object = None
+    tod_weights: object = None
+    scan_edges: object = None
+    freq_power_spectra: object = None
+    freq_power_spectra_fits: object = None
+
+    @property
+    def save_data(self):
+        return {f'averaged_tod/{self.gain_subtracted_tod_name}': self.tod_cleaned,
+                'averaged_tod/tod_original': self.tod_original,
+                'averaged_tod/weights': self.tod_weights,
+                'averaged_tod/scan_edges': self.scan_edges,
+                'averaged_tod/frequency_power_spectra': self.freq_power_spectra,
+                'averaged_tod/frequency_power_spectra_fits': self.freq_power_spectra_fits}, {}
+
+    def __call__(self, data, level2_data=None):
+        if isinstance(data, COMAPLevel2):
+            self.tod_cleaned = data[f'averaged_tod/{self.gain_subtracted_tod_name}']
+            self.tod_original = data['averaged_tod/tod_original']
+            self.tod_weights = data['averaged_tod/weights']
+            self.scan_edges = data['averaged_tod/scan_edges']
+            self.freq_power_spectra = data['averaged_tod/frequency_power_spectra']
+            self.freq_power_spectra_fits = data['averaged_tod/frequency_power_spectra_fits']
+            return self.STATE
+        self.average_tod(data, level2_data if level2_data is not None else self.level2)
+        return self.STATE
+
+    def average_tod(self, data: COMAPLevel1, level2_data: COMAPLevel2):
+        if self.gain_subtraction_name != 'gain_subtraction_fit':
+            raise NotImplementedError(f'gain function {self.gain_subtraction_name!r} has no device kernel')
+        obs = gpu_observation(data, self.device)
+        tsys0 = level2_data['vane/system_temperature'][0]
+        gain0 = level2_data['vane/system_gain'][0]
+        fit = level2_data['atmosphere/fit_values']
+        tod, orig, w = obs.average(fit, tsys0, gain0, calibrator=data.source_name in CALIBRATOR_LIST)
+        S = obs.S
+        self.tod_cleaned = _out(tod, self.device_outputs)
+        self.tod_original = _out(orig, self.device_outputs)
+        self.tod_weights = _out(w, self.device_outputs)
+        self.scan_edges = np.asarray(obs.edges)
+        self.freq_power_spectra = np.zeros((S, obs.F, 4, 15, 2))
+        self.freq_power_spectra_fits = np.zeros((S, obs.F, 4, 3))
+
+
+@dataclass
+class CheckLevel1File(PipelineFunction):
+    """Rejects sky dips and files shorter than MIN_TIME (Level1Averaging.py:323-356)."""
+    name: str = 'CheckLevel1File'
+    groups: list = field(default_factory=list)
+    overwrite: bool = True
+    STATE: bool = True
+    MIN_TIME: float = 300.0
+
+    def __call__(self, data, level2_data=None):
+        comment = str(data.attrs('comap', 'comment')).lower()
+        if 'sky dip' in comment or 'sky nod' in comment:
+            logging.info(f'Observation is a sky dip. (comment: {comment})')
+            self.STATE = False
+        mjd = to_host(data['spectrometer/MJD'])
+        if (mjd[-1] - mjd[0]) * 24 * 3600.0 < self.MIN_TIME:
+            self.STATE = False
+        return self.STATE
+
+
+@dataclass
+class AssignLevel1Data(PipelineFunction):
+    """Copies pointing / MJD / features into the Level-2 file (Level2Data.py:25-68)."""
+    name: str = 'AssignLevel1Data'
+    overwrite: bool = False
+
+    PATHS = ('spectrometer/MJD', 'spectrometer/feeds', 'spectrometer/bands',
+             'spectrometer/pixel_pointing/pixel_ra', 'spectrometer/pixel_pointing/pixel_dec',
+             'spectrometer/pixel_pointing/pixel_az', 'spectrometer/pixel_pointing/pixel_el')
+
+    def __post_init__(self):
+        self.data = {k: np.empty(1) for k in self.PATHS + ('spectrometer/features', 'spectrometer/frequency')}
+        self.attrs = {}
+        self.groups = list(self.data.keys())
+
+    @property
+    def save_data(self):
+        return self.data, self.attrs
+
+    def __call__(self, data, level2_data=None):
+        for k in self.PATHS:
+            self.data[k] = data[k]
+        self.data['spectrometer/features'] = data.features
+        self.data['spectrometer/frequency'] = data['spectrometer/bands']   # sic (Level2Data.py:59)
+        self.attrs['comap'] = dict(data.attrs('comap'))
+        return self.STATE

@@ -177,6 +177,47 @@ def generate_level1(cfg: SyntheticConfig) -> dict:
     return {'data': data, 'attrs': attrs, 'truth': {'tsys': tsys_t, 'gain': gain_t}}
 
 
+def level1_metadata(cfg: SyntheticConfig):
+    """Everything but the f32 cube, plus the per-sample signal model the device
+    generator (comap_synth_tod) turns into the cube:
+    returns (data dict without tod/band_average, attrs, level, mult, hot), the
+    last three f64 [F, T] (sky level K, multiplicative gain drift, hot-load
+    excess K)."""
+    T = cfg.n_samples
+    feeds = cfg.feeds()
+    F = feeds.size
+    pix = {k: np.empty((F, T)) for k in ('ra', 'dec', 'az', 'el')}
+    level = np.empty((F, T))
+    mult = np.empty((F, T))
+    t = np.arange(T)
+    vane = (t >= VANE_START) & (t < VANE_END)
+    hot = np.broadcast_to(hot_fraction(T) * (T_VANE_K - 2.73), (F, T)).copy()
+    for i, feed in enumerate(feeds):
+        rng = np.random.default_rng(np.random.SeedSequence([cfg.obs_id, int(feed), 99]))
+        pix['ra'][i], pix['dec'][i], pix['az'][i], pix['el'][i] = pointing(T, int(feed))
+        A = 1.0 / np.sin(np.radians(pix['el'][i]))
+        level[i] = np.where(vane, 0.0, 8.0 * (A - 1.4))
+        mult[i] = np.where(vane, 1.0, 1.0 + gain_drift(rng, T))
+    mjd = 59000.0 + cfg.obs_id * 0.1 + t / SAMPLE_RATE / 86400.0
+    freq = np.linspace(26.0, 34.0, N_BANDS * N_CHANNELS).reshape(N_BANDS, N_CHANNELS)
+    data = {
+        'spectrometer/features': features_vector(T),
+        'spectrometer/MJD': mjd,
+        'spectrometer/feeds': feeds,
+        'spectrometer/bands': freq.copy(),
+        'spectrometer/frequency': freq.copy(),
+        'spectrometer/pixel_pointing/pixel_ra': pix['ra'],
+        'spectrometer/pixel_pointing/pixel_dec': pix['dec'],
+        'spectrometer/pixel_pointing/pixel_az': pix['az'],
+        'spectrometer/pixel_pointing/pixel_el': pix['el'],
+        'hk/antenna0/deTracker/lissajous_status': scan_status(T, cfg.scan_len, cfg.scan_gap),
+        'hk/antenna0/deTracker/utc': mjd - 0.5 / SAMPLE_RATE / 86400.0,
+        'hk/antenna0/vane/Tvane': np.full(64, (T_VANE_K - 273.15) * 100.0),
+    }
+    attrs = {'comap': {'obsid': str(cfg.obs_id), 'source': cfg.source, 'comment': cfg.comment}}
+    return data, attrs, level, mult, hot
+
+
 def sha256(arr: np.ndarray) -> str:
     return hashlib.sha256(np.ascontiguousarray(arr).tobytes()).hexdigest()
 

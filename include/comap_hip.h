@@ -1,0 +1,174 @@
+/*
+ * comap_hip.h -- C ABI of the MI355X-native COMAP hot path (gfx950 HIP).
+ *
+ * Drop-in boundary.  Each entry point names the reference
+ * interface it replaces (paths relative to comancpipeline/ in
+ * SharperJBCA/COMAPreduce v0.9.1):
+ *
+ *   comap_medfilt_f64        Tools/median_filter/medfilt.pyx:26-33
+ *                            (medianFilter.cpp:4-30, Mediator.h:9-197)
+ *   comap_bin_values_f64     Tools/binFuncs.pyx:7-32  (binValues)
+ *   comap_l1_vane            Analysis/VaneCalibration.py:67-82,143-198
+ *   comap_l1_atmosphere      Analysis/Level1Averaging.py:197-246
+ *   comap_l1_average         Analysis/Level1Averaging.py:592-708,792-872
+ *                            + Analysis/GainSubtraction.py:17-209
+ *   comap_destripe_*         MapMaking/Destriper.py:85-263,402-503
+ *
+ * Conventions
+ *   - Plain C types only; no C++ exceptions cross this boundary.
+ *   - Every function returns 0 on success, a negative code on failure; the
+ *     message is available from comap_last_error(ctx).
+ *   - "host" arguments are caller-owned host arrays; "dev" arguments are
+ *     device pointers (hipMalloc'd / torch CUDA tensors) on ctx's device.
+ *   - Work is enqueued on the context's stream (comap_set_stream); functions
+ *     taking device pointers do not synchronise the host unless stated.
+ *   - One context per host thread / process; a context is not thread-safe.
+ *   - Pixel indices: int64 on the host API, int32 on device; -1 = off-map.
+ */
+#ifndef COMAP_HIP_H
+#define COMAP_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct comap_ctx comap_ctx;
+typedef struct comap_l1_plan comap_l1_plan;
+typedef struct comap_destriper comap_destriper;
+
+/* ------------------------------------------------------------ context */
+int comap_ctx_create(int device, comap_ctx **out);
+int comap_ctx_destroy(comap_ctx *ctx);
+const char *comap_last_error(const comap_ctx *ctx);
+/* hip stream (hipStream_t as void*); NULL = the legacy default stream */
+int comap_set_stream(comap_ctx *ctx, void *stream);
+int comap_synchronize(comap_ctx *ctx);
+/* Library build tag, e.g. "comap_hip gfx950 <date>" */
+const char *comap_version(void);
+
+/* ------------------------------------------------------------ drop-ins (host arrays) */
+/* In place, identical to medfilt.medfilt(x, w): out[i] = median of
+ * x'[i-w/2 .. i-w/2+w-1] with x'[j<w/2] = x[0], x'[j>=n] = x[n-1]; even w
+ * averages the two middle values.  Requires w <= n, w <= 7681 and a
+ * NaN-free x (returns -3 on NaN: the two-heap's NaN order is undefined). */
+int comap_medfilt_f64(comap_ctx *ctx, double *x_host, int64_t n, int32_t w);
+/* image[p] += weights[i] (or += 1 when weights == NULL) for 0 <= p < npix
+ * and (mask == NULL || mask[i] != 0).  Accumulates into image in place. */
+int comap_bin_values_f64(comap_ctx *ctx, double *image_host, int64_t npix,
+                         const int64_t *pixels_host, const double *weights_host,
+                         const int64_t *mask_host, int64_t n);
+
+/* ------------------------------------------------------------ L1 -> L2 */
+/* Observation description (device pointers).  Units are (feed, scan) pairs
+ * the reduction processes: units[4*u + {0,1,2,3}] = {feed index, scan index,
+ * first sample, n samples}. */
+typedef struct {
+    int32_t n_feeds;           /* F: feeds in the cube                     */
+    int32_t n_bands;           /* must be 4                                */
+    int32_t n_channels;        /* must be 1024                             */
+    int32_t n_scans;           /* S                                        */
+    int64_t n_samples;         /* T                                        */
+    const float *tod;          /* dev f32 [F][4][1024][T]                  */
+    const double *el;          /* dev f64 [F][T] (pixel_el, degrees)       */
+    int32_t n_units;           /* U                                        */
+    const int32_t *units_host; /* host int32 [U][4]                        */
+} comap_obs_desc;
+
+int comap_l1_plan_create(comap_ctx *ctx, const comap_obs_desc *desc, comap_l1_plan **out);
+int comap_l1_plan_destroy(comap_l1_plan *plan);
+
+/* Vane event [vane_start, vane_start + vane_len): per (feed, band) hot/cold
+ * sample offsets (relative to vane_start) in CSR form on the host:
+ * hot_idx[hot_off[fb] .. hot_off[fb+1]), fb = feed*4 + band; an empty hot
+ * or cold list leaves that (feed, band) at 0 (reference RuntimeError path).
+ * Writes tsys/gain dev f64 [F][4][1024] for this event. */
+int comap_l1_vane(comap_l1_plan *plan, int64_t vane_start, int64_t vane_len,
+                  const int32_t *hot_idx_host, const int64_t *hot_off_host,
+                  const int32_t *cold_idx_host, const int64_t *cold_off_host,
+                  double t_hot, double *tsys_dev, double *gain_dev);
+
+/* AtmosphereRemoval: writes fit_values dev f64 [S][F][4][2][1024]
+ * (offset, slope per channel; NaN outside the fitted channel set).  Units
+ * whose scan is constant-elevation (features == 9 throughout) are not
+ * supported (returns -4). Also caches the per-channel noise moments the
+ * Level-2 averaging reuses. */
+int comap_l1_atmosphere(comap_l1_plan *plan, double *fit_values_dev);
+
+/* Level1AveragingGainCorrection.average_tod for every unit.
+ *   fit_values dev [S][F][4][2][1024], tsys0/gain0 dev [F][4][1024]
+ *   (vane event 0), calibrator != 0 for calibrator sources.
+ * Outputs dev f64 [F][4][T]: tod (gain-subtracted residual), tod_original,
+ * weights.  Samples outside the units are left untouched (caller zeroes). */
+int comap_l1_average(comap_l1_plan *plan, const double *fit_values_dev,
+                     const double *tsys0_dev, const double *gain0_dev, int32_t calibrator,
+                     double *tod_out_dev, double *orig_out_dev, double *weights_out_dev);
+
+/* Debug/inspection: copies internal per-unit arrays (host f64):
+ * what = 0: normalisation rms [U][4][1024]; 1: median-filtered band mean
+ * [F][4][T]; 2: dG [F][T]; 3: regression x0,x1 [U][4][1024][2]. */
+int comap_l1_debug_fetch(comap_l1_plan *plan, int32_t what, double *out_host, int64_t n);
+
+/* Per-kernel timing with HIP events recorded on the plan's stream around
+ * every launch.  collect synchronises, returns per-kernel total ms and launch
+ * counts (ids: 0 vane, 1 moments/pass A, 2 atmos fit, 3 coef B, 4 band mean/
+ * pass B, 5 sliding median, 6 series sums, 7 regress/pass C, 8 gain weights,
+ * 9 coef D, 10 gain+band average/pass D, 11 scan weights) and resets. */
+int comap_l1_profile(comap_l1_plan *plan, int32_t enable);
+int comap_l1_profile_collect(comap_l1_plan *plan, double *ms_host, int64_t *counts_host, int32_t n);
+
+/* ------------------------------------------------------------ synthetic input (bench) */
+/* Fills a device-resident synthetic observation with the statistics of
+ * tod f32 [F][4][1024][T], band_average f32 [F][4][T].
+ * level/mult/hot dev f64 [F][T] are the per-sample sky level (K),
+ * multiplicative gain drift and hot-load excess prepared by the host. */
+int comap_synth_tod(comap_ctx *ctx, int32_t n_feeds, int64_t n_samples, uint64_t seed,
+                    const double *level_dev, const double *mult_dev, const double *hot_dev,
+                    float *tod_dev, float *band_average_dev);
+
+/* ------------------------------------------------------------ destriper */
+/* Destriper problem on one rank (MapMaking/Destriper.py:155-263): samples
+ * [N] with int32 pixel (-1 = off-map), f64 tod and weights, N a multiple of
+ * offset_length (<= 64), map of npix pixels.  Builds the constant
+ * offset<->pixel sparse operator and the sample-level maps once. */
+int comap_destripe_create(comap_ctx *ctx, const int32_t *pixels_dev, const double *tod_dev,
+                          const double *weights_dev, int64_t n_samples, int32_t offset_length,
+                          int64_t npix, comap_destriper **out);
+int comap_destripe_destroy(comap_destriper *d);
+int64_t comap_destripe_n_offsets(const comap_destriper *d);
+int comap_destripe_nnz(const comap_destriper *d, int64_t *nnz_offset_major, int64_t *nnz_pixel_major);
+/* Local (this rank) sample-level maps, summed in binValues order:
+ * h = sum w, hits = sum 1, naive_num = sum w tod (any may be NULL). */
+int comap_destripe_local_maps(comap_destriper *d, double *h_dev, double *hits_dev, double *naive_num_dev);
+/* mode 0: num = W x  (bin_offset_map of F x, local partial numerator);
+ * mode 1: num = naive_num - W x (numerator of the destriped map). */
+int comap_destripe_bin(comap_destriper *d, const double *x_dev, int32_t mode, double *num_dev);
+/* y = F^T W (z - m[p]) with m = num/h (num where h == 0), z = F x; when
+ * x_dev == NULL, z = tod (the CG right-hand side b).  h_dev == NULL uses the
+ * local weight map.  dot_dev (optional, needs x) receives y.x. */
+int comap_destripe_project(comap_destriper *d, const double *x_dev, const double *num_dev,
+                           const double *h_dev, double *y_dev, double *dot_dev);
+/* dot_dev[0] = sum a b over the N/L offsets (fixed-order reduction) */
+int comap_destripe_dot(comap_destriper *d, const double *a_dev, const double *b_dev, double *dot_dev);
+/* alpha = rr/pq; x += alpha p; r -= alpha q; rr_new = r.r (device scalars) */
+int comap_destripe_cg_update(comap_destriper *d, const double *rr_dev, const double *pq_dev,
+                             double *x_dev, double *r_dev, const double *p_dev, const double *q_dev,
+                             double *rr_new_dev);
+/* beta = rr_new/rr; p = r + beta p */
+int comap_destripe_cg_direction(comap_destriper *d, const double *rr_new_dev, const double *rr_dev,
+                                double *p_dev, const double *r_dev);
+/* out = num/h (num where h == 0); h_dev == NULL uses the local weight map */
+int comap_destripe_div_map(comap_destriper *d, const double *num_dev, const double *h_dev, double *out_dev);
+/* Whole single-rank destriper_iteration (no collectives): CG (one matvec
+ * per iteration, Destriper.py:85-152) to threshold / niter, then the final
+ * maps.  Writes offsets x [N/L] and map/naive/weight/hits [npix] (any map
+ * pointer may be NULL); *iters_out = iterations performed. */
+int comap_destripe_solve(comap_destriper *d, double threshold, int32_t niter, double *x_dev,
+                         double *map_dev, double *naive_dev, double *weight_dev,
+                         double *hits_dev, int32_t *iters_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* COMAP_HIP_H */

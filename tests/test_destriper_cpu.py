@@ -1,0 +1,99 @@
+"""Destriper: oracle pinned to the reference golden run, and the product's
+distributed CG driver (comapreduce_amd.mapmaking.destriper.cg_solve) checked
+on 2 CPU ranks (gloo) with the oracle's NumPy shard operators."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from comapreduce_amd import synthetic
+from oracle import destriper as od
+
+L = 50
+NPIX = 60 * 60
+
+
+@pytest.fixture(scope='module')
+def golden(golden_dir):
+    return np.load(os.path.join(golden_dir, 'golden_destriper.npz'))
+
+
+@pytest.fixture(scope='module')
+def problem(golden_dir):
+    meta = json.load(open(os.path.join(golden_dir, 'golden_meta.json')))['destriper_inputs']
+    p, t, w = synthetic.destriper_inputs()
+    assert [synthetic.sha256(a) for a in (p, t, w)] == meta['sha256']
+    return p, t, w
+
+
+def test_oracle_destriper_bit_exact(problem, golden):
+    p, t, w = problem
+    maps, x, it = od.destriper_iteration(p, t, w, L, NPIX, threshold=1e-6, niter=100)
+    assert np.array_equal(x, golden['destriper_offsets'])
+    for k in ('map', 'naive', 'weight', 'hits'):
+        assert np.array_equal(maps[k], golden[f'destriper_{k}']), k
+
+
+def test_oracle_destriper_fixed_iterations(problem, golden):
+    p, t, w = problem
+    maps, x, it = od.destriper_iteration(p, t, w, L, NPIX, threshold=0.0, niter=5)
+    assert it == 5
+    assert np.array_equal(x, golden['destriper_offsets_niter5'])
+    assert np.array_equal(maps['map'], golden['destriper_map_niter5'])
+
+
+def test_cg_driver_single_rank_matches_oracle(problem):
+    from comapreduce_amd.mapmaking.destriper import cg_solve
+    p, t, w = problem
+    ops = od.ShardOps(p, t, w, L, NPIX)
+    x, it, h, nnum = cg_solve(ops, lambda a: a, threshold=1e-6, niter=100)
+    _, xr, itr = od.destriper_iteration(p, t, w, L, NPIX, threshold=1e-6, niter=100)
+    assert it == itr
+    assert np.max(np.abs(x - xr)) <= 1e-9 * np.max(np.abs(xr))
+
+
+def _rank(rank, world, port, p, t, w, q):
+    import torch
+    import torch.distributed as dist
+    from comapreduce_amd.mapmaking.destriper import cg_solve
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    no = t.size // L
+    lo, hi = (no * rank // world) * L, (no * (rank + 1) // world) * L   # whole offsets per rank
+
+    def allreduce(a):
+        dist.all_reduce(torch.from_numpy(a), op=dist.ReduceOp.SUM)
+        return a
+
+    ops = od.ShardOps(p[lo:hi], t[lo:hi], w[lo:hi], L, NPIX)
+    x, it, h, nnum = cg_solve(ops, allreduce, threshold=1e-6, niter=100)
+    num = np.zeros(NPIX)
+    ops.bin(x, 1, num)
+    allreduce(num)
+    m = np.zeros(NPIX)
+    ops.div_map(num, h, m)
+    q.put((rank, x, it, m))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_cg_driver_two_ranks_gloo(problem):
+    p, t, w = problem
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = 29500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, p, t, w, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=300) for _ in range(2)], key=lambda r: r[0])
+    for pr in procs:
+        pr.join(timeout=60)
+    maps, xr, itr = od.destriper_iteration(p, t, w, L, NPIX, threshold=1e-6, niter=100)
+    x = np.concatenate([res[0][1], res[1][1]])
+    assert res[0][2] == res[1][2] == itr
+    assert np.max(np.abs(x - xr)) <= 1e-9 * np.max(np.abs(xr))
+    scale = np.max(np.abs(maps['map']))
+    assert np.max(np.abs(res[0][3] - maps['map'])) <= 1e-9 * scale

@@ -1,0 +1,55 @@
+"""GPU destriper vs the reference golden run (Destriper.destriper_iteration on
+2 feeds x 20k samples, 60x60 map, L = 50).  Weight and hit maps are summed in
+binValues' sample order -> bit-exact; offsets and maps within 1e-5 relative
+(north_star), measured against max |value| since destriped maps are ~0-mean."""
+import os
+
+import numpy as np
+import pytest
+
+from comapreduce_amd import synthetic
+
+pytestmark = pytest.mark.gpu
+L = 50
+NPIX = 3600
+
+
+@pytest.fixture(scope='module')
+def golden(golden_dir):
+    return np.load(os.path.join(golden_dir, 'golden_destriper.npz'))
+
+
+def rel(a, b):
+    return float(np.max(np.abs(a - b)) / np.max(np.abs(b)))
+
+
+def test_run_destriper_matches_reference(golden):
+    from comapreduce_amd.mapmaking.destriper import DeviceDestriper, run_destriper
+    p, t, w = synthetic.destriper_inputs()
+    maps = run_destriper(p, t, w, L, np.arange(NPIX), threshold=1e-6, niter=100)['All']
+    assert np.array_equal(maps['weight'], golden['destriper_weight'])
+    assert np.array_equal(maps['hits'], golden['destriper_hits'])
+    assert rel(maps['naive'], golden['destriper_naive']) < 1e-12
+    assert rel(maps['map'], golden['destriper_map']) < 1e-5
+    res = DeviceDestriper(p, t, w, L, NPIX).solve(1e-6, 100)
+    assert rel(res['x'].cpu().numpy(), golden['destriper_offsets']) < 1e-5
+
+
+def test_destriper_fixed_iterations_iterates(golden):
+    from comapreduce_amd.mapmaking.destriper import DeviceDestriper
+    p, t, w = synthetic.destriper_inputs()
+    res = DeviceDestriper(p, t, w, L, NPIX).solve(0.0, 5)
+    assert res['iters'] == 5
+    assert rel(res['x'].cpu().numpy(), golden['destriper_offsets_niter5']) < 1e-9
+    assert rel(res['maps']['map'].cpu().numpy(), golden['destriper_map_niter5']) < 1e-9
+
+
+def test_python_cg_driver_matches_native(golden):
+    """The RCCL-path driver (cg_solve over DeviceOps) == the native C++ loop."""
+    from comapreduce_amd.mapmaking.destriper import DeviceOps, cg_solve
+    p, t, w = synthetic.destriper_inputs()
+    ops = DeviceOps(p, t, w, L, NPIX)
+    x, it, h, nnum = cg_solve(ops, lambda a: a, threshold=1e-6, niter=100)
+    xn, itn, _ = ops.solve_native(1e-6, 100)
+    assert it == itn
+    assert np.array_equal(x.cpu().numpy(), xn.cpu().numpy())

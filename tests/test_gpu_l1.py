@@ -1,0 +1,109 @@
+"""GPU parity of the L1 -> L2 path against the reference golden vectors and
+the CPU oracle (tolerances from BASELINE.json north_star: bit-exact for
+indices / median selections, <= 1e-5 relative for calibrated TOD, spectra)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from comapreduce_amd import synthetic
+from comapreduce_amd.pipeline.datahandling import COMAPLevel2, level1_from_dict
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-5   # north_star: "within 1e-5 relative"
+
+
+def relmax(a, b):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    fin = np.isfinite(b)
+    assert np.array_equal(np.isfinite(a), fin), 'NaN pattern differs'
+    return np.max(np.abs(a[fin] - b[fin])) / max(np.max(np.abs(b[fin])), 1e-300)
+
+
+@pytest.fixture(scope='module')
+def meta(golden_dir):
+    return json.load(open(os.path.join(golden_dir, 'golden_meta.json')))
+
+
+@pytest.fixture(scope='module')
+def c1_run(meta, golden_dir):
+    from comapreduce_amd import Analysis as A
+    gen = synthetic.generate_level1(synthetic.SyntheticConfig(**meta['l1_c1_config']))
+    data = level1_from_dict(gen)
+    level2 = COMAPLevel2(filename='/nonexistent/none.hd5')
+    for cls in (A.MeasureSystemTemperature, A.AtmosphereRemoval, A.Level1AveragingGainCorrection):
+        st = cls(level2=level2)
+        assert st(data, level2)
+        level2.update(st)
+    return gen, data, level2, np.load(os.path.join(golden_dir, 'golden_l1_c1.npz'))
+
+
+def test_medfilt_dropin_bit_exact(meta, golden_dir):
+    from comapreduce_amd.tools.medfilt import medfilt
+    g = np.load(os.path.join(golden_dir, 'golden_medfilt.npz'))
+    for seed, n, w in meta['medfilt_cases']:
+        x = np.random.default_rng(seed).standard_normal(n)
+        y = medfilt(x, w)
+        assert y is x
+        assert np.array_equal(x, g[f'medfilt_{seed}_{n}_{w}']), (seed, n, w)
+
+
+def test_medfilt_dropin_ties_and_edges():
+    from comapreduce_amd.tools.medfilt import medfilt
+    rng = np.random.default_rng(9)
+    for n, w in [(6000, 6000), (12000, 6000), (7681, 7681), (513, 400), (2048, 2), (100, 1), (3000, 5)]:
+        x = np.round(rng.standard_normal(n), 1)   # heavy ties
+        assert np.array_equal(medfilt(x.copy(), w), oracle.medfilt(x.copy(), w)), (n, w)
+
+
+def test_binvalues_dropin_bit_exact(golden_dir):
+    from comapreduce_amd.tools.binfuncs import binValues
+    b = np.load(os.path.join(golden_dir, 'golden_binvalues.npz'))
+    rng = np.random.default_rng(21)
+    npix = 1000
+    pix = rng.integers(-50, npix + 50, 50_000).astype(np.int64)
+    w = rng.standard_normal(50_000)
+    mask = (rng.random(50_000) > 0.3).astype(np.int64)
+    for args, key in [((w,), 'binvalues_weighted'), ((), 'binvalues_hits'), ((w, mask), 'binvalues_masked')]:
+        img = np.zeros(npix)
+        binValues(img, pix, *args)
+        assert np.array_equal(img, b[key]), key
+
+
+def test_l1_vane_vs_reference(c1_run):
+    _, _, l2, g = c1_run
+    assert relmax(l2['vane/system_temperature'], g['vane__system_temperature']) < RTOL
+    assert relmax(l2['vane/system_gain'], g['vane__system_gain']) < RTOL
+
+
+def test_l1_atmosphere_vs_reference(c1_run):
+    _, _, l2, g = c1_run
+    assert relmax(l2['atmosphere/fit_values'], g['atmosphere__fit_values']) < RTOL
+
+
+def test_l1_averaged_tod_vs_reference(c1_run):
+    _, _, l2, g = c1_run
+    assert np.array_equal(l2['averaged_tod/scan_edges'], g['averaged_tod__scan_edges'])
+    for k in ('tod', 'tod_original', 'weights'):
+        assert relmax(l2[f'averaged_tod/{k}'], g[f'averaged_tod__{k}']) < RTOL, k
+    for k in ('frequency_power_spectra', 'frequency_power_spectra_fits'):
+        assert np.array_equal(l2[f'averaged_tod/{k}'], g[f'averaged_tod__{k}'])
+
+
+def test_l1_median_selection_bit_exact(c1_run):
+    """The device median of the device band mean == the oracle medfilt on the
+    same (reflect-padded) input vector, bit for bit."""
+    _, data, _, _ = c1_run
+    obs = data._gpu_observation
+    mb = obs.debug(4)
+    mf = obs.debug(1)
+    for f, s, t0, n in obs.units:
+        if n < 12000:
+            continue
+        for b in range(4):
+            m = mb[f, b, t0:t0 + n]
+            pad = np.concatenate([m[::-1], m, m[::-1]])
+            ref = oracle.medfilt(pad, 6000)[n:2 * n]
+            assert np.array_equal(mf[f, b, t0:t0 + n], ref), (f, s, b)

@@ -1,0 +1,88 @@
+"""Pins the CPU oracle to the reference's own outputs (tests/golden, made by
+tests/golden/make_golden.py running COMAPreduce v0.9.1 in the build container)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from oracle import l1 as ol1
+from comapreduce_amd import synthetic
+
+
+def meta(golden_dir):
+    return json.load(open(os.path.join(golden_dir, 'golden_meta.json')))
+
+
+def relmax(a, b):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    fin = np.isfinite(b)
+    assert np.array_equal(np.isfinite(a), fin), 'NaN pattern differs'
+    return np.max(np.abs(a[fin] - b[fin])) / max(np.max(np.abs(b[fin])), 1e-300)
+
+
+def test_medfilt_oracle_bit_exact(golden_dir):
+    g = np.load(os.path.join(golden_dir, 'golden_medfilt.npz'))
+    for seed, n, w in meta(golden_dir)['medfilt_cases']:
+        x = np.random.default_rng(seed).standard_normal(n)
+        assert np.array_equal(oracle.medfilt(x.copy(), w), g[f'medfilt_{seed}_{n}_{w}']), (seed, n, w)
+
+
+def test_medfilt_reference_build_matches_golden(golden_dir):
+    if oracle.ref_lib() is None:
+        pytest.skip('oracle/_ref not built (reference sources absent)')
+    g = np.load(os.path.join(golden_dir, 'golden_medfilt.npz'))
+    for seed, n, w in meta(golden_dir)['medfilt_cases']:
+        x = np.random.default_rng(seed).standard_normal(n)
+        assert np.array_equal(oracle.medfilt_reference(x.copy(), w), g[f'medfilt_{seed}_{n}_{w}'])
+
+
+def test_medfilt_oracle_vs_reference_random():
+    if oracle.ref_lib() is None:
+        pytest.skip('oracle/_ref not built')
+    rng = np.random.default_rng(5)
+    for n, w in [(3000, 6), (2500, 401), (1000, 3), (7000, 2000)]:
+        x = np.round(rng.standard_normal(n), 1)     # many ties
+        assert np.array_equal(oracle.medfilt(x.copy(), w), oracle.medfilt_reference(x.copy(), w))
+
+
+def test_binvalues_oracle_bit_exact(golden_dir):
+    b = np.load(os.path.join(golden_dir, 'golden_binvalues.npz'))
+    rng = np.random.default_rng(21)
+    npix = 1000
+    pix = rng.integers(-50, npix + 50, 50_000).astype(np.int64)
+    w = rng.standard_normal(50_000)
+    mask = (rng.random(50_000) > 0.3).astype(np.int64)
+    assert np.array_equal(oracle.bin_values(np.zeros(npix), pix, w), b['binvalues_weighted'])
+    assert np.array_equal(oracle.bin_values(np.zeros(npix), pix), b['binvalues_hits'])
+    assert np.array_equal(oracle.bin_values(np.zeros(npix), pix, w, mask), b['binvalues_masked'])
+
+
+def test_synthetic_inputs_reproducible(golden_dir):
+    m = meta(golden_dir)
+    gen = synthetic.generate_level1(synthetic.SyntheticConfig(**m['l1_c1_config']))
+    for k, v in gen['data'].items():
+        assert synthetic.sha256(v) == m['l1_c1_sha256'][k], k
+
+
+@pytest.fixture(scope='module')
+def c1(golden_dir):
+    m = meta(golden_dir)
+    gen = synthetic.generate_level1(synthetic.SyntheticConfig(**m['l1_c1_config']))
+    return gen, np.load(os.path.join(golden_dir, 'golden_l1_c1.npz'))
+
+
+def test_oracle_l1_matches_reference(c1):
+    gen, g = c1
+    out = ol1.reduce_level1(gen['data'])
+    assert np.array_equal(out['averaged_tod/scan_edges'], g['averaged_tod__scan_edges'])
+    # f32 nanmean sums inside the vane step are reproduced exactly
+    assert relmax(out['vane/system_temperature'], g['vane__system_temperature']) == 0.0
+    assert relmax(out['vane/system_gain'], g['vane__system_gain']) == 0.0
+    # closed-form solves vs block_diag/spsolve and CG: rounding-level
+    for k, tol in [('atmosphere/fit_values', 1e-9), ('averaged_tod/tod', 1e-8),
+                   ('averaged_tod/tod_original', 1e-8), ('averaged_tod/weights', 1e-9)]:
+        assert relmax(out[k], g[k.replace('/', '__')]) < tol, k
+    for k in ('averaged_tod/frequency_power_spectra', 'averaged_tod/frequency_power_spectra_fits'):
+        assert np.array_equal(out[k], g[k.replace('/', '__')])
