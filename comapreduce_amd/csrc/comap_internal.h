@@ -29,6 +29,10 @@ struct comap_ctx {
 
 int comap_fail(comap_ctx *ctx, int code, const std::string &msg);
 int comap_scratch(comap_ctx *ctx, size_t bytes, void **out);
+// med_dev[r] = np.nanmedian(float32 row r), rows_host[2r] = element offset in tod, [2r+1] = length
+int comap_row_nanmedian(comap_ctx *ctx, const float *tod, const int64_t *rows_host, int32_t nrows, float *med_dev);
+
+inline bool atmos_channel_host(int c) { return c >= 10 && c < 1014 && !(c >= 510 && c < 515); }
 
 // ------------------------------------------------------------------ constants
 namespace comap {
@@ -36,7 +40,7 @@ constexpr int kBands = 4;
 constexpr int kChannels = 1024;
 constexpr int kBC = kBands * kChannels;
 constexpr int kMedfiltWindow = 6000;           // int(50*120), Level1Averaging.py:833
-constexpr int kTile = 256;                     // samples per pass-B/D workgroup
+constexpr int kTile = 1024;                    // samples per pass-B/D workgroup (multiple of 256)
 constexpr double kDnuTau = (2e9 / 1024.0) * (1.0 / 50.0);   // Level1Averaging.py:671-672
 }  // namespace comap
 
@@ -105,6 +109,13 @@ struct comap_l1_plan {
     double *dsum = nullptr;            // [U*4][16] per-band constants for pass D
     double *xreg = nullptr;            // [U*4096][2] regression x0,x1 (debug)
     double *dG = nullptr;              // [F][T]
+    // NaN / calibrator paths
+    int32_t *rowbad = nullptr;         // [U*4096] non-finite samples per row (pass A)
+    int32_t nan_total = 0;             // total from the last pass A
+    bool filled = false;               // fill_bad_data applied to the device cube
+    double *ubs = nullptr;             // [U*4][4] fit normal-equation sums n, SA, SAA per (unit, band)
+    double *fitsum = nullptr;          // [2][U*4096] masked Sd, SAd (select_time path)
+    double *oa = nullptr;              // [U*4096][2] offset/slope L1AGC subtracts
     // per-kernel HIP-event timing (comap_l1_profile)
     bool prof_on = false;
     std::vector<hipEvent_t> prof_pool;

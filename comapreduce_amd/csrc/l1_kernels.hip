@@ -113,7 +113,8 @@ __global__ void __launch_bounds__(256) k_unit_sums(const int32_t *__restrict__ u
 constexpr int kCPW = 4;   // channel rows per wave
 __global__ void __launch_bounds__(256) k_moments(const float *__restrict__ tod, const double *__restrict__ A,
                                                  const int32_t *__restrict__ units, int64_t T,
-                                                 double *__restrict__ mom, int64_t UC, int32_t *nan_count)
+                                                 double *__restrict__ mom, int64_t UC, int32_t *nan_count,
+                                                 int32_t *__restrict__ rowbad)
 {
     const int wid = uniform(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -128,9 +129,9 @@ __global__ void __launch_bounds__(256) k_moments(const float *__restrict__ tod, 
     const double *a = A + (int64_t)f * T + t0;
 
     double sd[kCPW], sad[kCPW], su[kCPW], suu[kCPW], suv[kCPW];
+    int bad[kCPW];
 #pragma unroll
-    for (int r = 0; r < kCPW; ++r) sd[r] = sad[r] = su[r] = suu[r] = suv[r] = 0.0;
-    int bad = 0;
+    for (int r = 0; r < kCPW; ++r) { sd[r] = sad[r] = su[r] = suu[r] = suv[r] = 0.0; bad[r] = 0; }
     const int n4 = n >> 2;
     for (int k = lane; k < n4; k += 64) {
         const double a0 = a[4 * k], a1 = a[4 * k + 1], a2 = a[4 * k + 2], a3 = a[4 * k + 3];
@@ -139,7 +140,7 @@ __global__ void __launch_bounds__(256) k_moments(const float *__restrict__ tod, 
         for (int r = 0; r < kCPW; ++r) {
             const f32x4u x = *reinterpret_cast<const f32x4u *>(row0 + (int64_t)r * T + 4 * k);
             const double x0 = x.x, x1 = x.y, x2 = x.z, x3 = x.w;
-            bad += !isfinite(x.x) + !isfinite(x.y) + !isfinite(x.z) + !isfinite(x.w);
+            bad[r] += !isfinite(x.x) + !isfinite(x.y) + !isfinite(x.z) + !isfinite(x.w);
             sd[r] += (x0 + x1) + (x2 + x3);
             sad[r] = fma(a0, x0, sad[r]);
             sad[r] = fma(a1, x1, sad[r]);
@@ -158,15 +159,18 @@ __global__ void __launch_bounds__(256) k_moments(const float *__restrict__ tod, 
 #pragma unroll
         for (int r = 0; r < kCPW; ++r) {
             const float xf = row0[(int64_t)r * T + tt];
-            bad += !isfinite(xf);
+            bad[r] += !isfinite(xf);
             sd[r] += (double)xf;
             sad[r] = fma(at, (double)xf, sad[r]);
         }
     }
+    int tot = 0;
 #pragma unroll
     for (int r = 0; r < kCPW; ++r) {
         const double s0 = wave_sum(sd[r]), s1 = wave_sum(sad[r]), s2 = wave_sum(su[r]);
         const double s3 = wave_sum(suu[r]), s4 = wave_sum(suv[r]);
+        const int nb = (int)wave_sum((double)bad[r]);
+        tot += nb;
         if (lane == 0) {
             const int64_t idx = (int64_t)u * kBC + b * kChannels + c0 + r;
             mom[idx] = s0;
@@ -174,17 +178,138 @@ __global__ void __launch_bounds__(256) k_moments(const float *__restrict__ tod, 
             mom[2 * UC + idx] = s2;
             mom[3 * UC + idx] = s3;
             mom[4 * UC + idx] = s4;
+            rowbad[idx] = nb;
         }
     }
-    if (bad) atomicAdd(nan_count, bad);
+    if (lane == 0 && tot) atomicAdd(nan_count, tot);
+}
+
+// ------------------------------------------------------------------ NaN path: select_time + masked fit sums
+// fit_atmosphere (Level1Averaging.py:204-213) fits only the samples where all
+// 994 fitted channels of the band are finite.  One workgroup per
+// (unit, band, 1024-sample tile) marks valid[t]; a second kernel recomputes
+// the fit sums of that (unit, band) over the valid samples.
+__global__ void __launch_bounds__(256) k_select_time(const float *__restrict__ tod, const int32_t *__restrict__ units,
+                                                     const int32_t *__restrict__ pairs, int64_t T,
+                                                     const int64_t *__restrict__ voff, uint8_t *__restrict__ valid)
+{
+    const int pr = blockIdx.y;
+    const int u = pairs[2 * pr], b = pairs[2 * pr + 1];
+    const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const float *p = tod + (int64_t)(f * kBands + b) * kChannels * T + t0 + t;
+    bool ok = true;
+    for (int c = 10; c < 1014; ++c)
+        if (atmos_channel(c) && !isfinite(p[(int64_t)c * T])) ok = false;
+    valid[voff[pr] + t] = ok;
+}
+
+// per (pair, channel): Sd, SAd over valid t -> fs[0/1][u*4096+b*1024+c];
+// per pair: n, SA, SAA -> ub[(u*4+b)*4 + {0,1,2}]
+__global__ void __launch_bounds__(256) k_masked_fit_sums(const float *__restrict__ tod, const double *__restrict__ A,
+                                                         const int32_t *__restrict__ units,
+                                                         const int32_t *__restrict__ pairs, int64_t T,
+                                                         const int64_t *__restrict__ voff,
+                                                         const uint8_t *__restrict__ valid, int64_t UC,
+                                                         double *__restrict__ fs, double *__restrict__ ub)
+{
+    const int pr = blockIdx.y;
+    const int u = pairs[2 * pr], b = pairs[2 * pr + 1];
+    const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = blockIdx.x * 4 + wid;            // one wave per channel
+    const float *p = tod + ((int64_t)(f * kBands + b) * kChannels + c) * T + t0;
+    const double *a = A + (int64_t)f * T + t0;
+    const uint8_t *v = valid + voff[pr];
+    double s0 = 0, s1 = 0, cn = 0, sa = 0, saa = 0;
+    for (int t = lane; t < n; t += 64) {
+        if (!v[t]) continue;
+        const double x = p[t], at = a[t];
+        s0 += x;
+        s1 = fma(at, x, s1);
+        cn += 1.0;
+        sa += at;
+        saa = fma(at, at, saa);
+    }
+    s0 = wave_sum(s0); s1 = wave_sum(s1);
+    cn = wave_sum(cn); sa = wave_sum(sa); saa = wave_sum(saa);
+    if (lane == 0) {
+        const int64_t i = (int64_t)u * kBC + b * kChannels + c;
+        fs[i] = s0;
+        fs[UC + i] = s1;
+        if (c == 0) {
+            double *o = ub + 4 * ((int64_t)u * kBands + b);
+            o[0] = cn; o[1] = sa; o[2] = saa;
+        }
+    }
+}
+
+// ub[(u*4+b)] = unit airmass sums (NaN-free case: every sample is fitted)
+__global__ void k_ub_from_units(const double *__restrict__ us, int U, double *__restrict__ ub)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= U * kBands) return;
+    const double *q = us + 8 * (int64_t)(i / kBands);
+    ub[4 * (int64_t)i] = q[0];
+    ub[4 * (int64_t)i + 1] = q[1];
+    ub[4 * (int64_t)i + 2] = q[2];
+}
+
+// fill_bad_data (Level1Averaging.py:658-665): NaN -> the row's nanmedian (f32), in place
+__global__ void __launch_bounds__(256) k_fill_rows(float *__restrict__ tod, const int64_t *__restrict__ rows,
+                                                   const float *__restrict__ med, int nrows)
+{
+    const int r = blockIdx.y;
+    if (r >= nrows) return;
+    float *p = tod + rows[2 * r];
+    const int64_t n = rows[2 * r + 1];
+    const float m = med[r];
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        if (isnan(p[i])) p[i] = m;
+}
+
+// constant-elevation scans (Level1Averaging.py:242-244): fit = (nanmedian, 0) for every channel
+__global__ void k_fit_from_median(const int32_t *__restrict__ units, const int32_t *__restrict__ ulist, int nu,
+                                  const float *__restrict__ med, int F, double *__restrict__ fit)
+{
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= (int64_t)nu * kBC) return;
+    const int k = (int)(i / kBC), bc = (int)(i % kBC);
+    const int u = ulist[k];
+    const int f = units[4 * u], s = units[4 * u + 1];
+    const int b = bc / kChannels, c = bc % kChannels;
+    double *o = fit + (((int64_t)s * F + f) * kBands + b) * 2 * kChannels;
+    o[c] = (double)med[i];
+    o[kChannels + c] = 0.0;
+}
+
+// per (unit, channel) offset/slope L1AGC subtracts: the unit's scan fit, or
+// (nanmedian, 0) for calibrator sources (remove_atmosphere, :647-648)
+__global__ void k_gather_oa(const int32_t *__restrict__ units, const double *__restrict__ fit, int F, int U,
+                            const float *__restrict__ med, double *__restrict__ oa)
+{
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= (int64_t)U * kBC) return;
+    const int u = (int)(i / kBC), bc = (int)(i % kBC);
+    const int f = units[4 * u], s = units[4 * u + 1];
+    const int b = bc / kChannels, c = bc % kChannels;
+    if (med) {
+        oa[2 * i] = (double)med[i];
+        oa[2 * i + 1] = 0.0;
+    } else {
+        const double *o = fit + (((int64_t)s * F + f) * kBands + b) * 2 * kChannels;
+        oa[2 * i] = o[c];
+        oa[2 * i + 1] = o[kChannels + c];
+    }
 }
 
 // ------------------------------------------------------------------ atmosphere fit
 // AtmosphereRemoval.fit_atmosphere (Level1Averaging.py:197-227): the
 // block-diagonal spsolve is an independent 2x2 normal-equation solve per
 // channel: [[n, SA],[SA, SAA]] [o, a]^T = [Sd, SAd]^T.
-__global__ void k_atmos_fit(const int32_t *__restrict__ units, const double *__restrict__ us,
-                            const double *__restrict__ mom, int64_t UC, int F, int U,
+__global__ void k_atmos_fit(const int32_t *__restrict__ units, const double *__restrict__ ubs,
+                            const double *__restrict__ fs, int64_t UC, int F, int U,
                             double *__restrict__ fit)
 {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -193,11 +318,11 @@ __global__ void k_atmos_fit(const int32_t *__restrict__ units, const double *__r
     const int bc = (int)(i % kBC);
     const int b = bc / kChannels, c = bc % kChannels;
     const int f = units[4 * u], s = units[4 * u + 1];
-    const double *q = us + 8 * (int64_t)u;
+    const double *q = ubs + 4 * ((int64_t)u * kBands + b);
     const double n = q[0], sa = q[1], saa = q[2];
     double o = NAN, a = NAN;
-    if (atmos_channel(c) && n >= 100.0) {
-        const double sd = mom[i], sad = mom[UC + i];
+    if (atmos_channel(c) && n >= 100.0) {    // MINIMUM_CHUNK_SIZE (Level1Averaging.py:207-208)
+        const double sd = fs[i], sad = fs[UC + i];
         const double det = n * saa - sa * sa;
         o = (saa * sd - sa * sad) / det;
         a = (n * sad - sa * sd) / det;
@@ -213,21 +338,20 @@ __global__ void k_atmos_fit(const int32_t *__restrict__ units, const double *__r
 // channels; per (unit, band): beta = sum alpha o, gamma = sum alpha a, N.
 __global__ void __launch_bounds__(256) k_coef_b(const int32_t *__restrict__ units, const double *__restrict__ us,
                                                 const double *__restrict__ mom, int64_t UC,
-                                                const double *__restrict__ fit, int F,
+                                                const double *__restrict__ oa,
                                                 double *__restrict__ alpha, double *__restrict__ nf,
                                                 double *__restrict__ bsum)
 {
     __shared__ double red[4];
     const int ub = blockIdx.x;
     const int u = ub / kBands, b = ub % kBands;
-    const int f = units[4 * u], s = units[4 * u + 1], n = units[4 * u + 3];
+    const int n = units[4 * u + 3];
     const double *q = us + 8 * (int64_t)u;
     const double sv = q[3], svv = q[4], n4 = q[5];
-    const double *fo = fit + (((int64_t)s * F + f) * kBands + b) * 2 * kChannels;
     double beta = 0, gamma = 0, cnt = 0;
     for (int c = threadIdx.x; c < kChannels; c += blockDim.x) {
         const int64_t i = (int64_t)u * kBC + b * kChannels + c;
-        const double o = fo[c], a = fo[kChannels + c];
+        const double o = oa[2 * i], a = oa[2 * i + 1];
         double rms = NAN;
         if (n4 > 0 && isfinite(o) && isfinite(a)) {
             const double su = mom[2 * UC + i], suu = mom[3 * UC + i], suv = mom[4 * UC + i];
@@ -264,6 +388,27 @@ __global__ void __launch_bounds__(256) k_coef_b(const int32_t *__restrict__ unit
 // ------------------------------------------------------------------ pass B
 // Band mean over the median channels (nanmean, Level1Averaging.py:691-692):
 //   m_t = (sum_c alpha_c d_ct - beta - gamma A_t) / N
+// A lane owns kJ groups of 4 consecutive samples, group g at lane offset 256 g,
+// so one wave visits kTile = 256 kJ contiguous samples (4 kJ KB) of a channel
+// row per channel step: long DRAM/TLB runs despite the row stride.
+constexpr int kJ = kTile / 256;
+
+// x[4g+e] = d[r0 + 256 g + e] (0 beyond the scan end, nv0 = n - r0)
+__device__ __forceinline__ void load_groups(const float *__restrict__ p, int nv0, double (&x)[4 * kJ])
+{
+#pragma unroll
+    for (int g = 0; g < kJ; ++g) {
+        const int nv = nv0 - 256 * g;
+        if (nv >= 4) {
+            const f32x4u v = *reinterpret_cast<const f32x4u *>(p + 256 * g);
+            x[4 * g] = v.x; x[4 * g + 1] = v.y; x[4 * g + 2] = v.z; x[4 * g + 3] = v.w;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[4 * g + e] = (e < nv) ? (double)p[256 * g + e] : 0.0;
+        }
+    }
+}
+
 __global__ void __launch_bounds__(256) k_band_mean(const float *__restrict__ tod, const double *__restrict__ A,
                                                    const int32_t *__restrict__ units, const int32_t *__restrict__ tiles,
                                                    int64_t T, const double *__restrict__ alpha,
@@ -274,39 +419,34 @@ __global__ void __launch_bounds__(256) k_band_mean(const float *__restrict__ tod
     const int u = tiles[2 * blockIdx.x], toff = tiles[2 * blockIdx.x + 1];
     const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
     const int r0 = toff + 4 * lane;                 // first sample (relative) of this lane
-    const int64_t rowstride = T;
     const float *base = tod + (int64_t)(f * kBands + b) * kChannels * T + t0 + r0;
     const double *al = alpha + (int64_t)u * kBC + b * kChannels;
-    double acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0;
-    const bool full = (r0 + 3 < n);
-    const int nv = n - r0;   // valid samples for this lane (may be <= 0)
+    double acc[4 * kJ];
+#pragma unroll
+    for (int i = 0; i < 4 * kJ; ++i) acc[i] = 0.0;
+    const int nv0 = n - r0;
     auto body = [&](int c) {
         const double w = al[c];
-        const float *p = base + (int64_t)c * rowstride;
-        if (full) {
-            const f32x4u x = *reinterpret_cast<const f32x4u *>(p);
-            acc0 = fma(w, (double)x.x, acc0);
-            acc1 = fma(w, (double)x.y, acc1);
-            acc2 = fma(w, (double)x.z, acc2);
-            acc3 = fma(w, (double)x.w, acc3);
-        } else {
-            if (nv > 0) acc0 = fma(w, (double)p[0], acc0);
-            if (nv > 1) acc1 = fma(w, (double)p[1], acc1);
-            if (nv > 2) acc2 = fma(w, (double)p[2], acc2);
-        }
+        double x[4 * kJ];
+        load_groups(base + (int64_t)c * T, nv0, x);
+#pragma unroll
+        for (int i = 0; i < 4 * kJ; ++i) acc[i] = fma(w, x[i], acc[i]);
     };
-#pragma unroll 8
+#pragma unroll 2
     for (int c = 10; c < 507; ++c) body(c);
-#pragma unroll 8
+#pragma unroll 2
     for (int c = 518; c < 1014; ++c) body(c);
     const double *bs = bsum + 4 * ((int64_t)u * kBands + b);
     const double beta = bs[0], gamma = bs[1], cnt = bs[2];
     double *out = mb + (int64_t)(f * kBands + b) * T + t0 + r0;
     const double *a = A + (int64_t)f * T + t0 + r0;
-    const double accs[4] = {acc0, acc1, acc2, acc3};
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-        if (j < nv) out[j] = cnt > 0 ? (accs[j] - beta - gamma * a[j]) / cnt : NAN;
+    for (int g = 0; g < kJ; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int o = 256 * g + e;
+            if (o < nv0) out[o] = cnt > 0 ? (acc[4 * g + e] - beta - gamma * a[o]) / cnt : NAN;
+        }
 }
 
 // ------------------------------------------------------------------ series sums for pass C
@@ -472,7 +612,7 @@ __global__ void __launch_bounds__(1024) k_gain_weights(const double *__restrict_
 // dsum[ub][..] = {Sg_b, Gg_b, Dg_b, Sr_b, Gr_b, Dr_b, So_b, Go_b, Do_b, SKr, SW, SWo}
 __global__ void __launch_bounds__(256) k_coef_d(const int32_t *__restrict__ units, const double *__restrict__ us,
                                                 const double *__restrict__ mom, int64_t UC,
-                                                const double *__restrict__ fit, int F,
+                                                const double *__restrict__ oa,
                                                 const double *__restrict__ alpha, const double *__restrict__ nf,
                                                 const double *__restrict__ bsum, const double *__restrict__ ss,
                                                 const double *__restrict__ sdm, const double *__restrict__ tsys0,
@@ -484,14 +624,13 @@ __global__ void __launch_bounds__(256) k_coef_d(const int32_t *__restrict__ unit
     __shared__ double red[4];
     const int ub = blockIdx.x;
     const int u = ub / kBands, b = ub % kBands;
-    const int f = units[4 * u], s = units[4 * u + 1];
+    const int f = units[4 * u];
     const double *q = us + 8 * (int64_t)u;
     const double n = q[0], SA = q[1];
     const double *bs = bsum + 4 * (int64_t)ub;
     const bool band_on = bs[3] > 0;
     const double *sq = ss + 4 * (int64_t)ub;
     const double Smf = sq[0], Smm = sq[1], SAm = sq[2];
-    const double *fo = fit + (((int64_t)s * F + f) * kBands + b) * 2 * kChannels;
     const int gm = gmode[f];
     // gain path (Level1Averaging.py:710-725, 834-838):
     //   zero: y zeroed on the gain mask (gain function was called)
@@ -505,7 +644,7 @@ __global__ void __launch_bounds__(256) k_coef_d(const int32_t *__restrict__ unit
     for (int k = 0; k < 12; ++k) acc[k] = 0.0;
     for (int c = threadIdx.x; c < kChannels; c += blockDim.x) {
         const int64_t i = (int64_t)u * kBC + b * kChannels + c;
-        const double o = fo[c], a = fo[kChannels + c];
+        const double o = oa[2 * i], a = oa[2 * i + 1];
         const double al = alpha[i];
         const double tsv = tsys0[(int64_t)f * kBC + b * kChannels + c];
         // ---- filtered TOD coefficients
@@ -580,53 +719,53 @@ __global__ void __launch_bounds__(256) k_gain_avg(const float *__restrict__ tod,
     const float *base = tod + (int64_t)(f * kBands + b) * kChannels * T + t0 + r0;
     const int64_t kb = (int64_t)u * kBC + b * kChannels;
     const double *kg = kap + kb, *kr = kap + UC + kb, *ko = kap + 2 * UC + kb;
-    double g0 = 0, g1 = 0, g2 = 0, g3 = 0, rr0 = 0, rr1 = 0, rr2 = 0, rr3 = 0, o0 = 0, o1 = 0, o2 = 0, o3 = 0;
-    const bool full = (r0 + 3 < n);
-    const int nv = n - r0;
-#pragma unroll 4
+    double ag[4 * kJ], ar[4 * kJ], ao[4 * kJ];
+#pragma unroll
+    for (int i = 0; i < 4 * kJ; ++i) ag[i] = ar[i] = ao[i] = 0.0;
+    const int nv0 = n - r0;
+#pragma unroll 2
     for (int c = 0; c < kChannels; ++c) {
         const double wg = kg[c], wr = kr[c], wo = ko[c];
-        const float *p = base + (int64_t)c * T;
-        double x0, x1, x2, x3;
-        if (full) {
-            const f32x4u x = *reinterpret_cast<const f32x4u *>(p);
-            x0 = x.x; x1 = x.y; x2 = x.z; x3 = x.w;
-        } else {
-            x0 = nv > 0 ? (double)p[0] : 0.0;
-            x1 = nv > 1 ? (double)p[1] : 0.0;
-            x2 = nv > 2 ? (double)p[2] : 0.0;
-            x3 = 0.0;
+        double x[4 * kJ];
+        load_groups(base + (int64_t)c * T, nv0, x);
+#pragma unroll
+        for (int i = 0; i < 4 * kJ; ++i) {
+            ag[i] = fma(wg, x[i], ag[i]);
+            ar[i] = fma(wr, x[i], ar[i]);
+            ao[i] = fma(wo, x[i], ao[i]);
         }
-        g0 = fma(wg, x0, g0); g1 = fma(wg, x1, g1); g2 = fma(wg, x2, g2); g3 = fma(wg, x3, g3);
-        rr0 = fma(wr, x0, rr0); rr1 = fma(wr, x1, rr1); rr2 = fma(wr, x2, rr2); rr3 = fma(wr, x3, rr3);
-        o0 = fma(wo, x0, o0); o1 = fma(wo, x1, o1); o2 = fma(wo, x2, o2); o3 = fma(wo, x3, o3);
     }
     const double *ds = dsum + 16 * ((int64_t)u * kBands + b);
-    const double *a = A + (int64_t)f * T + t0;
-    const double *m = mf + (int64_t)(f * kBands + b) * T + t0;
-    const double gs[4] = {g0, g1, g2, g3}, rs[4] = {rr0, rr1, rr2, rr3}, os[4] = {o0, o1, o2, o3};
-    double at[4], mt[4];
+    const double *a = A + (int64_t)f * T + t0 + r0;
+    const double *m = mf + (int64_t)(f * kBands + b) * T + t0 + r0;
+    double at[4 * kJ], mt[4 * kJ];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const bool ok = j < nv;
-        at[j] = ok ? a[r0 + j] : 0.0;
-        mt[j] = ok ? m[r0 + j] : 0.0;
-        sg[b][4 * lane + j] = gs[j] + ds[0] + at[j] * ds[1] + mt[j] * ds[2];
-    }
+    for (int g = 0; g < kJ; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int i = 4 * g + e, o = 256 * g + e;
+            const bool ok = o < nv0;
+            at[i] = ok ? a[o] : 0.0;
+            mt[i] = ok ? m[o] : 0.0;
+            sg[b][256 * g + 4 * lane + e] = ag[i] + ds[0] + at[i] * ds[1] + mt[i] * ds[2];
+        }
     __syncthreads();
     double *to = tod_out + (int64_t)(f * kBands + b) * T + t0 + r0;
     double *oo = orig_out + (int64_t)(f * kBands + b) * T + t0 + r0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        if (j >= nv) break;
-        const int tl = 4 * lane + j;
-        const double dG = sg[0][tl] + sg[1][tl] + sg[2][tl] + sg[3][tl];
-        const double sr = rs[j] + ds[3] + at[j] * ds[4] + mt[j] * ds[5];
-        const double so = os[j] + ds[6] + at[j] * ds[7] + mt[j] * ds[8];
-        to[j] = (sr - dG * ds[9]) / ds[10];
-        oo[j] = so / ds[11];
-        if (b == 0) dG_out[(int64_t)f * T + t0 + r0 + j] = dG;
-    }
+    for (int g = 0; g < kJ; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int i = 4 * g + e, o = 256 * g + e;
+            if (o >= nv0) continue;
+            const int tl = 256 * g + 4 * lane + e;
+            const double dG = sg[0][tl] + sg[1][tl] + sg[2][tl] + sg[3][tl];
+            const double sr = ar[i] + ds[3] + at[i] * ds[4] + mt[i] * ds[5];
+            const double so = ao[i] + ds[6] + at[i] * ds[7] + mt[i] * ds[8];
+            to[o] = (sr - dG * ds[9]) / ds[10];
+            oo[o] = so / ds[11];
+            if (b == 0) dG_out[(int64_t)f * T + t0 + r0 + o] = dG;
+        }
 }
 
 // ------------------------------------------------------------------ scan weights
@@ -813,6 +952,10 @@ extern "C" int comap_l1_plan_create(comap_ctx *ctx, const comap_obs_desc *d, com
     rc |= dalloc(ctx, &p->dsum, 16 * (size_t)p->U * kBands);
     rc |= dalloc(ctx, &p->xreg, 2 * (size_t)UC);
     rc |= dalloc(ctx, &p->dG, (size_t)p->F * p->T);
+    rc |= dalloc(ctx, &p->rowbad, UC);
+    rc |= dalloc(ctx, &p->ubs, 4 * (size_t)p->U * kBands);
+    rc |= dalloc(ctx, &p->fitsum, 2 * (size_t)UC);
+    rc |= dalloc(ctx, &p->oa, 2 * (size_t)UC);
     if (rc) { delete p; return -2; }
     // median jobs: (unit, band) series, reflect-3 padded [rev, x, rev], outputs [n, 2n)
     // (bands of scans shorter than 2w are skipped by median_filter: no outputs)
@@ -848,7 +991,7 @@ extern "C" int comap_l1_plan_destroy(comap_l1_plan *p)
     if (!p) return 0;
     void *bufs[] = {p->units, p->tiles, p->airmass, p->unit_sums, p->mom,
                     p->nan_count, p->alpha, p->nf, p->bsum, p->mb, p->mf, p->ssum, p->sdm, p->gw,
-                    p->gmode, p->kap, p->dsum, p->xreg, p->dG};
+                    p->gmode, p->kap, p->dsum, p->xreg, p->dG, p->rowbad, p->ubs, p->fitsum, p->oa};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     comap_median_plan_free(&p->med);
@@ -864,30 +1007,149 @@ static int run_moments(comap_l1_plan *p)
     COMAP_CHECK(ctx, hipMemsetAsync(p->nan_count, 0, 4, ctx->stream));
     const int64_t grid = (int64_t)p->U * kBands * (kChannels / (4 * kCPW));
     PROF(p, KV_MOMENTS, k_moments<<<grid, 256, 0, ctx->stream>>>(p->tod, p->airmass, p->units, p->T, p->mom, UC,
-                                                                 p->nan_count));
+                                                                 p->nan_count, p->rowbad));
     COMAP_LAUNCH_CHECK(ctx);
-    int32_t nanc = 0;
-    COMAP_CHECK(ctx, hipMemcpyAsync(&nanc, p->nan_count, 4, hipMemcpyDeviceToHost, ctx->stream));
+    // one 4-byte read-back per pass A decides whether the NaN path runs
+    COMAP_CHECK(ctx, hipMemcpyAsync(&p->nan_total, p->nan_count, 4, hipMemcpyDeviceToHost, ctx->stream));
     COMAP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
-    if (nanc)
-        return comap_fail(ctx, -5, "non-finite samples in the Level-1 TOD: the NaN fill/"
-                                   "select_time path (fill_bad_data) is not implemented on the device");
     p->moments_valid = true;
     return 0;
 }
 
-extern "C" int comap_l1_atmosphere(comap_l1_plan *p, double *fit)
+static int fetch_rowbad(comap_l1_plan *p, std::vector<int32_t> &rb)
+{
+    comap_ctx *ctx = p->ctx;
+    rb.resize((size_t)p->U * kBC);
+    COMAP_CHECK(ctx, hipMemcpyAsync(rb.data(), p->rowbad, 4 * rb.size(), hipMemcpyDeviceToHost, ctx->stream));
+    COMAP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+// nanmedian (f32) of the given (unit, band*1024+channel) rows over their scans
+static int unit_row_medians(comap_l1_plan *p, const std::vector<int64_t> &rowids, float *med_dev)
+{
+    std::vector<int64_t> rows(2 * rowids.size());
+    for (size_t k = 0; k < rowids.size(); ++k) {
+        const int64_t i = rowids[k];
+        const int u = (int)(i / kBC), bc = (int)(i % kBC);
+        const int32_t *q = &p->units_h[4 * u];
+        rows[2 * k] = ((int64_t)q[0] * kBC + bc) * p->T + q[2];
+        rows[2 * k + 1] = q[3];
+    }
+    return comap_row_nanmedian(p->ctx, p->tod, rows.data(), (int32_t)rowids.size(), med_dev);
+}
+
+extern "C" int comap_l1_atmosphere(comap_l1_plan *p, const int32_t *const_el_units, int32_t n_const_el,
+                                   double *fit)
 {
     if (!p || !fit) return -1;
     comap_ctx *ctx = p->ctx;
+    hipStream_t st = ctx->stream;
     int rc = run_moments(p);
     if (rc) return rc;
     const int64_t UC = (int64_t)p->U * kBC;
-    const int64_t n = UC;
-    PROF(p, KV_ATMOS_FIT, k_atmos_fit<<<(n + 255) / 256, 256, 0, ctx->stream>>>(p->units, p->unit_sums, p->mom, UC,
-                                                                                p->F, p->U, fit));
+    const int UB = p->U * kBands;
+    k_ub_from_units<<<(UB + 255) / 256, 256, 0, st>>>(p->unit_sums, p->U, p->ubs);
     COMAP_LAUNCH_CHECK(ctx);
+    const double *fs = p->mom;
+    if (p->nan_total > 0) {
+        // select_time: (unit, band) pairs with a non-finite sample in a fitted channel
+        std::vector<int32_t> rb;
+        if ((rc = fetch_rowbad(p, rb))) return rc;
+        std::vector<int32_t> pairs;
+        std::vector<int64_t> voff(1, 0);
+        for (int u = 0; u < p->U; ++u)
+            for (int b = 0; b < kBands; ++b) {
+                bool any = false;
+                for (int c = 0; c < kChannels && !any; ++c)
+                    any = atmos_channel_host(c) && rb[(size_t)u * kBC + b * kChannels + c] > 0;
+                if (!any) continue;
+                pairs.push_back(u);
+                pairs.push_back(b);
+                voff.push_back(voff.back() + p->units_h[4 * u + 3]);
+            }
+        if (!pairs.empty()) {
+            const int np = (int)pairs.size() / 2;
+            int32_t *dpairs = nullptr;
+            int64_t *dvoff = nullptr;
+            uint8_t *valid = nullptr;
+            COMAP_CHECK(ctx, hipMalloc((void **)&dpairs, 4 * pairs.size()));
+            COMAP_CHECK(ctx, hipMalloc((void **)&dvoff, 8 * voff.size()));
+            COMAP_CHECK(ctx, hipMalloc((void **)&valid, voff.back() + 1));
+            COMAP_CHECK(ctx, hipMemcpyAsync(dpairs, pairs.data(), 4 * pairs.size(), hipMemcpyHostToDevice, st));
+            COMAP_CHECK(ctx, hipMemcpyAsync(dvoff, voff.data(), 8 * voff.size(), hipMemcpyHostToDevice, st));
+            COMAP_CHECK(ctx, hipMemcpyAsync(p->fitsum, p->mom, 16 * UC, hipMemcpyDeviceToDevice, st));
+            int maxn = 0;
+            for (int k = 0; k < np; ++k) maxn = std::max(maxn, p->units_h[4 * pairs[2 * k] + 3]);
+            k_select_time<<<dim3((maxn + 255) / 256, np), 256, 0, st>>>(p->tod, p->units, dpairs, p->T, dvoff, valid);
+            COMAP_LAUNCH_CHECK(ctx);
+            k_masked_fit_sums<<<dim3(kChannels / 4, np), 256, 0, st>>>(p->tod, p->airmass, p->units, dpairs, p->T,
+                                                                       dvoff, valid, UC, p->fitsum, p->ubs);
+            COMAP_LAUNCH_CHECK(ctx);
+            COMAP_CHECK(ctx, hipStreamSynchronize(st));
+            (void)hipFree(dpairs); (void)hipFree(dvoff); (void)hipFree(valid);
+            fs = p->fitsum;
+        }
+    }
+    PROF(p, KV_ATMOS_FIT, k_atmos_fit<<<(UC + 255) / 256, 256, 0, st>>>(p->units, p->ubs, fs, UC, p->F, p->U, fit));
+    COMAP_LAUNCH_CHECK(ctx);
+    if (n_const_el > 0) {
+        // constant-elevation scans: (nanmedian over the scan, 0) for every channel
+        std::vector<int64_t> ids;
+        for (int k = 0; k < n_const_el; ++k) {
+            const int u = const_el_units[k];
+            if (u < 0 || u >= p->U) return comap_fail(ctx, -1, "constant-elevation unit out of range");
+            for (int bc = 0; bc < kBC; ++bc) ids.push_back((int64_t)u * kBC + bc);
+        }
+        float *med = nullptr;
+        int32_t *dl = nullptr;
+        COMAP_CHECK(ctx, hipMalloc((void **)&med, 4 * ids.size()));
+        COMAP_CHECK(ctx, hipMalloc((void **)&dl, 4 * (size_t)n_const_el));
+        COMAP_CHECK(ctx, hipMemcpyAsync(dl, const_el_units, 4 * (size_t)n_const_el, hipMemcpyHostToDevice, st));
+        if ((rc = unit_row_medians(p, ids, med))) return rc;
+        const int64_t nt = (int64_t)n_const_el * kBC;
+        k_fit_from_median<<<(nt + 255) / 256, 256, 0, st>>>(p->units, dl, n_const_el, med, p->F, fit);
+        COMAP_LAUNCH_CHECK(ctx);
+        COMAP_CHECK(ctx, hipStreamSynchronize(st));
+        (void)hipFree(med); (void)hipFree(dl);
+    }
     return 0;
+}
+
+// fill_bad_data for every row holding a NaN, then pass A again on the filled cube
+static int fill_nan_rows(comap_l1_plan *p)
+{
+    comap_ctx *ctx = p->ctx;
+    hipStream_t st = ctx->stream;
+    std::vector<int32_t> rb;
+    int rc = fetch_rowbad(p, rb);
+    if (rc) return rc;
+    std::vector<int64_t> ids;
+    for (size_t i = 0; i < rb.size(); ++i)
+        if (rb[i] > 0) ids.push_back((int64_t)i);
+    if (ids.empty()) return 0;
+    float *med = nullptr;
+    int64_t *drows = nullptr;
+    std::vector<int64_t> rows(2 * ids.size());
+    for (size_t k = 0; k < ids.size(); ++k) {
+        const int u = (int)(ids[k] / kBC), bc = (int)(ids[k] % kBC);
+        const int32_t *q = &p->units_h[4 * u];
+        rows[2 * k] = ((int64_t)q[0] * kBC + bc) * p->T + q[2];
+        rows[2 * k + 1] = q[3];
+    }
+    COMAP_CHECK(ctx, hipMalloc((void **)&med, 4 * ids.size()));
+    COMAP_CHECK(ctx, hipMalloc((void **)&drows, 8 * rows.size()));
+    COMAP_CHECK(ctx, hipMemcpyAsync(drows, rows.data(), 8 * rows.size(), hipMemcpyHostToDevice, st));
+    if ((rc = comap_row_nanmedian(ctx, p->tod, rows.data(), (int32_t)ids.size(), med))) return rc;
+    for (size_t r0 = 0; r0 < ids.size(); r0 += 65535) {
+        const int nr = (int)std::min<size_t>(65535, ids.size() - r0);
+        k_fill_rows<<<dim3(16, nr), 256, 0, st>>>(const_cast<float *>(p->tod), drows + 2 * r0, med + r0, nr);
+        COMAP_LAUNCH_CHECK(ctx);
+    }
+    COMAP_CHECK(ctx, hipStreamSynchronize(st));
+    (void)hipFree(med); (void)hipFree(drows);
+    p->filled = true;
+    return run_moments(p);
 }
 
 extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const double *tsys0, const double *gain0,
@@ -895,23 +1157,28 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
 {
     if (!p || !fit || !tsys0 || !gain0 || !tod_out || !orig_out || !w_out) return -1;
     comap_ctx *ctx = p->ctx;
-    if (calibrator)
-        return comap_fail(ctx, -4, "calibrator sources (per-channel median atmosphere) are not "
-                                   "implemented on the device");
-    if (!p->moments_valid) {
-        int rc = run_moments(p);
-        if (rc) return rc;
-    }
+    int rc = 0;
+    if (!p->moments_valid && (rc = run_moments(p))) return rc;
+    if (p->nan_total > 0 && !p->filled && (rc = fill_nan_rows(p))) return rc;
     const int64_t UC = (int64_t)p->U * kBC;
     const int UB = p->U * kBands;
     hipStream_t st = ctx->stream;
-    PROF(p, KV_COEF_B, k_coef_b<<<UB, 256, 0, st>>>(p->units, p->unit_sums, p->mom, UC, fit, p->F, p->alpha,
-                                                    p->nf, p->bsum));
+    // offsets/slopes to subtract: the scan fits, or per-channel nanmedians for calibrators
+    float *cmed = nullptr;
+    if (calibrator) {
+        std::vector<int64_t> ids(UC);
+        for (int64_t i = 0; i < UC; ++i) ids[i] = i;
+        COMAP_CHECK(ctx, hipMalloc((void **)&cmed, 4 * (size_t)UC));
+        if ((rc = unit_row_medians(p, ids, cmed))) return rc;
+    }
+    k_gather_oa<<<(UC + 255) / 256, 256, 0, st>>>(p->units, fit, p->F, p->U, cmed, p->oa);
+    COMAP_LAUNCH_CHECK(ctx);
+    PROF(p, KV_COEF_B, k_coef_b<<<UB, 256, 0, st>>>(p->units, p->unit_sums, p->mom, UC, p->oa, p->alpha, p->nf,
+                                                    p->bsum));
     COMAP_LAUNCH_CHECK(ctx);
     PROF(p, KV_BAND_MEAN, k_band_mean<<<p->n_tiles, 256, 0, st>>>(p->tod, p->airmass, p->units, p->tiles, p->T,
                                                                   p->alpha, p->bsum, p->mb));
     COMAP_LAUNCH_CHECK(ctx);
-    int rc = 0;
     PROF(p, KV_MEDIAN, rc = comap_median_run(ctx, &p->med));
     if (rc) return rc;
     PROF(p, KV_SERIES_SUMS, k_series_sums<<<UB, 256, 0, st>>>(p->units, p->airmass, p->T, p->bsum, p->mf, p->ssum));
@@ -921,7 +1188,7 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
     COMAP_LAUNCH_CHECK(ctx);
     PROF(p, KV_GAIN_WEIGHTS, k_gain_weights<<<p->F, 1024, 0, st>>>(tsys0, p->gw, p->gmode));
     COMAP_LAUNCH_CHECK(ctx);
-    PROF(p, KV_COEF_D, k_coef_d<<<UB, 256, 0, st>>>(p->units, p->unit_sums, p->mom, UC, fit, p->F, p->alpha, p->nf,
+    PROF(p, KV_COEF_D, k_coef_d<<<UB, 256, 0, st>>>(p->units, p->unit_sums, p->mom, UC, p->oa, p->alpha, p->nf,
                                                     p->bsum, p->ssum, p->sdm, tsys0, gain0, p->gw, p->gmode,
                                                     calibrator, p->kap, p->dsum, p->xreg));
     COMAP_LAUNCH_CHECK(ctx);
@@ -930,8 +1197,13 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
     COMAP_LAUNCH_CHECK(ctx);
     PROF(p, KV_SCAN_WEIGHTS, k_scan_weights<<<UB, 256, 0, st>>>(p->units, p->T, tod_out, w_out));
     COMAP_LAUNCH_CHECK(ctx);
+    if (cmed) {
+        COMAP_CHECK(ctx, hipStreamSynchronize(st));
+        (void)hipFree(cmed);
+    }
     return 0;
 }
+
 
 extern "C" int comap_l1_vane(comap_l1_plan *p, int64_t vstart, int64_t vlen, const int32_t *hot_h,
                              const int64_t *hoff_h, const int32_t *cold_h, const int64_t *coff_h,

@@ -97,13 +97,12 @@ class GPUObservation:
         self.edges = np.asarray(to_host(data.scan_edges), dtype=np.int64).reshape(-1, 2)
         self.S = len(self.edges)
         self.feeds = np.asarray(to_host(data['spectrometer/feeds'])).reshape(-1)
-        for s, e in self.edges:
-            if e > s and np.all(self.features[s:e] == 9):
-                raise NotImplementedError('constant-elevation scan (features == 9): the per-channel '
-                                          'median atmosphere of filter_atmosphere is not implemented '
-                                          'on the device')
         units = [(f, s, int(a), int(b - a)) for f in range(F) for s, (a, b) in enumerate(self.edges) if b > a]
         self.units = np.ascontiguousarray(np.array(units, dtype=np.int32).reshape(-1, 4))
+        # constant-elevation scans (features == 9 throughout): median atmosphere (Level1Averaging.py:242-244)
+        const_scans = {s for s, (a, b) in enumerate(self.edges) if b > a and np.all(self.features[a:b] == 9)}
+        self.const_el_units = np.ascontiguousarray(
+            np.array([u for u, q in enumerate(self.units) if q[1] in const_scans], dtype=np.int32))
         desc = N.ObsDesc(F, B, C, self.S, T, self.tod.data_ptr(), self.el.data_ptr(), len(units),
                          N.hptr(self.units, ctypes.c_int32))
         plan = ctypes.c_void_p()
@@ -169,7 +168,9 @@ class GPUObservation:
         fit = torch.full((self.S, self.F, N_BANDS, 2, N_CHANNELS), float('nan'), dtype=torch.float64,
                          device=self.tdev)
         self._bind()
-        N.check(N.lib().comap_l1_atmosphere(self.plan, N.dptr(fit)), self.ctx, 'comap_l1_atmosphere')
+        ce = self.const_el_units
+        N.check(N.lib().comap_l1_atmosphere(self.plan, N.hptr(ce, ctypes.c_int32) if ce.size else None, int(ce.size),
+                                            N.dptr(fit)), self.ctx, 'comap_l1_atmosphere')
         return fit
 
     def average(self, fit_values, tsys0, gain0, calibrator: bool = False):

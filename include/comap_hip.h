@@ -90,15 +90,20 @@ int comap_l1_vane(comap_l1_plan *plan, int64_t vane_start, int64_t vane_len,
                   double t_hot, double *tsys_dev, double *gain_dev);
 
 /* AtmosphereRemoval: writes fit_values dev f64 [S][F][4][2][1024]
- * (offset, slope per channel; NaN outside the fitted channel set).  Units
- * whose scan is constant-elevation (features == 9 throughout) are not
- * supported (returns -4). Also caches the per-channel noise moments the
- * Level-2 averaging reuses. */
-int comap_l1_atmosphere(comap_l1_plan *plan, double *fit_values_dev);
+ * (offset, slope per channel; NaN outside the fitted channel set, or when
+ * fewer than 100 samples are finite in all fitted channels -- select_time).
+ * const_el_units_host lists the units whose scan is constant-elevation
+ * (features == 9 throughout): their fit is (per-channel nanmedian, 0).  Also
+ * caches the per-channel noise moments the Level-2 averaging reuses. */
+int comap_l1_atmosphere(comap_l1_plan *plan, const int32_t *const_el_units_host, int32_t n_const_el,
+                        double *fit_values_dev);
 
 /* Level1AveragingGainCorrection.average_tod for every unit.
  *   fit_values dev [S][F][4][2][1024], tsys0/gain0 dev [F][4][1024]
- *   (vane event 0), calibrator != 0 for calibrator sources.
+ *   (vane event 0), calibrator != 0 for calibrator sources (per-channel
+ *   nanmedian instead of the fit, no gain subtraction).
+ * NaN samples inside the units are replaced IN PLACE in the device cube by
+ * their channel's scan nanmedian (fill_bad_data) before the reduction.
  * Outputs dev f64 [F][4][T]: tod (gain-subtracted residual), tod_original,
  * weights.  Samples outside the units are left untouched (caller zeroes). */
 int comap_l1_average(comap_l1_plan *plan, const double *fit_values_dev,

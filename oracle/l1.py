@@ -385,19 +385,29 @@ def average_tod(tod, A, edges, fit_values, tsys0, gain0, feeds, source=''):
             'averaged_tod/frequency_power_spectra_fits': np.zeros((S, F, B, 3))}
 
 
-def reduce_level1(data):
+def scan_edges_calibrator(feats):
+    """RepointEdges.get_scan_positions_calibrator, DataHandling.py:231-245
+    (on_source: features not in {13, 0, 16}, :304-307)."""
+    idx = np.where((feats != 13) & (feats != 0) & (feats != 16))[0]
+    return np.array([[int(min(idx))], [int(max(idx))]]).T
+
+
+def reduce_level1(data, source=''):
     """Full MeasureSystemTemperature -> AtmosphereRemoval ->
     Level1AveragingGainCorrection on a dict of Level-1 datasets."""
     d = data
     feats = features(d['spectrometer/features'])
-    edges = scan_edges(d['hk/antenna0/deTracker/lissajous_status'], d['hk/antenna0/deTracker/utc'],
-                       d['spectrometer/MJD'], feats)
+    if source in CALIBRATORS:
+        edges = scan_edges_calibrator(feats)
+    else:
+        edges = scan_edges(d['hk/antenna0/deTracker/lissajous_status'], d['hk/antenna0/deTracker/utc'],
+                           d['spectrometer/MJD'], feats)
     tod = d['spectrometer/tod']
     t_hot = vane_temperature(d['spectrometer/MJD'][0], d['hk/antenna0/vane/Tvane'])
     tsys, gain = measure_system_temperature(tod, d['spectrometer/band_average'], feats, t_hot)
     A = airmass(d['spectrometer/pixel_pointing/pixel_el'])
     fit = filter_atmosphere(tod, A, edges, feats)
-    out = average_tod(tod, A, edges, fit, tsys[0], gain[0], d['spectrometer/feeds'])
+    out = average_tod(tod, A, edges, fit, tsys[0], gain[0], d['spectrometer/feeds'], source)
     out['vane/system_temperature'] = tsys
     out['vane/system_gain'] = gain
     out['atmosphere/fit_values'] = fit

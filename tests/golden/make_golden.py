@@ -196,6 +196,33 @@ def run_l1(out, meta, figdir):
         out[k.replace('/', '__')] = np.asarray(level2[k])
 
 
+def run_l1_variant(name, figdir):
+    """Edge-case observations (tests/golden/variants.py) through the same three stages."""
+    from comancpipeline.Analysis.DataHandling import COMAPLevel1, COMAPLevel2
+    from comancpipeline.Analysis.VaneCalibration import MeasureSystemTemperature
+    from comancpipeline.Analysis.Level1Averaging import AtmosphereRemoval, Level1AveragingGainCorrection
+    sys.path.insert(0, HERE)
+    import variants
+    gen = variants.make(name)
+    data = COMAPLevel1(overwrite=False, large_datasets=['spectrometer/tod'])
+    for k, v in gen['data'].items():
+        data[k] = CopyOnSlice(v) if k == 'spectrometer/tod' else v
+    for k, v in gen['attrs']['comap'].items():
+        data.set_attrs('comap', k, v)
+    level2 = COMAPLevel2(filename=os.path.join(figdir, 'does_not_exist.hd5'))
+    for cls in (MeasureSystemTemperature, AtmosphereRemoval, Level1AveragingGainCorrection):
+        stage = cls(level2=level2, figure_directory=figdir)
+        assert stage(data, level2), cls.__name__
+        level2.update(stage)
+    out = {}
+    for k in ('vane/system_temperature', 'vane/system_gain', 'atmosphere/fit_values',
+              'averaged_tod/tod', 'averaged_tod/tod_original', 'averaged_tod/weights',
+              'averaged_tod/scan_edges'):
+        out[k.replace('/', '__')] = np.asarray(level2[k])
+    np.savez_compressed(os.path.join(HERE, f'golden_l1_{name}.npz'), **out)
+    return {k: synthetic.sha256(v) for k, v in gen['data'].items()}
+
+
 def run_medfilt(out):
     from comancpipeline.Tools.median_filter import medfilt
     for seed, n, w in MEDFILT_CASES:
@@ -247,7 +274,21 @@ def run_destriper(out, meta):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--skip-l1', action='store_true')
+    ap.add_argument('--only-variants', action='store_true')
     args = ap.parse_args()
+    if args.only_variants:
+        os.environ.setdefault('MPLBACKEND', 'agg')
+        build_reference_helpers()
+        install_stubs()
+        figdir = os.path.join(SCRATCH, 'figures')
+        os.makedirs(figdir, exist_ok=True)
+        import variants
+        mp = os.path.join(HERE, 'golden_meta.json')
+        meta = json.load(open(mp))
+        for name in variants.NAMES:
+            meta[f'l1_{name}_sha256'] = run_l1_variant(name, figdir)
+        json.dump(meta, open(mp, 'w'), indent=1, default=str)
+        return
     os.environ.setdefault('MPLBACKEND', 'agg')
     build_reference_helpers()
     install_stubs()

@@ -1,0 +1,40 @@
+"""Edge-case Level-1 observations shared by make_golden.py and the tests.
+
+Each variant is the synthetic generator's output with a deterministic edit:
+  nan      NaNs inside the scan: a short burst in a fitted channel (select_time
+           drops those samples for the whole band), a partly-NaN fitted
+           channel, a fully-NaN unfitted channel, a single NaN sample
+           (fill_bad_data / select_time paths, Level1Averaging.py:204, 658-665)
+  constel  the scan's features are all 2**9 (constant-elevation: per-channel
+           nanmedian atmosphere, Level1Averaging.py:242-244)
+  calib    source 'TauA' (calibrator scan edges DataHandling.py:231-245,
+           median atmosphere + no gain subtraction, Level1Averaging.py:647-648, 719-724)
+"""
+import numpy as np
+
+from comapreduce_amd import synthetic
+
+T_EDGE = 16_000
+
+
+def make(name):
+    if name == 'calib':
+        cfg = synthetic.SyntheticConfig(n_feeds=1, n_samples=T_EDGE, obs_id=11, source='TauA')
+    else:
+        cfg = synthetic.SyntheticConfig(n_feeds=1, n_samples=T_EDGE, obs_id={'nan': 12, 'constel': 13}[name])
+    gen = synthetic.generate_level1(cfg)
+    d = gen['data']
+    if name == 'nan':
+        tod = d['spectrometer/tod']
+        tod[0, 0, 100, 3000:3010] = np.nan      # fitted channel: 10 samples leave select_time (band 0)
+        tod[0, 3, 700, 8000:8050] = np.nan      # fitted channel, band 3
+        tod[0, 1, 5, 1500:] = np.nan            # unfitted channel, NaN over the whole scan
+        tod[0, 2, 300, 5000] = np.nan           # single sample
+        d['spectrometer/band_average'] = np.nanmean(tod, axis=2).astype(np.float32)
+    elif name == 'constel':
+        f = d['spectrometer/features']
+        f[synthetic.SCAN_START:] = 2.0 ** 9
+    return gen
+
+
+NAMES = ('nan', 'constel', 'calib')

@@ -107,3 +107,24 @@ def test_l1_median_selection_bit_exact(c1_run):
             pad = np.concatenate([m[::-1], m, m[::-1]])
             ref = oracle.medfilt(pad, 6000)[n:2 * n]
             assert np.array_equal(mf[f, b, t0:t0 + n], ref), (f, s, b)
+
+
+@pytest.mark.parametrize('name', ['nan', 'constel', 'calib'])
+def test_l1_edge_variants_vs_reference(golden_dir, name):
+    """NaN fill/select_time, constant-elevation and calibrator paths on the device."""
+    import sys
+    sys.path.insert(0, golden_dir)
+    import variants
+    from comapreduce_amd import Analysis as A
+    gen = variants.make(name)
+    data = level1_from_dict(gen)
+    level2 = COMAPLevel2(filename='/nonexistent/none.hd5')
+    for cls in (A.MeasureSystemTemperature, A.AtmosphereRemoval, A.Level1AveragingGainCorrection):
+        st = cls(level2=level2)
+        assert st(data, level2)
+        level2.update(st)
+    g = np.load(os.path.join(golden_dir, f'golden_l1_{name}.npz'))
+    assert np.array_equal(level2['averaged_tod/scan_edges'], g['averaged_tod__scan_edges'])
+    for k in ('vane/system_temperature', 'vane/system_gain', 'atmosphere/fit_values', 'averaged_tod/tod',
+              'averaged_tod/tod_original', 'averaged_tod/weights'):
+        assert relmax(level2[k], g[k.replace('/', '__')]) < RTOL, (name, k)
