@@ -5,3 +5,4 @@ from ..pipeline.running import Runner, PipelineFunction, set_logging  # noqa: F4
 from ..pipeline.datahandling import HDF5Data, COMAPLevel1, COMAPLevel2, RepointEdges  # noqa: F401
 from ..stages.level1 import (MeasureSystemTemperature, AtmosphereRemoval,  # noqa: F401
                              Level1AveragingGainCorrection, CheckLevel1File, AssignLevel1Data)
+from ..stages.statistics import Spikes  # noqa: F401,E402

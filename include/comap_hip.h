@@ -123,6 +123,17 @@ int comap_l1_debug_fetch(comap_l1_plan *plan, int32_t what, double *out_host, in
 int comap_l1_profile(comap_l1_plan *plan, int32_t enable);
 int comap_l1_profile_collect(comap_l1_plan *plan, double *ms_host, int64_t *counts_host, int32_t n);
 
+/* ------------------------------------------------------------ Level-2 spike mask */
+/* Statistics.Spikes.run_fit_spikes (Analysis/Statistics.py:63-105) on a
+ * device Level-2 TOD f64 [n_rows][T] (rows = feed*4 + band), scans from
+ * edges_host [n_scans][2]: per row rms = tod_auto_rms (non-zero samples),
+ * per scan medfilt(w = medfilt_window) high-pass, |x| > threshold*rms,
+ * runs dilated as fit_spikes does with `step`.  mask_dev uint8 [n_rows][T]
+ * (0 outside the scans).  Synchronises. */
+int comap_spikes(comap_ctx *ctx, const double *tod_dev, int32_t n_rows, int64_t n_samples,
+                 const int64_t *edges_host, int32_t n_scans, int32_t medfilt_window, int32_t step,
+                 double threshold, uint8_t *mask_dev);
+
 /* ------------------------------------------------------------ synthetic input (bench) */
 /* Fills a device-resident synthetic observation with the statistics of
  * tod f32 [F][4][1024][T], band_average f32 [F][4][T].

@@ -223,6 +223,23 @@ def run_l1_variant(name, figdir):
     return {k: synthetic.sha256(v) for k, v in gen['data'].items()}
 
 
+def run_spikes():
+    """Statistics.Spikes (Statistics.py:31-105) on a Level-2 TOD with injected spikes."""
+    from comancpipeline.Analysis.DataHandling import COMAPLevel2
+    from comancpipeline.Analysis.Statistics import Spikes
+    sys.path.insert(0, HERE)
+    import variants
+    tod, edges = variants.spikes_level2(HERE)
+    l2 = COMAPLevel2(filename='/nonexistent/spikes.hd5')
+    l2['averaged_tod/tod'] = tod
+    l2['averaged_tod/scan_edges'] = edges
+    l2['spectrometer/feeds'] = np.array([1])
+    l2.set_attrs('comap', 'source', 'Field00')
+    st = Spikes(level2=l2)
+    assert st(l2, l2)
+    np.savez_compressed(os.path.join(HERE, 'golden_spikes.npz'), spike_mask=st.data['spikes/spike_mask'])
+
+
 def run_medfilt(out):
     from comancpipeline.Tools.median_filter import medfilt
     for seed, n, w in MEDFILT_CASES:
@@ -287,6 +304,7 @@ def main():
         meta = json.load(open(mp))
         for name in variants.NAMES:
             meta[f'l1_{name}_sha256'] = run_l1_variant(name, figdir)
+        run_spikes()
         json.dump(meta, open(mp, 'w'), indent=1, default=str)
         return
     os.environ.setdefault('MPLBACKEND', 'agg')

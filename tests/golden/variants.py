@@ -38,3 +38,19 @@ def make(name):
 
 
 NAMES = ('nan', 'constel', 'calib')
+
+
+def spikes_level2(golden_dir):
+    """Level-2 input of the Spikes golden: the C1 golden averaged_tod with
+    injected spikes (single samples, a 3-sample burst, one at a scan edge,
+    one at the first sample of the file) and one scan-band with a NaN."""
+    import os
+    g = np.load(os.path.join(golden_dir, 'golden_l1_c1.npz'))
+    tod = g['averaged_tod__tod'].copy()
+    edges = g['averaged_tod__scan_edges']
+    tod[0, 0, 5000] += 3.0
+    tod[0, 1, 9000:9003] -= 2.5
+    tod[0, 2, edges[0, 0]] += 4.0
+    tod[0, 3, 20000] += 1.0
+    tod[0, 3, 25000] = np.nan
+    return tod, edges

@@ -128,3 +128,19 @@ def test_l1_edge_variants_vs_reference(golden_dir, name):
     for k in ('vane/system_temperature', 'vane/system_gain', 'atmosphere/fit_values', 'averaged_tod/tod',
               'averaged_tod/tod_original', 'averaged_tod/weights'):
         assert relmax(level2[k], g[k.replace('/', '__')]) < RTOL, (name, k)
+
+
+def test_spikes_stage_bit_exact(golden_dir):
+    import sys
+    sys.path.insert(0, golden_dir)
+    import variants
+    from comapreduce_amd import Analysis as A
+    tod, edges = variants.spikes_level2(golden_dir)
+    l2 = COMAPLevel2(filename='/nonexistent/spk.hd5')
+    l2['averaged_tod/tod'] = tod
+    l2['averaged_tod/scan_edges'] = edges
+    l2.set_attrs('comap', 'source', 'Field00')
+    st = A.Spikes(level2=l2)
+    assert st(l2, l2)
+    g = np.load(os.path.join(golden_dir, 'golden_spikes.npz'))['spike_mask']
+    assert np.array_equal(st.data['spikes/spike_mask'], g)

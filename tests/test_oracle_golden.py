@@ -106,3 +106,13 @@ def test_oracle_l1_edge_variants(golden_dir, name):
     for k, tol in [('vane/system_temperature', 0.0), ('atmosphere/fit_values', 1e-9), ('averaged_tod/tod', t),
                    ('averaged_tod/tod_original', t), ('averaged_tod/weights', t)]:
         assert relmax(out[k], g[k.replace('/', '__')]) <= tol, k
+
+
+def test_oracle_spikes_bit_exact(golden_dir):
+    import sys
+    sys.path.insert(0, golden_dir)
+    import variants
+    from oracle import spikes
+    tod, edges = variants.spikes_level2(golden_dir)
+    g = np.load(os.path.join(golden_dir, 'golden_spikes.npz'))['spike_mask']
+    assert np.array_equal(spikes.spike_mask(tod, edges), g)
