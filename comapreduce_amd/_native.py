@@ -37,6 +37,7 @@ _SIGS = {
     'comap_synchronize': (c_int, [c_void_p]),
     'comap_version': (ctypes.c_char_p, []),
     'comap_medfilt_f64': (c_int, [c_void_p, P_double, c_int64, c_int32]),
+    'comap_medfilt_batch_f64': (c_int, [c_void_p, P_double, P_int64, c_int32, c_int32, c_int32, P_double]),
     'comap_bin_values_f64': (c_int, [c_void_p, P_double, c_int64, P_int64, P_double, P_int64, c_int64]),
     'comap_l1_plan_create': (c_int, [c_void_p, ctypes.POINTER(ObsDesc), ctypes.POINTER(c_void_p)]),
     'comap_l1_plan_destroy': (c_int, [c_void_p]),

@@ -110,6 +110,57 @@ extern "C" int comap_medfilt_f64(comap_ctx *ctx, double *x, int64_t n, int32_t w
     return rc;
 }
 
+// ------------------------------------------------------------------ batched median
+// Series s = x[offsets[s] .. offsets[s+1]).  mode 0: medfilt semantics, all
+// outputs; mode 1: the middle third of medfilt on [x[::-1], x, x[::-1]]
+// (Level1Averaging.py:696-700, COMAPData.py:72-81), computed without the pad.
+extern "C" int comap_medfilt_batch_f64(comap_ctx *ctx, const double *x, const int64_t *offsets, int32_t nseries,
+                                       int32_t w, int32_t mode, double *out)
+{
+    if (!ctx || !x || !offsets || !out || nseries < 0 || (mode != 0 && mode != 1)) return -1;
+    if (nseries == 0) return 0;
+    const int64_t total = offsets[nseries];
+    for (int s = 0; s < nseries; ++s) {
+        const int64_t n = offsets[s + 1] - offsets[s];
+        if (n < 0) return comap_fail(ctx, -1, "offsets must be non-decreasing");
+        // mode 1 equals medfilt on the padded array only when no output window
+        // reaches the pad's head/tail replacement: n >= w
+        if (n > 0 && n < w) return comap_fail(ctx, -1, "series shorter than the window");
+    }
+    for (int64_t i = 0; i < total; ++i)
+        if (std::isnan(x[i])) return comap_fail(ctx, -3, "medfilt input contains NaN");
+    char *s = nullptr;
+    int rc = comap_scratch(ctx, 16 * (size_t)total + 64, (void **)&s);
+    if (rc) return rc;
+    double *dsrc = (double *)s;
+    double *ddst = dsrc + total;
+    std::vector<MedJob> jobs(nseries);
+    for (int k = 0; k < nseries; ++k) {
+        const int64_t n = offsets[k + 1] - offsets[k];
+        MedJob &j = jobs[k];
+        j.src = dsrc + offsets[k];
+        j.dst = ddst + offsets[k];
+        j.n = n;
+        j.mode = mode;
+        j.pad_ = 0;
+        j.gate = nullptr;
+        j.out_lo = mode == 0 ? 0 : n;
+        j.out_hi = mode == 0 ? n : 2 * n;
+    }
+    hipStream_t st = ctx->stream;
+    COMAP_CHECK(ctx, hipMemcpyAsync(dsrc, x, 8 * total, hipMemcpyHostToDevice, st));
+    MedPlan mp;
+    rc = comap_median_plan(ctx, &mp, jobs, w);
+    if (!rc) rc = comap_median_run(ctx, &mp);
+    if (!rc) {
+        hipError_t e = hipMemcpyAsync(out, ddst, 8 * total, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) rc = comap_fail(ctx, -2, hipGetErrorString(e));
+    }
+    comap_median_plan_free(&mp);
+    return rc;
+}
+
 // ------------------------------------------------------------------ binValues drop-in
 __global__ void k_bin_keys(const int64_t *__restrict__ pix, const int64_t *__restrict__ mask, int64_t n,
                            int64_t npix, int32_t *__restrict__ keys, int32_t *__restrict__ vals)

@@ -54,6 +54,14 @@ const char *comap_version(void);
  * averages the two middle values.  Requires w <= n, w <= 7681 and a
  * NaN-free x (returns -3 on NaN: the two-heap's NaN order is undefined). */
 int comap_medfilt_f64(comap_ctx *ctx, double *x_host, int64_t n, int32_t w);
+/* Batched sliding median of nseries host series x[offsets[s]..offsets[s+1]).
+ * mode 0: medfilt semantics (as comap_medfilt_f64) for every output;
+ * mode 1: out = medfilt([x[::-1], x, x[::-1]], w)[n:2n], the reflect-padded
+ * high-pass filter of Level1Averaging.median_filter / COMAPData.median_filter
+ * (Level1Averaging.py:696-700, COMAPData.py:72-81), without materialising
+ * the pad (requires n >= w in both modes).  out_host has offsets[nseries] values. */
+int comap_medfilt_batch_f64(comap_ctx *ctx, const double *x_host, const int64_t *offsets_host,
+                            int32_t nseries, int32_t w, int32_t mode, double *out_host);
 /* image[p] += weights[i] (or += 1 when weights == NULL) for 0 <= p < npix
  * and (mask == NULL || mask[i] != 0).  Accumulates into image in place. */
 int comap_bin_values_f64(comap_ctx *ctx, double *image_host, int64_t npix,
