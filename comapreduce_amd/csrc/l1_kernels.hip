@@ -427,6 +427,7 @@ __global__ void __launch_bounds__(256) k_band_mean(const float *__restrict__ tod
     const int nv0 = n - r0;
     auto body = [&](int c) {
         const double w = al[c];
+        if (w == 0.0) return;                       // NaN channel: weight 0 must not read 0 * NaN
         double x[4 * kJ];
         load_groups(base + (int64_t)c * T, nv0, x);
 #pragma unroll
@@ -672,10 +673,10 @@ __global__ void __launch_bounds__(256) k_coef_d(const int32_t *__restrict__ unit
         if (c < 50 || c >= 974 || c == 512 || (c >= 510 && c < 515)) W = 0.0;
         const double nfg = nf[i] / gain0[(int64_t)f * kBC + b * kChannels + c];
         if (isnan(nfg) || fnan) W = 0.0;                       // residual[...,0] NaN
-        const double kr = W * nfg;
+        const double kr = (W == 0.0) ? 0.0 : W * nfg;          // never 0 * NaN
         double Wo = W;
         if (isnan(tsv) || fnan) Wo = 0.0;                      // (clean*Tsys)[...,0] NaN
-        const double ko = Wo * tsv;
+        const double ko = (Wo == 0.0) ? 0.0 : Wo * tsv;
         // ---- kappa (zero weights contribute exactly nothing, as NaN->0 does)
         const double kgfa = (kg == 0.0) ? 0.0 : kg * fa;
         const double krfa = (kr == 0.0) ? 0.0 : kr * fa;
@@ -726,6 +727,9 @@ __global__ void __launch_bounds__(256) k_gain_avg(const float *__restrict__ tod,
 #pragma unroll 2
     for (int c = 0; c < kChannels; ++c) {
         const double wg = kg[c], wr = kr[c], wo = ko[c];
+        // channels excluded from all three averages are not read at all: the
+        // reference zeroes their weights (and NaN data must not leak as 0 * NaN)
+        if (wg == 0.0 && wr == 0.0 && wo == 0.0) continue;
         double x[4 * kJ];
         load_groups(base + (int64_t)c * T, nv0, x);
 #pragma unroll
@@ -1255,6 +1259,10 @@ extern "C" int comap_l1_debug_fetch(comap_l1_plan *p, int32_t what, double *out,
     case 2: src = p->dG; cnt = (int64_t)p->F * p->T; break;
     case 3: src = p->xreg; cnt = 2 * UC; break;
     case 4: src = p->mb; cnt = (int64_t)p->F * kBands * p->T; break;
+    case 5: src = p->kap; cnt = 3 * UC; break;
+    case 6: src = p->dsum; cnt = (int64_t)p->U * kBands * 16; break;
+    case 7: src = p->alpha; cnt = UC; break;
+    case 8: src = p->oa; cnt = 2 * UC; break;
     default: return comap_fail(ctx, -1, "unknown debug array");
     }
     if (n < cnt) return comap_fail(ctx, -1, "debug buffer too small");

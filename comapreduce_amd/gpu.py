@@ -212,10 +212,11 @@ class GPUObservation:
         return int(self.units[:, 3].sum())
 
     def debug(self, what: int):
-        """Internal arrays (host f64): 0 rms [U,4,1024]; 1 mf [F,4,T]; 2 dG [F,T]; 3 x [U,4,1024,2]; 4 mb."""
+        """Internal arrays (host f64): 0 rms [U,4,1024]; 1 mf [F,4,T]; 2 dG [F,T]; 3 x [U,4,1024,2]; 4 mb;
+        5 kappa [3,U,4,1024]; 6 pass-D sums [U,4,16]; 7 alpha [U,4,1024]; 8 atmosphere (o, a) [U,4,1024,2]."""
         U = self.units.shape[0]
         shapes = {0: (U, 4, 1024), 1: (self.F, 4, self.T), 2: (self.F, self.T), 3: (U, 4, 1024, 2),
-                  4: (self.F, 4, self.T)}
+                  4: (self.F, 4, self.T), 5: (3, U, 4, 1024), 6: (U, 4, 16), 7: (U, 4, 1024), 8: (U, 4, 1024, 2)}
         out = np.empty(shapes[what])
         self._bind()
         N.check(N.lib().comap_l1_debug_fetch(self.plan, what, N.hptr(out, ctypes.c_double), out.size), self.ctx,

@@ -75,13 +75,23 @@ class CelestialWCS:
                 cands.append(lp)
             dp = min(cands, key=lambda lp: abs(lp - latpole))
             zz = np.cos(dp * D2R) * np.cos(d0 * D2R)
-            if abs(zz) < 1e-10:
-                ap = a0
+            if abs(zz) < 1e-10:      # native pole on a celestial pole: phi(a0) = phi0 fixes ap
+                ap = a0 + lonpole - phi0 - 180.0 if dp > 0 else a0 - lonpole + phi0
             else:
                 xx = (sthe0 - np.sin(dp * D2R) * np.sin(d0 * D2R)) / zz
                 yy = sphip * cthe0 / np.cos(d0 * D2R)
                 ap = a0 - np.arctan2(yy, xx) * R2D
         self.eul = (ap, 90.0 - dp, lonpole, np.cos((90.0 - dp) * D2R), np.sin((90.0 - dp) * D2R))
+        self.latpole = latpole
+        self.wcs = self          # astropy spelling: w.wcs.ctype / w.wcs.cdelt
+
+    def to_header(self):
+        """FITS WCS keywords (ordered list of (key, value)) for the map writer."""
+        return [('WCSAXES', 2), ('CRPIX1', float(self.crpix[0])), ('CRPIX2', float(self.crpix[1])),
+                ('CDELT1', float(self.cdelt[0])), ('CDELT2', float(self.cdelt[1])),
+                ('CUNIT1', 'deg'), ('CUNIT2', 'deg'), ('CTYPE1', self.ctype[0]), ('CTYPE2', self.ctype[1]),
+                ('CRVAL1', float(self.crval[0])), ('CRVAL2', float(self.crval[1])),
+                ('LONPOLE', float(self.phip)), ('LATPOLE', float(self.latpole))]
 
     def _native(self, lng, lat):
         e0, e1, e2, ce1, se1 = self.eul

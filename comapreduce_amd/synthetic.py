@@ -253,3 +253,70 @@ def destriper_inputs(n_feeds: int = 2, n_samples: int = 20_000, npix_side: int =
     weights = np.full(N, 1.0 / 0.1 ** 2)
     weights[rng.random(N) < 0.02] = 0.0
     return pointing, tod, weights
+
+
+def scan_edges_from_status(status: np.ndarray) -> np.ndarray:
+    """Scan edges with the reference's shared-endpoint convention
+    (RepointEdges.get_scan_positions_source, DataHandling.py:205-228)."""
+    scans = np.where(status == 1)[0]
+    d = np.diff(scans)
+    e = scans[np.concatenate(([0], np.where(d > 1)[0], [scans.size - 1]))]
+    return np.array([e[:-1], e[1:]]).T.astype(np.int64)
+
+
+def level2_mapmaking(obs_id: int, n_feeds: int = 19, n_samples: int = 45_000, sky_seed: int = 3,
+                     bad_feed_bits: dict | None = None, source: str = 'Field00',
+                     calibrator: str = 'TauA'):
+    """Synthetic Level-2 file contents for COMAPData.read_comap_data
+    (reference MapMaking/COMAPData.py:247-427): returns (datasets, attrs, filename).
+
+    averaged_tod/{tod,tod_original} f64 [F, 4, T] (zero outside scans, a run of
+    exact zeros inside one scan to exercise the ``tod == 0`` compaction),
+    spikes/spike_mask bool [F, 4, T], pixel pointing, MJD, feeds, and the
+    ``comap`` attrs source / bad_observation (indexed by feed number) /
+    ``{calibrator}_calibration_factor_band{0..3}``.
+    """
+    rng = np.random.default_rng(np.random.SeedSequence([obs_id, 7919]))
+    sky_rng = np.random.default_rng(sky_seed)
+    kx, ky, ph = sky_rng.uniform(0.5, 3.0, 4), sky_rng.uniform(0.5, 3.0, 4), sky_rng.uniform(0, 6.3, 4)
+    T = n_samples
+    status = scan_status(T)
+    edges = scan_edges_from_status(status)
+    inscan = np.zeros(T, dtype=bool)
+    for s, e in edges:
+        inscan[s:e] = True
+    t = np.arange(T)
+    feeds = np.arange(1, n_feeds + 1, dtype=np.int64)
+    ra = np.empty((n_feeds, T)); dec = np.empty_like(ra); az = np.empty_like(ra); el = np.empty_like(ra)
+    tod = np.zeros((n_feeds, N_BANDS, T)); tod_orig = np.zeros_like(tod)
+    spikes = np.zeros((n_feeds, N_BANDS, T), dtype=bool)
+    for i, f in enumerate(feeds):
+        r, d, a, e = pointing(T, int(f))
+        dr = 0.3 * np.sin(0.7 * obs_id)
+        ra[i], dec[i], az[i], el[i] = r + dr, d + 0.2 * np.cos(1.3 * obs_id), a, e
+        for b in range(N_BANDS):
+            x, y = np.radians(ra[i] - FIELD_RA), np.radians(dec[i] - FIELD_DEC)
+            sig = 0.05 * np.sin(kx[b] * 40 * x + ph[b]) * np.cos(ky[b] * 40 * y)
+            drift = np.cumsum(rng.standard_normal(T)) * 2e-4
+            white = rng.standard_normal(T) * 5e-3
+            v = sig + drift + white + 0.01 * b
+            tod_orig[i, b] = np.where(inscan, v + 0.1 * np.sin(t / 900.0), 0.0)
+            tod[i, b] = np.where(inscan, v, 0.0)
+            sp = rng.choice(T, 5, replace=False)
+            spikes[i, b, sp] = True
+    s0 = edges[0][0] + 3000
+    tod[0, :, s0:s0 + 137] = 0.0                     # masked run inside a scan
+    bad = np.zeros(20, dtype=np.int64)
+    for f, bits in (bad_feed_bits or {}).items():
+        bad[f] = bits
+    attrs = {'comap': {'source': source, 'obsid': obs_id, 'bad_observation': bad}}
+    for b in range(N_BANDS):
+        attrs['comap'][f'{calibrator}_calibration_factor_band{b}'] = rng.uniform(0.8, 1.2, 20)
+    mjd = 59000.0 + obs_id * 0.1 + t / SAMPLE_RATE / 86400.0
+    data = {'averaged_tod/tod': tod, 'averaged_tod/tod_original': tod_orig,
+            'averaged_tod/weights': np.ones_like(tod), 'averaged_tod/scan_edges': edges,
+            'spikes/spike_mask': spikes, 'spectrometer/feeds': feeds, 'spectrometer/MJD': mjd,
+            'spectrometer/pixel_pointing/pixel_ra': ra, 'spectrometer/pixel_pointing/pixel_dec': dec,
+            'spectrometer/pixel_pointing/pixel_az': az, 'spectrometer/pixel_pointing/pixel_el': el}
+    filename = f'comap-{obs_id:07d}-2020-06-01-000000_Level2Cont.hd5'
+    return data, attrs, filename

@@ -240,6 +240,59 @@ def run_spikes():
     np.savez_compressed(os.path.join(HERE, 'golden_spikes.npz'), spike_mask=st.data['spikes/spike_mask'])
 
 
+class _FakeH5:
+    """h5py.File stand-in over an in-memory (datasets, attrs) pair."""
+
+    def __init__(self, entry):
+        self._d, self._a = entry
+
+    def __getitem__(self, k):
+        if k in self._a and k not in self._d:
+            return types.SimpleNamespace(attrs=self._a[k])
+        return CopyOnSlice(np.asarray(self._d[k]))
+
+    def __contains__(self, k):
+        return k in self._d
+
+    def close(self):
+        pass
+
+
+def run_comapdata():
+    """MapMaking/COMAPData.read_comap_data on three synthetic Level-2 files.
+
+    Leaves absent from this image are replaced by the repo's restatements
+    (astropy WCS -> comapreduce_amd.mapmaking.wcs.CelestialWCS; healpy
+    Rotator -> mapmaking.astro.Rotator; astropy get_sun -> astro.sun_radec);
+    everything else (file/feed/scan loops, auto_rms, cuts, 400-sample median
+    via the compiled medianFilter.cpp, flattening, empty-offset cut) is the
+    reference's own code."""
+    import COMAPData
+    from comapreduce_amd.mapmaking import astro
+    from comapreduce_amd.mapmaking.wcs import CelestialWCS
+    sys.path.insert(0, HERE)
+    import comapdata_case as cc
+    store, names = cc.store()
+    COMAPData.h5py = types.SimpleNamespace(File=lambda fn, mode='r': _FakeH5(store[fn]))
+    COMAPData.hp = types.SimpleNamespace(rotator=types.SimpleNamespace(Rotator=astro.Rotator))
+    COMAPData.Time = lambda v, format='mjd': types.SimpleNamespace(mjd=float(v))
+
+    def get_sun(t):
+        ra, dec = astro.sun_radec(t.mjd)
+        return types.SimpleNamespace(ra=types.SimpleNamespace(deg=ra), dec=types.SimpleNamespace(deg=dec))
+    COMAPData.get_sun = get_sun
+    out = {}
+    for name, case in cc.CASES.items():
+        m = case['map']
+        map_info = {'wcs': CelestialWCS(m['crval'], m['cdelt'], m['crpix'], m['ctype']),
+                    'nxpix': m['nxpix'], 'nypix': m['nypix']}
+        res = COMAPData.read_comap_data(np.array(names), map_info, feeds=cc.FEEDS, **case['kw'])
+        for k, v in zip(cc.OUTPUTS, res):
+            out[f'{name}__{k}'] = np.asarray(v)[::cc.STRIDE] if k in cc.STRIDED else np.asarray(v)
+    np.savez_compressed(os.path.join(HERE, 'golden_comapdata.npz'), **out)
+    return {n: {k: synthetic.sha256(np.asarray(v)) for k, v in store[n][0].items()} for n in names}
+
+
 def run_medfilt(out):
     from comancpipeline.Tools.median_filter import medfilt
     for seed, n, w in MEDFILT_CASES:
@@ -292,7 +345,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--skip-l1', action='store_true')
     ap.add_argument('--only-variants', action='store_true')
+    ap.add_argument('--only-comapdata', action='store_true')
     args = ap.parse_args()
+    if args.only_comapdata:
+        build_reference_helpers()
+        install_stubs()
+        mp = os.path.join(HERE, 'golden_meta.json')
+        meta = json.load(open(mp))
+        meta['comapdata_sha256'] = run_comapdata()
+        json.dump(meta, open(mp, 'w'), indent=1, default=str)
+        return
     if args.only_variants:
         os.environ.setdefault('MPLBACKEND', 'agg')
         build_reference_helpers()
