@@ -1,0 +1,114 @@
+"""Map-making driver: mirror of reference comancpipeline/MapMaking/run_destriper.py.
+
+    python run_destriper.py parameters.ini
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 run_destriper.py parameters.ini
+
+One process per GPU (torch.distributed over RCCL, RANK/WORLD_SIZE from the
+environment) replaces mpi4py.  Per band: read_comap_data (host prep + one
+batched device median per rank) -> run_destriper (device CG, per-iteration
+SUM all-reduce of the map numerator) -> rank 0 writes the FITS maps.
+
+Reference behaviours kept: files lacking averaged_tod/tod are dropped; the
+source of the FIRST file decides calibrator mode (offset_length 250,
+threshold 1); files are split in blocks of ``len // size`` per rank, so the
+``len % size`` trailing files are not mapped (run_destriper.py:131-138).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+from . import comapdata as COMAPData
+from .destriper import run_destriper
+from .fits import write_image_hdus
+from ..tools.parser import Parser, sex2deg
+
+CALIBRATORS = COMAPData.CALIBRATORS
+
+
+def _rank_size():
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def write_map(prefix, maps, map_info, output_dir, iband, postfix=''):
+    """run_destriper.write_map (run_destriper.py:19-50)."""
+    os.makedirs(output_dir, exist_ok=True)
+    wcs, nx, ny = map_info['wcs'], map_info['nxpix'], map_info['nypix']
+    cards = wcs.to_header()
+    for k, v in maps.items():
+        images = [(None, np.reshape(v['map'], (ny, nx)))]
+        if 'naive' in v:
+            images.append(('Naive', np.reshape(v['naive'], (ny, nx))))
+        if 'weight' in v:
+            with np.errstate(divide='ignore'):
+                images.append(('Noise', np.reshape(np.sqrt(1. / v['weight']), (ny, nx))))
+        if 'hits' in v:
+            images.append(('Hits', np.reshape(v['hits'], (ny, nx))))
+        fname = '{}/{}_{}_Band{:02d}.fits'.format(output_dir, k, prefix, iband)
+        write_image_hdus(fname, images, cards)
+
+
+def main(filelistname, offset_length=50, feed_weights=None, prefix='fg9', output_dir='maps/fg9/', obsid_cuts=[],
+         feeds=[1, 2, 3, 5, 6, 9, 11, 12, 13, 14, 15, 16, 17, 18, 19], nxpix=480, nypix=480,
+         crval=['05:32:00.3', '+12:30:28.0'], crpix=[240, 240], ctype=['RA---CAR', 'DEC--CAR'],
+         cdelt=[-0.016666, 0.016666], use_gain_filter=True, calibration=True, calibrator='TauA', threshold=1e-6,
+         niter=100, healpix=False, bands=(0, 1, 2, 3), store=None):
+    """run_destriper.main (run_destriper.py:79-189).  ``store`` (tests) maps
+    filename -> (datasets, attrs) instead of reading files."""
+    rank, size = _rank_size()
+    input_filelist = np.loadtxt(filelistname, dtype=str, ndmin=1) if isinstance(filelistname, str) \
+        else np.asarray(filelistname)
+    open_file = COMAPData._opener(store)
+    filelist, source = [], None
+    for i, f in enumerate(input_filelist):
+        h = open_file(f)
+        if i == 0:
+            source = h.attrs('comap')['source'].split(',')[0]
+        if 'averaged_tod/tod' in h:
+            filelist.append(f)
+    filelist = np.array(filelist)
+    if isinstance(crval[0], str):
+        crval = [sex2deg(c, hours=hr) for c, hr in zip(crval, [True, False])]
+    map_info = COMAPData.map_info_from(crval, cdelt, crpix, ctype, nxpix, nypix)
+    step = filelist.size // size
+    lo, hi = step * rank, min(step * (rank + 1), filelist.size)
+    filelist = filelist[lo:hi]
+    if source in CALIBRATORS:
+        offset_length = 250
+        threshold = 1
+    if healpix:
+        raise NotImplementedError('HEALPix maps (write_map_healpix) are not built yet')
+    out = {}
+    for iband in bands:
+        tod, weights, pointing, remap, az, el, ra, dec, feedid, obsids = COMAPData.read_comap_data(
+            filelist, map_info, feed_weights=feed_weights, offset_length=offset_length, iband=iband, feeds=feeds,
+            use_gain_filter=use_gain_filter, calibration=calibration, calibrator=calibrator, healpix=healpix,
+            store=store)
+        pixel_edges = np.arange(nxpix * nypix)
+        maps = run_destriper(pointing, tod, weights, offset_length, pixel_edges, az, el, ra, dec, feedid, obsids,
+                             obsid_cuts, threshold=threshold, niter=niter, chi2_cutoff=20)
+        if rank == 0:
+            write_map(prefix, maps, map_info, output_dir, iband)
+        out[iband] = maps
+    return out
+
+
+def cli(argv):
+    """``__main__`` block of run_destriper.py (:191-212): everything from [Inputs]
+    except use_gain_filter / calibration / calibrator from [ReadData]."""
+    p = Parser(argv[0])
+    params = p['Inputs']
+    feeds = params['feeds']
+    feeds = [int(f) for f in (feeds if isinstance(feeds, list) else [feeds])]
+    as_list = lambda v: v if isinstance(v, list) else [v]  # noqa: E731
+    return main(params['filelistname'], offset_length=int(params['offset_length']), prefix=params['prefix'],
+                output_dir=params['output_dir'], feeds=feeds, feed_weights=params['feed_weights'],
+                nxpix=int(params['nxpix']), nypix=int(params['nypix']), crval=as_list(params['crval']),
+                crpix=as_list(params['crpix']), ctype=as_list(params['ctype']), cdelt=as_list(params['cdelt']),
+                use_gain_filter=p['ReadData']['use_gain_filter'], calibration=p['ReadData']['calibration'],
+                calibrator=p['ReadData']['calibrator'], threshold=10 ** float(params['threshold']),
+                niter=int(params['niter']), healpix=params['healpix'])

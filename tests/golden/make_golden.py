@@ -293,6 +293,16 @@ def run_comapdata():
     return {n: {k: synthetic.sha256(np.asarray(v)) for k, v in store[n][0].items()} for n in names}
 
 
+def run_parser():
+    """Tools/ParserClass.Parser on tests/golden/params_case.ini (our own fixture)."""
+    from comancpipeline.Tools import ParserClass
+    from comancpipeline.Tools import Coordinates
+    p = ParserClass.Parser(os.path.join(HERE, 'params_case.ini'))
+    return {'parsed': p.infodict,
+            'sex2deg': [Coordinates.sex2deg('11:20:00', hours=True), Coordinates.sex2deg('+52:00:00'),
+                        Coordinates.sex2deg('-00:30:36'), Coordinates.sex2deg('05:32:00.3', hours=True)]}
+
+
 def run_medfilt(out):
     from comancpipeline.Tools.median_filter import medfilt
     for seed, n, w in MEDFILT_CASES:
@@ -353,6 +363,7 @@ def main():
         mp = os.path.join(HERE, 'golden_meta.json')
         meta = json.load(open(mp))
         meta['comapdata_sha256'] = run_comapdata()
+        meta['parser_case'] = run_parser()
         json.dump(meta, open(mp, 'w'), indent=1, default=str)
         return
     if args.only_variants:

@@ -1,0 +1,77 @@
+"""run_destriper driver: .ini parsing (pinned to the reference Parser's output
+on tests/golden/params_case.ini), FITS map files, and the end-to-end
+read_comap_data -> destriper -> write_map chain on the GPU."""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, 'golden'))
+
+
+def test_parser_matches_reference(golden_dir):
+    from comapreduce_amd.tools.parser import Parser, sex2deg
+    ref = json.load(open(os.path.join(golden_dir, 'golden_meta.json')))['parser_case']
+    p = Parser(os.path.join(golden_dir, 'params_case.ini'))
+    assert p.infodict == ref['parsed']
+    got = [sex2deg('11:20:00', hours=True), sex2deg('+52:00:00'), sex2deg('-00:30:36'),
+           sex2deg('05:32:00.3', hours=True)]
+    assert got == ref['sex2deg']
+    with pytest.raises(AttributeError):
+        p['Missing']
+
+
+def test_fits_roundtrip(tmp_path):
+    from comapreduce_amd.mapmaking.fits import read_image_hdus
+    from comapreduce_amd.mapmaking.run_destriper import write_map
+    from comapreduce_amd.mapmaking.comapdata import map_info_from
+    mi = map_info_from([170.0, 52.0], [-1 / 60., 1 / 60.], [10, 8], ['RA---CAR', 'DEC--CAR'], 20, 16)
+    rng = np.random.default_rng(0)
+    v = {'map': rng.standard_normal(320), 'naive': rng.standard_normal(320),
+         'weight': rng.uniform(0, 2, 320), 'hits': rng.integers(0, 9, 320).astype(float)}
+    v['weight'][3] = 0.0
+    write_map('case', {'All': v}, mi, str(tmp_path), 2)
+    hdus = read_image_hdus(str(tmp_path / 'All_case_Band02.fits'))
+    assert [h.get('EXTNAME') for h, _ in hdus] == [None, 'Naive', 'Noise', 'Hits']
+    h0, m = hdus[0]
+    assert h0['SIMPLE'] is True and h0['BITPIX'] == -64 and h0['CTYPE1'] == 'RA---CAR'
+    assert h0['CRPIX1'] == 10.0 and h0['CDELT2'] == 1 / 60.
+    assert np.array_equal(m, v['map'].reshape(16, 20))
+    assert np.array_equal(hdus[1][1], v['naive'].reshape(16, 20))
+    with np.errstate(divide='ignore'):
+        assert np.array_equal(hdus[2][1], np.sqrt(1. / v['weight']).reshape(16, 20))
+    assert np.array_equal(hdus[3][1], v['hits'].reshape(16, 20))
+    assert os.path.getsize(tmp_path / 'All_case_Band02.fits') % 2880 == 0
+
+
+@pytest.mark.gpu
+def test_run_destriper_main_end_to_end(tmp_path):
+    """main() on the COMAPData fixture files vs the oracle chain
+    (oracle.comapdata -> oracle.destriper.destriper_iteration)."""
+    import comapdata_case as cc
+    from comapreduce_amd.mapmaking.run_destriper import main
+    from comapreduce_amd.mapmaking.fits import read_image_hdus
+    from oracle import comapdata as oc, destriper as od
+    store, names = cc.store()
+    names = names[:2]                                   # Field00 files (non-calibrator mode)
+    m = cc.CASES['car']['map']
+    out = main(names, offset_length=50, prefix='t', output_dir=str(tmp_path), feeds=cc.FEEDS,
+               nxpix=m['nxpix'], nypix=m['nypix'], crval=m['crval'], crpix=m['crpix'], ctype=m['ctype'],
+               cdelt=m['cdelt'], use_gain_filter=True, calibration=False, threshold=1e-6, niter=50,
+               bands=(0,), store=store)
+    from comapreduce_amd.mapmaking.comapdata import map_info_from
+    mi = map_info_from(m['crval'], m['cdelt'], m['crpix'], m['ctype'], m['nxpix'], m['nypix'])
+    tod, w, pix, *_ = oc.read_comap_data(names, store, mi, iband=0, offset_length=50, feeds=cc.FEEDS)
+    npix = m['nxpix'] * m['nypix']
+    ref, _, _ = od.destriper_iteration(pix, tod, w, 50, npix, threshold=1e-6, niter=50)
+    got = out[0]['All']
+    for k in ('naive', 'weight', 'hits'):
+        assert np.array_equal(np.nan_to_num(got[k]), np.nan_to_num(ref[k])), k
+    fin = np.isfinite(ref['map']) & (ref['weight'] > 0)
+    scale = np.max(np.abs(ref['map'][fin]))
+    assert np.max(np.abs(got['map'][fin] - ref['map'][fin])) <= 1e-6 * scale
+    hdus = read_image_hdus(str(tmp_path / 'All_t_Band00.fits'))
+    assert np.array_equal(np.nan_to_num(hdus[0][1].ravel()), np.nan_to_num(got['map']))
