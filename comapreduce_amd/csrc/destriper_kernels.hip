@@ -163,7 +163,7 @@ __global__ void k_sample_maps(const int32_t *__restrict__ skey, const int32_t *_
             const int32_t i = sval[k];
             const double wi = w[i];
             sh += wi;
-            sn += tod[i] * wi;
+            sn += __dmul_rn(tod[i], wi);   // binValues(weights=z*w): product rounded, never fused
             sc += 1.0;
         }
         h[p] = sh;

@@ -394,10 +394,11 @@ __global__ void __launch_bounds__(256) k_coef_b(const int32_t *__restrict__ unit
 constexpr int kJ = kTile / 256;
 
 // x[4g+e] = d[r0 + 256 g + e] (0 beyond the scan end, nv0 = n - r0)
-__device__ __forceinline__ void load_groups(const float *__restrict__ p, int nv0, double (&x)[4 * kJ])
+template <int J = kJ>
+__device__ __forceinline__ void load_groups(const float *__restrict__ p, int nv0, double (&x)[4 * J])
 {
 #pragma unroll
-    for (int g = 0; g < kJ; ++g) {
+    for (int g = 0; g < J; ++g) {
         const int nv = nv0 - 256 * g;
         if (nv >= 4) {
             const f32x4u v = *reinterpret_cast<const f32x4u *>(p + 256 * g);
@@ -409,6 +410,9 @@ __device__ __forceinline__ void load_groups(const float *__restrict__ p, int nv0
     }
 }
 
+// Pass B on 512-sample half tiles (two blocks per 1024-sample tile: ~7k
+// blocks for C2, enough to keep the tail of the grid short).
+constexpr int kJB = 2;
 __global__ void __launch_bounds__(256) k_band_mean(const float *__restrict__ tod, const double *__restrict__ A,
                                                    const int32_t *__restrict__ units, const int32_t *__restrict__ tiles,
                                                    int64_t T, const double *__restrict__ alpha,
@@ -416,22 +420,23 @@ __global__ void __launch_bounds__(256) k_band_mean(const float *__restrict__ tod
 {
     const int b = uniform(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const int u = tiles[2 * blockIdx.x], toff = tiles[2 * blockIdx.x + 1];
+    const int tile = blockIdx.x >> 1, half = blockIdx.x & 1;
+    const int u = tiles[2 * tile], toff = tiles[2 * tile + 1] + 256 * kJB * half;
     const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
     const int r0 = toff + 4 * lane;                 // first sample (relative) of this lane
     const float *base = tod + (int64_t)(f * kBands + b) * kChannels * T + t0 + r0;
     const double *al = alpha + (int64_t)u * kBC + b * kChannels;
-    double acc[4 * kJ];
+    double acc[4 * kJB];
 #pragma unroll
-    for (int i = 0; i < 4 * kJ; ++i) acc[i] = 0.0;
+    for (int i = 0; i < 4 * kJB; ++i) acc[i] = 0.0;
     const int nv0 = n - r0;
     auto body = [&](int c) {
         const double w = al[c];
         if (w == 0.0) return;                       // NaN channel: weight 0 must not read 0 * NaN
-        double x[4 * kJ];
-        load_groups(base + (int64_t)c * T, nv0, x);
+        double x[4 * kJB];
+        load_groups<kJB>(base + (int64_t)c * T, nv0, x);
 #pragma unroll
-        for (int i = 0; i < 4 * kJ; ++i) acc[i] = fma(w, x[i], acc[i]);
+        for (int i = 0; i < 4 * kJB; ++i) acc[i] = fma(w, x[i], acc[i]);
     };
 #pragma unroll 2
     for (int c = 10; c < 507; ++c) body(c);
@@ -442,7 +447,7 @@ __global__ void __launch_bounds__(256) k_band_mean(const float *__restrict__ tod
     double *out = mb + (int64_t)(f * kBands + b) * T + t0 + r0;
     const double *a = A + (int64_t)f * T + t0 + r0;
 #pragma unroll
-    for (int g = 0; g < kJ; ++g)
+    for (int g = 0; g < kJB; ++g)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int o = 256 * g + e;
@@ -485,8 +490,10 @@ __global__ void __launch_bounds__(256) k_series_sums(const int32_t *__restrict__
 // only sum_t d mf is new (sum d came from pass A).
 __global__ void __launch_bounds__(256) k_regress(const float *__restrict__ tod, const double *__restrict__ mf,
                                                  const int32_t *__restrict__ units, int64_t T,
-                                                 const double *__restrict__ bsum, double *__restrict__ sdm)
+                                                 const double *__restrict__ bsum, double *__restrict__ sdm,
+                                                 const int32_t *__restrict__ flag)
 {
+    if (*flag == 0) return;                         // legacy pass C: only after a fused-path mismatch
     const int wid = uniform(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int groups_per_band = kChannels / (4 * kCPW);
@@ -616,14 +623,17 @@ __global__ void __launch_bounds__(256) k_coef_d(const int32_t *__restrict__ unit
                                                 const double *__restrict__ oa,
                                                 const double *__restrict__ alpha, const double *__restrict__ nf,
                                                 const double *__restrict__ bsum, const double *__restrict__ ss,
-                                                const double *__restrict__ sdm, const double *__restrict__ tsys0,
+                                                double *__restrict__ sdm, const double *__restrict__ tsys0,
                                                 const double *__restrict__ gain0, const double *__restrict__ gw,
                                                 const int32_t *__restrict__ gmode, int calibrator,
                                                 double *__restrict__ kap, double *__restrict__ dsum,
-                                                double *__restrict__ xreg)
+                                                double *__restrict__ xreg, int phase,
+                                                const double *__restrict__ part, const int32_t *__restrict__ utile0,
+                                                int32_t *__restrict__ flag)
 {
     __shared__ double red[4];
     const int ub = blockIdx.x;
+    if (phase == 2 && *flag == 0) return;          // legacy path only runs after a fused-path mismatch
     const int u = ub / kBands, b = ub % kBands;
     const int f = units[4 * u];
     const double *q = us + 8 * (int64_t)u;
@@ -650,12 +660,21 @@ __global__ void __launch_bounds__(256) k_coef_d(const int32_t *__restrict__ unit
         const double tsv = tsys0[(int64_t)f * kBC + b * kChannels + c];
         // ---- filtered TOD coefficients
         double fa = 0, fb = 0, fg = 0, fd = 0, x0 = 0, x1 = 0;
+        double sdmi = 0.0;
+        if (phase == 1) {        // fused pass C+D: sum the per-block partials of this unit
+            for (int k = utile0[u]; k < utile0[u + 1]; ++k) sdmi += part[(int64_t)k * kBC + b * kChannels + c];
+            sdm[i] = sdmi;
+        } else if (phase == 2) {
+            sdmi = sdm[i];
+        }
         if (band_on && median_channel(c)) {
             if (al != 0.0) {
                 const double sy = al * (mom[i] - n * o - a * SA);
-                const double sym = al * (sdm[i] - o * Smf - a * SAm);
-                x0 = (Smm * sy - Smf * sym) / det;
-                x1 = (n * sym - Smf * sy) / det;
+                const double sym = al * (sdmi - o * Smf - a * SAm);
+                if (phase != 0) {    // phase 0: x unknown yet; kappa never depends on x unless x is NaN
+                    x0 = (Smm * sy - Smf * sym) / det;
+                    x1 = (n * sym - Smf * sy) / det;
+                }
                 fa = al; fb = -(al * o + x0); fg = -al * a; fd = -x1;
             } else {                      // NaN channel inside the regression set
                 fa = NAN; fb = NAN; fg = NAN; fd = NAN; x0 = NAN; x1 = NAN;
@@ -681,6 +700,12 @@ __global__ void __launch_bounds__(256) k_coef_d(const int32_t *__restrict__ unit
         const double kgfa = (kg == 0.0) ? 0.0 : kg * fa;
         const double krfa = (kr == 0.0) ? 0.0 : kr * fa;
         const double kofa = (ko == 0.0) ? 0.0 : ko * fa;
+        if (phase == 1) {        // kappa with the regression known must equal the phase-0 kappa
+            if (__double_as_longlong(kap[i]) != __double_as_longlong(kgfa) ||
+                __double_as_longlong(kap[UC + i]) != __double_as_longlong(krfa) ||
+                __double_as_longlong(kap[2 * UC + i]) != __double_as_longlong(kofa))
+                atomicOr(flag, 1);
+        }
         kap[i] = kgfa;
         kap[UC + i] = krfa;
         kap[2 * UC + i] = kofa;
@@ -692,7 +717,7 @@ __global__ void __launch_bounds__(256) k_coef_d(const int32_t *__restrict__ unit
     }
 #pragma unroll
     for (int k = 0; k < 12; ++k) acc[k] = block_sum256(acc[k], red);
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && phase != 0) {
         double *o = dsum + 16 * (int64_t)ub;
 #pragma unroll
         for (int k = 0; k < 12; ++k) o[k] = acc[k];
@@ -709,9 +734,10 @@ __global__ void __launch_bounds__(256) k_gain_avg(const float *__restrict__ tod,
                                                   int64_t T, int64_t UC, const double *__restrict__ kap,
                                                   const double *__restrict__ dsum, const double *__restrict__ mf,
                                                   double *__restrict__ tod_out, double *__restrict__ orig_out,
-                                                  double *__restrict__ dG_out)
+                                                  double *__restrict__ dG_out, const int32_t *__restrict__ flag)
 {
     __shared__ double sg[kBands][kTile];
+    if (*flag == 0) return;                         // legacy pass D: only after a fused-path mismatch
     const int b = uniform(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int u = tiles[2 * blockIdx.x], toff = tiles[2 * blockIdx.x + 1];
@@ -772,6 +798,130 @@ __global__ void __launch_bounds__(256) k_gain_avg(const float *__restrict__ tod,
         }
 }
 
+// ------------------------------------------------------------------ fused pass C+D
+// The pass-D channel weights kappa = (kg, kr, ko) x fa do not depend on the
+// regression (k_coef_d phase 0), so ONE read of the cube serves both:
+//   per channel   part[blk][b][c] = sum_{t in block} d_ct mf_bt       (pass C)
+//   per sample    Sg_t = sum_b sum_c kg_c d_ct,  Sr_bt, So_bt          (pass D)
+// k_coef_d phase 1 then solves the regression and folds the per-band
+// constants; k_finish applies them.  Block = 256 threads (wave b = band) on a
+// 512-sample half of a 1024-sample tile; lane owns 2 groups of 4 samples.
+constexpr int kJ2 = 2;
+__global__ void __launch_bounds__(256) k_regress_avg(const float *__restrict__ tod, const int32_t *__restrict__ units,
+                                                     const int32_t *__restrict__ tiles, int64_t T, int64_t UC,
+                                                     const double *__restrict__ kap, const double *__restrict__ mf,
+                                                     double *__restrict__ part, double *__restrict__ sr_out,
+                                                     double *__restrict__ so_out, double *__restrict__ sg_out)
+{
+    __shared__ double sg[kBands][256 * kJ2];
+    const int b = uniform(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int tile = blockIdx.x >> 1, half = blockIdx.x & 1;
+    const int u = tiles[2 * tile], toff = tiles[2 * tile + 1] + 256 * kJ2 * half;
+    const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
+    const int r0 = toff + 4 * lane;
+    const int nv0 = n - r0;                          // valid samples from this lane's first group
+    const float *base = tod + (int64_t)(f * kBands + b) * kChannels * T + t0 + r0;
+    const int64_t kb = (int64_t)u * kBC + b * kChannels;
+    const double *kg = kap + kb, *kr = kap + UC + kb, *ko = kap + 2 * UC + kb;
+    double *pp = part + (int64_t)blockIdx.x * kBC + b * kChannels;
+    const double *m = mf + (int64_t)(f * kBands + b) * T + t0 + r0;
+    double mt[4 * kJ2];
+#pragma unroll
+    for (int g = 0; g < kJ2; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) mt[4 * g + e] = (256 * g + e < nv0) ? m[256 * g + e] : 0.0;
+    double ag[4 * kJ2], ar[4 * kJ2], ao[4 * kJ2];
+#pragma unroll
+    for (int i = 0; i < 4 * kJ2; ++i) ag[i] = ar[i] = ao[i] = 0.0;
+    for (int c = 0; c < kChannels; ++c) {
+        const double wg = kg[c], wr = kr[c], wo = ko[c];
+        if (wg == 0.0 && wr == 0.0 && wo == 0.0) {   // channel in none of the averages: not read
+            if (lane == 0) pp[c] = 0.0;
+            continue;
+        }
+        const float *q = base + (int64_t)c * T;
+        double x[4 * kJ2];
+#pragma unroll
+        for (int g = 0; g < kJ2; ++g) {
+            const int nv = nv0 - 256 * g;
+            if (nv >= 4) {
+                const f32x4u v = *reinterpret_cast<const f32x4u *>(q + 256 * g);
+                x[4 * g] = v.x; x[4 * g + 1] = v.y; x[4 * g + 2] = v.z; x[4 * g + 3] = v.w;
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) x[4 * g + e] = (e < nv) ? (double)q[256 * g + e] : 0.0;
+            }
+        }
+        double pc = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4 * kJ2; ++i) {
+            ag[i] = fma(wg, x[i], ag[i]);
+            ar[i] = fma(wr, x[i], ar[i]);
+            ao[i] = fma(wo, x[i], ao[i]);
+            pc = fma(x[i], mt[i], pc);
+        }
+        pc = wave_sum(pc);
+        if (lane == 0) pp[c] = pc;
+    }
+#pragma unroll
+    for (int g = 0; g < kJ2; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sg[b][256 * g + 4 * lane + e] = ag[4 * g + e];
+    __syncthreads();
+    const int64_t rowo = (int64_t)(f * kBands + b) * T + t0 + r0;
+#pragma unroll
+    for (int g = 0; g < kJ2; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int i = 4 * g + e, o = 256 * g + e;
+            if (o >= nv0) continue;
+            sr_out[rowo + o] = ar[i];
+            so_out[rowo + o] = ao[i];
+            if (b == 0) {
+                const int tl = 256 * g + 4 * lane + e;
+                sg_out[(int64_t)f * T + t0 + r0 + o] = (sg[0][tl] + sg[1][tl]) + (sg[2][tl] + sg[3][tl]);
+            }
+        }
+}
+
+// Applies the per-band constants of k_coef_d phase 1 to the fused sums:
+//   dG    = Sg + sum_b (Dg0_b + A Dg1_b + mf_b Dg2_b)
+//   tod_b = (Sr_b + Dr0 + A Dr1 + mf Dr2 - dG SKr) / SW
+//   orig_b = (So_b + Do0 + A Do1 + mf Do2) / SWo
+__global__ void __launch_bounds__(256) k_finish(const int32_t *__restrict__ units, const int32_t *__restrict__ tiles,
+                                                int64_t T, const double *__restrict__ A,
+                                                const double *__restrict__ mf, const double *__restrict__ dsum,
+                                                double *__restrict__ tod_out, double *__restrict__ orig_out,
+                                                double *__restrict__ dG, const int32_t *__restrict__ flag)
+{
+    if (*flag != 0) return;                          // mismatch: the legacy passes produce the outputs
+    const int u = tiles[2 * blockIdx.x];
+    const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
+    const double *ds = dsum + 16 * (int64_t)u * kBands;
+    for (int k = threadIdx.x; k < kTile; k += 256) {
+        const int r = tiles[2 * blockIdx.x + 1] + k;
+        if (r >= n) break;
+        const int64_t t = t0 + r;
+        const double a = A[(int64_t)f * T + t];
+        double m[kBands], g = dG[(int64_t)f * T + t];
+#pragma unroll
+        for (int b = 0; b < kBands; ++b) {
+            m[b] = mf[(int64_t)(f * kBands + b) * T + t];
+            const double *d = ds + 16 * b;
+            g += d[0] + a * d[1] + m[b] * d[2];
+        }
+        dG[(int64_t)f * T + t] = g;
+#pragma unroll
+        for (int b = 0; b < kBands; ++b) {
+            const double *d = ds + 16 * b;
+            const int64_t o = (int64_t)(f * kBands + b) * T + t;
+            tod_out[o] = (tod_out[o] + d[3] + a * d[4] + m[b] * d[5] - g * d[9]) / d[10];
+            orig_out[o] = (orig_out[o] + d[6] + a * d[7] + m[b] * d[8]) / d[11];
+        }
+    }
+}
+
 // ------------------------------------------------------------------ scan weights
 // averaged_tod/weights = 1/auto_rms(residual)^2 per (band, scan)
 // (Level1Averaging.py:512-518, 867): nanstd of odd-even differences, ddof 0.
@@ -807,36 +957,44 @@ __global__ void __launch_bounds__(256) k_scan_weights(const int32_t *__restrict_
 // ------------------------------------------------------------------ vane
 // system_temperature_from_tod (VaneCalibration.py:67-82): per channel nanmean
 // over the hot and cold samples of the vane event; one wave per channel row.
+// system_temperature_from_tod (VaneCalibration.py:67-82) with the reference's
+// numerics.  tod[..., hot] is a fancy-index gather, which numpy lays out
+// F-ordered (strides (4, 4 n)), so its float32 nanmean reduces each channel
+// SEQUENTIALLY: s = ((0 + x0) + x1) + ... in float32 with NaN -> 0, then
+// float32(double(s) / count).  gain = double(float32(th - tc)) / (t_hot - 2.73)
+// and tsys = tc / gain in float64 (t_hot is an np.float64).  One thread per
+// channel row; a block's 256 rows read the same columns, so each cache line
+// is fetched once and re-used from L1 for the next 15 columns.
 __global__ void __launch_bounds__(256) k_vane(const float *__restrict__ tod, int64_t T, int F,
                                               int64_t vstart, const int32_t *__restrict__ hot,
                                               const int64_t *__restrict__ hoff, const int32_t *__restrict__ cold,
                                               const int64_t *__restrict__ coff, double t_hot,
                                               double *__restrict__ tsys, double *__restrict__ gain)
 {
-    const int lane = threadIdx.x & 63;
-    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);   // (f*4+b)*1024 + c
+    const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;   // (f*4+b)*1024 + c
     if (row >= (int64_t)F * kBC) return;
-    const int fb = (int)(row / kChannels);
+    const int fb = (int)(row / kChannels);                          // uniform: 1024 % 256 == 0
     const float *p = tod + row * T + vstart;
     const int64_t h0 = hoff[fb], h1 = hoff[fb + 1], k0 = coff[fb], k1 = coff[fb + 1];
     if (h1 == h0) return;   // no hot/cold found (RuntimeError path): leave zeros
-    // an empty cold list (all cold samples before the last hot one) gives NaN, as nanmean([]) does
-    double sh = 0, nh = 0, sc = 0, nc = 0;
-    for (int64_t j = h0 + lane; j < h1; j += 64) {
-        const float x = p[hot[j]];
-        if (!isnan(x)) { sh += x; nh += 1.0; }
+    float mean[2];
+    for (int side = 0; side < 2; ++side) {
+        const int32_t *idx = side == 0 ? hot : cold;
+        const int64_t j0 = side == 0 ? h0 : k0, j1 = side == 0 ? h1 : k1;
+        float s = 0.f;
+        int64_t cnt = 0;
+        for (int64_t j = j0; j < j1; ++j) {
+            const float x = p[idx[j]];
+            const bool ok = !isnan(x);
+            s += ok ? x : 0.f;
+            cnt += ok;
+        }
+        mean[side] = (float)((double)s / (double)cnt);   // empty list: nanmean([]) -> NaN
     }
-    for (int64_t j = k0 + lane; j < k1; j += 64) {
-        const float x = p[cold[j]];
-        if (!isnan(x)) { sc += x; nc += 1.0; }
-    }
-    sh = wave_sum(sh); nh = wave_sum(nh); sc = wave_sum(sc); nc = wave_sum(nc);
-    if (lane == 0) {
-        const double th = sh / nh, tc = sc / nc;
-        const double g = (th - tc) / (t_hot - 2.73);
-        gain[row] = g;
-        tsys[row] = tc / g;
-    }
+    const float d = mean[0] - mean[1];
+    const double g = (double)d / (t_hot - 2.73);
+    gain[row] = g;
+    tsys[row] = (double)mean[1] / g;
 }
 
 // ================================================================== host side
@@ -935,8 +1093,15 @@ extern "C" int comap_l1_plan_create(comap_ctx *ctx, const comap_obs_desc *d, com
     for (int u = 0; u < p->U; ++u)
         for (int t = 0; t < p->units_h[4 * u + 3]; t += kTile) { tiles.push_back(u); tiles.push_back(t); }
     p->n_tiles = (int64_t)tiles.size() / 2;
+    // fused pass C+D blocks (two per tile) of unit u: [utile0[u], utile0[u+1])
+    std::vector<int32_t> utile0(p->U + 1, 0);
+    for (int64_t k = 0; k < p->n_tiles; ++k) utile0[tiles[2 * k] + 1] += 2;
+    for (int u = 0; u < p->U; ++u) utile0[u + 1] += utile0[u];
     const int64_t UC = (int64_t)p->U * kBC;
     int rc = 0;
+    rc |= upload(ctx, (void **)&p->utile0, utile0.data(), utile0.size() * 4);
+    rc |= dalloc(ctx, &p->part, 2 * (size_t)p->n_tiles * kBC);
+    rc |= dalloc(ctx, &p->flag, 1);
     rc |= upload(ctx, (void **)&p->units, p->units_h.data(), p->units_h.size() * 4);
     rc |= upload(ctx, (void **)&p->tiles, tiles.data(), tiles.size() * 4);
     rc |= dalloc(ctx, &p->airmass, (size_t)p->F * p->T);
@@ -995,7 +1160,8 @@ extern "C" int comap_l1_plan_destroy(comap_l1_plan *p)
     if (!p) return 0;
     void *bufs[] = {p->units, p->tiles, p->airmass, p->unit_sums, p->mom,
                     p->nan_count, p->alpha, p->nf, p->bsum, p->mb, p->mf, p->ssum, p->sdm, p->gw,
-                    p->gmode, p->kap, p->dsum, p->xreg, p->dG, p->rowbad, p->ubs, p->fitsum, p->oa};
+                    p->gmode, p->kap, p->dsum, p->xreg, p->dG, p->rowbad, p->ubs, p->fitsum, p->oa,
+                    p->utile0, p->part, p->flag};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     comap_median_plan_free(&p->med);
@@ -1180,24 +1346,43 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
     PROF(p, KV_COEF_B, k_coef_b<<<UB, 256, 0, st>>>(p->units, p->unit_sums, p->mom, UC, p->oa, p->alpha, p->nf,
                                                     p->bsum));
     COMAP_LAUNCH_CHECK(ctx);
-    PROF(p, KV_BAND_MEAN, k_band_mean<<<p->n_tiles, 256, 0, st>>>(p->tod, p->airmass, p->units, p->tiles, p->T,
+    PROF(p, KV_BAND_MEAN, k_band_mean<<<2 * p->n_tiles, 256, 0, st>>>(p->tod, p->airmass, p->units, p->tiles, p->T,
                                                                   p->alpha, p->bsum, p->mb));
     COMAP_LAUNCH_CHECK(ctx);
     PROF(p, KV_MEDIAN, rc = comap_median_run(ctx, &p->med));
     if (rc) return rc;
     PROF(p, KV_SERIES_SUMS, k_series_sums<<<UB, 256, 0, st>>>(p->units, p->airmass, p->T, p->bsum, p->mf, p->ssum));
     COMAP_LAUNCH_CHECK(ctx);
-    const int64_t grid = (int64_t)p->U * kBands * (kChannels / (4 * kCPW));
-    PROF(p, KV_REGRESS, k_regress<<<grid, 256, 0, st>>>(p->tod, p->mf, p->units, p->T, p->bsum, p->sdm));
-    COMAP_LAUNCH_CHECK(ctx);
     PROF(p, KV_GAIN_WEIGHTS, k_gain_weights<<<p->F, 1024, 0, st>>>(tsys0, p->gw, p->gmode));
     COMAP_LAUNCH_CHECK(ctx);
-    PROF(p, KV_COEF_D, k_coef_d<<<UB, 256, 0, st>>>(p->units, p->unit_sums, p->mom, UC, p->oa, p->alpha, p->nf,
-                                                    p->bsum, p->ssum, p->sdm, tsys0, gain0, p->gw, p->gmode,
-                                                    calibrator, p->kap, p->dsum, p->xreg));
+    COMAP_CHECK(ctx, hipMemsetAsync(p->flag, 0, 4, st));
+    auto coef_d = [&](int phase) {
+        k_coef_d<<<UB, 256, 0, st>>>(p->units, p->unit_sums, p->mom, UC, p->oa, p->alpha, p->nf, p->bsum, p->ssum,
+                                     p->sdm, tsys0, gain0, p->gw, p->gmode, calibrator, p->kap, p->dsum, p->xreg,
+                                     phase, p->part, p->utile0, p->flag);
+    };
+    // fused pass C+D: kappa first, one read of the cube, then the regression and the constants
+    PROF(p, KV_COEF_D, coef_d(0));
+    COMAP_LAUNCH_CHECK(ctx);
+    PROF(p, KV_REGRESS_AVG, k_regress_avg<<<2 * p->n_tiles, 256, 0, st>>>(p->tod, p->units, p->tiles, p->T, UC,
+                                                                          p->kap, p->mf, p->part, tod_out, orig_out,
+                                                                          p->dG));
+    COMAP_LAUNCH_CHECK(ctx);
+    PROF(p, KV_COEF_D, coef_d(1));
+    COMAP_LAUNCH_CHECK(ctx);
+    // legacy separate passes C and D: exit at once unless phase 1 found a kappa that depends on the
+    // regression (a NaN regression coefficient), in which case they recompute the outputs exactly
+    const int64_t grid = (int64_t)p->U * kBands * (kChannels / (4 * kCPW));
+    PROF(p, KV_REGRESS, k_regress<<<grid, 256, 0, st>>>(p->tod, p->mf, p->units, p->T, p->bsum, p->sdm, p->flag));
+    COMAP_LAUNCH_CHECK(ctx);
+    PROF(p, KV_COEF_D, coef_d(2));
     COMAP_LAUNCH_CHECK(ctx);
     PROF(p, KV_GAIN_AVG, k_gain_avg<<<p->n_tiles, 256, 0, st>>>(p->tod, p->airmass, p->units, p->tiles, p->T, UC,
-                                                                p->kap, p->dsum, p->mf, tod_out, orig_out, p->dG));
+                                                                p->kap, p->dsum, p->mf, tod_out, orig_out, p->dG,
+                                                                p->flag));
+    COMAP_LAUNCH_CHECK(ctx);
+    PROF(p, KV_FINISH, k_finish<<<p->n_tiles, 256, 0, st>>>(p->units, p->tiles, p->T, p->airmass, p->mf, p->dsum,
+                                                            tod_out, orig_out, p->dG, p->flag));
     COMAP_LAUNCH_CHECK(ctx);
     PROF(p, KV_SCAN_WEIGHTS, k_scan_weights<<<UB, 256, 0, st>>>(p->units, p->T, tod_out, w_out));
     COMAP_LAUNCH_CHECK(ctx);
@@ -1238,7 +1423,7 @@ extern "C" int comap_l1_vane(comap_l1_plan *p, int64_t vstart, int64_t vlen, con
     COMAP_CHECK(ctx, hipMemsetAsync(tsys, 0, (size_t)FB * kChannels * 8, st));
     COMAP_CHECK(ctx, hipMemsetAsync(gain, 0, (size_t)FB * kChannels * 8, st));
     const int64_t rows = (int64_t)FB * kChannels;
-    PROF(p, KV_VANE, k_vane<<<(rows + 3) / 4, 256, 0, st>>>(p->tod, p->T, p->F, vstart, dh, dho, dc, dco, t_hot,
+    PROF(p, KV_VANE, k_vane<<<(rows + 255) / 256, 256, 0, st>>>(p->tod, p->T, p->F, vstart, dh, dho, dc, dco, t_hot,
                                                             tsys, gain));
     COMAP_LAUNCH_CHECK(ctx);
     // the host arrays may be freed by the caller after return

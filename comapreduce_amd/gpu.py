@@ -191,8 +191,10 @@ class GPUObservation:
         return out[0], out[1], out[2]
 
     KERNELS = ('vane', 'moments', 'atmos_fit', 'coef_b', 'band_mean', 'median', 'series_sums', 'regress',
-               'gain_weights', 'coef_d', 'gain_avg', 'scan_weights')
-    STREAMING = ('moments', 'band_mean', 'regress', 'gain_avg')   # the four HBM passes (A, B, C, D)
+               'gain_weights', 'coef_d', 'gain_avg', 'scan_weights', 'regress_avg', 'finish')
+    # the HBM streaming passes: A, B and the fused C+D (regress / gain_avg are the
+    # legacy separate C and D passes, launched but idle unless a NaN regression needs them)
+    STREAMING = ('moments', 'band_mean', 'regress_avg')
 
     def profile(self, enable: bool = True):
         """Record HIP events around every kernel launch of this plan."""
@@ -206,6 +208,12 @@ class GPUObservation:
                                                  N.hptr(cnt, ctypes.c_int64), 32), self.ctx,
                 'comap_l1_profile_collect')
         return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(self.KERNELS)}
+
+    def active_channel_fraction(self) -> float:
+        """Fraction of (unit, band, channel) rows the fused pass C+D reads (nonzero kappa):
+        channels excluded from every average are skipped (k_regress_avg)."""
+        kap = self.debug(5)
+        return float(np.mean(np.any(kap != 0.0, axis=0)))
 
     def scan_samples(self) -> int:
         """Sum over units of the scan lengths (samples each streaming pass visits per channel)."""

@@ -29,7 +29,7 @@ def test_run_destriper_matches_reference(golden):
     maps = run_destriper(p, t, w, L, np.arange(NPIX), threshold=1e-6, niter=100)['All']
     assert np.array_equal(maps['weight'], golden['destriper_weight'])
     assert np.array_equal(maps['hits'], golden['destriper_hits'])
-    assert rel(maps['naive'], golden['destriper_naive']) < 1e-12
+    assert np.array_equal(maps['naive'], golden['destriper_naive'])
     assert rel(maps['map'], golden['destriper_map']) < 1e-5
     res = DeviceDestriper(p, t, w, L, NPIX).solve(1e-6, 100)
     assert rel(res['x'].cpu().numpy(), golden['destriper_offsets']) < 1e-5

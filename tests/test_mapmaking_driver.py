@@ -68,8 +68,11 @@ def test_run_destriper_main_end_to_end(tmp_path):
     npix = m['nxpix'] * m['nypix']
     ref, _, _ = od.destriper_iteration(pix, tod, w, 50, npix, threshold=1e-6, niter=50)
     got = out[0]['All']
-    for k in ('naive', 'weight', 'hits'):
-        assert np.array_equal(np.nan_to_num(got[k]), np.nan_to_num(ref[k])), k
+    for k in ('weight', 'hits', 'naive'):
+        a, b = np.nan_to_num(got[k]), np.nan_to_num(ref[k])
+        bad = np.nonzero(a != b)[0]
+        assert bad.size == 0, (k, bad.size, bad[:5].tolist(), a[bad[:5]].tolist(), b[bad[:5]].tolist(),
+                               ref['weight'][bad[:5]].tolist())
     fin = np.isfinite(ref['map']) & (ref['weight'] > 0)
     scale = np.max(np.abs(ref['map'][fin]))
     assert np.max(np.abs(got['map'][fin] - ref['map'][fin])) <= 1e-6 * scale
