@@ -156,6 +156,7 @@ __global__ void k_sample_maps(const int32_t *__restrict__ skey, const int32_t *_
                               int64_t npix, const double *__restrict__ w, const double *__restrict__ tod,
                               double *__restrict__ h, double *__restrict__ hits, double *__restrict__ nnum)
 {
+#pragma clang fp contract(off)   // binValues(weights=z*w): the product is rounded before the add
     for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x) {
         const int64_t lo = lb32(skey, N, p), hi = lb32(skey, N, p + 1);
         double sh = 0.0, sc = 0.0, sn = 0.0;
@@ -163,7 +164,7 @@ __global__ void k_sample_maps(const int32_t *__restrict__ skey, const int32_t *_
             const int32_t i = sval[k];
             const double wi = w[i];
             sh += wi;
-            sn += __dmul_rn(tod[i], wi);   // binValues(weights=z*w): product rounded, never fused
+            sn += tod[i] * wi;
             sc += 1.0;
         }
         h[p] = sh;

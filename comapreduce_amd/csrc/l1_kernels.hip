@@ -807,6 +807,32 @@ __global__ void __launch_bounds__(256) k_gain_avg(const float *__restrict__ tod,
 // constants; k_finish applies them.  Block = 256 threads (wave b = band) on a
 // 512-sample half of a 1024-sample tile; lane owns 2 groups of 4 samples.
 constexpr int kJ2 = 2;
+
+// Sum 8 per-lane values over the 64 lanes of a wave; on return lane l holds
+// the total of value (l >> 3).  Butterfly transpose: 4 + 2 + 1 exchanges halve
+// the values carried, then 3 plain xor steps finish (10 shuffles, not 8 x 6).
+__device__ __forceinline__ double wave_reduce8(const double (&v)[8], int lane)
+{
+    const int b5 = (lane >> 5) & 1, b4 = (lane >> 4) & 1, b3 = (lane >> 3) & 1;
+    double a[4], c[2];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const double keep = b5 ? v[t + 4] : v[t];
+        const double send = b5 ? v[t] : v[t + 4];
+        a[t] = keep + __shfl_xor(send, 32, 64);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const double keep = b4 ? a[t + 2] : a[t];
+        const double send = b4 ? a[t] : a[t + 2];
+        c[t] = keep + __shfl_xor(send, 16, 64);
+    }
+    double r = (b3 ? c[1] : c[0]) + __shfl_xor(b3 ? c[0] : c[1], 8, 64);
+    r += __shfl_xor(r, 4, 64);
+    r += __shfl_xor(r, 2, 64);
+    r += __shfl_xor(r, 1, 64);
+    return r;
+}
 __global__ void __launch_bounds__(256) k_regress_avg(const float *__restrict__ tod, const int32_t *__restrict__ units,
                                                      const int32_t *__restrict__ tiles, int64_t T, int64_t UC,
                                                      const double *__restrict__ kap, const double *__restrict__ mf,
@@ -834,12 +860,14 @@ __global__ void __launch_bounds__(256) k_regress_avg(const float *__restrict__ t
     double ag[4 * kJ2], ar[4 * kJ2], ao[4 * kJ2];
 #pragma unroll
     for (int i = 0; i < 4 * kJ2; ++i) ag[i] = ar[i] = ao[i] = 0.0;
-    for (int c = 0; c < kChannels; ++c) {
+    for (int c8 = 0; c8 < kChannels; c8 += 8) {
+      double pcs[8];
+#pragma unroll
+      for (int cc = 0; cc < 8; ++cc) {
+        const int c = c8 + cc;
+        pcs[cc] = 0.0;
         const double wg = kg[c], wr = kr[c], wo = ko[c];
-        if (wg == 0.0 && wr == 0.0 && wo == 0.0) {   // channel in none of the averages: not read
-            if (lane == 0) pp[c] = 0.0;
-            continue;
-        }
+        if (wg == 0.0 && wr == 0.0 && wo == 0.0) continue;   // channel in none of the averages: not read
         const float *q = base + (int64_t)c * T;
         double x[4 * kJ2];
 #pragma unroll
@@ -861,8 +889,10 @@ __global__ void __launch_bounds__(256) k_regress_avg(const float *__restrict__ t
             ao[i] = fma(wo, x[i], ao[i]);
             pc = fma(x[i], mt[i], pc);
         }
-        pc = wave_sum(pc);
-        if (lane == 0) pp[c] = pc;
+        pcs[cc] = pc;
+      }
+      const double tot = wave_reduce8(pcs, lane);
+      if ((lane & 7) == 0) pp[c8 + (lane >> 3)] = tot;
     }
 #pragma unroll
     for (int g = 0; g < kJ2; ++g)

@@ -26,7 +26,7 @@
 
 namespace {
 
-constexpr int kWalkThreads = 512;
+constexpr int kWalkThreads = 256;   // = outputs per chunk (lc)
 
 __device__ __forceinline__ uint64_t key_of(double v)
 {
@@ -80,12 +80,13 @@ __global__ void __launch_bounds__(kWalkThreads) k_med_walk(const MedJob *__restr
                                                            const uint64_t *__restrict__ skeys,
                                                            const int32_t *__restrict__ svals, int32_t w, int32_t lc)
 {
+    // LDS: E (zone list, 16-B aligned for 4-entry reads) | U (sorted-series index of each union entry) | scans
     extern __shared__ __align__(16) unsigned char smem[];
-    uint64_t *keys = reinterpret_cast<uint64_t *>(smem);
-    uint16_t *pos = reinterpret_cast<uint16_t *>(smem + sizeof(uint64_t) * P);
-    uint32_t *E = reinterpret_cast<uint32_t *>(smem + (sizeof(uint64_t) + sizeof(uint16_t)) * P);
-    int *scan = reinterpret_cast<int *>(E + 2 * lc + 8);
-    __shared__ int s_tot;
+    uint32_t *E = reinterpret_cast<uint32_t *>(smem);
+    int32_t *U = reinterpret_cast<int32_t *>(smem + 4 * (2 * kWalkThreads + 16));
+    int *scanU = reinterpret_cast<int *>(U + P);
+    int *scanE = scanU + kWalkThreads;
+    __shared__ int s_ne;
 
     const int tid = threadIdx.x;
     const int jb = (int)chunks[2 * blockIdx.x];
@@ -97,104 +98,100 @@ __global__ void __launch_bounds__(kWalkThreads) k_med_walk(const MedJob *__restr
     const int c0 = (int)(i0 - job.out_lo);          // chunk offset inside the series' position space
     const int32_t s0 = seg[jb], ns = seg[jb + 1] - s0;
 
-    // ---- a. extract U in sorted order: entries of the sorted series with position in [c0, c0+M)
+    // ---- a. one compaction builds both U (union window, sorted order) and E (its zone
+    //         entries: offsets < L-1 or >= w, i.e. excluded by some output's window)
     const int per = (ns + kWalkThreads - 1) / kWalkThreads;
     const int b0 = tid * per, b1 = min(ns, b0 + per);
-    int cnt = 0;
-    for (int s = b0; s < b1; ++s) {
-        const int p = svals[s0 + s] - c0;
-        cnt += (p >= 0) & (p < M);
+    int cu = 0, ce = 0;
+    for (int q = b0; q < b1; ++q) {
+        const int p = svals[s0 + q] - c0;
+        const bool in = (p >= 0) & (p < M);
+        cu += in;
+        ce += in & ((p < L - 1) | (p >= w));
     }
-    scan[tid] = cnt;
+    scanU[tid] = cu;
+    scanE[tid] = ce;
     __syncthreads();
     for (int off = 1; off < kWalkThreads; off <<= 1) {
-        const int v = (tid >= off) ? scan[tid - off] : 0;
+        const int vu = (tid >= off) ? scanU[tid - off] : 0;
+        const int ve = (tid >= off) ? scanE[tid - off] : 0;
         __syncthreads();
-        scan[tid] += v;
+        scanU[tid] += vu;
+        scanE[tid] += ve;
         __syncthreads();
     }
-    int wr = scan[tid] - cnt;
-    for (int s = b0; s < b1; ++s) {
-        const int p = svals[s0 + s] - c0;
+    int wu = scanU[tid] - cu, we = scanE[tid] - ce;
+    if (tid == kWalkThreads - 1) s_ne = scanE[tid];
+    for (int q = b0; q < b1; ++q) {
+        const int p = svals[s0 + q] - c0;
         if ((p >= 0) & (p < M)) {
-            keys[wr] = skeys[s0 + s];
-            pos[wr] = (uint16_t)p;
-            ++wr;
+            if ((p < L - 1) | (p >= w)) E[we++] = ((uint32_t)wu << 16) | (uint32_t)p;
+            U[wu++] = q;
         }
     }
     __syncthreads();
-
-    // ---- b. zone entries (head [0, L-1), tail [w, M)) in rank order
-    const int per2 = (M + kWalkThreads - 1) / kWalkThreads;
-    const int e0 = tid * per2, e1 = min(M, e0 + per2);
-    int zc = 0;
-    for (int s = e0; s < e1; ++s) {
-        const int p = pos[s];
-        zc += (p < L - 1) | (p >= w);
-    }
-    __syncthreads();
-    scan[tid] = zc;
-    __syncthreads();
-    for (int off = 1; off < kWalkThreads; off <<= 1) {
-        const int v = (tid >= off) ? scan[tid - off] : 0;
-        __syncthreads();
-        scan[tid] += v;
-        __syncthreads();
-    }
-    int ew = scan[tid] - zc;
-    if (tid == kWalkThreads - 1) s_tot = scan[tid];
-    for (int s = e0; s < e1; ++s) {
-        const int p = pos[s];
-        if ((p < L - 1) | (p >= w)) E[ew++] = ((uint32_t)s << 16) | (uint32_t)p;
-    }
-    __syncthreads();
-    const int ne = s_tot;
-    if (tid < 8) E[ne + tid] = 0xffffffffu;   // sentinel rank 0xffff > any q
+    const int ne = s_ne;
+    if (tid < 16) E[ne + tid] = 0xffffffffu;   // sentinels: rank 0xffff > any q
     __syncthreads();
 
-    // ---- c. walk (E reads are wave-uniform: j advances in lockstep)
+    // ---- b. walk: from q = r, every excluded zone entry with rank <= q pushes q up by one.
+    //         E is read 4 entries per LDS access (wave-uniform addresses).
     if (tid < L) {
         const int k = tid;
         const int r_lo = (w % 2 == 0) ? (w / 2 - 1) : (w / 2);
         int q = r_lo;
         int j = 0;
+        int jstop = 0;
         for (;;) {
-            const uint32_t e = E[j];
-            if ((int)(e >> 16) > q) break;
-            const int pp = (int)(e & 0xffff);
-            q += (pp < k) | (pp >= k + w);
-            ++j;
+            const uint4 v = *reinterpret_cast<const uint4 *>(E + j);
+            const uint32_t es[4] = {v.x, v.y, v.z, v.w};
+            bool stop = false;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                if (!stop) {
+                    const uint32_t e = es[t];
+                    if ((int)(e >> 16) > q) {
+                        stop = true;
+                        jstop = j + t;
+                    } else {
+                        const int pp = (int)(e & 0xffff);
+                        q += (pp < k) | (pp >= k + w);
+                    }
+                }
+            }
+            if (stop) break;
+            j += 4;
         }
         const int q1 = q;
         double out;
+        const double v1 = val_of(skeys[s0 + U[q1]]);
         if (w % 2 == 0) {
             q = q1 + 1;
-            for (;;) {
+            for (j = jstop;; ++j) {
                 const uint32_t e = E[j];
                 if ((int)(e >> 16) > q) break;
                 const int pp = (int)(e & 0xffff);
                 q += (pp < k) | (pp >= k + w);
-                ++j;
             }
-            out = (val_of(keys[q]) + val_of(keys[q1])) / 2.0;
+            out = (val_of(skeys[s0 + U[q]]) + v1) / 2.0;
         } else {
-            out = val_of(keys[q1]);
+            out = v1;
         }
         job.dst[i0 + k - job.out_lo] = out;
     }
 }
 
 template <int P>
-size_t walk_smem(int lc) { return (sizeof(uint64_t) + sizeof(uint16_t)) * P + 4 * (2 * lc + 8) + 4 * kWalkThreads + 64; }
+size_t walk_smem(int) { return 4 * (2 * kWalkThreads + 16) + 4 * (size_t)P + 8 * kWalkThreads + 64; }
 
 }  // namespace
 
 void comap_median_geometry(int32_t w, int32_t *lc, int32_t *P)
 {
     int p = 1024;
-    while (p < w + 511) p <<= 1;
+    while (p < w + kWalkThreads - 1) p <<= 1;
     *P = p;
-    *lc = 512;
+    *lc = kWalkThreads;
 }
 
 // ------------------------------------------------------------------ plan
@@ -202,7 +199,7 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
 {
     mp->w = w;
     comap_median_geometry(w, &mp->lc, &mp->P);
-    if (mp->P > 8192) return comap_fail(ctx, -1, "median window too large (w <= 7681)");
+    if (mp->P > 16384) return comap_fail(ctx, -1, "median window too large (w <= 16129)");
     std::vector<int32_t> seg(jobs.size() + 1, 0);
     std::vector<int64_t> chunks;
     for (size_t j = 0; j < jobs.size(); ++j) {
@@ -274,6 +271,7 @@ int comap_median_run(comap_ctx *ctx, MedPlan *mp)
         CASE(2048)
         CASE(4096)
         CASE(8192)
+        CASE(16384)
 #undef CASE
     default:
         return comap_fail(ctx, -1, "median window too large");

@@ -53,7 +53,8 @@ def test_medfilt_dropin_bit_exact(meta, golden_dir):
 def test_medfilt_dropin_ties_and_edges():
     from comapreduce_amd.tools.medfilt import medfilt
     rng = np.random.default_rng(9)
-    for n, w in [(6000, 6000), (12000, 6000), (7681, 7681), (513, 400), (2048, 2), (100, 1), (3000, 5)]:
+    for n, w in [(6000, 6000), (12000, 6000), (7681, 7681), (513, 400), (2048, 2), (100, 1), (3000, 5),
+                 (20000, 9001), (16129, 16129), (700, 256), (1000, 255)]:
         x = np.round(rng.standard_normal(n), 1)   # heavy ties
         assert np.array_equal(medfilt(x.copy(), w), oracle.medfilt(x.copy(), w)), (n, w)
 
