@@ -60,7 +60,7 @@ struct MedJob {
 
 // Sliding-median plan: jobs, per-job sorted-key segments, chunk table, buffers.
 struct MedPlan {
-    int32_t w = 0, lc = 0, P = 0, njobs = 0;
+    int32_t w = 0, lc = 0, nwmax = 0, njobs = 0;
     int32_t nitems = 0;
     int64_t nchunks = 0;
     MedJob *jobs = nullptr;      // dev [njobs]
@@ -68,11 +68,11 @@ struct MedPlan {
     int64_t *chunks = nullptr;   // dev [nchunks][2] (job, i0)
     uint64_t *k0 = nullptr, *k1 = nullptr;
     int32_t *v0 = nullptr, *v1 = nullptr;
+    int32_t *rank = nullptr;     // dev [nitems] position -> sorted index
     void *temp = nullptr;
     size_t temp_bytes = 0;
 };
 
-void comap_median_geometry(int32_t w, int32_t *lc, int32_t *P);
 int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jobs, int32_t w);
 void comap_median_plan_free(MedPlan *mp);
 int comap_median_run(comap_ctx *ctx, MedPlan *mp);

@@ -8,16 +8,20 @@
 //
 // 1. k_med_keys: every series (job) contributes the Ns = n_out + w - 1 values
 //    its windows touch, as order-preserving u64 keys + positions.
-// 2. hipcub segmented radix sort: each series sorted ONCE (stable).
-// 3. k_med_walk, one workgroup per chunk of Lc consecutive outputs:
-//    a. the chunk's union U = positions [c, c+w+L-1) is extracted from the
-//       sorted series in sorted order (stream compaction) into LDS;
-//    b. output k's window excludes exactly the offsets < k (head zone) and
-//       >= k+w (tail zone); the 2(L-1) zone entries are compacted in rank
-//       order (list E);
-//    c. lane k walks E (wave-uniform LDS reads): from q = r, every excluded
-//       zone entry with rank <= q pushes q up by one -> q = rank in U of the
-//       r-th smallest window element.
+// 2. hipcub segmented radix sort: each series sorted ONCE (stable);
+//    k_med_rank inverts the permutation (rank of every position).
+// 3. k_med_walk, one workgroup per chunk of L = 256 consecutive outputs:
+//    a. the chunk's union window U = positions [c, c+w+L-1) is marked in an
+//       LDS bitmap indexed by rank (coalesced reads of rank[]), together with
+//       its "zone" Z (offsets < L-1 or >= w: excluded by some output's window);
+//       word popcount prefixes turn a rank into its index within U;
+//    b. the zone entries, in rank order, form the list E = (U index, offset);
+//    c. lane k walks E (4 entries per wave-uniform LDS read): from q = r, every
+//       excluded zone entry with U index <= q pushes q up by one -> q = index in
+//       U of the r-th smallest element of k's window; a binary search over the
+//       word prefixes maps q back to a rank, hence to the value.
+// Series longer than kMaxOut outputs are split into independent sub-jobs so
+// the per-chunk bitmaps stay within LDS.
 #include "comap_internal.h"
 
 #include <hipcub/hipcub.hpp>
@@ -73,19 +77,32 @@ __global__ void __launch_bounds__(256) k_med_keys(const MedJob *__restrict__ job
     }
 }
 
-template <int P>
+__global__ void __launch_bounds__(256) k_med_rank(const int32_t *__restrict__ seg, int32_t njobs,
+                                                  const int32_t *__restrict__ svals, int32_t *__restrict__ rank)
+{
+    const int jb = blockIdx.y;
+    if (jb >= njobs) return;
+    const int32_t s0 = seg[jb], ns = seg[jb + 1] - s0;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += gridDim.x * blockDim.x)
+        rank[s0 + svals[s0 + i]] = i;
+}
+
 __global__ void __launch_bounds__(kWalkThreads) k_med_walk(const MedJob *__restrict__ jobs,
                                                            const int64_t *__restrict__ chunks,
                                                            const int32_t *__restrict__ seg,
                                                            const uint64_t *__restrict__ skeys,
-                                                           const int32_t *__restrict__ svals, int32_t w, int32_t lc)
+                                                           const int32_t *__restrict__ svals,
+                                                           const int32_t *__restrict__ rank, int32_t w,
+                                                           int32_t lc, int32_t nwmax)
 {
-    // LDS: E (zone list, 16-B aligned for 4-entry reads) | U (sorted-series index of each union entry) | scans
+    // LDS: E (16-B aligned for 4-entry reads) | U bitmap | Z bitmap | U word prefixes | scans
     extern __shared__ __align__(16) unsigned char smem[];
     uint32_t *E = reinterpret_cast<uint32_t *>(smem);
-    int32_t *U = reinterpret_cast<int32_t *>(smem + 4 * (2 * kWalkThreads + 16));
-    int *scanU = reinterpret_cast<int *>(U + P);
-    int *scanE = scanU + kWalkThreads;
+    uint32_t *Ub = E + (2 * kWalkThreads + 16);
+    uint32_t *Zb = Ub + nwmax;
+    int32_t *Up = reinterpret_cast<int32_t *>(Zb + nwmax);
+    int *scanU = Up + nwmax;
+    int *scanZ = scanU + kWalkThreads;
     __shared__ int s_ne;
 
     const int tid = threadIdx.x;
@@ -97,45 +114,57 @@ __global__ void __launch_bounds__(kWalkThreads) k_med_walk(const MedJob *__restr
     const int M = w + L - 1;
     const int c0 = (int)(i0 - job.out_lo);          // chunk offset inside the series' position space
     const int32_t s0 = seg[jb], ns = seg[jb + 1] - s0;
+    const int nw = (ns + 31) >> 5;
 
-    // ---- a. one compaction builds both U (union window, sorted order) and E (its zone
-    //         entries: offsets < L-1 or >= w, i.e. excluded by some output's window)
-    const int per = (ns + kWalkThreads - 1) / kWalkThreads;
-    const int b0 = tid * per, b1 = min(ns, b0 + per);
-    int cu = 0, ce = 0;
-    for (int q = b0; q < b1; ++q) {
-        const int p = svals[s0 + q] - c0;
-        const bool in = (p >= 0) & (p < M);
-        cu += in;
-        ce += in & ((p < L - 1) | (p >= w));
+    // ---- a. bitmaps of the union window and its zone, indexed by rank
+    for (int i = tid; i < nw; i += kWalkThreads) { Ub[i] = 0u; Zb[i] = 0u; }
+    __syncthreads();
+    for (int i = tid; i < M; i += kWalkThreads) {
+        const int r = rank[s0 + c0 + i];
+        const uint32_t bit = 1u << (r & 31);
+        atomicOr(&Ub[r >> 5], bit);
+        if ((i < L - 1) | (i >= w)) atomicOr(&Zb[r >> 5], bit);
     }
+    __syncthreads();
+    // per-thread contiguous word ranges; prefix sums of set bits
+    const int wpt = (nw + kWalkThreads - 1) / kWalkThreads;
+    const int wb = min(nw, tid * wpt), we = min(nw, wb + wpt);
+    int cu = 0, cz = 0;
+    for (int k = wb; k < we; ++k) { cu += __popc(Ub[k]); cz += __popc(Zb[k]); }
     scanU[tid] = cu;
-    scanE[tid] = ce;
+    scanZ[tid] = cz;
     __syncthreads();
     for (int off = 1; off < kWalkThreads; off <<= 1) {
         const int vu = (tid >= off) ? scanU[tid - off] : 0;
-        const int ve = (tid >= off) ? scanE[tid - off] : 0;
+        const int vz = (tid >= off) ? scanZ[tid - off] : 0;
         __syncthreads();
         scanU[tid] += vu;
-        scanE[tid] += ve;
+        scanZ[tid] += vz;
         __syncthreads();
     }
-    int wu = scanU[tid] - cu, we = scanE[tid] - ce;
-    if (tid == kWalkThreads - 1) s_ne = scanE[tid];
-    for (int q = b0; q < b1; ++q) {
-        const int p = svals[s0 + q] - c0;
-        if ((p >= 0) & (p < M)) {
-            if ((p < L - 1) | (p >= w)) E[we++] = ((uint32_t)wu << 16) | (uint32_t)p;
-            U[wu++] = q;
+    // ---- b. word prefixes and the zone list E in rank order
+    int u = scanU[tid] - cu, z = scanZ[tid] - cz;
+    if (tid == kWalkThreads - 1) s_ne = scanZ[tid];
+    for (int k = wb; k < we; ++k) {
+        const uint32_t ub = Ub[k];
+        Up[k] = u;
+        uint32_t zb = Zb[k];
+        while (zb) {
+            const int b = __builtin_ctz(zb);
+            const int r = 32 * k + b;
+            const int ui = u + __popc(ub & ((1u << b) - 1u));
+            const int p = svals[s0 + r] - c0;
+            E[z++] = ((uint32_t)ui << 16) | (uint32_t)p;
+            zb &= zb - 1u;
         }
+        u += __popc(ub);
     }
     __syncthreads();
     const int ne = s_ne;
-    if (tid < 16) E[ne + tid] = 0xffffffffu;   // sentinels: rank 0xffff > any q
+    if (tid < 16) E[ne + tid] = 0xffffffffu;   // sentinels: index 0xffff > any q
     __syncthreads();
 
-    // ---- b. walk: from q = r, every excluded zone entry with rank <= q pushes q up by one.
-    //         E is read 4 entries per LDS access (wave-uniform addresses).
+    // ---- c. walk
     if (tid < L) {
         const int k = tid;
         const int r_lo = (w % 2 == 0) ? (w / 2 - 1) : (w / 2);
@@ -162,9 +191,20 @@ __global__ void __launch_bounds__(kWalkThreads) k_med_walk(const MedJob *__restr
             if (stop) break;
             j += 4;
         }
+        // U index -> rank: the last word whose prefix is <= q holds it
+        auto select = [&](int qi) -> int {
+            int lo = 0, hi = nw - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (Up[mid] <= qi) lo = mid; else hi = mid - 1;
+            }
+            uint32_t bits = Ub[lo];
+            for (int t = qi - Up[lo]; t > 0; --t) bits &= bits - 1u;
+            return 32 * lo + __builtin_ctz(bits);
+        };
         const int q1 = q;
+        const double v1 = val_of(skeys[s0 + select(q1)]);
         double out;
-        const double v1 = val_of(skeys[s0 + U[q1]]);
         if (w % 2 == 0) {
             q = q1 + 1;
             for (j = jstop;; ++j) {
@@ -173,7 +213,7 @@ __global__ void __launch_bounds__(kWalkThreads) k_med_walk(const MedJob *__restr
                 const int pp = (int)(e & 0xffff);
                 q += (pp < k) | (pp >= k + w);
             }
-            out = (val_of(skeys[s0 + U[q]]) + v1) / 2.0;
+            out = (val_of(skeys[s0 + select(q)]) + v1) / 2.0;
         } else {
             out = v1;
         }
@@ -181,37 +221,47 @@ __global__ void __launch_bounds__(kWalkThreads) k_med_walk(const MedJob *__restr
     }
 }
 
-template <int P>
-size_t walk_smem(int) { return 4 * (2 * kWalkThreads + 16) + 4 * (size_t)P + 8 * kWalkThreads + 64; }
+size_t walk_smem(int nwmax) { return 4 * (2 * kWalkThreads + 16) + 12 * (size_t)nwmax + 8 * kWalkThreads + 64; }
 
 }  // namespace
 
-void comap_median_geometry(int32_t w, int32_t *lc, int32_t *P)
-{
-    int p = 1024;
-    while (p < w + kWalkThreads - 1) p <<= 1;
-    *P = p;
-    *lc = kWalkThreads;
-}
-
 // ------------------------------------------------------------------ plan
-int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jobs, int32_t w)
+// Jobs with more than kMaxOut outputs are split into sub-jobs (each its own
+// sorted segment), so a segment never exceeds kMaxOut + w - 1 values.
+constexpr int64_t kMaxOut = 65536;
+constexpr int32_t kMaxWindow = 32768;   // keeps U indices and offsets within 16 bits
+
+int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jobs_in, int32_t w)
 {
     mp->w = w;
-    comap_median_geometry(w, &mp->lc, &mp->P);
-    if (mp->P > 16384) return comap_fail(ctx, -1, "median window too large (w <= 16129)");
+    mp->lc = kWalkThreads;
+    if (w < 1 || w > kMaxWindow) return comap_fail(ctx, -1, "median window must be 1 <= w <= 32768");
+    std::vector<MedJob> jobs;
+    for (const MedJob &j : jobs_in) {
+        if (j.out_hi - j.out_lo <= kMaxOut) { jobs.push_back(j); continue; }
+        for (int64_t lo = j.out_lo; lo < j.out_hi; lo += kMaxOut) {
+            MedJob sj = j;
+            sj.out_lo = lo;
+            sj.out_hi = std::min(j.out_hi, lo + kMaxOut);
+            sj.dst = j.dst + (lo - j.out_lo);      // dst is indexed from out_lo
+            jobs.push_back(sj);
+        }
+    }
     std::vector<int32_t> seg(jobs.size() + 1, 0);
     std::vector<int64_t> chunks;
+    int64_t nsmax = 0;
     for (size_t j = 0; j < jobs.size(); ++j) {
         const int64_t nout = jobs[j].out_hi - jobs[j].out_lo;
         const int64_t ns = nout > 0 ? nout + w - 1 : 0;
         if ((int64_t)seg[j] + ns >= (1ll << 31)) return comap_fail(ctx, -1, "median plan too large");
         seg[j + 1] = seg[j] + (int32_t)ns;
+        nsmax = std::max(nsmax, ns);
         for (int64_t i0 = jobs[j].out_lo; i0 < jobs[j].out_hi; i0 += mp->lc) {
             chunks.push_back((int64_t)j);
             chunks.push_back(i0);
         }
     }
+    mp->nwmax = (int32_t)((nsmax + 31) / 32);
     mp->njobs = (int32_t)jobs.size();
     mp->nitems = seg.back();
     mp->nchunks = (int64_t)chunks.size() / 2;
@@ -224,6 +274,7 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
     COMAP_CHECK(ctx, alloc((void **)&mp->k1, 8 * (size_t)mp->nitems));
     COMAP_CHECK(ctx, alloc((void **)&mp->v0, 4 * (size_t)mp->nitems));
     COMAP_CHECK(ctx, alloc((void **)&mp->v1, 4 * (size_t)mp->nitems));
+    COMAP_CHECK(ctx, alloc((void **)&mp->rank, 4 * (size_t)mp->nitems));
     COMAP_CHECK(ctx, hipMemcpyAsync(mp->jobs, jobs.data(), sizeof(MedJob) * jobs.size(), hipMemcpyHostToDevice, st));
     COMAP_CHECK(ctx, hipMemcpyAsync(mp->seg, seg.data(), 4 * seg.size(), hipMemcpyHostToDevice, st));
     if (!chunks.empty())
@@ -234,13 +285,17 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
                                                                  0, 64, st));
     mp->temp_bytes = tb;
     COMAP_CHECK(ctx, alloc(&mp->temp, tb));
+    const size_t sm = walk_smem(mp->nwmax);
+    if (sm > 160 * 1024) return comap_fail(ctx, -1, "median plan: LDS budget exceeded");
+    COMAP_CHECK(ctx, hipFuncSetAttribute((const void *)k_med_walk, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)sm));
     COMAP_CHECK(ctx, hipStreamSynchronize(st));   // host vectors go out of scope
     return 0;
 }
 
 void comap_median_plan_free(MedPlan *mp)
 {
-    void *b[] = {mp->jobs, mp->seg, mp->chunks, mp->k0, mp->k1, mp->v0, mp->v1, mp->temp};
+    void *b[] = {mp->jobs, mp->seg, mp->chunks, mp->k0, mp->k1, mp->v0, mp->v1, mp->rank, mp->temp};
     for (void *p : b)
         if (p) (void)hipFree(p);
     *mp = MedPlan();
@@ -257,25 +312,11 @@ int comap_median_run(comap_ctx *ctx, MedPlan *mp)
     COMAP_CHECK(ctx, hipcub::DeviceSegmentedRadixSort::SortPairs(mp->temp, tb, mp->k0, mp->k1, mp->v0, mp->v1,
                                                                  (int)mp->nitems, mp->njobs, mp->seg, mp->seg + 1,
                                                                  0, 64, st));
-    switch (mp->P) {
-#define CASE(PP)                                                                                         \
-    case PP: {                                                                                           \
-        const size_t sm = walk_smem<PP>(mp->lc);                                                          \
-        COMAP_CHECK(ctx, hipFuncSetAttribute((const void *)k_med_walk<PP>,                               \
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));      \
-        k_med_walk<PP><<<mp->nchunks, kWalkThreads, sm, st>>>(mp->jobs, mp->chunks, mp->seg, mp->k1,     \
-                                                              mp->v1, mp->w, mp->lc);                    \
-        break;                                                                                           \
-    }
-        CASE(1024)
-        CASE(2048)
-        CASE(4096)
-        CASE(8192)
-        CASE(16384)
-#undef CASE
-    default:
-        return comap_fail(ctx, -1, "median window too large");
-    }
+    k_med_rank<<<g1, 256, 0, st>>>(mp->seg, mp->njobs, mp->v1, mp->rank);
+    COMAP_LAUNCH_CHECK(ctx);
+    k_med_walk<<<mp->nchunks, kWalkThreads, walk_smem(mp->nwmax), st>>>(mp->jobs, mp->chunks, mp->seg, mp->k1,
+                                                                         mp->v1, mp->rank, mp->w, mp->lc,
+                                                                         mp->nwmax);
     COMAP_LAUNCH_CHECK(ctx);
     return 0;
 }

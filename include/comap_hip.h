@@ -51,7 +51,7 @@ const char *comap_version(void);
 /* ------------------------------------------------------------ drop-ins (host arrays) */
 /* In place, identical to medfilt.medfilt(x, w): out[i] = median of
  * x'[i-w/2 .. i-w/2+w-1] with x'[j<w/2] = x[0], x'[j>=n] = x[n-1]; even w
- * averages the two middle values.  Requires w <= n, w <= 16129 and a
+ * averages the two middle values.  Requires w <= n, w <= 32768 and a
  * NaN-free x (returns -3 on NaN: the two-heap's NaN order is undefined). */
 int comap_medfilt_f64(comap_ctx *ctx, double *x_host, int64_t n, int32_t w);
 /* Batched sliding median of nseries host series x[offsets[s]..offsets[s+1]).

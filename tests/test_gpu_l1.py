@@ -59,6 +59,18 @@ def test_medfilt_dropin_ties_and_edges():
         assert np.array_equal(medfilt(x.copy(), w), oracle.medfilt(x.copy(), w)), (n, w)
 
 
+def test_medfilt_long_series_split():
+    """Series longer than one median sub-job (65536 outputs) are split internally."""
+    from comapreduce_amd.tools.medfilt import medfilt, medfilt_batch
+    rng = np.random.default_rng(10)
+    x = np.round(rng.standard_normal(150_001), 2)
+    assert np.array_equal(medfilt(x.copy(), 401), oracle.medfilt(x.copy(), 401))
+    y = np.round(rng.standard_normal(140_000), 2)
+    got = medfilt_batch([y], 400, reflect=True)[0]
+    z = np.concatenate((y[::-1], y, y[::-1]))
+    assert np.array_equal(got, oracle.medfilt(z, 400)[y.size:2 * y.size])
+
+
 def test_binvalues_dropin_bit_exact(golden_dir):
     from comapreduce_amd.tools.binfuncs import binValues
     b = np.load(os.path.join(golden_dir, 'golden_binvalues.npz'))
