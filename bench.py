@@ -79,16 +79,20 @@ def build_observation(F, T, obs_id, device):
     return data
 
 
-def reduce_step(data, device):
-    """One full L1 -> L2 reduction (outputs stay on the device)."""
+def reduce_step(data, device, timing=None):
+    """One full L1 -> L2 reduction (outputs stay on the device).  ``timing``
+    (a dict) collects host wall time per stage call (enqueue + host work)."""
     from comapreduce_amd import Analysis as A
     from comapreduce_amd.pipeline.datahandling import COMAPLevel2
     level2 = COMAPLevel2(filename='/nonexistent/level2.hd5')
     for cls in (A.MeasureSystemTemperature, A.AtmosphereRemoval, A.Level1AveragingGainCorrection):
+        t0 = time.perf_counter()
         st = cls(level2=level2, device=device, device_outputs=True)
         if not st(data, level2):
             raise RuntimeError(f'{cls.__name__} stopped the file')
         level2.update(st)
+        if timing is not None:
+            timing[cls.__name__] = timing.get(cls.__name__, 0.0) + (time.perf_counter() - t0) * 1e3
     return level2
 
 
@@ -174,8 +178,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    host_ms = {}
     for _ in range(args.steps):
-        level2 = reduce_step(data, device)
+        level2 = reduce_step(data, device, host_ms)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
@@ -243,6 +248,8 @@ def main():
                                  'survey_4pass_equiv_frac':
                                      SURVEY_BYTES_PER_SAMPCH * scan_sc / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
             'kernel_ms_per_step': {k: v[0] / args.steps for k, v in prof.items()},
+            'host_stage_ms_per_step': {k: v / args.steps for k, v in host_ms.items()},
+            'host_vane_search_ms': getattr(obs, 'last_vane_search_ms', None),
             'pass_GBs': {k: pass_bytes[k] / (stream[k][0] / max(stream[k][1], 1) * 1e-3) / 1e9
                          for k in obs.STREAMING if stream[k][1] > 0},
         }

@@ -43,6 +43,7 @@ _SIGS = {
     'comap_l1_plan_destroy': (c_int, [c_void_p]),
     'comap_l1_vane': (c_int, [c_void_p, c_int64, c_int64, P_int32, P_int64, P_int32, P_int64, c_double,
                               c_void_p, c_void_p]),
+    'comap_l1_prefetch': (c_int, [c_void_p]),
     'comap_l1_atmosphere': (c_int, [c_void_p, P_int32, c_int32, c_void_p]),
     'comap_l1_average': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
     'comap_l1_debug_fetch': (c_int, [c_void_p, c_int32, P_double, c_int64]),

@@ -96,6 +96,10 @@ struct comap_l1_plan {
     double *mom = nullptr;             // [5][U*4096]: Sd, SAd, Su, Suu, Suv
     int32_t *nan_count = nullptr;      // [1]
     bool moments_valid = false;
+    bool moments_pending = false;      // pass A enqueued, NaN count not read back yet
+    bool prefetched = false;           // comap_l1_prefetch launched pass A for the next atmosphere call
+    int32_t *nan_host = nullptr;       // pinned [1]
+    hipEvent_t mom_event = nullptr;
     double *alpha = nullptr;           // [U*4096] 1/rms on median channels (0 off-set, NaN bad)
     double *nf = nullptr;              // [U*4096] rms (normalisation factor)
     double *bsum = nullptr;            // [U*4][4]: beta, gamma, N, skip

@@ -410,9 +410,10 @@ __device__ __forceinline__ void load_groups(const float *__restrict__ p, int nv0
     }
 }
 
-// Pass B on 512-sample half tiles (two blocks per 1024-sample tile: ~7k
-// blocks for C2, enough to keep the tail of the grid short).
+// Pass B on 256·kJB-sample sub-tiles (kTile/(256 kJB) blocks per 1024-sample
+// tile: ~14k blocks for C2, so the last round of the grid is a small fraction).
 constexpr int kJB = 2;
+constexpr int kSubB = kTile / (256 * kJB);
 __global__ void __launch_bounds__(256) k_band_mean(const float *__restrict__ tod, const double *__restrict__ A,
                                                    const int32_t *__restrict__ units, const int32_t *__restrict__ tiles,
                                                    int64_t T, const double *__restrict__ alpha,
@@ -420,8 +421,8 @@ __global__ void __launch_bounds__(256) k_band_mean(const float *__restrict__ tod
 {
     const int b = uniform(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const int tile = blockIdx.x >> 1, half = blockIdx.x & 1;
-    const int u = tiles[2 * tile], toff = tiles[2 * tile + 1] + 256 * kJB * half;
+    const int tile = blockIdx.x / kSubB, sub = blockIdx.x % kSubB;
+    const int u = tiles[2 * tile], toff = tiles[2 * tile + 1] + 256 * kJB * sub;
     const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
     const int r0 = toff + 4 * lane;                 // first sample (relative) of this lane
     const float *base = tod + (int64_t)(f * kBands + b) * kChannels * T + t0 + r0;
@@ -805,8 +806,9 @@ __global__ void __launch_bounds__(256) k_gain_avg(const float *__restrict__ tod,
 //   per sample    Sg_t = sum_b sum_c kg_c d_ct,  Sr_bt, So_bt          (pass D)
 // k_coef_d phase 1 then solves the regression and folds the per-band
 // constants; k_finish applies them.  Block = 256 threads (wave b = band) on a
-// 512-sample half of a 1024-sample tile; lane owns 2 groups of 4 samples.
+// 256·kJ2-sample sub-tile of a 1024-sample tile; lane owns kJ2 groups of 4 samples.
 constexpr int kJ2 = 2;
+constexpr int kSub2 = kTile / (256 * kJ2);   // fused blocks per 1024-sample tile
 
 // Sum 8 per-lane values over the 64 lanes of a wave; on return lane l holds
 // the total of value (l >> 3).  Butterfly transpose: 4 + 2 + 1 exchanges halve
@@ -842,8 +844,8 @@ __global__ void __launch_bounds__(256) k_regress_avg(const float *__restrict__ t
     __shared__ double sg[kBands][256 * kJ2];
     const int b = uniform(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const int tile = blockIdx.x >> 1, half = blockIdx.x & 1;
-    const int u = tiles[2 * tile], toff = tiles[2 * tile + 1] + 256 * kJ2 * half;
+    const int tile = blockIdx.x / kSub2, sub = blockIdx.x % kSub2;
+    const int u = tiles[2 * tile], toff = tiles[2 * tile + 1] + 256 * kJ2 * sub;
     const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
     const int r0 = toff + 4 * lane;
     const int nv0 = n - r0;                          // valid samples from this lane's first group
@@ -1125,13 +1127,15 @@ extern "C" int comap_l1_plan_create(comap_ctx *ctx, const comap_obs_desc *d, com
     p->n_tiles = (int64_t)tiles.size() / 2;
     // fused pass C+D blocks (two per tile) of unit u: [utile0[u], utile0[u+1])
     std::vector<int32_t> utile0(p->U + 1, 0);
-    for (int64_t k = 0; k < p->n_tiles; ++k) utile0[tiles[2 * k] + 1] += 2;
+    for (int64_t k = 0; k < p->n_tiles; ++k) utile0[tiles[2 * k] + 1] += kSub2;
     for (int u = 0; u < p->U; ++u) utile0[u + 1] += utile0[u];
     const int64_t UC = (int64_t)p->U * kBC;
     int rc = 0;
     rc |= upload(ctx, (void **)&p->utile0, utile0.data(), utile0.size() * 4);
-    rc |= dalloc(ctx, &p->part, 2 * (size_t)p->n_tiles * kBC);
+    rc |= dalloc(ctx, &p->part, (size_t)kSub2 * p->n_tiles * kBC);
     rc |= dalloc(ctx, &p->flag, 1);
+    if (hipHostMalloc((void **)&p->nan_host, 4, hipHostMallocDefault) != hipSuccess) rc |= 1;
+    if (hipEventCreateWithFlags(&p->mom_event, hipEventDisableTiming) != hipSuccess) rc |= 1;
     rc |= upload(ctx, (void **)&p->units, p->units_h.data(), p->units_h.size() * 4);
     rc |= upload(ctx, (void **)&p->tiles, tiles.data(), tiles.size() * 4);
     rc |= dalloc(ctx, &p->airmass, (size_t)p->F * p->T);
@@ -1195,12 +1199,17 @@ extern "C" int comap_l1_plan_destroy(comap_l1_plan *p)
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     comap_median_plan_free(&p->med);
+    if (p->nan_host) (void)hipHostFree(p->nan_host);
+    if (p->mom_event) (void)hipEventDestroy(p->mom_event);
     for (hipEvent_t e : p->prof_pool) (void)hipEventDestroy(e);
     delete p;
     return 0;
 }
 
-static int run_moments(comap_l1_plan *p)
+// Pass A is enqueued without waiting: the 4-byte NaN count comes back through
+// pinned memory behind an event, so host work (the vane sample search) can
+// overlap the 56 GB read.  wait_moments() makes nan_total valid.
+static int launch_moments(comap_l1_plan *p)
 {
     comap_ctx *ctx = p->ctx;
     const int64_t UC = (int64_t)p->U * kBC;
@@ -1209,11 +1218,34 @@ static int run_moments(comap_l1_plan *p)
     PROF(p, KV_MOMENTS, k_moments<<<grid, 256, 0, ctx->stream>>>(p->tod, p->airmass, p->units, p->T, p->mom, UC,
                                                                  p->nan_count, p->rowbad));
     COMAP_LAUNCH_CHECK(ctx);
-    // one 4-byte read-back per pass A decides whether the NaN path runs
-    COMAP_CHECK(ctx, hipMemcpyAsync(&p->nan_total, p->nan_count, 4, hipMemcpyDeviceToHost, ctx->stream));
-    COMAP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    COMAP_CHECK(ctx, hipMemcpyAsync(p->nan_host, p->nan_count, 4, hipMemcpyDeviceToHost, ctx->stream));
+    COMAP_CHECK(ctx, hipEventRecord(p->mom_event, ctx->stream));
+    p->moments_pending = true;
     p->moments_valid = true;
     return 0;
+}
+
+static int wait_moments(comap_l1_plan *p)
+{
+    if (!p->moments_pending) return 0;
+    COMAP_CHECK(p->ctx, hipEventSynchronize(p->mom_event));
+    p->nan_total = *p->nan_host;
+    p->moments_pending = false;
+    return 0;
+}
+
+static int run_moments(comap_l1_plan *p)
+{
+    int rc = launch_moments(p);
+    return rc ? rc : wait_moments(p);
+}
+
+extern "C" int comap_l1_prefetch(comap_l1_plan *p)
+{
+    if (!p) return -1;
+    int rc = launch_moments(p);
+    if (!rc) p->prefetched = true;
+    return rc;
 }
 
 static int fetch_rowbad(comap_l1_plan *p, std::vector<int32_t> &rb)
@@ -1245,7 +1277,8 @@ extern "C" int comap_l1_atmosphere(comap_l1_plan *p, const int32_t *const_el_uni
     if (!p || !fit) return -1;
     comap_ctx *ctx = p->ctx;
     hipStream_t st = ctx->stream;
-    int rc = run_moments(p);
+    int rc = p->prefetched ? wait_moments(p) : run_moments(p);   // pass A, unless comap_l1_prefetch ran it
+    p->prefetched = false;
     if (rc) return rc;
     const int64_t UC = (int64_t)p->U * kBC;
     const int UB = p->U * kBands;
@@ -1359,6 +1392,7 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
     comap_ctx *ctx = p->ctx;
     int rc = 0;
     if (!p->moments_valid && (rc = run_moments(p))) return rc;
+    if ((rc = wait_moments(p))) return rc;
     if (p->nan_total > 0 && !p->filled && (rc = fill_nan_rows(p))) return rc;
     const int64_t UC = (int64_t)p->U * kBC;
     const int UB = p->U * kBands;
@@ -1376,7 +1410,7 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
     PROF(p, KV_COEF_B, k_coef_b<<<UB, 256, 0, st>>>(p->units, p->unit_sums, p->mom, UC, p->oa, p->alpha, p->nf,
                                                     p->bsum));
     COMAP_LAUNCH_CHECK(ctx);
-    PROF(p, KV_BAND_MEAN, k_band_mean<<<2 * p->n_tiles, 256, 0, st>>>(p->tod, p->airmass, p->units, p->tiles, p->T,
+    PROF(p, KV_BAND_MEAN, k_band_mean<<<kSubB * p->n_tiles, 256, 0, st>>>(p->tod, p->airmass, p->units, p->tiles, p->T,
                                                                   p->alpha, p->bsum, p->mb));
     COMAP_LAUNCH_CHECK(ctx);
     PROF(p, KV_MEDIAN, rc = comap_median_run(ctx, &p->med));
@@ -1394,7 +1428,7 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
     // fused pass C+D: kappa first, one read of the cube, then the regression and the constants
     PROF(p, KV_COEF_D, coef_d(0));
     COMAP_LAUNCH_CHECK(ctx);
-    PROF(p, KV_REGRESS_AVG, k_regress_avg<<<2 * p->n_tiles, 256, 0, st>>>(p->tod, p->units, p->tiles, p->T, UC,
+    PROF(p, KV_REGRESS_AVG, k_regress_avg<<<kSub2 * p->n_tiles, 256, 0, st>>>(p->tod, p->units, p->tiles, p->T, UC,
                                                                           p->kap, p->mf, p->part, tod_out, orig_out,
                                                                           p->dG));
     COMAP_LAUNCH_CHECK(ctx);

@@ -14,6 +14,7 @@ CPU fallback (missing library or GPU -> exception).
 from __future__ import annotations
 
 import ctypes
+import time
 
 import numpy as np
 
@@ -139,6 +140,9 @@ class GPUObservation:
         tsys = torch.zeros((nV, self.F, N_BANDS, N_CHANNELS), dtype=torch.float64, device=self.tdev)
         gain = torch.zeros_like(tsys)
         self._bind()
+        # pass A does not depend on the vane: start it now so the host search below overlaps it
+        N.check(N.lib().comap_l1_prefetch(self.plan), self.ctx, 'comap_l1_prefetch')
+        t_search = time.perf_counter()
         for iv, (s, e) in enumerate(ev):
             ba = to_host(band_average[:, :, s:e])
             hot_l, cold_l = [], []
@@ -156,6 +160,7 @@ class GPUObservation:
             cold = np.ascontiguousarray(np.concatenate(cold_l).astype(np.int32))
             hoff = np.asarray(hoff, dtype=np.int64)
             coff = np.asarray(coff, dtype=np.int64)
+            self.last_vane_search_ms = (time.perf_counter() - t_search) * 1e3
             N.check(N.lib().comap_l1_vane(self.plan, int(s), int(e - s), N.hptr(hot, ctypes.c_int32),
                                           N.hptr(hoff, ctypes.c_int64), N.hptr(cold, ctypes.c_int32),
                                           N.hptr(coff, ctypes.c_int64), float(t_hot),

@@ -97,6 +97,9 @@ int comap_l1_vane(comap_l1_plan *plan, int64_t vane_start, int64_t vane_len,
                   const int32_t *cold_idx_host, const int64_t *cold_off_host,
                   double t_hot, double *tsys_dev, double *gain_dev);
 
+/* Enqueue pass A (the per-channel moments AtmosphereRemoval needs) without
+ * waiting, so host work can overlap it; the next comap_l1_atmosphere uses it. */
+int comap_l1_prefetch(comap_l1_plan *plan);
 /* AtmosphereRemoval: writes fit_values dev f64 [S][F][4][2][1024]
  * (offset, slope per channel; NaN outside the fitted channel set, or when
  * fewer than 100 samples are finite in all fitted channels -- select_time).
