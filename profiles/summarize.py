@@ -5,25 +5,26 @@ kernel stats  : average duration per kernel (rocprofv3 --stats)
 traffic       : per-kernel HBM bytes per launch = (2 x FETCH_SIZE + WRITE_SIZE) x 1024
                 (gfx950 FETCH_SIZE under-reports wide coalesced reads by 2x,
                 MI355X_MICROARCH.md §HBM), averaged over launches.
-Writes profiles/traffic_latest.json keyed by bench kernel names so bench.py
-can report roofline.traffic.
+Writes <out>/summary/{<tag>_kernel_stats.csv,<tag>_traffic.json,traffic_latest.json}
+(under gpurun_out/, which is what travels back from the GPU box); copy them
+into profiles/ to commit -- bench.py reads profiles/traffic_latest.json for
+roofline.traffic.
 """
 import csv
 import glob
 import json
 import os
+import re
 import shutil
 import sys
 
-NAMES = {'k_moments': 'moments', 'k_band_mean': 'band_mean', 'k_regress': 'regress', 'k_gain_avg': 'gain_avg',
-         'k_med_walk': 'median_walk', 'k_med_keys': 'median_keys', 'k_vane': 'vane'}
+KERNEL_RE = re.compile(r'\bk_(\w+)\s*(?:\(|$)')
 
 
 def short(name):
-    for k, v in NAMES.items():
-        if k in name:
-            return v
-    return None
+    """'k_regress_avg(float const*, ...)' -> 'regress_avg' (the bench's kernel key)."""
+    m = KERNEL_RE.search(name.strip())
+    return m.group(1) if m else None
 
 
 def counter_bytes(d, counter):
@@ -42,7 +43,8 @@ def counter_bytes(d, counter):
 
 def main():
     out, tag = sys.argv[1], sys.argv[2]
-    here = os.path.dirname(os.path.abspath(__file__))
+    here = os.path.join(out, 'summary')
+    os.makedirs(here, exist_ok=True)
     stats = glob.glob(os.path.join(out, 'trace', '**', '*kernel_stats.csv'), recursive=True)
     if stats:
         shutil.copy(stats[0], os.path.join(here, f'{tag}_kernel_stats.csv'))
