@@ -72,6 +72,42 @@ def find_hot_cold_from_tod(tod):
     return hot, cold[cold > hot[-1]]
 
 
+def find_hot_cold_batch(ba):
+    """find_hot_cold_from_tod for every row of ``ba`` [n, L] at once.
+
+    The same NumPy operations as the per-series function, applied along the
+    last (contiguous) axis: row reductions use the same pairwise summation and
+    the same dtype promotions, so the selected samples are identical (checked
+    against the per-series function in tests/test_vane_search.py).  Returns
+    (hot, hoff, cold, coff): concatenated int32 sample offsets and int64 row
+    offsets; a row where either search comes back empty (the reference's
+    RuntimeError path) contributes no samples."""
+    x = np.ascontiguousarray(ba)
+    n, L = x.shape
+    N2 = (L // 2) * 2
+    rms0 = np.nanstd(x[:, 1:N2:2] - x[:, :N2:2], axis=1) / np.sqrt(2)
+    v = x * 1.0
+    rng = np.nanmax(v, axis=1, keepdims=True) - np.nanmin(v, axis=1, keepdims=True)
+    v /= rng
+    rms = rms0[:, None] / rng
+    mid = (np.nanmax(v, axis=1, keepdims=True) + np.nanmin(v, axis=1, keepdims=True)) / 2.0
+    flat = np.abs(np.gradient(v, axis=1)) < 2e-3
+    hot = np.greater(v - mid, 15 * rms) & flat
+    cold = np.less(v - mid, 15 * rms) & flat
+    ok = hot.any(axis=1) & cold.any(axis=1)
+    col = np.arange(L)
+    last_hot = np.where(hot, col, -1).max(axis=1)
+    hot &= ok[:, None]
+    cold &= ok[:, None] & (col[None, :] > last_hot[:, None])
+    hr, hc = np.nonzero(hot)
+    cr, cc = np.nonzero(cold)
+    hoff = np.zeros(n + 1, dtype=np.int64)
+    coff = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(np.bincount(hr, minlength=n), out=hoff[1:])
+    np.cumsum(np.bincount(cr, minlength=n), out=coff[1:])
+    return hc.astype(np.int32), hoff, cc.astype(np.int32), coff
+
+
 def vane_events(features):
     """find_vane_samples (VaneCalibration.py:56-65): [[start, end], ...]."""
     flag = features == 13
@@ -140,26 +176,28 @@ class GPUObservation:
         tsys = torch.zeros((nV, self.F, N_BANDS, N_CHANNELS), dtype=torch.float64, device=self.tdev)
         gain = torch.zeros_like(tsys)
         self._bind()
-        # pass A does not depend on the vane: start it now so the host search below overlaps it
+        # The band-average windows are copied first (pinned, asynchronous), then pass A
+        # (which does not depend on the vane) is queued behind them, so the host search
+        # below waits only for the copies and overlaps the 56 GB read.
+        windows, copied = [], None
+        if isinstance(band_average, torch.Tensor) and band_average.is_cuda:
+            for s, e in ev:
+                w = torch.empty(tuple(band_average.shape[:2]) + (int(e - s),), dtype=band_average.dtype,
+                                pin_memory=True)
+                w.copy_(band_average[:, :, s:e], non_blocking=True)
+                windows.append(w)
+            copied = torch.cuda.Event()
+            copied.record()
+        else:
+            windows = [to_host(band_average[:, :, s:e]) for s, e in ev]
         N.check(N.lib().comap_l1_prefetch(self.plan), self.ctx, 'comap_l1_prefetch')
         t_search = time.perf_counter()
+        if copied is not None:
+            copied.synchronize()
+            windows = [w.numpy() for w in windows]
         for iv, (s, e) in enumerate(ev):
-            ba = to_host(band_average[:, :, s:e])
-            hot_l, cold_l = [], []
-            hoff, coff = [0], [0]
-            for f in range(self.F):
-                for b in range(N_BANDS):
-                    h, c = find_hot_cold_from_tod(ba[f, b])
-                    if h is None or c is None:      # RuntimeError path: (feed, band) stays 0
-                        h = c = np.zeros(0, dtype=int)
-                    hot_l.append(h)
-                    cold_l.append(c)
-                    hoff.append(hoff[-1] + len(h))
-                    coff.append(coff[-1] + len(c))
-            hot = np.ascontiguousarray(np.concatenate(hot_l).astype(np.int32))
-            cold = np.ascontiguousarray(np.concatenate(cold_l).astype(np.int32))
-            hoff = np.asarray(hoff, dtype=np.int64)
-            coff = np.asarray(coff, dtype=np.int64)
+            ba = windows[iv]
+            hot, hoff, cold, coff = find_hot_cold_batch(ba.reshape(self.F * N_BANDS, -1))
             self.last_vane_search_ms = (time.perf_counter() - t_search) * 1e3
             N.check(N.lib().comap_l1_vane(self.plan, int(s), int(e - s), N.hptr(hot, ctypes.c_int32),
                                           N.hptr(hoff, ctypes.c_int64), N.hptr(cold, ctypes.c_int32),
