@@ -9,7 +9,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, '_lib', 'libcomap_hip.so')
+LIB_PATH = os.environ.get('COMAP_HIP_LIB') or os.path.join(_HERE, '_lib', 'libcomap_hip.so')
 
 _lib = None
 _lock = threading.Lock()

@@ -124,6 +124,13 @@ struct comap_l1_plan {
     int32_t *utile0 = nullptr;         // [U+1] first fused block of each unit
     double *part = nullptr;            // [2*NT][4096] per-block regression partials sum d mf
     int32_t *flag = nullptr;           // [1] phase-1 kappa mismatch -> legacy passes C, D run
+    // compacted channel lists per (unit, band), ascending, padded with weight-0 entries to a multiple of 8
+    int32_t *blist = nullptr;          // [U*4][1024] pass-B channels (alpha != 0)
+    int32_t *bcnt = nullptr;           // [U*4]
+    double *bw = nullptr;              // [U*4][1024] alpha of each listed channel
+    int32_t *dlist = nullptr;          // [U*4][1024] pass-C+D channels (any kappa != 0)
+    int32_t *dcnt = nullptr;           // [U*4]
+    double *dw = nullptr;              // [U*4][1024][4] (kg, kr, ko, 0) of each listed channel
     // per-kernel HIP-event timing (comap_l1_profile)
     bool prof_on = false;
     std::vector<hipEvent_t> prof_pool;

@@ -64,6 +64,34 @@ __device__ __forceinline__ bool gain_masked(int c)
     return c < 20 || c >= 1004 || (c >= 507 && c < 517);
 }
 
+// ------------------------------------------------------------------ channel-list compaction
+// Wave 0 of a block writes, in ascending order, the channels c with live(c)
+// into list[0..cnt) and emit(j, c) for each, then pads list to a multiple of 8
+// with channel 0 / pad(j) (weight-0 entries the streaming passes never let
+// contribute).  Lane l scans channels 16l..16l+15.  Returns cnt on every lane.
+template <typename Live, typename Emit, typename Pad>
+__device__ __forceinline__ int wave_compact_channels(int lane, Live live, Emit emit, Pad pad, int32_t *list)
+{
+    const int c0 = lane * 16;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) bits |= (live(c0 + i) ? 1u : 0u) << i;
+    const int m = __popc(bits);
+    int incl = m;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    int pos = incl - m;
+    for (int i = 0; i < 16; ++i)
+        if ((bits >> i) & 1u) { list[pos] = c0 + i; emit(pos, c0 + i); ++pos; }
+    const int cnt = __shfl(incl, 63, 64);
+    const int j = cnt + lane;
+    if (lane < 8 && j < ((cnt + 7) & ~7)) { list[j] = 0; pad(j); }
+    return cnt;
+}
+
 // ------------------------------------------------------------------ airmass
 // COMAPLevel1.airmass: 1/sin(el*pi/180) (DataHandling.py:398-401)
 __global__ void k_airmass(const double *__restrict__ el, double *__restrict__ A, int64_t n)
@@ -340,9 +368,11 @@ __global__ void __launch_bounds__(256) k_coef_b(const int32_t *__restrict__ unit
                                                 const double *__restrict__ mom, int64_t UC,
                                                 const double *__restrict__ oa,
                                                 double *__restrict__ alpha, double *__restrict__ nf,
-                                                double *__restrict__ bsum)
+                                                double *__restrict__ bsum, int32_t *__restrict__ blist,
+                                                int32_t *__restrict__ bcnt, double *__restrict__ bw)
 {
     __shared__ double red[4];
+    __shared__ double s_al[kChannels];
     const int ub = blockIdx.x;
     const int u = ub / kBands, b = ub % kBands;
     const int n = units[4 * u + 3];
@@ -373,6 +403,7 @@ __global__ void __launch_bounds__(256) k_coef_b(const int32_t *__restrict__ unit
             }
         }
         alpha[i] = al;
+        s_al[c] = al;
     }
     beta = block_sum256(beta, red);
     gamma = block_sum256(gamma, red);
@@ -382,6 +413,13 @@ __global__ void __launch_bounds__(256) k_coef_b(const int32_t *__restrict__ unit
         o[0] = beta; o[1] = gamma; o[2] = cnt;
         // median_filter skips the band when fewer than 2w finite band-mean samples
         o[3] = (cnt > 0 && n >= 2 * kMedfiltWindow) ? 1.0 : 0.0;
+    }
+    if (threadIdx.x < 64) {      // pass-B channel list: the median channels with alpha != 0
+        double *w = bw + (int64_t)ub * kChannels;
+        const int nc = wave_compact_channels(
+            threadIdx.x, [&](int c) { return s_al[c] != 0.0; }, [&](int j, int c) { w[j] = s_al[c]; },
+            [&](int j) { w[j] = 0.0; }, blist + (int64_t)ub * kChannels);
+        if (threadIdx.x == 0) bcnt[ub] = nc;
     }
 }
 
@@ -410,13 +448,67 @@ __device__ __forceinline__ void load_groups(const float *__restrict__ p, int nv0
     }
 }
 
+// Raw f32 groups of one channel row: r[g] = d[r0 + 256 g .. +3] (zeros beyond
+// the scan end; FULL = the whole sub-tile lies inside the scan, no checks).
+template <int J, bool FULL>
+__device__ __forceinline__ void load_raw(const float *__restrict__ p, int nv0, f32x4u (&r)[J])
+{
+#pragma unroll
+    for (int g = 0; g < J; ++g) {
+        const int nv = nv0 - 256 * g;
+        if (FULL || nv >= 4) {
+            r[g] = *reinterpret_cast<const f32x4u *>(p + 256 * g);
+        } else {
+            f32x4u v = {0.f, 0.f, 0.f, 0.f};
+            if (nv > 0) v.x = p[256 * g];
+            if (nv > 1) v.y = p[256 * g + 1];
+            if (nv > 2) v.z = p[256 * g + 2];
+            r[g] = v;
+        }
+    }
+}
+
 // Pass B on 256·kJB-sample sub-tiles (kTile/(256 kJB) blocks per 1024-sample
-// tile: ~14k blocks for C2, so the last round of the grid is a small fraction).
-constexpr int kJB = 2;
+// tile: ~7k blocks for C2).  The wave walks its (unit, band)'s compacted
+// channel list (k_coef_b) four entries at a time: 4 x kJB independent 16-B
+// loads are in flight before the first FMA, with no per-channel branch.
+#ifndef COMAP_KJB
+#define COMAP_KJB 4
+#endif
+#ifndef COMAP_BB
+#define COMAP_BB 4
+#endif
+constexpr int kJB = COMAP_KJB;
+constexpr int kBB = COMAP_BB;              // channel-list entries per load batch
 constexpr int kSubB = kTile / (256 * kJB);
+template <bool FULL>
+__device__ __forceinline__ void band_mean_sum(const float *__restrict__ base, int64_t T, int nv0,
+                                              const int32_t *__restrict__ lst, const double *__restrict__ wl,
+                                              int cnt, double (&acc)[4 * kJB])
+{
+    for (int j = 0; j < cnt; j += kBB) {
+        f32x4u r[kBB][kJB];
+#pragma unroll
+        for (int q = 0; q < kBB; ++q) load_raw<kJB, FULL>(base + (int64_t)lst[j + q] * T, nv0, r[q]);
+#pragma unroll
+        for (int q = 0; q < kBB; ++q) {
+            const double w = wl[j + q];            // 0 on pad entries
+            const bool live = j + q < cnt;         // pads must not read 0 * NaN
+#pragma unroll
+            for (int g = 0; g < kJB; ++g) {
+                acc[4 * g + 0] = fma(w, live ? (double)r[q][g].x : 0.0, acc[4 * g + 0]);
+                acc[4 * g + 1] = fma(w, live ? (double)r[q][g].y : 0.0, acc[4 * g + 1]);
+                acc[4 * g + 2] = fma(w, live ? (double)r[q][g].z : 0.0, acc[4 * g + 2]);
+                acc[4 * g + 3] = fma(w, live ? (double)r[q][g].w : 0.0, acc[4 * g + 3]);
+            }
+        }
+    }
+}
+
 __global__ void __launch_bounds__(256) k_band_mean(const float *__restrict__ tod, const double *__restrict__ A,
                                                    const int32_t *__restrict__ units, const int32_t *__restrict__ tiles,
-                                                   int64_t T, const double *__restrict__ alpha,
+                                                   int64_t T, const int32_t *__restrict__ blist,
+                                                   const int32_t *__restrict__ bcnt, const double *__restrict__ bw,
                                                    const double *__restrict__ bsum, double *__restrict__ mb)
 {
     const int b = uniform(threadIdx.x >> 6);
@@ -424,27 +516,21 @@ __global__ void __launch_bounds__(256) k_band_mean(const float *__restrict__ tod
     const int tile = blockIdx.x / kSubB, sub = blockIdx.x % kSubB;
     const int u = tiles[2 * tile], toff = tiles[2 * tile + 1] + 256 * kJB * sub;
     const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
+    if (toff >= n) return;
     const int r0 = toff + 4 * lane;                 // first sample (relative) of this lane
     const float *base = tod + (int64_t)(f * kBands + b) * kChannels * T + t0 + r0;
-    const double *al = alpha + (int64_t)u * kBC + b * kChannels;
+    const int ub = u * kBands + b;
+    const int32_t *lst = blist + (int64_t)ub * kChannels;
+    const double *wl = bw + (int64_t)ub * kChannels;
+    const int cnt = bcnt[ub];
     double acc[4 * kJB];
 #pragma unroll
     for (int i = 0; i < 4 * kJB; ++i) acc[i] = 0.0;
     const int nv0 = n - r0;
-    auto body = [&](int c) {
-        const double w = al[c];
-        if (w == 0.0) return;                       // NaN channel: weight 0 must not read 0 * NaN
-        double x[4 * kJB];
-        load_groups<kJB>(base + (int64_t)c * T, nv0, x);
-#pragma unroll
-        for (int i = 0; i < 4 * kJB; ++i) acc[i] = fma(w, x[i], acc[i]);
-    };
-#pragma unroll 2
-    for (int c = 10; c < 507; ++c) body(c);
-#pragma unroll 2
-    for (int c = 518; c < 1014; ++c) body(c);
-    const double *bs = bsum + 4 * ((int64_t)u * kBands + b);
-    const double beta = bs[0], gamma = bs[1], cnt = bs[2];
+    if (n - toff >= 256 * kJB) band_mean_sum<true>(base, T, nv0, lst, wl, cnt, acc);
+    else band_mean_sum<false>(base, T, nv0, lst, wl, cnt, acc);
+    const double *bs = bsum + 4 * (int64_t)ub;
+    const double beta = bs[0], gamma = bs[1], cn = bs[2];
     double *out = mb + (int64_t)(f * kBands + b) * T + t0 + r0;
     const double *a = A + (int64_t)f * T + t0 + r0;
 #pragma unroll
@@ -452,7 +538,7 @@ __global__ void __launch_bounds__(256) k_band_mean(const float *__restrict__ tod
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int o = 256 * g + e;
-            if (o < nv0) out[o] = cnt > 0 ? (acc[4 * g + e] - beta - gamma * a[o]) / cnt : NAN;
+            if (o < nv0) out[o] = cn > 0 ? (acc[4 * g + e] - beta - gamma * a[o]) / cn : NAN;
         }
 }
 
@@ -630,9 +716,11 @@ __global__ void __launch_bounds__(256) k_coef_d(const int32_t *__restrict__ unit
                                                 double *__restrict__ kap, double *__restrict__ dsum,
                                                 double *__restrict__ xreg, int phase,
                                                 const double *__restrict__ part, const int32_t *__restrict__ utile0,
-                                                int32_t *__restrict__ flag)
+                                                int32_t *__restrict__ flag, int32_t *__restrict__ dlist,
+                                                int32_t *__restrict__ dcnt, double *__restrict__ dw)
 {
     __shared__ double red[4];
+    __shared__ double s_kap[3][kChannels];
     const int ub = blockIdx.x;
     if (phase == 2 && *flag == 0) return;          // legacy path only runs after a fused-path mismatch
     const int u = ub / kBands, b = ub % kBands;
@@ -663,7 +751,9 @@ __global__ void __launch_bounds__(256) k_coef_d(const int32_t *__restrict__ unit
         double fa = 0, fb = 0, fg = 0, fd = 0, x0 = 0, x1 = 0;
         double sdmi = 0.0;
         if (phase == 1) {        // fused pass C+D: sum the per-block partials of this unit
-            for (int k = utile0[u]; k < utile0[u + 1]; ++k) sdmi += part[(int64_t)k * kBC + b * kChannels + c];
+            // (only the channels on the phase-0 list were read; the others have sum_t d mf = 0)
+            if (kap[i] != 0.0 || kap[UC + i] != 0.0 || kap[2 * UC + i] != 0.0)
+                for (int k = utile0[u]; k < utile0[u + 1]; ++k) sdmi += part[(int64_t)k * kBC + b * kChannels + c];
             sdm[i] = sdmi;
         } else if (phase == 2) {
             sdmi = sdm[i];
@@ -710,6 +800,9 @@ __global__ void __launch_bounds__(256) k_coef_d(const int32_t *__restrict__ unit
         kap[i] = kgfa;
         kap[UC + i] = krfa;
         kap[2 * UC + i] = kofa;
+        s_kap[0][c] = kgfa;
+        s_kap[1][c] = krfa;
+        s_kap[2][c] = kofa;
         if (kg != 0.0) { acc[0] += kg * fb; acc[1] += kg * fg; acc[2] += kg * fd; }
         if (kr != 0.0) { acc[3] += kr * fb; acc[4] += kr * fg; acc[5] += kr * fd; acc[9] += kr; }
         if (ko != 0.0) { acc[6] += ko * fb; acc[7] += ko * fg; acc[8] += ko * fd; }
@@ -722,6 +815,18 @@ __global__ void __launch_bounds__(256) k_coef_d(const int32_t *__restrict__ unit
         double *o = dsum + 16 * (int64_t)ub;
 #pragma unroll
         for (int k = 0; k < 12; ++k) o[k] = acc[k];
+    }
+    if (phase == 0 && threadIdx.x < 64) {     // fused-pass channel list: any kappa != 0
+        double *w = dw + 4 * (int64_t)ub * kChannels;
+        const int nc = wave_compact_channels(
+            threadIdx.x,
+            [&](int c) { return s_kap[0][c] != 0.0 || s_kap[1][c] != 0.0 || s_kap[2][c] != 0.0; },
+            [&](int j, int c) {
+                w[4 * j] = s_kap[0][c]; w[4 * j + 1] = s_kap[1][c]; w[4 * j + 2] = s_kap[2][c]; w[4 * j + 3] = 0.0;
+            },
+            [&](int j) { w[4 * j] = w[4 * j + 1] = w[4 * j + 2] = w[4 * j + 3] = 0.0; },
+            dlist + (int64_t)ub * kChannels);
+        if (threadIdx.x == 0) dcnt[ub] = nc;
     }
 }
 
@@ -807,7 +912,13 @@ __global__ void __launch_bounds__(256) k_gain_avg(const float *__restrict__ tod,
 // k_coef_d phase 1 then solves the regression and folds the per-band
 // constants; k_finish applies them.  Block = 256 threads (wave b = band) on a
 // 256·kJ2-sample sub-tile of a 1024-sample tile; lane owns kJ2 groups of 4 samples.
-constexpr int kJ2 = 2;
+#ifndef COMAP_KJ2
+#define COMAP_KJ2 2
+#endif
+#ifndef COMAP_RA_MINW
+#define COMAP_RA_MINW 1
+#endif
+constexpr int kJ2 = COMAP_KJ2;
 constexpr int kSub2 = kTile / (256 * kJ2);   // fused blocks per 1024-sample tile
 
 // Sum 8 per-lane values over the 64 lanes of a wave; on return lane l holds
@@ -835,9 +946,53 @@ __device__ __forceinline__ double wave_reduce8(const double (&v)[8], int lane)
     r += __shfl_xor(r, 1, 64);
     return r;
 }
-__global__ void __launch_bounds__(256) k_regress_avg(const float *__restrict__ tod, const int32_t *__restrict__ units,
-                                                     const int32_t *__restrict__ tiles, int64_t T, int64_t UC,
-                                                     const double *__restrict__ kap, const double *__restrict__ mf,
+template <bool FULL>
+__device__ __forceinline__ void regress_avg_sum(const float *__restrict__ base, int64_t T, int nv0, int lane,
+                                                const int32_t *__restrict__ lst, const double *__restrict__ wl,
+                                                int cnt, const double (&mt)[4 * kJ2], double (&ag)[4 * kJ2],
+                                                double (&ar)[4 * kJ2], double (&ao)[4 * kJ2],
+                                                double *__restrict__ pp)
+{
+    for (int j8 = 0; j8 < cnt; j8 += 8) {
+        double pcs[8];
+#pragma unroll
+        for (int h = 0; h < 8; h += 4) {
+            f32x4u r[4][kJ2];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) load_raw<kJ2, FULL>(base + (int64_t)lst[j8 + h + q] * T, nv0, r[q]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int j = j8 + h + q;
+                const double wg = wl[4 * j], wr = wl[4 * j + 1], wo = wl[4 * j + 2];   // 0 on pads
+                const bool live = j < cnt;                                            // no 0 * NaN on pads
+                double pc = 0.0;
+#pragma unroll
+                for (int g = 0; g < kJ2; ++g) {
+                    const double xs[4] = {(double)r[q][g].x, (double)r[q][g].y, (double)r[q][g].z,
+                                          (double)r[q][g].w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int i = 4 * g + e;
+                        const double x = live ? xs[e] : 0.0;
+                        ag[i] = fma(wg, x, ag[i]);
+                        ar[i] = fma(wr, x, ar[i]);
+                        ao[i] = fma(wo, x, ao[i]);
+                        pc = fma(x, mt[i], pc);
+                    }
+                }
+                pcs[h + q] = pc;
+            }
+        }
+        const double tot = wave_reduce8(pcs, lane);
+        const int j = j8 + (lane >> 3);
+        if ((lane & 7) == 0 && j < cnt) pp[lst[j]] = tot;
+    }
+}
+
+__global__ void __launch_bounds__(256, COMAP_RA_MINW) k_regress_avg(const float *__restrict__ tod, const int32_t *__restrict__ units,
+                                                     const int32_t *__restrict__ tiles, int64_t T,
+                                                     const int32_t *__restrict__ dlist, const int32_t *__restrict__ dcnt,
+                                                     const double *__restrict__ dw, const double *__restrict__ mf,
                                                      double *__restrict__ part, double *__restrict__ sr_out,
                                                      double *__restrict__ so_out, double *__restrict__ sg_out)
 {
@@ -850,8 +1005,10 @@ __global__ void __launch_bounds__(256) k_regress_avg(const float *__restrict__ t
     const int r0 = toff + 4 * lane;
     const int nv0 = n - r0;                          // valid samples from this lane's first group
     const float *base = tod + (int64_t)(f * kBands + b) * kChannels * T + t0 + r0;
-    const int64_t kb = (int64_t)u * kBC + b * kChannels;
-    const double *kg = kap + kb, *kr = kap + UC + kb, *ko = kap + 2 * UC + kb;
+    const int ub = u * kBands + b;
+    const int32_t *lst = dlist + (int64_t)ub * kChannels;
+    const double *wl = dw + 4 * (int64_t)ub * kChannels;
+    const int cnt = dcnt[ub];
     double *pp = part + (int64_t)blockIdx.x * kBC + b * kChannels;
     const double *m = mf + (int64_t)(f * kBands + b) * T + t0 + r0;
     double mt[4 * kJ2];
@@ -862,40 +1019,8 @@ __global__ void __launch_bounds__(256) k_regress_avg(const float *__restrict__ t
     double ag[4 * kJ2], ar[4 * kJ2], ao[4 * kJ2];
 #pragma unroll
     for (int i = 0; i < 4 * kJ2; ++i) ag[i] = ar[i] = ao[i] = 0.0;
-    for (int c8 = 0; c8 < kChannels; c8 += 8) {
-      double pcs[8];
-#pragma unroll
-      for (int cc = 0; cc < 8; ++cc) {
-        const int c = c8 + cc;
-        pcs[cc] = 0.0;
-        const double wg = kg[c], wr = kr[c], wo = ko[c];
-        if (wg == 0.0 && wr == 0.0 && wo == 0.0) continue;   // channel in none of the averages: not read
-        const float *q = base + (int64_t)c * T;
-        double x[4 * kJ2];
-#pragma unroll
-        for (int g = 0; g < kJ2; ++g) {
-            const int nv = nv0 - 256 * g;
-            if (nv >= 4) {
-                const f32x4u v = *reinterpret_cast<const f32x4u *>(q + 256 * g);
-                x[4 * g] = v.x; x[4 * g + 1] = v.y; x[4 * g + 2] = v.z; x[4 * g + 3] = v.w;
-            } else {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) x[4 * g + e] = (e < nv) ? (double)q[256 * g + e] : 0.0;
-            }
-        }
-        double pc = 0.0;
-#pragma unroll
-        for (int i = 0; i < 4 * kJ2; ++i) {
-            ag[i] = fma(wg, x[i], ag[i]);
-            ar[i] = fma(wr, x[i], ar[i]);
-            ao[i] = fma(wo, x[i], ao[i]);
-            pc = fma(x[i], mt[i], pc);
-        }
-        pcs[cc] = pc;
-      }
-      const double tot = wave_reduce8(pcs, lane);
-      if ((lane & 7) == 0) pp[c8 + (lane >> 3)] = tot;
-    }
+    if (n - toff >= 256 * kJ2) regress_avg_sum<true>(base, T, nv0, lane, lst, wl, cnt, mt, ag, ar, ao, pp);
+    else regress_avg_sum<false>(base, T, nv0, lane, lst, wl, cnt, mt, ag, ar, ao, pp);
 #pragma unroll
     for (int g = 0; g < kJ2; ++g)
 #pragma unroll
@@ -1134,6 +1259,12 @@ extern "C" int comap_l1_plan_create(comap_ctx *ctx, const comap_obs_desc *d, com
     rc |= upload(ctx, (void **)&p->utile0, utile0.data(), utile0.size() * 4);
     rc |= dalloc(ctx, &p->part, (size_t)kSub2 * p->n_tiles * kBC);
     rc |= dalloc(ctx, &p->flag, 1);
+    rc |= dalloc(ctx, &p->blist, (size_t)p->U * kBC);
+    rc |= dalloc(ctx, &p->bcnt, (size_t)p->U * kBands);
+    rc |= dalloc(ctx, &p->bw, (size_t)p->U * kBC);
+    rc |= dalloc(ctx, &p->dlist, (size_t)p->U * kBC);
+    rc |= dalloc(ctx, &p->dcnt, (size_t)p->U * kBands);
+    rc |= dalloc(ctx, &p->dw, 4 * (size_t)p->U * kBC);
     if (hipHostMalloc((void **)&p->nan_host, 4, hipHostMallocDefault) != hipSuccess) rc |= 1;
     if (hipEventCreateWithFlags(&p->mom_event, hipEventDisableTiming) != hipSuccess) rc |= 1;
     rc |= upload(ctx, (void **)&p->units, p->units_h.data(), p->units_h.size() * 4);
@@ -1195,7 +1326,7 @@ extern "C" int comap_l1_plan_destroy(comap_l1_plan *p)
     void *bufs[] = {p->units, p->tiles, p->airmass, p->unit_sums, p->mom,
                     p->nan_count, p->alpha, p->nf, p->bsum, p->mb, p->mf, p->ssum, p->sdm, p->gw,
                     p->gmode, p->kap, p->dsum, p->xreg, p->dG, p->rowbad, p->ubs, p->fitsum, p->oa,
-                    p->utile0, p->part, p->flag};
+                    p->utile0, p->part, p->flag, p->blist, p->bcnt, p->bw, p->dlist, p->dcnt, p->dw};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     comap_median_plan_free(&p->med);
@@ -1408,10 +1539,10 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
     k_gather_oa<<<(UC + 255) / 256, 256, 0, st>>>(p->units, fit, p->F, p->U, cmed, p->oa);
     COMAP_LAUNCH_CHECK(ctx);
     PROF(p, KV_COEF_B, k_coef_b<<<UB, 256, 0, st>>>(p->units, p->unit_sums, p->mom, UC, p->oa, p->alpha, p->nf,
-                                                    p->bsum));
+                                                    p->bsum, p->blist, p->bcnt, p->bw));
     COMAP_LAUNCH_CHECK(ctx);
     PROF(p, KV_BAND_MEAN, k_band_mean<<<kSubB * p->n_tiles, 256, 0, st>>>(p->tod, p->airmass, p->units, p->tiles, p->T,
-                                                                  p->alpha, p->bsum, p->mb));
+                                                                  p->blist, p->bcnt, p->bw, p->bsum, p->mb));
     COMAP_LAUNCH_CHECK(ctx);
     PROF(p, KV_MEDIAN, rc = comap_median_run(ctx, &p->med));
     if (rc) return rc;
@@ -1423,14 +1554,14 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
     auto coef_d = [&](int phase) {
         k_coef_d<<<UB, 256, 0, st>>>(p->units, p->unit_sums, p->mom, UC, p->oa, p->alpha, p->nf, p->bsum, p->ssum,
                                      p->sdm, tsys0, gain0, p->gw, p->gmode, calibrator, p->kap, p->dsum, p->xreg,
-                                     phase, p->part, p->utile0, p->flag);
+                                     phase, p->part, p->utile0, p->flag, p->dlist, p->dcnt, p->dw);
     };
     // fused pass C+D: kappa first, one read of the cube, then the regression and the constants
     PROF(p, KV_COEF_D, coef_d(0));
     COMAP_LAUNCH_CHECK(ctx);
-    PROF(p, KV_REGRESS_AVG, k_regress_avg<<<kSub2 * p->n_tiles, 256, 0, st>>>(p->tod, p->units, p->tiles, p->T, UC,
-                                                                          p->kap, p->mf, p->part, tod_out, orig_out,
-                                                                          p->dG));
+    PROF(p, KV_REGRESS_AVG, k_regress_avg<<<kSub2 * p->n_tiles, 256, 0, st>>>(p->tod, p->units, p->tiles, p->T,
+                                                                          p->dlist, p->dcnt, p->dw, p->mf, p->part,
+                                                                          tod_out, orig_out, p->dG));
     COMAP_LAUNCH_CHECK(ctx);
     PROF(p, KV_COEF_D, coef_d(1));
     COMAP_LAUNCH_CHECK(ctx);
