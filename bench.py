@@ -29,8 +29,9 @@ sys.path.insert(0, ROOT)
 
 ALGO_BYTES_PER_SAMPCH_PASS = 4      # one f32 read of the cube per streaming pass
 SURVEY_BYTES_PER_SAMPCH = 16        # 4 passes (A, B, C, D) x 4 B
-# this design streams the cube 3 times: A (moments), B (band mean) and the fused C+D
-# (regress_avg), which skips the channels that are in no average
+# this design streams the cube 3 times: A (moments), B (band means + every per-sample
+# output sum, band_sums) and C (regression sums, regress); B and C read only the
+# median_filter channels
 HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 
 
@@ -206,10 +207,9 @@ def main():
         value = world * samp_ch * args.steps / elapsed
         scan_sc = obs.scan_samples() * 4096
         stream = {k: prof[k] for k in obs.STREAMING}
-        active = obs.active_channel_fraction()
-        # bytes each pass must read: A all 1024 channels, B the 993 median_filter channels,
-        # C+D the channels with a nonzero weight
-        frac = {'moments': 1.0, 'band_mean': 993 / 1024, 'regress_avg': active}
+        # bytes each pass must read: A all 1024 channels, B the median_filter channels with a
+        # finite 1/rms, C those channels in the bands the median filter did not skip
+        frac = obs.pass_fractions()
         pass_bytes = {k: ALGO_BYTES_PER_SAMPCH_PASS * scan_sc * frac[k] for k in obs.STREAMING}
         dom = max(stream, key=lambda k: stream[k][0])
         ms_avg = stream[dom][0] / max(stream[dom][1], 1)
@@ -243,7 +243,7 @@ def main():
             'l1_step_roofline': {'passes': len(obs.STREAMING), 'design_bytes': design_bytes,
                                  'achieved_GBs': design_bytes / (step_ms * 1e-3) / 1e9,
                                  'frac': design_bytes / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                                 'fused_pass_active_channels': active,
+                                 'pass_channel_fraction': frac,
                                  'survey_4pass_bytes': SURVEY_BYTES_PER_SAMPCH * scan_sc,
                                  'survey_4pass_equiv_frac':
                                      SURVEY_BYTES_PER_SAMPCH * scan_sc / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},

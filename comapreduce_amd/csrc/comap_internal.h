@@ -120,17 +120,12 @@ struct comap_l1_plan {
     double *ubs = nullptr;             // [U*4][4] fit normal-equation sums n, SA, SAA per (unit, band)
     double *fitsum = nullptr;          // [2][U*4096] masked Sd, SAd (select_time path)
     double *oa = nullptr;              // [U*4096][2] offset/slope L1AGC subtracts
-    // fused pass C+D
-    int32_t *utile0 = nullptr;         // [U+1] first fused block of each unit
-    double *part = nullptr;            // [2*NT][4096] per-block regression partials sum d mf
     int32_t *flag = nullptr;           // [1] phase-1 kappa mismatch -> legacy passes C, D run
-    // compacted channel lists per (unit, band), ascending, padded with weight-0 entries to a multiple of 8
-    int32_t *blist = nullptr;          // [U*4][1024] pass-B channels (alpha != 0)
-    int32_t *bcnt = nullptr;           // [U*4]
-    double *bw = nullptr;              // [U*4][1024] alpha of each listed channel
-    int32_t *dlist = nullptr;          // [U*4][1024] pass-C+D channels (any kappa != 0)
+    // channel list per (unit, band) for passes B and C: the median channels with alpha != 0,
+    // ascending (k_coef_d phase 0)
+    int32_t *dlist = nullptr;          // [U*4][1024]
     int32_t *dcnt = nullptr;           // [U*4]
-    double *dw = nullptr;              // [U*4][1024][4] (kg, kr, ko, 0) of each listed channel
+    double *dw = nullptr;              // [U*4][1024][4] (alpha, kg, kr, ko) of each listed channel
     // per-kernel HIP-event timing (comap_l1_profile)
     bool prof_on = false;
     std::vector<hipEvent_t> prof_pool;
@@ -141,6 +136,6 @@ struct comap_l1_plan {
 
 // kernel ids for comap_l1_profile_collect
 enum L1Kernel {
-    KV_VANE = 0, KV_MOMENTS, KV_ATMOS_FIT, KV_COEF_B, KV_BAND_MEAN, KV_MEDIAN, KV_SERIES_SUMS,
+    KV_VANE = 0, KV_MOMENTS, KV_ATMOS_FIT, KV_COEF_B, KV_BAND_SUMS, KV_MEDIAN, KV_SERIES_SUMS,
     KV_REGRESS, KV_GAIN_WEIGHTS, KV_COEF_D, KV_GAIN_AVG, KV_SCAN_WEIGHTS, KV_REGRESS_AVG, KV_FINISH, KV_COUNT
 };

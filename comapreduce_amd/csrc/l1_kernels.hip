@@ -368,11 +368,9 @@ __global__ void __launch_bounds__(256) k_coef_b(const int32_t *__restrict__ unit
                                                 const double *__restrict__ mom, int64_t UC,
                                                 const double *__restrict__ oa,
                                                 double *__restrict__ alpha, double *__restrict__ nf,
-                                                double *__restrict__ bsum, int32_t *__restrict__ blist,
-                                                int32_t *__restrict__ bcnt, double *__restrict__ bw)
+                                                double *__restrict__ bsum)
 {
     __shared__ double red[4];
-    __shared__ double s_al[kChannels];
     const int ub = blockIdx.x;
     const int u = ub / kBands, b = ub % kBands;
     const int n = units[4 * u + 3];
@@ -403,7 +401,6 @@ __global__ void __launch_bounds__(256) k_coef_b(const int32_t *__restrict__ unit
             }
         }
         alpha[i] = al;
-        s_al[c] = al;
     }
     beta = block_sum256(beta, red);
     gamma = block_sum256(gamma, red);
@@ -414,24 +411,23 @@ __global__ void __launch_bounds__(256) k_coef_b(const int32_t *__restrict__ unit
         // median_filter skips the band when fewer than 2w finite band-mean samples
         o[3] = (cnt > 0 && n >= 2 * kMedfiltWindow) ? 1.0 : 0.0;
     }
-    if (threadIdx.x < 64) {      // pass-B channel list: the median channels with alpha != 0
-        double *w = bw + (int64_t)ub * kChannels;
-        const int nc = wave_compact_channels(
-            threadIdx.x, [&](int c) { return s_al[c] != 0.0; }, [&](int j, int c) { w[j] = s_al[c]; },
-            [&](int j) { w[j] = 0.0; }, blist + (int64_t)ub * kChannels);
-        if (threadIdx.x == 0) bcnt[ub] = nc;
-    }
 }
 
 // ------------------------------------------------------------------ pass B
-// Band mean over the median channels (nanmean, Level1Averaging.py:691-692):
-//   m_t = (sum_c alpha_c d_ct - beta - gamma A_t) / N
-// A lane owns kJ groups of 4 consecutive samples, group g at lane offset 256 g,
-// so one wave visits kTile = 256 kJ contiguous samples (4 kJ KB) of a channel
-// row per channel step: long DRAM/TLB runs despite the row stride.
-constexpr int kJ = kTile / 256;
+// One read of the cube BEFORE the median serves every per-sample channel sum
+// of the reduction (Level1Averaging.py:691-692, 841-867; GainSubtraction.py:201):
+//   m_t   = (sum_c alpha_c d_ct - beta - gamma A_t) / N      band mean -> median
+//   Sg_t  = sum_b sum_c kg_c d_ct                             gain template (dG)
+//   Sr_bt = sum_c kr_c d_ct,  So_bt = sum_c ko_c d_ct         residual / original band sums
+// The kappa weights (k_coef_d phase 0) depend on the regression only through
+// a NaN coefficient, which phase 1 detects (then the legacy pass D runs), so
+// they are known here; the regression enters later only through per-band
+// constants (k_finish).  The wave walks its (unit, band)'s channel list
+// (k_coef_d phase 0: the median channels with alpha != 0, a superset of the
+// kappa channels) four entries at a time, 4 x kJB 16-B loads in flight.
 
 // x[4g+e] = d[r0 + 256 g + e] (0 beyond the scan end, nv0 = n - r0)
+constexpr int kJ = kTile / 256;
 template <int J = kJ>
 __device__ __forceinline__ void load_groups(const float *__restrict__ p, int nv0, double (&x)[4 * J])
 {
@@ -468,77 +464,101 @@ __device__ __forceinline__ void load_raw(const float *__restrict__ p, int nv0, f
     }
 }
 
-// Pass B on 256·kJB-sample sub-tiles (kTile/(256 kJB) blocks per 1024-sample
-// tile: ~7k blocks for C2).  The wave walks its (unit, band)'s compacted
-// channel list (k_coef_b) four entries at a time: 4 x kJB independent 16-B
-// loads are in flight before the first FMA, with no per-channel branch.
 #ifndef COMAP_KJB
-#define COMAP_KJB 4
+#define COMAP_KJB 2
 #endif
-#ifndef COMAP_BB
-#define COMAP_BB 4
-#endif
-constexpr int kJB = COMAP_KJB;
-constexpr int kBB = COMAP_BB;              // channel-list entries per load batch
-constexpr int kSubB = kTile / (256 * kJB);
-template <bool FULL>
-__device__ __forceinline__ void band_mean_sum(const float *__restrict__ base, int64_t T, int nv0,
-                                              const int32_t *__restrict__ lst, const double *__restrict__ wl,
-                                              int cnt, double (&acc)[4 * kJB])
+constexpr int kJB = COMAP_KJB;             // groups of 4 samples per lane
+constexpr int kSubB = kTile / (256 * kJB); // pass-B blocks per 1024-sample tile
+
+struct BandAcc {
+    double m[4 * kJB], g[4 * kJB], r[4 * kJB], o[4 * kJB];
+};
+
+__device__ __forceinline__ void band_fma(BandAcc &a, const double *__restrict__ w, const f32x4u (&r)[kJB])
 {
-    for (int j = 0; j < cnt; j += kBB) {
-        f32x4u r[kBB][kJB];
+    const double wa = w[0], wg = w[1], wr = w[2], wo = w[3];
 #pragma unroll
-        for (int q = 0; q < kBB; ++q) load_raw<kJB, FULL>(base + (int64_t)lst[j + q] * T, nv0, r[q]);
+    for (int g = 0; g < kJB; ++g)
 #pragma unroll
-        for (int q = 0; q < kBB; ++q) {
-            const double w = wl[j + q];            // 0 on pad entries
-            const bool live = j + q < cnt;         // pads must not read 0 * NaN
-#pragma unroll
-            for (int g = 0; g < kJB; ++g) {
-                acc[4 * g + 0] = fma(w, live ? (double)r[q][g].x : 0.0, acc[4 * g + 0]);
-                acc[4 * g + 1] = fma(w, live ? (double)r[q][g].y : 0.0, acc[4 * g + 1]);
-                acc[4 * g + 2] = fma(w, live ? (double)r[q][g].z : 0.0, acc[4 * g + 2]);
-                acc[4 * g + 3] = fma(w, live ? (double)r[q][g].w : 0.0, acc[4 * g + 3]);
-            }
+        for (int e = 0; e < 4; ++e) {
+            const int i = 4 * g + e;
+            const double x = (double)r[g][e];
+            a.m[i] = fma(wa, x, a.m[i]);
+            a.g[i] = fma(wg, x, a.g[i]);
+            a.r[i] = fma(wr, x, a.r[i]);
+            a.o[i] = fma(wo, x, a.o[i]);
         }
+}
+
+template <bool FULL>
+__device__ __forceinline__ void band_sums(const float *__restrict__ base, int64_t T, int nv0,
+                                          const int32_t *__restrict__ lst, const double *__restrict__ wl, int cnt,
+                                          BandAcc &a)
+{
+    int j = 0;
+    for (; j + 4 <= cnt; j += 4) {
+        f32x4u r[4][kJB];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) load_raw<kJB, FULL>(base + (int64_t)lst[j + q] * T, nv0, r[q]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) band_fma(a, wl + 4 * (j + q), r[q]);
+    }
+    for (; j < cnt; ++j) {
+        f32x4u r[kJB];
+        load_raw<kJB, FULL>(base + (int64_t)lst[j] * T, nv0, r);
+        band_fma(a, wl + 4 * j, r);
     }
 }
 
-__global__ void __launch_bounds__(256) k_band_mean(const float *__restrict__ tod, const double *__restrict__ A,
+// Block = 4 waves (wave b = band b) on a 256 kJB-sample sub-tile of a 1024-sample tile.
+__global__ void __launch_bounds__(256) k_band_sums(const float *__restrict__ tod, const double *__restrict__ A,
                                                    const int32_t *__restrict__ units, const int32_t *__restrict__ tiles,
-                                                   int64_t T, const int32_t *__restrict__ blist,
-                                                   const int32_t *__restrict__ bcnt, const double *__restrict__ bw,
-                                                   const double *__restrict__ bsum, double *__restrict__ mb)
+                                                   int64_t T, const int32_t *__restrict__ dlist,
+                                                   const int32_t *__restrict__ dcnt, const double *__restrict__ dw,
+                                                   const double *__restrict__ bsum, double *__restrict__ mb,
+                                                   double *__restrict__ sr_out, double *__restrict__ so_out,
+                                                   double *__restrict__ sg_out)
 {
+    __shared__ double sg[kBands][256 * kJB];
     const int b = uniform(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int tile = blockIdx.x / kSubB, sub = blockIdx.x % kSubB;
     const int u = tiles[2 * tile], toff = tiles[2 * tile + 1] + 256 * kJB * sub;
     const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
-    if (toff >= n) return;
+    if (toff >= n) return;                          // whole block: past the scan end
     const int r0 = toff + 4 * lane;                 // first sample (relative) of this lane
+    const int nv0 = n - r0;
     const float *base = tod + (int64_t)(f * kBands + b) * kChannels * T + t0 + r0;
     const int ub = u * kBands + b;
-    const int32_t *lst = blist + (int64_t)ub * kChannels;
-    const double *wl = bw + (int64_t)ub * kChannels;
-    const int cnt = bcnt[ub];
-    double acc[4 * kJB];
+    BandAcc acc;
 #pragma unroll
-    for (int i = 0; i < 4 * kJB; ++i) acc[i] = 0.0;
-    const int nv0 = n - r0;
-    if (n - toff >= 256 * kJB) band_mean_sum<true>(base, T, nv0, lst, wl, cnt, acc);
-    else band_mean_sum<false>(base, T, nv0, lst, wl, cnt, acc);
+    for (int i = 0; i < 4 * kJB; ++i) acc.m[i] = acc.g[i] = acc.r[i] = acc.o[i] = 0.0;
+    const int32_t *lst = dlist + (int64_t)ub * kChannels;
+    const double *wl = dw + 4 * (int64_t)ub * kChannels;
+    if (n - toff >= 256 * kJB) band_sums<true>(base, T, nv0, lst, wl, dcnt[ub], acc);
+    else band_sums<false>(base, T, nv0, lst, wl, dcnt[ub], acc);
+#pragma unroll
+    for (int g = 0; g < kJB; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sg[b][256 * g + 4 * lane + e] = acc.g[4 * g + e];
+    __syncthreads();
     const double *bs = bsum + 4 * (int64_t)ub;
     const double beta = bs[0], gamma = bs[1], cn = bs[2];
-    double *out = mb + (int64_t)(f * kBands + b) * T + t0 + r0;
+    const int64_t rowo = (int64_t)(f * kBands + b) * T + t0 + r0;
     const double *a = A + (int64_t)f * T + t0 + r0;
 #pragma unroll
     for (int g = 0; g < kJB; ++g)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const int o = 256 * g + e;
-            if (o < nv0) out[o] = cn > 0 ? (acc[4 * g + e] - beta - gamma * a[o]) / cn : NAN;
+            const int i = 4 * g + e, o = 256 * g + e;
+            if (o >= nv0) continue;
+            mb[rowo + o] = cn > 0 ? (acc.m[i] - beta - gamma * a[o]) / cn : NAN;
+            sr_out[rowo + o] = acc.r[i];
+            so_out[rowo + o] = acc.o[i];
+            if (b == 0) {
+                const int tl = 256 * g + 4 * lane + e;
+                sg_out[(int64_t)f * T + t0 + r0 + o] = (sg[0][tl] + sg[1][tl]) + (sg[2][tl] + sg[3][tl]);
+            }
         }
 }
 
@@ -574,38 +594,40 @@ __global__ void __launch_bounds__(256) k_series_sums(const int32_t *__restrict__
 
 // ------------------------------------------------------------------ pass C
 // Regression of each median channel on [1, mf] (Level1Averaging.py:701-705):
-// only sum_t d mf is new (sum d came from pass A).
+// only sum_t d mf is new (sum d came from pass A).  Row streaming like pass
+// A: a wave owns kRPW entries of the (unit, band)'s channel list and walks
+// the scan 4 samples per lane, sharing the mf loads between its rows.  Bands
+// the median filter skipped need no regression and are not read.
+constexpr int kRPW = 8;
+constexpr int kRegBlocks = kChannels / (4 * kRPW);   // blocks per (unit, band)
 __global__ void __launch_bounds__(256) k_regress(const float *__restrict__ tod, const double *__restrict__ mf,
                                                  const int32_t *__restrict__ units, int64_t T,
-                                                 const double *__restrict__ bsum, double *__restrict__ sdm,
-                                                 const int32_t *__restrict__ flag)
+                                                 const double *__restrict__ bsum, const int32_t *__restrict__ dlist,
+                                                 const int32_t *__restrict__ dcnt, double *__restrict__ sdm)
 {
-    if (*flag == 0) return;                         // legacy pass C: only after a fused-path mismatch
     const int wid = uniform(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const int groups_per_band = kChannels / (4 * kCPW);
-    int bid = blockIdx.x;
-    const int g = bid % groups_per_band; bid /= groups_per_band;
-    const int b = bid % kBands;
-    const int u = bid / kBands;
+    const int ub = blockIdx.x / kRegBlocks, g = blockIdx.x % kRegBlocks;
+    const int u = ub / kBands, b = ub % kBands;
+    const int cnt = dcnt[ub];
+    const int j0 = g * 4 * kRPW + wid * kRPW;
+    if (j0 >= cnt || bsum[4 * (int64_t)ub + 3] <= 0) return;
     const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
-    const int c0 = g * 4 * kCPW + wid * kCPW;
-    const int64_t ob = (int64_t)u * kBC + b * kChannels + c0;
-    if (bsum[4 * ((int64_t)u * kBands + b) + 3] <= 0) {   // band skipped by the median filter
-        if (lane < kCPW) sdm[ob + lane] = 0.0;
-        return;
-    }
-    const float *row0 = tod + ((int64_t)(f * kBands + b) * kChannels + c0) * T + t0;
-    const double *m = mf + (int64_t)(f * kBands + b) * T + t0;
-    double acc[kCPW];
+    const int32_t *lst = dlist + (int64_t)ub * kChannels;
+    const float *band = tod + (int64_t)(f * kBands + b) * kChannels * T + t0;
+    const float *row[kRPW];
 #pragma unroll
-    for (int r = 0; r < kCPW; ++r) acc[r] = 0.0;
+    for (int r = 0; r < kRPW; ++r) row[r] = band + (int64_t)lst[j0 + r < cnt ? j0 + r : j0] * T;   // pad: re-read
+    const double *m = mf + (int64_t)(f * kBands + b) * T + t0;
+    double acc[kRPW];
+#pragma unroll
+    for (int r = 0; r < kRPW; ++r) acc[r] = 0.0;
     const int n4 = n >> 2;
     for (int k = lane; k < n4; k += 64) {
         const double m0 = m[4 * k], m1 = m[4 * k + 1], m2 = m[4 * k + 2], m3 = m[4 * k + 3];
 #pragma unroll
-        for (int r = 0; r < kCPW; ++r) {
-            const f32x4u x = *reinterpret_cast<const f32x4u *>(row0 + (int64_t)r * T + 4 * k);
+        for (int r = 0; r < kRPW; ++r) {
+            const f32x4u x = *reinterpret_cast<const f32x4u *>(row[r] + 4 * k);
             double s = acc[r];
             s = fma(m0, (double)x.x, s);
             s = fma(m1, (double)x.y, s);
@@ -617,12 +639,13 @@ __global__ void __launch_bounds__(256) k_regress(const float *__restrict__ tod, 
     const int tt = 4 * n4 + lane;
     if (lane < 4 && tt < n) {
 #pragma unroll
-        for (int r = 0; r < kCPW; ++r) acc[r] = fma(m[tt], (double)row0[(int64_t)r * T + tt], acc[r]);
+        for (int r = 0; r < kRPW; ++r) acc[r] = fma(m[tt], (double)row[r][tt], acc[r]);
     }
+    double *out = sdm + (int64_t)u * kBC + b * kChannels;
 #pragma unroll
-    for (int r = 0; r < kCPW; ++r) {
+    for (int r = 0; r < kRPW; ++r) {
         const double s = wave_sum(acc[r]);
-        if (lane == 0) sdm[ob + r] = s;
+        if (lane == 0 && j0 + r < cnt) out[lst[j0 + r]] = s;
     }
 }
 
@@ -715,12 +738,11 @@ __global__ void __launch_bounds__(256) k_coef_d(const int32_t *__restrict__ unit
                                                 const int32_t *__restrict__ gmode, int calibrator,
                                                 double *__restrict__ kap, double *__restrict__ dsum,
                                                 double *__restrict__ xreg, int phase,
-                                                const double *__restrict__ part, const int32_t *__restrict__ utile0,
                                                 int32_t *__restrict__ flag, int32_t *__restrict__ dlist,
                                                 int32_t *__restrict__ dcnt, double *__restrict__ dw)
 {
     __shared__ double red[4];
-    __shared__ double s_kap[3][kChannels];
+    __shared__ double s_kap[4][kChannels];     // alpha, kg, kr, ko (phase 0 channel list)
     const int ub = blockIdx.x;
     if (phase == 2 && *flag == 0) return;          // legacy path only runs after a fused-path mismatch
     const int u = ub / kBands, b = ub % kBands;
@@ -749,17 +771,9 @@ __global__ void __launch_bounds__(256) k_coef_d(const int32_t *__restrict__ unit
         const double tsv = tsys0[(int64_t)f * kBC + b * kChannels + c];
         // ---- filtered TOD coefficients
         double fa = 0, fb = 0, fg = 0, fd = 0, x0 = 0, x1 = 0;
-        double sdmi = 0.0;
-        if (phase == 1) {        // fused pass C+D: sum the per-block partials of this unit
-            // (only the channels on the phase-0 list were read; the others have sum_t d mf = 0)
-            if (kap[i] != 0.0 || kap[UC + i] != 0.0 || kap[2 * UC + i] != 0.0)
-                for (int k = utile0[u]; k < utile0[u + 1]; ++k) sdmi += part[(int64_t)k * kBC + b * kChannels + c];
-            sdm[i] = sdmi;
-        } else if (phase == 2) {
-            sdmi = sdm[i];
-        }
         if (band_on && median_channel(c)) {
             if (al != 0.0) {
+                const double sdmi = (phase != 0) ? sdm[i] : 0.0;   // pass C (every listed channel)
                 const double sy = al * (mom[i] - n * o - a * SA);
                 const double sym = al * (sdmi - o * Smf - a * SAm);
                 if (phase != 0) {    // phase 0: x unknown yet; kappa never depends on x unless x is NaN
@@ -800,9 +814,10 @@ __global__ void __launch_bounds__(256) k_coef_d(const int32_t *__restrict__ unit
         kap[i] = kgfa;
         kap[UC + i] = krfa;
         kap[2 * UC + i] = kofa;
-        s_kap[0][c] = kgfa;
-        s_kap[1][c] = krfa;
-        s_kap[2][c] = kofa;
+        s_kap[0][c] = al;
+        s_kap[1][c] = kgfa;
+        s_kap[2][c] = krfa;
+        s_kap[3][c] = kofa;
         if (kg != 0.0) { acc[0] += kg * fb; acc[1] += kg * fg; acc[2] += kg * fd; }
         if (kr != 0.0) { acc[3] += kr * fb; acc[4] += kr * fg; acc[5] += kr * fd; acc[9] += kr; }
         if (ko != 0.0) { acc[6] += ko * fb; acc[7] += ko * fg; acc[8] += ko * fd; }
@@ -816,15 +831,21 @@ __global__ void __launch_bounds__(256) k_coef_d(const int32_t *__restrict__ unit
 #pragma unroll
         for (int k = 0; k < 12; ++k) o[k] = acc[k];
     }
-    if (phase == 0 && threadIdx.x < 64) {     // fused-pass channel list: any kappa != 0
+    __syncthreads();
+    if (phase == 0 && threadIdx.x < 64) {
+        // channel list of passes B and C: the median channels with alpha != 0 (every kappa
+        // channel is one of them: fa = alpha), with their (alpha, kg, kr, ko) weights
         double *w = dw + 4 * (int64_t)ub * kChannels;
         const int nc = wave_compact_channels(
-            threadIdx.x,
-            [&](int c) { return s_kap[0][c] != 0.0 || s_kap[1][c] != 0.0 || s_kap[2][c] != 0.0; },
+            threadIdx.x, [&](int c) { return s_kap[0][c] != 0.0; },
             [&](int j, int c) {
-                w[4 * j] = s_kap[0][c]; w[4 * j + 1] = s_kap[1][c]; w[4 * j + 2] = s_kap[2][c]; w[4 * j + 3] = 0.0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) w[4 * j + k] = s_kap[k][c];
             },
-            [&](int j) { w[4 * j] = w[4 * j + 1] = w[4 * j + 2] = w[4 * j + 3] = 0.0; },
+            [&](int j) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) w[4 * j + k] = 0.0;
+            },
             dlist + (int64_t)ub * kChannels);
         if (threadIdx.x == 0) dcnt[ub] = nc;
     }
@@ -901,144 +922,6 @@ __global__ void __launch_bounds__(256) k_gain_avg(const float *__restrict__ tod,
             to[o] = (sr - dG * ds[9]) / ds[10];
             oo[o] = so / ds[11];
             if (b == 0) dG_out[(int64_t)f * T + t0 + r0 + o] = dG;
-        }
-}
-
-// ------------------------------------------------------------------ fused pass C+D
-// The pass-D channel weights kappa = (kg, kr, ko) x fa do not depend on the
-// regression (k_coef_d phase 0), so ONE read of the cube serves both:
-//   per channel   part[blk][b][c] = sum_{t in block} d_ct mf_bt       (pass C)
-//   per sample    Sg_t = sum_b sum_c kg_c d_ct,  Sr_bt, So_bt          (pass D)
-// k_coef_d phase 1 then solves the regression and folds the per-band
-// constants; k_finish applies them.  Block = 256 threads (wave b = band) on a
-// 256·kJ2-sample sub-tile of a 1024-sample tile; lane owns kJ2 groups of 4 samples.
-#ifndef COMAP_KJ2
-#define COMAP_KJ2 2
-#endif
-#ifndef COMAP_RA_MINW
-#define COMAP_RA_MINW 1
-#endif
-constexpr int kJ2 = COMAP_KJ2;
-constexpr int kSub2 = kTile / (256 * kJ2);   // fused blocks per 1024-sample tile
-
-// Sum 8 per-lane values over the 64 lanes of a wave; on return lane l holds
-// the total of value (l >> 3).  Butterfly transpose: 4 + 2 + 1 exchanges halve
-// the values carried, then 3 plain xor steps finish (10 shuffles, not 8 x 6).
-__device__ __forceinline__ double wave_reduce8(const double (&v)[8], int lane)
-{
-    const int b5 = (lane >> 5) & 1, b4 = (lane >> 4) & 1, b3 = (lane >> 3) & 1;
-    double a[4], c[2];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        const double keep = b5 ? v[t + 4] : v[t];
-        const double send = b5 ? v[t] : v[t + 4];
-        a[t] = keep + __shfl_xor(send, 32, 64);
-    }
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        const double keep = b4 ? a[t + 2] : a[t];
-        const double send = b4 ? a[t] : a[t + 2];
-        c[t] = keep + __shfl_xor(send, 16, 64);
-    }
-    double r = (b3 ? c[1] : c[0]) + __shfl_xor(b3 ? c[0] : c[1], 8, 64);
-    r += __shfl_xor(r, 4, 64);
-    r += __shfl_xor(r, 2, 64);
-    r += __shfl_xor(r, 1, 64);
-    return r;
-}
-template <bool FULL>
-__device__ __forceinline__ void regress_avg_sum(const float *__restrict__ base, int64_t T, int nv0, int lane,
-                                                const int32_t *__restrict__ lst, const double *__restrict__ wl,
-                                                int cnt, const double (&mt)[4 * kJ2], double (&ag)[4 * kJ2],
-                                                double (&ar)[4 * kJ2], double (&ao)[4 * kJ2],
-                                                double *__restrict__ pp)
-{
-    for (int j8 = 0; j8 < cnt; j8 += 8) {
-        double pcs[8];
-#pragma unroll
-        for (int h = 0; h < 8; h += 4) {
-            f32x4u r[4][kJ2];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) load_raw<kJ2, FULL>(base + (int64_t)lst[j8 + h + q] * T, nv0, r[q]);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int j = j8 + h + q;
-                const double wg = wl[4 * j], wr = wl[4 * j + 1], wo = wl[4 * j + 2];   // 0 on pads
-                const bool live = j < cnt;                                            // no 0 * NaN on pads
-                double pc = 0.0;
-#pragma unroll
-                for (int g = 0; g < kJ2; ++g) {
-                    const double xs[4] = {(double)r[q][g].x, (double)r[q][g].y, (double)r[q][g].z,
-                                          (double)r[q][g].w};
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int i = 4 * g + e;
-                        const double x = live ? xs[e] : 0.0;
-                        ag[i] = fma(wg, x, ag[i]);
-                        ar[i] = fma(wr, x, ar[i]);
-                        ao[i] = fma(wo, x, ao[i]);
-                        pc = fma(x, mt[i], pc);
-                    }
-                }
-                pcs[h + q] = pc;
-            }
-        }
-        const double tot = wave_reduce8(pcs, lane);
-        const int j = j8 + (lane >> 3);
-        if ((lane & 7) == 0 && j < cnt) pp[lst[j]] = tot;
-    }
-}
-
-__global__ void __launch_bounds__(256, COMAP_RA_MINW) k_regress_avg(const float *__restrict__ tod, const int32_t *__restrict__ units,
-                                                     const int32_t *__restrict__ tiles, int64_t T,
-                                                     const int32_t *__restrict__ dlist, const int32_t *__restrict__ dcnt,
-                                                     const double *__restrict__ dw, const double *__restrict__ mf,
-                                                     double *__restrict__ part, double *__restrict__ sr_out,
-                                                     double *__restrict__ so_out, double *__restrict__ sg_out)
-{
-    __shared__ double sg[kBands][256 * kJ2];
-    const int b = uniform(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const int tile = blockIdx.x / kSub2, sub = blockIdx.x % kSub2;
-    const int u = tiles[2 * tile], toff = tiles[2 * tile + 1] + 256 * kJ2 * sub;
-    const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
-    const int r0 = toff + 4 * lane;
-    const int nv0 = n - r0;                          // valid samples from this lane's first group
-    const float *base = tod + (int64_t)(f * kBands + b) * kChannels * T + t0 + r0;
-    const int ub = u * kBands + b;
-    const int32_t *lst = dlist + (int64_t)ub * kChannels;
-    const double *wl = dw + 4 * (int64_t)ub * kChannels;
-    const int cnt = dcnt[ub];
-    double *pp = part + (int64_t)blockIdx.x * kBC + b * kChannels;
-    const double *m = mf + (int64_t)(f * kBands + b) * T + t0 + r0;
-    double mt[4 * kJ2];
-#pragma unroll
-    for (int g = 0; g < kJ2; ++g)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) mt[4 * g + e] = (256 * g + e < nv0) ? m[256 * g + e] : 0.0;
-    double ag[4 * kJ2], ar[4 * kJ2], ao[4 * kJ2];
-#pragma unroll
-    for (int i = 0; i < 4 * kJ2; ++i) ag[i] = ar[i] = ao[i] = 0.0;
-    if (n - toff >= 256 * kJ2) regress_avg_sum<true>(base, T, nv0, lane, lst, wl, cnt, mt, ag, ar, ao, pp);
-    else regress_avg_sum<false>(base, T, nv0, lane, lst, wl, cnt, mt, ag, ar, ao, pp);
-#pragma unroll
-    for (int g = 0; g < kJ2; ++g)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) sg[b][256 * g + 4 * lane + e] = ag[4 * g + e];
-    __syncthreads();
-    const int64_t rowo = (int64_t)(f * kBands + b) * T + t0 + r0;
-#pragma unroll
-    for (int g = 0; g < kJ2; ++g)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int i = 4 * g + e, o = 256 * g + e;
-            if (o >= nv0) continue;
-            sr_out[rowo + o] = ar[i];
-            so_out[rowo + o] = ao[i];
-            if (b == 0) {
-                const int tl = 256 * g + 4 * lane + e;
-                sg_out[(int64_t)f * T + t0 + r0 + o] = (sg[0][tl] + sg[1][tl]) + (sg[2][tl] + sg[3][tl]);
-            }
         }
 }
 
@@ -1250,18 +1133,9 @@ extern "C" int comap_l1_plan_create(comap_ctx *ctx, const comap_obs_desc *d, com
     for (int u = 0; u < p->U; ++u)
         for (int t = 0; t < p->units_h[4 * u + 3]; t += kTile) { tiles.push_back(u); tiles.push_back(t); }
     p->n_tiles = (int64_t)tiles.size() / 2;
-    // fused pass C+D blocks (two per tile) of unit u: [utile0[u], utile0[u+1])
-    std::vector<int32_t> utile0(p->U + 1, 0);
-    for (int64_t k = 0; k < p->n_tiles; ++k) utile0[tiles[2 * k] + 1] += kSub2;
-    for (int u = 0; u < p->U; ++u) utile0[u + 1] += utile0[u];
     const int64_t UC = (int64_t)p->U * kBC;
     int rc = 0;
-    rc |= upload(ctx, (void **)&p->utile0, utile0.data(), utile0.size() * 4);
-    rc |= dalloc(ctx, &p->part, (size_t)kSub2 * p->n_tiles * kBC);
     rc |= dalloc(ctx, &p->flag, 1);
-    rc |= dalloc(ctx, &p->blist, (size_t)p->U * kBC);
-    rc |= dalloc(ctx, &p->bcnt, (size_t)p->U * kBands);
-    rc |= dalloc(ctx, &p->bw, (size_t)p->U * kBC);
     rc |= dalloc(ctx, &p->dlist, (size_t)p->U * kBC);
     rc |= dalloc(ctx, &p->dcnt, (size_t)p->U * kBands);
     rc |= dalloc(ctx, &p->dw, 4 * (size_t)p->U * kBC);
@@ -1326,7 +1200,7 @@ extern "C" int comap_l1_plan_destroy(comap_l1_plan *p)
     void *bufs[] = {p->units, p->tiles, p->airmass, p->unit_sums, p->mom,
                     p->nan_count, p->alpha, p->nf, p->bsum, p->mb, p->mf, p->ssum, p->sdm, p->gw,
                     p->gmode, p->kap, p->dsum, p->xreg, p->dG, p->rowbad, p->ubs, p->fitsum, p->oa,
-                    p->utile0, p->part, p->flag, p->blist, p->bcnt, p->bw, p->dlist, p->dcnt, p->dw};
+                    p->flag, p->dlist, p->dcnt, p->dw};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     comap_median_plan_free(&p->med);
@@ -1539,14 +1413,7 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
     k_gather_oa<<<(UC + 255) / 256, 256, 0, st>>>(p->units, fit, p->F, p->U, cmed, p->oa);
     COMAP_LAUNCH_CHECK(ctx);
     PROF(p, KV_COEF_B, k_coef_b<<<UB, 256, 0, st>>>(p->units, p->unit_sums, p->mom, UC, p->oa, p->alpha, p->nf,
-                                                    p->bsum, p->blist, p->bcnt, p->bw));
-    COMAP_LAUNCH_CHECK(ctx);
-    PROF(p, KV_BAND_MEAN, k_band_mean<<<kSubB * p->n_tiles, 256, 0, st>>>(p->tod, p->airmass, p->units, p->tiles, p->T,
-                                                                  p->blist, p->bcnt, p->bw, p->bsum, p->mb));
-    COMAP_LAUNCH_CHECK(ctx);
-    PROF(p, KV_MEDIAN, rc = comap_median_run(ctx, &p->med));
-    if (rc) return rc;
-    PROF(p, KV_SERIES_SUMS, k_series_sums<<<UB, 256, 0, st>>>(p->units, p->airmass, p->T, p->bsum, p->mf, p->ssum));
+                                                    p->bsum));
     COMAP_LAUNCH_CHECK(ctx);
     PROF(p, KV_GAIN_WEIGHTS, k_gain_weights<<<p->F, 1024, 0, st>>>(tsys0, p->gw, p->gmode));
     COMAP_LAUNCH_CHECK(ctx);
@@ -1554,22 +1421,29 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
     auto coef_d = [&](int phase) {
         k_coef_d<<<UB, 256, 0, st>>>(p->units, p->unit_sums, p->mom, UC, p->oa, p->alpha, p->nf, p->bsum, p->ssum,
                                      p->sdm, tsys0, gain0, p->gw, p->gmode, calibrator, p->kap, p->dsum, p->xreg,
-                                     phase, p->part, p->utile0, p->flag, p->dlist, p->dcnt, p->dw);
+                                     phase, p->flag, p->dlist, p->dcnt, p->dw);
     };
-    // fused pass C+D: kappa first, one read of the cube, then the regression and the constants
+    // phase 0: the kappa weights and the channel list (no regression needed)
     PROF(p, KV_COEF_D, coef_d(0));
     COMAP_LAUNCH_CHECK(ctx);
-    PROF(p, KV_REGRESS_AVG, k_regress_avg<<<kSub2 * p->n_tiles, 256, 0, st>>>(p->tod, p->units, p->tiles, p->T,
-                                                                          p->dlist, p->dcnt, p->dw, p->mf, p->part,
-                                                                          tod_out, orig_out, p->dG));
+    // pass B: band means + every per-sample sum of the outputs in one read of the cube
+    PROF(p, KV_BAND_SUMS, k_band_sums<<<kSubB * p->n_tiles, 256, 0, st>>>(p->tod, p->airmass, p->units, p->tiles,
+                                                                        p->T, p->dlist, p->dcnt, p->dw, p->bsum,
+                                                                        p->mb, tod_out, orig_out, p->dG));
     COMAP_LAUNCH_CHECK(ctx);
+    PROF(p, KV_MEDIAN, rc = comap_median_run(ctx, &p->med));
+    if (rc) return rc;
+    PROF(p, KV_SERIES_SUMS, k_series_sums<<<UB, 256, 0, st>>>(p->units, p->airmass, p->T, p->bsum, p->mf, p->ssum));
+    COMAP_LAUNCH_CHECK(ctx);
+    // pass C: the regression sums against the median-filtered band means
+    PROF(p, KV_REGRESS, k_regress<<<UB * kRegBlocks, 256, 0, st>>>(p->tod, p->mf, p->units, p->T, p->bsum, p->dlist,
+                                                                   p->dcnt, p->sdm));
+    COMAP_LAUNCH_CHECK(ctx);
+    // phase 1: regression solve, per-band constants, kappa re-check
     PROF(p, KV_COEF_D, coef_d(1));
     COMAP_LAUNCH_CHECK(ctx);
-    // legacy separate passes C and D: exit at once unless phase 1 found a kappa that depends on the
-    // regression (a NaN regression coefficient), in which case they recompute the outputs exactly
-    const int64_t grid = (int64_t)p->U * kBands * (kChannels / (4 * kCPW));
-    PROF(p, KV_REGRESS, k_regress<<<grid, 256, 0, st>>>(p->tod, p->mf, p->units, p->T, p->bsum, p->sdm, p->flag));
-    COMAP_LAUNCH_CHECK(ctx);
+    // legacy pass D: exits at once unless phase 1 found a kappa that depends on the regression
+    // (a NaN regression coefficient), in which case it recomputes the outputs exactly
     PROF(p, KV_COEF_D, coef_d(2));
     COMAP_LAUNCH_CHECK(ctx);
     PROF(p, KV_GAIN_AVG, k_gain_avg<<<p->n_tiles, 256, 0, st>>>(p->tod, p->airmass, p->units, p->tiles, p->T, UC,
@@ -1643,6 +1517,17 @@ extern "C" int comap_l1_debug_fetch(comap_l1_plan *p, int32_t what, double *out,
     case 6: src = p->dsum; cnt = (int64_t)p->U * kBands * 16; break;
     case 7: src = p->alpha; cnt = UC; break;
     case 8: src = p->oa; cnt = 2 * UC; break;
+    case 9: {   // per (unit, band): channel-list length, median band on
+        const int UB = p->U * kBands;
+        if (n < 2 * (int64_t)UB) return comap_fail(ctx, -1, "debug buffer too small");
+        std::vector<int32_t> c(UB);
+        std::vector<double> bs(4 * (size_t)UB);
+        COMAP_CHECK(ctx, hipMemcpyAsync(c.data(), p->dcnt, 4 * (size_t)UB, hipMemcpyDeviceToHost, ctx->stream));
+        COMAP_CHECK(ctx, hipMemcpyAsync(bs.data(), p->bsum, 32 * (size_t)UB, hipMemcpyDeviceToHost, ctx->stream));
+        COMAP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+        for (int i = 0; i < UB; ++i) { out[2 * i] = c[i]; out[2 * i + 1] = bs[4 * (size_t)i + 3] > 0 ? 1.0 : 0.0; }
+        return 0;
+    }
     default: return comap_fail(ctx, -1, "unknown debug array");
     }
     if (n < cnt) return comap_fail(ctx, -1, "debug buffer too small");

@@ -233,11 +233,12 @@ class GPUObservation:
             out[:, torch.as_tensor(np.flatnonzero(big), device=self.tdev)] = 0
         return out[0], out[1], out[2]
 
-    KERNELS = ('vane', 'moments', 'atmos_fit', 'coef_b', 'band_mean', 'median', 'series_sums', 'regress',
-               'gain_weights', 'coef_d', 'gain_avg', 'scan_weights', 'regress_avg', 'finish')
-    # the HBM streaming passes: A, B and the fused C+D (regress / gain_avg are the
-    # legacy separate C and D passes, launched but idle unless a NaN regression needs them)
-    STREAMING = ('moments', 'band_mean', 'regress_avg')
+    KERNELS = ('vane', 'moments', 'atmos_fit', 'coef_b', 'band_sums', 'median', 'series_sums', 'regress',
+               'gain_weights', 'coef_d', 'gain_avg', 'scan_weights', 'unused', 'finish')
+    # the HBM streaming passes: A (per-channel moments), B (band means + every per-sample
+    # output sum) and C (regression sums); gain_avg is the legacy pass D, launched but idle
+    # unless a NaN regression coefficient needs it
+    STREAMING = ('moments', 'band_sums', 'regress')
 
     def profile(self, enable: bool = True):
         """Record HIP events around every kernel launch of this plan."""
@@ -252,11 +253,15 @@ class GPUObservation:
                 'comap_l1_profile_collect')
         return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(self.KERNELS)}
 
-    def active_channel_fraction(self) -> float:
-        """Fraction of (unit, band, channel) rows the fused pass C+D reads (nonzero kappa):
-        channels excluded from every average are skipped (k_regress_avg)."""
-        kap = self.debug(5)
-        return float(np.mean(np.any(kap != 0.0, axis=0)))
+    def pass_fractions(self) -> dict:
+        """Fraction of the cube's (unit, band, channel) rows each streaming pass reads:
+        A all; B the channel list (median channels with finite alpha); C the list of the
+        bands the median filter did not skip.  Rows are weighted by scan length."""
+        d = self.debug(9).reshape(-1, 4, 2)
+        n = self.units[:, 3].astype(np.float64)[:, None]
+        tot = float(n.sum()) * 4 * N_CHANNELS
+        return {'moments': 1.0, 'band_sums': float((d[..., 0] * n).sum()) / tot,
+                'regress': float((d[..., 0] * d[..., 1] * n).sum()) / tot}
 
     def scan_samples(self) -> int:
         """Sum over units of the scan lengths (samples each streaming pass visits per channel)."""
@@ -264,10 +269,12 @@ class GPUObservation:
 
     def debug(self, what: int):
         """Internal arrays (host f64): 0 rms [U,4,1024]; 1 mf [F,4,T]; 2 dG [F,T]; 3 x [U,4,1024,2]; 4 mb;
-        5 kappa [3,U,4,1024]; 6 pass-D sums [U,4,16]; 7 alpha [U,4,1024]; 8 atmosphere (o, a) [U,4,1024,2]."""
+        5 kappa [3,U,4,1024]; 6 pass-D sums [U,4,16]; 7 alpha [U,4,1024]; 8 atmosphere (o, a) [U,4,1024,2];
+        9 per (unit, band): channel-list length, median band on [U,4,2]."""
         U = self.units.shape[0]
         shapes = {0: (U, 4, 1024), 1: (self.F, 4, self.T), 2: (self.F, self.T), 3: (U, 4, 1024, 2),
-                  4: (self.F, 4, self.T), 5: (3, U, 4, 1024), 6: (U, 4, 16), 7: (U, 4, 1024), 8: (U, 4, 1024, 2)}
+                  4: (self.F, 4, self.T), 5: (3, U, 4, 1024), 6: (U, 4, 16), 7: (U, 4, 1024), 8: (U, 4, 1024, 2),
+                  9: (U, 4, 2)}
         out = np.empty(shapes[what])
         self._bind()
         N.check(N.lib().comap_l1_debug_fetch(self.plan, what, N.hptr(out, ctypes.c_double), out.size), self.ctx,
