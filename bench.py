@@ -45,6 +45,7 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-destriper', action='store_true')
     ap.add_argument('--destriper-iters', type=int, default=100)
+    ap.add_argument('--c5-obs', type=int, default=8, help='observations per GPU in the C5 destriper leg (0: skip)')
     ap.add_argument('--check', action='store_true', help='compare one unit against the CPU oracle')
     return ap.parse_args()
 
@@ -153,6 +154,49 @@ def destriper_leg(level2, data, niter, device):
             'n_offsets': int(tod.numel() // 50), 'setup_s': setup, 'nnz': prob.nnz()}
 
 
+def destriper_c5_leg(n_obs, niter, device, world, rank):
+    """C5: the destriper on n_obs synthetic observations' Level-2 TOD
+    (19 feeds x 180,000 samples each, one band, L = 50, 480x480 1' CAR map) per GPU,
+    weak-scaled: every rank holds its own observations; with several ranks the map
+    numerator and the CG scalars are summed over RCCL every iteration.  Roofline on
+    SURVEY §8(d)'s algorithmic bytes: 24 B per sample + 80 B per offset per iteration."""
+    import torch
+    import torch.distributed as dist
+    from comapreduce_amd import synthetic
+    from comapreduce_amd.mapmaking import destriper as D
+    L, npix = 50, 480 * 480
+    pix, tod, w = synthetic.destriper_inputs_device(n_obs, offset_length=L, device=device, seed=1000 + rank)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    prob = D.DeviceDestriper(pix, tod, w, L, npix, device=device)
+    torch.cuda.synchronize()
+    setup = time.perf_counter() - t0
+    prob.solve(threshold=0.0, niter=3)   # warm (graph capture, RCCL communicators)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = prob.solve(threshold=0.0, niter=niter)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([dt], device='cuda', dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        dt = float(e.item())
+    N = int(tod.numel())
+    NO = N // L
+    it = max(res['iters'], 1)
+    algo = 24 * N + 80 * NO
+    ms = dt / it * 1e3
+    return {'config': f'C5: {n_obs} obs x 19 feeds x 180000 samples per GPU, L={L}, 480x480 CAR, '
+                      f'{niter} CG iterations (no early exit)',
+            'cg_iters_per_s': it / dt, 'ms_per_iter': ms, 'iters': res['iters'],
+            'n_samples_per_gpu': N, 'n_offsets_per_gpu': NO, 'nnz': prob.nnz(), 'setup_s': setup,
+            'algo_bytes_per_iter_per_gpu': algo, 'achieved_GBs_per_gpu': algo / (ms * 1e-3) / 1e9,
+            'roofline_frac': algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+
+
 def main():
     args = parse()
     import torch
@@ -203,6 +247,10 @@ def main():
             dist.all_reduce(v, op=dist.ReduceOp.MIN)
             dstr['cg_iters_per_s_min_over_ranks'] = float(v.item())
 
+    c5 = None
+    if not args.no_destriper and args.c5_obs > 0:
+        c5 = destriper_c5_leg(args.c5_obs, args.destriper_iters, device, world, rank)
+
     if rank == 0:
         value = world * samp_ch * args.steps / elapsed
         scan_sc = obs.scan_samples() * 4096
@@ -213,7 +261,8 @@ def main():
         pass_bytes = {k: ALGO_BYTES_PER_SAMPCH_PASS * scan_sc * frac[k] for k in obs.STREAMING}
         dom = max(stream, key=lambda k: stream[k][0])
         ms_avg = stream[dom][0] / max(stream[dom][1], 1)
-        algo_bytes = pass_bytes[dom]
+        # passes B and C run as one launch per unit group (pipelined with the median)
+        algo_bytes = pass_bytes[dom] * args.steps / max(stream[dom][1], 1)
         achieved = algo_bytes / (ms_avg * 1e-3) / 1e9
         design_bytes = sum(pass_bytes.values())
         traffic = None
@@ -250,11 +299,14 @@ def main():
             'kernel_ms_per_step': {k: v[0] / args.steps for k, v in prof.items()},
             'host_stage_ms_per_step': {k: v / args.steps for k, v in host_ms.items()},
             'host_vane_search_ms': getattr(obs, 'last_vane_search_ms', None),
-            'pass_GBs': {k: pass_bytes[k] / (stream[k][0] / max(stream[k][1], 1) * 1e-3) / 1e9
+            'pass_GBs': {k: pass_bytes[k] / (stream[k][0] / args.steps * 1e-3) / 1e9
                          for k in obs.STREAMING if stream[k][1] > 0},
+            'launches_per_step': {k: stream[k][1] / args.steps for k in obs.STREAMING},
         }
         if dstr is not None:
             line['destriper'] = dstr
+        if c5 is not None:
+            line['destriper_c5'] = c5
         if check is not None:
             line['check'] = check
         if not args.no_cpu_baseline and world == 1:

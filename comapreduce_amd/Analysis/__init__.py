@@ -4,5 +4,6 @@ run_average.py:46-48 does with ``comancpipeline.Analysis``."""
 from ..pipeline.running import Runner, PipelineFunction, set_logging  # noqa: F401
 from ..pipeline.datahandling import HDF5Data, COMAPLevel1, COMAPLevel2, RepointEdges  # noqa: F401
 from ..stages.level1 import (MeasureSystemTemperature, AtmosphereRemoval,  # noqa: F401
-                             Level1AveragingGainCorrection, CheckLevel1File, AssignLevel1Data)
+                             Level1AveragingGainCorrection, Level1Averaging, CheckLevel1File,
+                             AssignLevel1Data)
 from ..stages.statistics import Spikes  # noqa: F401,E402

@@ -47,6 +47,7 @@ _SIGS = {
     'comap_l1_atmosphere': (c_int, [c_void_p, P_int32, c_int32, c_void_p]),
     'comap_l1_average': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
     'comap_l1_debug_fetch': (c_int, [c_void_p, c_int32, P_double, c_int64]),
+    'comap_l1_channel_bin': (c_int, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     'comap_l1_profile': (c_int, [c_void_p, c_int32]),
     'comap_l1_profile_collect': (c_int, [c_void_p, P_double, P_int64, c_int32]),
     'comap_spikes': (c_int, [c_void_p, c_void_p, c_int32, c_int64, P_int64, c_int32, c_int32, c_int32, c_double,

@@ -58,8 +58,19 @@ struct MedJob {
     const double *gate; // optional: skip the job when *gate <= 0 (band count N_b)
 };
 
-// Sliding-median plan: jobs, per-job sorted-key segments, chunk table, buffers.
+// A k_med_slide work item: outputs [o0, o1) of one job.
+struct SlideSeg {
+    int32_t job, pad_;
+    int64_t o0, o1;
+};
+
+// Sliding-median plan.  slide: k_med_slide over `segs` (windows up to ~12k);
+// otherwise the global-sort path (jobs, per-job sorted-key segments, chunk table, buffers).
 struct MedPlan {
+    bool slide = false;
+    SlideSeg *segs = nullptr;    // dev [nsegs]
+    int32_t nsegs = 0;
+    int32_t kper = 0;
     int32_t w = 0, lc = 0, nwmax = 0, njobs = 0;
     int32_t nitems = 0;
     int64_t nchunks = 0;
@@ -75,7 +86,8 @@ struct MedPlan {
 
 int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jobs, int32_t w);
 void comap_median_plan_free(MedPlan *mp);
-int comap_median_run(comap_ctx *ctx, MedPlan *mp);
+int comap_median_run(comap_ctx *ctx, MedPlan *mp, hipStream_t stream);
+inline int comap_median_run(comap_ctx *ctx, MedPlan *mp) { return comap_median_run(ctx, mp, ctx->stream); }
 
 // ------------------------------------------------------------------ L1 plan
 struct comap_l1_plan {
@@ -88,8 +100,16 @@ struct comap_l1_plan {
     int32_t *units = nullptr;          // dev [U][4]
     int32_t *tiles = nullptr;          // dev [NT][2] (unit, t_off)
     int64_t n_tiles = 0;
-    // sliding median: one job per (unit, band)
-    MedPlan med;
+    // pass B -> median -> pass C software pipeline over unit groups (comap_l1_average):
+    // group g = units [grp_u0[g], grp_u0[g+1]) = tiles [grp_tile0[g], grp_tile0[g+1]);
+    // its sliding medians (one job per (unit, band)) run on the side stream
+    static constexpr int kMaxGroups = 4;
+    int32_t ngroups = 0;
+    int32_t grp_u0[kMaxGroups + 1] = {0};
+    int64_t grp_tile0[kMaxGroups + 1] = {0};
+    MedPlan medg[kMaxGroups];
+    hipStream_t side = nullptr;
+    hipEvent_t ev_b[kMaxGroups] = {}, ev_m[kMaxGroups] = {};
     // device workspaces
     double *airmass = nullptr;         // [F][T]
     double *unit_sums = nullptr;       // [U][8]: n, SA, SAA, Sv, Svv, N4

@@ -42,13 +42,29 @@ struct comap_destriper {
     // sample-level maps (local)
     double *h = nullptr, *hits = nullptr, *nnum = nullptr;   // [npix]
     // reduction scratch
-    double *part = nullptr;    // [kRedBlocks]
-    double *scal = nullptr;    // [16] device scalars
+    double *part = nullptr;    // [kPartMax] block partials
+    double *scal = nullptr;    // [16] device scalars: rr0, rr, pq, rr_new, threshold
+    // device-resident CG of comap_destripe_solve (fixed pointers: graph-replayable)
+    double *cg = nullptr;          // [4 NO + npix]: x, r, p, q | num
+    int32_t *flags = nullptr;      // [2]: stop, iterations
+    int32_t *flags_host = nullptr; // pinned [2]
+    double *thr_host = nullptr;    // pinned [1]
+    hipStream_t cs = nullptr;      // CG stream (graph capture needs a non-default stream)
+    hipEvent_t ev = nullptr;
+    hipGraphExec_t batch = nullptr;   // kCgBatch iterations
 };
 
 namespace {
 
 constexpr int kRedBlocks = 256;
+constexpr int kPartMax = 8192;     // >= every reduction grid below
+constexpr int kBinLanes = 16;      // lanes per pixel row in k_ds_bin
+constexpr int kCgBatch = 16;       // CG iterations per replayed graph (one host check per batch)
+
+// Device-side CG stop flag (comap_destripe_solve): once set, every kernel of the
+// remaining enqueued iterations returns at once, so iterations run as replayed
+// hipGraph batches with one host round trip per batch.
+__device__ __forceinline__ bool cg_done(const int32_t *done) { return done && *done; }
 
 __device__ __forceinline__ double wave_sum(double v)
 {
@@ -57,8 +73,10 @@ __device__ __forceinline__ double wave_sum(double v)
     return v;
 }
 
-// One wave per offset (L <= 64): unique pixels in first-occurrence order,
-// weights summed in sample order.  pass 0 counts, pass 1 fills.
+// One wave per offset: lane l owns samples l, l + 64, ... (K per lane, L <= 64 K).
+// Unique pixels in first-occurrence order, weights summed in sample order.
+// pass 0 counts (and sums ws = sum w, tw = sum w tod), pass 1 fills.
+template <int K>
 __global__ void __launch_bounds__(256) k_ds_entries(const int32_t *__restrict__ pix, const double *__restrict__ w,
                                                     const double *__restrict__ tod, int64_t NO, int L, int pass,
                                                     int64_t *__restrict__ cnt, const int64_t *__restrict__ orow,
@@ -68,36 +86,70 @@ __global__ void __launch_bounds__(256) k_ds_entries(const int32_t *__restrict__ 
     const int lane = threadIdx.x & 63;
     const int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (o >= NO) return;
-    const int64_t i = o * L + lane;
-    const bool in = lane < L;
-    const int32_t p = in ? pix[i] : -2;
-    const double wi = in ? w[i] : 0.0;
-    // first occurrence of p among lanes < lane, and the in-order group sum
-    bool first = in;
-    double gsum = 0.0;
-    for (int j = 0; j < L; ++j) {
-        const int32_t pj = __shfl(p, j, 64);
-        const double wj = __shfl(wi, j, 64);
-        if (pj == p) {
-            if (j < lane) first = false;
-            gsum += wj;
-        }
+    int32_t p[K];
+    double wi[K], gsum[K];
+    bool first[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int sidx = lane + 64 * k;
+        const bool in = sidx < L;
+        p[k] = in ? pix[o * L + sidx] : -2;
+        wi[k] = in ? w[o * L + sidx] : 0.0;
+        first[k] = in;
+        gsum[k] = 0.0;
     }
-    const bool keep = first && gsum != 0.0;
-    const unsigned long long m = __ballot(keep);
+    // every sample in order (chunk kk, lane j): first occurrence and the in-order group sum
+#pragma unroll
+    for (int kk = 0; kk < K; ++kk)
+        for (int j = 0; j < 64; ++j) {
+            const int32_t pj = __shfl(p[kk], j, 64);
+            const double wj = __shfl(wi[kk], j, 64);
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if (pj == p[k]) {
+                    if (j + 64 * kk < lane + 64 * k) first[k] = false;
+                    gsum[k] += wj;
+                }
+        }
+    unsigned long long m[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) m[k] = __ballot(first[k] && gsum[k] != 0.0);
     if (pass == 0) {
-        if (lane == 0) cnt[o] = __popcll(m);
-        const double s = wave_sum(wi);
-        const double st = wave_sum(in ? wi * tod[i] : 0.0);
-        if (lane == 0) { ws[o] = s; tw[o] = st; }
+        int64_t c = 0;
+        double sw = 0.0, st = 0.0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            c += __popcll(m[k]);
+            sw += wi[k];
+            if (lane + 64 * k < L) st += wi[k] * tod[o * L + lane + 64 * k];
+        }
+        sw = wave_sum(sw);
+        st = wave_sum(st);
+        if (lane == 0) { cnt[o] = c; ws[o] = sw; tw[o] = st; }
         return;
     }
-    if (keep) {
-        const int rank = __popcll(m & ((1ull << lane) - 1ull));
-        const int64_t e = orow[o] + rank;
-        opix[e] = p;
-        ow[e] = gsum;
+    int base = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        if ((m[k] >> lane) & 1ull) {
+            const int64_t e = orow[o] + base + __popcll(m[k] & ((1ull << lane) - 1ull));
+            opix[e] = p[k];
+            ow[e] = gsum[k];
+        }
+        base += __popcll(m[k]);
     }
+}
+
+static void launch_entries(int L, unsigned blocks, hipStream_t st, const int32_t *pix, const double *w,
+                           const double *tod, int64_t NO, int pass, int64_t *cnt, const int64_t *orow,
+                           int32_t *opix, double *ow, double *ws, double *tw)
+{
+    if (L <= 64)
+        k_ds_entries<1><<<blocks, 256, 0, st>>>(pix, w, tod, NO, L, pass, cnt, orow, opix, ow, ws, tw);
+    else if (L <= 128)
+        k_ds_entries<2><<<blocks, 256, 0, st>>>(pix, w, tod, NO, L, pass, cnt, orow, opix, ow, ws, tw);
+    else
+        k_ds_entries<4><<<blocks, 256, 0, st>>>(pix, w, tod, NO, L, pass, cnt, orow, opix, ow, ws, tw);
 }
 
 // keys for the pixel-major transpose: pixel of each offset-major entry (npix for off-map)
@@ -173,15 +225,24 @@ __global__ void k_sample_maps(const int32_t *__restrict__ skey, const int32_t *_
     }
 }
 
-// num_p = sum_e s_e x_o(e)   (mode 0); mode 1: num = nnum - W x (final destriped numerator)
+// num_p = sum_e s_e x_o(e)   (mode 0); mode 1: num = nnum - W x (final destriped numerator).
+// kBinLanes lanes per pixel row (rows hold 0 .. thousands of entries): lane-strided, then a
+// kBinLanes-lane reduction.
 __global__ void __launch_bounds__(256) k_ds_bin(const int64_t *__restrict__ prow, const int32_t *__restrict__ poff,
                                                 const double *__restrict__ pw, const double *__restrict__ x,
-                                                int64_t npix, const double *__restrict__ base, double *__restrict__ num)
+                                                int64_t npix, const double *__restrict__ base, double *__restrict__ num,
+                                                const int32_t *__restrict__ done)
 {
-    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x) {
+    if (cg_done(done)) return;
+    const int sub = threadIdx.x & (kBinLanes - 1);
+    const int64_t step = (int64_t)gridDim.x * blockDim.x / kBinLanes;
+    for (int64_t p = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kBinLanes; p < npix; p += step) {
         double s = 0.0;
-        for (int64_t k = prow[p]; k < prow[p + 1]; ++k) s = fma(pw[k], x[poff[k]], s);
-        num[p] = base ? base[p] - s : s;
+        const int64_t e1 = prow[p + 1];
+        for (int64_t k = prow[p] + sub; k < e1; k += kBinLanes) s = fma(pw[k], x[poff[k]], s);
+#pragma unroll
+        for (int o = kBinLanes / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, kBinLanes);
+        if (sub == 0) num[p] = base ? base[p] - s : s;
     }
 }
 
@@ -191,31 +252,34 @@ __device__ __forceinline__ double map_value(const double *num, const double *h, 
     return hv != 0.0 ? num[q] / hv : num[q];
 }
 
-// y_o = ws_o x_o - sum_e s_e m_p(e)  (x == NULL: y_o = tw_o - ..., the b vector)
-// block partials of y.x (when dot_part != NULL)
+// y_o = ws_o x_o - sum_e s_e m_p(e)  (x == NULL: y_o = tw_o - ..., the b vector).
+// One wave per offset: lanes over its entries (coalesced entry reads, map gathers),
+// one wave reduction; block partials of y.x (when dot_part != NULL).
 __global__ void __launch_bounds__(256) k_ds_project(const int64_t *__restrict__ orow, const int32_t *__restrict__ opix,
                                                     const double *__restrict__ ow, const double *__restrict__ ws,
                                                     const double *__restrict__ tw, const double *__restrict__ x,
                                                     const double *__restrict__ num, const double *__restrict__ h,
                                                     int64_t NO, int64_t npix, double *__restrict__ y,
-                                                    double *__restrict__ dot_part)
+                                                    double *__restrict__ dot_part, const int32_t *__restrict__ done)
 {
     __shared__ double red[4];
+    if (cg_done(done)) return;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     double acc = 0.0;
-    for (int64_t o = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; o < NO; o += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t o = (int64_t)blockIdx.x * 4 + wid; o < NO; o += (int64_t)gridDim.x * 4) {
         double g = 0.0;
-        for (int64_t e = orow[o]; e < orow[o + 1]; ++e) {
+        const int64_t e1 = orow[o + 1];
+        for (int64_t e = orow[o] + lane; e < e1; e += 64) {
             const int32_t p = opix[e];
-            const int64_t q = (p >= 0) ? p : npix - 1;   // m[-1]
-            g = fma(ow[e], map_value(num, h, q), g);
+            g = fma(ow[e], map_value(num, h, p >= 0 ? p : npix - 1), g);   // m[-1] for off-map samples
         }
+        g = wave_sum(g);
         const double v = (x ? ws[o] * x[o] : tw[o]) - g;
-        y[o] = v;
-        if (dot_part) acc = fma(v, x[o], acc);
+        if (lane == 0) y[o] = v;
+        if (dot_part) acc = fma(v, x[o], acc);      // v is wave-uniform: every lane holds the same acc
     }
     if (dot_part) {
-        acc = wave_sum(acc);
-        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+        if (lane == 0) red[wid] = acc;
         __syncthreads();
         if (threadIdx.x == 0) dot_part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
     }
@@ -234,9 +298,11 @@ __global__ void __launch_bounds__(256) k_dot_part(const double *__restrict__ a, 
     if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-__global__ void __launch_bounds__(256) k_dot_final(const double *__restrict__ part, int n, double *__restrict__ out)
+__global__ void __launch_bounds__(256) k_dot_final(const double *__restrict__ part, int n, double *__restrict__ out,
+                                                   const int32_t *__restrict__ done)
 {
     __shared__ double red[4];
+    if (cg_done(done)) return;
     double acc = 0.0;
     for (int i = threadIdx.x; i < n; i += blockDim.x) acc += part[i];
     acc = wave_sum(acc);
@@ -249,9 +315,10 @@ __global__ void __launch_bounds__(256) k_dot_final(const double *__restrict__ pa
 __global__ void __launch_bounds__(256) k_cg_update(const double *__restrict__ rr, const double *__restrict__ pq,
                                                    double *__restrict__ x, double *__restrict__ r,
                                                    const double *__restrict__ p, const double *__restrict__ q,
-                                                   int64_t n, double *__restrict__ part)
+                                                   int64_t n, double *__restrict__ part, const int32_t *__restrict__ done)
 {
     __shared__ double red[4];
+    if (cg_done(done)) return;
     const double a = rr[0] / pq[0];
     double acc = 0.0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -267,11 +334,24 @@ __global__ void __launch_bounds__(256) k_cg_update(const double *__restrict__ rr
 }
 
 __global__ void k_cg_direction(const double *__restrict__ rr_new, const double *__restrict__ rr, double *__restrict__ p,
-                               const double *__restrict__ r, int64_t n)
+                               const double *__restrict__ r, int64_t n, const int32_t *__restrict__ done)
 {
+    if (cg_done(done)) return;
     const double beta = rr_new[0] / rr[0];
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         p[i] = r[i] + beta * p[i];
+}
+
+// End of one CG iteration (Destriper.py:136-152): rr = rr_new, count it, stop when
+// delta = rr_new / rr0 is NaN or below the threshold (scal[4]).
+__global__ void k_cg_check(double *__restrict__ scal, int32_t *__restrict__ flags)
+{
+    if (threadIdx.x != 0 || flags[0]) return;
+    const double rrn = scal[3];
+    scal[1] = rrn;
+    flags[1] += 1;
+    const double delta = rrn / scal[0];
+    if (isnan(delta) || delta < scal[4]) flags[0] = 1;
 }
 
 __global__ void k_div_map(const double *__restrict__ num, const double *__restrict__ h, int64_t npix,
@@ -282,6 +362,7 @@ __global__ void k_div_map(const double *__restrict__ num, const double *__restri
 }
 
 inline unsigned grid_for(int64_t n, int64_t cap = 4096) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, cap)); }
+inline unsigned project_grid(int64_t NO) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((NO + 3) / 4, kPartMax)); }
 
 template <typename T>
 int dalloc(comap_ctx *ctx, T **p, size_t n)
@@ -295,7 +376,7 @@ int dot(comap_destriper *d, const double *a, const double *b, double *out)
     comap_ctx *ctx = d->ctx;
     k_dot_part<<<kRedBlocks, 256, 0, ctx->stream>>>(a, b, d->NO, d->part);
     COMAP_LAUNCH_CHECK(ctx);
-    k_dot_final<<<1, 256, 0, ctx->stream>>>(d->part, kRedBlocks, out);
+    k_dot_final<<<1, 256, 0, ctx->stream>>>(d->part, kRedBlocks, out, nullptr);
     COMAP_LAUNCH_CHECK(ctx);
     return 0;
 }
@@ -306,7 +387,7 @@ extern "C" int comap_destripe_create(comap_ctx *ctx, const int32_t *pix, const d
                                      int64_t N, int32_t L, int64_t npix, comap_destriper **out)
 {
     if (!ctx || !pix || !tod || !w || !out) return -1;
-    if (L < 1 || L > 64) return comap_fail(ctx, -1, "offset_length must be in [1, 64]");
+    if (L < 1 || L > 256) return comap_fail(ctx, -1, "offset_length must be in [1, 256]");
     if (N <= 0 || N % L) return comap_fail(ctx, -1, "n_samples must be a positive multiple of offset_length");
     if (npix <= 0 || npix >= (1ll << 31) - 1 || N >= (1ll << 31)) return comap_fail(ctx, -1, "size limits exceeded");
     hipStream_t st = ctx->stream;
@@ -320,14 +401,14 @@ extern "C" int comap_destripe_create(comap_ctx *ctx, const int32_t *pix, const d
     rc |= dalloc(ctx, &d->h, npix);
     rc |= dalloc(ctx, &d->hits, npix);
     rc |= dalloc(ctx, &d->nnum, npix);
-    rc |= dalloc(ctx, &d->part, kRedBlocks);
+    rc |= dalloc(ctx, &d->part, kPartMax);
     rc |= dalloc(ctx, &d->scal, 16);
     if (rc) { comap_destripe_destroy(d); return -2; }
     // ---- offset-major entries
     int64_t *cnt = nullptr;
     if (dalloc(ctx, &cnt, d->NO + 1)) { comap_destripe_destroy(d); return -2; }
     const unsigned gblocks = (unsigned)((d->NO + 3) / 4);
-    k_ds_entries<<<gblocks, 256, 0, st>>>(pix, w, tod, d->NO, L, 0, cnt, nullptr, nullptr, nullptr, d->ws, d->tw);
+    launch_entries(L, gblocks, st, pix, w, tod, d->NO, 0, cnt, nullptr, nullptr, nullptr, d->ws, d->tw);
     COMAP_LAUNCH_CHECK(ctx);
     size_t tb = 0;
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, d->orow, (int)(d->NO + 1), st);
@@ -342,7 +423,7 @@ extern "C" int comap_destripe_create(comap_ctx *ctx, const int32_t *pix, const d
     rc |= dalloc(ctx, &d->opix, d->nnz);
     rc |= dalloc(ctx, &d->ow, d->nnz);
     if (rc) { comap_destripe_destroy(d); return -2; }
-    k_ds_entries<<<gblocks, 256, 0, st>>>(pix, w, tod, d->NO, L, 1, nullptr, d->orow, d->opix, d->ow, nullptr, nullptr);
+    launch_entries(L, gblocks, st, pix, w, tod, d->NO, 1, nullptr, d->orow, d->opix, d->ow, nullptr, nullptr);
     COMAP_LAUNCH_CHECK(ctx);
     // ---- pixel-major transpose (stable radix sort keeps offset order within a pixel)
     const int64_t sortn = std::max<int64_t>(d->nnz, N);
@@ -383,9 +464,16 @@ extern "C" int comap_destripe_create(comap_ctx *ctx, const int32_t *pix, const d
 extern "C" int comap_destripe_destroy(comap_destriper *d)
 {
     if (!d) return 0;
-    void *b[] = {d->orow, d->opix, d->ow, d->ws, d->tw, d->prow, d->poff, d->pw, d->h, d->hits, d->nnum, d->part, d->scal};
+    if (d->cs) (void)hipStreamSynchronize(d->cs);
+    void *b[] = {d->orow, d->opix, d->ow, d->ws, d->tw, d->prow, d->poff, d->pw, d->h, d->hits, d->nnum, d->part, d->scal,
+                 d->cg, d->flags};
     for (void *p : b)
         if (p) (void)hipFree(p);
+    if (d->flags_host) (void)hipHostFree(d->flags_host);
+    if (d->thr_host) (void)hipHostFree(d->thr_host);
+    if (d->batch) (void)hipGraphExecDestroy(d->batch);
+    if (d->ev) (void)hipEventDestroy(d->ev);
+    if (d->cs) (void)hipStreamDestroy(d->cs);
     delete d;
     return 0;
 }
@@ -415,8 +503,8 @@ extern "C" int comap_destripe_bin(comap_destriper *d, const double *x, int32_t m
 {
     if (!d || !x || !num) return -1;
     comap_ctx *ctx = d->ctx;
-    k_ds_bin<<<grid_for(d->npix), 256, 0, ctx->stream>>>(d->prow, d->poff, d->pw, x, d->npix,
-                                                          mode == 1 ? d->nnum : nullptr, num);
+    k_ds_bin<<<grid_for(d->npix * kBinLanes), 256, 0, ctx->stream>>>(d->prow, d->poff, d->pw, x, d->npix,
+                                                                      mode == 1 ? d->nnum : nullptr, num, nullptr);
     COMAP_LAUNCH_CHECK(ctx);
     return 0;
 }
@@ -428,11 +516,12 @@ extern "C" int comap_destripe_project(comap_destriper *d, const double *x, const
     comap_ctx *ctx = d->ctx;
     const double *hh = h ? h : d->h;
     const bool want = dot_out && x;
-    k_ds_project<<<kRedBlocks, 256, 0, ctx->stream>>>(d->orow, d->opix, d->ow, d->ws, d->tw, x, num, hh, d->NO,
-                                                      d->npix, y, want ? d->part : nullptr);
+    const unsigned pg = project_grid(d->NO);
+    k_ds_project<<<pg, 256, 0, ctx->stream>>>(d->orow, d->opix, d->ow, d->ws, d->tw, x, num, hh, d->NO, d->npix, y,
+                                              want ? d->part : nullptr, nullptr);
     COMAP_LAUNCH_CHECK(ctx);
     if (want) {
-        k_dot_final<<<1, 256, 0, ctx->stream>>>(d->part, kRedBlocks, dot_out);
+        k_dot_final<<<1, 256, 0, ctx->stream>>>(d->part, (int)pg, dot_out, nullptr);
         COMAP_LAUNCH_CHECK(ctx);
     }
     return 0;
@@ -449,9 +538,9 @@ extern "C" int comap_destripe_cg_update(comap_destriper *d, const double *rr, co
 {
     if (!d) return -1;
     comap_ctx *ctx = d->ctx;
-    k_cg_update<<<kRedBlocks, 256, 0, ctx->stream>>>(rr, pq, x, r, p, q, d->NO, d->part);
+    k_cg_update<<<kRedBlocks, 256, 0, ctx->stream>>>(rr, pq, x, r, p, q, d->NO, d->part, nullptr);
     COMAP_LAUNCH_CHECK(ctx);
-    k_dot_final<<<1, 256, 0, ctx->stream>>>(d->part, kRedBlocks, rr_new);
+    k_dot_final<<<1, 256, 0, ctx->stream>>>(d->part, kRedBlocks, rr_new, nullptr);
     COMAP_LAUNCH_CHECK(ctx);
     return 0;
 }
@@ -461,7 +550,7 @@ extern "C" int comap_destripe_cg_direction(comap_destriper *d, const double *rr_
 {
     if (!d) return -1;
     comap_ctx *ctx = d->ctx;
-    k_cg_direction<<<grid_for(d->NO), 256, 0, ctx->stream>>>(rr_new, rr, p, r, d->NO);
+    k_cg_direction<<<grid_for(d->NO), 256, 0, ctx->stream>>>(rr_new, rr, p, r, d->NO, nullptr);
     COMAP_LAUNCH_CHECK(ctx);
     return 0;
 }
@@ -475,51 +564,100 @@ extern "C" int comap_destripe_div_map(comap_destriper *d, const double *num, con
     return 0;
 }
 
-// Single-rank CG (Destriper.py:85-152 with p == pb, r == rb: one matvec per
-// iteration) followed by the final maps of destriper_iteration (:419-451).
+// ---------------------------------------------------------------- device-resident CG
+// One CG iteration (Destriper.py:85-152 with p == pb, r == rb) on the problem's own
+// vectors; every kernel returns at once after k_cg_check has set the stop flag.
+static void enqueue_iteration(comap_destriper *d, hipStream_t st)
+{
+    const int64_t NO = d->NO, np = d->npix;
+    double *x = d->cg, *r = x + NO, *p = r + NO, *q = p + NO, *num = q + NO;
+    double *rr = d->scal + 1, *pq = d->scal + 2, *rrn = d->scal + 3;
+    const int32_t *done = d->flags;
+    const unsigned pg = project_grid(NO);
+    k_ds_bin<<<grid_for(np * kBinLanes), 256, 0, st>>>(d->prow, d->poff, d->pw, p, np, nullptr, num, done);
+    k_ds_project<<<pg, 256, 0, st>>>(d->orow, d->opix, d->ow, d->ws, d->tw, p, num, d->h, NO, np, q, d->part, done);
+    k_dot_final<<<1, 256, 0, st>>>(d->part, (int)pg, pq, done);
+    k_cg_update<<<kRedBlocks, 256, 0, st>>>(rr, pq, x, r, p, q, NO, d->part, done);
+    k_dot_final<<<1, 256, 0, st>>>(d->part, kRedBlocks, rrn, done);
+    k_cg_direction<<<grid_for(NO), 256, 0, st>>>(rrn, rr, p, r, NO, done);
+    k_cg_check<<<1, 64, 0, st>>>(d->scal, d->flags);
+}
+
+// CG state, stream and the kCgBatch-iteration graph, created on first use.
+static int cg_setup(comap_destriper *d)
+{
+    if (d->batch) return 0;
+    comap_ctx *ctx = d->ctx;
+    if (!d->cg && (dalloc(ctx, &d->cg, 4 * (size_t)d->NO + (size_t)d->npix) || dalloc(ctx, &d->flags, 2))) return -2;
+    if (!d->flags_host) COMAP_CHECK(ctx, hipHostMalloc((void **)&d->flags_host, 8, hipHostMallocDefault));
+    if (!d->thr_host) COMAP_CHECK(ctx, hipHostMalloc((void **)&d->thr_host, 8, hipHostMallocDefault));
+    if (!d->cs) COMAP_CHECK(ctx, hipStreamCreateWithFlags(&d->cs, hipStreamNonBlocking));
+    if (!d->ev) COMAP_CHECK(ctx, hipEventCreateWithFlags(&d->ev, hipEventDisableTiming));
+    hipGraph_t g = nullptr;
+    COMAP_CHECK(ctx, hipStreamBeginCapture(d->cs, hipStreamCaptureModeThreadLocal));
+    for (int i = 0; i < kCgBatch; ++i) enqueue_iteration(d, d->cs);
+    COMAP_CHECK(ctx, hipStreamEndCapture(d->cs, &g));
+    const hipError_t e = hipGraphInstantiate(&d->batch, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    COMAP_CHECK(ctx, e);
+    return 0;
+}
+
+// Single-rank destriper_iteration: CG (one matvec per iteration) to threshold /
+// niter, then the final maps (:419-451).  Iterations are queued kCgBatch at a
+// time as one graph launch; a device-side stop flag makes the iterations after
+// convergence no-ops, so the iterates and the count equal a per-iteration loop's.
 extern "C" int comap_destripe_solve(comap_destriper *d, double threshold, int32_t niter, double *x, double *map,
                                     double *naive, double *weight, double *hits, int32_t *iters_out)
 {
     if (!d || !x || niter < 0) return -1;
     comap_ctx *ctx = d->ctx;
-    hipStream_t st = ctx->stream;
+    int rc = cg_setup(d);
+    if (rc) return rc;
+    hipStream_t st = d->cs;
     const int64_t NO = d->NO, np = d->npix;
-    double *buf = nullptr;
-    if (dalloc(ctx, &buf, 3 * (size_t)NO + (size_t)np)) return -2;
-    double *r = buf, *p = buf + NO, *q = buf + 2 * NO, *num = buf + 3 * NO;
-    double *rr0 = d->scal, *rr = d->scal + 1, *pq = d->scal + 2, *rrn = d->scal + 3;
-    int rc = 0;
-    COMAP_CHECK(ctx, hipMemsetAsync(x, 0, 8 * NO, st));
-    // b = op_Ax(tod, extend=False); r = p = b (x0 = 0)
-    rc |= comap_destripe_project(d, nullptr, d->nnum, d->h, r, nullptr);
+    double *cx = d->cg, *r = cx + NO, *p = r + NO, *num = p + 2 * NO;
+    // inputs were produced on the caller's stream
+    COMAP_CHECK(ctx, hipEventRecord(d->ev, ctx->stream));
+    COMAP_CHECK(ctx, hipStreamWaitEvent(st, d->ev, 0));
+    d->thr_host[0] = threshold;
+    COMAP_CHECK(ctx, hipMemcpyAsync(d->scal + 4, d->thr_host, 8, hipMemcpyHostToDevice, st));
+    COMAP_CHECK(ctx, hipMemsetAsync(cx, 0, 8 * NO, st));
+    COMAP_CHECK(ctx, hipMemsetAsync(d->flags, 0, 8, st));
+    // b = op_Ax(tod, extend=False); r = p = b (x0 = 0); rr = rr0 = b.b
+    k_ds_project<<<project_grid(NO), 256, 0, st>>>(d->orow, d->opix, d->ow, d->ws, d->tw, nullptr, d->nnum, d->h, NO,
+                                                   np, r, nullptr, nullptr);
+    COMAP_LAUNCH_CHECK(ctx);
     COMAP_CHECK(ctx, hipMemcpyAsync(p, r, 8 * NO, hipMemcpyDeviceToDevice, st));
-    rc |= dot(d, r, r, rr0);
-    COMAP_CHECK(ctx, hipMemcpyAsync(rr, rr0, 8, hipMemcpyDeviceToDevice, st));
-    double h_rr0 = 0, h_rrn = 0;
-    COMAP_CHECK(ctx, hipMemcpyAsync(&h_rr0, rr0, 8, hipMemcpyDeviceToHost, st));
-    int it = 0;
-    for (int i = 0; i < niter && !rc; ++i) {
-        rc |= comap_destripe_bin(d, p, 0, num);
-        rc |= comap_destripe_project(d, p, num, d->h, q, pq);
-        rc |= comap_destripe_cg_update(d, rr, pq, x, r, p, q, rrn);
-        rc |= comap_destripe_cg_direction(d, rrn, rr, p, r);
-        COMAP_CHECK(ctx, hipMemcpyAsync(rr, rrn, 8, hipMemcpyDeviceToDevice, st));
-        COMAP_CHECK(ctx, hipMemcpyAsync(&h_rrn, rrn, 8, hipMemcpyDeviceToHost, st));
+    k_dot_part<<<kRedBlocks, 256, 0, st>>>(r, r, NO, d->part);
+    k_dot_final<<<1, 256, 0, st>>>(d->part, kRedBlocks, d->scal, nullptr);
+    COMAP_LAUNCH_CHECK(ctx);
+    COMAP_CHECK(ctx, hipMemcpyAsync(d->scal + 1, d->scal, 8, hipMemcpyDeviceToDevice, st));
+    d->flags_host[0] = d->flags_host[1] = 0;
+    for (int enq = 0; enq < niter;) {
+        const int k = std::min(kCgBatch, niter - enq);
+        if (k == kCgBatch) {
+            COMAP_CHECK(ctx, hipGraphLaunch(d->batch, st));
+        } else {
+            for (int i = 0; i < k; ++i) enqueue_iteration(d, st);
+            COMAP_LAUNCH_CHECK(ctx);
+        }
+        enq += k;
+        COMAP_CHECK(ctx, hipMemcpyAsync(d->flags_host, d->flags, 8, hipMemcpyDeviceToHost, st));
         COMAP_CHECK(ctx, hipStreamSynchronize(st));
-        it = i + 1;
-        const double delta = h_rrn / h_rr0;
-        if (std::isnan(delta) || delta < threshold) break;
+        if (d->flags_host[0]) break;
     }
-    if (iters_out) *iters_out = it;
+    if (iters_out) *iters_out = d->flags_host[1];
+    COMAP_CHECK(ctx, hipMemcpyAsync(x, cx, 8 * NO, hipMemcpyDeviceToDevice, st));
     // final maps: map = (sum w tod - W x) / h ; naive = sum w tod / h
     if (map) {
-        rc |= comap_destripe_bin(d, x, 1, num);
-        rc |= comap_destripe_div_map(d, num, d->h, map);
+        k_ds_bin<<<grid_for(np * kBinLanes), 256, 0, st>>>(d->prow, d->poff, d->pw, cx, np, d->nnum, num, nullptr);
+        k_div_map<<<grid_for(np), 256, 0, st>>>(num, d->h, np, map);
     }
-    if (naive) rc |= comap_destripe_div_map(d, d->nnum, d->h, naive);
+    if (naive) k_div_map<<<grid_for(np), 256, 0, st>>>(d->nnum, d->h, np, naive);
+    COMAP_LAUNCH_CHECK(ctx);
     if (weight) COMAP_CHECK(ctx, hipMemcpyAsync(weight, d->h, 8 * np, hipMemcpyDeviceToDevice, st));
     if (hits) COMAP_CHECK(ctx, hipMemcpyAsync(hits, d->hits, 8 * np, hipMemcpyDeviceToDevice, st));
     COMAP_CHECK(ctx, hipStreamSynchronize(st));
-    (void)hipFree(buf);
-    return rc;
+    return 0;
 }

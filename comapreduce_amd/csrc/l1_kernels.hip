@@ -26,6 +26,10 @@
 
 using namespace comap;
 
+#ifndef COMAP_GROUPS
+#define COMAP_GROUPS 1      // unit groups of the pass B / median / pass C pipeline (2 measured no faster with the sort-path median)
+#endif
+
 typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
 
 __device__ __forceinline__ double wave_sum(double v)
@@ -519,7 +523,7 @@ __device__ __forceinline__ void band_sums(const float *__restrict__ base, int64_
 // Block = 4 waves (wave b = band b) on a 256 kJB-sample sub-tile of a 1024-sample tile.
 __global__ void __launch_bounds__(256) k_band_sums(const float *__restrict__ tod, const double *__restrict__ A,
                                                    const int32_t *__restrict__ units, const int32_t *__restrict__ tiles,
-                                                   int64_t T, const int32_t *__restrict__ dlist,
+                                                   int64_t tile0, int64_t T, const int32_t *__restrict__ dlist,
                                                    const int32_t *__restrict__ dcnt, const double *__restrict__ dw,
                                                    const double *__restrict__ bsum, double *__restrict__ mb,
                                                    double *__restrict__ sr_out, double *__restrict__ so_out,
@@ -528,7 +532,7 @@ __global__ void __launch_bounds__(256) k_band_sums(const float *__restrict__ tod
     __shared__ double sg[kBands][256 * kJB];
     const int b = uniform(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const int tile = blockIdx.x / kSubB, sub = blockIdx.x % kSubB;
+    const int tile = (int)(tile0 + blockIdx.x / kSubB), sub = blockIdx.x % kSubB;
     const int u = tiles[2 * tile], toff = tiles[2 * tile + 1] + 256 * kJB * sub;
     const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
     if (toff >= n) return;                          // whole block: past the scan end
@@ -570,12 +574,12 @@ __global__ void __launch_bounds__(256) k_band_sums(const float *__restrict__ tod
 
 // ------------------------------------------------------------------ series sums for pass C
 // ss[ub] = {sum mf, sum mf^2, sum A mf}; zeroes mf of skipped bands.
-__global__ void __launch_bounds__(256) k_series_sums(const int32_t *__restrict__ units, const double *__restrict__ A,
+__global__ void __launch_bounds__(256) k_series_sums(int ub0, const int32_t *__restrict__ units, const double *__restrict__ A,
                                                      int64_t T, const double *__restrict__ bsum,
                                                      double *__restrict__ mf, double *__restrict__ ss)
 {
     __shared__ double red[4];
-    const int ub = blockIdx.x;
+    const int ub = ub0 + blockIdx.x;
     const int u = ub / kBands, b = ub % kBands;
     const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
     const bool run = bsum[4 * (int64_t)ub + 3] > 0;
@@ -606,14 +610,14 @@ __global__ void __launch_bounds__(256) k_series_sums(const int32_t *__restrict__
 // the median filter skipped need no regression and are not read.
 constexpr int kRPW = 8;
 constexpr int kRegBlocks = kChannels / (4 * kRPW);   // blocks per (unit, band)
-__global__ void __launch_bounds__(256) k_regress(const float *__restrict__ tod, const double *__restrict__ mf,
+__global__ void __launch_bounds__(256) k_regress(int ub0, const float *__restrict__ tod, const double *__restrict__ mf,
                                                  const int32_t *__restrict__ units, int64_t T,
                                                  const double *__restrict__ bsum, const int32_t *__restrict__ dlist,
                                                  const int32_t *__restrict__ dcnt, double *__restrict__ sdm)
 {
     const int wid = uniform(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const int ub = blockIdx.x / kRegBlocks, g = blockIdx.x % kRegBlocks;
+    const int ub = ub0 + blockIdx.x / kRegBlocks, g = blockIdx.x % kRegBlocks;
     const int u = ub / kBands, b = ub % kBands;
     const int cnt = dcnt[ub];
     const int j0 = g * 4 * kRPW + wid * kRPW;
@@ -1043,9 +1047,68 @@ __global__ void __launch_bounds__(256) k_vane(const float *__restrict__ tod, int
     tsys[row] = (double)mean[1] / g;
 }
 
+// ------------------------------------------------------------------ generic channel binning
+// Level1Averaging.average_tod (Level1Averaging.py:292-321): per (feed, band) and
+// bin k of bw channels,
+//   x_ct  = f32(d_ct / g_c)                   (tod /= system_gain, in place on the f32 copy)
+//   avg_k = sum_c x w_c / W_k,   sq_k = sum_c f32(x x) w_c / W_k,   std = sqrt(sq - avg^2)
+// with w = 1/Tsys^2 (edge channels zeroed by the caller) and W_k its per-bin sum.
+// numpy reduces the middle (channel) axis sequentially: same order here, each
+// product rounded before the add.  Block = 4 waves (wave = band) on a
+// 1024-sample tile; every channel is read (masked ones too: NaN * 0 stays NaN).
+__global__ void __launch_bounds__(256) k_channel_bin(const float *__restrict__ tod, int64_t T, int32_t bw,
+                                                     int32_t nbin, const double *__restrict__ w,
+                                                     const double *__restrict__ g, const double *__restrict__ wsum,
+                                                     double *__restrict__ avg, double *__restrict__ sd)
+{
+#pragma clang fp contract(off)
+    const int b = uniform(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int64_t ntile = (T + kTile - 1) / kTile;
+    const int f = (int)(blockIdx.x / ntile);
+    const int64_t t0 = (int64_t)(blockIdx.x % ntile) * kTile;
+    const int64_t r0 = t0 + 4 * lane;
+    const int nv0 = (int)std::max<int64_t>(-1, std::min<int64_t>(T - r0, 1 << 20));
+    const int64_t fb = (int64_t)f * kBands + b;
+    const float *base = tod + fb * kChannels * T + r0;
+    const double *wc = w + fb * kChannels, *gc = g + fb * kChannels;
+    const bool full = t0 + kTile <= T;
+    for (int k = 0; k < nbin; ++k) {
+        double s1[4 * kJ], s2[4 * kJ];
+#pragma unroll
+        for (int i = 0; i < 4 * kJ; ++i) s1[i] = s2[i] = 0.0;
+        for (int c = k * bw; c < (k + 1) * bw; ++c) {
+            const double wv = wc[c], gv = gc[c];
+            f32x4u r[kJ];
+            if (full) load_raw<kJ, true>(base + (int64_t)c * T, nv0, r);
+            else load_raw<kJ, false>(base + (int64_t)c * T, nv0, r);
+#pragma unroll
+            for (int q = 0; q < kJ; ++q)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float x = (float)((double)r[q][e] / gv);
+                    s1[4 * q + e] += (double)x * wv;
+                    s2[4 * q + e] += (double)(x * x) * wv;
+                }
+        }
+        const double W = wsum[fb * nbin + k];
+        double *ao = avg + (fb * nbin + k) * T + r0, *so = sd + (fb * nbin + k) * T + r0;
+#pragma unroll
+        for (int q = 0; q < kJ; ++q)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int o = 256 * q + e;
+                if (o >= nv0) continue;
+                const double a = s1[4 * q + e] / W, sq = s2[4 * q + e] / W;
+                ao[o] = a;
+                so[o] = sqrt(sq - a * a);
+            }
+    }
+}
+
 // ================================================================== host side
 // HIP events around each launch on the plan's stream (comap_l1_profile)
-static int prof_begin(comap_l1_plan *p)
+static int prof_begin(comap_l1_plan *p, hipStream_t st)
 {
     if (!p->prof_on) return -1;
     const int idx = (int)p->prof_rec.size() * 2;
@@ -1054,23 +1117,24 @@ static int prof_begin(comap_l1_plan *p)
         if (hipEventCreate(&e) != hipSuccess) return -1;
         p->prof_pool.push_back(e);
     }
-    (void)hipEventRecord(p->prof_pool[idx], p->ctx->stream);
+    (void)hipEventRecord(p->prof_pool[idx], st);
     return idx;
 }
 
-static void prof_end(comap_l1_plan *p, int id, int idx)
+static void prof_end(comap_l1_plan *p, int id, int idx, hipStream_t st)
 {
     if (idx < 0) return;
-    (void)hipEventRecord(p->prof_pool[idx + 1], p->ctx->stream);
+    (void)hipEventRecord(p->prof_pool[idx + 1], st);
     p->prof_rec.push_back({id, idx});
 }
 
-#define PROF(p, id, ...)                     \
+#define PROF_ON(p, id, st, ...)              \
     do {                                     \
-        const int _pi = prof_begin(p);       \
+        const int _pi = prof_begin(p, st);   \
         __VA_ARGS__;                         \
-        prof_end(p, id, _pi);                \
+        prof_end(p, id, _pi, st);            \
     } while (0)
+#define PROF(p, id, ...) PROF_ON(p, id, (p)->ctx->stream, __VA_ARGS__)
 
 extern "C" int comap_l1_profile(comap_l1_plan *p, int32_t enable)
 {
@@ -1171,26 +1235,44 @@ extern "C" int comap_l1_plan_create(comap_ctx *ctx, const comap_obs_desc *d, com
     rc |= dalloc(ctx, &p->fitsum, 2 * (size_t)UC);
     rc |= dalloc(ctx, &p->oa, 2 * (size_t)UC);
     if (rc) { delete p; return -2; }
-    // median jobs: (unit, band) series, reflect-3 padded [rev, x, rev], outputs [n, 2n)
-    // (bands of scans shorter than 2w are skipped by median_filter: no outputs)
-    std::vector<MedJob> jobs((size_t)p->U * kBands);
-    for (int u = 0; u < p->U; ++u) {
-        const int32_t f = p->units_h[4 * u], t0 = p->units_h[4 * u + 2], n = p->units_h[4 * u + 3];
-        for (int b = 0; b < kBands; ++b) {
-            MedJob &j = jobs[(size_t)u * kBands + b];
-            const int64_t off = (int64_t)(f * kBands + b) * p->T + t0;
-            j.src = p->mb + off;
-            j.dst = p->mf + off;
-            j.n = n;
-            j.out_lo = n;
-            j.out_hi = (n >= 2 * kMedfiltWindow) ? 2 * (int64_t)n : (int64_t)n;
-            j.mode = 1;
-            j.pad_ = 0;
-            j.gate = p->bsum + 4 * ((int64_t)u * kBands + b) + 3;
+    // pass B / median / pass C pipeline groups (comap_l1_average): contiguous unit ranges
+    p->ngroups = std::max(1, std::min(std::min((int)COMAP_GROUPS, comap_l1_plan::kMaxGroups), (int)p->U));
+    {
+        std::vector<int64_t> tu(p->U + 1, 0);
+        for (int u = 0; u < p->U; ++u) tu[u + 1] = tu[u] + (p->units_h[4 * u + 3] + kTile - 1) / kTile;
+        for (int g = 0; g <= p->ngroups; ++g) {
+            p->grp_u0[g] = (int32_t)((int64_t)p->U * g / p->ngroups);
+            p->grp_tile0[g] = tu[p->grp_u0[g]];
         }
     }
-    rc = comap_median_plan(ctx, &p->med, jobs, kMedfiltWindow);
-    if (rc) { comap_l1_plan_destroy(p); return rc; }
+    bool ok = hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking) == hipSuccess;
+    for (int g = 0; g < p->ngroups && ok; ++g)
+        ok = hipEventCreateWithFlags(&p->ev_b[g], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&p->ev_m[g], hipEventDisableTiming) == hipSuccess;
+    if (!ok) { comap_l1_plan_destroy(p); return comap_fail(ctx, -2, "side stream / events"); }
+    // median jobs per group: (unit, band) series, reflect-3 padded [rev, x, rev], outputs [n, 2n)
+    // (bands of scans shorter than 2w are skipped by median_filter: no outputs)
+    for (int g = 0; g < p->ngroups; ++g) {
+        std::vector<MedJob> jobs;
+        for (int u = p->grp_u0[g]; u < p->grp_u0[g + 1]; ++u) {
+            const int32_t f = p->units_h[4 * u], t0 = p->units_h[4 * u + 2], n = p->units_h[4 * u + 3];
+            for (int b = 0; b < kBands; ++b) {
+                MedJob j;
+                const int64_t off = (int64_t)(f * kBands + b) * p->T + t0;
+                j.src = p->mb + off;
+                j.dst = p->mf + off;
+                j.n = n;
+                j.out_lo = n;
+                j.out_hi = (n >= 2 * kMedfiltWindow) ? 2 * (int64_t)n : (int64_t)n;
+                j.mode = 1;
+                j.pad_ = 0;
+                j.gate = p->bsum + 4 * ((int64_t)u * kBands + b) + 3;
+                jobs.push_back(j);
+            }
+        }
+        rc = comap_median_plan(ctx, &p->medg[g], jobs, kMedfiltWindow);
+        if (rc) { comap_l1_plan_destroy(p); return rc; }
+    }
     // airmass and per-unit airmass sums depend only on the pointing
     k_airmass<<<2048, 256, 0, ctx->stream>>>(p->el, p->airmass, (int64_t)p->F * p->T);
     COMAP_LAUNCH_CHECK(ctx);
@@ -1203,13 +1285,19 @@ extern "C" int comap_l1_plan_create(comap_ctx *ctx, const comap_obs_desc *d, com
 extern "C" int comap_l1_plan_destroy(comap_l1_plan *p)
 {
     if (!p) return 0;
+    if (p->side) (void)hipStreamSynchronize(p->side);
     void *bufs[] = {p->units, p->tiles, p->airmass, p->unit_sums, p->mom,
                     p->nan_count, p->alpha, p->nf, p->bsum, p->mb, p->mf, p->ssum, p->sdm, p->gw,
                     p->gmode, p->kap, p->dsum, p->xreg, p->dG, p->rowbad, p->ubs, p->fitsum, p->oa,
                     p->flag, p->dlist, p->dcnt, p->dw};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
-    comap_median_plan_free(&p->med);
+    for (int g = 0; g < comap_l1_plan::kMaxGroups; ++g) {
+        comap_median_plan_free(&p->medg[g]);
+        if (p->ev_b[g]) (void)hipEventDestroy(p->ev_b[g]);
+        if (p->ev_m[g]) (void)hipEventDestroy(p->ev_m[g]);
+    }
+    if (p->side) (void)hipStreamDestroy(p->side);
     if (p->nan_host) (void)hipHostFree(p->nan_host);
     if (p->mom_event) (void)hipEventDestroy(p->mom_event);
     for (hipEvent_t e : p->prof_pool) (void)hipEventDestroy(e);
@@ -1432,19 +1520,34 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
     // phase 0: the kappa weights and the channel list (no regression needed)
     PROF(p, KV_COEF_D, coef_d(0));
     COMAP_LAUNCH_CHECK(ctx);
-    // pass B: band means + every per-sample sum of the outputs in one read of the cube
-    PROF(p, KV_BAND_SUMS, k_band_sums<<<kSubB * p->n_tiles, 256, 0, st>>>(p->tod, p->airmass, p->units, p->tiles,
-                                                                        p->T, p->dlist, p->dcnt, p->dw, p->bsum,
-                                                                        p->mb, tod_out, orig_out, p->dG));
-    COMAP_LAUNCH_CHECK(ctx);
-    PROF(p, KV_MEDIAN, rc = comap_median_run(ctx, &p->med));
-    if (rc) return rc;
-    PROF(p, KV_SERIES_SUMS, k_series_sums<<<UB, 256, 0, st>>>(p->units, p->airmass, p->T, p->bsum, p->mf, p->ssum));
-    COMAP_LAUNCH_CHECK(ctx);
-    // pass C: the regression sums against the median-filtered band means
-    PROF(p, KV_REGRESS, k_regress<<<UB * kRegBlocks, 256, 0, st>>>(p->tod, p->mf, p->units, p->T, p->bsum, p->dlist,
-                                                                   p->dcnt, p->sdm));
-    COMAP_LAUNCH_CHECK(ctx);
+    // Pass B (band means + every per-sample output sum), the sliding median and pass C
+    // (regression sums) are software-pipelined over the unit groups on two streams:
+    //   main: B0 B1 .. | wait M0: C0 | wait M1: C1 ..     side: wait B0: M0 | wait B1: M1 ..
+    // so each group's median (latency-bound) runs under the next group's streaming pass.
+    hipStream_t side = p->side;
+    for (int g = 0; g < p->ngroups; ++g) {
+        const int64_t t0 = p->grp_tile0[g], nt = p->grp_tile0[g + 1] - t0;
+        const int ub0 = p->grp_u0[g] * kBands, nub = (p->grp_u0[g + 1] - p->grp_u0[g]) * kBands;
+        PROF(p, KV_BAND_SUMS, k_band_sums<<<kSubB * nt, 256, 0, st>>>(p->tod, p->airmass, p->units, p->tiles, t0,
+                                                                    p->T, p->dlist, p->dcnt, p->dw, p->bsum,
+                                                                    p->mb, tod_out, orig_out, p->dG));
+        COMAP_LAUNCH_CHECK(ctx);
+        COMAP_CHECK(ctx, hipEventRecord(p->ev_b[g], st));
+        COMAP_CHECK(ctx, hipStreamWaitEvent(side, p->ev_b[g], 0));
+        PROF_ON(p, KV_MEDIAN, side, rc = comap_median_run(ctx, &p->medg[g], side));
+        if (rc) return rc;
+        PROF_ON(p, KV_SERIES_SUMS, side, k_series_sums<<<nub, 256, 0, side>>>(ub0, p->units, p->airmass, p->T,
+                                                                             p->bsum, p->mf, p->ssum));
+        COMAP_LAUNCH_CHECK(ctx);
+        COMAP_CHECK(ctx, hipEventRecord(p->ev_m[g], side));
+    }
+    for (int g = 0; g < p->ngroups; ++g) {
+        const int ub0 = p->grp_u0[g] * kBands, nub = (p->grp_u0[g + 1] - p->grp_u0[g]) * kBands;
+        COMAP_CHECK(ctx, hipStreamWaitEvent(st, p->ev_m[g], 0));
+        PROF(p, KV_REGRESS, k_regress<<<nub * kRegBlocks, 256, 0, st>>>(ub0, p->tod, p->mf, p->units, p->T, p->bsum,
+                                                                       p->dlist, p->dcnt, p->sdm));
+        COMAP_LAUNCH_CHECK(ctx);
+    }
     // phase 1: regression solve, per-band constants, kappa re-check
     PROF(p, KV_COEF_D, coef_d(1));
     COMAP_LAUNCH_CHECK(ctx);
@@ -1539,5 +1642,18 @@ extern "C" int comap_l1_debug_fetch(comap_l1_plan *p, int32_t what, double *out,
     if (n < cnt) return comap_fail(ctx, -1, "debug buffer too small");
     COMAP_CHECK(ctx, hipMemcpyAsync(out, src, cnt * 8, hipMemcpyDeviceToHost, ctx->stream));
     COMAP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+extern "C" int comap_l1_channel_bin(comap_l1_plan *p, int32_t bin_size, const double *weights, const double *gain,
+                                    const double *wsum, double *avg, double *stddev)
+{
+    if (!p || !weights || !gain || !wsum || !avg || !stddev) return -1;
+    comap_ctx *ctx = p->ctx;
+    if (bin_size < 1 || kChannels % bin_size) return comap_fail(ctx, -1, "bin_size must divide 1024");
+    const int64_t ntile = (p->T + kTile - 1) / kTile;
+    k_channel_bin<<<(unsigned)(p->F * ntile), 256, 0, ctx->stream>>>(p->tod, p->T, bin_size, kChannels / bin_size,
+                                                                     weights, gain, wsum, avg, stddev);
+    COMAP_LAUNCH_CHECK(ctx);
     return 0;
 }

@@ -27,6 +27,8 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 
 namespace {
 
@@ -221,6 +223,222 @@ __global__ void __launch_bounds__(kWalkThreads) k_med_walk(const MedJob *__restr
     }
 }
 
+// ------------------------------------------------------------------ sliding sorted window
+// k_med_slide: one workgroup walks a segment of a series chunk by chunk
+// (kSlideL outputs per chunk), keeping the chunk's union window U sorted in
+// LDS as (key, position) pairs.  Moving to the next chunk removes the kSlideL
+// positions that leave and merges the kSlideL that enter: both small sets are
+// sorted by counting ranks (one broadcast LDS sweep per element), after which
+// every element's new index is known in closed form -- its old index minus
+// the leaving elements below it plus the entering elements below it -- so
+// the merge is one parallel scatter (survivors: contiguous per-thread runs
+// whose two counts advance linearly after one binary search).  The per-output
+// walk over the zone list E is the one k_med_walk uses, with U explicit (no
+// rank bitmaps).  No global sort: every value is keyed once as it enters and
+// once as it leaves.  Positions are kept mod 2^16 and compared relative to the
+// chunk's first union position (the live span is < 2^16).
+constexpr int kSlideL = 256;           // outputs per chunk
+constexpr int kSlideThreads = 512;     // threads 0..255: entering set; 256..511: leaving set
+
+struct KP {
+    uint64_t k;
+    int r;        // position relative to the current union start
+};
+
+__device__ __forceinline__ bool kp_less(const KP &a, const KP &b) { return a.k < b.k || (a.k == b.k && a.r < b.r); }
+
+template <int kPer>   // U entries per thread: w + kSlideL - 1 <= kPer * kSlideThreads
+__global__ void __launch_bounds__(kSlideThreads) k_med_slide(const MedJob *__restrict__ jobs,
+                                                             const SlideSeg *__restrict__ segs, int32_t w)
+{
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int Mcap = w + kSlideL - 1;
+    uint64_t *sk = reinterpret_cast<uint64_t *>(smem);     // U keys [Mcap]
+    uint64_t *xk = sk + Mcap;                              // staging keys: entering | leaving [2L]
+    uint64_t *ok = xk + 2 * kSlideL;                       // sorted keys:  entering | leaving [2L]
+    uint16_t *sp = reinterpret_cast<uint16_t *>(ok + 2 * kSlideL);   // U positions mod 2^16
+    uint16_t *xp = sp + Mcap;
+    uint16_t *op = xp + 2 * kSlideL;
+    uint32_t *E = reinterpret_cast<uint32_t *>(((uintptr_t)(op + 2 * kSlideL) + 15) & ~(uintptr_t)15);   // [2L+16]
+    __shared__ int s_scan[kSlideThreads / 64];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wid = tid >> 6;
+    const SlideSeg sg = segs[blockIdx.x];
+    const MedJob job = jobs[sg.job];
+    if (job.gate && *job.gate <= 0.0) return;
+    const int h = w / 2;
+
+    int64_t i0 = sg.o0;
+    int L = (int)min((int64_t)kSlideL, sg.o1 - i0);
+    int64_t P = i0 - h;                     // first union position of the current chunk
+    auto rel = [&](uint16_t p16) -> int { return (int)(uint16_t)(p16 - (uint16_t)P); };
+
+    // One merge round: positions [a, b) enter, [P, P + nr) leave (na, nr <= kSlideL).
+    auto round = [&](int M, int64_t a, int na, int nr) -> int {
+        const int half = tid >> 8, tl = tid & (kSlideL - 1);
+        const int n = half ? nr : na;
+        uint64_t *hx = xk + half * kSlideL, *ho = ok + half * kSlideL;
+        uint16_t *hxp = xp + half * kSlideL, *hop = op + half * kSlideL;
+        KP me = {0, 0};
+        if (tl < n) {
+            const int64_t pos = half ? P + tl : a + tl;
+            me.k = key_of(xprime(job, pos, h));
+            me.r = (int)(pos - P);
+            hx[tl] = me.k;
+            hxp[tl] = (uint16_t)pos;
+        }
+        __syncthreads();
+        if (tl < n) {               // counting rank within the set (distinct positions: a permutation)
+            int rk = 0;
+            for (int j = 0; j < n; ++j) {
+                const KP o = {hx[j], rel(hxp[j])};
+                rk += kp_less(o, me);
+            }
+            ho[rk] = me.k;
+            hop[rk] = hxp[tl];
+        }
+        __syncthreads();
+        const uint64_t *nk = ok, *rk = ok + kSlideL;
+        const uint16_t *np = op, *rp = op + kSlideL;
+        auto lb = [&](const uint64_t *k, const uint16_t *p, int cnt, const KP &x) -> int {
+            int lo = 0, hi = cnt;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                const KP o = {k[mid], rel(p[mid])};
+                if (kp_less(o, x)) lo = mid + 1; else hi = mid;
+            }
+            return lo;
+        };
+        // survivors: a contiguous run of U per thread
+        const int per = (M + kSlideThreads - 1) / kSlideThreads;
+        const int ib = min(M, tid * per);
+        uint64_t mk[kPer];
+        uint32_t mpf[kPer];          // pos16 | fin << 16 (fin = 0xffff: leaving)
+        int iR = 0, iN = 0;
+        if (ib < M) {
+            const KP x0 = {sk[ib], rel(sp[ib])};
+            iR = lb(rk, rp, nr, x0);
+            iN = lb(nk, np, na, x0);
+        }
+#pragma unroll
+        for (int m = 0; m < kPer; ++m) {
+            const int i = ib + m;
+            mpf[m] = 0xffff0000u;
+            if (m < per && i < M) {
+                const uint16_t p16 = sp[i];
+                const KP x = {sk[i], rel(p16)};
+                while (iR < nr && kp_less(KP{rk[iR], rel(rp[iR])}, x)) ++iR;
+                while (iN < na && kp_less(KP{nk[iN], rel(np[iN])}, x)) ++iN;
+                mk[m] = x.k;
+                if (x.r >= nr) mpf[m] = (uint32_t)p16 | ((uint32_t)(i - iR + iN) << 16);
+            }
+        }
+        // entering element tid: its rank in the set + the survivors below it
+        int efin = -1;
+        uint64_t ek = 0;
+        uint16_t ep = 0;
+        if (tid < na) {
+            ek = nk[tid];
+            ep = np[tid];
+            const KP x = {ek, rel(ep)};
+            efin = tid + lb(sk, sp, M, x) - lb(rk, rp, nr, x);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < kPer; ++m) {
+            const uint32_t f = mpf[m] >> 16;
+            if (f != 0xffffu) { sk[f] = mk[m]; sp[f] = (uint16_t)(mpf[m] & 0xffffu); }
+        }
+        if (efin >= 0) { sk[efin] = ek; sp[efin] = ep; }
+        __syncthreads();
+        return M - nr + na;
+    };
+
+    // initial union of the first chunk: positions [P, P + w + L - 1)
+    int M = 0;
+    for (int64_t a = P; a < P + w + L - 1; a += kSlideL)
+        M = round(M, a, (int)min((int64_t)kSlideL, P + w + L - 1 - a), 0);
+    const int r_lo = (w % 2 == 0) ? (w / 2 - 1) : (w / 2);
+    for (;;) {
+        // ---- zone list E in U order: offsets < L-1 or >= w (excluded by some output's window)
+        const int per = (M + kSlideThreads - 1) / kSlideThreads;
+        const int ib = min(M, tid * per), ie = min(M, ib + per);
+        int cz = 0;
+        for (int i = ib; i < ie; ++i) {
+            const int pz = rel(sp[i]);
+            cz += (pz < L - 1) | (pz >= w);
+        }
+        int incl = cz;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) s_scan[wid] = incl;
+        __syncthreads();
+        int off = 0, ne = 0;
+#pragma unroll
+        for (int v = 0; v < kSlideThreads / 64; ++v) {
+            const int x = s_scan[v];
+            off += (v < wid) ? x : 0;
+            ne += x;
+        }
+        int z = off + incl - cz;
+        for (int i = ib; i < ie; ++i) {
+            const int pz = rel(sp[i]);
+            if ((pz < L - 1) | (pz >= w)) E[z++] = ((uint32_t)i << 16) | (uint32_t)pz;
+        }
+        if (tid < 16) E[ne + tid] = 0xffffffffu;   // sentinels: U index 0xffff > any q
+        __syncthreads();
+        // ---- walk: output k's r-th smallest = U[q], q pushed up by every excluded zone entry below it
+        if (tid < L) {
+            const int k = tid;
+            int q = r_lo, j = 0, jstop = 0;
+            for (;;) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(E + j);
+                const uint32_t es[4] = {v.x, v.y, v.z, v.w};
+                bool stop = false;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    if (!stop) {
+                        const uint32_t e = es[t];
+                        if ((int)(e >> 16) > q) { stop = true; jstop = j + t; }
+                        else { const int pp = (int)(e & 0xffff); q += (pp < k) | (pp >= k + w); }
+                    }
+                }
+                if (stop) break;
+                j += 4;
+            }
+            const double v1 = val_of(sk[q]);
+            double out = v1;
+            if (w % 2 == 0) {
+                q = q + 1;
+                for (j = jstop;; ++j) {
+                    const uint32_t e = E[j];
+                    if ((int)(e >> 16) > q) break;
+                    const int pp = (int)(e & 0xffff);
+                    q += (pp < k) | (pp >= k + w);
+                }
+                out = (val_of(sk[q]) + v1) / 2.0;
+            }
+            job.dst[i0 + k - job.out_lo] = out;
+        }
+        // ---- next chunk: positions [P, P+L) leave, [P+w+L-1, P+L+w+L'-1) enter
+        const int64_t i1 = i0 + L;
+        if (i1 >= sg.o1) break;
+        const int L1 = (int)min((int64_t)kSlideL, sg.o1 - i1);
+        __syncthreads();          // E and U reads of the walk are done
+        M = round(M, P + w + L - 1, L1, L);
+        i0 = i1; L = L1; P = i0 - h;
+    }
+}
+
+size_t slide_smem(int w)
+{
+    return (size_t)(w + kSlideL - 1 + 4 * kSlideL) * 10 + 16 + 4 * (2 * kSlideL + 16);
+}
+
 size_t walk_smem(int nwmax) { return 4 * (2 * kWalkThreads + 16) + 12 * (size_t)nwmax + 8 * kWalkThreads + 64; }
 
 }  // namespace
@@ -231,11 +449,60 @@ size_t walk_smem(int nwmax) { return 4 * (2 * kWalkThreads + 16) + 12 * (size_t)
 constexpr int64_t kMaxOut = 65536;
 constexpr int32_t kMaxWindow = 32768;   // keeps U indices and offsets within 16 bits
 
+// Sliding-window plan: every job cut into segments of whole chunks, enough of
+// them to fill the chip (each segment pays one initial sort of its first window).
+static int plan_slide(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jobs, int32_t w)
+{
+    mp->slide = true;
+    const int mcap = w + kSlideL - 1;
+    mp->kper = mcap <= 4 * kSlideThreads ? 4 : mcap <= 8 * kSlideThreads ? 8 : mcap <= 16 * kSlideThreads ? 16 : 32;
+    int64_t total = 0;
+    for (const MedJob &j : jobs) total += std::max<int64_t>(0, j.out_hi - j.out_lo);
+    // aim for >= 1024 segments, but never shorter than max(8 chunks, 2 windows) of outputs
+    const int64_t want = (total + 1023) / 1024;
+    int64_t seg_len = std::max<int64_t>(want, std::max<int64_t>(8 * kSlideL, 2 * (int64_t)w));
+    seg_len = (seg_len + kSlideL - 1) / kSlideL * kSlideL;
+    std::vector<SlideSeg> segs;
+    for (size_t j = 0; j < jobs.size(); ++j) {
+        const int64_t lo = jobs[j].out_lo, hi = jobs[j].out_hi;
+        if (hi <= lo) continue;
+        const int64_t nseg = (hi - lo + seg_len - 1) / seg_len;
+        const int64_t len = ((hi - lo + nseg - 1) / nseg + kSlideL - 1) / kSlideL * kSlideL;   // balanced
+        for (int64_t o = lo; o < hi; o += len) {
+            SlideSeg sg;
+            sg.job = (int32_t)j; sg.pad_ = 0; sg.o0 = o; sg.o1 = std::min(hi, o + len);
+            segs.push_back(sg);
+        }
+    }
+    mp->nsegs = (int32_t)segs.size();
+    mp->njobs = (int32_t)jobs.size();
+    hipStream_t st = ctx->stream;
+    COMAP_CHECK(ctx, hipMalloc((void **)&mp->jobs, sizeof(MedJob) * std::max<size_t>(1, jobs.size())));
+    COMAP_CHECK(ctx, hipMalloc((void **)&mp->segs, sizeof(SlideSeg) * std::max<size_t>(1, segs.size())));
+    if (!jobs.empty())
+        COMAP_CHECK(ctx, hipMemcpyAsync(mp->jobs, jobs.data(), sizeof(MedJob) * jobs.size(), hipMemcpyHostToDevice, st));
+    if (!segs.empty())
+        COMAP_CHECK(ctx, hipMemcpyAsync(mp->segs, segs.data(), sizeof(SlideSeg) * segs.size(), hipMemcpyHostToDevice, st));
+    const int sm = (int)slide_smem(w);
+    COMAP_CHECK(ctx, hipFuncSetAttribute((const void *)k_med_slide<4>, hipFuncAttributeMaxDynamicSharedMemorySize, sm));
+    COMAP_CHECK(ctx, hipFuncSetAttribute((const void *)k_med_slide<8>, hipFuncAttributeMaxDynamicSharedMemorySize, sm));
+    COMAP_CHECK(ctx, hipFuncSetAttribute((const void *)k_med_slide<16>, hipFuncAttributeMaxDynamicSharedMemorySize, sm));
+    COMAP_CHECK(ctx, hipFuncSetAttribute((const void *)k_med_slide<32>, hipFuncAttributeMaxDynamicSharedMemorySize, sm));
+    COMAP_CHECK(ctx, hipStreamSynchronize(st));   // host vectors go out of scope
+    return 0;
+}
+
 int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jobs_in, int32_t w)
 {
     mp->w = w;
     mp->lc = kWalkThreads;
     if (w < 1 || w > kMaxWindow) return comap_fail(ctx, -1, "median window must be 1 <= w <= 32768");
+    const char *force = getenv("COMAP_MEDIAN_PATH");         // "sort" / "slide": test both paths
+    const int mcap = w + kSlideL - 1;
+    const bool fits = slide_smem(w) <= 160 * 1024 && mcap <= 32 * kSlideThreads && mcap + kSlideL < 65536;
+    // the global-sort path is the default (measured faster at w = 6000); the sliding
+    // sorted window is selected with COMAP_MEDIAN_PATH=slide
+    if (fits && force && !strcmp(force, "slide")) return plan_slide(ctx, mp, jobs_in, w);
     std::vector<MedJob> jobs;
     for (const MedJob &j : jobs_in) {
         if (j.out_hi - j.out_lo <= kMaxOut) { jobs.push_back(j); continue; }
@@ -295,16 +562,27 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
 
 void comap_median_plan_free(MedPlan *mp)
 {
-    void *b[] = {mp->jobs, mp->seg, mp->chunks, mp->k0, mp->k1, mp->v0, mp->v1, mp->rank, mp->temp};
+    void *b[] = {mp->jobs, mp->seg, mp->chunks, mp->k0, mp->k1, mp->v0, mp->v1, mp->rank, mp->temp, mp->segs};
     for (void *p : b)
         if (p) (void)hipFree(p);
     *mp = MedPlan();
 }
 
-int comap_median_run(comap_ctx *ctx, MedPlan *mp)
+int comap_median_run(comap_ctx *ctx, MedPlan *mp, hipStream_t st)
 {
+    if (mp->slide) {
+        if (mp->nsegs == 0) return 0;
+        const size_t sm = slide_smem(mp->w);
+        switch (mp->kper) {
+        case 4: k_med_slide<4><<<mp->nsegs, kSlideThreads, sm, st>>>(mp->jobs, mp->segs, mp->w); break;
+        case 8: k_med_slide<8><<<mp->nsegs, kSlideThreads, sm, st>>>(mp->jobs, mp->segs, mp->w); break;
+        case 16: k_med_slide<16><<<mp->nsegs, kSlideThreads, sm, st>>>(mp->jobs, mp->segs, mp->w); break;
+        default: k_med_slide<32><<<mp->nsegs, kSlideThreads, sm, st>>>(mp->jobs, mp->segs, mp->w); break;
+        }
+        COMAP_LAUNCH_CHECK(ctx);
+        return 0;
+    }
     if (mp->nchunks == 0) return 0;
-    hipStream_t st = ctx->stream;
     dim3 g1(64, (unsigned)mp->njobs);
     k_med_keys<<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, mp->k0, mp->v0);
     COMAP_LAUNCH_CHECK(ctx);

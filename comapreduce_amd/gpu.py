@@ -233,6 +233,29 @@ class GPUObservation:
             out[:, torch.as_tensor(np.flatnonzero(big), device=self.tdev)] = 0
         return out[0], out[1], out[2]
 
+    def channel_bin(self, tsys0, gain0, bin_size: int = 512, mask=None):
+        """Level1Averaging.average_tod (Level1Averaging.py:292-321): (avg, stddev) CUDA f64
+        [F, 4, 1024 // bin_size, T].  The weights 1/Tsys^2 (zeroed on ``mask``) and their
+        per-bin sums are formed on the host with the reference's NumPy expressions (the
+        per-bin sum is numpy's pairwise sum over the contiguous bin axis)."""
+        torch = _torch()
+        if bin_size < 1 or N_CHANNELS % bin_size:
+            raise ValueError(f'frequency_bin_size {bin_size} must divide {N_CHANNELS}')
+        nb = N_CHANNELS // bin_size
+        w = 1.0 / np.asarray(to_host(tsys0), dtype=np.float64).reshape(self.F, N_BANDS, N_CHANNELS) ** 2
+        if mask is not None:
+            w[..., np.asarray(mask, dtype=bool)] = 0
+        wsum = np.sum(w.reshape(self.F, N_BANDS, nb, bin_size), axis=-1)
+        wd = to_device(np.ascontiguousarray(w), torch.float64, self.tdev)
+        sd = to_device(np.ascontiguousarray(wsum), torch.float64, self.tdev)
+        gn = to_device(gain0, torch.float64, self.tdev)
+        out = torch.empty((2, self.F, N_BANDS, nb, self.T), dtype=torch.float64, device=self.tdev)
+        self._bind()
+        N.check(N.lib().comap_l1_channel_bin(self.plan, int(bin_size), N.dptr(wd), N.dptr(gn), N.dptr(sd),
+                                             N.dptr(out[0]), N.dptr(out[1])), self.ctx, 'comap_l1_channel_bin')
+        self._keep_bin = (wd, sd, gn)   # inputs must outlive the enqueued kernel
+        return out[0], out[1]
+
     KERNELS = ('vane', 'moments', 'atmos_fit', 'coef_b', 'band_sums', 'median', 'series_sums', 'regress',
                'gain_weights', 'coef_d', 'gain_avg', 'scan_weights', 'unused', 'finish')
     # the HBM streaming passes: A (per-channel moments), B (band means + every per-sample

@@ -7,6 +7,7 @@ semantics as the reference; the numerical work runs on the GPU through
   MeasureSystemTemperature        VaneCalibration.py:21-198
   AtmosphereRemoval               Level1Averaging.py:156-246
   Level1AveragingGainCorrection   Level1Averaging.py:473-872
+  Level1Averaging                 Level1Averaging.py:249-321
   CheckLevel1File                 Level1Averaging.py:323-356
   AssignLevel1Data                Level2Data.py:25-68
 
@@ -157,6 +158,52 @@ class Level1AveragingGainCorrection(PipelineFunction):
         self.scan_edges = np.asarray(obs.edges)
         self.freq_power_spectra = np.zeros((S, obs.F, 4, 15, 2))
         self.freq_power_spectra_fits = np.zeros((S, obs.F, 4, 3))
+
+
+@dataclass
+class Level1Averaging(PipelineFunction):
+    """Generic 1/Tsys^2-weighted frequency binning of the Level-1 cube
+    (Level1Averaging.py:249-321): per (feed, band), channels in blocks of
+    ``frequency_bin_size``; tod / gain weighted by 1/Tsys^2 with the edge
+    channels [:10], [-10:] and 511..513 masked; mean and standard deviation per
+    bin -> spectrometer/tod, spectrometer/tod_stddev f64 [F, 4, 1024/bin, T].
+    Uses vane event 0 of ``self.level2``.  The reference's ``__call__(data)``
+    cannot be reached from its Runner, which calls ``(data, level2)`` (:275);
+    both forms work here.  One device pass over the resident cube."""
+    name: str = 'Level1Averaging'
+    tod: object = field(default_factory=lambda: np.zeros(1))
+    tod_stddev: object = field(default_factory=lambda: np.zeros(1))
+    frequency_bin_size: int = 512
+    N_CHANNELS: int = 1024
+    STATE: bool = True
+    device: int = 0
+    device_outputs: bool = False
+
+    def __post_init__(self):
+        m = np.zeros(self.N_CHANNELS, dtype=bool)
+        m[:10] = True
+        m[-10:] = True
+        m[511:514] = True
+        self.frequency_mask = m
+
+    @property
+    def save_data(self):
+        return {'spectrometer/tod': self.tod, 'spectrometer/tod_stddev': self.tod_stddev}, {}
+
+    def __call__(self, data, level2_data=None):
+        if isinstance(data, COMAPLevel2):
+            return self.STATE
+        self.average_tod(data)
+        return self.STATE
+
+    def average_tod(self, data: COMAPLevel1):
+        level2 = self.level2
+        obs = gpu_observation(data, self.device)
+        tsys0 = level2['vane/system_temperature'][0]
+        gain0 = level2['vane/system_gain'][0]
+        avg, sd = obs.channel_bin(tsys0, gain0, self.frequency_bin_size, self.frequency_mask)
+        self.tod = _out(avg, self.device_outputs)
+        self.tod_stddev = _out(sd, self.device_outputs)
 
 
 @dataclass

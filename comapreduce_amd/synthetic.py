@@ -320,3 +320,39 @@ def level2_mapmaking(obs_id: int, n_feeds: int = 19, n_samples: int = 45_000, sk
             'spectrometer/pixel_pointing/pixel_az': az, 'spectrometer/pixel_pointing/pixel_el': el}
     filename = f'comap-{obs_id:07d}-2020-06-01-000000_Level2Cont.hd5'
     return data, attrs, filename
+
+
+def destriper_inputs_device(n_obs: int, n_feeds: int = 19, n_samples: int = 180_000, offset_length: int = 50,
+                            nx: int = 480, ny: int = 480, cdelt: float = 1.0 / 60.0, device: int = 0, seed: int = 0):
+    """Destriper inputs at the SURVEY.md §8(d) C5 scale, generated on the device
+    (bench only): n_obs observations x n_feeds feeds x n_samples samples of one
+    band, each (obs, feed) series cut to a multiple of offset_length; Lissajous
+    pointing over an nx x ny CAR field (pixel = floor(x + 0.5), off-map -> -1),
+    smooth sky + random-walk (1/f) offsets + white noise, inverse-variance
+    weights.  Returns (pixels int32, tod f64, weights f64) CUDA tensors."""
+    import math
+    import torch
+    dev = torch.device('cuda', device)
+    g = torch.Generator(device=dev)
+    g.manual_seed(int(seed))
+    n = n_samples // offset_length * offset_length
+    S = n_obs * n_feeds
+    t = torch.arange(n, device=dev, dtype=torch.float64)[None, :]
+    k = torch.arange(S, device=dev, dtype=torch.float64)[:, None]
+    ra = 4.2 * torch.sin(2 * math.pi * t / (1250.0 + 7.0 * k) + 0.37 * k)       # degrees from the field centre
+    dec = 4.2 * torch.sin(2 * math.pi * t / (1700.0 + 5.0 * k) + 1.1 * k)
+    px = torch.floor(-ra / cdelt + (nx / 2 - 1) + 0.5)
+    py = torch.floor(dec / cdelt + (ny / 2 - 1) + 0.5)
+    ok = (px >= 0) & (px <= nx - 1) & (py >= 0) & (py <= ny - 1)
+    pix = torch.where(ok, py * nx + px, torch.full_like(px, -1)).to(torch.int32)
+    del px, py, ok
+    sky = 0.05 * torch.sin(2.1 * ra) * torch.cos(1.7 * dec)
+    del ra, dec
+    no = n // offset_length
+    steps = torch.randn((S, no), generator=g, device=dev, dtype=torch.float64) * 2e-3
+    sky += torch.cumsum(steps, dim=1).repeat_interleave(offset_length, dim=1)
+    del steps
+    sigma = 4e-3 + 2e-3 * torch.rand((S, 1), generator=g, device=dev, dtype=torch.float64)
+    sky += sigma * torch.randn((S, n), generator=g, device=dev, dtype=torch.float64)
+    w = (1.0 / sigma ** 2).expand(S, n).contiguous()
+    return pix.reshape(-1), sky.reshape(-1), w.reshape(-1)

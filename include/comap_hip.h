@@ -12,6 +12,7 @@
  *   comap_l1_atmosphere      Analysis/Level1Averaging.py:197-246
  *   comap_l1_average         Analysis/Level1Averaging.py:592-708,792-872
  *                            + Analysis/GainSubtraction.py:17-209
+ *   comap_l1_channel_bin     Analysis/Level1Averaging.py:249-321 (Level1Averaging)
  *   comap_destripe_*         MapMaking/Destriper.py:85-263,402-503
  *
  * Conventions
@@ -121,16 +122,29 @@ int comap_l1_average(comap_l1_plan *plan, const double *fit_values_dev,
                      const double *tsys0_dev, const double *gain0_dev, int32_t calibrator,
                      double *tod_out_dev, double *orig_out_dev, double *weights_out_dev);
 
+/* Level1Averaging.average_tod (Analysis/Level1Averaging.py:292-321): generic
+ * 1/Tsys^2-weighted frequency binning of the whole cube.  Per (feed, band) and
+ * bin k of bin_size channels: x = f32(d / gain_c), avg = sum_c x w_c / wsum_k,
+ * stddev = sqrt(sum_c f32(x*x) w_c / wsum_k - avg^2), channel sums in channel
+ * order.  weights/gain dev f64 [F][4][1024] (weights = 1/Tsys^2 with the edge
+ * mask applied by the caller), wsum dev f64 [F][4][1024/bin_size];
+ * avg/stddev dev f64 [F][4][1024/bin_size][T]. */
+int comap_l1_channel_bin(comap_l1_plan *plan, int32_t bin_size, const double *weights_dev,
+                         const double *gain_dev, const double *wsum_dev, double *avg_dev, double *stddev_dev);
+
 /* Debug/inspection: copies internal per-unit arrays (host f64):
  * what = 0: normalisation rms [U][4][1024]; 1: median-filtered band mean
- * [F][4][T]; 2: dG [F][T]; 3: regression x0,x1 [U][4][1024][2]. */
+ * [F][4][T]; 2: dG [F][T]; 3: regression x0,x1 [U][4][1024][2]; 4: band mean
+ * [F][4][T]; 5: kappa [3][U][4][1024]; 6: per-band constants [U][4][16];
+ * 7: alpha [U][4][1024]; 8: offsets/slopes [U][4][1024][2]; 9: per (unit,
+ * band) channel-list length and median-band flag [U][4][2]. */
 int comap_l1_debug_fetch(comap_l1_plan *plan, int32_t what, double *out_host, int64_t n);
 
-/* Per-kernel timing with HIP events recorded on the plan's stream around
+/* Per-kernel timing with HIP events recorded on the launching stream around
  * every launch.  collect synchronises, returns per-kernel total ms and launch
- * counts (ids: 0 vane, 1 moments/pass A, 2 atmos fit, 3 coef B, 4 band mean/
+ * counts (ids: 0 vane, 1 moments/pass A, 2 atmos fit, 3 coef B, 4 band sums/
  * pass B, 5 sliding median, 6 series sums, 7 regress/pass C, 8 gain weights,
- * 9 coef D, 10 gain+band average/pass D, 11 scan weights) and resets. */
+ * 9 coef D, 10 legacy pass D, 11 scan weights, 12 unused, 13 finish) and resets. */
 int comap_l1_profile(comap_l1_plan *plan, int32_t enable);
 int comap_l1_profile_collect(comap_l1_plan *plan, double *ms_host, int64_t *counts_host, int32_t n);
 
@@ -157,7 +171,7 @@ int comap_synth_tod(comap_ctx *ctx, int32_t n_feeds, int64_t n_samples, uint64_t
 /* ------------------------------------------------------------ destriper */
 /* Destriper problem on one rank (MapMaking/Destriper.py:155-263): samples
  * [N] with int32 pixel (-1 = off-map), f64 tod and weights, N a multiple of
- * offset_length (<= 64), map of npix pixels.  Builds the constant
+ * offset_length (<= 256; calibrators use 250), map of npix pixels.  Builds the constant
  * offset<->pixel sparse operator and the sample-level maps once. */
 int comap_destripe_create(comap_ctx *ctx, const int32_t *pixels_dev, const double *tod_dev,
                           const double *weights_dev, int64_t n_samples, int32_t offset_length,
@@ -189,8 +203,11 @@ int comap_destripe_cg_direction(comap_destriper *d, const double *rr_new_dev, co
 int comap_destripe_div_map(comap_destriper *d, const double *num_dev, const double *h_dev, double *out_dev);
 /* Whole single-rank destriper_iteration (no collectives): CG (one matvec
  * per iteration, Destriper.py:85-152) to threshold / niter, then the final
- * maps.  Writes offsets x [N/L] and map/naive/weight/hits [npix] (any map
- * pointer may be NULL); *iters_out = iterations performed. */
+ * maps.  Iterations run as replayed hipGraph batches on the problem's own
+ * stream with a device-side stop flag (identical iterates and count to a
+ * per-iteration loop).  Writes offsets x [N/L] and map/naive/weight/hits
+ * [npix] (any map pointer may be NULL); *iters_out = iterations performed.
+ * Synchronises. */
 int comap_destripe_solve(comap_destriper *d, double threshold, int32_t niter, double *x_dev,
                          double *map_dev, double *naive_dev, double *weight_dev,
                          double *hits_dev, int32_t *iters_out);

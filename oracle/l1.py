@@ -412,3 +412,30 @@ def reduce_level1(data, source=''):
     out['vane/system_gain'] = gain
     out['atmosphere/fit_values'] = fit
     return out
+
+
+# ------------------------------------------------------------------ generic channel binning
+def level1_averaging(tod, tsys, gain, frequency_bin_size=512):
+    """Level1Averaging.average_tod, Level1Averaging.py:292-321 (masks :265-273):
+    tod f32 [F, B, C, T]; tsys, gain [F, B, C] (vane event 0).  Same NumPy
+    expressions per (feed, band) as the reference."""
+    F, B, C, T = tod.shape
+    mask = np.zeros(C, dtype=bool)
+    mask[:10] = True
+    mask[-10:] = True
+    mask[511:514] = True
+    nlow = C // frequency_bin_size
+    avg = np.zeros((F, B, nlow, T))
+    sd = np.zeros((F, B, nlow, T))
+    for f in range(F):
+        for b in range(B):
+            x = np.array(tod[f, b])                          # fresh f32 copy (h5py slice)
+            x /= gain[f, b, :, None]
+            w = (1. / tsys ** 2)[f, b, :, None]
+            w[mask, :] = 0
+            wsum = np.sum(np.reshape(w, (nlow, frequency_bin_size)), axis=1)
+            a = np.sum(np.reshape(x * w, (nlow, frequency_bin_size, T)), axis=1) / wsum[:, None]
+            q = np.sum(np.reshape(x ** 2 * w, (nlow, frequency_bin_size, T)), axis=1) / wsum[:, None]
+            avg[f, b] = a
+            sd[f, b] = np.sqrt(q - a ** 2)
+    return avg, sd

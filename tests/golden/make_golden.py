@@ -32,9 +32,10 @@ What it does
    golden_medfilt.npz    medfilt.medfilt known-answer tests
    golden_binvalues.npz  binFuncs.binValues known-answer tests
    golden_destriper.npz  Destriper.destriper_iteration on a small problem
+   golden_binning.npz    Level1Averaging.average_tod on the C1 observation (strided)
    golden_meta.json      input SHA-256s, reference timings, provenance
 
-Usage:  python tests/golden/make_golden.py [--skip-l1]
+Usage:  python tests/golden/make_golden.py [--skip-l1 | --only-variants | --only-comapdata | --only-binning]
 """
 import argparse
 import json
@@ -303,6 +304,35 @@ def run_parser():
                         Coordinates.sex2deg('-00:30:36'), Coordinates.sex2deg('05:32:00.3', hours=True)]}
 
 
+BINNING_STRIDE = 7    # golden_binning.npz keeps every 7th sample of the C1 outputs
+
+
+def run_binning():
+    """Level1Averaging.average_tod (Level1Averaging.py:292-321) on the C1 observation,
+    with the vane solution of the reference's own MeasureSystemTemperature.  The
+    stage's __call__(data) is unreachable from Runner (:275), so average_tod is
+    called directly, as a user would."""
+    from comancpipeline.Analysis.DataHandling import COMAPLevel1, COMAPLevel2
+    from comancpipeline.Analysis.VaneCalibration import MeasureSystemTemperature
+    from comancpipeline.Analysis.Level1Averaging import Level1Averaging
+    figdir = os.path.join(SCRATCH, 'figures')
+    os.makedirs(figdir, exist_ok=True)
+    gen = synthetic.generate_level1(synthetic.SyntheticConfig(n_feeds=1, n_samples=30_000, obs_id=1))
+    data = COMAPLevel1(overwrite=False, large_datasets=['spectrometer/tod'])
+    for k, v in gen['data'].items():
+        data[k] = CopyOnSlice(v) if k == 'spectrometer/tod' else v
+    for k, v in gen['attrs']['comap'].items():
+        data.set_attrs('comap', k, v)
+    level2 = COMAPLevel2(filename=os.path.join(figdir, 'does_not_exist.hd5'))
+    vane = MeasureSystemTemperature(level2=level2, figure_directory=figdir)
+    assert vane(data, level2)
+    level2.update(vane)
+    st = Level1Averaging(level2=level2)
+    st.average_tod(data)
+    np.savez_compressed(os.path.join(HERE, 'golden_binning.npz'), stride=BINNING_STRIDE,
+                        tod=st.tod[..., ::BINNING_STRIDE], tod_stddev=st.tod_stddev[..., ::BINNING_STRIDE])
+
+
 def run_medfilt(out):
     from comancpipeline.Tools.median_filter import medfilt
     for seed, n, w in MEDFILT_CASES:
@@ -356,7 +386,14 @@ def main():
     ap.add_argument('--skip-l1', action='store_true')
     ap.add_argument('--only-variants', action='store_true')
     ap.add_argument('--only-comapdata', action='store_true')
+    ap.add_argument('--only-binning', action='store_true')
     args = ap.parse_args()
+    if args.only_binning:
+        os.environ.setdefault('MPLBACKEND', 'agg')
+        build_reference_helpers()
+        install_stubs()
+        run_binning()
+        return
     if args.only_comapdata:
         build_reference_helpers()
         install_stubs()

@@ -53,3 +53,26 @@ def test_python_cg_driver_matches_native(golden):
     xn, itn, _ = ops.solve_native(1e-6, 100)
     assert it == itn
     assert np.array_equal(x.cpu().numpy(), xn.cpu().numpy())
+
+
+@pytest.mark.parametrize('L,threshold,niter', [(250, 1.0, 100), (250, 0.0, 7), (50, 0.0, 37), (100, 1e-6, 100)])
+def test_destriper_offset_lengths_vs_oracle(L, threshold, niter):
+    """Calibrator offsets (L = 250, threshold 1: run_destriper.py:142-144), L = 100, and
+    iteration counts that are not a multiple of the device graph batch, against the
+    NumPy restatement of destriper_iteration (oracle/destriper.py)."""
+    import oracle.destriper as od
+    from comapreduce_amd.mapmaking.destriper import DeviceDestriper, DeviceOps, cg_solve
+    p, t, w = synthetic.destriper_inputs()
+    ref, xr, itr = od.destriper_iteration(p, t, w, L, NPIX, threshold=threshold, niter=niter)
+    res = DeviceDestriper(p, t, w, L, NPIX).solve(threshold, niter)
+    assert res['iters'] == itr
+    assert rel(res['x'].cpu().numpy(), xr) < 1e-9
+    m = {k: v.cpu().numpy() for k, v in res['maps'].items()}
+    assert np.array_equal(m['weight'], ref['weight'])
+    assert np.array_equal(m['hits'], ref['hits'])
+    assert rel(m['map'], ref['map']) < 1e-9
+    # the per-call (RCCL-path) driver reproduces the graph-batched native loop exactly
+    ops = DeviceOps(p, t, w, L, NPIX)
+    x, it, _, _ = cg_solve(ops, lambda a: a, threshold=threshold, niter=niter)
+    assert it == itr
+    assert np.array_equal(x.cpu().numpy(), res['x'].cpu().numpy())

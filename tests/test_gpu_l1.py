@@ -50,7 +50,11 @@ def test_medfilt_dropin_bit_exact(meta, golden_dir):
         assert np.array_equal(x, g[f'medfilt_{seed}_{n}_{w}']), (seed, n, w)
 
 
-def test_medfilt_dropin_ties_and_edges():
+@pytest.mark.parametrize('path', ['slide', 'sort'])
+def test_medfilt_dropin_ties_and_edges(path, monkeypatch):
+    """Both device median paths: the sliding sorted window (windows up to ~12k)
+    and the global-sort path (every window; forced with COMAP_MEDIAN_PATH=sort)."""
+    monkeypatch.setenv('COMAP_MEDIAN_PATH', path)
     from comapreduce_amd.tools.medfilt import medfilt
     rng = np.random.default_rng(9)
     for n, w in [(6000, 6000), (12000, 6000), (7681, 7681), (513, 400), (2048, 2), (100, 1), (3000, 5),
@@ -59,8 +63,10 @@ def test_medfilt_dropin_ties_and_edges():
         assert np.array_equal(medfilt(x.copy(), w), oracle.medfilt(x.copy(), w)), (n, w)
 
 
-def test_medfilt_long_series_split():
-    """Series longer than one median sub-job (65536 outputs) are split internally."""
+@pytest.mark.parametrize('path', ['slide', 'sort'])
+def test_medfilt_long_series_split(path, monkeypatch):
+    """Series longer than one median sub-job / segment are split internally."""
+    monkeypatch.setenv('COMAP_MEDIAN_PATH', path)
     from comapreduce_amd.tools.medfilt import medfilt, medfilt_batch
     rng = np.random.default_rng(10)
     x = np.round(rng.standard_normal(150_001), 2)
@@ -159,3 +165,30 @@ def test_spikes_stage_bit_exact(golden_dir):
     assert st(l2, l2)
     g = np.load(os.path.join(golden_dir, 'golden_spikes.npz'))['spike_mask']
     assert np.array_equal(st.data['spikes/spike_mask'], g)
+
+
+def test_level1_averaging_vs_reference(meta, golden_dir):
+    """Level1Averaging (Level1Averaging.py:249-321), called as the reference's
+    one-argument __call__, against the reference golden (C1 observation)."""
+    from comapreduce_amd import Analysis as A
+    gen = synthetic.generate_level1(synthetic.SyntheticConfig(**meta['l1_c1_config']))
+    data = level1_from_dict(gen)
+    level2 = COMAPLevel2(filename='/nonexistent/none.hd5')
+    vane = A.MeasureSystemTemperature(level2=level2)
+    assert vane(data, level2)
+    level2.update(vane)
+    st = A.Level1Averaging(level2=level2)
+    assert st(data)
+    g = np.load(os.path.join(golden_dir, 'golden_binning.npz'))
+    s = int(g['stride'])
+    assert st.tod.shape == (1, 4, 2, meta['l1_c1_config']['n_samples'])
+    assert relmax(st.tod[..., ::s], g['tod']) < 1e-12
+    assert relmax(st.tod_stddev[..., ::s], g['tod_stddev']) < 1e-9
+    # half-size bins exercise the generic bin loop
+    st4 = A.Level1Averaging(level2=level2, frequency_bin_size=256)
+    assert st4(data, level2)
+    ref_a, ref_s = __import__('oracle.l1', fromlist=['x']).level1_averaging(
+        gen['data']['spectrometer/tod'], np.asarray(level2['vane/system_temperature'])[0],
+        np.asarray(level2['vane/system_gain'])[0], 256)
+    assert relmax(st4.tod, ref_a) < 1e-12
+    assert relmax(st4.tod_stddev, ref_s) < 1e-9

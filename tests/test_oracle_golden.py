@@ -116,3 +116,16 @@ def test_oracle_spikes_bit_exact(golden_dir):
     tod, edges = variants.spikes_level2(golden_dir)
     g = np.load(os.path.join(golden_dir, 'golden_spikes.npz'))['spike_mask']
     assert np.array_equal(spikes.spike_mask(tod, edges), g)
+
+
+def test_level1_averaging_oracle_vs_reference(golden_dir):
+    """Level1Averaging.average_tod (generic channel binning): the NumPy restatement
+    against the reference run on the C1 observation (make_golden.py --only-binning)."""
+    g = np.load(os.path.join(golden_dir, 'golden_binning.npz'))
+    l1 = np.load(os.path.join(golden_dir, 'golden_l1_c1.npz'))
+    gen = synthetic.generate_level1(synthetic.SyntheticConfig(**meta(golden_dir)['l1_c1_config']))
+    avg, sd = ol1.level1_averaging(gen['data']['spectrometer/tod'], l1['vane__system_temperature'][0],
+                                   l1['vane__system_gain'][0])
+    s = int(g['stride'])
+    assert np.array_equal(avg[..., ::s], g['tod'])
+    assert np.array_equal(sd[..., ::s], g['tod_stddev'])
