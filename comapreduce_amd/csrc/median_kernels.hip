@@ -25,6 +25,7 @@
 #include "comap_internal.h"
 
 #include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_segmented_radix_sort.hpp>
 
 #include <algorithm>
 #include <cstdlib>
@@ -439,6 +440,22 @@ size_t slide_smem(int w)
     return (size_t)(w + kSlideL - 1 + 4 * kSlideL) * 10 + 16 + 4 * (2 * kSlideL + 16);
 }
 
+// Segmented radix sort of the series keys (u64 keys, i32 positions).
+#ifndef COMAP_SORT_RB
+#define COMAP_SORT_RB 8
+#endif
+#ifndef COMAP_SORT_IPT
+#define COMAP_SORT_IPT 8
+#endif
+using SegSortConfig = rocprim::segmented_radix_sort_config<COMAP_SORT_RB, rocprim::kernel_config<256, COMAP_SORT_IPT>,
+                                                           rocprim::DisabledWarpSortConfig, false>;
+hipError_t seg_sort(void *tmp, size_t &tb, const uint64_t *k0, uint64_t *k1, const int32_t *v0, int32_t *v1,
+                    int n, int nseg, const int32_t *seg, hipStream_t st)
+{
+    return rocprim::segmented_radix_sort_pairs<SegSortConfig>(tmp, tb, k0, k1, v0, v1, (unsigned)n, (unsigned)nseg,
+                                                              seg, seg + 1, 0u, 64u, st);
+}
+
 size_t walk_smem(int nwmax) { return 4 * (2 * kWalkThreads + 16) + 12 * (size_t)nwmax + 8 * kWalkThreads + 64; }
 
 }  // namespace
@@ -547,9 +564,7 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
     if (!chunks.empty())
         COMAP_CHECK(ctx, hipMemcpyAsync(mp->chunks, chunks.data(), 8 * chunks.size(), hipMemcpyHostToDevice, st));
     size_t tb = 0;
-    COMAP_CHECK(ctx, hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, tb, mp->k0, mp->k1, mp->v0, mp->v1,
-                                                                 (int)mp->nitems, mp->njobs, mp->seg, mp->seg + 1,
-                                                                 0, 64, st));
+    COMAP_CHECK(ctx, seg_sort(nullptr, tb, mp->k0, mp->k1, mp->v0, mp->v1, (int)mp->nitems, mp->njobs, mp->seg, st));
     mp->temp_bytes = tb;
     COMAP_CHECK(ctx, alloc(&mp->temp, tb));
     const size_t sm = walk_smem(mp->nwmax);
@@ -587,9 +602,7 @@ int comap_median_run(comap_ctx *ctx, MedPlan *mp, hipStream_t st)
     k_med_keys<<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, mp->k0, mp->v0);
     COMAP_LAUNCH_CHECK(ctx);
     size_t tb = mp->temp_bytes;
-    COMAP_CHECK(ctx, hipcub::DeviceSegmentedRadixSort::SortPairs(mp->temp, tb, mp->k0, mp->k1, mp->v0, mp->v1,
-                                                                 (int)mp->nitems, mp->njobs, mp->seg, mp->seg + 1,
-                                                                 0, 64, st));
+    COMAP_CHECK(ctx, seg_sort(mp->temp, tb, mp->k0, mp->k1, mp->v0, mp->v1, (int)mp->nitems, mp->njobs, mp->seg, st));
     k_med_rank<<<g1, 256, 0, st>>>(mp->seg, mp->njobs, mp->v1, mp->rank);
     COMAP_LAUNCH_CHECK(ctx);
     k_med_walk<<<mp->nchunks, kWalkThreads, walk_smem(mp->nwmax), st>>>(mp->jobs, mp->chunks, mp->seg, mp->k1,
