@@ -59,6 +59,8 @@ namespace {
 constexpr int kRedBlocks = 256;
 constexpr int kPartMax = 8192;     // >= every reduction grid below
 constexpr int kBinLanes = 16;      // lanes per pixel row in k_ds_bin
+constexpr int kBinU = 4;           // entry loads in flight per lane (k_ds_bin)
+constexpr int kProjU = 4;          // entry loads in flight per lane (k_ds_project)
 constexpr int kCgBatch = 16;       // CG iterations per replayed graph (one host check per batch)
 
 // Device-side CG stop flag (comap_destripe_solve): once set, every kernel of the
@@ -225,12 +227,21 @@ __global__ void k_sample_maps(const int32_t *__restrict__ skey, const int32_t *_
     }
 }
 
-// num_p = sum_e s_e x_o(e)   (mode 0); mode 1: num = nnum - W x (final destriped numerator).
-// kBinLanes lanes per pixel row (rows hold 0 .. thousands of entries): lane-strided, then a
-// kBinLanes-lane reduction.
+__device__ __forceinline__ double map_value(const double *num, const double *h, int64_t q)
+{
+    const double hv = h[q];
+    return hv != 0.0 ? num[q] / hv : num[q];
+}
+
+// num_p = sum_e s_e x_o(e); base != NULL: num = base - W x (final destriped numerator);
+// hdiv != NULL: num = m = (W x) / h, the map itself (single rank: k_ds_project then gathers
+// one array).  kBinLanes lanes per pixel row (rows hold 0 .. thousands of entries),
+// lane-strided; each lane issues kBinU entry loads, then kBinU gathers, before its fmas
+// (in entry order, so the sum is the plain lane-strided one), then a kBinLanes-lane reduction.
 __global__ void __launch_bounds__(256) k_ds_bin(const int64_t *__restrict__ prow, const int32_t *__restrict__ poff,
                                                 const double *__restrict__ pw, const double *__restrict__ x,
-                                                int64_t npix, const double *__restrict__ base, double *__restrict__ num,
+                                                int64_t npix, const double *__restrict__ base,
+                                                const double *__restrict__ hdiv, double *__restrict__ num,
                                                 const int32_t *__restrict__ done)
 {
     if (cg_done(done)) return;
@@ -239,22 +250,36 @@ __global__ void __launch_bounds__(256) k_ds_bin(const int64_t *__restrict__ prow
     for (int64_t p = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kBinLanes; p < npix; p += step) {
         double s = 0.0;
         const int64_t e1 = prow[p + 1];
-        for (int64_t k = prow[p] + sub; k < e1; k += kBinLanes) s = fma(pw[k], x[poff[k]], s);
+        for (int64_t k = prow[p] + sub; k < e1; k += kBinLanes * kBinU) {
+            int32_t o[kBinU];
+            double a[kBinU], xv[kBinU];
+#pragma unroll
+            for (int u = 0; u < kBinU; ++u) {
+                const bool in = k + u * kBinLanes < e1;
+                o[u] = in ? poff[k + u * kBinLanes] : 0;
+                a[u] = in ? pw[k + u * kBinLanes] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < kBinU; ++u) xv[u] = x[o[u]];
+#pragma unroll
+            for (int u = 0; u < kBinU; ++u)
+                if (k + u * kBinLanes < e1) s = fma(a[u], xv[u], s);
+        }
 #pragma unroll
         for (int o = kBinLanes / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, kBinLanes);
-        if (sub == 0) num[p] = base ? base[p] - s : s;
+        if (sub == 0) {
+            if (base) s = base[p] - s;
+            else if (hdiv) { const double hv = hdiv[p]; s = hv != 0.0 ? s / hv : s; }
+            num[p] = s;
+        }
     }
 }
 
-__device__ __forceinline__ double map_value(const double *num, const double *h, int64_t q)
-{
-    const double hv = h[q];
-    return hv != 0.0 ? num[q] / hv : num[q];
-}
-
 // y_o = ws_o x_o - sum_e s_e m_p(e)  (x == NULL: y_o = tw_o - ..., the b vector).
-// One wave per offset: lanes over its entries (coalesced entry reads, map gathers),
-// one wave reduction; block partials of y.x (when dot_part != NULL).
+// G lanes per offset (G = 16 for L <= 64: 256/G offsets per block sweep); each lane issues
+// kProjU entry loads then kProjU map gathers before its fmas; m = num / h, or num itself
+// when h == NULL (k_ds_bin already divided).  Block partials of y.x (dot_part != NULL).
+template <int G>
 __global__ void __launch_bounds__(256) k_ds_project(const int64_t *__restrict__ orow, const int32_t *__restrict__ opix,
                                                     const double *__restrict__ ow, const double *__restrict__ ws,
                                                     const double *__restrict__ tw, const double *__restrict__ x,
@@ -264,21 +289,40 @@ __global__ void __launch_bounds__(256) k_ds_project(const int64_t *__restrict__ 
 {
     __shared__ double red[4];
     if (cg_done(done)) return;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    constexpr int kPer = 256 / G;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, sub = threadIdx.x & (G - 1);
     double acc = 0.0;
-    for (int64_t o = (int64_t)blockIdx.x * 4 + wid; o < NO; o += (int64_t)gridDim.x * 4) {
+    for (int64_t o0 = (int64_t)blockIdx.x * kPer; o0 < NO; o0 += (int64_t)gridDim.x * kPer) {
+        const int64_t o = o0 + threadIdx.x / G;
+        const bool valid = o < NO;
+        const int64_t e1 = valid ? orow[o + 1] : 0;
         double g = 0.0;
-        const int64_t e1 = orow[o + 1];
-        for (int64_t e = orow[o] + lane; e < e1; e += 64) {
-            const int32_t p = opix[e];
-            g = fma(ow[e], map_value(num, h, p >= 0 ? p : npix - 1), g);   // m[-1] for off-map samples
+        for (int64_t e = (valid ? orow[o] : 0) + sub; e < e1; e += G * kProjU) {
+            int32_t q[kProjU];
+            double a[kProjU], mv[kProjU];
+#pragma unroll
+            for (int u = 0; u < kProjU; ++u) {
+                const bool in = e + u * G < e1;
+                const int32_t pp = in ? opix[e + u * G] : 0;
+                q[u] = pp >= 0 ? pp : (int32_t)(npix - 1);   // m[-1] for off-map samples
+                a[u] = in ? ow[e + u * G] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < kProjU; ++u) mv[u] = h ? map_value(num, h, q[u]) : num[q[u]];
+#pragma unroll
+            for (int u = 0; u < kProjU; ++u)
+                if (e + u * G < e1) g = fma(a[u], mv[u], g);
         }
-        g = wave_sum(g);
-        const double v = (x ? ws[o] * x[o] : tw[o]) - g;
-        if (lane == 0) y[o] = v;
-        if (dot_part) acc = fma(v, x[o], acc);      // v is wave-uniform: every lane holds the same acc
+#pragma unroll
+        for (int s = G / 2; s > 0; s >>= 1) g += __shfl_xor(g, s, G);
+        if (valid && sub == 0) {
+            const double v = (x ? ws[o] * x[o] : tw[o]) - g;
+            y[o] = v;
+            if (dot_part) acc = fma(v, x[o], acc);
+        }
     }
     if (dot_part) {
+        acc = wave_sum(acc);
         if (lane == 0) red[wid] = acc;
         __syncthreads();
         if (threadIdx.x == 0) dot_part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
@@ -362,7 +406,30 @@ __global__ void k_div_map(const double *__restrict__ num, const double *__restri
 }
 
 inline unsigned grid_for(int64_t n, int64_t cap = 4096) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, cap)); }
-inline unsigned project_grid(int64_t NO) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((NO + 3) / 4, kPartMax)); }
+inline int project_lanes(int L) { return L <= 64 ? 16 : (L <= 128 ? 32 : 64); }
+inline unsigned project_grid(int64_t NO, int L)
+{
+    const int64_t per = 256 / project_lanes(L);
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>((NO + per - 1) / per, kPartMax));
+}
+
+// k_ds_project with the lane group sized to the offset length; returns its grid (= partials).
+unsigned launch_project(const comap_destriper *d, hipStream_t st, const double *x, const double *num,
+                        const double *h, double *y, double *part, const int32_t *done)
+{
+    const unsigned pg = project_grid(d->NO, d->L);
+    switch (project_lanes(d->L)) {
+    case 16:
+        k_ds_project<16><<<pg, 256, 0, st>>>(d->orow, d->opix, d->ow, d->ws, d->tw, x, num, h, d->NO, d->npix, y, part, done);
+        break;
+    case 32:
+        k_ds_project<32><<<pg, 256, 0, st>>>(d->orow, d->opix, d->ow, d->ws, d->tw, x, num, h, d->NO, d->npix, y, part, done);
+        break;
+    default:
+        k_ds_project<64><<<pg, 256, 0, st>>>(d->orow, d->opix, d->ow, d->ws, d->tw, x, num, h, d->NO, d->npix, y, part, done);
+    }
+    return pg;
+}
 
 template <typename T>
 int dalloc(comap_ctx *ctx, T **p, size_t n)
@@ -504,7 +571,8 @@ extern "C" int comap_destripe_bin(comap_destriper *d, const double *x, int32_t m
     if (!d || !x || !num) return -1;
     comap_ctx *ctx = d->ctx;
     k_ds_bin<<<grid_for(d->npix * kBinLanes), 256, 0, ctx->stream>>>(d->prow, d->poff, d->pw, x, d->npix,
-                                                                      mode == 1 ? d->nnum : nullptr, num, nullptr);
+                                                                      mode == 1 ? d->nnum : nullptr, nullptr, num,
+                                                                      nullptr);
     COMAP_LAUNCH_CHECK(ctx);
     return 0;
 }
@@ -516,9 +584,7 @@ extern "C" int comap_destripe_project(comap_destriper *d, const double *x, const
     comap_ctx *ctx = d->ctx;
     const double *hh = h ? h : d->h;
     const bool want = dot_out && x;
-    const unsigned pg = project_grid(d->NO);
-    k_ds_project<<<pg, 256, 0, ctx->stream>>>(d->orow, d->opix, d->ow, d->ws, d->tw, x, num, hh, d->NO, d->npix, y,
-                                              want ? d->part : nullptr, nullptr);
+    const unsigned pg = launch_project(d, ctx->stream, x, num, hh, y, want ? d->part : nullptr, nullptr);
     COMAP_LAUNCH_CHECK(ctx);
     if (want) {
         k_dot_final<<<1, 256, 0, ctx->stream>>>(d->part, (int)pg, dot_out, nullptr);
@@ -573,9 +639,9 @@ static void enqueue_iteration(comap_destriper *d, hipStream_t st)
     double *x = d->cg, *r = x + NO, *p = r + NO, *q = p + NO, *num = q + NO;
     double *rr = d->scal + 1, *pq = d->scal + 2, *rrn = d->scal + 3;
     const int32_t *done = d->flags;
-    const unsigned pg = project_grid(NO);
-    k_ds_bin<<<grid_for(np * kBinLanes), 256, 0, st>>>(d->prow, d->poff, d->pw, p, np, nullptr, num, done);
-    k_ds_project<<<pg, 256, 0, st>>>(d->orow, d->opix, d->ow, d->ws, d->tw, p, num, d->h, NO, np, q, d->part, done);
+    // the bin writes the map m = (W p) / h itself, so the projection gathers one array
+    k_ds_bin<<<grid_for(np * kBinLanes), 256, 0, st>>>(d->prow, d->poff, d->pw, p, np, nullptr, d->h, num, done);
+    const unsigned pg = launch_project(d, st, p, num, nullptr, q, d->part, done);
     k_dot_final<<<1, 256, 0, st>>>(d->part, (int)pg, pq, done);
     k_cg_update<<<kRedBlocks, 256, 0, st>>>(rr, pq, x, r, p, q, NO, d->part, done);
     k_dot_final<<<1, 256, 0, st>>>(d->part, kRedBlocks, rrn, done);
@@ -625,8 +691,7 @@ extern "C" int comap_destripe_solve(comap_destriper *d, double threshold, int32_
     COMAP_CHECK(ctx, hipMemsetAsync(cx, 0, 8 * NO, st));
     COMAP_CHECK(ctx, hipMemsetAsync(d->flags, 0, 8, st));
     // b = op_Ax(tod, extend=False); r = p = b (x0 = 0); rr = rr0 = b.b
-    k_ds_project<<<project_grid(NO), 256, 0, st>>>(d->orow, d->opix, d->ow, d->ws, d->tw, nullptr, d->nnum, d->h, NO,
-                                                   np, r, nullptr, nullptr);
+    launch_project(d, st, nullptr, d->nnum, d->h, r, nullptr, nullptr);
     COMAP_LAUNCH_CHECK(ctx);
     COMAP_CHECK(ctx, hipMemcpyAsync(p, r, 8 * NO, hipMemcpyDeviceToDevice, st));
     k_dot_part<<<kRedBlocks, 256, 0, st>>>(r, r, NO, d->part);
@@ -651,7 +716,8 @@ extern "C" int comap_destripe_solve(comap_destriper *d, double threshold, int32_
     COMAP_CHECK(ctx, hipMemcpyAsync(x, cx, 8 * NO, hipMemcpyDeviceToDevice, st));
     // final maps: map = (sum w tod - W x) / h ; naive = sum w tod / h
     if (map) {
-        k_ds_bin<<<grid_for(np * kBinLanes), 256, 0, st>>>(d->prow, d->poff, d->pw, cx, np, d->nnum, num, nullptr);
+        k_ds_bin<<<grid_for(np * kBinLanes), 256, 0, st>>>(d->prow, d->poff, d->pw, cx, np, d->nnum, nullptr, num,
+                                                           nullptr);
         k_div_map<<<grid_for(np), 256, 0, st>>>(num, d->h, np, map);
     }
     if (naive) k_div_map<<<grid_for(np), 256, 0, st>>>(d->nnum, d->h, np, naive);
