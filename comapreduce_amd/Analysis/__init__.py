@@ -6,4 +6,5 @@ from ..pipeline.datahandling import HDF5Data, COMAPLevel1, COMAPLevel2, RepointE
 from ..stages.level1 import (MeasureSystemTemperature, AtmosphereRemoval,  # noqa: F401
                              Level1AveragingGainCorrection, Level1Averaging, CheckLevel1File,
                              AssignLevel1Data)
-from ..stages.statistics import Spikes  # noqa: F401,E402
+from ..stages.statistics import Spikes, NoiseStatistics  # noqa: F401,E402
+from ..stages.level2 import Level2FitPowerSpectrum  # noqa: F401,E402

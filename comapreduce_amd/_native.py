@@ -52,6 +52,8 @@ _SIGS = {
     'comap_l1_profile_collect': (c_int, [c_void_p, P_double, P_int64, c_int32]),
     'comap_spikes': (c_int, [c_void_p, c_void_p, c_int32, c_int64, P_int64, c_int32, c_int32, c_int32, c_double,
                              c_void_p]),
+    'comap_power_spectra': (c_int, [c_void_p, c_void_p, c_int32, c_int64, P_int64, c_int32, c_void_p, c_int32,
+                                    P_int64, c_void_p]),
     'comap_synth_tod': (c_int, [c_void_p, c_int32, c_int64, ctypes.c_uint64, c_void_p, c_void_p, c_void_p,
                                 c_void_p, c_void_p]),
     'comap_destripe_create': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int64,

@@ -159,6 +159,22 @@ int comap_spikes(comap_ctx *ctx, const double *tod_dev, int32_t n_rows, int64_t 
                  const int64_t *edges_host, int32_t n_scans, int32_t medfilt_window, int32_t step,
                  double threshold, uint8_t *mask_dev);
 
+/* ------------------------------------------------------------ Level-2 power spectra (FFT noise QA) */
+/* Positive-frequency power spectra of every (row, scan) of a device Level-2
+ * TOD f64 [n_rows][T] (rows = feed*4 + band), scans from edges_host
+ * [n_scans][2]; replaces the per-series np.fft calls of
+ *   mode 0: Level2FitPowerSpectrum.run (Analysis/Level2Data.py:275-278),
+ *           |fft(x)|**2 / n;
+ *   mode 1: NoiseStatistics.power_spectrum (Analysis/Statistics.py:155),
+ *           |fft(x)**2|.
+ * mask_dev (optional, uint8 [n_rows][T]): masked samples are first replaced
+ * by np.interp over the unmasked samples of the scan (Statistics.py:216-221).
+ * Scan k writes out_dev[out_offsets_host[k] + r*nk + (j-1)] for
+ * j = 1 .. nk = (n-1)/2 (fftfreq(n) > 0), n = scan length.  Synchronises. */
+int comap_power_spectra(comap_ctx *ctx, const double *tod_dev, int32_t n_rows, int64_t n_samples,
+                        const int64_t *edges_host, int32_t n_scans, const uint8_t *mask_dev, int32_t mode,
+                        const int64_t *out_offsets_host, double *out_dev);
+
 /* ------------------------------------------------------------ synthetic input (bench) */
 /* Fills a device-resident synthetic observation with the statistics of
  * tod f32 [F][4][1024][T], band_average f32 [F][4][T].

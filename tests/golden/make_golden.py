@@ -33,9 +33,10 @@ What it does
    golden_binvalues.npz  binFuncs.binValues known-answer tests
    golden_destriper.npz  Destriper.destriper_iteration on a small problem
    golden_binning.npz    Level1Averaging.average_tod on the C1 observation (strided)
+   golden_noise.npz      Level2FitPowerSpectrum + NoiseStatistics (variants.noise_level2)
    golden_meta.json      input SHA-256s, reference timings, provenance
 
-Usage:  python tests/golden/make_golden.py [--skip-l1 | --only-variants | --only-comapdata | --only-binning]
+Usage:  python tests/golden/make_golden.py [--skip-l1 | --only-variants | --only-comapdata | --only-binning | --only-noise]
 """
 import argparse
 import json
@@ -241,6 +242,48 @@ def run_spikes():
     np.savez_compressed(os.path.join(HERE, 'golden_spikes.npz'), spike_mask=st.data['spikes/spike_mask'])
 
 
+def run_noise():
+    """Level2FitPowerSpectrum (Level2Data.py:224-329) and NoiseStatistics
+    (Statistics.py:107-224) on the noise-QA Level-2 input (variants.noise_level2)."""
+    from comancpipeline.Analysis.DataHandling import COMAPLevel2
+    from comancpipeline.Analysis.Level2Data import Level2FitPowerSpectrum
+    from comancpipeline.Analysis.Statistics import NoiseStatistics
+    sys.path.insert(0, HERE)
+    import variants
+    tod, edges, mask, feeds = variants.noise_level2(HERE)
+    figdir = os.path.join(SCRATCH, 'figures_noise')
+    os.makedirs(figdir, exist_ok=True)
+    out = {'tod': tod, 'scan_edges': edges, 'spike_mask': mask, 'feeds': feeds}
+    timings = {}
+    l2 = COMAPLevel2(filename='/nonexistent/noise.hd5')
+    l2['averaged_tod/tod'] = tod
+    l2['averaged_tod/scan_edges'] = edges
+    l2['spectrometer/feeds'] = feeds
+    l2.set_attrs('comap', 'source', 'Field00')
+    l2.set_attrs('comap', 'obsid', 1)
+    st = Level2FitPowerSpectrum(level2=l2, figure_directory=figdir)
+    t0 = time.perf_counter()
+    assert st(l2, l2)
+    timings['Level2FitPowerSpectrum'] = time.perf_counter() - t0
+    out['fnoise_fit_parameters'] = st.data['fnoise_fits/fnoise_fit_parameters']
+    out['fnoise_auto_rms'] = st.data['fnoise_fits/auto_rms']
+    for with_mask in (False, True):
+        l2n = COMAPLevel2(filename='/nonexistent/noise.hd5')
+        l2n['averaged_tod/tod'] = tod
+        l2n['averaged_tod/scan_edges'] = edges
+        l2n['spectrometer/feeds'] = feeds
+        if with_mask:
+            l2n['spikes/spike_mask'] = mask
+        l2n.set_attrs('comap', 'source', 'Field00')
+        ns = NoiseStatistics(level2=l2n)
+        t0 = time.perf_counter()
+        assert ns(l2n, l2n)
+        timings[f'NoiseStatistics_mask{int(with_mask)}'] = time.perf_counter() - t0
+        out[f'fnoise_mask{int(with_mask)}'] = ns.data['noise_statistics/fnoise']
+    np.savez_compressed(os.path.join(HERE, 'golden_noise.npz'), **out)
+    return timings
+
+
 class _FakeH5:
     """h5py.File stand-in over an in-memory (datasets, attrs) pair."""
 
@@ -387,7 +430,17 @@ def main():
     ap.add_argument('--only-variants', action='store_true')
     ap.add_argument('--only-comapdata', action='store_true')
     ap.add_argument('--only-binning', action='store_true')
+    ap.add_argument('--only-noise', action='store_true')
     args = ap.parse_args()
+    if args.only_noise:
+        os.environ.setdefault('MPLBACKEND', 'agg')
+        build_reference_helpers()
+        install_stubs()
+        mp = os.path.join(HERE, 'golden_meta.json')
+        meta = json.load(open(mp))
+        meta['reference_timings_s_noise'] = run_noise()
+        json.dump(meta, open(mp, 'w'), indent=1, default=str)
+        return
     if args.only_binning:
         os.environ.setdefault('MPLBACKEND', 'agg')
         build_reference_helpers()

@@ -54,3 +54,31 @@ def spikes_level2(golden_dir):
     tod[0, 3, 20000] += 1.0
     tod[0, 3, 25000] = np.nan
     return tod, edges
+
+
+def noise_level2(golden_dir):
+    """Level-2 input of the noise-QA goldens (Level2FitPowerSpectrum,
+    NoiseStatistics): feed 1 = the C1 golden averaged_tod plus two narrow
+    lines (1.7 Hz, 6.3 Hz) so the find_peaks masking runs; feed 20 = a copy
+    (skipped by Level2FitPowerSpectrum: feed > 19); one all-zero scan-band
+    (nansum == 0 skip).  A spike mask with a few runs, one touching a scan
+    edge, for NoiseStatistics' interpolation."""
+    import os
+    g = np.load(os.path.join(golden_dir, 'golden_l1_c1.npz'))
+    one = g['averaged_tod__tod'][0]
+    edges = g['averaged_tod__scan_edges']
+    T = one.shape[-1]
+    t = np.arange(T) / 50.0
+    rng = np.random.default_rng(2024)
+    tod = np.stack([one, one * 1.3 + 0.01 * rng.standard_normal(one.shape)]).astype(np.float64)
+    sd = np.nanstd(np.diff(one, axis=-1))
+    tod[0] += sd * (3.0 * np.sin(2 * np.pi * 1.7 * t) + 2.0 * np.sin(2 * np.pi * 6.3 * t + 0.4))
+    s1, e1 = edges[1]
+    tod[1, 2, s1:e1] = 0.0
+    mask = np.zeros(tod.shape, dtype=bool)
+    mask[0, 0, 4000:4210] = True
+    mask[0, 1, edges[0, 0]:edges[0, 0] + 150] = True
+    mask[0, 3, e1 - 120:e1] = True
+    mask[1, 1, 12000:12001] = True
+    feeds = np.array([1, 20])
+    return tod, edges, mask, feeds
