@@ -204,11 +204,17 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    device = local
+    # one rank per GPU (the driver's torchrun); COMAP_DIST_BACKEND=gloo with more ranks than
+    # GPUs is a rehearsal mode only (ranks share devices; RCCL refuses duplicate GPUs)
+    backend = os.environ.get('COMAP_DIST_BACKEND', 'nccl')
+    device = local % max(torch.cuda.device_count(), 1) if backend == 'gloo' else local
     torch.cuda.set_device(device)
     if world > 1:
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        dist.init_process_group('nccl', device_id=torch.device('cuda', device))
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', device))
+        else:
+            dist.init_process_group(backend)
     F, T = args.feeds, args.samples
     data = build_observation(F, T, obs_id=rank + 1, device=device)
     samp_ch = F * 4 * 1024 * T

@@ -76,3 +76,46 @@ def test_destriper_offset_lengths_vs_oracle(L, threshold, niter):
     x, it, _, _ = cg_solve(ops, lambda a: a, threshold=threshold, niter=niter)
     assert it == itr
     assert np.array_equal(x.cpu().numpy(), res['x'].cpu().numpy())
+
+
+def _gloo_rank(rank, world, port, p, t, w, q):
+    import torch
+    import torch.distributed as dist
+    from comapreduce_amd.mapmaking.destriper import DeviceDestriper
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    no = t.size // L
+    lo, hi = (no * rank // world) * L, (no * (rank + 1) // world) * L   # whole offsets per rank
+    res = DeviceDestriper(p[lo:hi], t[lo:hi], w[lo:hi], L, NPIX, device=0).solve(1e-6, 100)
+    q.put((rank, res['x'].cpu().numpy(), res['iters'], {k: v.cpu().numpy() for k, v in res['maps'].items()}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_destriper_two_ranks_distributed_path(golden):
+    """DeviceDestriper's multi-rank path (cg_solve over DeviceOps, map numerator,
+    weights, hits and CG scalars all-reduced every iteration) on 2 ranks sharing
+    cuda:0 over gloo -- the same code the RCCL run executes, with the samples
+    split at an offset boundary; the joined offsets and the maps must match the
+    reference golden as the single-rank solve does."""
+    import torch.multiprocessing as mp
+    p, t, w = synthetic.destriper_inputs()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = 29700 + os.getpid() % 200
+    procs = [ctx.Process(target=_gloo_rank, args=(r, 2, port, p, t, w, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=240) for _ in range(2)], key=lambda r: r[0])
+    for pr in procs:
+        pr.join(timeout=60)
+    x = np.concatenate([res[0][1], res[1][1]])
+    assert res[0][2] == res[1][2]
+    assert rel(x, golden['destriper_offsets']) < 1e-5
+    m = res[0][3]
+    assert rel(m['weight'], golden['destriper_weight']) < 1e-12   # two partial sums, then the all-reduce
+    assert np.array_equal(m['hits'], golden['destriper_hits'])
+    assert rel(m['map'], golden['destriper_map']) < 1e-5
+    assert rel(m['naive'], golden['destriper_naive']) < 1e-5
