@@ -58,6 +58,10 @@ _SIGS = {
                                 c_void_p, c_void_p]),
     'comap_destripe_create': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int64,
                                       ctypes.POINTER(c_void_p)]),
+    'comap_destripe_dist_bin': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    'comap_destripe_dist_project': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    'comap_destripe_dist_update': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    'comap_destripe_dist_direction': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     'comap_destripe_destroy': (c_int, [c_void_p]),
     'comap_destripe_n_offsets': (c_int64, [c_void_p]),
     'comap_destripe_nnz': (c_int, [c_void_p, P_int64, P_int64]),

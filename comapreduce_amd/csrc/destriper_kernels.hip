@@ -630,6 +630,54 @@ extern "C" int comap_destripe_div_map(comap_destriper *d, const double *num, con
     return 0;
 }
 
+// ---------------------------------------------------------------- multi-rank CG pieces
+// One CG iteration split at its three all-reduce points (map numerator, p.q,
+// r.r), every kernel gated by the device stop flag so the host can queue a
+// batch of iterations (with the collectives between the pieces) and check the
+// flag once per batch.  scal: [0] rr0, [1] rr, [2] pq, [3] rr_new, [4] threshold.
+extern "C" int comap_destripe_dist_bin(comap_destriper *d, const double *p, double *num, const int32_t *flags)
+{
+    if (!d || !p || !num || !flags) return -1;
+    comap_ctx *ctx = d->ctx;
+    k_ds_bin<<<grid_for(d->npix * kBinLanes), 256, 0, ctx->stream>>>(d->prow, d->poff, d->pw, p, d->npix, nullptr,
+                                                                      nullptr, num, flags);
+    COMAP_LAUNCH_CHECK(ctx);
+    return 0;
+}
+
+extern "C" int comap_destripe_dist_project(comap_destriper *d, const double *p, const double *num, const double *h,
+                                           double *q, double *scal, const int32_t *flags)
+{
+    if (!d || !p || !num || !h || !q || !scal || !flags) return -1;
+    comap_ctx *ctx = d->ctx;
+    const unsigned pg = launch_project(d, ctx->stream, p, num, h, q, d->part, flags);
+    k_dot_final<<<1, 256, 0, ctx->stream>>>(d->part, (int)pg, scal + 2, flags);
+    COMAP_LAUNCH_CHECK(ctx);
+    return 0;
+}
+
+extern "C" int comap_destripe_dist_update(comap_destriper *d, double *scal, double *x, double *r, const double *p,
+                                          const double *q, const int32_t *flags)
+{
+    if (!d || !scal || !x || !r || !p || !q || !flags) return -1;
+    comap_ctx *ctx = d->ctx;
+    k_cg_update<<<kRedBlocks, 256, 0, ctx->stream>>>(scal + 1, scal + 2, x, r, p, q, d->NO, d->part, flags);
+    k_dot_final<<<1, 256, 0, ctx->stream>>>(d->part, kRedBlocks, scal + 3, flags);
+    COMAP_LAUNCH_CHECK(ctx);
+    return 0;
+}
+
+extern "C" int comap_destripe_dist_direction(comap_destriper *d, double *scal, double *p, const double *r,
+                                             int32_t *flags)
+{
+    if (!d || !scal || !p || !r || !flags) return -1;
+    comap_ctx *ctx = d->ctx;
+    k_cg_direction<<<grid_for(d->NO), 256, 0, ctx->stream>>>(scal + 3, scal + 1, p, r, d->NO, flags);
+    k_cg_check<<<1, 64, 0, ctx->stream>>>(scal, flags);
+    COMAP_LAUNCH_CHECK(ctx);
+    return 0;
+}
+
 // ---------------------------------------------------------------- device-resident CG
 // One CG iteration (Destriper.py:85-152 with p == pb, r == rb) on the problem's own
 // vectors; every kernel returns at once after k_cg_check has set the stop flag.

@@ -85,6 +85,45 @@ def cg_solve(ops, allreduce, threshold=1e-6, niter=100, h=None, nnum=None):
     return x, it, h, nnum
 
 
+def cg_solve_batched(ops, allreduce, threshold=1e-6, niter=100, batch=16):
+    """Multi-rank CG of the device path: the iterates of ``cg_solve`` (same
+    order of operations and cross-rank sums), but with the convergence test on
+    the device (comap_destripe_dist_direction's stop flag) so ``batch``
+    iterations -- kernels and all-reduces -- are queued per host round trip.
+    Iterations queued after convergence are no-ops (their all-reduces sum
+    stale buffers that are not read again).  Returns (x, iterations, h, nnum)."""
+    torch = ops.torch
+    h0, _, n0 = ops.local_maps()
+    h = allreduce(h0)
+    nnum = allreduce(n0)
+    NO = ops.n_offsets
+    x, r, q = ops.zeros(NO), ops.zeros(NO), ops.zeros(NO)
+    num = ops.zeros(ops.npix)
+    ops.project(None, nnum, h, r)
+    p = ops.copy(r)
+    scal = ops.zeros(8)
+    ops.dot(r, r, scal[0:1])
+    allreduce(scal[0:1])
+    scal[1:2].copy_(scal[0:1])
+    scal[4] = float(threshold)
+    flags = torch.zeros(2, dtype=torch.int32, device=ops.dev)
+    enq = 0
+    while enq < niter:
+        k = min(batch, niter - enq)
+        for _ in range(k):
+            ops.dist_bin(p, num, flags)
+            allreduce(num)
+            ops.dist_project(p, num, h, q, scal, flags)
+            allreduce(scal[2:3])
+            ops.dist_update(scal, x, r, p, q, flags)
+            allreduce(scal[3:4])
+            ops.dist_direction(scal, p, r, flags)
+        enq += k
+        if int(flags[0].item()):
+            break
+    return x, int(flags[1].item()), h, nnum
+
+
 class DeviceOps:
     """One rank's destriper operator on the GPU (comap_destripe_* C ABI)."""
 
@@ -177,6 +216,21 @@ class DeviceOps:
     def cg_direction(self, rr_new, rr, p, r):
         self._c('comap_destripe_cg_direction', self.h, N.dptr(rr_new), N.dptr(rr), N.dptr(p), N.dptr(r))
 
+    # ---- multi-rank iteration pieces (device stop flag; see cg_solve_batched)
+    def dist_bin(self, p, num, flags):
+        self._c('comap_destripe_dist_bin', self.h, N.dptr(p), N.dptr(num), N.dptr(flags))
+
+    def dist_project(self, p, num, h, q, scal, flags):
+        self._c('comap_destripe_dist_project', self.h, N.dptr(p), N.dptr(num), N.dptr(h), N.dptr(q), N.dptr(scal),
+                N.dptr(flags))
+
+    def dist_update(self, scal, x, r, p, q, flags):
+        self._c('comap_destripe_dist_update', self.h, N.dptr(scal), N.dptr(x), N.dptr(r), N.dptr(p), N.dptr(q),
+                N.dptr(flags))
+
+    def dist_direction(self, scal, p, r, flags):
+        self._c('comap_destripe_dist_direction', self.h, N.dptr(scal), N.dptr(p), N.dptr(r), N.dptr(flags))
+
     def div_map(self, num, h, out):
         self._c('comap_destripe_div_map', self.h, N.dptr(num), N.dptr(h), N.dptr(out))
 
@@ -206,7 +260,7 @@ class DeviceDestriper:
             x, it, maps = ops.solve_native(threshold, niter)
             maps['map2'] = maps['weight']
             return {'x': x, 'iters': it, 'maps': maps}
-        x, it, h, nnum = cg_solve(ops, torch_allreduce, threshold, niter)
+        x, it, h, nnum = cg_solve_batched(ops, torch_allreduce, threshold, niter)
         _, hits, _ = ops.local_maps()
         torch_allreduce(hits)
         num = ops.zeros(ops.npix)

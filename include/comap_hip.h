@@ -215,6 +215,26 @@ int comap_destripe_cg_update(comap_destriper *d, const double *rr_dev, const dou
 /* beta = rr_new/rr; p = r + beta p */
 int comap_destripe_cg_direction(comap_destriper *d, const double *rr_new_dev, const double *rr_dev,
                                 double *p_dev, const double *r_dev);
+/* Multi-rank CG iteration (Destriper.py:85-152 with p == pb), split at the
+ * three cross-rank sums the caller performs between the calls:
+ *   dist_bin        num = W p (local numerator)          -> all-reduce num
+ *   dist_project    q = F^T W (F p - m[p]), m = num/h;
+ *                   scal[2] = local q.p                   -> all-reduce scal[2]
+ *   dist_update     alpha = scal[1]/scal[2]; x += alpha p; r -= alpha q;
+ *                   scal[3] = local r.r                   -> all-reduce scal[3]
+ *   dist_direction  p = r + (scal[3]/scal[1]) p; scal[1] = scal[3];
+ *                   flags[1] += 1; flags[0] = 1 when scal[3]/scal[0] is NaN
+ *                   or below scal[4] (threshold).
+ * Every kernel returns at once when flags[0] is set, so a batch of iterations
+ * can be queued with one host check of flags per batch.  scal_dev f64 [>= 5]:
+ * rr0, rr, pq, rr_new, threshold; flags_dev int32 [2]: stop, iterations. */
+int comap_destripe_dist_bin(comap_destriper *d, const double *p_dev, double *num_dev, const int32_t *flags_dev);
+int comap_destripe_dist_project(comap_destriper *d, const double *p_dev, const double *num_dev,
+                                const double *h_dev, double *q_dev, double *scal_dev, const int32_t *flags_dev);
+int comap_destripe_dist_update(comap_destriper *d, double *scal_dev, double *x_dev, double *r_dev,
+                               const double *p_dev, const double *q_dev, const int32_t *flags_dev);
+int comap_destripe_dist_direction(comap_destriper *d, double *scal_dev, double *p_dev, const double *r_dev,
+                                  int32_t *flags_dev);
 /* out = num/h (num where h == 0); h_dev == NULL uses the local weight map */
 int comap_destripe_div_map(comap_destriper *d, const double *num_dev, const double *h_dev, double *out_dev);
 /* Whole single-rank destriper_iteration (no collectives): CG (one matvec

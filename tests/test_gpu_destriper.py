@@ -55,6 +55,19 @@ def test_python_cg_driver_matches_native(golden):
     assert np.array_equal(x.cpu().numpy(), xn.cpu().numpy())
 
 
+@pytest.mark.parametrize('threshold,niter', [(1e-6, 100), (0.0, 37)])
+def test_batched_cg_driver_matches_native(threshold, niter):
+    """The multi-rank driver (cg_solve_batched: device stop flag, 16 iterations per
+    host check) == the native loop, including a count that stops mid-batch."""
+    from comapreduce_amd.mapmaking.destriper import DeviceOps, cg_solve_batched
+    p, t, w = synthetic.destriper_inputs()
+    ops = DeviceOps(p, t, w, L, NPIX)
+    x, it, h, nnum = cg_solve_batched(ops, lambda a: a, threshold=threshold, niter=niter)
+    xn, itn, _ = ops.solve_native(threshold, niter)
+    assert it == itn
+    assert np.array_equal(x.cpu().numpy(), xn.cpu().numpy())
+
+
 @pytest.mark.parametrize('L,threshold,niter', [(250, 1.0, 100), (250, 0.0, 7), (50, 0.0, 37), (100, 1e-6, 100)])
 def test_destriper_offset_lengths_vs_oracle(L, threshold, niter):
     """Calibrator offsets (L = 250, threshold 1: run_destriper.py:142-144), L = 100, and
