@@ -42,7 +42,7 @@ struct comap_destriper {
     // sample-level maps (local)
     double *h = nullptr, *hits = nullptr, *nnum = nullptr;   // [npix]
     // reduction scratch
-    double *part = nullptr;    // [kPartMax] block partials
+    double *part = nullptr;    // [2 kPartMax] block partials
     double *scal = nullptr;    // [16] device scalars: rr0, rr, pq, rr_new, threshold
     // device-resident CG of comap_destripe_solve (fixed pointers: graph-replayable)
     double *cg = nullptr;          // [4 NO + npix]: x, r, p, q | num
@@ -73,6 +73,17 @@ __device__ __forceinline__ double wave_sum(double v)
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
+}
+
+// Fixed-order sum of n block partials by one 256-thread block (k_dot_final's order).
+__device__ __forceinline__ double block_final_sum(const double *__restrict__ part, int n, double *red)
+{
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) acc += part[i];
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    return (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // One wave per offset: lane l owns samples l, l + 64, ... (K per lane, L <= 64 K).
@@ -347,12 +358,8 @@ __global__ void __launch_bounds__(256) k_dot_final(const double *__restrict__ pa
 {
     __shared__ double red[4];
     if (cg_done(done)) return;
-    double acc = 0.0;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) acc += part[i];
-    acc = wave_sum(acc);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
-    __syncthreads();
-    if (threadIdx.x == 0) out[0] = (red[0] + red[1]) + (red[2] + red[3]);
+    const double sum = block_final_sum(part, n, red);
+    if (threadIdx.x == 0) out[0] = sum;
 }
 
 // x += a p ; r -= a q ; a = rr / pq ; partials of r.r
@@ -375,6 +382,60 @@ __global__ void __launch_bounds__(256) k_cg_update(const double *__restrict__ rr
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
     __syncthreads();
     if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// Fused single-rank CG tail (comap_destripe_solve): no separate final-sum or check
+// launches.  Every block re-derives the global sums from the previous kernel's block
+// partials in k_dot_final's order, so all blocks hold identical values and no block
+// waits on another.  scal: [0] rr0, [1] rr of this iteration (for beta), [3] current rr.
+//   k_cg_update_fused: pq = sum(pq partials); a = scal[3] / pq; x += a p; r -= a q;
+//                      r.r partials into part_rr; block 0 saves scal[1] = scal[3]
+//   k_cg_direction_fused: rr_new = sum(part_rr); p = r + (rr_new / scal[1]) p;
+//                      block 0: scal[3] = rr_new, count, stop test (k_cg_check)
+__global__ void __launch_bounds__(256) k_cg_update_fused(double *__restrict__ scal, const double *__restrict__ part_pq,
+                                                         int npq, double *__restrict__ x, double *__restrict__ r,
+                                                         const double *__restrict__ p, const double *__restrict__ q,
+                                                         int64_t n, double *__restrict__ part_rr,
+                                                         const int32_t *__restrict__ done)
+{
+    __shared__ double red[4];
+    if (cg_done(done)) return;
+    const double pq = block_final_sum(part_pq, npq, red);
+    const double rr = scal[3];
+    const double a = rr / pq;
+    __syncthreads();
+    double acc = 0.0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        x[i] += a * p[i];
+        const double ri = r[i] - a * q[i];
+        r[i] = ri;
+        acc = fma(ri, ri, acc);
+    }
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        part_rr[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+        if (blockIdx.x == 0) { scal[1] = rr; scal[2] = pq; }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_cg_direction_fused(double *__restrict__ scal, const double *__restrict__ part_rr,
+                                                            int nrr, double *__restrict__ p, const double *__restrict__ r,
+                                                            int64_t n, int32_t *flags)
+{
+    __shared__ double red[4];
+    if (flags[0]) return;
+    const double rrn = block_final_sum(part_rr, nrr, red);
+    const double beta = rrn / scal[1];
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        p[i] = r[i] + beta * p[i];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        scal[3] = rrn;
+        flags[1] += 1;
+        const double delta = rrn / scal[0];
+        if (isnan(delta) || delta < scal[4]) flags[0] = 1;
+    }
 }
 
 __global__ void k_cg_direction(const double *__restrict__ rr_new, const double *__restrict__ rr, double *__restrict__ p,
@@ -468,7 +529,7 @@ extern "C" int comap_destripe_create(comap_ctx *ctx, const int32_t *pix, const d
     rc |= dalloc(ctx, &d->h, npix);
     rc |= dalloc(ctx, &d->hits, npix);
     rc |= dalloc(ctx, &d->nnum, npix);
-    rc |= dalloc(ctx, &d->part, kPartMax);
+    rc |= dalloc(ctx, &d->part, 2 * (size_t)kPartMax);   // [0, kPartMax): p.q / dots, then r.r of the fused CG
     rc |= dalloc(ctx, &d->scal, 16);
     if (rc) { comap_destripe_destroy(d); return -2; }
     // ---- offset-major entries
@@ -689,12 +750,14 @@ static void enqueue_iteration(comap_destriper *d, hipStream_t st)
     const int32_t *done = d->flags;
     // the bin writes the map m = (W p) / h itself, so the projection gathers one array
     k_ds_bin<<<grid_for(np * kBinLanes), 256, 0, st>>>(d->prow, d->poff, d->pw, p, np, nullptr, d->h, num, done);
+    // 4 launches per iteration: the p.q / r.r finals and the stop test are folded into
+    // the update and direction kernels (same arithmetic and order as k_dot_final + k_cg_check)
+    (void)rr; (void)pq; (void)rrn;
     const unsigned pg = launch_project(d, st, p, num, nullptr, q, d->part, done);
-    k_dot_final<<<1, 256, 0, st>>>(d->part, (int)pg, pq, done);
-    k_cg_update<<<kRedBlocks, 256, 0, st>>>(rr, pq, x, r, p, q, NO, d->part, done);
-    k_dot_final<<<1, 256, 0, st>>>(d->part, kRedBlocks, rrn, done);
-    k_cg_direction<<<grid_for(NO), 256, 0, st>>>(rrn, rr, p, r, NO, done);
-    k_cg_check<<<1, 64, 0, st>>>(d->scal, d->flags);
+    k_cg_update_fused<<<kRedBlocks, 256, 0, st>>>(d->scal, d->part, (int)pg, x, r, p, q, NO, d->part + kPartMax,
+                                                  done);
+    k_cg_direction_fused<<<grid_for(NO), 256, 0, st>>>(d->scal, d->part + kPartMax, kRedBlocks, p, r, NO,
+                                                       d->flags);
 }
 
 // CG state, stream and the kCgBatch-iteration graph, created on first use.
@@ -746,6 +809,7 @@ extern "C" int comap_destripe_solve(comap_destriper *d, double threshold, int32_
     k_dot_final<<<1, 256, 0, st>>>(d->part, kRedBlocks, d->scal, nullptr);
     COMAP_LAUNCH_CHECK(ctx);
     COMAP_CHECK(ctx, hipMemcpyAsync(d->scal + 1, d->scal, 8, hipMemcpyDeviceToDevice, st));
+    COMAP_CHECK(ctx, hipMemcpyAsync(d->scal + 3, d->scal, 8, hipMemcpyDeviceToDevice, st));   // current rr (fused CG)
     d->flags_host[0] = d->flags_host[1] = 0;
     for (int enq = 0; enq < niter;) {
         const int k = std::min(kCgBatch, niter - enq);

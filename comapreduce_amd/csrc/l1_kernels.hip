@@ -608,7 +608,10 @@ __global__ void __launch_bounds__(256) k_series_sums(int ub0, const int32_t *__r
 // A: a wave owns kRPW entries of the (unit, band)'s channel list and walks
 // the scan 4 samples per lane, sharing the mf loads between its rows.  Bands
 // the median filter skipped need no regression and are not read.
-constexpr int kRPW = 8;
+#ifndef COMAP_RPW
+#define COMAP_RPW 8
+#endif
+constexpr int kRPW = COMAP_RPW;
 constexpr int kRegBlocks = kChannels / (4 * kRPW);   // blocks per (unit, band)
 __global__ void __launch_bounds__(256) k_regress(int ub0, const float *__restrict__ tod, const double *__restrict__ mf,
                                                  const int32_t *__restrict__ units, int64_t T,
