@@ -58,7 +58,6 @@ namespace {
 
 constexpr int kRedBlocks = 256;
 constexpr int kPartMax = 8192;     // >= every reduction grid below
-constexpr int kBinLanes = 16;      // lanes per pixel row in k_ds_bin
 constexpr int kBinU = 4;           // entry loads in flight per lane (k_ds_bin)
 constexpr int kProjU = 4;          // entry loads in flight per lane (k_ds_project)
 constexpr int kCgBatch = 16;       // CG iterations per replayed graph (one host check per batch)
@@ -249,6 +248,7 @@ __device__ __forceinline__ double map_value(const double *num, const double *h, 
 // one array).  kBinLanes lanes per pixel row (rows hold 0 .. thousands of entries),
 // lane-strided; each lane issues kBinU entry loads, then kBinU gathers, before its fmas
 // (in entry order, so the sum is the plain lane-strided one), then a kBinLanes-lane reduction.
+template <int kBinLanes>
 __global__ void __launch_bounds__(256) k_ds_bin(const int64_t *__restrict__ prow, const int32_t *__restrict__ poff,
                                                 const double *__restrict__ pw, const double *__restrict__ x,
                                                 int64_t npix, const double *__restrict__ base,
@@ -467,6 +467,24 @@ __global__ void k_div_map(const double *__restrict__ num, const double *__restri
 }
 
 inline unsigned grid_for(int64_t n, int64_t cap = 4096) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, cap)); }
+// k_ds_bin with kBinLanes sized to the mean pixel-row length (sparse C4-like maps
+// hold ~5 entries per pixel: 16 lanes per row would leave most lanes idle and
+// need several latency-bound grid sweeps); one sweep over all rows.
+void launch_bin(const comap_destriper *d, hipStream_t st, const double *x, const double *base, const double *hdiv,
+                double *num, const int32_t *done)
+{
+    const int64_t np = d->npix;
+    const int64_t mean = np ? d->nnzp / np : 0;
+    const int lanes = mean >= 24 ? 16 : (mean >= 10 ? 8 : 4);
+    const unsigned g = grid_for(np * lanes, 65536);
+    if (lanes == 16)
+        k_ds_bin<16><<<g, 256, 0, st>>>(d->prow, d->poff, d->pw, x, np, base, hdiv, num, done);
+    else if (lanes == 8)
+        k_ds_bin<8><<<g, 256, 0, st>>>(d->prow, d->poff, d->pw, x, np, base, hdiv, num, done);
+    else
+        k_ds_bin<4><<<g, 256, 0, st>>>(d->prow, d->poff, d->pw, x, np, base, hdiv, num, done);
+}
+
 inline int project_lanes(int L) { return L <= 64 ? 16 : (L <= 128 ? 32 : 64); }
 inline unsigned project_grid(int64_t NO, int L)
 {
@@ -631,9 +649,7 @@ extern "C" int comap_destripe_bin(comap_destriper *d, const double *x, int32_t m
 {
     if (!d || !x || !num) return -1;
     comap_ctx *ctx = d->ctx;
-    k_ds_bin<<<grid_for(d->npix * kBinLanes), 256, 0, ctx->stream>>>(d->prow, d->poff, d->pw, x, d->npix,
-                                                                      mode == 1 ? d->nnum : nullptr, nullptr, num,
-                                                                      nullptr);
+    launch_bin(d, ctx->stream, x, mode == 1 ? d->nnum : nullptr, nullptr, num, nullptr);
     COMAP_LAUNCH_CHECK(ctx);
     return 0;
 }
@@ -700,8 +716,7 @@ extern "C" int comap_destripe_dist_bin(comap_destriper *d, const double *p, doub
 {
     if (!d || !p || !num || !flags) return -1;
     comap_ctx *ctx = d->ctx;
-    k_ds_bin<<<grid_for(d->npix * kBinLanes), 256, 0, ctx->stream>>>(d->prow, d->poff, d->pw, p, d->npix, nullptr,
-                                                                      nullptr, num, flags);
+    launch_bin(d, ctx->stream, p, nullptr, nullptr, num, flags);
     COMAP_LAUNCH_CHECK(ctx);
     return 0;
 }
@@ -741,18 +756,16 @@ extern "C" int comap_destripe_dist_direction(comap_destriper *d, double *scal, d
 
 // ---------------------------------------------------------------- device-resident CG
 // One CG iteration (Destriper.py:85-152 with p == pb, r == rb) on the problem's own
-// vectors; every kernel returns at once after k_cg_check has set the stop flag.
+// vectors; every kernel returns at once after the stop flag is set.
 static void enqueue_iteration(comap_destriper *d, hipStream_t st)
 {
-    const int64_t NO = d->NO, np = d->npix;
+    const int64_t NO = d->NO;
     double *x = d->cg, *r = x + NO, *p = r + NO, *q = p + NO, *num = q + NO;
-    double *rr = d->scal + 1, *pq = d->scal + 2, *rrn = d->scal + 3;
     const int32_t *done = d->flags;
     // the bin writes the map m = (W p) / h itself, so the projection gathers one array
-    k_ds_bin<<<grid_for(np * kBinLanes), 256, 0, st>>>(d->prow, d->poff, d->pw, p, np, nullptr, d->h, num, done);
+    launch_bin(d, st, p, nullptr, d->h, num, done);
     // 4 launches per iteration: the p.q / r.r finals and the stop test are folded into
     // the update and direction kernels (same arithmetic and order as k_dot_final + k_cg_check)
-    (void)rr; (void)pq; (void)rrn;
     const unsigned pg = launch_project(d, st, p, num, nullptr, q, d->part, done);
     k_cg_update_fused<<<kRedBlocks, 256, 0, st>>>(d->scal, d->part, (int)pg, x, r, p, q, NO, d->part + kPartMax,
                                                   done);
@@ -828,8 +841,7 @@ extern "C" int comap_destripe_solve(comap_destriper *d, double threshold, int32_
     COMAP_CHECK(ctx, hipMemcpyAsync(x, cx, 8 * NO, hipMemcpyDeviceToDevice, st));
     // final maps: map = (sum w tod - W x) / h ; naive = sum w tod / h
     if (map) {
-        k_ds_bin<<<grid_for(np * kBinLanes), 256, 0, st>>>(d->prow, d->poff, d->pw, cx, np, d->nnum, nullptr, num,
-                                                           nullptr);
+        launch_bin(d, st, cx, d->nnum, nullptr, num, nullptr);
         k_div_map<<<grid_for(np), 256, 0, st>>>(num, d->h, np, map);
     }
     if (naive) k_div_map<<<grid_for(np), 256, 0, st>>>(d->nnum, d->h, np, naive);
