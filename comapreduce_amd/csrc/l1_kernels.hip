@@ -26,6 +26,12 @@
 
 using namespace comap;
 
+#ifndef COMAP_ALIGN_A
+#define COMAP_ALIGN_A 0      // pass A: peel to 128-B row alignment (measured slower: 9.27 -> 9.61 ms at C2)
+#endif
+#ifndef COMAP_ALIGN_C
+#define COMAP_ALIGN_C 1      // pass C: peel to 128-B row alignment (measured 8.98 -> 8.82 ms at C2)
+#endif
 #ifndef COMAP_GROUPS
 #define COMAP_GROUPS 1      // unit groups of the pass B / median / pass C pipeline (2 measured no faster with the sort-path median)
 #endif
@@ -165,7 +171,7 @@ __global__ void __launch_bounds__(256) k_moments(const float *__restrict__ tod, 
 #pragma unroll
     for (int r = 0; r < kCPW; ++r) { sd[r] = sad[r] = su[r] = suu[r] = suv[r] = 0.0; bad[r] = 0; }
     const int n4 = n >> 2;
-    for (int k = lane; k < n4; k += 64) {
+    auto group = [&](int k) {
         const double a0 = a[4 * k], a1 = a[4 * k + 1], a2 = a[4 * k + 2], a3 = a[4 * k + 3];
         const double v = a0 - a2;
 #pragma unroll
@@ -183,7 +189,14 @@ __global__ void __launch_bounds__(256) k_moments(const float *__restrict__ tod, 
             suu[r] = fma(uu, uu, suu[r]);
             suv[r] = fma(uu, v, suv[r]);
         }
-    }
+    };
+    // groups of 4 stay on the scan's stride-4 pairs (normalise_data); when the row start
+    // is 16-B aligned, peel the groups before its first 128-B boundary so every wave
+    // load covers 8 whole lines
+    const int64_t idx0 = row0 - tod;
+    const int hg = (COMAP_ALIGN_A && (idx0 & 3) == 0) ? min(n4, (int)((-idx0) & 31) >> 2) : 0;
+    if (lane < hg) group(lane);
+    for (int k = hg + lane; k < n4; k += 64) group(k);
     // tail samples n4*4 .. n-1 (at most 3)
     const int tt = 4 * n4 + lane;
     if (lane < 4 && tt < n) {
@@ -635,7 +648,22 @@ __global__ void __launch_bounds__(256) k_regress(int ub0, const float *__restric
     double acc[kRPW];
 #pragma unroll
     for (int r = 0; r < kRPW; ++r) acc[r] = 0.0;
-    const int n4 = n >> 2;
+#if COMAP_ALIGN_C
+    // peel the samples before the first 128-B boundary of row 0 (every row of the
+    // band shares it when T is a multiple of 32), so each wave load covers 8 whole lines
+    const int head = (int)min((int64_t)n, (-(int64_t)(row[0] - tod)) & 31);
+    if (lane < head) {
+#pragma unroll
+        for (int r = 0; r < kRPW; ++r) acc[r] = fma(m[lane], (double)row[r][lane], acc[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < kRPW; ++r) row[r] += head;
+    m += head;
+    const int nb = n - head;
+#else
+    const int nb = n;
+#endif
+    const int n4 = nb >> 2;
     for (int k = lane; k < n4; k += 64) {
         const double m0 = m[4 * k], m1 = m[4 * k + 1], m2 = m[4 * k + 2], m3 = m[4 * k + 3];
 #pragma unroll
@@ -650,7 +678,7 @@ __global__ void __launch_bounds__(256) k_regress(int ub0, const float *__restric
         }
     }
     const int tt = 4 * n4 + lane;
-    if (lane < 4 && tt < n) {
+    if (lane < 4 && tt < nb) {
 #pragma unroll
         for (int r = 0; r < kRPW; ++r) acc[r] = fma(m[tt], (double)row[r][tt], acc[r]);
     }
