@@ -100,6 +100,10 @@ struct comap_l1_plan {
     int32_t *units = nullptr;          // dev [U][4]
     int32_t *tiles = nullptr;          // dev [NT][2] (unit, t_off)
     int64_t n_tiles = 0;
+    // pass-B tiles: per unit from t_off = -(t0 mod 32) when T is a multiple of 32, so the
+    // 4 KB row runs start on 128-B boundaries (the few samples before the scan are read
+    // from the same row and never written out)
+    int32_t *tiles_b = nullptr;        // dev [NTB][2] (unit, t_off)
     // pass B -> median -> pass C software pipeline over unit groups (comap_l1_average):
     // group g = units [grp_u0[g], grp_u0[g+1]) = tiles [grp_tile0[g], grp_tile0[g+1]);
     // its sliding medians (one job per (unit, band)) run on the side stream
@@ -107,6 +111,7 @@ struct comap_l1_plan {
     int32_t ngroups = 0;
     int32_t grp_u0[kMaxGroups + 1] = {0};
     int64_t grp_tile0[kMaxGroups + 1] = {0};
+    int64_t grpb_tile0[kMaxGroups + 1] = {0};
     MedPlan medg[kMaxGroups];
     hipStream_t side = nullptr;
     hipEvent_t ev_b[kMaxGroups] = {}, ev_m[kMaxGroups] = {};

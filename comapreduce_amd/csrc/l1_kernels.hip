@@ -32,6 +32,9 @@ using namespace comap;
 #ifndef COMAP_ALIGN_C
 #define COMAP_ALIGN_C 1      // pass C: peel to 128-B row alignment (measured 8.98 -> 8.82 ms at C2)
 #endif
+#ifndef COMAP_ALIGN_B
+#define COMAP_ALIGN_B 1      // pass B: 128-B aligned tiles
+#endif
 #ifndef COMAP_GROUPS
 #define COMAP_GROUPS 1      // unit groups of the pass B / median / pass C pipeline (2 measured no faster with the sort-path median)
 #endif
@@ -574,7 +577,7 @@ __global__ void __launch_bounds__(256) k_band_sums(const float *__restrict__ tod
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int i = 4 * g + e, o = 256 * g + e;
-            if (o >= nv0) continue;
+            if (o >= nv0 || r0 + o < 0) continue;   // before the scan: aligned-tile lead-in
             mb[rowo + o] = cn > 0 ? (acc.m[i] - beta - gamma * a[o]) / cn : NAN;
             sr_out[rowo + o] = acc.r[i];
             so_out[rowo + o] = acc.o[i];
@@ -1234,6 +1237,13 @@ extern "C" int comap_l1_plan_create(comap_ctx *ctx, const comap_obs_desc *d, com
     for (int u = 0; u < p->U; ++u)
         for (int t = 0; t < p->units_h[4 * u + 3]; t += kTile) { tiles.push_back(u); tiles.push_back(t); }
     p->n_tiles = (int64_t)tiles.size() / 2;
+    std::vector<int32_t> tiles_b;
+    std::vector<int64_t> tub(p->U + 1, 0);
+    for (int u = 0; u < p->U; ++u) {
+        const int shift = (COMAP_ALIGN_B && p->T % 32 == 0) ? (p->units_h[4 * u + 2] & 31) : 0;
+        for (int t = -shift; t < p->units_h[4 * u + 3]; t += kTile) { tiles_b.push_back(u); tiles_b.push_back(t); }
+        tub[u + 1] = (int64_t)tiles_b.size() / 2;
+    }
     const int64_t UC = (int64_t)p->U * kBC;
     int rc = 0;
     rc |= dalloc(ctx, &p->flag, 1);
@@ -1244,6 +1254,7 @@ extern "C" int comap_l1_plan_create(comap_ctx *ctx, const comap_obs_desc *d, com
     if (hipEventCreateWithFlags(&p->mom_event, hipEventDisableTiming) != hipSuccess) rc |= 1;
     rc |= upload(ctx, (void **)&p->units, p->units_h.data(), p->units_h.size() * 4);
     rc |= upload(ctx, (void **)&p->tiles, tiles.data(), tiles.size() * 4);
+    rc |= upload(ctx, (void **)&p->tiles_b, tiles_b.data(), tiles_b.size() * 4);
     rc |= dalloc(ctx, &p->airmass, (size_t)p->F * p->T);
     rc |= dalloc(ctx, &p->unit_sums, 8 * (size_t)p->U);
     rc |= dalloc(ctx, &p->mom, 5 * (size_t)UC);
@@ -1274,6 +1285,7 @@ extern "C" int comap_l1_plan_create(comap_ctx *ctx, const comap_obs_desc *d, com
         for (int g = 0; g <= p->ngroups; ++g) {
             p->grp_u0[g] = (int32_t)((int64_t)p->U * g / p->ngroups);
             p->grp_tile0[g] = tu[p->grp_u0[g]];
+            p->grpb_tile0[g] = tub[p->grp_u0[g]];
         }
     }
     bool ok = hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking) == hipSuccess;
@@ -1317,7 +1329,7 @@ extern "C" int comap_l1_plan_destroy(comap_l1_plan *p)
 {
     if (!p) return 0;
     if (p->side) (void)hipStreamSynchronize(p->side);
-    void *bufs[] = {p->units, p->tiles, p->airmass, p->unit_sums, p->mom,
+    void *bufs[] = {p->units, p->tiles, p->tiles_b, p->airmass, p->unit_sums, p->mom,
                     p->nan_count, p->alpha, p->nf, p->bsum, p->mb, p->mf, p->ssum, p->sdm, p->gw,
                     p->gmode, p->kap, p->dsum, p->xreg, p->dG, p->rowbad, p->ubs, p->fitsum, p->oa,
                     p->flag, p->dlist, p->dcnt, p->dw};
@@ -1557,9 +1569,9 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
     // so each group's median (latency-bound) runs under the next group's streaming pass.
     hipStream_t side = p->side;
     for (int g = 0; g < p->ngroups; ++g) {
-        const int64_t t0 = p->grp_tile0[g], nt = p->grp_tile0[g + 1] - t0;
+        const int64_t t0 = p->grpb_tile0[g], nt = p->grpb_tile0[g + 1] - t0;
         const int ub0 = p->grp_u0[g] * kBands, nub = (p->grp_u0[g + 1] - p->grp_u0[g]) * kBands;
-        PROF(p, KV_BAND_SUMS, k_band_sums<<<kSubB * nt, 256, 0, st>>>(p->tod, p->airmass, p->units, p->tiles, t0,
+        PROF(p, KV_BAND_SUMS, k_band_sums<<<kSubB * nt, 256, 0, st>>>(p->tod, p->airmass, p->units, p->tiles_b, t0,
                                                                     p->T, p->dlist, p->dcnt, p->dw, p->bsum,
                                                                     p->mb, tod_out, orig_out, p->dG));
         COMAP_LAUNCH_CHECK(ctx);
