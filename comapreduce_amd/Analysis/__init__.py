@@ -8,3 +8,7 @@ from ..stages.level1 import (MeasureSystemTemperature, AtmosphereRemoval,  # noq
                              AssignLevel1Data)
 from ..stages.statistics import Spikes, NoiseStatistics  # noqa: F401,E402
 from ..stages.level2 import Level2FitPowerSpectrum  # noqa: F401,E402
+
+STAGES = ('CheckLevel1File', 'AssignLevel1Data', 'MeasureSystemTemperature', 'AtmosphereRemoval',
+          'Level1AveragingGainCorrection', 'Level1Averaging', 'Level2FitPowerSpectrum', 'Spikes',
+          'NoiseStatistics')

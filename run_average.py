@@ -29,7 +29,11 @@ def create_tod_processing(configuration, rank=0, size=1, device=0):
     processes = {Analysis.CheckLevel1File: {'overwrite': True},
                  Analysis.AssignLevel1Data: {'overwrite': False, 'write': True}}
     for name in g['processes']:
-        cls = getattr(Analysis, name)
+        cls = getattr(Analysis, name, None)
+        if cls is None:
+            raise NotImplementedError(
+                f"stage {name!r} is not provided by comapreduce_amd (outside the L1->L2 / noise-QA scope of "
+                f"DESIGN.md; available: {', '.join(Analysis.STAGES)}); remove it from [Global] processes")
         kw = dict(configuration.get(name, {}))
         kw['figure_directory'] = g['level2_figures']
         if 'device' in getattr(cls, '__dataclass_fields__', {}):
