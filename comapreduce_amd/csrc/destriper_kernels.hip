@@ -47,6 +47,8 @@ struct comap_destriper {
     // device-resident CG of comap_destripe_solve (fixed pointers: graph-replayable)
     double *cg = nullptr;          // [4 NO + npix]: x, r, p, q | num
     int32_t *flags = nullptr;      // [2]: stop, iterations
+    int32_t *hrow = nullptr;       // [nh] pixel rows with entries (the CG bin skips empty rows)
+    int64_t nh = 0;
     int32_t *flags_host = nullptr; // pinned [2]
     double *thr_host = nullptr;    // pinned [1]
     hipStream_t cs = nullptr;      // CG stream (graph capture needs a non-default stream)
@@ -253,12 +255,14 @@ __global__ void __launch_bounds__(256) k_ds_bin(const int64_t *__restrict__ prow
                                                 const double *__restrict__ pw, const double *__restrict__ x,
                                                 int64_t npix, const double *__restrict__ base,
                                                 const double *__restrict__ hdiv, double *__restrict__ num,
-                                                const int32_t *__restrict__ done)
+                                                const int32_t *__restrict__ done, const int32_t *__restrict__ rows = nullptr)
 {
     if (cg_done(done)) return;
     const int sub = threadIdx.x & (kBinLanes - 1);
     const int64_t step = (int64_t)gridDim.x * blockDim.x / kBinLanes;
-    for (int64_t p = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kBinLanes; p < npix; p += step) {
+    // rows != NULL: only the listed (non-empty) rows, npix = their count
+    for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kBinLanes; i < npix; i += step) {
+        const int64_t p = rows ? (int64_t)rows[i] : i;
         double s = 0.0;
         const int64_t e1 = prow[p + 1];
         for (int64_t k = prow[p] + sub; k < e1; k += kBinLanes * kBinU) {
@@ -470,19 +474,22 @@ inline unsigned grid_for(int64_t n, int64_t cap = 4096) { return (unsigned)std::
 // k_ds_bin with kBinLanes sized to the mean pixel-row length (sparse C4-like maps
 // hold ~5 entries per pixel: 16 lanes per row would leave most lanes idle and
 // need several latency-bound grid sweeps); one sweep over all rows.
+// hit_rows: only the non-empty rows (d->hrow; the caller's num must hold 0 on the
+// empty rows, as the CG's own map buffer does).
 void launch_bin(const comap_destriper *d, hipStream_t st, const double *x, const double *base, const double *hdiv,
-                double *num, const int32_t *done)
+                double *num, const int32_t *done, bool hit_rows = false)
 {
-    const int64_t np = d->npix;
+    const int64_t np = hit_rows ? d->nh : d->npix;
+    const int32_t *rows = hit_rows ? d->hrow : nullptr;
     const int64_t mean = np ? d->nnzp / np : 0;
     const int lanes = mean >= 24 ? 16 : (mean >= 10 ? 8 : 4);
     const unsigned g = grid_for(np * lanes, 65536);
     if (lanes == 16)
-        k_ds_bin<16><<<g, 256, 0, st>>>(d->prow, d->poff, d->pw, x, np, base, hdiv, num, done);
+        k_ds_bin<16><<<g, 256, 0, st>>>(d->prow, d->poff, d->pw, x, np, base, hdiv, num, done, rows);
     else if (lanes == 8)
-        k_ds_bin<8><<<g, 256, 0, st>>>(d->prow, d->poff, d->pw, x, np, base, hdiv, num, done);
+        k_ds_bin<8><<<g, 256, 0, st>>>(d->prow, d->poff, d->pw, x, np, base, hdiv, num, done, rows);
     else
-        k_ds_bin<4><<<g, 256, 0, st>>>(d->prow, d->poff, d->pw, x, np, base, hdiv, num, done);
+        k_ds_bin<4><<<g, 256, 0, st>>>(d->prow, d->poff, d->pw, x, np, base, hdiv, num, done, rows);
 }
 
 inline int project_lanes(int L) { return L <= 64 ? 16 : (L <= 128 ? 32 : 64); }
@@ -589,7 +596,19 @@ extern "C" int comap_destripe_create(comap_ctx *ctx, const int32_t *pix, const d
     k_rowptr<<<grid_for(npix + 1), 256, 0, st>>>(k1, d->nnz, npix, d->prow);
     COMAP_LAUNCH_CHECK(ctx);
     COMAP_CHECK(ctx, hipMemcpyAsync(&d->nnzp, d->prow + npix, 8, hipMemcpyDeviceToHost, st));
-    COMAP_CHECK(ctx, hipStreamSynchronize(st));
+    {
+        std::vector<int64_t> ph(npix + 1);
+        COMAP_CHECK(ctx, hipMemcpyAsync(ph.data(), d->prow, 8 * (size_t)(npix + 1), hipMemcpyDeviceToHost, st));
+        COMAP_CHECK(ctx, hipStreamSynchronize(st));
+        std::vector<int32_t> hr;
+        for (int64_t q = 0; q < npix; ++q)
+            if (ph[q + 1] > ph[q]) hr.push_back((int32_t)q);
+        d->nh = (int64_t)hr.size();
+        rc |= dalloc(ctx, &d->hrow, hr.size());
+        if (!rc && !hr.empty())
+            COMAP_CHECK(ctx, hipMemcpyAsync(d->hrow, hr.data(), 4 * hr.size(), hipMemcpyHostToDevice, st));
+        COMAP_CHECK(ctx, hipStreamSynchronize(st));
+    }
     rc |= dalloc(ctx, &d->poff, d->nnzp);
     rc |= dalloc(ctx, &d->pw, d->nnzp);
     if (rc) { comap_destripe_destroy(d); return -2; }
@@ -612,7 +631,7 @@ extern "C" int comap_destripe_destroy(comap_destriper *d)
     if (!d) return 0;
     if (d->cs) (void)hipStreamSynchronize(d->cs);
     void *b[] = {d->orow, d->opix, d->ow, d->ws, d->tw, d->prow, d->poff, d->pw, d->h, d->hits, d->nnum, d->part, d->scal,
-                 d->cg, d->flags};
+                 d->cg, d->flags, d->hrow};
     for (void *p : b)
         if (p) (void)hipFree(p);
     if (d->flags_host) (void)hipHostFree(d->flags_host);
@@ -763,7 +782,7 @@ static void enqueue_iteration(comap_destriper *d, hipStream_t st)
     double *x = d->cg, *r = x + NO, *p = r + NO, *q = p + NO, *num = q + NO;
     const int32_t *done = d->flags;
     // the bin writes the map m = (W p) / h itself, so the projection gathers one array
-    launch_bin(d, st, p, nullptr, d->h, num, done);
+    launch_bin(d, st, p, nullptr, d->h, num, done, true);   // empty rows of num stay 0
     // 4 launches per iteration: the p.q / r.r finals and the stop test are folded into
     // the update and direction kernels (same arithmetic and order as k_dot_final + k_cg_check)
     const unsigned pg = launch_project(d, st, p, num, nullptr, q, d->part, done);
@@ -813,6 +832,7 @@ extern "C" int comap_destripe_solve(comap_destriper *d, double threshold, int32_
     d->thr_host[0] = threshold;
     COMAP_CHECK(ctx, hipMemcpyAsync(d->scal + 4, d->thr_host, 8, hipMemcpyHostToDevice, st));
     COMAP_CHECK(ctx, hipMemsetAsync(cx, 0, 8 * NO, st));
+    COMAP_CHECK(ctx, hipMemsetAsync(num, 0, 8 * np, st));   // the CG bin writes only the non-empty rows
     COMAP_CHECK(ctx, hipMemsetAsync(d->flags, 0, 8, st));
     // b = op_Ax(tod, extend=False); r = p = b (x0 = 0); rr = rr0 = b.b
     launch_project(d, st, nullptr, d->nnum, d->h, r, nullptr, nullptr);
