@@ -40,6 +40,18 @@ using namespace comap;
 #endif
 
 typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
+#ifndef COMAP_NT
+#define COMAP_NT 1   // measured at C2: pass B 9.55 -> 8.75 ms, pass C 8.86 -> 7.89 ms, pass A unchanged
+#endif
+// streaming load of 4 cube samples (COMAP_NT: non-temporal, no L2 allocation)
+__device__ __forceinline__ f32x4u ld4(const float *p)
+{
+#if COMAP_NT
+    return __builtin_nontemporal_load(reinterpret_cast<const f32x4u *>(p));
+#else
+    return *reinterpret_cast<const f32x4u *>(p);
+#endif
+}
 
 __device__ __forceinline__ double wave_sum(double v)
 {
@@ -179,7 +191,7 @@ __global__ void __launch_bounds__(256) k_moments(const float *__restrict__ tod, 
         const double v = a0 - a2;
 #pragma unroll
         for (int r = 0; r < kCPW; ++r) {
-            const f32x4u x = *reinterpret_cast<const f32x4u *>(row0 + (int64_t)r * T + 4 * k);
+            const f32x4u x = ld4(row0 + (int64_t)r * T + 4 * k);
             const double x0 = x.x, x1 = x.y, x2 = x.z, x3 = x.w;
             bad[r] += !isfinite(x.x) + !isfinite(x.y) + !isfinite(x.z) + !isfinite(x.w);
             sd[r] += (x0 + x1) + (x2 + x3);
@@ -473,7 +485,7 @@ __device__ __forceinline__ void load_raw(const float *__restrict__ p, int nv0, f
     for (int g = 0; g < J; ++g) {
         const int nv = nv0 - 256 * g;
         if (FULL || nv >= 4) {
-            r[g] = *reinterpret_cast<const f32x4u *>(p + 256 * g);
+            r[g] = ld4(p + 256 * g);
         } else {
             f32x4u v = {0.f, 0.f, 0.f, 0.f};
             if (nv > 0) v.x = p[256 * g];
@@ -671,7 +683,7 @@ __global__ void __launch_bounds__(256) k_regress(int ub0, const float *__restric
         const double m0 = m[4 * k], m1 = m[4 * k + 1], m2 = m[4 * k + 2], m3 = m[4 * k + 3];
 #pragma unroll
         for (int r = 0; r < kRPW; ++r) {
-            const f32x4u x = *reinterpret_cast<const f32x4u *>(row[r] + 4 * k);
+            const f32x4u x = ld4(row[r] + 4 * k);
             double s = acc[r];
             s = fma(m0, (double)x.x, s);
             s = fma(m1, (double)x.y, s);
