@@ -53,6 +53,19 @@ __device__ __forceinline__ f32x4u ld4(const float *p)
 #endif
 }
 
+#ifndef COMAP_NT_A
+#define COMAP_NT_A COMAP_NT   // measured at C2 (AUNR=4): NT 8.82 ms, plain 9.19 ms
+#endif
+// pass A's cube loads (COMAP_NT_A selects non-temporal independently of B / C)
+__device__ __forceinline__ f32x4u ld4a(const float *p)
+{
+#if COMAP_NT_A
+    return __builtin_nontemporal_load(reinterpret_cast<const f32x4u *>(p));
+#else
+    return *reinterpret_cast<const f32x4u *>(p);
+#endif
+}
+
 __device__ __forceinline__ double wave_sum(double v)
 {
 #pragma unroll
@@ -166,6 +179,9 @@ __global__ void __launch_bounds__(256) k_unit_sums(const int32_t *__restrict__ u
 #ifndef COMAP_CPW
 #define COMAP_CPW 4   // measured at C2: 8 rows per wave 9.28 -> 10.13 ms
 #endif
+#ifndef COMAP_AUNR
+#define COMAP_AUNR 4  // sample groups per lane per trip (loads in flight = COMAP_AUNR x kCPW); measured at C2: 1 -> 9.39 ms, 2 -> 9.15, 4 -> 8.82, 8 -> 9.08
+#endif
 constexpr int kCPW = COMAP_CPW;   // channel rows per wave
 __global__ void __launch_bounds__(256) k_moments(const float *__restrict__ tod, const double *__restrict__ A,
                                                  const int32_t *__restrict__ units, int64_t T,
@@ -194,7 +210,7 @@ __global__ void __launch_bounds__(256) k_moments(const float *__restrict__ tod, 
         const double v = a0 - a2;
 #pragma unroll
         for (int r = 0; r < kCPW; ++r) {
-            const f32x4u x = ld4(row0 + (int64_t)r * T + 4 * k);
+            const f32x4u x = ld4a(row0 + (int64_t)r * T + 4 * k);
             const double x0 = x.x, x1 = x.y, x2 = x.z, x3 = x.w;
             bad[r] += !isfinite(x.x) + !isfinite(x.y) + !isfinite(x.z) + !isfinite(x.w);
             sd[r] += (x0 + x1) + (x2 + x3);
@@ -214,7 +230,40 @@ __global__ void __launch_bounds__(256) k_moments(const float *__restrict__ tod, 
     const int64_t idx0 = row0 - tod;
     const int hg = (COMAP_ALIGN_A && (idx0 & 3) == 0) ? min(n4, (int)((-idx0) & 31) >> 2) : 0;
     if (lane < hg) group(lane);
-    for (int k = hg + lane; k < n4; k += 64) group(k);
+    int k = hg + lane;
+#if COMAP_AUNR > 1
+    // COMAP_AUNR sample groups per lane per trip: every row load of the trip is issued
+    // before any is accumulated (same per-lane summation order as the plain loop)
+    for (; k + 64 * (COMAP_AUNR - 1) < n4; k += 64 * COMAP_AUNR) {
+        f32x4u xs[COMAP_AUNR][kCPW];
+#pragma unroll
+        for (int j = 0; j < COMAP_AUNR; ++j)
+#pragma unroll
+            for (int r = 0; r < kCPW; ++r) xs[j][r] = ld4a(row0 + (int64_t)r * T + 4 * (k + 64 * j));
+#pragma unroll
+        for (int j = 0; j < COMAP_AUNR; ++j) {
+            const int kk = k + 64 * j;
+            const double a0 = a[4 * kk], a1 = a[4 * kk + 1], a2 = a[4 * kk + 2], a3 = a[4 * kk + 3];
+            const double v = a0 - a2;
+#pragma unroll
+            for (int r = 0; r < kCPW; ++r) {
+                const f32x4u x = xs[j][r];
+                const double x0 = x.x, x1 = x.y, x2 = x.z, x3 = x.w;
+                bad[r] += !isfinite(x.x) + !isfinite(x.y) + !isfinite(x.z) + !isfinite(x.w);
+                sd[r] += (x0 + x1) + (x2 + x3);
+                sad[r] = fma(a0, x0, sad[r]);
+                sad[r] = fma(a1, x1, sad[r]);
+                sad[r] = fma(a2, x2, sad[r]);
+                sad[r] = fma(a3, x3, sad[r]);
+                const double uu = x0 - x2;
+                su[r] += uu;
+                suu[r] = fma(uu, uu, suu[r]);
+                suv[r] = fma(uu, v, suv[r]);
+            }
+        }
+    }
+#endif
+    for (; k < n4; k += 64) group(k);
     // tail samples n4*4 .. n-1 (at most 3)
     const int tt = 4 * n4 + lane;
     if (lane < 4 && tt < n) {
