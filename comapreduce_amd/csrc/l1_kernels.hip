@@ -554,7 +554,7 @@ __device__ __forceinline__ void load_raw(const float *__restrict__ p, int nv0, f
 #define COMAP_KJB 4
 #endif
 #ifndef COMAP_BB
-#define COMAP_BB 2
+#define COMAP_BB 2   // measured at C2: 2 -> 8.76 ms, 4 -> 8.98
 #endif
 constexpr int kJB = COMAP_KJB;             // groups of 4 samples per lane
 constexpr int kBB = COMAP_BB;              // channel-list entries per load batch
@@ -691,6 +691,9 @@ __global__ void __launch_bounds__(256) k_series_sums(int ub0, const int32_t *__r
 #ifndef COMAP_RPW
 #define COMAP_RPW 8
 #endif
+#ifndef COMAP_CUNR
+#define COMAP_CUNR 1   // sample groups per lane per trip in pass C; measured at C2: 1 -> 7.90 ms, 2 -> 8.07, (RPW 4) 2 -> 8.64, 4 -> 8.39
+#endif
 constexpr int kRPW = COMAP_RPW;
 constexpr int kRegBlocks = kChannels / (4 * kRPW);   // blocks per (unit, band)
 __global__ void __launch_bounds__(256) k_regress(int ub0, const float *__restrict__ tod, const double *__restrict__ mf,
@@ -731,7 +734,32 @@ __global__ void __launch_bounds__(256) k_regress(int ub0, const float *__restric
     const int nb = n;
 #endif
     const int n4 = nb >> 2;
-    for (int k = lane; k < n4; k += 64) {
+    int k = lane;
+#if COMAP_CUNR > 1
+    // COMAP_CUNR sample groups per trip, all row loads issued first (per-lane order unchanged)
+    for (; k + 64 * (COMAP_CUNR - 1) < n4; k += 64 * COMAP_CUNR) {
+        f32x4u xs[COMAP_CUNR][kRPW];
+#pragma unroll
+        for (int j = 0; j < COMAP_CUNR; ++j)
+#pragma unroll
+            for (int r = 0; r < kRPW; ++r) xs[j][r] = ld4(row[r] + 4 * (k + 64 * j));
+#pragma unroll
+        for (int j = 0; j < COMAP_CUNR; ++j) {
+            const int kk = k + 64 * j;
+            const double m0 = m[4 * kk], m1 = m[4 * kk + 1], m2 = m[4 * kk + 2], m3 = m[4 * kk + 3];
+#pragma unroll
+            for (int r = 0; r < kRPW; ++r) {
+                double s = acc[r];
+                s = fma(m0, (double)xs[j][r].x, s);
+                s = fma(m1, (double)xs[j][r].y, s);
+                s = fma(m2, (double)xs[j][r].z, s);
+                s = fma(m3, (double)xs[j][r].w, s);
+                acc[r] = s;
+            }
+        }
+    }
+#endif
+    for (; k < n4; k += 64) {
         const double m0 = m[4 * k], m1 = m[4 * k + 1], m2 = m[4 * k + 2], m3 = m[4 * k + 3];
 #pragma unroll
         for (int r = 0; r < kRPW; ++r) {
