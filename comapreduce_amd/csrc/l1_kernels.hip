@@ -182,6 +182,12 @@ __global__ void __launch_bounds__(256) k_unit_sums(const int32_t *__restrict__ u
 #ifndef COMAP_AUNR
 #define COMAP_AUNR 4  // sample groups per lane per trip (loads in flight = COMAP_AUNR x kCPW); measured at C2: 1 -> 9.39 ms, 2 -> 9.15, 4 -> 8.82, 8 -> 9.08
 #endif
+#ifndef COMAP_A_BADSUM
+// 1: a row's non-finite flag is !isfinite(sum d) -- NaN/Inf propagate through the f64
+// sum and f32 samples cannot overflow it (|x| < 3.4e38, n < 2^31), so the flag is exact
+// and rowbad / nan_count count flagged rows; 0: per-sample isfinite counts
+#define COMAP_A_BADSUM 0
+#endif
 constexpr int kCPW = COMAP_CPW;   // channel rows per wave
 __global__ void __launch_bounds__(256) k_moments(const float *__restrict__ tod, const double *__restrict__ A,
                                                  const int32_t *__restrict__ units, int64_t T,
@@ -212,7 +218,7 @@ __global__ void __launch_bounds__(256) k_moments(const float *__restrict__ tod, 
         for (int r = 0; r < kCPW; ++r) {
             const f32x4u x = ld4a(row0 + (int64_t)r * T + 4 * k);
             const double x0 = x.x, x1 = x.y, x2 = x.z, x3 = x.w;
-            bad[r] += !isfinite(x.x) + !isfinite(x.y) + !isfinite(x.z) + !isfinite(x.w);
+            if (!COMAP_A_BADSUM) bad[r] += !isfinite(x.x) + !isfinite(x.y) + !isfinite(x.z) + !isfinite(x.w);
             sd[r] += (x0 + x1) + (x2 + x3);
             sad[r] = fma(a0, x0, sad[r]);
             sad[r] = fma(a1, x1, sad[r]);
@@ -249,7 +255,7 @@ __global__ void __launch_bounds__(256) k_moments(const float *__restrict__ tod, 
             for (int r = 0; r < kCPW; ++r) {
                 const f32x4u x = xs[j][r];
                 const double x0 = x.x, x1 = x.y, x2 = x.z, x3 = x.w;
-                bad[r] += !isfinite(x.x) + !isfinite(x.y) + !isfinite(x.z) + !isfinite(x.w);
+                if (!COMAP_A_BADSUM) bad[r] += !isfinite(x.x) + !isfinite(x.y) + !isfinite(x.z) + !isfinite(x.w);
                 sd[r] += (x0 + x1) + (x2 + x3);
                 sad[r] = fma(a0, x0, sad[r]);
                 sad[r] = fma(a1, x1, sad[r]);
@@ -271,7 +277,7 @@ __global__ void __launch_bounds__(256) k_moments(const float *__restrict__ tod, 
 #pragma unroll
         for (int r = 0; r < kCPW; ++r) {
             const float xf = row0[(int64_t)r * T + tt];
-            bad[r] += !isfinite(xf);
+            if (!COMAP_A_BADSUM) bad[r] += !isfinite(xf);
             sd[r] += (double)xf;
             sad[r] = fma(at, (double)xf, sad[r]);
         }
@@ -281,7 +287,7 @@ __global__ void __launch_bounds__(256) k_moments(const float *__restrict__ tod, 
     for (int r = 0; r < kCPW; ++r) {
         const double s0 = wave_sum(sd[r]), s1 = wave_sum(sad[r]), s2 = wave_sum(su[r]);
         const double s3 = wave_sum(suu[r]), s4 = wave_sum(suv[r]);
-        const int nb = (int)wave_sum((double)bad[r]);
+        const int nb = COMAP_A_BADSUM ? (int)!isfinite(s0) : (int)wave_sum((double)bad[r]);
         tot += nb;
         if (lane == 0) {
             const int64_t idx = (int64_t)u * kBC + b * kChannels + c0 + r;
