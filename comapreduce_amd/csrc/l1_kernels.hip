@@ -66,6 +66,16 @@ __device__ __forceinline__ f32x4u ld4a(const float *p)
 #endif
 }
 
+typedef float f32x4a __attribute__((ext_vector_type(4)));   // 16-B aligned
+__device__ __forceinline__ f32x4a ld4al(const float *p)
+{
+#if COMAP_NT_A
+    return __builtin_nontemporal_load(reinterpret_cast<const f32x4a *>(p));
+#else
+    return *reinterpret_cast<const f32x4a *>(p);
+#endif
+}
+
 __device__ __forceinline__ double wave_sum(double v)
 {
 #pragma unroll
@@ -182,6 +192,9 @@ __global__ void __launch_bounds__(256) k_unit_sums(const int32_t *__restrict__ u
 #ifndef COMAP_AUNR
 #define COMAP_AUNR 4  // sample groups per lane per trip (loads in flight = COMAP_AUNR x kCPW); measured at C2: 1 -> 9.39 ms, 2 -> 9.15, 4 -> 8.82, 8 -> 9.08
 #endif
+#ifndef COMAP_A_ALD
+#define COMAP_A_ALD 0   // >0: aligned 16-B loads + lane shuffle, COMAP_A_ALD groups per trip; measured at C2: 2 -> 17.0 ms, 4 -> 22.3 ms vs 8.85 off (parity green)
+#endif
 #ifndef COMAP_A_BADSUM
 // 1: a row's non-finite flag is !isfinite(sum d) -- NaN/Inf propagate through the f64
 // sum and f32 samples cannot overflow it (|x| < 3.4e38, n < 2^31), so the flag is exact
@@ -237,6 +250,59 @@ __global__ void __launch_bounds__(256) k_moments(const float *__restrict__ tod, 
     const int hg = (COMAP_ALIGN_A && (idx0 & 3) == 0) ? min(n4, (int)((-idx0) & 31) >> 2) : 0;
     if (lane < hg) group(lane);
     int k = hg + lane;
+#if COMAP_A_ALD
+    // Scan rows start 12 B into a 16-B chunk here (t0 = 3 mod 4), so the plain
+    // 16-B loads are misaligned.  Wave-uniform trips: lane l loads the aligned
+    // chunk l of the trip's row window, takes its neighbour's chunk by a lane
+    // shuffle (lane 63 loads chunk 64 itself) and assembles its 4 samples.
+    // Lane l still handles groups hg + l + 64 i in order (same sums).
+    for (int kb = hg; kb + 64 * COMAP_A_ALD <= n4; kb += 64 * COMAP_A_ALD, k += 64 * COMAP_A_ALD) {
+        f32x4a lo[COMAP_A_ALD][kCPW], ex[COMAP_A_ALD][kCPW];
+        int mis[kCPW];
+#pragma unroll
+        for (int r = 0; r < kCPW; ++r) mis[r] = uniform((int)((reinterpret_cast<uintptr_t>(row0 + (int64_t)r * T) >> 2) & 3));
+#pragma unroll
+        for (int j = 0; j < COMAP_A_ALD; ++j)
+#pragma unroll
+            for (int r = 0; r < kCPW; ++r) {
+                const float *q = row0 + (int64_t)r * T + 4 * (kb + 64 * j) - mis[r];
+                lo[j][r] = ld4al(q + 4 * lane);
+                ex[j][r] = lo[j][r];
+                if (lane == 63 && mis[r]) ex[j][r] = ld4al(q + 256);
+            }
+#pragma unroll
+        for (int j = 0; j < COMAP_A_ALD; ++j) {
+            const int kk = k + 64 * j;
+            const double a0 = a[4 * kk], a1 = a[4 * kk + 1], a2 = a[4 * kk + 2], a3 = a[4 * kk + 3];
+            const double v = a0 - a2;
+#pragma unroll
+            for (int r = 0; r < kCPW; ++r) {
+                const f32x4a L = lo[j][r];
+                f32x4a N;
+                N.x = __shfl_down(L.x, 1, 64); N.y = __shfl_down(L.y, 1, 64); N.z = __shfl_down(L.z, 1, 64);
+                if (lane == 63) { N.x = ex[j][r].x; N.y = ex[j][r].y; N.z = ex[j][r].z; }
+                float y0, y1, y2, y3;
+                switch (mis[r]) {
+                case 0: y0 = L.x; y1 = L.y; y2 = L.z; y3 = L.w; break;
+                case 1: y0 = L.y; y1 = L.z; y2 = L.w; y3 = N.x; break;
+                case 2: y0 = L.z; y1 = L.w; y2 = N.x; y3 = N.y; break;
+                default: y0 = L.w; y1 = N.x; y2 = N.y; y3 = N.z; break;
+                }
+                const double x0 = y0, x1 = y1, x2 = y2, x3 = y3;
+                if (!COMAP_A_BADSUM) bad[r] += !isfinite(y0) + !isfinite(y1) + !isfinite(y2) + !isfinite(y3);
+                sd[r] += (x0 + x1) + (x2 + x3);
+                sad[r] = fma(a0, x0, sad[r]);
+                sad[r] = fma(a1, x1, sad[r]);
+                sad[r] = fma(a2, x2, sad[r]);
+                sad[r] = fma(a3, x3, sad[r]);
+                const double uu = x0 - x2;
+                su[r] += uu;
+                suu[r] = fma(uu, uu, suu[r]);
+                suv[r] = fma(uu, v, suv[r]);
+            }
+        }
+    }
+#endif
 #if COMAP_AUNR > 1
     // COMAP_AUNR sample groups per lane per trip: every row load of the trip is issued
     // before any is accumulated (same per-lane summation order as the plain loop)
