@@ -4,21 +4,34 @@
 Metric (BASELINE.json): TOD samples x channels / s for the L1 -> L2 reduction
 (MeasureSystemTemperature -> AtmosphereRemoval -> Level1AveragingGainCorrection)
 of the full 19-feed x 4 x 1024-channel x 180,000-sample synthetic observation
-(configs[1], 56 GB f32 resident in HBM) per GPU, plus the destriper's CG
-iterations / s on the resulting band-0 Level-2 TOD.
+(configs[1], C2: 56 GB f32 resident in HBM), plus the destriper's CG
+iterations / s on that observation's Level-2 TOD (configs[3], C4) and on a
+multi-observation HBM-resident field (configs[4], C5).
 
-One step = one complete reduction of one observation (every kernel of the
+One step = one complete reduction of the observation (every kernel of the
 three stages; the plan/airmass set-up happens once per observation, like
-opening the file).  N GPUs: one process per GPU (torch.distributed.run), each
-reducing its own observation (obs_id = rank + 1) with no collective in the
-reduction -- the reference's file-level MPI parallelism -- so scaling is
-"weak"; the driver derives efficiency from the per-N values.
+opening the file).
 
-    python bench.py [--gpus N --steps K --warmup W]
+N GPUs (``--gpus N``; the script launches its own N ranks through
+torch.distributed.run when started without WORLD_SIZE, one process per GPU):
+  --mode shard (default)  configs[2], C3: ONE observation's (feed, scan) units
+                          are split over the ranks (pipeline/sharding.py), each
+                          rank generates and holds only its feeds, and reduces
+                          its units with no collective -> "scaling": "strong";
+                          value = the observation's samples x channels per step
+                          / the slowest rank's time.
+  --mode obs              one whole observation per rank (the reference's
+                          file-level MPI split) -> "scaling": "weak".
+The C5 destriper leg is weak-scaled (8 observations per GPU) with an RCCL
+all-reduce of the map numerator and CG scalars every iteration.
+
+    python bench.py [--gpus N --steps K --warmup W --mode shard|obs]
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,6 +46,8 @@ SURVEY_BYTES_PER_SAMPCH = 16        # 4 passes (A, B, C, D) x 
 # output sum, band_sums) and C (regression sums, regress); B and C read only the
 # median_filter channels
 HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+DESTRIPER_BYTES_PER_SAMPLE = 24     # per CG iteration
+DESTRIPER_BYTES_PER_OFFSET = 80
 
 
 def parse():
@@ -40,6 +55,8 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--mode', choices=('shard', 'obs'), default='shard',
+                    help='N > 1: shard one observation over the ranks (C3, strong) or one observation per rank (weak)')
     ap.add_argument('--feeds', type=int, default=19)
     ap.add_argument('--samples', type=int, default=180_000)
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -50,35 +67,70 @@ def parse():
     return ap.parse_args()
 
 
-def build_observation(F, T, obs_id, device):
-    """Device-resident synthetic Level-1 observation."""
+# ---------------------------------------------------------------- N-GPU launch
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """Run this script on n ranks (one process per GPU) via torch.distributed.run
+    and return its exit code.  Called before anything touches the GPU; the ranks
+    are child processes (no exec)."""
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={n}',
+           '--master-addr', '127.0.0.1', '--master-port', str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    return subprocess.run(cmd, env=env).returncode
+
+
+# ---------------------------------------------------------------- observation
+def build_observation(F, T, obs_id, device, rank=0, world=1):
+    """Device-resident synthetic Level-1 observation; with
+    world > 1 only this rank's shard: the feeds its (feed, scan) units touch,
+    generated on device with the same samples the full cube holds, and the
+    unit filter that restricts the reduction to its units.
+    Returns (COMAPLevel1, Shard)."""
     import torch
     from comapreduce_amd import _native as N
     from comapreduce_amd import synthetic
     from comapreduce_amd.pipeline.datahandling import COMAPLevel1
+    from comapreduce_amd.pipeline.sharding import shard_for, slice_feeds
     cfg = synthetic.SyntheticConfig(n_feeds=F, n_samples=T, obs_id=obs_id)
     meta, attrs, level, mult, hot = synthetic.level1_metadata(cfg)
+    full = COMAPLevel1(overwrite=False, large_datasets=['spectrometer/tod'])
+    for k, v in meta.items():
+        full[k] = v
+    for p, a in attrs.items():
+        for k, v in a.items():
+            full.set_attrs(p, k, v)
+    sh = shard_for(full.scan_edges, F, rank, world)
+    lo, hi = sh.f_lo, sh.f_hi
+    if hi <= lo:
+        raise RuntimeError(f'rank {rank}: no unit to reduce (world {world} > units)')
+    Fs = hi - lo
     dev = torch.device('cuda', device)
-    lv = torch.from_numpy(level).to(dev)
-    mu = torch.from_numpy(mult).to(dev)
-    ho = torch.from_numpy(hot).to(dev)
-    tod = torch.empty((F, 4, 1024, T), dtype=torch.float32, device=dev)
-    ba = torch.empty((F, 4, T), dtype=torch.float32, device=dev)
+    lv = torch.from_numpy(np.ascontiguousarray(level[lo:hi])).to(dev)
+    mu = torch.from_numpy(np.ascontiguousarray(mult[lo:hi])).to(dev)
+    ho = torch.from_numpy(np.ascontiguousarray(hot[lo:hi])).to(dev)
+    tod = torch.empty((Fs, 4, 1024, T), dtype=torch.float32, device=dev)
+    ba = torch.empty((Fs, 4, T), dtype=torch.float32, device=dev)
     c = N.ctx(device)
     N.bind_stream(c, dev)
-    N.check(N.lib().comap_synth_tod(c, F, T, 1000 + obs_id, N.dptr(lv), N.dptr(mu), N.dptr(ho), N.dptr(tod),
+    N.check(N.lib().comap_synth_tod(c, Fs, lo, T, 1000 + obs_id, N.dptr(lv), N.dptr(mu), N.dptr(ho), N.dptr(tod),
                                     N.dptr(ba)), c, 'comap_synth_tod')
     torch.cuda.synchronize(dev)
     del lv, mu, ho
-    data = COMAPLevel1(overwrite=False, large_datasets=['spectrometer/tod'])
-    for k, v in meta.items():
-        data[k] = v
-    data['spectrometer/tod'] = tod
-    data['spectrometer/band_average'] = ba
-    for p, a in attrs.items():
-        for k, v in a.items():
-            data.set_attrs(p, k, v)
-    return data
+    full['spectrometer/tod'] = tod
+    full['spectrometer/band_average'] = ba
+    if world == 1:
+        return full, sh
+    # the shard's feeds: tod/band_average already hold only them
+    part = slice_feeds(full, lo, hi, sh.local_filter())
+    part['spectrometer/tod'] = tod
+    part['spectrometer/band_average'] = ba
+    return part, sh
 
 
 def reduce_step(data, device, timing=None):
@@ -98,9 +150,15 @@ def reduce_step(data, device, timing=None):
     return level2
 
 
-def cpu_baseline():
-    """The CPU oracle (a NumPy/C restatement of the reference, 'port') on a
-    bounded sample: the C1 observation (1 feed x 4 x 1024 x 30,000)."""
+# ---------------------------------------------------------------- CPU baselines
+def cpu_baseline(level2=None, data=None):
+    """The CPU oracle (a NumPy/C restatement of the reference, 'port') timed on
+    this host on a bounded sample -- the C1 observation (1 feed x 4 x 1024 x
+    30,000) -- next to the reference itself ('reference'), which cannot travel
+    to the GPU box and was timed in the build container by
+    tests/golden/make_golden.py (tests/golden/golden_meta.json).  Destriper: the
+    oracle's CG iterations / s on this observation's C4 problem (a few timed
+    iterations) and the reference's, timed likewise in the build container."""
     from threadpoolctl import threadpool_limits
     import oracle.l1 as ol1
     from comapreduce_amd import synthetic
@@ -110,9 +168,48 @@ def cpu_baseline():
         ol1.reduce_level1(gen['data'])
         dt = time.perf_counter() - t0
     n = 1 * 4 * 1024 * 30_000
-    return {'value': n / dt, 'unit': 'samples*channels/s', 'cores': 1, 'kind': 'port',
-            'sample': f'C1 observation 1x4x1024x30000 ({n} samp*ch), full vane+atmosphere+L2 reduce, '
-                      f'{dt:.2f} s on 1 host core (oracle/l1.py)'}
+    out = {'value': n / dt, 'unit': 'samples*channels/s', 'cores': 1, 'kind': 'port',
+           'sample': f'C1 observation 1x4x1024x30000 ({n} samp*ch), full vane+atmosphere+L2 reduce, '
+                     f'{dt:.2f} s on 1 host core of the GPU box (oracle/l1.py)'}
+    meta = json.load(open(os.path.join(ROOT, 'tests', 'golden', 'golden_meta.json')))
+    tr = meta.get('reference_timings_s_c1')
+    if tr:
+        rs = float(sum(tr.values()))
+        nref = int(meta.get('reference_samples_channels_c1', n))
+        out['reference'] = {
+            'value': nref / rs, 'unit': 'samples*channels/s', 'cores': 1, 'kind': 'reference',
+            'sample': f'the reference v0.9.1 itself (MeasureSystemTemperature + AtmosphereRemoval + '
+                      f'Level1AveragingGainCorrection, PNG writing on) on the same C1 observation: {rs:.2f} s, '
+                      f'1 process, 8-core Xeon build container (no GPU box: the reference never travels); '
+                      f'tests/golden/golden_meta.json reference_timings_s_c1'}
+    dref = meta.get('reference_destriper_c4')
+    if dref:
+        out['destriper_reference'] = {
+            'value': dref['iters_per_s'], 'unit': 'CG iterations/s', 'cores': 1, 'kind': 'reference',
+            'sample': f"reference Destriper.cgm on a C4-size problem ({dref['n_samples']} samples, "
+                      f"{dref['n_offsets']} offsets, 480x480 map, L=50): {dref['iters']} iterations in "
+                      f"{dref['seconds']:.1f} s (3 matvecs/iteration as shipped), build container; "
+                      'tests/golden/golden_meta.json reference_destriper_c4'}
+    return out
+
+
+def cpu_destriper_port(tod, w, pix, L, npix, iters=3):
+    """The oracle's destriper (NumPy + C binValues, one matvec per iteration) on the
+    C4 problem: a few fixed iterations (bounded sample)."""
+    from threadpoolctl import threadpool_limits
+    import oracle.destriper as od
+    p = np.asarray(pix, dtype=np.int64)
+    t = np.asarray(tod, dtype=np.float64)
+    ww = np.asarray(w, dtype=np.float64)
+    with threadpool_limits(1):
+        A = lambda x: od.op_Ax(x, p, ww, L, npix)          # noqa: E731
+        b = od.op_Ax(t, p, ww, L, npix, extend=False)
+        t0 = time.perf_counter()
+        od.cgm(A, b, threshold=0.0, niter=iters)
+        dt = time.perf_counter() - t0
+    return {'value': iters / dt, 'unit': 'CG iterations/s', 'cores': 1, 'kind': 'port',
+            'sample': f'oracle/destriper.py cgm, {iters} iterations on the C4 problem ({t.size} samples), '
+                      f'{dt:.2f} s on 1 host core of the GPU box'}
 
 
 def check_against_oracle(data, level2, device):
@@ -134,12 +231,45 @@ def check_against_oracle(data, level2, device):
     return {'unit': [f, s, t0, n], 'tod_rel_err': err, 'fit_rel_err': ferr}
 
 
-def destriper_leg(level2, data, niter, device):
-    """Destriper CG iterations/s on the band-0 Level-2 TOD of this observation
-    (C4-like: 19 feeds, L=50, 480x480 CAR map at 1'), single rank."""
+# ---------------------------------------------------------------- destriper legs
+def level2_store(level2, data, obsid):
+    """The Level-2 'file' read_comap_data reads (COMAPData.py:247-427), built from a
+    reduced observation: {filename: (datasets, attrs)} on the host."""
+    from comapreduce_amd.pipeline.datahandling import to_host
+    F = int(np.asarray(to_host(data['spectrometer/feeds'])).size)
+    ds = {'averaged_tod/tod': to_host(level2['averaged_tod/tod']),
+          'averaged_tod/tod_original': to_host(level2['averaged_tod/tod_original']),
+          'averaged_tod/weights': to_host(level2['averaged_tod/weights']),
+          'averaged_tod/scan_edges': np.asarray(to_host(level2['averaged_tod/scan_edges'])),
+          'spectrometer/feeds': np.asarray(to_host(data['spectrometer/feeds'])),
+          'spectrometer/MJD': np.asarray(to_host(data['spectrometer/MJD']))}
+    for k in ('ra', 'dec', 'az', 'el'):
+        ds[f'spectrometer/pixel_pointing/pixel_{k}'] = np.asarray(to_host(data[f'spectrometer/pixel_pointing/pixel_{k}']))
+    attrs = {'comap': {'source': 'Field00', 'obsid': obsid, 'bad_observation': np.zeros(max(20, F + 1), np.int64)}}
+    name = f'comap-{obsid:07d}-2020-06-01-000000_Level2Cont.hd5'
+    return {name: (ds, attrs)}
+
+
+def c4_map_info():
+    """480 x 480 CAR map at 1' on the synthetic field centre."""
+    from comapreduce_amd import synthetic
+    from comapreduce_amd.mapmaking.comapdata import map_info_from
+    return map_info_from([synthetic.FIELD_RA, synthetic.FIELD_DEC], [-1.0 / 60.0, 1.0 / 60.0], [240, 240],
+                         ['RA---CAR', 'DEC--CAR'], 480, 480)
+
+
+def destriper_leg(level2, data, niter, device, want_cpu=False):
+    """C4: COMAPData.read_comap_data (host prep + batched device w=400 median) on this
+    observation's Level-2 output (band 0, 19 feeds, L = 50, 480x480 CAR), then the
+    device destriper's CG iterations / s (single rank, threshold 0: no early exit)."""
     import torch
+    from comapreduce_amd.mapmaking import comapdata as CD
     from comapreduce_amd.mapmaking import destriper as D
-    tod, w, pix = D.level2_to_destriper_inputs(level2, data, band=0, offset_length=50)
+    store = level2_store(level2, data, obsid=int(data.obsid) if data.obsid > 0 else 1)
+    t0 = time.perf_counter()
+    tod, w, pix = CD.read_comap_data(list(store), c4_map_info(), iband=0, offset_length=50, store=store,
+                                     device=device)[:3]
+    prep = time.perf_counter() - t0
     t0 = time.perf_counter()
     prob = D.DeviceDestriper(pix, tod, w, 50, 480 * 480, device=device)
     torch.cuda.synchronize()
@@ -150,8 +280,13 @@ def destriper_leg(level2, data, niter, device):
     res = prob.solve(threshold=0.0, niter=niter)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    return {'cg_iters_per_s': res['iters'] / dt, 'iters': res['iters'], 'n_samples': int(tod.numel()),
-            'n_offsets': int(tod.numel() // 50), 'setup_s': setup, 'nnz': prob.nnz()}
+    out = {'config': 'C4: read_comap_data (band 0, 19 feeds) -> destriper, L=50, 480x480 CAR, '
+                     f'{niter} CG iterations (no early exit), single rank',
+           'cg_iters_per_s': res['iters'] / dt, 'iters': res['iters'], 'n_samples': int(tod.size),
+           'n_offsets': int(tod.size // 50), 'prep_s': prep, 'setup_s': setup, 'nnz': prob.nnz()}
+    if want_cpu:
+        out['cpu_port'] = cpu_destriper_port(tod, w, pix, 50, 480 * 480)
+    return out
 
 
 def destriper_c5_leg(n_obs, niter, device, world, rank):
@@ -187,25 +322,28 @@ def destriper_c5_leg(n_obs, niter, device, world, rank):
     N = int(tod.numel())
     NO = N // L
     it = max(res['iters'], 1)
-    algo = 24 * N + 80 * NO
+    algo = DESTRIPER_BYTES_PER_SAMPLE * N + DESTRIPER_BYTES_PER_OFFSET * NO
     ms = dt / it * 1e3
     return {'config': f'C5: {n_obs} obs x 19 feeds x 180000 samples per GPU, L={L}, 480x480 CAR, '
-                      f'{niter} CG iterations (no early exit)',
+                      f'{niter} CG iterations (no early exit), {world} rank(s)',
             'cg_iters_per_s': it / dt, 'ms_per_iter': ms, 'iters': res['iters'],
             'n_samples_per_gpu': N, 'n_offsets_per_gpu': NO, 'nnz': prob.nnz(), 'setup_s': setup,
             'algo_bytes_per_iter_per_gpu': algo, 'achieved_GBs_per_gpu': algo / (ms * 1e-3) / 1e9,
             'roofline_frac': algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
+# ---------------------------------------------------------------- main
 def main():
     args = parse()
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     import torch
     import torch.distributed as dist
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    # one rank per GPU (the driver's torchrun); COMAP_DIST_BACKEND=gloo with more ranks than
-    # GPUs is a rehearsal mode only (ranks share devices; RCCL refuses duplicate GPUs)
+    # one rank per GPU; COMAP_DIST_BACKEND=gloo with more ranks than GPUs is a rehearsal
+    # mode only (ranks share devices; RCCL refuses duplicate GPUs)
     backend = os.environ.get('COMAP_DIST_BACKEND', 'nccl')
     device = local % max(torch.cuda.device_count(), 1) if backend == 'gloo' else local
     torch.cuda.set_device(device)
@@ -216,8 +354,13 @@ def main():
         else:
             dist.init_process_group(backend)
     F, T = args.feeds, args.samples
-    data = build_observation(F, T, obs_id=rank + 1, device=device)
-    samp_ch = F * 4 * 1024 * T
+    shard = args.mode == 'shard' and world > 1
+    if shard:
+        data, sh = build_observation(F, T, obs_id=1, device=device, rank=rank, world=world)
+    else:
+        data, sh = build_observation(F, T, obs_id=rank + 1, device=device)
+    cube_sampch = F * 4 * 1024 * T                 # one observation's cube
+    job_sampch = cube_sampch if shard else world * cube_sampch
 
     for _ in range(max(args.warmup, 1)):       # the first step also creates the plan
         level2 = reduce_step(data, device)
@@ -244,10 +387,13 @@ def main():
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
 
+    frac = obs.pass_fractions()
+    vane_search_ms = getattr(obs, 'last_vane_search_ms', None)
     check = check_against_oracle(data, level2, device) if (args.check and rank == 0) else None
     dstr = None
-    if not args.no_destriper:
-        dstr = destriper_leg(level2, data, args.destriper_iters, device)
+    if not args.no_destriper and not shard:
+        dstr = destriper_leg(level2, data, args.destriper_iters, device,
+                             want_cpu=(rank == 0 and world == 1 and not args.no_cpu_baseline))
         if world > 1:
             v = torch.tensor([dstr['cg_iters_per_s']], device='cuda', dtype=torch.float64)
             dist.all_reduce(v, op=dist.ReduceOp.MIN)
@@ -255,27 +401,36 @@ def main():
 
     c5 = None
     if not args.no_destriper and args.c5_obs > 0:
+        del data, level2, obs
+        torch.cuda.empty_cache()
         c5 = destriper_c5_leg(args.c5_obs, args.destriper_iters, device, world, rank)
 
     if rank == 0:
-        value = world * samp_ch * args.steps / elapsed
-        scan_sc = obs.scan_samples() * 4096
-        stream = {k: prof[k] for k in obs.STREAMING}
-        # bytes each pass must read: A all 1024 channels, B the median_filter channels with a
-        # finite 1/rms, C those channels in the bands the median filter did not skip
-        frac = obs.pass_fractions()
-        pass_bytes = {k: ALGO_BYTES_PER_SAMPCH_PASS * scan_sc * frac[k] for k in obs.STREAMING}
+        value = job_sampch * args.steps / elapsed
+        scan_sc = sh.samples_x_channels()
+        stream = {k: prof[k] for k in type_streaming()}
+        pass_bytes = {k: ALGO_BYTES_PER_SAMPCH_PASS * scan_sc * frac[k] for k in type_streaming()}
         dom = max(stream, key=lambda k: stream[k][0])
         ms_avg = stream[dom][0] / max(stream[dom][1], 1)
-        # passes B and C run as one launch per unit group (pipelined with the median)
         algo_bytes = pass_bytes[dom] * args.steps / max(stream[dom][1], 1)
         achieved = algo_bytes / (ms_avg * 1e-3) / 1e9
         design_bytes = sum(pass_bytes.values())
         traffic = None
         tpath = os.path.join(ROOT, 'profiles', 'traffic_latest.json')
-        if os.path.exists(tpath):
+        if os.path.exists(tpath) and world == 1:
             traffic = json.load(open(tpath)).get(dom)
         step_ms = elapsed / args.steps * 1e3
+        rank0_ms = (t1 - t0) / args.steps * 1e3
+        if shard:
+            workload = (f'C3: one {F}-feed x 4 x 1024 ch x {T}-sample L1 observation sharded by (feed, scan) units '
+                        f'over {world} GPUs, no collectives (rank 0: feeds {sh.f_lo}..{sh.f_hi - 1}, '
+                        f'{len(sh.units)} units)')
+            par = f'(feed, scan)-sharded x{world}'
+        else:
+            workload = (f'C2: {F}-feed x 4 x 1024 ch x {T} samples L1 observation per GPU '
+                        f'({cube_sampch * 4 / 1e9:.1f} GB f32 resident in HBM), vane + atmosphere + '
+                        'L1AveragingGainCorrection')
+            par = f'observation-parallel x{world}'
         line = {
             'metric': 'TOD samples x channels / s (L1 -> L2 reduction)',
             'value': value,
@@ -285,29 +440,28 @@ def main():
             'warmup': args.warmup,
             'ms_per_step': step_ms,
             'higher_is_better': True,
-            'scaling': 'weak',
+            'scaling': 'strong' if shard else 'weak',
             'vs_baseline': None,
             'dtype': 'f32 in, f64 accumulate',
             'data': 'synthetic (SURVEY.md §8d spec, generated on device)',
-            'config': {'workload': f'C2: {F}-feed x 4 x 1024 ch x {T} samples L1 observation per GPU '
-                                   f'({samp_ch * 4 / 1e9:.1f} GB f32 resident in HBM), vane + atmosphere + '
-                                   'L1AveragingGainCorrection', 'parallelism': f'observation-parallel x{world}'},
+            'config': {'workload': workload, 'parallelism': par},
             'roofline': {'bound': 'hbm', 'kernel': dom, 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
                          'algo_bytes_per_launch': algo_bytes, 'avg_launch_ms': ms_avg},
-            'l1_step_roofline': {'passes': len(obs.STREAMING), 'design_bytes': design_bytes,
-                                 'achieved_GBs': design_bytes / (step_ms * 1e-3) / 1e9,
-                                 'frac': design_bytes / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            'l1_step_roofline': {'passes': len(type_streaming()), 'design_bytes': design_bytes,
+                                 'rank0_ms_per_step': rank0_ms,
+                                 'achieved_GBs': design_bytes / (rank0_ms * 1e-3) / 1e9,
+                                 'frac': design_bytes / (rank0_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                                  'pass_channel_fraction': frac,
                                  'survey_4pass_bytes': SURVEY_BYTES_PER_SAMPCH * scan_sc,
                                  'survey_4pass_equiv_frac':
-                                     SURVEY_BYTES_PER_SAMPCH * scan_sc / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
+                                     SURVEY_BYTES_PER_SAMPCH * scan_sc / (rank0_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
             'kernel_ms_per_step': {k: v[0] / args.steps for k, v in prof.items()},
             'host_stage_ms_per_step': {k: v / args.steps for k, v in host_ms.items()},
-            'host_vane_search_ms': getattr(obs, 'last_vane_search_ms', None),
+            'host_vane_search_ms': vane_search_ms,
             'pass_GBs': {k: pass_bytes[k] / (stream[k][0] / args.steps * 1e-3) / 1e9
-                         for k in obs.STREAMING if stream[k][1] > 0},
-            'launches_per_step': {k: stream[k][1] / args.steps for k in obs.STREAMING},
+                         for k in type_streaming() if stream[k][1] > 0},
+            'launches_per_step': {k: stream[k][1] / args.steps for k in type_streaming()},
         }
         if dstr is not None:
             line['destriper'] = dstr
@@ -316,10 +470,18 @@ def main():
         if check is not None:
             line['check'] = check
         if not args.no_cpu_baseline and world == 1:
-            line['cpu_baseline'] = cpu_baseline()
+            cb = cpu_baseline()
+            if dstr is not None and 'cpu_port' in dstr:
+                cb['destriper_port'] = dstr.pop('cpu_port')
+            line['cpu_baseline'] = cb
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def type_streaming():
+    from comapreduce_amd.gpu import GPUObservation
+    return GPUObservation.STREAMING
 
 
 if __name__ == '__main__':

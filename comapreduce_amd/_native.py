@@ -54,7 +54,7 @@ _SIGS = {
                              c_void_p]),
     'comap_power_spectra': (c_int, [c_void_p, c_void_p, c_int32, c_int64, P_int64, c_int32, c_void_p, c_int32,
                                     P_int64, c_void_p]),
-    'comap_synth_tod': (c_int, [c_void_p, c_int32, c_int64, ctypes.c_uint64, c_void_p, c_void_p, c_void_p,
+    'comap_synth_tod': (c_int, [c_void_p, c_int32, c_int32, c_int64, ctypes.c_uint64, c_void_p, c_void_p, c_void_p,
                                 c_void_p, c_void_p]),
     'comap_destripe_create': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int64,
                                       ctypes.POINTER(c_void_p)]),
@@ -107,8 +107,18 @@ def lib():
     return _lib
 
 
-def ctx(device=0):
-    """Per-process context for ``device`` (created on first use)."""
+def current_device():
+    """torch's current HIP device of this thread (the rank's GPU under torchrun)."""
+    import torch
+    return torch.cuda.current_device()
+
+
+def ctx(device=None):
+    """Per-process context for ``device`` (default: torch's current device),
+    created on first use.  Creating it does not change the current device."""
+    if device is None:
+        device = current_device()
+    device = int(device)
     c = _ctx.get(device)
     if c is None:
         out = c_void_p()

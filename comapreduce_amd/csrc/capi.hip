@@ -46,7 +46,10 @@ extern "C" int comap_ctx_create(int device, comap_ctx **out)
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
     if (e != hipSuccess || ndev <= device || device < 0) return -6;
-    if (hipSetDevice(device) != hipSuccess) return -6;
+    // the caller's current device is left as it was (DeviceGuard restores it)
+    DeviceGuard g(device);
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || cur != device) return -6;
     auto *c = new comap_ctx();
     c->device = device;
     *out = c;
@@ -56,6 +59,7 @@ extern "C" int comap_ctx_create(int device, comap_ctx **out)
 extern "C" int comap_ctx_destroy(comap_ctx *ctx)
 {
     if (!ctx) return 0;
+    COMAP_DEVICE_GUARD(ctx);
     if (ctx->scratch) {
         (void)hipStreamSynchronize(ctx->stream);
         (void)hipFree(ctx->scratch);
@@ -76,6 +80,7 @@ extern "C" int comap_set_stream(comap_ctx *ctx, void *stream)
 extern "C" int comap_synchronize(comap_ctx *ctx)
 {
     if (!ctx) return -1;
+    COMAP_DEVICE_GUARD(ctx);
     COMAP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
     return 0;
 }
@@ -84,6 +89,7 @@ extern "C" int comap_synchronize(comap_ctx *ctx)
 extern "C" int comap_medfilt_f64(comap_ctx *ctx, double *x, int64_t n, int32_t w)
 {
     if (!ctx || !x) return -1;
+    COMAP_DEVICE_GUARD(ctx);
     if (w < 1 || n < w) return comap_fail(ctx, -1, "medfilt requires 1 <= w <= n");
     for (int64_t i = 0; i < n; ++i)
         if (std::isnan(x[i])) return comap_fail(ctx, -3, "medfilt input contains NaN");
@@ -118,6 +124,7 @@ extern "C" int comap_medfilt_batch_f64(comap_ctx *ctx, const double *x, const in
                                        int32_t w, int32_t mode, double *out)
 {
     if (!ctx || !x || !offsets || !out || nseries < 0 || (mode != 0 && mode != 1)) return -1;
+    COMAP_DEVICE_GUARD(ctx);
     if (nseries == 0) return 0;
     const int64_t total = offsets[nseries];
     for (int s = 0; s < nseries; ++s) {
@@ -201,6 +208,7 @@ extern "C" int comap_bin_values_f64(comap_ctx *ctx, double *image, int64_t npix,
                                     const double *weights, const int64_t *mask, int64_t n)
 {
     if (!ctx || !image || (!pixels && n > 0)) return -1;
+    COMAP_DEVICE_GUARD(ctx);
     if (npix <= 0 || n <= 0) return 0;
     if (npix >= (1ll << 31) - 1 || n >= (1ll << 31)) return comap_fail(ctx, -1, "binValues size limit exceeded");
     int end_bit = 1;

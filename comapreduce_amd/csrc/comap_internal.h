@@ -27,6 +27,45 @@ struct comap_ctx {
 
 #define COMAP_LAUNCH_CHECK(ctx) COMAP_CHECK(ctx, hipGetLastError())
 
+// Every entry point that allocates or launches makes its context's device current
+// for the call and restores the caller's device on return: the process shares one
+// HIP runtime with torch, whose current device must not move under it.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        else if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard()
+    {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard &) = delete;
+    DeviceGuard &operator=(const DeviceGuard &) = delete;
+};
+#define COMAP_DEVICE_GUARD(ctx) DeviceGuard _comap_dg((ctx)->device)
+
+// Device buffers owned by one call: freed on every return path (error returns
+// included) unless released to a longer-lived owner.
+struct DevTemps {
+    std::vector<void *> p;
+    template <typename T>
+    hipError_t alloc(T **out, size_t n)
+    {
+        void *q = nullptr;
+        const hipError_t e = hipMalloc(&q, sizeof(T) * (n ? n : 1));
+        if (e == hipSuccess) p.push_back(q);
+        *out = (T *)q;
+        return e;
+    }
+    ~DevTemps()
+    {
+        for (void *q : p) (void)hipFree(q);
+    }
+};
+
 int comap_fail(comap_ctx *ctx, int code, const std::string &msg);
 int comap_scratch(comap_ctx *ctx, size_t bytes, void **out);
 // med_dev[r] = np.nanmedian(float32 row r), rows_host[2r] = element offset in tod, [2r+1] = length

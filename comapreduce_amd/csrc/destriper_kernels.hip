@@ -540,6 +540,7 @@ extern "C" int comap_destripe_create(comap_ctx *ctx, const int32_t *pix, const d
                                      int64_t N, int32_t L, int64_t npix, comap_destriper **out)
 {
     if (!ctx || !pix || !tod || !w || !out) return -1;
+    COMAP_DEVICE_GUARD(ctx);
     if (L < 1 || L > 256) return comap_fail(ctx, -1, "offset_length must be in [1, 256]");
     if (N <= 0 || N % L) return comap_fail(ctx, -1, "n_samples must be a positive multiple of offset_length");
     if (npix <= 0 || npix >= (1ll << 31) - 1 || N >= (1ll << 31)) return comap_fail(ctx, -1, "size limits exceeded");
@@ -629,6 +630,7 @@ extern "C" int comap_destripe_create(comap_ctx *ctx, const int32_t *pix, const d
 extern "C" int comap_destripe_destroy(comap_destriper *d)
 {
     if (!d) return 0;
+    COMAP_DEVICE_GUARD(d->ctx);
     if (d->cs) (void)hipStreamSynchronize(d->cs);
     void *b[] = {d->orow, d->opix, d->ow, d->ws, d->tw, d->prow, d->poff, d->pw, d->h, d->hits, d->nnum, d->part, d->scal,
                  d->cg, d->flags, d->hrow};
@@ -656,6 +658,7 @@ extern "C" int comap_destripe_nnz(const comap_destriper *d, int64_t *nnz_offset_
 extern "C" int comap_destripe_local_maps(comap_destriper *d, double *h, double *hits, double *naive_num)
 {
     if (!d) return -1;
+    COMAP_DEVICE_GUARD(d->ctx);
     comap_ctx *ctx = d->ctx;
     const size_t b = 8 * (size_t)d->npix;
     if (h) COMAP_CHECK(ctx, hipMemcpyAsync(h, d->h, b, hipMemcpyDeviceToDevice, ctx->stream));
@@ -667,6 +670,7 @@ extern "C" int comap_destripe_local_maps(comap_destriper *d, double *h, double *
 extern "C" int comap_destripe_bin(comap_destriper *d, const double *x, int32_t mode, double *num)
 {
     if (!d || !x || !num) return -1;
+    COMAP_DEVICE_GUARD(d->ctx);
     comap_ctx *ctx = d->ctx;
     launch_bin(d, ctx->stream, x, mode == 1 ? d->nnum : nullptr, nullptr, num, nullptr);
     COMAP_LAUNCH_CHECK(ctx);
@@ -677,6 +681,7 @@ extern "C" int comap_destripe_project(comap_destriper *d, const double *x, const
                                       double *y, double *dot_out)
 {
     if (!d || !num || !y) return -1;
+    COMAP_DEVICE_GUARD(d->ctx);
     comap_ctx *ctx = d->ctx;
     const double *hh = h ? h : d->h;
     const bool want = dot_out && x;
@@ -692,6 +697,7 @@ extern "C" int comap_destripe_project(comap_destriper *d, const double *x, const
 extern "C" int comap_destripe_dot(comap_destriper *d, const double *a, const double *b, double *out)
 {
     if (!d || !a || !b || !out) return -1;
+    COMAP_DEVICE_GUARD(d->ctx);
     return dot(d, a, b, out);
 }
 
@@ -699,6 +705,7 @@ extern "C" int comap_destripe_cg_update(comap_destriper *d, const double *rr, co
                                         const double *p, const double *q, double *rr_new)
 {
     if (!d) return -1;
+    COMAP_DEVICE_GUARD(d->ctx);
     comap_ctx *ctx = d->ctx;
     k_cg_update<<<kRedBlocks, 256, 0, ctx->stream>>>(rr, pq, x, r, p, q, d->NO, d->part, nullptr);
     COMAP_LAUNCH_CHECK(ctx);
@@ -711,6 +718,7 @@ extern "C" int comap_destripe_cg_direction(comap_destriper *d, const double *rr_
                                            const double *r)
 {
     if (!d) return -1;
+    COMAP_DEVICE_GUARD(d->ctx);
     comap_ctx *ctx = d->ctx;
     k_cg_direction<<<grid_for(d->NO), 256, 0, ctx->stream>>>(rr_new, rr, p, r, d->NO, nullptr);
     COMAP_LAUNCH_CHECK(ctx);
@@ -720,6 +728,7 @@ extern "C" int comap_destripe_cg_direction(comap_destriper *d, const double *rr_
 extern "C" int comap_destripe_div_map(comap_destriper *d, const double *num, const double *h, double *out)
 {
     if (!d || !num || !out) return -1;
+    COMAP_DEVICE_GUARD(d->ctx);
     comap_ctx *ctx = d->ctx;
     k_div_map<<<grid_for(d->npix), 256, 0, ctx->stream>>>(num, h ? h : d->h, d->npix, out);
     COMAP_LAUNCH_CHECK(ctx);
@@ -734,6 +743,7 @@ extern "C" int comap_destripe_div_map(comap_destriper *d, const double *num, con
 extern "C" int comap_destripe_dist_bin(comap_destriper *d, const double *p, double *num, const int32_t *flags)
 {
     if (!d || !p || !num || !flags) return -1;
+    COMAP_DEVICE_GUARD(d->ctx);
     comap_ctx *ctx = d->ctx;
     launch_bin(d, ctx->stream, p, nullptr, nullptr, num, flags);
     COMAP_LAUNCH_CHECK(ctx);
@@ -744,6 +754,7 @@ extern "C" int comap_destripe_dist_project(comap_destriper *d, const double *p, 
                                            double *q, double *scal, const int32_t *flags)
 {
     if (!d || !p || !num || !h || !q || !scal || !flags) return -1;
+    COMAP_DEVICE_GUARD(d->ctx);
     comap_ctx *ctx = d->ctx;
     const unsigned pg = launch_project(d, ctx->stream, p, num, h, q, d->part, flags);
     k_dot_final<<<1, 256, 0, ctx->stream>>>(d->part, (int)pg, scal + 2, flags);
@@ -755,6 +766,7 @@ extern "C" int comap_destripe_dist_update(comap_destriper *d, double *scal, doub
                                           const double *q, const int32_t *flags)
 {
     if (!d || !scal || !x || !r || !p || !q || !flags) return -1;
+    COMAP_DEVICE_GUARD(d->ctx);
     comap_ctx *ctx = d->ctx;
     k_cg_update<<<kRedBlocks, 256, 0, ctx->stream>>>(scal + 1, scal + 2, x, r, p, q, d->NO, d->part, flags);
     k_dot_final<<<1, 256, 0, ctx->stream>>>(d->part, kRedBlocks, scal + 3, flags);
@@ -766,6 +778,7 @@ extern "C" int comap_destripe_dist_direction(comap_destriper *d, double *scal, d
                                              int32_t *flags)
 {
     if (!d || !scal || !p || !r || !flags) return -1;
+    COMAP_DEVICE_GUARD(d->ctx);
     comap_ctx *ctx = d->ctx;
     k_cg_direction<<<grid_for(d->NO), 256, 0, ctx->stream>>>(scal + 3, scal + 1, p, r, d->NO, flags);
     k_cg_check<<<1, 64, 0, ctx->stream>>>(scal, flags);
@@ -820,6 +833,7 @@ extern "C" int comap_destripe_solve(comap_destriper *d, double threshold, int32_
                                     double *naive, double *weight, double *hits, int32_t *iters_out)
 {
     if (!d || !x || niter < 0) return -1;
+    COMAP_DEVICE_GUARD(d->ctx);
     comap_ctx *ctx = d->ctx;
     int rc = cg_setup(d);
     if (rc) return rc;

@@ -1344,6 +1344,7 @@ extern "C" int comap_l1_profile(comap_l1_plan *p, int32_t enable)
 extern "C" int comap_l1_profile_collect(comap_l1_plan *p, double *ms, int64_t *counts, int32_t n)
 {
     if (!p || !ms || !counts) return -1;
+    COMAP_DEVICE_GUARD(p->ctx);
     comap_ctx *ctx = p->ctx;
     COMAP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
     for (auto &r : p->prof_rec) {
@@ -1379,6 +1380,7 @@ static int dalloc(comap_ctx *ctx, T **p, size_t count)
 extern "C" int comap_l1_plan_create(comap_ctx *ctx, const comap_obs_desc *d, comap_l1_plan **out)
 {
     if (!ctx || !d || !out) return -1;
+    COMAP_DEVICE_GUARD(ctx);
     if (d->n_bands != kBands || d->n_channels != kChannels)
         return comap_fail(ctx, -1, "only 4 bands x 1024 channels are supported");
     if (d->n_units <= 0 || d->n_samples <= 0 || d->n_feeds <= 0)
@@ -1492,6 +1494,7 @@ extern "C" int comap_l1_plan_create(comap_ctx *ctx, const comap_obs_desc *d, com
 extern "C" int comap_l1_plan_destroy(comap_l1_plan *p)
 {
     if (!p) return 0;
+    COMAP_DEVICE_GUARD(p->ctx);
     if (p->side) (void)hipStreamSynchronize(p->side);
     void *bufs[] = {p->units, p->tiles, p->tiles_b, p->airmass, p->unit_sums, p->mom,
                     p->nan_count, p->alpha, p->nf, p->bsum, p->mb, p->mf, p->ssum, p->sdm, p->gw,
@@ -1549,6 +1552,7 @@ static int run_moments(comap_l1_plan *p)
 extern "C" int comap_l1_prefetch(comap_l1_plan *p)
 {
     if (!p) return -1;
+    COMAP_DEVICE_GUARD(p->ctx);
     int rc = launch_moments(p);
     if (!rc) p->prefetched = true;
     return rc;
@@ -1581,6 +1585,7 @@ extern "C" int comap_l1_atmosphere(comap_l1_plan *p, const int32_t *const_el_uni
                                    double *fit)
 {
     if (!p || !fit) return -1;
+    COMAP_DEVICE_GUARD(p->ctx);
     comap_ctx *ctx = p->ctx;
     hipStream_t st = ctx->stream;
     int rc = p->prefetched ? wait_moments(p) : run_moments(p);   // pass A, unless comap_l1_prefetch ran it
@@ -1695,6 +1700,7 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
                                 int32_t calibrator, double *tod_out, double *orig_out, double *w_out)
 {
     if (!p || !fit || !tsys0 || !gain0 || !tod_out || !orig_out || !w_out) return -1;
+    COMAP_DEVICE_GUARD(p->ctx);
     comap_ctx *ctx = p->ctx;
     int rc = 0;
     if (!p->moments_valid && (rc = run_moments(p))) return rc;
@@ -1784,6 +1790,7 @@ extern "C" int comap_l1_vane(comap_l1_plan *p, int64_t vstart, int64_t vlen, con
                              double t_hot, double *tsys, double *gain)
 {
     if (!p || !hoff_h || !coff_h || !tsys || !gain) return -1;
+    COMAP_DEVICE_GUARD(p->ctx);
     comap_ctx *ctx = p->ctx;
     const int FB = p->F * kBands;
     if (vstart < 0 || vstart + vlen > p->T) return comap_fail(ctx, -1, "vane event out of range");
@@ -1819,6 +1826,7 @@ extern "C" int comap_l1_vane(comap_l1_plan *p, int64_t vstart, int64_t vlen, con
 extern "C" int comap_l1_debug_fetch(comap_l1_plan *p, int32_t what, double *out, int64_t n)
 {
     if (!p || !out) return -1;
+    COMAP_DEVICE_GUARD(p->ctx);
     comap_ctx *ctx = p->ctx;
     const int64_t UC = (int64_t)p->U * kBC;
     const double *src = nullptr;
@@ -1856,6 +1864,7 @@ extern "C" int comap_l1_channel_bin(comap_l1_plan *p, int32_t bin_size, const do
                                     const double *wsum, double *avg, double *stddev)
 {
     if (!p || !weights || !gain || !wsum || !avg || !stddev) return -1;
+    COMAP_DEVICE_GUARD(p->ctx);
     comap_ctx *ctx = p->ctx;
     if (bin_size < 1 || kChannels % bin_size) return comap_fail(ctx, -1, "bin_size must divide 1024");
     const int64_t ntile = (p->T + kTile - 1) / kTile;

@@ -182,6 +182,7 @@ extern "C" int comap_spikes(comap_ctx *ctx, const double *tod, int32_t n_rows, i
                             int32_t n_scans, int32_t medfilt_window, int32_t step, double threshold, uint8_t *mask)
 {
     if (!ctx || !tod || !mask || n_rows <= 0 || T <= 0) return -1;
+    COMAP_DEVICE_GUARD(ctx);
     if (medfilt_window < 1 || medfilt_window > 1023 || step < 1) return comap_fail(ctx, -1, "unsupported spike window");
     hipStream_t st = ctx->stream;
     double *comp = nullptr, *rms = nullptr, *mf = nullptr, *gate = nullptr;

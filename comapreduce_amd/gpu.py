@@ -118,8 +118,9 @@ def vane_events(features):
 class GPUObservation:
     """One observation resident on one GPU, with its reduction plan."""
 
-    def __init__(self, data, device: int = 0):
+    def __init__(self, data, device: int = None):
         torch = _torch()
+        device = N.current_device() if device is None else int(device)
         self.device = device
         self.tdev = torch.device('cuda', device)
         self.ctx = N.ctx(device)
@@ -135,6 +136,13 @@ class GPUObservation:
         self.S = len(self.edges)
         self.feeds = np.asarray(to_host(data['spectrometer/feeds'])).reshape(-1)
         units = [(f, s, int(a), int(b - a)) for f in range(F) for s, (a, b) in enumerate(self.edges) if b > a]
+        # a shard of a sharded observation (pipeline/sharding.py) reduces only its own units
+        filt = getattr(data, 'unit_filter', None)
+        if filt is not None:
+            keep = {(int(f), int(s)) for f, s in np.asarray(filt).reshape(-1, 2)}
+            units = [q for q in units if (q[0], q[1]) in keep]
+        if not units:
+            raise ValueError('observation (shard) has no (feed, scan) unit to reduce')
         self.units = np.ascontiguousarray(np.array(units, dtype=np.int32).reshape(-1, 4))
         # constant-elevation scans (features == 9 throughout): median atmosphere (Level1Averaging.py:242-244)
         const_scans = {s for s, (a, b) in enumerate(self.edges) if b > a and np.all(self.features[a:b] == 9)}
@@ -305,8 +313,10 @@ class GPUObservation:
         return out
 
 
-def gpu_observation(data, device: int = 0) -> GPUObservation:
-    """The GPUObservation cached on a Level-1 data object (created on first use)."""
+def gpu_observation(data, device: int = None) -> GPUObservation:
+    """The GPUObservation cached on a Level-1 data object (created on first use);
+    ``device`` None = torch's current device."""
+    device = N.current_device() if device is None else int(device)
     obs = getattr(data, '_gpu_observation', None)
     if obs is None or obs.device != device:
         obs = GPUObservation(data, device)

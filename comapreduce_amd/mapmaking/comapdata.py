@@ -229,10 +229,12 @@ class _FilePrep:
 
 def read_comap_data(filelist, map_info, feed_weights=None, iband=0, use_gain_filter=True, offset_length=50,
                     feeds=[i + 1 for i in range(19)], calibration=False, calibrator='TauA', healpix=False,
-                    store=None):
+                    store=None, device=None):
     """COMAPData.read_comap_data (COMAPData.py:471-577): same arguments and
     return tuple ``(tod, weights, pointing, remapping_array, az, el, ra, dec,
-    feedid, obsids)``.  ``store`` (tests) maps filename -> (datasets, attrs)."""
+    feedid, obsids)``.  ``store`` (tests) maps filename -> (datasets, attrs);
+    ``device``: the rank's GPU for the batched median (default: torch's
+    current device)."""
     from ..tools.medfilt import medfilt_batch
     if healpix:
         raise NotImplementedError('HEALPix pixelisation (read_pixels_healpix) is not built yet')
@@ -245,7 +247,7 @@ def read_comap_data(filelist, map_info, feed_weights=None, iband=0, use_gain_fil
         ds = int(info['datasize'])
         pix.append(read_pixels(f, ds, offset_length, feeds, map_info))
         preps.append(_FilePrep(f, ds, offset_length, feeds, use_gain_filter, iband, calibration, calibrator, queue))
-    filtered = medfilt_batch(queue, MEDFILT_STEP, reflect=True)
+    filtered = medfilt_batch(queue, MEDFILT_STEP, reflect=True, device=device)
     parts = [p.finish(filtered) for p in preps]
     N = sum(i['N'] for i in sizes)
     tod, weights, az, el, ra, dec = (np.zeros(N) for _ in range(6))

@@ -127,9 +127,10 @@ def cg_solve_batched(ops, allreduce, threshold=1e-6, niter=100, batch=16):
 class DeviceOps:
     """One rank's destriper operator on the GPU (comap_destripe_* C ABI)."""
 
-    def __init__(self, pixels, tod, weights, offset_length, npix, device=0):
+    def __init__(self, pixels, tod, weights, offset_length, npix, device=None):
         import torch
         self.torch = torch
+        device = N.current_device() if device is None else int(device)
         self.dev = torch.device('cuda', device)
         self.ctx = N.ctx(device)
         self.pix = self._t(pixels, torch.int32)
@@ -247,7 +248,7 @@ class DeviceOps:
 class DeviceDestriper:
     """Convenience wrapper: the whole destriper_iteration on device tensors."""
 
-    def __init__(self, pixels, tod, weights, offset_length, npix, device=0):
+    def __init__(self, pixels, tod, weights, offset_length, npix, device=None):
         self.ops = DeviceOps(pixels, tod, weights, offset_length, npix, device)
 
     def nnz(self):

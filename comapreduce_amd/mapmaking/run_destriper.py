@@ -56,10 +56,14 @@ def main(filelistname, offset_length=50, feed_weights=None, prefix='fg9', output
          feeds=[1, 2, 3, 5, 6, 9, 11, 12, 13, 14, 15, 16, 17, 18, 19], nxpix=480, nypix=480,
          crval=['05:32:00.3', '+12:30:28.0'], crpix=[240, 240], ctype=['RA---CAR', 'DEC--CAR'],
          cdelt=[-0.016666, 0.016666], use_gain_filter=True, calibration=True, calibrator='TauA', threshold=1e-6,
-         niter=100, healpix=False, bands=(0, 1, 2, 3), store=None):
+         niter=100, healpix=False, bands=(0, 1, 2, 3), store=None, device=None):
     """run_destriper.main (run_destriper.py:79-189).  ``store`` (tests) maps
-    filename -> (datasets, attrs) instead of reading files."""
+    filename -> (datasets, attrs) instead of reading files; ``device`` is the
+    rank's GPU (default: torch's current device, LOCAL_RANK under torchrun)."""
     rank, size = _rank_size()
+    if device is None:
+        import torch
+        device = torch.cuda.current_device()
     input_filelist = np.loadtxt(filelistname, dtype=str, ndmin=1) if isinstance(filelistname, str) \
         else np.asarray(filelistname)
     open_file = COMAPData._opener(store)
@@ -87,10 +91,11 @@ def main(filelistname, offset_length=50, feed_weights=None, prefix='fg9', output
         tod, weights, pointing, remap, az, el, ra, dec, feedid, obsids = COMAPData.read_comap_data(
             filelist, map_info, feed_weights=feed_weights, offset_length=offset_length, iband=iband, feeds=feeds,
             use_gain_filter=use_gain_filter, calibration=calibration, calibrator=calibrator, healpix=healpix,
-            store=store)
+            store=store, device=device)
         pixel_edges = np.arange(nxpix * nypix)
         maps = run_destriper(pointing, tod, weights, offset_length, pixel_edges, az, el, ra, dec, feedid, obsids,
-                             obsid_cuts, threshold=threshold, niter=niter, chi2_cutoff=20)
+                             obsid_cuts, threshold=threshold, niter=niter, chi2_cutoff=20,
+                             device=device)
         if rank == 0:
             write_map(prefix, maps, map_info, output_dir, iband)
         out[iband] = maps

@@ -46,7 +46,7 @@ class MeasureSystemTemperature(PipelineFunction):
     overwrite: bool = False
     STATE: bool = True
     figure_directory: str = 'figures'
-    device: int = 0
+    device: int = None      # None: torch's current device (LOCAL_RANK under torchrun)
     device_outputs: bool = False
 
     def __call__(self, data, level2_data=None):
@@ -80,7 +80,7 @@ class AtmosphereRemoval(PipelineFunction):
     overwrite: bool = False
     STATE: bool = True
     fit_values: object = None
-    device: int = 0
+    device: int = None      # None: torch's current device (LOCAL_RANK under torchrun)
     device_outputs: bool = False
 
     @property
@@ -113,7 +113,7 @@ class Level1AveragingGainCorrection(PipelineFunction):
     gain_subtracted_tod_name: str = 'tod'
     frequency_bin_size: int = 512
     N_CHANNELS: int = 1024
-    device: int = 0
+    device: int = None      # None: torch's current device (LOCAL_RANK under torchrun)
     device_outputs: bool = False
     tod_cleaned: object = None
     tod_original: object = None
@@ -176,7 +176,7 @@ class Level1Averaging(PipelineFunction):
     frequency_bin_size: int = 512
     N_CHANNELS: int = 1024
     STATE: bool = True
-    device: int = 0
+    device: int = None      # None: torch's current device (LOCAL_RANK under torchrun)
     device_outputs: bool = False
 
     def __post_init__(self):

@@ -49,7 +49,7 @@ class Level2FitPowerSpectrum(PipelineFunction):
     N_CHANNELS: int = 1024
     STATE: bool = True
     overwrite: bool = False
-    device: int = 0
+    device: int = None      # None: torch's current device (LOCAL_RANK under torchrun)
     data: dict = field(default_factory=dict)
 
     @property

@@ -19,9 +19,10 @@ from ..pipeline.datahandling import CALIBRATOR_LIST, COMAPLevel2, to_host
 from ..pipeline.running import PipelineFunction
 
 
-def spike_mask(tod, scan_edges, medfilt_window=100, step=100, threshold=10.0, device=0):
+def spike_mask(tod, scan_edges, medfilt_window=100, step=100, threshold=10.0, device=None):
     """Device spike mask of a Level-2 TOD [F, B, T] (NumPy or CUDA tensor) -> CUDA bool [F, B, T]."""
     torch = _torch()
+    device = N.current_device() if device is None else int(device)
     dev = torch.device('cuda', device)
     t = to_device(tod, torch.float64, dev)
     F, B, T = t.shape
@@ -41,7 +42,7 @@ class Spikes(PipelineFunction):
     STATE: bool = True
     MEDIAN_FILTER_STEP: int = 100
     SPIKE_THRESHOLD: float = 10
-    device: int = 0
+    device: int = None      # None: torch's current device (LOCAL_RANK under torchrun)
     device_outputs: bool = False
     data: dict = field(default_factory=lambda: {'spikes/spike_mask': np.empty(1)})
 
@@ -94,7 +95,7 @@ class NoiseStatistics(PipelineFunction):
     overwrite: bool = False
     STATE: bool = True
     N_FN_PARAMETERS: int = 3
-    device: int = 0
+    device: int = None      # None: torch's current device (LOCAL_RANK under torchrun)
     data: dict = field(default_factory=lambda: {'noise_statistics/fnoise': np.empty(1),
                                                 'noise_statistics/auto_rms': np.empty(1)})
 

@@ -55,6 +55,7 @@ class SyntheticConfig:
     comment: str = 'synthetic lissajous'
     scan_len: int = SCAN_LEN
     scan_gap: int = SCAN_GAP
+    min_last: int = 12_500                # a later scan shorter than this is not started
 
     def feeds(self):
         if self.feed_numbers is not None:
@@ -153,7 +154,7 @@ def generate_level1(cfg: SyntheticConfig) -> dict:
             generate_feed(cfg, int(feed))
     band_average = np.nanmean(tod, axis=2).astype(np.float32)
     mjd = 59000.0 + cfg.obs_id * 0.1 + np.arange(T) / SAMPLE_RATE / 86400.0
-    status = scan_status(T, cfg.scan_len, cfg.scan_gap)
+    status = scan_status(T, cfg.scan_len, cfg.scan_gap, cfg.min_last)
     # housekeeping sampled half a sample earlier than the spectrometer
     hk_utc = mjd - 0.5 / SAMPLE_RATE / 86400.0
     freq = np.linspace(26.0, 34.0, N_BANDS * N_CHANNELS).reshape(N_BANDS, N_CHANNELS)
@@ -210,7 +211,7 @@ def level1_metadata(cfg: SyntheticConfig):
         'spectrometer/pixel_pointing/pixel_dec': pix['dec'],
         'spectrometer/pixel_pointing/pixel_az': pix['az'],
         'spectrometer/pixel_pointing/pixel_el': pix['el'],
-        'hk/antenna0/deTracker/lissajous_status': scan_status(T, cfg.scan_len, cfg.scan_gap),
+        'hk/antenna0/deTracker/lissajous_status': scan_status(T, cfg.scan_len, cfg.scan_gap, cfg.min_last),
         'hk/antenna0/deTracker/utc': mjd - 0.5 / SAMPLE_RATE / 86400.0,
         'hk/antenna0/vane/Tvane': np.full(64, (T_VANE_K - 273.15) * 100.0),
     }

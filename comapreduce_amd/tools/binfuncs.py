@@ -13,7 +13,8 @@ import numpy as np
 from .. import _native as N
 
 
-def binValues(image, pixels, weights=None, mask=None):
+def binValues(image, pixels, weights=None, mask=None, device=None):
+    """``device``: HIP device to run on (default: torch's current device)."""
     if not (isinstance(image, np.ndarray) and image.dtype == np.float64 and image.flags.c_contiguous):
         raise TypeError('image must be a C-contiguous float64 ndarray')
     pix = np.ascontiguousarray(pixels, dtype=np.int64)
@@ -21,7 +22,7 @@ def binValues(image, pixels, weights=None, mask=None):
     m = None if mask is None else np.ascontiguousarray(mask, dtype=np.int64)
     if w is not None and w.size != pix.size:
         raise ValueError('weights and pixels differ in length')
-    c = N.ctx(0)
+    c = N.ctx(device)
     N.check(N.lib().comap_bin_values_f64(c, N.hptr(image, ctypes.c_double), image.size,
                                          N.hptr(pix, ctypes.c_int64),
                                          None if w is None else N.hptr(w, ctypes.c_double),

@@ -31,7 +31,7 @@ def positive_bins(n):
     return max((int(n) - 1) // 2, 0)
 
 
-def power_spectra(tod, scan_edges, mode='level2', spike_mask=None, device=0):
+def power_spectra(tod, scan_edges, mode='level2', spike_mask=None, device=None):
     """Device power spectra of a Level-2 TOD [F, B, T] (NumPy or CUDA tensor).
 
     Returns one host array per scan, shape [F, B, (n-1)//2] with n the scan
@@ -40,6 +40,7 @@ def power_spectra(tod, scan_edges, mode='level2', spike_mask=None, device=0):
     [F, B, T] (bool) is interpolated over first (NoiseStatistics).
     """
     torch = _torch()
+    device = N.current_device() if device is None else int(device)
     dev = torch.device('cuda', device)
     t = to_device(tod, torch.float64, dev)
     F, B, T = t.shape

@@ -179,8 +179,10 @@ int comap_power_spectra(comap_ctx *ctx, const double *tod_dev, int32_t n_rows, i
 /* Fills a device-resident synthetic observation with the statistics of
  * tod f32 [F][4][1024][T], band_average f32 [F][4][T].
  * level/mult/hot dev f64 [F][T] are the per-sample sky level (K),
- * multiplicative gain drift and hot-load excess prepared by the host. */
-int comap_synth_tod(comap_ctx *ctx, int32_t n_feeds, int64_t n_samples, uint64_t seed,
+ * multiplicative gain drift and hot-load excess prepared by the host.
+ * feed0: index of the first generated feed in the whole observation (a feed
+ * shard of an observation gets the same samples as the full cube). */
+int comap_synth_tod(comap_ctx *ctx, int32_t n_feeds, int32_t feed0, int64_t n_samples, uint64_t seed,
                     const double *level_dev, const double *mult_dev, const double *hot_dev,
                     float *tod_dev, float *band_average_dev);
 

@@ -72,7 +72,7 @@ def test_host_prep_matches_reference_with_checker_median(case_store, golden, nam
     import oracle
     from comapreduce_amd.tools import medfilt as mf
 
-    def checker(series, w, reflect=False):
+    def checker(series, w, reflect=False, device=None):
         out = []
         for s in series:
             z = np.concatenate((s[::-1], s, s[::-1])) if reflect else s.copy()

@@ -1,0 +1,97 @@
+"""Full-size C2 parity (BASELINE configs[1]): the 19-feed x 4 x 1024 x 180,000
+observation (56 GB f32, generated on device exactly as bench.py does) reduced
+by the three device stages, checked against the CPU oracle (oracle/l1.py,
+pinned to the reference goldens) on (feed, scan) units that cover the first,
+a middle and the last feed and the first, middle and last scans:
+
+  * vane Tsys / gain of each checked feed: bit-exact (VaneCalibration.py:67-198);
+  * atmosphere fit of each unit: <= 1e-5 relative (Level1Averaging.py:197-227);
+  * averaged_tod tod / tod_original / weights of each unit: <= 1e-5 relative
+    (Level1Averaging.py:792-872, north_star tolerance);
+  * shapes and the finite / zero pattern of every averaged_tod array.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-5
+F, T = 19, 180_000
+
+
+def relmax(a, b):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    fin = np.isfinite(b)
+    assert np.array_equal(np.isfinite(a), fin), 'NaN pattern differs'
+    return np.max(np.abs(a[fin] - b[fin])) / max(np.max(np.abs(b[fin])), 1e-300)
+
+
+@pytest.fixture(scope='module')
+def c2():
+    import torch
+    import bench
+    from comapreduce_amd.pipeline.datahandling import to_host
+    data, sh = bench.build_observation(F, T, obs_id=1, device=0)
+    level2 = bench.reduce_step(data, 0)
+    torch.cuda.synchronize()
+    host = {k: to_host(level2[k]) for k in ('vane/system_temperature', 'vane/system_gain', 'atmosphere/fit_values',
+                                            'averaged_tod/tod', 'averaged_tod/tod_original',
+                                            'averaged_tod/weights')}
+    host['averaged_tod/scan_edges'] = np.asarray(level2['averaged_tod/scan_edges'])
+    yield data, sh, host
+    del data, level2
+    torch.cuda.empty_cache()
+
+
+def test_c2_shapes_and_patterns(c2):
+    data, sh, h = c2
+    edges = h['averaged_tod/scan_edges']
+    S = len(edges)
+    assert S >= 10
+    assert h['vane/system_temperature'].shape == (1, F, 4, 1024)
+    assert h['atmosphere/fit_values'].shape == (S, F, 4, 2, 1024)
+    inside = np.zeros(T, dtype=bool)
+    for s, e in edges:
+        inside[s:e] = True
+    for k in ('averaged_tod/tod', 'averaged_tod/tod_original', 'averaged_tod/weights'):
+        a = h[k]
+        assert a.shape == (F, 4, T), k
+        assert np.isfinite(a).all(), k
+        assert not a[..., ~inside].any(), k          # samples outside every scan stay 0
+        assert (a[..., inside] != 0).mean() > 0.999, k
+    fit = h['atmosphere/fit_values']
+    fitted = np.zeros(1024, dtype=bool)
+    fitted[10:1014] = True
+    fitted[510:515] = False                          # Level1Averaging.py:201-202
+    assert np.isfinite(fit[..., fitted]).all()
+    assert np.isnan(fit[..., ~fitted]).all()
+    # every scan's weights are constant per (feed, band, scan) (1/auto_rms^2)
+    w = h['averaged_tod/weights']
+    for s, e in edges:
+        seg = w[..., s:e]
+        assert np.array_equal(seg, np.broadcast_to(seg[..., :1], seg.shape))
+
+
+@pytest.mark.parametrize('f,which', [(0, 'first'), (9, 'middle'), (18, 'last'), (5, 'first'), (13, 'middle')])
+def test_c2_units_vs_oracle(c2, f, which):
+    import oracle.l1 as ol1
+    data, sh, h = c2
+    edges = h['averaged_tod/scan_edges']
+    s = {'first': 0, 'middle': len(edges) // 2, 'last': len(edges) - 1}[which]
+    t0, t1 = (int(v) for v in edges[s])
+    tod_f = data['spectrometer/tod'][f].cpu().numpy()
+    ba_f = data['spectrometer/band_average'][f].cpu().numpy()
+    el = np.asarray(data['spectrometer/pixel_pointing/pixel_el'])[f]
+    A = 1.0 / np.sin(el * np.pi / 180.0)
+    # vane (event 0) of this feed: bit-exact
+    tsys, gain = ol1.measure_system_temperature(tod_f[None], ba_f[None], data.features, data.vane_temperature)
+    assert np.array_equal(h['vane/system_temperature'][:, f], tsys[:, 0])
+    assert np.array_equal(h['vane/system_gain'][:, f], gain[:, 0])
+    # atmosphere fit of the unit
+    fit = np.stack([np.stack(ol1.fit_atmosphere(A[t0:t1], tod_f[b, :, t0:t1])) for b in range(4)])
+    assert relmax(h['atmosphere/fit_values'][s, f], fit) < RTOL
+    # the unit's Level-2 TOD
+    r, o, w, _ = ol1.reduce_scan(tod_f[..., t0:t1].copy(), A[t0:t1], h['atmosphere/fit_values'][s, f],
+                                 tsys[0, 0], gain[0, 0], is_first_scan=(s == 0))
+    assert relmax(h['averaged_tod/tod'][f, :, t0:t1], r) < RTOL
+    assert relmax(h['averaged_tod/tod_original'][f, :, t0:t1], o) < RTOL
+    assert relmax(h['averaged_tod/weights'][f, :, t0:t1], np.broadcast_to(w[:, None], (4, t1 - t0))) < RTOL

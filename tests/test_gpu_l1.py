@@ -192,3 +192,74 @@ def test_level1_averaging_vs_reference(meta, golden_dir):
         np.asarray(level2['vane/system_gain'])[0], 256)
     assert relmax(st4.tod, ref_a) < 1e-12
     assert relmax(st4.tod_stddev, ref_s) < 1e-9
+
+
+# ---------------------------------------------------------------- multi-feed observation + C3 shards
+F3 = dict(n_feeds=3, n_samples=30_000, obs_id=5, feed_numbers=(1, 2, 20))
+
+
+@pytest.fixture(scope='module')
+def f3_gen():
+    return synthetic.generate_level1(synthetic.SyntheticConfig(**F3))
+
+
+def _reduce(data):
+    from comapreduce_amd import Analysis as A
+    level2 = COMAPLevel2(filename='/nonexistent/none.hd5')
+    for cls in (A.MeasureSystemTemperature, A.AtmosphereRemoval, A.Level1AveragingGainCorrection):
+        st = cls(level2=level2)
+        assert st(data, level2)
+        level2.update(st)
+    return level2
+
+
+KEYS = ('vane/system_temperature', 'vane/system_gain', 'atmosphere/fit_values', 'averaged_tod/tod',
+        'averaged_tod/tod_original', 'averaged_tod/weights')
+
+
+def test_multi_feed_observation_vs_oracle(f3_gen):
+    """F = 3 feeds, every (feed, scan) unit, against oracle.l1.reduce_level1; feed
+    number 20 is skipped by the reducer (Level1Averaging.py:817-818): its
+    averaged_tod rows stay 0 while its vane and atmosphere are still computed."""
+    import oracle.l1 as ol1
+    l2 = _reduce(level1_from_dict(f3_gen))
+    ref = ol1.reduce_level1(f3_gen['data'])
+    for k in ('vane/system_temperature', 'vane/system_gain'):
+        assert np.array_equal(l2[k], ref[k]), k
+    for k in KEYS[2:]:
+        assert relmax(l2[k], ref[k]) < RTOL, k
+    for k in ('averaged_tod/tod', 'averaged_tod/tod_original', 'averaged_tod/weights'):
+        assert not np.asarray(l2[k])[2].any(), k
+        assert np.asarray(l2[k])[:2].any(), k
+    assert np.isfinite(np.asarray(l2['atmosphere/fit_values'])[:, 2, :, :, 10:1014][..., :500]).all()
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_shards_bit_identical(f3_gen, world):
+    """C3 on the device: each shard (its feeds, its units only) reduced by its own
+    plan; the assembled owned slices equal the unsharded device run bit for bit."""
+    from comapreduce_amd.pipeline import sharding
+    full = _reduce(level1_from_dict(f3_gen))
+    shards, outs = [], []
+    for r in range(world):
+        sh, part = sharding.shard_level1(level1_from_dict(f3_gen), r, world)
+        l2 = _reduce(part)
+        shards.append(sh)
+        outs.append({k: l2[k] for k in KEYS})
+    S = len(full['averaged_tod/scan_edges'])
+    got = sharding.assemble(shards, outs, 3, S, F3['n_samples'])
+    for k in KEYS:
+        assert np.array_equal(got[k], np.asarray(full[k]), equal_nan=True), k
+
+
+def test_context_keeps_current_device():
+    """Creating a context and running a drop-in leave torch's current device alone."""
+    import torch
+    from comapreduce_amd import _native as N
+    from comapreduce_amd.tools.medfilt import medfilt_batch
+    before = torch.cuda.current_device()
+    for d in range(torch.cuda.device_count()):
+        N.ctx(d)
+        assert torch.cuda.current_device() == before
+    medfilt_batch([np.arange(1000.0)], 401, reflect=True)
+    assert torch.cuda.current_device() == before
