@@ -284,23 +284,41 @@ def destriper_leg(level2, data, niter, device, want_cpu=False):
                      f'{niter} CG iterations (no early exit), single rank',
            'cg_iters_per_s': res['iters'] / dt, 'iters': res['iters'], 'n_samples': int(tod.size),
            'n_offsets': int(tod.size // 50), 'prep_s': prep, 'setup_s': setup, 'nnz': prob.nnz()}
+    # all 4 sidebands: one batched read (one device median call) and ONE batched solve
+    t0 = time.perf_counter()
+    r = CD.read_comap_data_bands(list(store), c4_map_info(), bands=(0, 1, 2, 3), offset_length=50, store=store,
+                                 device=device)
+    prep4 = time.perf_counter() - t0
+    prob4 = D.DeviceDestriper(r['pointing'], r['tod'], r['weights'], 50, 480 * 480, device=device, keep=r['keep'])
+    prob4.solve(threshold=0.0, niter=3)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res4 = prob4.solve(threshold=0.0, niter=niter)
+    torch.cuda.synchronize()
+    dt4 = time.perf_counter() - t0
+    it4 = max(res4['iters'])
+    out['bands4'] = {'config': 'C4, all 4 sidebands batched (read_comap_data_bands -> one batched solve)',
+                     'band_iters_per_s': 4 * it4 / dt4, 'cg_iters_per_s': it4 / dt4, 'iters': res4['iters'],
+                     'n_samples_union': int(r['pointing'].size), 'prep_s': prep4}
     if want_cpu:
         out['cpu_port'] = cpu_destriper_port(tod, w, pix, 50, 480 * 480)
     return out
 
 
-def destriper_c5_leg(n_obs, niter, device, world, rank):
+def destriper_c5_leg(n_obs, niter, device, world, rank, n_bands=1):
     """C5: the destriper on n_obs synthetic observations' Level-2 TOD
-    (19 feeds x 180,000 samples each, one band, L = 50, 480x480 1' CAR map) per GPU,
-    weak-scaled: every rank holds its own observations; with several ranks the map
-    numerator and the CG scalars are summed over RCCL every iteration.  Roofline on
-    SURVEY §8(d)'s algorithmic bytes: 24 B per sample + 80 B per offset per iteration."""
+    (19 feeds x 180,000 samples each, L = 50, 480x480 1' CAR map) per GPU, weak-scaled:
+    every rank holds its own observations; with several ranks the map numerator and
+    the CG scalars are summed over RCCL every iteration.  n_bands > 1: that many
+    sidebands on the same pointing as one batched system.  Roofline on SURVEY
+    §8(d)'s algorithmic bytes: 24 B per sample + 80 B per offset per band-iteration."""
     import torch
     import torch.distributed as dist
     from comapreduce_amd import synthetic
     from comapreduce_amd.mapmaking import destriper as D
     L, npix = 50, 480 * 480
-    pix, tod, w = synthetic.destriper_inputs_device(n_obs, offset_length=L, device=device, seed=1000 + rank)
+    pix, tod, w = synthetic.destriper_inputs_device(n_obs, offset_length=L, device=device, seed=1000 + rank,
+                                                    n_bands=n_bands)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     prob = D.DeviceDestriper(pix, tod, w, L, npix, device=device)
@@ -319,17 +337,19 @@ def destriper_c5_leg(n_obs, niter, device, world, rank):
         e = torch.tensor([dt], device='cuda', dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         dt = float(e.item())
-    N = int(tod.numel())
+    N = int(pix.numel())
     NO = N // L
-    it = max(res['iters'], 1)
-    algo = DESTRIPER_BYTES_PER_SAMPLE * N + DESTRIPER_BYTES_PER_OFFSET * NO
+    it = max(max(res['iters']) if n_bands > 1 else res['iters'], 1)
+    algo = DESTRIPER_BYTES_PER_SAMPLE * N + DESTRIPER_BYTES_PER_OFFSET * NO     # per band-iteration
     ms = dt / it * 1e3
-    return {'config': f'C5: {n_obs} obs x 19 feeds x 180000 samples per GPU, L={L}, 480x480 CAR, '
-                      f'{niter} CG iterations (no early exit), {world} rank(s)',
-            'cg_iters_per_s': it / dt, 'ms_per_iter': ms, 'iters': res['iters'],
+    ms_band = ms / n_bands
+    return {'config': f'C5: {n_obs} obs x 19 feeds x 180000 samples per GPU, {n_bands} band(s) per solve, L={L}, '
+                      f'480x480 CAR, {niter} CG iterations (no early exit), {world} rank(s)',
+            'cg_iters_per_s': it / dt, 'band_iters_per_s': n_bands * it / dt, 'ms_per_iter': ms,
+            'ms_per_band_iter': ms_band, 'iters': res['iters'],
             'n_samples_per_gpu': N, 'n_offsets_per_gpu': NO, 'nnz': prob.nnz(), 'setup_s': setup,
-            'algo_bytes_per_iter_per_gpu': algo, 'achieved_GBs_per_gpu': algo / (ms * 1e-3) / 1e9,
-            'roofline_frac': algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+            'algo_bytes_per_band_iter_per_gpu': algo, 'achieved_GBs_per_gpu': algo / (ms_band * 1e-3) / 1e9,
+            'roofline_frac': algo / (ms_band * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
 # ---------------------------------------------------------------- main
@@ -404,6 +424,8 @@ def main():
         del data, level2, obs
         torch.cuda.empty_cache()
         c5 = destriper_c5_leg(args.c5_obs, args.destriper_iters, device, world, rank)
+        torch.cuda.empty_cache()
+        c5['bands4'] = destriper_c5_leg(args.c5_obs, args.destriper_iters, device, world, rank, n_bands=4)
 
     if rank == 0:
         value = job_sampch * args.steps / elapsed

@@ -148,8 +148,8 @@ extern "C" int comap_power_spectra(comap_ctx *ctx, const double *tod, int32_t n_
                                    const int64_t *out_offsets, double *out)
 {
     if (!ctx || !tod || !out || !edges || !out_offsets || n_rows <= 0 || T <= 0 || n_scans < 0)
-    COMAP_DEVICE_GUARD(ctx);
         return comap_fail(ctx, -1, "comap_power_spectra: bad arguments");
+    COMAP_DEVICE_GUARD(ctx);
     if (mode != 0 && mode != 1) return comap_fail(ctx, -1, "comap_power_spectra: mode must be 0 or 1");
     hipStream_t st = ctx->stream;
     int64_t nmax = 0;

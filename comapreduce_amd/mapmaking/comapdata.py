@@ -235,33 +235,10 @@ def read_comap_data(filelist, map_info, feed_weights=None, iband=0, use_gain_fil
     feedid, obsids)``.  ``store`` (tests) maps filename -> (datasets, attrs);
     ``device``: the rank's GPU for the batched median (default: torch's
     current device)."""
-    from ..tools.medfilt import medfilt_batch
     if healpix:
         raise NotImplementedError('HEALPix pixelisation (read_pixels_healpix) is not built yet')
-    open_file = _opener(store)
-    Nfeeds = len(feeds)
-    files = [open_file(fn) for fn in filelist]
-    sizes = [countDataSize(f, Nfeeds, offset_length) for f in files]
-    queue, preps, pix = [], [], []
-    for fn, f, info in zip(filelist, files, sizes):
-        ds = int(info['datasize'])
-        pix.append(read_pixels(f, ds, offset_length, feeds, map_info))
-        preps.append(_FilePrep(f, ds, offset_length, feeds, use_gain_filter, iband, calibration, calibrator, queue))
-    filtered = medfilt_batch(queue, MEDFILT_STEP, reflect=True, device=device)
-    parts = [p.finish(filtered) for p in preps]
-    N = sum(i['N'] for i in sizes)
-    tod, weights, az, el, ra, dec = (np.zeros(N) for _ in range(6))
-    pointing = np.zeros(N, dtype=int)
-    feedid = np.zeros(N, dtype=int)
-    obsids = np.zeros(N, dtype=int)
-    last = 0
-    for fn, out, p in zip(filelist, parts, pix):
-        n = out[0].size
-        for arr, v in zip((tod, weights, az, el, ra, dec, feedid), out):
-            arr[last:last + n] = v
-        pointing[last:last + n] = p.ravel()
-        obsids[last:last + n] = int(os.path.basename(fn).split('-')[1])
-        last += n
+    (tod,), (weights,), pointing, az, el, ra, dec, feedid, obsids = _read_uncut(
+        filelist, map_info, (iband,), use_gain_filter, offset_length, feeds, calibration, calibrator, store, device)
     mask = ~np.isfinite(tod)
     tod[mask] = 0
     weights[mask] = 0
@@ -271,3 +248,85 @@ def read_comap_data(filelist, map_info, feed_weights=None, iband=0, use_gain_fil
     weights[~np.isfinite(weights)] = 0
     remapping_array = find_unique_values(np.unique(pointing))
     return tod, weights, pointing, remapping_array.astype(int), az, el, ra, dec, feedid, obsids
+
+
+def _read_uncut(filelist, map_info, bands, use_gain_filter, offset_length, feeds, calibration, calibrator, store,
+                device):
+    """Per-band tod / weights (lists) and the band-independent vectors of
+    read_comap_data before its NaN and empty-offset cuts.  Every band's
+    400-sample high-pass series of every file go through ONE batched device
+    median call."""
+    from ..tools.medfilt import medfilt_batch
+    open_file = _opener(store)
+    Nfeeds = len(feeds)
+    files = [open_file(fn) for fn in filelist]
+    sizes = [countDataSize(f, Nfeeds, offset_length) for f in files]
+    queue, preps, pix = [], [], []
+    for fn, f, info in zip(filelist, files, sizes):
+        ds = int(info['datasize'])
+        pix.append(read_pixels(f, ds, offset_length, feeds, map_info))
+        preps.append([_FilePrep(f, ds, offset_length, feeds, use_gain_filter, b, calibration, calibrator, queue)
+                      for b in bands])
+    filtered = medfilt_batch(queue, MEDFILT_STEP, reflect=True, device=device)
+    parts = [[p.finish(filtered) for p in per_band] for per_band in preps]
+    N = sum(i['N'] for i in sizes)
+    tods = [np.zeros(N) for _ in bands]
+    wts = [np.zeros(N) for _ in bands]
+    az, el, ra, dec = (np.zeros(N) for _ in range(4))
+    pointing = np.zeros(N, dtype=int)
+    feedid = np.zeros(N, dtype=int)
+    obsids = np.zeros(N, dtype=int)
+    last = 0
+    for fn, outs, p in zip(filelist, parts, pix):
+        n = outs[0][0].size
+        for k, out in enumerate(outs):
+            tods[k][last:last + n] = out[0]
+            wts[k][last:last + n] = out[1]
+        for arr, v in zip((az, el, ra, dec, feedid), outs[0][2:]):
+            arr[last:last + n] = v
+        pointing[last:last + n] = p.ravel()
+        obsids[last:last + n] = int(os.path.basename(fn).split('-')[1])
+        last += n
+    return tods, wts, pointing, az, el, ra, dec, feedid, obsids
+
+
+def read_comap_data_bands(filelist, map_info, bands=(0, 1, 2, 3), use_gain_filter=True, offset_length=50,
+                          feeds=[i + 1 for i in range(19)], calibration=False, calibrator='TauA', healpix=False,
+                          store=None, device=None):
+    """read_comap_data for several bands at once, for the batched destriper
+    (run_destriper.py:146-189 calls read_comap_data once per band on the same
+    files; only tod and weights depend on the band).
+
+    Each band gets the reference's NaN cut (tod and weight 0).  The reference
+    then drops the offsets whose weights are all zero -- per band, so the
+    bands' sample sets differ; here the samples of every offset that ANY band
+    keeps are returned, with keep[b, o] saying whether band b's own
+    read_comap_data would have kept offset o (its weights there are all 0 when
+    not).  Band b's kept samples, in order, are exactly what
+    read_comap_data(iband=b) returns.
+
+    Returns dict: tod, weights [nb, N]; keep uint8 [nb, N/L]; pointing, az, el,
+    ra, dec, feedid, obsids [N]; remapping_array (unique pixels of the union)."""
+    if healpix:
+        raise NotImplementedError('HEALPix pixelisation (read_pixels_healpix) is not built yet')
+    tods, wts, pointing, az, el, ra, dec, feedid, obsids = _read_uncut(
+        filelist, map_info, tuple(bands), use_gain_filter, offset_length, feeds, calibration, calibrator, store,
+        device)
+    keeps = []
+    for t, w in zip(tods, wts):
+        bad = ~np.isfinite(t)
+        t[bad] = 0
+        w[bad] = 0
+        keeps.append((w != 0).reshape(-1, offset_length).any(axis=1))
+    keep = np.stack(keeps) if keeps else np.zeros((0, pointing.size // offset_length), dtype=bool)
+    union = keep.any(axis=0)
+    sel = np.repeat(union, offset_length)
+    tod = np.stack([t[sel] for t in tods])
+    weights = np.stack([w[sel] for w in wts])
+    weights[~np.isfinite(weights)] = 0
+    pointing = pointing[sel]
+    out = {'tod': tod, 'weights': weights, 'keep': keep[:, union].astype(np.uint8), 'pointing': pointing,
+           'az': az[sel], 'el': el[sel], 'ra': ra[sel], 'dec': dec[sel], 'feedid': feedid[sel],
+           'obsids': obsids[sel]}
+    out['remapping_array'] = find_unique_values(np.unique(pointing)).astype(int)
+    return out

@@ -50,6 +50,8 @@ def cg_solve(ops, allreduce, threshold=1e-6, niter=100, h=None, nnum=None):
     rank's samples; allreduce(array) sums in place across ranks.  h / nnum
     are the global weight map and naive numerator (computed when None).
     Returns (x, iterations, h, nnum)."""
+    if getattr(ops, 'nb', 1) != 1:
+        raise ValueError('cg_solve drives one band; batched bands use cg_solve_batched')
     if h is None or nnum is None:
         h0, _, n0 = ops.local_maps()
         h = allreduce(h0)
@@ -88,25 +90,28 @@ def cg_solve(ops, allreduce, threshold=1e-6, niter=100, h=None, nnum=None):
 def cg_solve_batched(ops, allreduce, threshold=1e-6, niter=100, batch=16):
     """Multi-rank CG of the device path: the iterates of ``cg_solve`` (same
     order of operations and cross-rank sums), but with the convergence test on
-    the device (comap_destripe_dist_direction's stop flag) so ``batch``
+    the device (comap_destripe_dist_direction's stop flags) so ``batch``
     iterations -- kernels and all-reduces -- are queued per host round trip.
     Iterations queued after convergence are no-ops (their all-reduces sum
-    stale buffers that are not read again).  Returns (x, iterations, h, nnum)."""
+    stale buffers that are not read again).  Works for every band of a batched
+    problem at once (vectors interleaved [n][nb], one all-reduce per sum for
+    all bands).  Returns (x, iterations per band (list), h, nnum)."""
     torch = ops.torch
+    nb = ops.nb
     h0, _, n0 = ops.local_maps()
     h = allreduce(h0)
     nnum = allreduce(n0)
     NO = ops.n_offsets
-    x, r, q = ops.zeros(NO), ops.zeros(NO), ops.zeros(NO)
-    num = ops.zeros(ops.npix)
+    x, r, q = ops.zeros(NO * nb), ops.zeros(NO * nb), ops.zeros(NO * nb)
+    num = ops.zeros(ops.npix * nb)
     ops.project(None, nnum, h, r)
     p = ops.copy(r)
-    scal = ops.zeros(8)
-    ops.dot(r, r, scal[0:1])
-    allreduce(scal[0:1])
-    scal[1:2].copy_(scal[0:1])
-    scal[4] = float(threshold)
-    flags = torch.zeros(2, dtype=torch.int32, device=ops.dev)
+    scal = ops.zeros(4 * nb + 1)        # rr0, rr, pq, rr_new (nb each), threshold
+    ops.dot(r, r, scal[0:nb])
+    allreduce(scal[0:nb])
+    scal[nb:2 * nb].copy_(scal[0:nb])
+    scal[4 * nb] = float(threshold)
+    flags = torch.zeros(2 + 2 * nb, dtype=torch.int32, device=ops.dev)
     enq = 0
     while enq < niter:
         k = min(batch, niter - enq)
@@ -114,30 +119,42 @@ def cg_solve_batched(ops, allreduce, threshold=1e-6, niter=100, batch=16):
             ops.dist_bin(p, num, flags)
             allreduce(num)
             ops.dist_project(p, num, h, q, scal, flags)
-            allreduce(scal[2:3])
+            allreduce(scal[2 * nb:3 * nb])
             ops.dist_update(scal, x, r, p, q, flags)
-            allreduce(scal[3:4])
+            allreduce(scal[3 * nb:4 * nb])
             ops.dist_direction(scal, p, r, flags)
         enq += k
         if int(flags[0].item()):
             break
-    return x, int(flags[1].item()), h, nnum
+    return x, [int(v) for v in flags[2 + nb:2 + 2 * nb].tolist()], h, nnum
 
 
 class DeviceOps:
-    """One rank's destriper operator on the GPU (comap_destripe_* C ABI)."""
+    """One rank's destriper operator on the GPU (comap_destripe_* C ABI).
 
-    def __init__(self, pixels, tod, weights, offset_length, npix, device=None):
+    ``tod``/``weights`` are [N] (one band) or [n_bands, N] (several sidebands on
+    the same ``pixels``, solved as one batched system -- comap_destripe_create_bands;
+    3 bands are padded to 4 with an empty band).  ``keep`` (optional, [n_bands,
+    N/L]) marks the offsets each band's data prep kept.  Per-band vectors are
+    interleaved band-fastest ([N/L][nb], [npix][nb])."""
+
+    def __init__(self, pixels, tod, weights, offset_length, npix, device=None, keep=None):
         import torch
         self.torch = torch
         device = N.current_device() if device is None else int(device)
         self.dev = torch.device('cuda', device)
         self.ctx = N.ctx(device)
         self.pix = self._t(pixels, torch.int32)
-        self.tod = self._t(tod, torch.float64)
-        self.w = self._t(weights, torch.float64)
-        n = self.tod.numel()
-        if self.pix.numel() != n or self.w.numel() != n:
+        tod2 = self._t2(tod, torch.float64)
+        w2 = self._t2(weights, torch.float64)
+        self.n_bands = int(tod2.shape[0])           # bands the caller asked for
+        if w2.shape != tod2.shape:
+            raise ValueError('tod and weights must have the same shape')
+        if self.n_bands not in (1, 2, 3, 4):
+            raise ValueError('1 to 4 bands per problem')
+        self.nb = 4 if self.n_bands == 3 else self.n_bands
+        n = int(tod2.shape[1])
+        if self.pix.numel() != n:
             raise ValueError('pointing, tod and weights must have the same length')
         if n % offset_length:
             raise ValueError('number of samples must be a multiple of offset_length')
@@ -145,11 +162,23 @@ class DeviceOps:
         if pmax >= npix:
             raise IndexError(f'pixel index {pmax} out of range for a map of {npix} pixels')
         self.L, self.npix = int(offset_length), int(npix)
+        kp = None
+        if keep is not None:
+            kp = self._t2(keep, torch.uint8)
+            if kp.shape != (self.n_bands, n // self.L):
+                raise ValueError('keep must be [n_bands, n_samples // offset_length]')
+        if self.nb != self.n_bands:              # pad 3 -> 4 bands with an empty band
+            z = torch.zeros((1, n), dtype=torch.float64, device=self.dev)
+            tod2, w2 = torch.cat([tod2, z]), torch.cat([w2, z])
+            if kp is not None:
+                kp = torch.cat([kp, torch.zeros((1, n // self.L), dtype=torch.uint8, device=self.dev)])
+        self.tod, self.w, self.keep = tod2.contiguous(), w2.contiguous(), kp
         h = ctypes.c_void_p()
         N.bind_stream(self.ctx, self.dev)
-        N.check(N.lib().comap_destripe_create(self.ctx, N.dptr(self.pix), N.dptr(self.tod), N.dptr(self.w), n,
-                                              self.L, self.npix, ctypes.byref(h)), self.ctx,
-                'comap_destripe_create')
+        N.check(N.lib().comap_destripe_create_bands(self.ctx, N.dptr(self.pix), N.dptr(self.tod), N.dptr(self.w),
+                                                    None if kp is None else N.dptr(kp), n, self.L, self.npix,
+                                                    self.nb, ctypes.byref(h)), self.ctx,
+                'comap_destripe_create_bands')
         self.h = h
         self.n_offsets = int(N.lib().comap_destripe_n_offsets(h))
 
@@ -158,6 +187,16 @@ class DeviceOps:
         if isinstance(a, torch.Tensor):
             return a.to(device=self.dev, dtype=dt).contiguous().reshape(-1)
         return torch.from_numpy(np.ascontiguousarray(a)).to(device=self.dev, dtype=dt).reshape(-1)
+
+    def _t2(self, a, dt):
+        torch = self.torch
+        t = a if isinstance(a, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(a))
+        t = t.to(device=self.dev, dtype=dt)
+        return t.reshape(1, -1).contiguous() if t.dim() == 1 else t.contiguous()
+
+    def split_bands(self, v):
+        """[n*nb] interleaved -> [n_bands, n] (contiguous copy, padding band dropped)."""
+        return v.reshape(-1, self.nb).t()[:self.n_bands].contiguous()
 
     def __del__(self):
         try:
@@ -237,19 +276,27 @@ class DeviceOps:
 
     # ---- single-rank native solve (no Python per iteration)
     def solve_native(self, threshold, niter):
-        x = self.zeros(self.n_offsets)
-        maps = {k: self.zeros(self.npix) for k in ('map', 'naive', 'weight', 'hits')}
-        it = ctypes.c_int32(0)
+        """x [N/L * nb], iterations per band (list), maps {k: [npix * nb]} (interleaved)."""
+        nb = self.nb
+        x = self.zeros(self.n_offsets * nb)
+        maps = {k: self.zeros(self.npix * nb) for k in ('map', 'naive', 'weight', 'hits')}
+        it = (ctypes.c_int32 * nb)()
         self._c('comap_destripe_solve', self.h, float(threshold), int(niter), N.dptr(x), N.dptr(maps['map']),
-                N.dptr(maps['naive']), N.dptr(maps['weight']), N.dptr(maps['hits']), ctypes.byref(it))
-        return x, int(it.value), maps
+                N.dptr(maps['naive']), N.dptr(maps['weight']), N.dptr(maps['hits']),
+                ctypes.cast(it, ctypes.POINTER(ctypes.c_int32)))
+        return x, [int(v) for v in it][:self.n_bands], maps
 
 
 class DeviceDestriper:
-    """Convenience wrapper: the whole destriper_iteration on device tensors."""
+    """Convenience wrapper: the whole destriper_iteration on device tensors.
 
-    def __init__(self, pixels, tod, weights, offset_length, npix, device=None):
-        self.ops = DeviceOps(pixels, tod, weights, offset_length, npix, device)
+    One band ([N] tod/weights): solve() -> {'x': [N/L], 'iters': int,
+    'maps': {k: [npix]}}.  Several bands ([n_bands, N], one batched system):
+    {'x': [n_bands, N/L], 'iters': [per band], 'maps': {k: [n_bands, npix]}}."""
+
+    def __init__(self, pixels, tod, weights, offset_length, npix, device=None, keep=None):
+        self.ops = DeviceOps(pixels, tod, weights, offset_length, npix, device, keep)
+        self.multi = np.ndim(tod) == 2 if not hasattr(tod, 'dim') else tod.dim() == 2
 
     def nnz(self):
         return self.ops.nnz()
@@ -259,19 +306,24 @@ class DeviceDestriper:
         ops = self.ops
         if d is None or d.get_world_size() == 1:
             x, it, maps = ops.solve_native(threshold, niter)
+        else:
+            x, it, h, nnum = cg_solve_batched(ops, torch_allreduce, threshold, niter)
+            _, hits, _ = ops.local_maps()
+            torch_allreduce(hits)
+            num = ops.zeros(ops.npix * ops.nb)
+            ops.bin(x, 1, num)
+            torch_allreduce(num)
+            maps = {'map': ops.zeros(ops.npix * ops.nb), 'naive': ops.zeros(ops.npix * ops.nb), 'weight': h,
+                    'hits': hits}
+            ops.div_map(num, h, maps['map'])
+            ops.div_map(nnum, h, maps['naive'])
+            it = it[:ops.n_bands]
+        if not self.multi:
             maps['map2'] = maps['weight']
-            return {'x': x, 'iters': it, 'maps': maps}
-        x, it, h, nnum = cg_solve_batched(ops, torch_allreduce, threshold, niter)
-        _, hits, _ = ops.local_maps()
-        torch_allreduce(hits)
-        num = ops.zeros(ops.npix)
-        ops.bin(x, 1, num)
-        torch_allreduce(num)
-        maps = {'map': ops.zeros(ops.npix), 'naive': ops.zeros(ops.npix), 'weight': h, 'hits': hits}
-        ops.div_map(num, h, maps['map'])
-        ops.div_map(nnum, h, maps['naive'])
-        maps['map2'] = h
-        return {'x': x, 'iters': it, 'maps': maps}
+            return {'x': x, 'iters': it[0], 'maps': maps}
+        maps = {k: ops.split_bands(v) for k, v in maps.items()}
+        maps['map2'] = maps['weight']
+        return {'x': ops.split_bands(x), 'iters': it, 'maps': maps}
 
 
 def run_destriper(_pointing, _tod, _weights, offset_length, pixel_edges, az=None, el=None, ra=None, dec=None,
@@ -296,6 +348,38 @@ def run_destriper(_pointing, _tod, _weights, offset_length, pixel_edges, az=None
         return {'All': {'map': None, 'naive': None, 'weight': None, 'map2': None}}
     maps = {k: v.cpu().numpy() for k, v in res['maps'].items()}
     return {'All': maps}
+
+
+def run_destriper_bands(_pointing, _tods, _weights, offset_length, pixel_edges, keep=None, threshold=1e-6,
+                        niter=100, device=None):
+    """run_destriper for several sidebands on the same pointing in ONE batched
+    device solve (the reference calls run_destriper once per band,
+    run_destriper.py:146-189).  _tods/_weights [n_bands, N]; keep [n_bands, N/L]
+    as returned by comapdata.read_comap_data_bands.  Returns one
+    {'All': maps} per band (host maps on rank 0, None maps on other ranks);
+    band b's maps and iteration count are those of run_destriper on band b's
+    own samples, and its offsets (``x``, rank 0: also under 'offsets') cover
+    the union of the bands' offsets (0 where band b dropped the offset)."""
+    import torch
+    if device is None:
+        device = torch.cuda.current_device()
+    npix = int(pixel_edges[-1]) + 1
+    tods = np.asarray(_tods, dtype=np.float64)
+    if tods.ndim != 2:
+        raise ValueError('_tods must be [n_bands, N]')
+    dd = DeviceDestriper(np.asarray(_pointing), tods, np.asarray(_weights, dtype=np.float64), int(offset_length), npix,
+                         device, keep=None if keep is None else np.asarray(keep, dtype=np.uint8))
+    res = dd.solve(threshold, niter)
+    d = _dist()
+    rank = d.get_rank() if d is not None else 0
+    out = []
+    for b in range(tods.shape[0]):
+        if rank != 0:
+            out.append({'All': {'map': None, 'naive': None, 'weight': None, 'map2': None}})
+            continue
+        maps = {k: v[b].cpu().numpy() for k, v in res['maps'].items()}
+        out.append({'All': maps, 'iters': res['iters'][b], 'offsets': res['x'][b].cpu().numpy()})
+    return out
 
 
 # ---------------------------------------------------------------- bench helper

@@ -20,7 +20,7 @@ import os
 import numpy as np
 
 from . import comapdata as COMAPData
-from .destriper import run_destriper
+from .destriper import run_destriper, run_destriper_bands
 from .fits import write_image_hdus
 from ..tools.parser import Parser, sex2deg
 
@@ -56,10 +56,14 @@ def main(filelistname, offset_length=50, feed_weights=None, prefix='fg9', output
          feeds=[1, 2, 3, 5, 6, 9, 11, 12, 13, 14, 15, 16, 17, 18, 19], nxpix=480, nypix=480,
          crval=['05:32:00.3', '+12:30:28.0'], crpix=[240, 240], ctype=['RA---CAR', 'DEC--CAR'],
          cdelt=[-0.016666, 0.016666], use_gain_filter=True, calibration=True, calibrator='TauA', threshold=1e-6,
-         niter=100, healpix=False, bands=(0, 1, 2, 3), store=None, device=None):
+         niter=100, healpix=False, bands=(0, 1, 2, 3), store=None, device=None, batch_bands=True):
     """run_destriper.main (run_destriper.py:79-189).  ``store`` (tests) maps
     filename -> (datasets, attrs) instead of reading files; ``device`` is the
-    rank's GPU (default: torch's current device, LOCAL_RANK under torchrun)."""
+    rank's GPU (default: torch's current device, LOCAL_RANK under torchrun).
+    ``batch_bands``: the bands share the pointing, so they are read with one
+    batched median call and solved as ONE batched device system
+    (read_comap_data_bands + run_destriper_bands); False runs the reference's
+    per-band loop.  The maps are the same either way."""
     rank, size = _rank_size()
     if device is None:
         import torch
@@ -87,6 +91,19 @@ def main(filelistname, offset_length=50, feed_weights=None, prefix='fg9', output
     if healpix:
         raise NotImplementedError('HEALPix maps (write_map_healpix) are not built yet')
     out = {}
+    if batch_bands and len(bands) > 1:
+        r = COMAPData.read_comap_data_bands(filelist, map_info, bands=bands, offset_length=offset_length, feeds=feeds,
+                                            use_gain_filter=use_gain_filter, calibration=calibration,
+                                            calibrator=calibrator, healpix=healpix, store=store, device=device)
+        pixel_edges = np.arange(nxpix * nypix)
+        res = run_destriper_bands(r['pointing'], r['tod'], r['weights'], offset_length, pixel_edges, keep=r['keep'],
+                                  threshold=threshold, niter=niter, device=device)
+        for iband, maps in zip(bands, res):
+            maps = {'All': maps['All']}
+            if rank == 0:
+                write_map(prefix, maps, map_info, output_dir, iband)
+            out[iband] = maps
+        return out
     for iband in bands:
         tod, weights, pointing, remap, az, el, ra, dec, feedid, obsids = COMAPData.read_comap_data(
             filelist, map_info, feed_weights=feed_weights, offset_length=offset_length, iband=iband, feeds=feeds,

@@ -324,13 +324,26 @@ def level2_mapmaking(obs_id: int, n_feeds: int = 19, n_samples: int = 45_000, sk
 
 
 def destriper_inputs_device(n_obs: int, n_feeds: int = 19, n_samples: int = 180_000, offset_length: int = 50,
-                            nx: int = 480, ny: int = 480, cdelt: float = 1.0 / 60.0, device: int = 0, seed: int = 0):
+                            nx: int = 480, ny: int = 480, cdelt: float = 1.0 / 60.0, device: int = 0, seed: int = 0,
+                            n_bands: int = 1):
     """Destriper inputs at the SURVEY.md §8(d) C5 scale, generated on the device
-    (bench only): n_obs observations x n_feeds feeds x n_samples samples of one
-    band, each (obs, feed) series cut to a multiple of offset_length; Lissajous
+    (bench only): n_obs observations x n_feeds feeds x n_samples samples,
+    each (obs, feed) series cut to a multiple of offset_length; Lissajous
     pointing over an nx x ny CAR field (pixel = floor(x + 0.5), off-map -> -1),
     smooth sky + random-walk (1/f) offsets + white noise, inverse-variance
-    weights.  Returns (pixels int32, tod f64, weights f64) CUDA tensors."""
+    weights.  Returns (pixels int32 [N], tod f64, weights f64) CUDA tensors;
+    tod / weights are [N] for n_bands = 1, else [n_bands, N] (the same sky and
+    pointing, independent offsets and noise per band)."""
+    if n_bands > 1:
+        pix, t0, w0 = destriper_inputs_device(n_obs, n_feeds, n_samples, offset_length, nx, ny, cdelt, device, seed)
+        import torch
+        tods, ws = [t0], [w0]
+        for b in range(1, n_bands):
+            _, tb, wb = destriper_inputs_device(n_obs, n_feeds, n_samples, offset_length, nx, ny, cdelt, device,
+                                                seed + 7919 * b)
+            tods.append(tb)
+            ws.append(wb)
+        return pix, torch.stack(tods), torch.stack(ws)
     import math
     import torch
     dev = torch.device('cuda', device)

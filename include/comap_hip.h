@@ -194,8 +194,21 @@ int comap_synth_tod(comap_ctx *ctx, int32_t n_feeds, int32_t feed0, int64_t n_sa
 int comap_destripe_create(comap_ctx *ctx, const int32_t *pixels_dev, const double *tod_dev,
                           const double *weights_dev, int64_t n_samples, int32_t offset_length,
                           int64_t npix, comap_destriper **out);
+/* n_bands (1, 2 or 4) sidebands on the same pointing solved as one batched
+ * system (run_destriper.py:146-189 loops the bands over one pointing):
+ * tod/weights dev f64 [n_bands][N] band-major; keep_dev (optional, uint8
+ * [n_bands][N/L]): 0 marks an offset the band's data prep dropped (all its
+ * weights are 0 in that band; its samples are then left out of the band's
+ * hit map, COMAPData.py:550-568).  Every per-band vector of the functions below
+ * is interleaved band-fastest: offsets [N/L][n_bands], maps [npix][n_bands];
+ * each band's CG keeps its own scalars, stop test and iteration count.
+ * comap_destripe_create is this with n_bands = 1. */
+int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pixels_dev, const double *tod_dev,
+                                const double *weights_dev, const uint8_t *keep_dev, int64_t n_samples,
+                                int32_t offset_length, int64_t npix, int32_t n_bands, comap_destriper **out);
 int comap_destripe_destroy(comap_destriper *d);
 int64_t comap_destripe_n_offsets(const comap_destriper *d);
+int32_t comap_destripe_n_bands(const comap_destriper *d);
 int comap_destripe_nnz(const comap_destriper *d, int64_t *nnz_offset_major, int64_t *nnz_pixel_major);
 /* Local (this rank) sample-level maps, summed in binValues order:
  * h = sum w, hits = sum 1, naive_num = sum w tod (any may be NULL). */
@@ -208,7 +221,7 @@ int comap_destripe_bin(comap_destriper *d, const double *x_dev, int32_t mode, do
  * local weight map.  dot_dev (optional, needs x) receives y.x. */
 int comap_destripe_project(comap_destriper *d, const double *x_dev, const double *num_dev,
                            const double *h_dev, double *y_dev, double *dot_dev);
-/* dot_dev[0] = sum a b over the N/L offsets (fixed-order reduction) */
+/* dot_dev[b] = sum a b over the N/L offsets, per band (fixed-order reduction) */
 int comap_destripe_dot(comap_destriper *d, const double *a_dev, const double *b_dev, double *dot_dev);
 /* alpha = rr/pq; x += alpha p; r -= alpha q; rr_new = r.r (device scalars) */
 int comap_destripe_cg_update(comap_destriper *d, const double *rr_dev, const double *pq_dev,
@@ -218,18 +231,20 @@ int comap_destripe_cg_update(comap_destriper *d, const double *rr_dev, const dou
 int comap_destripe_cg_direction(comap_destriper *d, const double *rr_new_dev, const double *rr_dev,
                                 double *p_dev, const double *r_dev);
 /* Multi-rank CG iteration (Destriper.py:85-152 with p == pb), split at the
- * three cross-rank sums the caller performs between the calls:
+ * three cross-rank sums the caller performs between the calls (NB = bands):
  *   dist_bin        num = W p (local numerator)          -> all-reduce num
  *   dist_project    q = F^T W (F p - m[p]), m = num/h;
- *                   scal[2] = local q.p                   -> all-reduce scal[2]
- *   dist_update     alpha = scal[1]/scal[2]; x += alpha p; r -= alpha q;
- *                   scal[3] = local r.r                   -> all-reduce scal[3]
- *   dist_direction  p = r + (scal[3]/scal[1]) p; scal[1] = scal[3];
- *                   flags[1] += 1; flags[0] = 1 when scal[3]/scal[0] is NaN
- *                   or below scal[4] (threshold).
- * Every kernel returns at once when flags[0] is set, so a batch of iterations
- * can be queued with one host check of flags per batch.  scal_dev f64 [>= 5]:
- * rr0, rr, pq, rr_new, threshold; flags_dev int32 [2]: stop, iterations. */
+ *                   pq = local q.p                        -> all-reduce pq
+ *   dist_update     alpha = rr/pq; x += alpha p; r -= alpha q;
+ *                   rr_new = local r.r                    -> all-reduce rr_new
+ *   dist_direction  p = r + (rr_new/rr) p; rr = rr_new; per band: count the
+ *                   iteration, stop when rr_new/rr0 is NaN or below threshold.
+ * scal_dev f64 [4 NB + 1], k-major: rr0[NB], rr[NB], pq[NB], rr_new[NB],
+ * threshold; flags_dev int32 [2 + 2 NB]: all bands stopped, iterations any band
+ * ran, stopped[NB], iterations[NB].  A stopped band is left unchanged and every
+ * kernel returns at once when flags[0] is set, so a batch of iterations can be
+ * queued with one host check of flags per batch (NB = 1: rr0, rr, pq, rr_new,
+ * threshold / stop, iterations). */
 int comap_destripe_dist_bin(comap_destriper *d, const double *p_dev, double *num_dev, const int32_t *flags_dev);
 int comap_destripe_dist_project(comap_destriper *d, const double *p_dev, const double *num_dev,
                                 const double *h_dev, double *q_dev, double *scal_dev, const int32_t *flags_dev);
@@ -239,13 +254,13 @@ int comap_destripe_dist_direction(comap_destriper *d, double *scal_dev, double *
                                   int32_t *flags_dev);
 /* out = num/h (num where h == 0); h_dev == NULL uses the local weight map */
 int comap_destripe_div_map(comap_destriper *d, const double *num_dev, const double *h_dev, double *out_dev);
-/* Whole single-rank destriper_iteration (no collectives): CG (one matvec
- * per iteration, Destriper.py:85-152) to threshold / niter, then the final
- * maps.  Iterations run as replayed hipGraph batches on the problem's own
- * stream with a device-side stop flag (identical iterates and count to a
- * per-iteration loop).  Writes offsets x [N/L] and map/naive/weight/hits
- * [npix] (any map pointer may be NULL); *iters_out = iterations performed.
- * Synchronises. */
+/* Whole single-rank destriper_iteration (no collectives) for every band: CG
+ * (one matvec per iteration, Destriper.py:85-152) to threshold / niter, then
+ * the final maps.  Iterations run as replayed hipGraph batches on the
+ * problem's own stream with device-side stop flags (identical iterates and
+ * count to a per-iteration loop, per band).  Writes offsets x [N/L][NB] and
+ * map/naive/weight/hits [npix][NB] (any map pointer may be NULL);
+ * iters_out[b] = iterations band b performed.  Synchronises. */
 int comap_destripe_solve(comap_destriper *d, double threshold, int32_t niter, double *x_dev,
                          double *map_dev, double *naive_dev, double *weight_dev,
                          double *hits_dev, int32_t *iters_out);

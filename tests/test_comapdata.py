@@ -140,3 +140,34 @@ def test_transform_to_1d_offmap():
     w = CelestialWCS([10.0, 0.0], [-1.0, 1.0], [3, 3], ['RA---CAR', 'DEC--CAR'])
     idx = transform_to_1d(np.array([10.0, 20.0, 10.0, 9.0]), np.array([0.0, 0.0, 5.0, 1.0]), w, 5, 5)
     assert idx.tolist() == [2 * 5 + 2, -1, -1, 3 * 5 + 3]
+
+
+def test_read_comap_data_bands_equals_per_band(case_store, monkeypatch):
+    """read_comap_data_bands (one call for all bands, the batched destriper's
+    input) restricted to band b's kept offsets == read_comap_data(iband=b)."""
+    import oracle
+    from comapreduce_amd.tools import medfilt as mf
+
+    def checker(series, w, reflect=False, device=None):
+        out = []
+        for s in series:
+            z = np.concatenate((s[::-1], s, s[::-1])) if reflect else s.copy()
+            y = oracle.medfilt(z.astype(np.float64), int(w))
+            out.append(y[s.size:2 * s.size] if reflect else y)
+        return out
+    monkeypatch.setattr(mf, 'medfilt_batch', checker)
+    store, names = case_store
+    case = cc.CASES['car']
+    kw = {k: v for k, v in case['kw'].items() if k != 'iband'}
+    r = cd.read_comap_data_bands(names, map_info(case['map']), bands=(0, 1, 2, 3), feeds=cc.FEEDS, store=store, **kw)
+    L = kw.get('offset_length', 50)
+    assert r['tod'].shape[0] == 4 and r['keep'].shape == (4, r['pointing'].size // L)
+    for b in range(4):
+        one = cd.read_comap_data(names, map_info(case['map']), feeds=cc.FEEDS, store=store, iband=b, **kw)
+        sel = np.repeat(r['keep'][b].astype(bool), L)
+        for k, v in (('tod', r['tod'][b]), ('weights', r['weights'][b]), ('pointing', r['pointing']),
+                     ('az', r['az']), ('feedid', r['feedid']), ('obsids', r['obsids'])):
+            i = cc.OUTPUTS.index(k)
+            assert np.array_equal(v[sel], one[i]), (b, k)
+        # dropped offsets carry no weight in that band
+        assert not r['weights'][b][~sel].any()

@@ -78,3 +78,32 @@ def test_run_destriper_main_end_to_end(tmp_path):
     assert np.max(np.abs(got['map'][fin] - ref['map'][fin])) <= 1e-6 * scale
     hdus = read_image_hdus(str(tmp_path / 'All_t_Band00.fits'))
     assert np.array_equal(np.nan_to_num(hdus[0][1].ravel()), np.nan_to_num(got['map']))
+
+
+@pytest.mark.gpu
+def test_run_destriper_main_bands_batched(tmp_path):
+    """main() with the 4 bands batched (read_comap_data_bands + one batched
+    device solve) == the oracle chain run band by band."""
+    import comapdata_case as cc
+    from comapreduce_amd.mapmaking.run_destriper import main
+    from comapreduce_amd.mapmaking.comapdata import map_info_from
+    from oracle import comapdata as oc, destriper as od
+    store, names = cc.store()
+    names = names[:2]
+    m = cc.CASES['car']['map']
+    out = main(names, offset_length=50, prefix='t', output_dir=str(tmp_path), feeds=cc.FEEDS,
+               nxpix=m['nxpix'], nypix=m['nypix'], crval=m['crval'], crpix=m['crpix'], ctype=m['ctype'],
+               cdelt=m['cdelt'], use_gain_filter=True, calibration=False, threshold=1e-6, niter=50,
+               bands=(0, 1, 2, 3), store=store)
+    mi = map_info_from(m['crval'], m['cdelt'], m['crpix'], m['ctype'], m['nxpix'], m['nypix'])
+    npix = m['nxpix'] * m['nypix']
+    for b in range(4):
+        tod, w, pix, *_ = oc.read_comap_data(names, store, mi, iband=b, offset_length=50, feeds=cc.FEEDS)
+        ref, _, _ = od.destriper_iteration(pix, tod, w, 50, npix, threshold=1e-6, niter=50)
+        got = out[b]['All']
+        for k in ('weight', 'hits', 'naive'):
+            assert np.array_equal(np.nan_to_num(got[k]), np.nan_to_num(ref[k])), (b, k)
+        fin = np.isfinite(ref['map']) & (ref['weight'] > 0)
+        scale = np.max(np.abs(ref['map'][fin]))
+        assert np.max(np.abs(got['map'][fin] - ref['map'][fin])) <= 1e-6 * scale, b
+        assert os.path.exists(tmp_path / f'All_t_Band{b:02d}.fits')
