@@ -233,46 +233,70 @@ class DeviceOps:
         N.bind_stream(self.ctx, self.dev)
         N.check(getattr(N.lib(), fn)(*args), self.ctx, fn)
 
+    # ---- operand checks: every device buffer handed to the C ABI must hold what the
+    # kernels index (offset vectors [N/L * nb], maps [npix * nb], nb scalars, ...)
+    def _v(self, t):
+        if t.numel() < self.n_offsets * self.nb or t.dtype != self.torch.float64:
+            raise ValueError(f'offset vector must be float64 with >= {self.n_offsets * self.nb} values')
+        return N.dptr(t)
+
+    def _m(self, t):
+        if t.numel() < self.npix * self.nb or t.dtype != self.torch.float64:
+            raise ValueError(f'map must be float64 with >= {self.npix * self.nb} values')
+        return N.dptr(t)
+
+    def _s(self, t, n=None):
+        n = self.nb if n is None else n
+        if t.numel() < n or t.dtype != self.torch.float64:
+            raise ValueError(f'scalar buffer must be float64 with >= {n} values')
+        return N.dptr(t)
+
+    def _f(self, t):
+        if t.numel() < 2 + 2 * self.nb or t.dtype != self.torch.int32:
+            raise ValueError(f'flags must be int32 with >= {2 + 2 * self.nb} values')
+        return N.dptr(t)
+
     # ---- operator pieces
     def local_maps(self):
-        h, hits, nn = self.zeros(self.npix), self.zeros(self.npix), self.zeros(self.npix)
-        self._c('comap_destripe_local_maps', self.h, N.dptr(h), N.dptr(hits), N.dptr(nn))
+        h, hits, nn = (self.zeros(self.npix * self.nb) for _ in range(3))
+        self._c('comap_destripe_local_maps', self.h, self._m(h), self._m(hits), self._m(nn))
         return h, hits, nn
 
     def bin(self, x, mode, out):
-        self._c('comap_destripe_bin', self.h, N.dptr(x), int(mode), N.dptr(out))
+        self._c('comap_destripe_bin', self.h, self._v(x), int(mode), self._m(out))
 
     def project(self, x, num, h, y, dot=None):
-        self._c('comap_destripe_project', self.h, None if x is None else N.dptr(x), N.dptr(num), N.dptr(h),
-                N.dptr(y), None if dot is None else N.dptr(dot))
+        self._c('comap_destripe_project', self.h, None if x is None else self._v(x), self._m(num), self._m(h),
+                self._v(y), None if dot is None else self._s(dot))
 
     def dot(self, a, b, out):
-        self._c('comap_destripe_dot', self.h, N.dptr(a), N.dptr(b), N.dptr(out))
+        self._c('comap_destripe_dot', self.h, self._v(a), self._v(b), self._s(out))
 
     def cg_update(self, rr, pq, x, r, p, q, rr_new):
-        self._c('comap_destripe_cg_update', self.h, N.dptr(rr), N.dptr(pq), N.dptr(x), N.dptr(r), N.dptr(p),
-                N.dptr(q), N.dptr(rr_new))
+        self._c('comap_destripe_cg_update', self.h, self._s(rr), self._s(pq), self._v(x), self._v(r), self._v(p),
+                self._v(q), self._s(rr_new))
 
     def cg_direction(self, rr_new, rr, p, r):
-        self._c('comap_destripe_cg_direction', self.h, N.dptr(rr_new), N.dptr(rr), N.dptr(p), N.dptr(r))
+        self._c('comap_destripe_cg_direction', self.h, self._s(rr_new), self._s(rr), self._v(p), self._v(r))
 
-    # ---- multi-rank iteration pieces (device stop flag; see cg_solve_batched)
+    # ---- multi-rank iteration pieces (device stop flags; see cg_solve_batched)
     def dist_bin(self, p, num, flags):
-        self._c('comap_destripe_dist_bin', self.h, N.dptr(p), N.dptr(num), N.dptr(flags))
+        self._c('comap_destripe_dist_bin', self.h, self._v(p), self._m(num), self._f(flags))
 
     def dist_project(self, p, num, h, q, scal, flags):
-        self._c('comap_destripe_dist_project', self.h, N.dptr(p), N.dptr(num), N.dptr(h), N.dptr(q), N.dptr(scal),
-                N.dptr(flags))
+        self._c('comap_destripe_dist_project', self.h, self._v(p), self._m(num), self._m(h), self._v(q),
+                self._s(scal, 4 * self.nb + 1), self._f(flags))
 
     def dist_update(self, scal, x, r, p, q, flags):
-        self._c('comap_destripe_dist_update', self.h, N.dptr(scal), N.dptr(x), N.dptr(r), N.dptr(p), N.dptr(q),
-                N.dptr(flags))
+        self._c('comap_destripe_dist_update', self.h, self._s(scal, 4 * self.nb + 1), self._v(x), self._v(r),
+                self._v(p), self._v(q), self._f(flags))
 
     def dist_direction(self, scal, p, r, flags):
-        self._c('comap_destripe_dist_direction', self.h, N.dptr(scal), N.dptr(p), N.dptr(r), N.dptr(flags))
+        self._c('comap_destripe_dist_direction', self.h, self._s(scal, 4 * self.nb + 1), self._v(p), self._v(r),
+                self._f(flags))
 
     def div_map(self, num, h, out):
-        self._c('comap_destripe_div_map', self.h, N.dptr(num), N.dptr(h), N.dptr(out))
+        self._c('comap_destripe_div_map', self.h, self._m(num), self._m(h), self._m(out))
 
     # ---- single-rank native solve (no Python per iteration)
     def solve_native(self, threshold, niter):
