@@ -48,9 +48,14 @@ struct DeviceGuard {
 #define COMAP_DEVICE_GUARD(ctx) DeviceGuard _comap_dg((ctx)->device)
 
 // Device buffers owned by one call: freed on every return path (error returns
-// included) unless released to a longer-lived owner.
+// included).  With a stream, the destructor first waits for the work queued on
+// it (kernels may still read the buffers).
 struct DevTemps {
     std::vector<void *> p;
+    hipStream_t st = nullptr;
+    explicit DevTemps(hipStream_t s = nullptr) : st(s) {}
+    DevTemps(const DevTemps &) = delete;
+    DevTemps &operator=(const DevTemps &) = delete;
     template <typename T>
     hipError_t alloc(T **out, size_t n)
     {
@@ -62,6 +67,7 @@ struct DevTemps {
     }
     ~DevTemps()
     {
+        if (!p.empty() && st) (void)hipStreamSynchronize(st);
         for (void *q : p) (void)hipFree(q);
     }
 };
@@ -180,7 +186,10 @@ struct comap_l1_plan {
     // NaN / calibrator paths
     int32_t *rowbad = nullptr;         // [U*4096] non-finite samples per row (pass A)
     int32_t nan_total = 0;             // total from the last pass A
-    bool filled = false;               // fill_bad_data applied to the device cube
+    bool filled = false;               // fill_bad_data applied to the device cube (until restore_nan)
+    int64_t *nanpos = nullptr;         // [nanpos_cap] cube element offsets the fill overwrote
+    int64_t nanpos_cap = 0;
+    int64_t *nanpos_n = nullptr;       // [1] entries used
     double *ubs = nullptr;             // [U*4][4] fit normal-equation sums n, SA, SAA per (unit, band)
     double *fitsum = nullptr;          // [2][U*4096] masked Sd, SAd (select_time path)
     double *oa = nullptr;              // [U*4096][2] offset/slope L1AGC subtracts

@@ -440,17 +440,36 @@ __global__ void k_ub_from_units(const double *__restrict__ us, int U, double *__
     ub[4 * (int64_t)i + 2] = q[2];
 }
 
-// fill_bad_data (Level1Averaging.py:658-665): NaN -> the row's nanmedian (f32), in place
+// fill_bad_data (Level1Averaging.py:658-665): NaN -> the row's nanmedian (f32).  The
+// reference fills its per-feed copy (DataHandling.py:176-177 hands every stage a fresh
+// h5py read); here the resident cube is filled for the duration of comap_l1_average
+// and every overwritten position is recorded, so k_restore_nan puts the NaNs back.
 __global__ void __launch_bounds__(256) k_fill_rows(float *__restrict__ tod, const int64_t *__restrict__ rows,
-                                                   const float *__restrict__ med, int nrows)
+                                                   const float *__restrict__ med, int nrows, int64_t *__restrict__ pos,
+                                                   int64_t cap, int64_t *__restrict__ npos)
 {
     const int r = blockIdx.y;
     if (r >= nrows) return;
-    float *p = tod + rows[2 * r];
+    const int64_t off = rows[2 * r];
+    float *p = tod + off;
     const int64_t n = rows[2 * r + 1];
     const float m = med[r];
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        if (isnan(p[i])) p[i] = m;
+        if (isnan(p[i])) {
+            const unsigned long long k = atomicAdd(reinterpret_cast<unsigned long long *>(npos), 1ull);
+            if ((int64_t)k < cap) {   // cap = the non-finite count of pass A >= NaN count
+                pos[k] = off + i;
+                p[i] = m;
+            }
+        }
+}
+
+__global__ void k_restore_nan(float *__restrict__ tod, const int64_t *__restrict__ pos, const int64_t *__restrict__ npos,
+                              int64_t cap)
+{
+    const int64_t n = min(*npos, cap);
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        tod[pos[i]] = __int_as_float(0x7fc00000);
 }
 
 // constant-elevation scans (Level1Averaging.py:242-244): fit = (nanmedian, 0) for every channel
@@ -965,7 +984,14 @@ __global__ void __launch_bounds__(256) k_coef_d(const int32_t *__restrict__ unit
     // gain path (Level1Averaging.py:710-725, 834-838):
     //   zero: y zeroed on the gain mask (gain function was called)
     //   use_dg: dG enters the residual
-    const bool gain_called = !calibrator;
+    // gain_subtraction first runs fit_power_spectrum's gate (:552-589) on the band-0
+    // channel mean: np.fft of n <= 4 samples leaves no finite PSD bin (ValueError /
+    // IndexError), so dG = None and the gain function (and its in-place zeroing) never
+    // runs.  For n >= 5 and finite samples the gate passes (every band-0 channel outside
+    // the median set is 0, so the channel nanmean is finite); +-inf samples are outside
+    // parity.
+    const bool gate = n >= 5.0;
+    const bool gain_called = !calibrator && gate;
     const bool zero = gain_called;
     const bool use_dg = gain_called && gm == 0;
     const double det = n * Smm - Smf * Smf;
@@ -1499,7 +1525,7 @@ extern "C" int comap_l1_plan_destroy(comap_l1_plan *p)
     void *bufs[] = {p->units, p->tiles, p->tiles_b, p->airmass, p->unit_sums, p->mom,
                     p->nan_count, p->alpha, p->nf, p->bsum, p->mb, p->mf, p->ssum, p->sdm, p->gw,
                     p->gmode, p->kap, p->dsum, p->xreg, p->dG, p->rowbad, p->ubs, p->fitsum, p->oa,
-                    p->flag, p->dlist, p->dcnt, p->dw};
+                    p->flag, p->dlist, p->dcnt, p->dw, p->nanpos, p->nanpos_n};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (int g = 0; g < comap_l1_plan::kMaxGroups; ++g) {
@@ -1617,9 +1643,10 @@ extern "C" int comap_l1_atmosphere(comap_l1_plan *p, const int32_t *const_el_uni
             int32_t *dpairs = nullptr;
             int64_t *dvoff = nullptr;
             uint8_t *valid = nullptr;
-            COMAP_CHECK(ctx, hipMalloc((void **)&dpairs, 4 * pairs.size()));
-            COMAP_CHECK(ctx, hipMalloc((void **)&dvoff, 8 * voff.size()));
-            COMAP_CHECK(ctx, hipMalloc((void **)&valid, voff.back() + 1));
+            DevTemps tmp(st);
+            COMAP_CHECK(ctx, tmp.alloc(&dpairs, pairs.size()));
+            COMAP_CHECK(ctx, tmp.alloc(&dvoff, voff.size()));
+            COMAP_CHECK(ctx, tmp.alloc(&valid, voff.back() + 1));
             COMAP_CHECK(ctx, hipMemcpyAsync(dpairs, pairs.data(), 4 * pairs.size(), hipMemcpyHostToDevice, st));
             COMAP_CHECK(ctx, hipMemcpyAsync(dvoff, voff.data(), 8 * voff.size(), hipMemcpyHostToDevice, st));
             COMAP_CHECK(ctx, hipMemcpyAsync(p->fitsum, p->mom, 16 * UC, hipMemcpyDeviceToDevice, st));
@@ -1630,8 +1657,6 @@ extern "C" int comap_l1_atmosphere(comap_l1_plan *p, const int32_t *const_el_uni
             k_masked_fit_sums<<<dim3(kChannels / 4, np), 256, 0, st>>>(p->tod, p->airmass, p->units, dpairs, p->T,
                                                                        dvoff, valid, UC, p->fitsum, p->ubs);
             COMAP_LAUNCH_CHECK(ctx);
-            COMAP_CHECK(ctx, hipStreamSynchronize(st));
-            (void)hipFree(dpairs); (void)hipFree(dvoff); (void)hipFree(valid);
             fs = p->fitsum;
         }
     }
@@ -1647,15 +1672,14 @@ extern "C" int comap_l1_atmosphere(comap_l1_plan *p, const int32_t *const_el_uni
         }
         float *med = nullptr;
         int32_t *dl = nullptr;
-        COMAP_CHECK(ctx, hipMalloc((void **)&med, 4 * ids.size()));
-        COMAP_CHECK(ctx, hipMalloc((void **)&dl, 4 * (size_t)n_const_el));
+        DevTemps tmp(st);
+        COMAP_CHECK(ctx, tmp.alloc(&med, ids.size()));
+        COMAP_CHECK(ctx, tmp.alloc(&dl, (size_t)n_const_el));
         COMAP_CHECK(ctx, hipMemcpyAsync(dl, const_el_units, 4 * (size_t)n_const_el, hipMemcpyHostToDevice, st));
         if ((rc = unit_row_medians(p, ids, med))) return rc;
         const int64_t nt = (int64_t)n_const_el * kBC;
         k_fit_from_median<<<(nt + 255) / 256, 256, 0, st>>>(p->units, dl, n_const_el, med, p->F, fit);
         COMAP_LAUNCH_CHECK(ctx);
-        COMAP_CHECK(ctx, hipStreamSynchronize(st));
-        (void)hipFree(med); (void)hipFree(dl);
     }
     return 0;
 }
@@ -1681,19 +1705,43 @@ static int fill_nan_rows(comap_l1_plan *p)
         rows[2 * k] = ((int64_t)q[0] * kBC + bc) * p->T + q[2];
         rows[2 * k + 1] = q[3];
     }
-    COMAP_CHECK(ctx, hipMalloc((void **)&med, 4 * ids.size()));
-    COMAP_CHECK(ctx, hipMalloc((void **)&drows, 8 * rows.size()));
+    DevTemps tmp(st);
+    COMAP_CHECK(ctx, tmp.alloc(&med, ids.size()));
+    COMAP_CHECK(ctx, tmp.alloc(&drows, rows.size()));
+    // positions the fill overwrites (restored by restore_nan): at most pass A's non-finite count
+    const int64_t cap = std::max<int64_t>(p->nan_total, 1);
+    if (cap > p->nanpos_cap) {
+        if (p->nanpos) (void)hipFree(p->nanpos);
+        p->nanpos = nullptr;
+        p->nanpos_cap = 0;
+        COMAP_CHECK(ctx, hipMalloc((void **)&p->nanpos, 8 * (size_t)cap));
+        p->nanpos_cap = cap;
+    }
+    if (!p->nanpos_n) COMAP_CHECK(ctx, hipMalloc((void **)&p->nanpos_n, 8));
+    COMAP_CHECK(ctx, hipMemsetAsync(p->nanpos_n, 0, 8, st));
     COMAP_CHECK(ctx, hipMemcpyAsync(drows, rows.data(), 8 * rows.size(), hipMemcpyHostToDevice, st));
     if ((rc = comap_row_nanmedian(ctx, p->tod, rows.data(), (int32_t)ids.size(), med))) return rc;
+    p->filled = true;   // from here on the cube must be restored (restore_nan), even after an error
     for (size_t r0 = 0; r0 < ids.size(); r0 += 65535) {
         const int nr = (int)std::min<size_t>(65535, ids.size() - r0);
-        k_fill_rows<<<dim3(16, nr), 256, 0, st>>>(const_cast<float *>(p->tod), drows + 2 * r0, med + r0, nr);
+        k_fill_rows<<<dim3(16, nr), 256, 0, st>>>(const_cast<float *>(p->tod), drows + 2 * r0, med + r0, nr,
+                                                  p->nanpos, p->nanpos_cap, p->nanpos_n);
         COMAP_LAUNCH_CHECK(ctx);
     }
-    COMAP_CHECK(ctx, hipStreamSynchronize(st));
-    (void)hipFree(med); (void)hipFree(drows);
-    p->filled = true;
     return run_moments(p);
+}
+
+// Puts back the NaNs fill_nan_rows overwrote (stream-ordered after the reduction), so
+// every later stage sees the raw cube again; the next pass A re-reads it.
+static int restore_nan(comap_l1_plan *p)
+{
+    if (!p->filled) return 0;
+    comap_ctx *ctx = p->ctx;
+    k_restore_nan<<<256, 256, 0, ctx->stream>>>(const_cast<float *>(p->tod), p->nanpos, p->nanpos_n, p->nanpos_cap);
+    p->filled = false;
+    p->moments_valid = false;
+    COMAP_LAUNCH_CHECK(ctx);
+    return 0;
 }
 
 extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const double *tsys0, const double *gain0,
@@ -1705,16 +1753,22 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
     int rc = 0;
     if (!p->moments_valid && (rc = run_moments(p))) return rc;
     if ((rc = wait_moments(p))) return rc;
+    // the NaN fill is undone (restore_nan) on every return from here on
+    struct Restore {
+        comap_l1_plan *p;
+        ~Restore() { (void)restore_nan(p); }
+    } restore{p};
     if (p->nan_total > 0 && !p->filled && (rc = fill_nan_rows(p))) return rc;
     const int64_t UC = (int64_t)p->U * kBC;
     const int UB = p->U * kBands;
     hipStream_t st = ctx->stream;
+    DevTemps tmp(st);
     // offsets/slopes to subtract: the scan fits, or per-channel nanmedians for calibrators
     float *cmed = nullptr;
     if (calibrator) {
         std::vector<int64_t> ids(UC);
         for (int64_t i = 0; i < UC; ++i) ids[i] = i;
-        COMAP_CHECK(ctx, hipMalloc((void **)&cmed, 4 * (size_t)UC));
+        COMAP_CHECK(ctx, tmp.alloc(&cmed, (size_t)UC));
         if ((rc = unit_row_medians(p, ids, cmed))) return rc;
     }
     k_gather_oa<<<(UC + 255) / 256, 256, 0, st>>>(p->units, fit, p->F, p->U, cmed, p->oa);
@@ -1777,10 +1831,6 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
     COMAP_LAUNCH_CHECK(ctx);
     PROF(p, KV_SCAN_WEIGHTS, k_scan_weights<<<UB, 256, 0, st>>>(p->units, p->T, tod_out, w_out));
     COMAP_LAUNCH_CHECK(ctx);
-    if (cmed) {
-        COMAP_CHECK(ctx, hipStreamSynchronize(st));
-        (void)hipFree(cmed);
-    }
     return 0;
 }
 

@@ -220,7 +220,10 @@ def run_l1_variant(name, figdir):
     for k in ('vane/system_temperature', 'vane/system_gain', 'atmosphere/fit_values',
               'averaged_tod/tod', 'averaged_tod/tod_original', 'averaged_tod/weights',
               'averaged_tod/scan_edges'):
-        out[k.replace('/', '__')] = np.asarray(level2[k])
+        v = np.asarray(level2[k])
+        if name == 'f3' and k in ('averaged_tod/tod', 'averaged_tod/tod_original', 'averaged_tod/weights'):
+            v = v[..., ::variants.F3_STRIDE]
+        out[k.replace('/', '__')] = v
     np.savez_compressed(os.path.join(HERE, f'golden_l1_{name}.npz'), **out)
     return {k: synthetic.sha256(v) for k, v in gen['data'].items()}
 
@@ -424,6 +427,31 @@ def run_destriper(out, meta):
                                     seed=7, sha256=[synthetic.sha256(a) for a in (pointing, tod, weights)])
 
 
+def run_destriper_timing(meta):
+    """The reference's CG at C4 size (19 feeds x 180,000 samples, L = 50,
+    480 x 480 map) timed here for the bench line's CPU baseline: destriper_iteration with
+    niter = 4 and niter = 1 (threshold 0), the difference / 3 = seconds per CG iteration
+    (3 op_Ax calls each, as shipped)."""
+    import Destriper
+    L = 50
+    pointing, tod, weights = synthetic.destriper_inputs(n_feeds=19, n_samples=180_000, npix_side=480)
+    pixel_edges = np.arange(480 * 480)
+    z = np.zeros(tod.size)
+    feedid = np.repeat(np.arange(1, 20), tod.size // 19)
+    obsids = np.ones(tod.size, dtype=int)
+    secs = {}
+    for niter in (1, 4):
+        t0 = time.perf_counter()
+        Destriper.destriper_iteration(pointing, z, tod, weights, L, pixel_edges, feedid, obsids, threshold=0.0,
+                                      niter=niter)
+        secs[niter] = time.perf_counter() - t0
+    per = (secs[4] - secs[1]) / 3
+    meta['reference_destriper_c4'] = {'n_samples': int(tod.size), 'n_offsets': int(tod.size // L),
+                                      'iters': 3, 'seconds': secs[4] - secs[1], 'iters_per_s': 1.0 / per,
+                                      'inputs': 'synthetic.destriper_inputs(n_feeds=19, n_samples=180000, '
+                                                'npix_side=480)', 'host': '8-core Xeon build container, 1 process'}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--skip-l1', action='store_true')
@@ -431,7 +459,24 @@ def main():
     ap.add_argument('--only-comapdata', action='store_true')
     ap.add_argument('--only-binning', action='store_true')
     ap.add_argument('--only-noise', action='store_true')
+    ap.add_argument('--only-variants-new', action='store_true', help='tinyscan + f3 variants only')
+    ap.add_argument('--only-timing', action='store_true', help='reference destriper C4 timing only')
     args = ap.parse_args()
+    if args.only_variants_new or args.only_timing:
+        os.environ.setdefault('MPLBACKEND', 'agg')
+        build_reference_helpers()
+        install_stubs()
+        mp = os.path.join(HERE, 'golden_meta.json')
+        meta = json.load(open(mp))
+        if args.only_variants_new:
+            figdir = os.path.join(SCRATCH, 'figures')
+            os.makedirs(figdir, exist_ok=True)
+            for name in ('tinyscan', 'f3'):
+                meta[f'l1_{name}_sha256'] = run_l1_variant(name, figdir)
+        if args.only_timing:
+            run_destriper_timing(meta)
+        json.dump(meta, open(mp, 'w'), indent=1, default=str)
+        return
     if args.only_noise:
         os.environ.setdefault('MPLBACKEND', 'agg')
         build_reference_helpers()

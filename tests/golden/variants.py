@@ -9,6 +9,12 @@ Each variant is the synthetic generator's output with a deterministic edit:
            nanmedian atmosphere, Level1Averaging.py:242-244)
   calib    source 'TauA' (calibrator scan edges DataHandling.py:231-245,
            median atmosphere + no gain subtraction, Level1Averaging.py:647-648, 719-724)
+  tinyscan two extra Lissajous runs of 2 and 3 samples right after the first scan, so
+           scans 1 and 2 are 3 and 4 samples long: fit_power_spectrum raises
+           (ValueError / IndexError, Level1Averaging.py:552-589) and dG = None
+           (:834-838); the atmosphere fit has < 100 samples (NaN fit)
+  f3       3 feeds numbered 1, 2, 20, T = 30,000 (two full scans): multi-feed unit
+           tables, per-feed gain weights, and the feeds > 19 skip (:817-818)
 """
 import numpy as np
 
@@ -18,10 +24,13 @@ T_EDGE = 16_000
 
 
 def make(name):
+    if name == 'f3':
+        return synthetic.generate_level1(synthetic.SyntheticConfig(**F3_CONFIG))
     if name == 'calib':
         cfg = synthetic.SyntheticConfig(n_feeds=1, n_samples=T_EDGE, obs_id=11, source='TauA')
     else:
-        cfg = synthetic.SyntheticConfig(n_feeds=1, n_samples=T_EDGE, obs_id={'nan': 12, 'constel': 13}[name])
+        cfg = synthetic.SyntheticConfig(n_feeds=1, n_samples=T_EDGE,
+                                        obs_id={'nan': 12, 'constel': 13, 'tinyscan': 14}[name])
     gen = synthetic.generate_level1(cfg)
     d = gen['data']
     if name == 'nan':
@@ -34,10 +43,17 @@ def make(name):
     elif name == 'constel':
         f = d['spectrometer/features']
         f[synthetic.SCAN_START:] = 2.0 ** 9
+    elif name == 'tinyscan':
+        st = d['hk/antenna0/deTracker/lissajous_status']
+        e0 = synthetic.SCAN_START + synthetic.SCAN_LEN       # first run is [1500, 15500)
+        st[e0 + 1:e0 + 3] = 1                                # run of 2 -> scan of 3 samples
+        st[e0 + 4:e0 + 7] = 1                                # run of 3 -> scan of 4 samples
     return gen
 
 
-NAMES = ('nan', 'constel', 'calib')
+F3_CONFIG = dict(n_feeds=3, n_samples=30_000, obs_id=5, feed_numbers=(1, 2, 20))
+F3_STRIDE = 7          # the f3 golden keeps averaged_tod/* at every 7th sample (fixture size)
+NAMES = ('nan', 'constel', 'calib', 'tinyscan', 'f3')
 
 
 def spikes_level2(golden_dir):

@@ -129,7 +129,7 @@ def test_l1_median_selection_bit_exact(c1_run):
             assert np.array_equal(mf[f, b, t0:t0 + n], ref), (f, s, b)
 
 
-@pytest.mark.parametrize('name', ['nan', 'constel', 'calib'])
+@pytest.mark.parametrize('name', ['nan', 'constel', 'calib', 'tinyscan', 'f3'])
 def test_l1_edge_variants_vs_reference(golden_dir, name):
     """NaN fill/select_time, constant-elevation and calibrator paths on the device."""
     import sys
@@ -148,7 +148,10 @@ def test_l1_edge_variants_vs_reference(golden_dir, name):
     for k in ('vane/system_temperature', 'vane/system_gain'):
         assert np.array_equal(level2[k], g[k.replace('/', '__')]), (name, k)
     for k in ('atmosphere/fit_values', 'averaged_tod/tod', 'averaged_tod/tod_original', 'averaged_tod/weights'):
-        assert relmax(level2[k], g[k.replace('/', '__')]) < RTOL, (name, k)
+        v = np.asarray(level2[k])
+        if name == 'f3' and k.startswith('averaged_tod'):
+            v = v[..., ::variants.F3_STRIDE]
+        assert relmax(v, g[k.replace('/', '__')]) < RTOL, (name, k)
 
 
 def test_spikes_stage_bit_exact(golden_dir):
@@ -263,3 +266,30 @@ def test_context_keeps_current_device():
         assert torch.cuda.current_device() == before
     medfilt_batch([np.arange(1000.0)], 401, reflect=True)
     assert torch.cuda.current_device() == before
+
+
+def test_nan_fill_leaves_raw_cube(golden_dir):
+    """fill_bad_data is applied for the L1AGC reduction only: afterwards the resident
+    cube holds its NaNs again, so a later stage (Level1Averaging, a re-run of
+    L1AGC) sees the raw data, as every reference stage does (DataHandling.py:176-177)."""
+    import sys
+    import oracle.l1 as ol1
+    sys.path.insert(0, golden_dir)
+    import variants
+    from comapreduce_amd import Analysis as A
+    gen = variants.make('nan')
+    raw = gen['data']['spectrometer/tod'].copy()
+    data = level1_from_dict(gen)
+    l2 = _reduce(data)
+    dev = data._gpu_observation.tod.cpu().numpy()
+    assert np.array_equal(np.isnan(dev), np.isnan(raw))
+    assert np.array_equal(dev, raw, equal_nan=True)
+    st = A.Level1Averaging(level2=l2)
+    assert st(data, l2)
+    ref_a, ref_s = ol1.level1_averaging(raw, np.asarray(l2['vane/system_temperature'])[0],
+                                        np.asarray(l2['vane/system_gain'])[0], 512)
+    assert relmax(st.tod, ref_a) < 1e-12
+    # a second L1AGC on the same plan gives the same outputs as the first
+    again = A.Level1AveragingGainCorrection(level2=l2)
+    assert again(data, l2)
+    assert np.array_equal(again.tod_cleaned, np.asarray(l2['averaged_tod/tod']), equal_nan=True)
