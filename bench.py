@@ -64,6 +64,7 @@ def parse():
     ap.add_argument('--destriper-iters', type=int, default=100)
     ap.add_argument('--c5-obs', type=int, default=8, help='observations per GPU in the C5 destriper leg (0: skip)')
     ap.add_argument('--check', action='store_true', help='compare one unit against the CPU oracle')
+    ap.add_argument('--no-e2e', action='store_true', help='skip the host-cube -> host-Level-2 leg')
     return ap.parse_args()
 
 
@@ -133,15 +134,16 @@ def build_observation(F, T, obs_id, device, rank=0, world=1):
     return part, sh
 
 
-def reduce_step(data, device, timing=None):
-    """One full L1 -> L2 reduction (outputs stay on the device).  ``timing``
-    (a dict) collects host wall time per stage call (enqueue + host work)."""
+def reduce_step(data, device, timing=None, device_outputs=True):
+    """One full L1 -> L2 reduction (outputs stay on the device unless
+    device_outputs=False, the Runner's host arrays).  ``timing`` (a dict) collects
+    host wall time per stage call (enqueue + host work)."""
     from comapreduce_amd import Analysis as A
     from comapreduce_amd.pipeline.datahandling import COMAPLevel2
     level2 = COMAPLevel2(filename='/nonexistent/level2.hd5')
     for cls in (A.MeasureSystemTemperature, A.AtmosphereRemoval, A.Level1AveragingGainCorrection):
         t0 = time.perf_counter()
-        st = cls(level2=level2, device=device, device_outputs=True)
+        st = cls(level2=level2, device=device, device_outputs=device_outputs)
         if not st(data, level2):
             raise RuntimeError(f'{cls.__name__} stopped the file')
         level2.update(st)
@@ -352,6 +354,41 @@ def destriper_c5_leg(n_obs, niter, device, world, rank, n_bands=1):
             'roofline_frac': algo / (ms_band * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
+def e2e_leg(F, T, device):
+    """C2 from host memory, the Runner path (Running.py:120-153): the Level-1 cube is
+    a pageable host NumPy array (as read from a file), the stages upload it
+    (gpu.upload: pinned double-buffered chunks on a copy stream), reduce, and hand
+    back host Level-2 arrays.  Timed: upload + the three stages + outputs to host."""
+    import torch
+    from comapreduce_amd.gpu import gpu_observation
+    from comapreduce_amd.pipeline.datahandling import COMAPLevel1
+    dev_data, _ = build_observation(F, T, obs_id=1, device=device)
+    host = COMAPLevel1(overwrite=False, large_datasets=['spectrometer/tod'])
+    for k, v in dev_data.items():
+        host[k] = v.cpu().numpy() if hasattr(v, 'cpu') else v
+    for p, a in dev_data.items(attr=True):
+        for k, v in a.items():
+            host.set_attrs(p, k, v)
+    del dev_data
+    torch.cuda.empty_cache()
+    nbytes = host['spectrometer/tod'].nbytes
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    gpu_observation(host, device)                  # upload (what the first stage does)
+    torch.cuda.synchronize()
+    t_up = time.perf_counter() - t0
+    level2 = reduce_step(host, device, device_outputs=False)
+    torch.cuda.synchronize()
+    t_all = time.perf_counter() - t0
+    assert isinstance(level2['averaged_tod/tod'], np.ndarray)
+    sampch = F * 4 * 1024 * T
+    del host, level2
+    torch.cuda.empty_cache()
+    return {'config': f'C2 from a host (pageable) cube: upload + 3 stages + host Level-2 outputs, {F} feeds',
+            'value': sampch / t_all, 'unit': 'samples*channels/s', 'seconds': t_all, 'upload_s': t_up,
+            'upload_GBs': nbytes / t_up / 1e9, 'reduce_and_outputs_s': t_all - t_up}
+
+
 # ---------------------------------------------------------------- main
 def main():
     args = parse()
@@ -427,6 +464,10 @@ def main():
         torch.cuda.empty_cache()
         c5['bands4'] = destriper_c5_leg(args.c5_obs, args.destriper_iters, device, world, rank, n_bands=4)
 
+    e2e = None
+    if not args.no_e2e and world == 1:
+        e2e = e2e_leg(F, T, device)
+
     if rank == 0:
         value = job_sampch * args.steps / elapsed
         scan_sc = sh.samples_x_channels()
@@ -489,6 +530,8 @@ def main():
             line['destriper'] = dstr
         if c5 is not None:
             line['destriper_c5'] = c5
+        if e2e is not None:
+            line['end_to_end_host'] = e2e
         if check is not None:
             line['check'] = check
         if not args.no_cpu_baseline and world == 1:

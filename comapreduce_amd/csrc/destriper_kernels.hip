@@ -78,7 +78,9 @@ struct comap_destriper {
 
 namespace {
 
-constexpr int kRedBlocks = 256;
+constexpr int kRedBlocks = 256;   // dot-product grids (k_dot_part)
+constexpr int kUpdBlocks = 512;   // CG update grid: its r.r partials are re-summed by every direction block
+constexpr int kDirBlocks = 1024;  // CG direction grid cap
 constexpr int kPartMax = 8192;     // >= every reduction grid below
 constexpr int kBinU = 4;           // entry loads in flight per lane (k_ds_bin)
 constexpr int kProjU = 4;          // entry loads in flight per lane (k_ds_project)
@@ -124,6 +126,16 @@ __device__ __forceinline__ void stb(double *__restrict__ p, const double (&v)[NB
 #pragma unroll
         for (int b = 0; b < NB; ++b) p[b] = v[b];
     }
+}
+
+// XCD-aware block order (bijective for any grid): blocks b and b + 8 share an XCD
+// (MI355X_MICROARCH.md, workgroup dispatch), so logical block ids are dealt to the 8
+// groups in contiguous runs -- each XCD's L2 then serves a contiguous range of map rows
+// (k_ds_bin) or of offsets (k_ds_project), whose x / map gathers overlap.
+__device__ __forceinline__ int64_t xcd_block(int64_t bid, int64_t nwg)
+{
+    const int64_t q = nwg / 8, r = nwg % 8, x = bid % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
 }
 
 __device__ __forceinline__ double wave_sum(double v)
@@ -366,8 +378,9 @@ __global__ void __launch_bounds__(256) k_ds_bin(const int64_t *__restrict__ prow
     if (cg_done(flags)) return;
     const int sub = threadIdx.x & (kBinLanes - 1);
     const int64_t step = (int64_t)gridDim.x * blockDim.x / kBinLanes;
+    const int64_t lb = xcd_block(blockIdx.x, gridDim.x);
     // rows != NULL: only the listed (non-empty) rows, npix = their count
-    for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kBinLanes; i < npix; i += step) {
+    for (int64_t i = (lb * blockDim.x + threadIdx.x) / kBinLanes; i < npix; i += step) {
         const int64_t p = rows ? (int64_t)rows[i] : i;
         double s[NB];
 #pragma unroll
@@ -432,7 +445,10 @@ __global__ void __launch_bounds__(256) k_ds_project(const int64_t *__restrict__ 
     double acc[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) acc[b] = 0.0;
-    for (int64_t o0 = (int64_t)blockIdx.x * kPer; o0 < NO; o0 += (int64_t)gridDim.x * kPer) {
+    // each logical block takes a contiguous run of offset sweeps (time-contiguous samples)
+    const int64_t sweeps = (NO + kPer - 1) / kPer, per = (sweeps + gridDim.x - 1) / gridDim.x;
+    const int64_t s0 = xcd_block(blockIdx.x, gridDim.x) * per, s1 = min(s0 + per, sweeps);
+    for (int64_t o0 = s0 * kPer; o0 < s1 * kPer; o0 += kPer) {
         const int64_t o = o0 + threadIdx.x / G;
         const bool valid = o < NO;
         const int64_t e1 = valid ? orow[o + 1] : 0;
@@ -507,8 +523,11 @@ __global__ void __launch_bounds__(256) k_dot_part(const double *__restrict__ a, 
 #pragma unroll
     for (int b = 0; b < NB; ++b) acc[b] = 0.0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        double av[NB], cv[NB];
+        ldb<NB>(a + i * NB, av);
+        ldb<NB>(c + i * NB, cv);
 #pragma unroll
-        for (int b = 0; b < NB; ++b) acc[b] = fma(a[i * NB + b], c[i * NB + b], acc[b]);
+        for (int b = 0; b < NB; ++b) acc[b] = fma(av[b], cv[b], acc[b]);
     }
 #pragma unroll
     for (int b = 0; b < NB; ++b) block_partial(acc[b], red, part + (int64_t)b * kPartMax + blockIdx.x);
@@ -528,6 +547,43 @@ __global__ void __launch_bounds__(256) k_dot_final(const double *__restrict__ pa
     }
 }
 
+// one offset's x += a p ; r -= a q for the live bands, accumulating r.r (16-B vector access)
+template <int NB>
+__device__ __forceinline__ void update_row(double *__restrict__ x, double *__restrict__ r, const double *__restrict__ p,
+                                           const double *__restrict__ q, const double (&a)[NB], const bool (&live)[NB],
+                                           double (&acc)[NB])
+{
+    double xv[NB], rv[NB], pv[NB], qv[NB];
+    ldb<NB>(r, rv);
+    ldb<NB>(p, pv);
+    ldb<NB>(q, qv);
+    ldb<NB>(x, xv);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        if (live[b]) {
+            xv[b] += a[b] * pv[b];
+            rv[b] = rv[b] - a[b] * qv[b];
+        }
+        acc[b] = fma(rv[b], rv[b], acc[b]);
+    }
+    stb<NB>(x, xv);
+    stb<NB>(r, rv);
+}
+
+// p = r + beta p for the live bands of one offset
+template <int NB>
+__device__ __forceinline__ void direction_row(double *__restrict__ p, const double *__restrict__ r,
+                                              const double (&beta)[NB], const bool (&live)[NB])
+{
+    double pv[NB], rv[NB];
+    ldb<NB>(p, pv);
+    ldb<NB>(r, rv);
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+        if (live[b]) pv[b] = rv[b] + beta[b] * pv[b];
+    stb<NB>(p, pv);
+}
+
 // x += a p ; r -= a q ; a = rr / pq per band (bands already stopped are left alone);
 // per-band partials of r.r
 template <int NB>
@@ -542,19 +598,8 @@ __global__ void __launch_bounds__(256) k_cg_update(const double *__restrict__ rr
     bool live[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) { a[b] = rr[b] / pq[b]; live[b] = !band_stopped(flags, b); acc[b] = 0.0; }
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            const int64_t k = i * NB + b;
-            double ri = r[k];
-            if (live[b]) {
-                x[k] += a[b] * p[k];
-                ri = ri - a[b] * q[k];
-                r[k] = ri;
-            }
-            acc[b] = fma(ri, ri, acc[b]);
-        }
-    }
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        update_row<NB>(x + i * NB, r + i * NB, p + i * NB, q + i * NB, a, live, acc);
 #pragma unroll
     for (int b = 0; b < NB; ++b) block_partial(acc[b], red, part + (int64_t)b * kPartMax + blockIdx.x);
 }
@@ -610,19 +655,8 @@ __global__ void __launch_bounds__(256) k_cg_update_fused(double *__restrict__ sc
         live[b] = !band_stopped(flags, b);
         acc[b] = 0.0;
     }
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            const int64_t k = i * NB + b;
-            double ri = r[k];
-            if (live[b]) {
-                x[k] += a[b] * p[k];
-                ri = ri - a[b] * q[k];
-                r[k] = ri;
-            }
-            acc[b] = fma(ri, ri, acc[b]);
-        }
-    }
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        update_row<NB>(x + i * NB, r + i * NB, p + i * NB, q + i * NB, a, live, acc);
 #pragma unroll
     for (int b = 0; b < NB; ++b) block_partial(acc[b], red, part_rr + (int64_t)b * kPartMax + blockIdx.x);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -647,11 +681,8 @@ __global__ void __launch_bounds__(256) k_cg_direction_fused(double *__restrict__
         beta[b] = rrn[b] / scal[NB + b];
         live[b] = !flags[2 + b];
     }
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-#pragma unroll
-        for (int b = 0; b < NB; ++b)
-            if (live[b]) p[i * NB + b] = r[i * NB + b] + beta[b] * p[i * NB + b];
-    }
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        direction_row<NB>(p + i * NB, r + i * NB, beta, live);
     // block 0 only, after its own sweep: a band that stops here never reads p again
     if (blockIdx.x == 0 && threadIdx.x == 0) cg_check<NB>(scal, flags, rrn);
 }
@@ -666,11 +697,8 @@ __global__ void k_cg_direction(const double *__restrict__ rr_new, const double *
     bool live[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) { beta[b] = rr_new[b] / rr[b]; live[b] = !band_stopped(flags, b); }
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-#pragma unroll
-        for (int b = 0; b < NB; ++b)
-            if (live[b]) p[i * NB + b] = r[i * NB + b] + beta[b] * p[i * NB + b];
-    }
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        direction_row<NB>(p + i * NB, r + i * NB, beta, live);
 }
 
 template <int NB>
@@ -980,9 +1008,9 @@ extern "C" int comap_destripe_cg_update(comap_destriper *d, const double *rr, co
     if (!d) return -1;
     COMAP_DEVICE_GUARD(d->ctx);
     comap_ctx *ctx = d->ctx;
-    COMAP_NB_SWITCH(d->nb, k_cg_update<NB><<<kRedBlocks, 256, 0, ctx->stream>>>(rr, pq, x, r, p, q, d->NO, d->part,
+    COMAP_NB_SWITCH(d->nb, k_cg_update<NB><<<kUpdBlocks, 256, 0, ctx->stream>>>(rr, pq, x, r, p, q, d->NO, d->part,
                                                                                  nullptr);
-                    k_dot_final<NB><<<1, 256, 0, ctx->stream>>>(d->part, kRedBlocks, rr_new, nullptr));
+                    k_dot_final<NB><<<1, 256, 0, ctx->stream>>>(d->part, kUpdBlocks, rr_new, nullptr));
     COMAP_LAUNCH_CHECK(ctx);
     return 0;
 }
@@ -1045,9 +1073,9 @@ extern "C" int comap_destripe_dist_update(comap_destriper *d, double *scal, doub
     COMAP_DEVICE_GUARD(d->ctx);
     comap_ctx *ctx = d->ctx;
     const int nb = d->nb;
-    COMAP_NB_SWITCH(nb, k_cg_update<NB><<<kRedBlocks, 256, 0, ctx->stream>>>(scal + nb, scal + 2 * nb, x, r, p, q,
+    COMAP_NB_SWITCH(nb, k_cg_update<NB><<<kUpdBlocks, 256, 0, ctx->stream>>>(scal + nb, scal + 2 * nb, x, r, p, q,
                                                                               d->NO, d->part, flags);
-                    k_dot_final<NB><<<1, 256, 0, ctx->stream>>>(d->part, kRedBlocks, scal + 3 * nb, flags));
+                    k_dot_final<NB><<<1, 256, 0, ctx->stream>>>(d->part, kUpdBlocks, scal + 3 * nb, flags));
     COMAP_LAUNCH_CHECK(ctx);
     return 0;
 }
@@ -1081,10 +1109,11 @@ static void enqueue_iteration(comap_destriper *d, hipStream_t st)
     const unsigned pg = launch_project(d, st, p, num, nullptr, q, d->part, flags);
     double *part_rr = d->part + (size_t)d->nb * kPartMax;
     COMAP_NB_SWITCH(d->nb,
-                    k_cg_update_fused<NB><<<kRedBlocks, 256, 0, st>>>(d->scal, d->part, (int)pg, x, r, p, q, d->NO,
+                    k_cg_update_fused<NB><<<kUpdBlocks, 256, 0, st>>>(d->scal, d->part, (int)pg, x, r, p, q, d->NO,
                                                                       part_rr, flags);
-                    k_cg_direction_fused<NB><<<grid_for(d->NO), 256, 0, st>>>(d->scal, part_rr, kRedBlocks, p, r,
-                                                                              d->NO, d->flags));
+                    k_cg_direction_fused<NB><<<grid_for(d->NO, kDirBlocks), 256, 0, st>>>(d->scal, part_rr,
+                                                                                          kUpdBlocks, p, r, d->NO,
+                                                                                          d->flags));
 }
 
 // CG state, stream and the kCgBatch-iteration graph, created on first use.

@@ -202,7 +202,11 @@ class _FilePrep:
                 w_file[start + N - Nten:start + N] = 0
                 if not self.calib_source:
                     seg = tod_file[start:start + N]
-                    keep = np.nonzero(seg != 0)[0]
+                    # the reference passes non-finite samples to medianFilter.cpp, whose
+                    # two-heap order is undefined for NaN; they end with tod = 0 and
+                    # weight 0 (COMAPData.py:550-552), so here they are left out of the
+                    # median input (parity for series holding NaN is unpinned)
+                    keep = np.nonzero((seg != 0) & np.isfinite(seg))[0]
                     vals = seg[keep]
                     if vals.size > 2 * MEDFILT_STEP:
                         slot = len(queue)

@@ -171,3 +171,37 @@ def test_read_comap_data_bands_equals_per_band(case_store, monkeypatch):
             assert np.array_equal(v[sel], one[i]), (b, k)
         # dropped offsets carry no weight in that band
         assert not r['weights'][b][~sel].any()
+
+
+def test_nan_samples_do_not_abort_prep(case_store, monkeypatch):
+    """A non-finite Level-2 sample (e.g. a zero vane gain upstream) is left out of
+    the 400-sample median input instead of aborting the run; it ends with tod 0 and
+    weight 0 as in the reference (COMAPData.py:550-552)."""
+    import oracle
+    from comapreduce_amd.tools import medfilt as mf
+    seen = []
+
+    def checker(series, w, reflect=False, device=None):
+        out = []
+        for s in series:
+            assert np.isfinite(s).all()
+            seen.append(s.size)
+            z = np.concatenate((s[::-1], s, s[::-1])) if reflect else s.copy()
+            y = oracle.medfilt(z.astype(np.float64), int(w))
+            out.append(y[s.size:2 * s.size] if reflect else y)
+        return out
+    monkeypatch.setattr(mf, 'medfilt_batch', checker)
+    store, names = case_store
+    ds, attrs = store[names[1]]
+    ds = dict(ds)
+    tod = ds['averaged_tod/tod'].copy()
+    s0, e0 = ds['averaged_tod/scan_edges'][0]
+    tod[0, 0, s0 + 2500:s0 + 2510] = np.nan
+    ds['averaged_tod/tod'] = tod
+    st = dict(store)
+    st[names[1]] = (ds, attrs)
+    case = cc.CASES['car']
+    res = cd.read_comap_data([names[1]], map_info(case['map']), feeds=cc.FEEDS, store=st, **case['kw'])
+    t, w = res[0], res[1]
+    assert np.isfinite(t).all() and np.isfinite(w).all()
+    assert seen
