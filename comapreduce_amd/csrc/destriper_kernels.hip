@@ -79,7 +79,7 @@ struct comap_destriper {
 namespace {
 
 constexpr int kRedBlocks = 256;   // dot-product grids (k_dot_part)
-constexpr int kUpdBlocks = 512;   // CG update grid: its r.r partials are re-summed by every direction block
+constexpr int kUpdBlocks = 1024;  // CG update grid: its r.r partials are re-summed by every direction block
 constexpr int kDirBlocks = 1024;  // CG direction grid cap
 constexpr int kPartMax = 8192;     // >= every reduction grid below
 constexpr int kBinU = 4;           // entry loads in flight per lane (k_ds_bin)
@@ -130,10 +130,18 @@ __device__ __forceinline__ void stb(double *__restrict__ p, const double (&v)[NB
 
 // XCD-aware block order (bijective for any grid): blocks b and b + 8 share an XCD
 // (MI355X_MICROARCH.md, workgroup dispatch), so logical block ids are dealt to the 8
-// groups in contiguous runs -- each XCD's L2 then serves a contiguous range of map rows
-// (k_ds_bin) or of offsets (k_ds_project), whose x / map gathers overlap.
+// groups in contiguous runs (each XCD's L2 then serves a contiguous range of map rows
+// or offsets).  Measured at C5 and NOT used (COMAP_DS_XCD=0): k_ds_bin 111 -> 131 us,
+// k_ds_project (contiguous offset runs per block) 114 -> 151 us for one band, 200 -> 234
+// and 233 -> 290 us for four -- the round-robin order streams the entry arrays with
+// every XCD on neighbouring lines, and the map / offset vectors are re-read from the
+// 256 MB Infinity Cache either way.
+#ifndef COMAP_DS_XCD
+#define COMAP_DS_XCD 0
+#endif
 __device__ __forceinline__ int64_t xcd_block(int64_t bid, int64_t nwg)
 {
+    if (!COMAP_DS_XCD) return bid;
     const int64_t q = nwg / 8, r = nwg % 8, x = bid % 8;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
 }
@@ -146,10 +154,22 @@ __device__ __forceinline__ double wave_sum(double v)
 }
 
 // Fixed-order sum of n block partials by one 256-thread block (k_dot_final's order).
+// Each thread adds part[tid], part[tid + 256], ... in that order; the loads are issued
+// 8 at a time before the adds (a serial load -> add chain costs one L2 round trip per
+// partial: ~40 us for 4 bands x 2k partials at C4, most of the CG update kernel).
 __device__ __forceinline__ double block_final_sum(const double *__restrict__ part, int n, double *red)
 {
     double acc = 0.0;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) acc += part[i];
+    constexpr int kB = 8;
+    int i = threadIdx.x;
+    for (; i + (kB - 1) * 256 < n; i += kB * 256) {
+        double v[kB];
+#pragma unroll
+        for (int k = 0; k < kB; ++k) v[k] = part[i + k * 256];
+#pragma unroll
+        for (int k = 0; k < kB; ++k) acc += v[k];
+    }
+    for (; i < n; i += 256) acc += part[i];
     acc = wave_sum(acc);
     __syncthreads();
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
@@ -445,10 +465,14 @@ __global__ void __launch_bounds__(256) k_ds_project(const int64_t *__restrict__ 
     double acc[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) acc[b] = 0.0;
+#if COMAP_DS_XCD
     // each logical block takes a contiguous run of offset sweeps (time-contiguous samples)
     const int64_t sweeps = (NO + kPer - 1) / kPer, per = (sweeps + gridDim.x - 1) / gridDim.x;
     const int64_t s0 = xcd_block(blockIdx.x, gridDim.x) * per, s1 = min(s0 + per, sweeps);
     for (int64_t o0 = s0 * kPer; o0 < s1 * kPer; o0 += kPer) {
+#else
+    for (int64_t o0 = (int64_t)blockIdx.x * kPer; o0 < NO; o0 += (int64_t)gridDim.x * kPer) {
+#endif
         const int64_t o = o0 + threadIdx.x / G;
         const bool valid = o < NO;
         const int64_t e1 = valid ? orow[o + 1] : 0;
