@@ -41,6 +41,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cmath>
+#include <cstdlib>
 
 struct comap_destriper {
     comap_ctx *ctx = nullptr;
@@ -69,6 +70,7 @@ struct comap_destriper {
     int32_t *flags = nullptr;      // [2 + 2 nb]
     int32_t *hrow = nullptr;       // [nh] pixel rows with entries (the CG bin skips empty rows)
     int64_t nh = 0;
+    int32_t *perm = nullptr;       // [NO] internal offset position -> caller's offset (NULL: identity)
     int32_t *flags_host = nullptr; // pinned [2 + 2 nb]
     double *thr_host = nullptr;    // pinned [1]
     hipStream_t cs = nullptr;      // CG stream (graph capture needs a non-default stream)
@@ -284,6 +286,71 @@ void launch_entries(int L, unsigned blocks, hipStream_t st, const int32_t *pix, 
         k_ds_entries<2, NB><<<blocks, 256, 0, st>>>(pix, w, tod, N, NO, L, pass, cnt, orow, opix, ow, ws, tw);
     else
         k_ds_entries<4, NB><<<blocks, 256, 0, st>>>(pix, w, tod, N, NO, L, pass, cnt, orow, opix, ow, ws, tw);
+}
+
+// Processing order of the offsets.  In time order the offsets in flight at once
+// cover the whole scan pattern, so the projection's map gathers (npix x 8 NB bytes,
+// 7.4 MB for 4 bands at 480^2) miss the 4 MB XCD L2s.  Sorting offsets by the pixel
+// of their first on-map sample makes concurrently processed offsets look at one band
+// of map rows, and puts offsets that cross the same pixels next to each other in the
+// CG vectors (the bin's x gathers).  Key: that pixel (npix when the offset is all
+// off-map); a stable sort keeps time order among equal keys.
+__global__ void k_offset_keys(const int64_t *__restrict__ orow, const int32_t *__restrict__ opix, int64_t NO,
+                              int64_t npix, int32_t *__restrict__ key, int32_t *__restrict__ val)
+{
+    for (int64_t o = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; o < NO; o += (int64_t)gridDim.x * blockDim.x) {
+        int32_t k = (int32_t)npix;
+        for (int64_t e = orow[o]; e < orow[o + 1]; ++e)
+            if (opix[e] >= 0) { k = opix[e]; break; }
+        key[o] = k;
+        val[o] = (int32_t)o;
+    }
+}
+
+__global__ void k_perm_counts(const int64_t *__restrict__ orow, const int32_t *__restrict__ perm, int64_t NO,
+                              int64_t *__restrict__ cnt)
+{
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < NO; k += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t o = perm[k];
+        cnt[k] = orow[o + 1] - orow[o];
+    }
+}
+
+// new offset k = old offset perm[k]: one wave copies its entry row
+template <int NB>
+__global__ void __launch_bounds__(256) k_perm_entries(const int64_t *__restrict__ orow, const int32_t *__restrict__ opix,
+                                                      const double *__restrict__ ow, const double *__restrict__ ws,
+                                                      const double *__restrict__ tw, const int32_t *__restrict__ perm,
+                                                      int64_t NO, const int64_t *__restrict__ orow2,
+                                                      int32_t *__restrict__ opix2, double *__restrict__ ow2,
+                                                      double *__restrict__ ws2, double *__restrict__ tw2)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (k >= NO) return;
+    const int64_t o = perm[k];
+    const int64_t e0 = orow[o], n = orow[o + 1] - e0, f0 = orow2[k];
+    for (int64_t j = lane; j < n; j += 64) {
+        opix2[f0 + j] = opix[e0 + j];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) ow2[(f0 + j) * NB + b] = ow[(e0 + j) * NB + b];
+    }
+    if (lane < NB) {
+        ws2[k * NB + lane] = ws[o * NB + lane];
+        tw2[k * NB + lane] = tw[o * NB + lane];
+    }
+}
+
+// x_out[perm[k]] = x[k] per band (internal offset order -> the caller's)
+template <int NB>
+__global__ void k_unpermute(const double *__restrict__ x, const int32_t *__restrict__ perm, int64_t NO,
+                            double *__restrict__ out)
+{
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < NO; k += (int64_t)gridDim.x * blockDim.x) {
+        double v[NB];
+        ldb<NB>(x + k * NB, v);
+        stb<NB>(out + (int64_t)perm[k] * NB, v);
+    }
 }
 
 // keys for the pixel-major transpose: pixel of each offset-major entry (npix for off-map)
@@ -879,12 +946,12 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     COMAP_NB_SWITCH(nb, launch_entries<NB>(L, gblocks, st, pix, w, tod, N, d->NO, 0, cnt, nullptr, nullptr, nullptr,
                                            d->ws, d->tw));
     COMAP_LAUNCH_CHECK(ctx);
-    size_t tb = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, d->orow, (int)(d->NO + 1), st);
+    size_t scan_tb = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tb, cnt, d->orow, (int)(d->NO + 1), st);
     char *scan_tmp = nullptr;
-    COMAP_CHECK(ctx, tmp.alloc(&scan_tmp, tb));
+    COMAP_CHECK(ctx, tmp.alloc(&scan_tmp, scan_tb));
     COMAP_CHECK(ctx, hipMemsetAsync(cnt + d->NO, 0, 8, st));
-    COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, cnt, d->orow, (int)(d->NO + 1), st));
+    COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_tb, cnt, d->orow, (int)(d->NO + 1), st));
     COMAP_CHECK(ctx, hipMemcpyAsync(&d->nnz, d->orow + d->NO, 8, hipMemcpyDeviceToHost, st));
     COMAP_CHECK(ctx, hipStreamSynchronize(st));
     rc |= dalloc(ctx, &d->opix, d->nnz);
@@ -893,7 +960,6 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     COMAP_NB_SWITCH(nb, launch_entries<NB>(L, gblocks, st, pix, w, tod, N, d->NO, 1, nullptr, d->orow, d->opix, d->ow,
                                            nullptr, nullptr));
     COMAP_LAUNCH_CHECK(ctx);
-    // ---- pixel-major transpose (stable radix sort keeps offset order within a pixel)
     const int64_t sortn = std::max<int64_t>(d->nnz, N);
     int32_t *k0 = nullptr, *k1 = nullptr, *v0 = nullptr, *v1 = nullptr, *eoff = nullptr;
     COMAP_CHECK(ctx, tmp.alloc(&k0, sortn));
@@ -902,13 +968,49 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     COMAP_CHECK(ctx, tmp.alloc(&v1, sortn));
     COMAP_CHECK(ctx, tmp.alloc(&eoff, d->nnz));
     int end_bit = 1;
-    while ((1ll << end_bit) <= npix) ++end_bit;
-    k_entry_keys<<<grid_for(d->NO), 256, 0, st>>>(d->orow, d->NO, d->opix, npix, k0, v0, eoff);
-    COMAP_LAUNCH_CHECK(ctx);
-    tb = 0;
+    while ((1ll << (end_bit)) <= npix) ++end_bit;
+    size_t tb = 0;
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k0, k1, v0, v1, (int)sortn, 0, end_bit, st);
     char *sort_tmp = nullptr;
     COMAP_CHECK(ctx, tmp.alloc(&sort_tmp, tb));
+    // ---- spatial processing order of the offsets (COMAP_DS_ORDER=0 keeps time order)
+    const char *ord = getenv("COMAP_DS_ORDER");
+    if (!(ord && ord[0] == '0')) {
+        k_offset_keys<<<grid_for(d->NO), 256, 0, st>>>(d->orow, d->opix, d->NO, npix, k0, v0);
+        COMAP_LAUNCH_CHECK(ctx);
+        if (dalloc(ctx, &d->perm, d->NO)) return -2;
+        COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(sort_tmp, tb, k0, k1, v0, d->perm, (int)d->NO, 0, end_bit,
+                                                            st));
+        int64_t *orow2 = nullptr, *cnt2 = nullptr;
+        int32_t *opix2 = nullptr;
+        double *ow2 = nullptr, *ws2 = nullptr, *tw2 = nullptr;
+        if (dalloc(ctx, &orow2, d->NO + 1) || dalloc(ctx, &opix2, d->nnz) || dalloc(ctx, &ow2, d->nnz * NB) ||
+            dalloc(ctx, &ws2, d->NO * NB) || dalloc(ctx, &tw2, d->NO * NB)) {
+            for (void *q : {(void *)orow2, (void *)opix2, (void *)ow2, (void *)ws2, (void *)tw2})
+                if (q) (void)hipFree(q);
+            return -2;
+        }
+        // the new arrays replace the old ones now (comap_destripe_destroy frees whatever d holds)
+        std::swap(d->orow, orow2);
+        std::swap(d->opix, opix2);
+        std::swap(d->ow, ow2);
+        std::swap(d->ws, ws2);
+        std::swap(d->tw, tw2);
+        DevTemps old(st);   // the time-ordered arrays, freed once the copies below have run
+        old.p = {(void *)orow2, (void *)opix2, (void *)ow2, (void *)ws2, (void *)tw2};
+        COMAP_CHECK(ctx, tmp.alloc(&cnt2, d->NO + 1));
+        k_perm_counts<<<grid_for(d->NO), 256, 0, st>>>(orow2, d->perm, d->NO, cnt2);
+        COMAP_LAUNCH_CHECK(ctx);
+        COMAP_CHECK(ctx, hipMemsetAsync(cnt2 + d->NO, 0, 8, st));
+        COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_tb, cnt2, d->orow,
+                                                          (int)(d->NO + 1), st));
+        COMAP_NB_SWITCH(nb, k_perm_entries<NB><<<gblocks, 256, 0, st>>>(orow2, opix2, ow2, ws2, tw2, d->perm, d->NO,
+                                                                         d->orow, d->opix, d->ow, d->ws, d->tw));
+        COMAP_LAUNCH_CHECK(ctx);
+    }
+    // ---- pixel-major transpose (stable radix sort keeps offset order within a pixel)
+    k_entry_keys<<<grid_for(d->NO), 256, 0, st>>>(d->orow, d->NO, d->opix, npix, k0, v0, eoff);
+    COMAP_LAUNCH_CHECK(ctx);
     COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(sort_tmp, tb, k0, k1, v0, v1, (int)d->nnz, 0, end_bit, st));
     k_rowptr<<<grid_for(npix + 1), 256, 0, st>>>(k1, d->nnz, npix, d->prow);
     COMAP_LAUNCH_CHECK(ctx);
@@ -957,7 +1059,7 @@ extern "C" int comap_destripe_destroy(comap_destriper *d)
     COMAP_DEVICE_GUARD(d->ctx);
     if (d->cs) (void)hipStreamSynchronize(d->cs);
     void *b[] = {d->orow, d->opix, d->ow, d->ws, d->tw, d->prow, d->poff, d->pw, d->h, d->hits, d->nnum, d->part, d->scal,
-                 d->cg, d->flags, d->hrow};
+                 d->cg, d->flags, d->hrow, d->perm};
     for (void *p : b)
         if (p) (void)hipFree(p);
     if (d->flags_host) (void)hipHostFree(d->flags_host);
@@ -1047,6 +1149,22 @@ extern "C" int comap_destripe_cg_direction(comap_destriper *d, const double *rr_
     comap_ctx *ctx = d->ctx;
     COMAP_NB_SWITCH(d->nb, k_cg_direction<NB><<<grid_for(d->NO), 256, 0, ctx->stream>>>(rr_new, rr, p, r, d->NO,
                                                                                          nullptr));
+    COMAP_LAUNCH_CHECK(ctx);
+    return 0;
+}
+
+extern "C" int comap_destripe_offsets_natural(comap_destriper *d, const double *x_internal, double *x_out)
+{
+    if (!d || !x_internal || !x_out || x_internal == x_out) return -1;
+    COMAP_DEVICE_GUARD(d->ctx);
+    comap_ctx *ctx = d->ctx;
+    if (d->perm) {
+        COMAP_NB_SWITCH(d->nb, k_unpermute<NB><<<grid_for(d->NO), 256, 0, ctx->stream>>>(x_internal, d->perm, d->NO,
+                                                                                         x_out));
+    } else {
+        COMAP_CHECK(ctx, hipMemcpyAsync(x_out, x_internal, 8 * (size_t)d->NO * d->nb, hipMemcpyDeviceToDevice,
+                                        ctx->stream));
+    }
     COMAP_LAUNCH_CHECK(ctx);
     return 0;
 }
@@ -1210,7 +1328,12 @@ extern "C" int comap_destripe_solve(comap_destriper *d, double threshold, int32_
     }
     if (iters_out)
         for (int b = 0; b < nb; ++b) iters_out[b] = d->flags_host[2 + nb + b];
-    COMAP_CHECK(ctx, hipMemcpyAsync(x, cx, 8 * n, hipMemcpyDeviceToDevice, st));
+    if (d->perm) {
+        COMAP_NB_SWITCH(nb, k_unpermute<NB><<<grid_for(d->NO), 256, 0, st>>>(cx, d->perm, d->NO, x));
+        COMAP_LAUNCH_CHECK(ctx);
+    } else {
+        COMAP_CHECK(ctx, hipMemcpyAsync(x, cx, 8 * n, hipMemcpyDeviceToDevice, st));
+    }
     // final maps: map = (sum w tod - W x) / h ; naive = sum w tod / h
     if (map) {
         launch_bin(d, st, cx, d->nnum, nullptr, num, nullptr);

@@ -49,7 +49,8 @@ def cg_solve(ops, allreduce, threshold=1e-6, niter=100, h=None, nnum=None):
     ops: operator object (DeviceOps or oracle.destriper.ShardOps) for this
     rank's samples; allreduce(array) sums in place across ranks.  h / nnum
     are the global weight map and naive numerator (computed when None).
-    Returns (x, iterations, h, nnum)."""
+    Returns (x, iterations, h, nnum); for DeviceOps x is in the problem's internal
+    offset order (DeviceOps.natural converts)."""
     if getattr(ops, 'nb', 1) != 1:
         raise ValueError('cg_solve drives one band; batched bands use cg_solve_batched')
     if h is None or nnum is None:
@@ -95,7 +96,8 @@ def cg_solve_batched(ops, allreduce, threshold=1e-6, niter=100, batch=16):
     Iterations queued after convergence are no-ops (their all-reduces sum
     stale buffers that are not read again).  Works for every band of a batched
     problem at once (vectors interleaved [n][nb], one all-reduce per sum for
-    all bands).  Returns (x, iterations per band (list), h, nnum)."""
+    all bands).  Returns (x in the problem's internal offset order -- see
+    DeviceOps.natural --, iterations per band (list), h, nnum)."""
     torch = ops.torch
     nb = ops.nb
     h0, _, n0 = ops.local_maps()
@@ -193,6 +195,13 @@ class DeviceOps:
         t = a if isinstance(a, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(a))
         t = t.to(device=self.dev, dtype=dt)
         return t.reshape(1, -1).contiguous() if t.dim() == 1 else t.contiguous()
+
+    def natural(self, x):
+        """Offset vector in the caller's offset order (the C side processes offsets in
+        a spatially sorted internal order; every other vector here is internal)."""
+        out = self.zeros(self.n_offsets * self.nb)
+        self._c('comap_destripe_offsets_natural', self.h, self._v(x), self._v(out))
+        return out
 
     def split_bands(self, v):
         """[n*nb] interleaved -> [n_bands, n] (contiguous copy, padding band dropped)."""
@@ -342,6 +351,7 @@ class DeviceDestriper:
             ops.div_map(num, h, maps['map'])
             ops.div_map(nnum, h, maps['naive'])
             it = it[:ops.n_bands]
+            x = ops.natural(x)
         if not self.multi:
             maps['map2'] = maps['weight']
             return {'x': x, 'iters': it[0], 'maps': maps}

@@ -202,13 +202,19 @@ int comap_destripe_create(comap_ctx *ctx, const int32_t *pixels_dev, const doubl
  * hit map, COMAPData.py:550-568).  Every per-band vector of the functions below
  * is interleaved band-fastest: offsets [N/L][n_bands], maps [npix][n_bands];
  * each band's CG keeps its own scalars, stop test and iteration count.
- * comap_destripe_create is this with n_bands = 1. */
+ * comap_destripe_create is this with n_bands = 1.
+ * Offset order: the problem processes its offsets in an internal (spatially
+ * sorted) order; every offset vector the functions below take or return is in
+ * that order, except the x of comap_destripe_solve, which is in the caller's
+ * order.  comap_destripe_offsets_natural converts an internal vector. */
 int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pixels_dev, const double *tod_dev,
                                 const double *weights_dev, const uint8_t *keep_dev, int64_t n_samples,
                                 int32_t offset_length, int64_t npix, int32_t n_bands, comap_destriper **out);
 int comap_destripe_destroy(comap_destriper *d);
 int64_t comap_destripe_n_offsets(const comap_destriper *d);
 int32_t comap_destripe_n_bands(const comap_destriper *d);
+/* x_out [N/L][NB] (caller's offset order) from x_internal (internal order); x_out != x_internal */
+int comap_destripe_offsets_natural(comap_destriper *d, const double *x_internal_dev, double *x_out_dev);
 int comap_destripe_nnz(const comap_destriper *d, int64_t *nnz_offset_major, int64_t *nnz_pixel_major);
 /* Local (this rank) sample-level maps, summed in binValues order:
  * h = sum w, hits = sum 1, naive_num = sum w tod (any may be NULL). */
