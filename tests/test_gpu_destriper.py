@@ -186,3 +186,48 @@ def test_batched_bands_multirank_driver_matches_native():
     xn, itn, _ = ops.solve_native(1e-6, 100)
     assert it == itn
     assert np.array_equal(ops.natural(x).cpu().numpy(), xn.cpu().numpy())
+
+
+@pytest.mark.parametrize('niter', [37, 100])
+def test_graph_driver_matches_batched(niter):
+    """The captured-graph multi-rank driver (kernels + collectives of 16 iterations
+    per replay) == the eager batched driver, bit for bit (one rank, identity sums)."""
+    from comapreduce_amd.mapmaking.destriper import DeviceOps, cg_solve_batched, cg_solve_graph
+    p, tods, ws, keep = _bands_problem(4)
+    ops = DeviceOps(p, tods, ws, L, NPIX, keep=keep)
+    xg, itg, _, _ = cg_solve_graph(ops, lambda a: a, threshold=1e-6, niter=niter)
+    xb, itb, _, _ = cg_solve_batched(ops, lambda a: a, threshold=1e-6, niter=niter)
+    assert itg == itb
+    assert np.array_equal(xg.cpu().numpy(), xb.cpu().numpy())
+
+
+def _nccl_graph_rank(port, q):
+    """One-rank RCCL process group: the graph driver captures real ncclAllReduce calls."""
+    import torch
+    import torch.distributed as dist
+    from comapreduce_amd.mapmaking.destriper import DeviceOps, cg_solve_batched, cg_solve_graph
+    torch.cuda.set_device(0)
+    dist.init_process_group('nccl', init_method=f'tcp://127.0.0.1:{port}', rank=0, world_size=1,
+                            device_id=torch.device('cuda', 0))
+
+    def ar(t):
+        dist.all_reduce(t)
+        return t
+    p, tods, ws, keep = _bands_problem(4)
+    ops = DeviceOps(p, tods, ws, L, NPIX, keep=keep)
+    xg, itg, _, _ = cg_solve_graph(ops, ar, threshold=1e-6, niter=48)
+    xb, itb, _, _ = cg_solve_batched(ops, ar, threshold=1e-6, niter=48)
+    q.put((itg, itb, bool(np.array_equal(xg.cpu().numpy(), xb.cpu().numpy()))))
+    dist.destroy_process_group()
+
+
+def test_graph_driver_captures_rccl_allreduce():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = 29900 + os.getpid() % 90
+    pr = ctx.Process(target=_nccl_graph_rank, args=(port, q))
+    pr.start()
+    itg, itb, same = q.get(timeout=240)
+    pr.join(timeout=60)
+    assert itg == itb and same
