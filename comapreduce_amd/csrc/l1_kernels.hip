@@ -23,6 +23,7 @@
 #include "comap_internal.h"
 
 #include <cmath>
+#include <cstdlib>
 
 using namespace comap;
 
@@ -1470,7 +1471,10 @@ extern "C" int comap_l1_plan_create(comap_ctx *ctx, const comap_obs_desc *d, com
     rc |= dalloc(ctx, &p->oa, 2 * (size_t)UC);
     if (rc) { delete p; return -2; }
     // pass B / median / pass C pipeline groups (comap_l1_average): contiguous unit ranges
-    p->ngroups = std::max(1, std::min(std::min((int)COMAP_GROUPS, comap_l1_plan::kMaxGroups), (int)p->U));
+    // COMAP_GROUPS (env) overrides the compiled default -- measurement knob
+    int groups = COMAP_GROUPS;
+    if (const char *g = getenv("COMAP_GROUPS")) groups = atoi(g);
+    p->ngroups = std::max(1, std::min(std::min(groups, comap_l1_plan::kMaxGroups), (int)p->U));
     {
         std::vector<int64_t> tu(p->U + 1, 0);
         for (int u = 0; u < p->U; ++u) tu[u + 1] = tu[u] + (p->units_h[4 * u + 3] + kTile - 1) / kTile;
@@ -1480,7 +1484,15 @@ extern "C" int comap_l1_plan_create(comap_ctx *ctx, const comap_obs_desc *d, com
             p->grpb_tile0[g] = tub[p->grp_u0[g]];
         }
     }
-    bool ok = hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking) == hipSuccess;
+    // the median side stream may run at a higher priority than the streaming passes
+    // (COMAP_SIDE_PRIO=1): its latency-bound kernels then take CU slots first while
+    // the next group's bandwidth-bound pass B runs on the rest
+    int prio = 0;
+    if (const char *sp = getenv("COMAP_SIDE_PRIO"); sp && sp[0] == '1') {
+        int lo = 0, hi = 0;
+        if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess) prio = hi;
+    }
+    bool ok = hipStreamCreateWithPriority(&p->side, hipStreamNonBlocking, prio) == hipSuccess;
     for (int g = 0; g < p->ngroups && ok; ++g)
         ok = hipEventCreateWithFlags(&p->ev_b[g], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&p->ev_m[g], hipEventDisableTiming) == hipSuccess;
