@@ -65,6 +65,8 @@ def parse():
     ap.add_argument('--c5-obs', type=int, default=8, help='observations per GPU in the C5 destriper leg (0: skip)')
     ap.add_argument('--check', action='store_true', help='compare one unit against the CPU oracle')
     ap.add_argument('--no-e2e', action='store_true', help='skip the host-cube -> host-Level-2 leg')
+    ap.add_argument('--shard-of', type=int, default=0,
+                    help='measurement aid: reduce only rank 0\'s C3 shard of an N-way split, in this one process')
     return ap.parse_args()
 
 
@@ -414,6 +416,8 @@ def main():
     shard = args.mode == 'shard' and world > 1
     if shard:
         data, sh = build_observation(F, T, obs_id=1, device=device, rank=rank, world=world)
+    elif args.shard_of > 1:
+        data, sh = build_observation(F, T, obs_id=1, device=device, rank=0, world=args.shard_of)
     else:
         data, sh = build_observation(F, T, obs_id=rank + 1, device=device)
     cube_sampch = F * 4 * 1024 * T                 # one observation's cube
