@@ -190,6 +190,11 @@ struct comap_l1_plan {
     int64_t *nanpos = nullptr;         // [nanpos_cap] cube element offsets the fill overwrote
     int64_t nanpos_cap = 0;
     int64_t *nanpos_n = nullptr;       // [1] entries used
+    // comap_l1_vane's hot/cold index lists: host arrays are copied into pinned staging
+    // and uploaded asynchronously (no host wait); the event guards the staging reuse
+    char *vane_pinned = nullptr, *vane_dev = nullptr;
+    size_t vane_cap = 0;
+    hipEvent_t vane_ev = nullptr;
     double *ubs = nullptr;             // [U*4][4] fit normal-equation sums n, SA, SAA per (unit, band)
     double *fitsum = nullptr;          // [2][U*4096] masked Sd, SAd (select_time path)
     double *oa = nullptr;              // [U*4096][2] offset/slope L1AGC subtracts
