@@ -520,13 +520,29 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
     // the global-sort path is the default (measured faster at w = 6000); the sliding
     // sorted window is selected with COMAP_MEDIAN_PATH=slide
     if (fits && force && !strcmp(force, "slide")) return plan_slide(ctx, mp, jobs_in, w);
+    // Sub-job length: at most kMaxOut outputs (LDS bitmaps), and short enough that
+    // there are >= kMinSegs sorted segments -- the segmented sort runs one block per
+    // segment, so a plan of few long series (a C3 shard: ~100 of 16k outputs) would
+    // leave most CUs idle; each extra segment re-sorts w - 1 values.
+    const char *ms = getenv("COMAP_MEDIAN_MINSEGS");
+    const int64_t kMinSegs = ms ? atoll(ms) : 512;
+    int64_t total_out = 0;
+    for (const MedJob &j : jobs_in) total_out += std::max<int64_t>(0, j.out_hi - j.out_lo);
+    int64_t max_out = kMaxOut;
+    if (kMinSegs > 0 && total_out > 0) {
+        const int64_t want = (total_out + kMinSegs - 1) / kMinSegs;
+        max_out = std::min<int64_t>(kMaxOut, std::max<int64_t>(4 * (int64_t)kWalkThreads,
+                                                               (want + kWalkThreads - 1) / kWalkThreads * kWalkThreads));
+    }
     std::vector<MedJob> jobs;
     for (const MedJob &j : jobs_in) {
-        if (j.out_hi - j.out_lo <= kMaxOut) { jobs.push_back(j); continue; }
-        for (int64_t lo = j.out_lo; lo < j.out_hi; lo += kMaxOut) {
+        if (j.out_hi - j.out_lo <= max_out) { jobs.push_back(j); continue; }
+        const int64_t nsub = (j.out_hi - j.out_lo + max_out - 1) / max_out;
+        const int64_t len = ((j.out_hi - j.out_lo + nsub - 1) / nsub + kWalkThreads - 1) / kWalkThreads * kWalkThreads;
+        for (int64_t lo = j.out_lo; lo < j.out_hi; lo += len) {
             MedJob sj = j;
             sj.out_lo = lo;
-            sj.out_hi = std::min(j.out_hi, lo + kMaxOut);
+            sj.out_hi = std::min(j.out_hi, lo + len);
             sj.dst = j.dst + (lo - j.out_lo);      // dst is indexed from out_lo
             jobs.push_back(sj);
         }
