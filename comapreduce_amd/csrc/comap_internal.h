@@ -125,6 +125,8 @@ struct MedPlan {
     uint64_t *k0 = nullptr, *k1 = nullptr;
     int32_t *v0 = nullptr, *v1 = nullptr;
     int32_t *rank = nullptr;     // dev [nitems] position -> sorted index
+    bool key32 = true;           // sort 32-bit proxies + exact run fix-up (else u64 keys)
+    int32_t *redo = nullptr;     // dev [3][njobs]: segment re-sort flags, begin, end
     void *temp = nullptr;
     size_t temp_bytes = 0;
 };

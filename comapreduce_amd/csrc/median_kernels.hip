@@ -7,10 +7,16 @@
 // (hi + lo) / 2 in f64, the order Mediator::getMedian uses (Mediator.h:91-99).
 //
 // 1. k_med_keys: every series (job) contributes the Ns = n_out + w - 1 values
-//    its windows touch, as order-preserving u64 keys + positions.
-// 2. hipcub segmented radix sort: each series sorted ONCE (stable);
+//    its windows touch, as 32-bit order-preserving keys of the value rounded to
+//    f32 (a monotone map, so the f64 order only differs inside runs of equal
+//    proxies) + positions.
+// 2. rocprim segmented radix sort (4 digit passes instead of 8); k_med_fix then
+//    re-sorts every run of equal proxies by the exact u64 key of the f64 value
+//    (runs are a few elements on real data).  A segment with a run longer than
+//    kFixRun is flagged and re-sorted whole on 64-bit keys (a second segmented
+//    sort over the flagged segments only -- the others are passed as empty).
 //    k_med_rank inverts the permutation (rank of every position).
-// 3. k_med_walk, one workgroup per chunk of L = 256 consecutive outputs:
+// 3. k_med_walk, one workgroup per chunk of L = 128 consecutive outputs:
 //    a. the chunk's union window U = positions [c, c+w+L-1) is marked in an
 //       LDS bitmap indexed by rank (coalesced reads of rank[]), together with
 //       its "zone" Z (offsets < L-1 or >= w: excluded by some output's window);
@@ -64,14 +70,90 @@ __device__ __forceinline__ double xprime(const MedJob &j, int64_t pos, int h)
     return j.src[q < 0 ? 0 : q];
 }
 
+// order-preserving 32-bit proxy: the key of the value rounded to f32 (monotone non-decreasing in v)
+__device__ __forceinline__ uint32_t key32_of(double v)
+{
+    const uint32_t b = __float_as_uint((float)v);
+    return (b >> 31) ? ~b : (b | 0x80000000u);
+}
+
+template <typename K>
 __global__ void __launch_bounds__(256) k_med_keys(const MedJob *__restrict__ jobs, const int32_t *__restrict__ seg,
-                                                  int32_t njobs, int32_t w, uint64_t *__restrict__ keys,
+                                                  int32_t njobs, int32_t w, K *__restrict__ keys,
                                                   int32_t *__restrict__ vals)
 {
     const int jb = blockIdx.y;
     if (jb >= njobs) return;
     const MedJob job = jobs[jb];
     const int32_t s0 = seg[jb], ns = seg[jb + 1] - s0;
+    const int h = w / 2;
+    const int64_t base = job.out_lo - h;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += gridDim.x * blockDim.x) {
+        const double v = xprime(job, base + i, h);
+        if constexpr (sizeof(K) == 4) keys[s0 + i] = key32_of(v);
+        else keys[s0 + i] = key_of(v);
+        vals[s0 + i] = i;
+    }
+}
+
+constexpr int kFixRun = 32;   // longest run of equal proxies k_med_fix re-sorts in place
+
+// Exact order inside runs of equal proxy keys: the thread at a run's first element
+// insertion-sorts the run's positions by (u64 key of the f64 value, position) --
+// the order the 64-bit sort gives.  Longer runs flag the segment for the full re-sort.
+__global__ void __launch_bounds__(256) k_med_fix(const MedJob *__restrict__ jobs, const int32_t *__restrict__ seg,
+                                                 int32_t njobs, int32_t w, const uint32_t *__restrict__ skeys,
+                                                 int32_t *__restrict__ svals, int32_t *__restrict__ redo)
+{
+    const int jb = blockIdx.y;
+    if (jb >= njobs) return;
+    const int32_t s0 = seg[jb], ns = seg[jb + 1] - s0;
+    const int h = w / 2;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += gridDim.x * blockDim.x) {
+        const uint32_t k = skeys[s0 + i];
+        if (i + 1 >= ns || skeys[s0 + i + 1] != k) continue;     // not part of a run, or not its start
+        if (i > 0 && skeys[s0 + i - 1] == k) continue;
+        int e = i + 2;
+        while (e < ns && e - i <= kFixRun && skeys[s0 + e] == k) ++e;
+        if (e - i > kFixRun) { redo[jb] = 1; continue; }
+        const MedJob job = jobs[jb];
+        const int64_t base = job.out_lo - h;
+        uint64_t rk[kFixRun];
+        int32_t rp[kFixRun];
+        const int n = e - i;
+        for (int t = 0; t < n; ++t) {
+            const int32_t p = svals[s0 + i + t];
+            const uint64_t kk = key_of(xprime(job, base + p, h));
+            int u = t;
+            while (u > 0 && (rk[u - 1] > kk || (rk[u - 1] == kk && rp[u - 1] > p))) {
+                rk[u] = rk[u - 1];
+                rp[u] = rp[u - 1];
+                --u;
+            }
+            rk[u] = kk;
+            rp[u] = p;
+        }
+        for (int t = 0; t < n; ++t) svals[s0 + i + t] = rp[t];
+    }
+}
+
+// Segments flagged by k_med_fix: full 64-bit keys and the [begin, end) of the
+// second sort (empty for the others).
+__global__ void __launch_bounds__(256) k_med_redo(const MedJob *__restrict__ jobs, const int32_t *__restrict__ seg,
+                                                  int32_t njobs, int32_t w, const int32_t *__restrict__ redo,
+                                                  uint64_t *__restrict__ keys, int32_t *__restrict__ vals,
+                                                  int32_t *__restrict__ beg, int32_t *__restrict__ end)
+{
+    const int jb = blockIdx.y;
+    if (jb >= njobs) return;
+    const int32_t s0 = seg[jb], ns = seg[jb + 1] - s0;
+    const bool on = redo[jb] != 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        beg[jb] = s0;
+        end[jb] = on ? s0 + ns : s0;
+    }
+    if (!on) return;
+    const MedJob job = jobs[jb];
     const int h = w / 2;
     const int64_t base = job.out_lo - h;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += gridDim.x * blockDim.x) {
@@ -90,14 +172,13 @@ __global__ void __launch_bounds__(256) k_med_rank(const int32_t *__restrict__ se
         rank[s0 + svals[s0 + i]] = i;
 }
 
-__global__ void __launch_bounds__(kWalkThreads) k_med_walk(const MedJob *__restrict__ jobs,
-                                                           const int64_t *__restrict__ chunks,
-                                                           const int32_t *__restrict__ seg,
-                                                           const uint64_t *__restrict__ skeys,
-                                                           const int32_t *__restrict__ svals,
-                                                           const int32_t *__restrict__ rank, int32_t w,
-                                                           int32_t lc, int32_t nwmax)
+template <int LT>   // threads = outputs per chunk
+__global__ void __launch_bounds__(LT) k_med_walk(const MedJob *__restrict__ jobs, const int64_t *__restrict__ chunks,
+                                                 const int32_t *__restrict__ seg, const int32_t *__restrict__ svals,
+                                                 const int32_t *__restrict__ rank, int32_t w, int32_t nwmax)
 {
+    constexpr int kWalkThreads = LT;
+    const int lc = LT;
     // LDS: E (16-B aligned for 4-entry reads) | U bitmap | Z bitmap | U word prefixes | scans
     extern __shared__ __align__(16) unsigned char smem[];
     uint32_t *E = reinterpret_cast<uint32_t *>(smem);
@@ -205,8 +286,11 @@ __global__ void __launch_bounds__(kWalkThreads) k_med_walk(const MedJob *__restr
             for (int t = qi - Up[lo]; t > 0; --t) bits &= bits - 1u;
             return 32 * lo + __builtin_ctz(bits);
         };
+        const int h = w / 2;
+        const int64_t base = job.out_lo - h;
+        auto value = [&](int qi) -> double { return xprime(job, base + svals[s0 + select(qi)], h); };
         const int q1 = q;
-        const double v1 = val_of(skeys[s0 + select(q1)]);
+        const double v1 = value(q1);
         double out;
         if (w % 2 == 0) {
             q = q1 + 1;
@@ -216,7 +300,7 @@ __global__ void __launch_bounds__(kWalkThreads) k_med_walk(const MedJob *__restr
                 const int pp = (int)(e & 0xffff);
                 q += (pp < k) | (pp >= k + w);
             }
-            out = (val_of(skeys[s0 + select(q)]) + v1) / 2.0;
+            out = (value(q) + v1) / 2.0;
         } else {
             out = v1;
         }
@@ -449,14 +533,15 @@ size_t slide_smem(int w)
 #endif
 using SegSortConfig = rocprim::segmented_radix_sort_config<COMAP_SORT_RB, rocprim::kernel_config<256, COMAP_SORT_IPT>,
                                                            rocprim::DisabledWarpSortConfig, false>;
-hipError_t seg_sort(void *tmp, size_t &tb, const uint64_t *k0, uint64_t *k1, const int32_t *v0, int32_t *v1,
-                    int n, int nseg, const int32_t *seg, hipStream_t st)
+template <typename K>
+hipError_t seg_sort(void *tmp, size_t &tb, const K *k0, K *k1, const int32_t *v0, int32_t *v1, int n, int nseg,
+                    const int32_t *beg, const int32_t *end, hipStream_t st)
 {
     return rocprim::segmented_radix_sort_pairs<SegSortConfig>(tmp, tb, k0, k1, v0, v1, (unsigned)n, (unsigned)nseg,
-                                                              seg, seg + 1, 0u, 64u, st);
+                                                              beg, end, 0u, 8u * (unsigned)sizeof(K), st);
 }
 
-size_t walk_smem(int nwmax) { return 4 * (2 * kWalkThreads + 16) + 12 * (size_t)nwmax + 8 * kWalkThreads + 64; }
+size_t walk_smem(int nwmax, int lt) { return 4 * (2 * (size_t)lt + 16) + 12 * (size_t)nwmax + 8 * (size_t)lt + 64; }
 
 }  // namespace
 
@@ -512,7 +597,13 @@ static int plan_slide(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
 int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jobs_in, int32_t w)
 {
     mp->w = w;
-    mp->lc = kWalkThreads;
+    // outputs per walk chunk (64 / 128 / 256 / 512): per output, the chunk's bitmap
+    // setup costs ~(w + L) / L and the walk ~L zone entries; 128 measured fastest at w = 6000
+    const char *lenv = getenv("COMAP_MEDIAN_L");
+    mp->lc = lenv ? atoi(lenv) : 128;
+    if (mp->lc != 64 && mp->lc != 256 && mp->lc != 512) mp->lc = 128;
+    const char *k32 = getenv("COMAP_MEDIAN_KEY32");           // 0: sort the full u64 keys directly
+    mp->key32 = !(k32 && !strcmp(k32, "0"));
     if (w < 1 || w > kMaxWindow) return comap_fail(ctx, -1, "median window must be 1 <= w <= 32768");
     const char *force = getenv("COMAP_MEDIAN_PATH");         // "sort" / "slide": test both paths
     const int mcap = w + kSlideL - 1;
@@ -525,20 +616,20 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
     // segment, so a plan of few long series (a C3 shard: ~100 of 16k outputs) would
     // leave most CUs idle; each extra segment re-sorts w - 1 values.
     const char *ms = getenv("COMAP_MEDIAN_MINSEGS");
-    const int64_t kMinSegs = ms ? atoll(ms) : 512;
+    const int64_t kMinSegs = ms ? atoll(ms) : 0;   // measured: splitting costs more than it fills (off)
     int64_t total_out = 0;
     for (const MedJob &j : jobs_in) total_out += std::max<int64_t>(0, j.out_hi - j.out_lo);
     int64_t max_out = kMaxOut;
     if (kMinSegs > 0 && total_out > 0) {
         const int64_t want = (total_out + kMinSegs - 1) / kMinSegs;
         max_out = std::min<int64_t>(kMaxOut, std::max<int64_t>(4 * (int64_t)kWalkThreads,
-                                                               (want + kWalkThreads - 1) / kWalkThreads * kWalkThreads));
+                                                               (want + mp->lc - 1) / mp->lc * mp->lc));
     }
     std::vector<MedJob> jobs;
     for (const MedJob &j : jobs_in) {
         if (j.out_hi - j.out_lo <= max_out) { jobs.push_back(j); continue; }
         const int64_t nsub = (j.out_hi - j.out_lo + max_out - 1) / max_out;
-        const int64_t len = ((j.out_hi - j.out_lo + nsub - 1) / nsub + kWalkThreads - 1) / kWalkThreads * kWalkThreads;
+        const int64_t len = ((j.out_hi - j.out_lo + nsub - 1) / nsub + mp->lc - 1) / mp->lc * mp->lc;
         for (int64_t lo = j.out_lo; lo < j.out_hi; lo += len) {
             MedJob sj = j;
             sj.out_lo = lo;
@@ -575,25 +666,31 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
     COMAP_CHECK(ctx, alloc((void **)&mp->v0, 4 * (size_t)mp->nitems));
     COMAP_CHECK(ctx, alloc((void **)&mp->v1, 4 * (size_t)mp->nitems));
     COMAP_CHECK(ctx, alloc((void **)&mp->rank, 4 * (size_t)mp->nitems));
+    COMAP_CHECK(ctx, alloc((void **)&mp->redo, 4 * 3 * jobs.size()));   // flags | begin | end
     COMAP_CHECK(ctx, hipMemcpyAsync(mp->jobs, jobs.data(), sizeof(MedJob) * jobs.size(), hipMemcpyHostToDevice, st));
     COMAP_CHECK(ctx, hipMemcpyAsync(mp->seg, seg.data(), 4 * seg.size(), hipMemcpyHostToDevice, st));
     if (!chunks.empty())
         COMAP_CHECK(ctx, hipMemcpyAsync(mp->chunks, chunks.data(), 8 * chunks.size(), hipMemcpyHostToDevice, st));
-    size_t tb = 0;
-    COMAP_CHECK(ctx, seg_sort(nullptr, tb, mp->k0, mp->k1, mp->v0, mp->v1, (int)mp->nitems, mp->njobs, mp->seg, st));
+    size_t tb = 0, tb32 = 0;
+    COMAP_CHECK(ctx, seg_sort(nullptr, tb, mp->k0, mp->k1, mp->v0, mp->v1, (int)mp->nitems, mp->njobs, mp->seg,
+                              mp->seg + 1, st));
+    COMAP_CHECK(ctx, seg_sort(nullptr, tb32, (const uint32_t *)mp->k0, (uint32_t *)mp->k1, mp->v0, mp->v1,
+                              (int)mp->nitems, mp->njobs, mp->seg, mp->seg + 1, st));
+    tb = std::max(tb, tb32);
     mp->temp_bytes = tb;
     COMAP_CHECK(ctx, alloc(&mp->temp, tb));
-    const size_t sm = walk_smem(mp->nwmax);
+    const size_t sm = walk_smem(mp->nwmax, mp->lc);
     if (sm > 160 * 1024) return comap_fail(ctx, -1, "median plan: LDS budget exceeded");
-    COMAP_CHECK(ctx, hipFuncSetAttribute((const void *)k_med_walk, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)sm));
+    const void *wk = mp->lc == 64 ? (const void *)k_med_walk<64> : mp->lc == 128 ? (const void *)k_med_walk<128>
+                   : mp->lc == 512 ? (const void *)k_med_walk<512> : (const void *)k_med_walk<256>;
+    COMAP_CHECK(ctx, hipFuncSetAttribute(wk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
     COMAP_CHECK(ctx, hipStreamSynchronize(st));   // host vectors go out of scope
     return 0;
 }
 
 void comap_median_plan_free(MedPlan *mp)
 {
-    void *b[] = {mp->jobs, mp->seg, mp->chunks, mp->k0, mp->k1, mp->v0, mp->v1, mp->rank, mp->temp, mp->segs};
+    void *b[] = {mp->jobs, mp->seg, mp->chunks, mp->k0, mp->k1, mp->v0, mp->v1, mp->rank, mp->temp, mp->segs, mp->redo};
     for (void *p : b)
         if (p) (void)hipFree(p);
     *mp = MedPlan();
@@ -615,15 +712,38 @@ int comap_median_run(comap_ctx *ctx, MedPlan *mp, hipStream_t st)
     }
     if (mp->nchunks == 0) return 0;
     dim3 g1(64, (unsigned)mp->njobs);
-    k_med_keys<<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, mp->k0, mp->v0);
-    COMAP_LAUNCH_CHECK(ctx);
     size_t tb = mp->temp_bytes;
-    COMAP_CHECK(ctx, seg_sort(mp->temp, tb, mp->k0, mp->k1, mp->v0, mp->v1, (int)mp->nitems, mp->njobs, mp->seg, st));
+    if (mp->key32) {
+        uint32_t *k0 = (uint32_t *)mp->k0, *k1 = (uint32_t *)mp->k1;
+        int32_t *flag = mp->redo, *beg = mp->redo + mp->njobs, *end = beg + mp->njobs;
+        k_med_keys<uint32_t><<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, k0, mp->v0);
+        COMAP_LAUNCH_CHECK(ctx);
+        COMAP_CHECK(ctx, seg_sort(mp->temp, tb, (const uint32_t *)k0, k1, mp->v0, mp->v1, (int)mp->nitems, mp->njobs,
+                                  mp->seg, mp->seg + 1, st));
+        COMAP_CHECK(ctx, hipMemsetAsync(flag, 0, 4 * (size_t)mp->njobs, st));
+        k_med_fix<<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, k1, mp->v1, flag);
+        COMAP_LAUNCH_CHECK(ctx);
+        // the flagged segments (if any) again on exact 64-bit keys; the rest are empty ranges
+        k_med_redo<<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, flag, mp->k0, mp->v0, beg, end);
+        COMAP_LAUNCH_CHECK(ctx);
+        tb = mp->temp_bytes;
+        COMAP_CHECK(ctx, seg_sort(mp->temp, tb, (const uint64_t *)mp->k0, mp->k1, mp->v0, mp->v1, (int)mp->nitems,
+                                  mp->njobs, beg, end, st));
+    } else {
+        k_med_keys<uint64_t><<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, mp->k0, mp->v0);
+        COMAP_LAUNCH_CHECK(ctx);
+        COMAP_CHECK(ctx, seg_sort(mp->temp, tb, (const uint64_t *)mp->k0, mp->k1, mp->v0, mp->v1, (int)mp->nitems,
+                                  mp->njobs, mp->seg, mp->seg + 1, st));
+    }
     k_med_rank<<<g1, 256, 0, st>>>(mp->seg, mp->njobs, mp->v1, mp->rank);
     COMAP_LAUNCH_CHECK(ctx);
-    k_med_walk<<<mp->nchunks, kWalkThreads, walk_smem(mp->nwmax), st>>>(mp->jobs, mp->chunks, mp->seg, mp->k1,
-                                                                         mp->v1, mp->rank, mp->w, mp->lc,
-                                                                         mp->nwmax);
+    const size_t sm = walk_smem(mp->nwmax, mp->lc);
+    switch (mp->lc) {
+    case 64: k_med_walk<64><<<mp->nchunks, 64, sm, st>>>(mp->jobs, mp->chunks, mp->seg, mp->v1, mp->rank, mp->w, mp->nwmax); break;
+    case 128: k_med_walk<128><<<mp->nchunks, 128, sm, st>>>(mp->jobs, mp->chunks, mp->seg, mp->v1, mp->rank, mp->w, mp->nwmax); break;
+    case 512: k_med_walk<512><<<mp->nchunks, 512, sm, st>>>(mp->jobs, mp->chunks, mp->seg, mp->v1, mp->rank, mp->w, mp->nwmax); break;
+    default: k_med_walk<256><<<mp->nchunks, 256, sm, st>>>(mp->jobs, mp->chunks, mp->seg, mp->v1, mp->rank, mp->w, mp->nwmax); break;
+    }
     COMAP_LAUNCH_CHECK(ctx);
     return 0;
 }

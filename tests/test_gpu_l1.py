@@ -77,6 +77,32 @@ def test_medfilt_long_series_split(path, monkeypatch):
     assert np.array_equal(got, oracle.medfilt(z, 400)[y.size:2 * y.size])
 
 
+@pytest.mark.parametrize('key32,lc', [('1', '128'), ('0', '128'), ('1', '64'), ('1', '256'), ('1', '512')])
+def test_medfilt_sort_proxy_runs(key32, lc, monkeypatch):
+    """Global-sort path with 32-bit proxy keys: values that round to the same
+    f32 but differ in f64 (short runs: fixed in place; runs > 32: the segment is
+    re-sorted on u64 keys), signed zeros and negative values; u64-key path and
+    the 64/256/512-output walk chunks for comparison."""
+    monkeypatch.setenv('COMAP_MEDIAN_PATH', 'sort')
+    monkeypatch.setenv('COMAP_MEDIAN_KEY32', key32)
+    monkeypatch.setenv('COMAP_MEDIAN_L', lc)
+    from comapreduce_amd.tools.medfilt import medfilt, medfilt_batch
+    rng = np.random.default_rng(12)
+    n = 20000
+    eps = rng.integers(0, 5, n) * 1e-13
+    short = np.round(rng.standard_normal(n), 4) + eps            # runs of ~1-3 equal proxies
+    long_ = np.round(rng.standard_normal(n), 1) + eps            # runs of hundreds -> segment re-sort
+    flat = 1.0 + rng.integers(0, 40, n) * 2.0 ** -45              # one proxy for the whole series
+    zeros = np.where(rng.random(n) < 0.5, 0.0, -0.0) * (rng.random(n) < 0.9) + (rng.random(n) < 0.1) * -1e-300
+    for x, w in ((short, 6000), (long_, 6000), (flat, 401), (zeros, 400), (short[:7000], 7000)):
+        assert np.array_equal(medfilt(x.copy(), w), oracle.medfilt(x.copy(), w)), (w, x[:3])
+    series = [short, long_[:9000], flat[:6500]]
+    got = medfilt_batch(series, 6000, reflect=True)
+    for s, g in zip(series, got):
+        z = np.concatenate((s[::-1], s, s[::-1]))
+        assert np.array_equal(g, oracle.medfilt(z, 6000)[s.size:2 * s.size])
+
+
 def test_binvalues_dropin_bit_exact(golden_dir):
     from comapreduce_amd.tools.binfuncs import binValues
     b = np.load(os.path.join(golden_dir, 'golden_binvalues.npz'))
