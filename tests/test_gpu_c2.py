@@ -95,3 +95,114 @@ def test_c2_units_vs_oracle(c2, f, which):
     assert relmax(h['averaged_tod/tod'][f, :, t0:t1], r) < RTOL
     assert relmax(h['averaged_tod/tod_original'][f, :, t0:t1], o) < RTOL
     assert relmax(h['averaged_tod/weights'][f, :, t0:t1], np.broadcast_to(w[:, None], (4, t1 - t0))) < RTOL
+
+
+# ---------------------------------------------------------------- C4 / C5 destriper parity
+def rel(a, b):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    return np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300)
+
+
+@pytest.fixture(scope='module')
+def c4(c2):
+    """C4 inputs: COMAPData.read_comap_data (band 0, 19 feeds, L = 50, 480x480 CAR) on
+    the C2 observation's Level-2 output -- the device-median prep the bench times."""
+    import bench
+    from comapreduce_amd.mapmaking import comapdata as CD
+    data, _, h = c2
+    store = bench.level2_store(h, data, obsid=1)
+    res = CD.read_comap_data(list(store), bench.c4_map_info(), iband=0, offset_length=50, store=store, device=0)
+    return store, res
+
+
+def test_c4_prep_device_median_matches_checker(c4, monkeypatch):
+    """The C4 prep with the device w = 400 median == the same prep with the oracle's
+    medianFilter.cpp restatement (COMAPData.py:471-577), every output bit for bit."""
+    import bench
+    import oracle
+    from comapreduce_amd.mapmaking import comapdata as CD
+    from comapreduce_amd.tools import medfilt as mf
+    store, dev = c4
+
+    def checker(series, w, reflect=False, device=None):
+        out = []
+        for s in series:
+            z = np.concatenate((s[::-1], s, s[::-1])) if reflect else s.copy()
+            y = oracle.medfilt(z.astype(np.float64), int(w))
+            out.append(y[s.size:2 * s.size] if reflect else y)
+        return out
+    monkeypatch.setattr(mf, 'medfilt_batch', checker)
+    host = CD.read_comap_data(list(store), bench.c4_map_info(), iband=0, offset_length=50, store=store)
+    # 19 feeds x ~178k scan samples, ~half kept after the reference's az/el percentile, scan-edge and
+    # empty-offset cuts (COMAPData.py:330-360, 550-568)
+    assert dev[0].size > 1_500_000 and dev[0].size % 50 == 0
+    for a, b in zip(dev, host):
+        assert np.array_equal(np.asarray(a), np.asarray(b))
+
+
+def test_c4_destriper_vs_oracle(c4):
+    """C4 solve (threshold 0, 20 CG iterations) against oracle/destriper.py
+    (Destriper.py:155-263, 402-453): weight / hits / naive bit-exact, offsets and
+    map <= 1e-5 relative (north_star)."""
+    import oracle.destriper as od
+    from comapreduce_amd.mapmaking.destriper import DeviceDestriper
+    _, (tod, w, pix) = c4[0], c4[1][:3]
+    npix = 480 * 480
+    res = DeviceDestriper(pix, tod, w, 50, npix, device=0).solve(threshold=0.0, niter=20)
+    ref, xr, itr = od.destriper_iteration(np.asarray(pix, np.int64), tod, w, 50, npix, threshold=0.0, niter=20)
+    assert res['iters'] == itr == 20
+    m = {k: v.cpu().numpy() for k, v in res['maps'].items()}
+    for k in ('weight', 'hits', 'naive'):
+        assert np.array_equal(m[k], ref[k]), k
+    assert rel(m['map'], ref['map']) < 1e-5
+    assert rel(res['x'].cpu().numpy(), xr) < 1e-5
+
+
+def test_c4_four_bands_batched_vs_oracle(c4):
+    """All 4 sidebands of C4 (read_comap_data_bands -> one batched solve) == each band
+    prepared and solved alone by the oracle path (its own kept offsets)."""
+    import bench
+    import oracle.destriper as od
+    from comapreduce_amd.mapmaking import comapdata as CD
+    from comapreduce_amd.mapmaking.destriper import DeviceDestriper
+    store = c4[0]
+    npix, niter = 480 * 480, 8
+    r = CD.read_comap_data_bands(list(store), bench.c4_map_info(), bands=(0, 1, 2, 3), offset_length=50,
+                                 store=store, device=0)
+    res = DeviceDestriper(r['pointing'], r['tod'], r['weights'], 50, npix, device=0, keep=r['keep']).solve(0.0, niter)
+    for b in range(4):
+        tb, wb, pb = CD.read_comap_data(list(store), bench.c4_map_info(), iband=b, offset_length=50, store=store,
+                                        device=0)[:3]
+        ref, xr, itr = od.destriper_iteration(np.asarray(pb, np.int64), tb, wb, 50, npix, threshold=0.0, niter=niter)
+        assert res['iters'][b] == itr
+        m = {k: v[b].cpu().numpy() for k, v in res['maps'].items()}
+        for k in ('weight', 'hits', 'naive'):
+            assert np.array_equal(m[k], ref[k]), (b, k)
+        assert rel(m['map'], ref['map']) < 1e-5, b
+        x = res['x'][b].cpu().numpy()
+        assert rel(x[r['keep'][b].astype(bool)], xr) < 1e-5, b
+
+
+def test_c5_two_observations_two_bands_vs_oracle():
+    """Reduced C5: 2 observations x 19 feeds x 180,000 samples (6.8 M samples, 137k
+    offsets, 480x480 CAR), 2 sidebands batched, 12 CG iterations, against the oracle
+    per band."""
+    import torch
+    import oracle.destriper as od
+    from comapreduce_amd import synthetic
+    from comapreduce_amd.mapmaking.destriper import DeviceDestriper
+    L, npix, niter = 50, 480 * 480, 12
+    pix, tod, w = synthetic.destriper_inputs_device(2, offset_length=L, device=0, seed=1000, n_bands=2)
+    res = DeviceDestriper(pix, tod, w, L, npix, device=0).solve(threshold=0.0, niter=niter)
+    p, t, ww = pix.cpu().numpy().astype(np.int64), tod.cpu().numpy(), w.cpu().numpy()
+    del pix, tod, w
+    torch.cuda.empty_cache()
+    assert p.size == 2 * 19 * 180_000
+    for b in range(2):
+        ref, xr, itr = od.destriper_iteration(p, t[b], ww[b], L, npix, threshold=0.0, niter=niter)
+        assert res['iters'][b] == itr == niter
+        m = {k: v[b].cpu().numpy() for k, v in res['maps'].items()}
+        for k in ('weight', 'hits', 'naive'):
+            assert np.array_equal(m[k], ref[k]), (b, k)
+        assert rel(m['map'], ref['map']) < 1e-5, b
+        assert rel(res['x'][b].cpu().numpy(), xr) < 1e-5, b
