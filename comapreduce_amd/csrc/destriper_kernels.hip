@@ -81,7 +81,8 @@ struct comap_destriper {
 namespace {
 
 constexpr int kRedBlocks = 256;   // dot-product grids (k_dot_part)
-constexpr int kUpdBlocks = 1024;  // CG update grid: its r.r partials are re-summed by every direction block
+constexpr int kUpdBlocks = 1024;  // CG update grid cap: its r.r partials are re-summed by every direction block
+constexpr int kProjBlocks = 1024; // k_ds_project grid cap: its p.q partials are re-summed by every update block
 constexpr int kDirBlocks = 1024;  // CG direction grid cap
 constexpr int kPartMax = 8192;     // >= every reduction grid below
 constexpr int kBinU = 4;           // entry loads in flight per lane (k_ds_bin)
@@ -179,6 +180,44 @@ __device__ __forceinline__ double block_final_sum(const double *__restrict__ par
     return (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// block_final_sum for NB bands at once (band b's partials at part + b kPartMax): the
+// same per-band order and result, with every band's loads in flight together.
+// red: 4 NB doubles.
+template <int NB>
+__device__ __forceinline__ void block_final_sums(const double *__restrict__ part, int n, double *red, double (&out)[NB])
+{
+    double acc[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[b] = 0.0;
+    constexpr int kB = 4;
+    int i = threadIdx.x;
+    for (; i + (kB - 1) * 256 < n; i += kB * 256) {
+        double v[NB][kB];
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+#pragma unroll
+            for (int k = 0; k < kB; ++k) v[b][k] = part[(int64_t)b * kPartMax + i + k * 256];
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+#pragma unroll
+            for (int k = 0; k < kB; ++k) acc[b] += v[b][k];
+    }
+    for (; i < n; i += 256) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[b] += part[(int64_t)b * kPartMax + i];
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[b] = wave_sum(acc[b]);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) red[4 * b + (threadIdx.x >> 6)] = acc[b];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < NB; ++b) out[b] = (red[4 * b] + red[4 * b + 1]) + (red[4 * b + 2] + red[4 * b + 3]);
+}
+
 // Block partial (4 waves) of a per-thread accumulator; thread 0 writes *out.
 __device__ __forceinline__ void block_partial(double acc, double *red, double *out)
 {
@@ -187,6 +226,26 @@ __device__ __forceinline__ void block_partial(double acc, double *red, double *o
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
     __syncthreads();
     if (threadIdx.x == 0) *out = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// block_partial of NB accumulators with one pair of barriers; band b's partial goes to
+// part[b kPartMax] (same value as block_partial per band).  red: 4 NB doubles.
+template <int NB>
+__device__ __forceinline__ void block_partials(double (&acc)[NB], double *red, double *part)
+{
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[b] = wave_sum(acc[b]);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) red[4 * b + (threadIdx.x >> 6)] = acc[b];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+            part[(int64_t)b * kPartMax] = (red[4 * b] + red[4 * b + 1]) + (red[4 * b + 2] + red[4 * b + 3]);
+    }
 }
 
 // One wave per offset: lane l owns samples l, l + 64, ... (K per lane, L <= 64 K).
@@ -525,7 +584,7 @@ __global__ void __launch_bounds__(256) k_ds_project(const int64_t *__restrict__ 
                                                     int64_t NO, int64_t npix, double *__restrict__ y,
                                                     double *__restrict__ dot_part, const int32_t *__restrict__ flags)
 {
-    __shared__ double red[4];
+    __shared__ double red[4 * NB];
     if (cg_done(flags)) return;
     constexpr int kPer = 256 / G;
     const int sub = threadIdx.x & (G - 1);
@@ -599,8 +658,7 @@ __global__ void __launch_bounds__(256) k_ds_project(const int64_t *__restrict__ 
         }
     }
     if (dot_part) {
-#pragma unroll
-        for (int b = 0; b < NB; ++b) block_partial(acc[b], red, dot_part + (int64_t)b * kPartMax + blockIdx.x);
+        block_partials<NB>(acc, red, dot_part + blockIdx.x);
     }
 }
 
@@ -609,7 +667,7 @@ template <int NB>
 __global__ void __launch_bounds__(256) k_dot_part(const double *__restrict__ a, const double *__restrict__ c, int64_t n,
                                                   double *__restrict__ part)
 {
-    __shared__ double red[4];
+    __shared__ double red[4 * NB];
     double acc[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) acc[b] = 0.0;
@@ -620,8 +678,7 @@ __global__ void __launch_bounds__(256) k_dot_part(const double *__restrict__ a, 
 #pragma unroll
         for (int b = 0; b < NB; ++b) acc[b] = fma(av[b], cv[b], acc[b]);
     }
-#pragma unroll
-    for (int b = 0; b < NB; ++b) block_partial(acc[b], red, part + (int64_t)b * kPartMax + blockIdx.x);
+    block_partials<NB>(acc, red, part + blockIdx.x);
 }
 
 // out[b] = fixed-order sum of band b's n partials
@@ -683,7 +740,7 @@ __global__ void __launch_bounds__(256) k_cg_update(const double *__restrict__ rr
                                                    const double *__restrict__ p, const double *__restrict__ q,
                                                    int64_t n, double *__restrict__ part, const int32_t *__restrict__ flags)
 {
-    __shared__ double red[4];
+    __shared__ double red[4 * NB];
     if (cg_done(flags)) return;
     double a[NB], acc[NB];
     bool live[NB];
@@ -691,14 +748,13 @@ __global__ void __launch_bounds__(256) k_cg_update(const double *__restrict__ rr
     for (int b = 0; b < NB; ++b) { a[b] = rr[b] / pq[b]; live[b] = !band_stopped(flags, b); acc[b] = 0.0; }
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         update_row<NB>(x + i * NB, r + i * NB, p + i * NB, q + i * NB, a, live, acc);
-#pragma unroll
-    for (int b = 0; b < NB; ++b) block_partial(acc[b], red, part + (int64_t)b * kPartMax + blockIdx.x);
+    block_partials<NB>(acc, red, part + blockIdx.x);
 }
 
 // End-of-iteration bookkeeping (Destriper.py:136-152) by one thread, per band still
 // running: rr = rr_new, count it, stop when delta = rr_new / rr0 is NaN or below the
 // threshold; flags[1] counts iterations any band ran, flags[0] = every band stopped.
-template <int NB>
+template <int NB, bool kSetRr = true>
 __device__ __forceinline__ void cg_check(double *__restrict__ scal, int32_t *__restrict__ flags, const double *rrn)
 {
     bool any = false, all = true;
@@ -706,7 +762,7 @@ __device__ __forceinline__ void cg_check(double *__restrict__ scal, int32_t *__r
     for (int b = 0; b < NB; ++b) {
         if (!flags[2 + b]) {
             any = true;
-            scal[NB + b] = rrn[b];
+            if (kSetRr) scal[NB + b] = rrn[b];   // the per-piece update reads rr there
             scal[3 * NB + b] = rrn[b];
             flags[2 + NB + b] += 1;
             const double delta = rrn[b] / scal[b];
@@ -734,13 +790,13 @@ __global__ void __launch_bounds__(256) k_cg_update_fused(double *__restrict__ sc
                                                          int64_t n, double *__restrict__ part_rr,
                                                          const int32_t *__restrict__ flags)
 {
-    __shared__ double red[4];
+    __shared__ double red[4 * NB];
     if (cg_done(flags)) return;
     double pq[NB], rr[NB], a[NB], acc[NB];
     bool live[NB];
+    block_final_sums<NB>(part_pq, npq, red, pq);
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-        pq[b] = block_final_sum(part_pq + (int64_t)b * kPartMax, npq, red);
         rr[b] = scal[3 * NB + b];
         a[b] = rr[b] / pq[b];
         live[b] = !band_stopped(flags, b);
@@ -748,8 +804,7 @@ __global__ void __launch_bounds__(256) k_cg_update_fused(double *__restrict__ sc
     }
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         update_row<NB>(x + i * NB, r + i * NB, p + i * NB, q + i * NB, a, live, acc);
-#pragma unroll
-    for (int b = 0; b < NB; ++b) block_partial(acc[b], red, part_rr + (int64_t)b * kPartMax + blockIdx.x);
+    block_partials<NB>(acc, red, part_rr + blockIdx.x);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
 #pragma unroll
         for (int b = 0; b < NB; ++b)
@@ -762,20 +817,22 @@ __global__ void __launch_bounds__(256) k_cg_direction_fused(double *__restrict__
                                                             int nrr, double *__restrict__ p, const double *__restrict__ r,
                                                             int64_t n, int32_t *flags)
 {
-    __shared__ double red[4];
+    __shared__ double red[4 * NB];
     if (flags[0]) return;
     double rrn[NB], beta[NB];
     bool live[NB];
+    block_final_sums<NB>(part_rr, nrr, red, rrn);
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-        rrn[b] = block_final_sum(part_rr + (int64_t)b * kPartMax, nrr, red);
         beta[b] = rrn[b] / scal[NB + b];
         live[b] = !flags[2 + b];
     }
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         direction_row<NB>(p + i * NB, r + i * NB, beta, live);
-    // block 0 only, after its own sweep: a band that stops here never reads p again
-    if (blockIdx.x == 0 && threadIdx.x == 0) cg_check<NB>(scal, flags, rrn);
+    // block 0 only, after its own sweep: a band that stops here never reads p again.
+    // scal[NB+b] is left alone -- other blocks may still be reading it for beta; the
+    // fused update takes rr from scal[3NB+b] and rewrites scal[NB+b] itself.
+    if (blockIdx.x == 0 && threadIdx.x == 0) cg_check<NB, false>(scal, flags, rrn);
 }
 
 // p = r + (rr_new / rr) p per band still running
@@ -810,6 +867,9 @@ __global__ void k_div_map(const double *__restrict__ num, const double *__restri
 }
 
 inline unsigned grid_for(int64_t n, int64_t cap = 4096) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, cap)); }
+// CG update grid: one offset row per thread up to kUpdBlocks blocks (the fused and the
+// per-piece paths use the same grid, hence the same r.r partials)
+inline unsigned upd_grid(int64_t NO) { return grid_for(NO, kUpdBlocks); }
 
 // every templated launch dispatches on the problem's band count (1, 2 or 4)
 #define COMAP_NB_SWITCH(nb, ...)                                 \
@@ -851,7 +911,7 @@ inline int project_lanes(int L) { return L <= 64 ? 16 : (L <= 128 ? 32 : 64); }
 inline unsigned project_grid(int64_t NO, int L)
 {
     const int64_t per = 256 / project_lanes(L);
-    return (unsigned)std::max<int64_t>(1, std::min<int64_t>((NO + per - 1) / per, kPartMax));
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>((NO + per - 1) / per, kProjBlocks));
 }
 
 // k_ds_project with the lane group sized to the offset length; returns its grid (= partials).
@@ -1134,9 +1194,9 @@ extern "C" int comap_destripe_cg_update(comap_destriper *d, const double *rr, co
     if (!d) return -1;
     COMAP_DEVICE_GUARD(d->ctx);
     comap_ctx *ctx = d->ctx;
-    COMAP_NB_SWITCH(d->nb, k_cg_update<NB><<<kUpdBlocks, 256, 0, ctx->stream>>>(rr, pq, x, r, p, q, d->NO, d->part,
+    COMAP_NB_SWITCH(d->nb, k_cg_update<NB><<<upd_grid(d->NO), 256, 0, ctx->stream>>>(rr, pq, x, r, p, q, d->NO, d->part,
                                                                                  nullptr);
-                    k_dot_final<NB><<<1, 256, 0, ctx->stream>>>(d->part, kUpdBlocks, rr_new, nullptr));
+                    k_dot_final<NB><<<1, 256, 0, ctx->stream>>>(d->part, (int)upd_grid(d->NO), rr_new, nullptr));
     COMAP_LAUNCH_CHECK(ctx);
     return 0;
 }
@@ -1215,9 +1275,9 @@ extern "C" int comap_destripe_dist_update(comap_destriper *d, double *scal, doub
     COMAP_DEVICE_GUARD(d->ctx);
     comap_ctx *ctx = d->ctx;
     const int nb = d->nb;
-    COMAP_NB_SWITCH(nb, k_cg_update<NB><<<kUpdBlocks, 256, 0, ctx->stream>>>(scal + nb, scal + 2 * nb, x, r, p, q,
+    COMAP_NB_SWITCH(nb, k_cg_update<NB><<<upd_grid(d->NO), 256, 0, ctx->stream>>>(scal + nb, scal + 2 * nb, x, r, p, q,
                                                                               d->NO, d->part, flags);
-                    k_dot_final<NB><<<1, 256, 0, ctx->stream>>>(d->part, kUpdBlocks, scal + 3 * nb, flags));
+                    k_dot_final<NB><<<1, 256, 0, ctx->stream>>>(d->part, (int)upd_grid(d->NO), scal + 3 * nb, flags));
     COMAP_LAUNCH_CHECK(ctx);
     return 0;
 }
@@ -1251,11 +1311,11 @@ static void enqueue_iteration(comap_destriper *d, hipStream_t st)
     const unsigned pg = launch_project(d, st, p, num, nullptr, q, d->part, flags);
     double *part_rr = d->part + (size_t)d->nb * kPartMax;
     COMAP_NB_SWITCH(d->nb,
-                    k_cg_update_fused<NB><<<kUpdBlocks, 256, 0, st>>>(d->scal, d->part, (int)pg, x, r, p, q, d->NO,
-                                                                      part_rr, flags);
+                    k_cg_update_fused<NB><<<upd_grid(d->NO), 256, 0, st>>>(d->scal, d->part, (int)pg, x, r, p, q,
+                                                                           d->NO, part_rr, flags);
                     k_cg_direction_fused<NB><<<grid_for(d->NO, kDirBlocks), 256, 0, st>>>(d->scal, part_rr,
-                                                                                          kUpdBlocks, p, r, d->NO,
-                                                                                          d->flags));
+                                                                                          (int)upd_grid(d->NO), p, r,
+                                                                                          d->NO, d->flags));
 }
 
 // CG state, stream and the kCgBatch-iteration graph, created on first use.

@@ -118,9 +118,39 @@ __global__ void __launch_bounds__(256) k_med_fix(const MedJob *__restrict__ jobs
         if (e - i > kFixRun) { redo[jb] = 1; continue; }
         const MedJob job = jobs[jb];
         const int64_t base = job.out_lo - h;
+        const int n = e - i;
+        auto before = [](uint64_t ka, int32_t pa, uint64_t kb, int32_t pb) { return ka < kb || (ka == kb && pa < pb); };
+        if (n <= 8) {
+            // the common case: a register-resident odd-even transposition sort (padded to 8)
+            uint64_t kk[8];
+            int32_t pp[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                if (t < n) {
+                    pp[t] = svals[s0 + i + t];
+                    kk[t] = key_of(xprime(job, base + pp[t], h));
+                } else {
+                    kk[t] = ~0ull;
+                    pp[t] = 0x7fffffff;
+                }
+            }
+#pragma unroll
+            for (int rnd = 0; rnd < 8; ++rnd) {
+#pragma unroll
+                for (int t = rnd & 1; t + 1 < 8; t += 2) {
+                    if (before(kk[t + 1], pp[t + 1], kk[t], pp[t])) {
+                        const uint64_t tk = kk[t]; kk[t] = kk[t + 1]; kk[t + 1] = tk;
+                        const int32_t tp = pp[t]; pp[t] = pp[t + 1]; pp[t + 1] = tp;
+                    }
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+                if (t < n) svals[s0 + i + t] = pp[t];
+            continue;
+        }
         uint64_t rk[kFixRun];
         int32_t rp[kFixRun];
-        const int n = e - i;
         for (int t = 0; t < n; ++t) {
             const int32_t p = svals[s0 + i + t];
             const uint64_t kk = key_of(xprime(job, base + p, h));

@@ -18,13 +18,16 @@ import re
 import shutil
 import sys
 
-KERNEL_RE = re.compile(r'\bk_(\w+)\s*(?:\(|$)')
+KERNEL_RE = re.compile(r'\bk_(\w+)\s*(<[^()]*>)?\s*(?:\(|$)')
 
 
 def short(name):
-    """'k_regress_avg(float const*, ...)' -> 'regress_avg' (the bench's kernel key)."""
+    """'k_regress_avg(float const*, ...)' -> 'regress_avg' (the bench's kernel key);
+    templates keep their arguments: 'k_ds_project<16, 4>(...)' -> 'ds_project<16,4>'."""
     m = KERNEL_RE.search(name.strip())
-    return m.group(1) if m else None
+    if not m:
+        return None
+    return m.group(1) + (m.group(2).replace(' ', '') if m.group(2) else '')
 
 
 def counter_bytes(d, counter):
@@ -43,6 +46,7 @@ def counter_bytes(d, counter):
 
 def main():
     out, tag = sys.argv[1], sys.argv[2]
+    latest = '--no-latest' not in sys.argv[3:]
     here = os.path.join(out, 'summary')
     os.makedirs(here, exist_ok=True)
     stats = glob.glob(os.path.join(out, 'trace', '**', '*kernel_stats.csv'), recursive=True)
@@ -55,8 +59,9 @@ def main():
         traffic[k] = {'hbm_bytes_per_launch': (2 * fetch.get(k, 0.0) + write.get(k, 0.0)) * 1024,
                       'fetch_size_kb': fetch.get(k), 'write_size_kb': write.get(k)}
     json.dump(traffic, open(os.path.join(here, f'{tag}_traffic.json'), 'w'), indent=1)
-    json.dump({k: v['hbm_bytes_per_launch'] for k, v in traffic.items()},
-              open(os.path.join(here, 'traffic_latest.json'), 'w'), indent=1)
+    if latest:
+        json.dump({k: v['hbm_bytes_per_launch'] for k, v in traffic.items()},
+                  open(os.path.join(here, 'traffic_latest.json'), 'w'), indent=1)
     print(json.dumps(traffic, indent=1))
 
 
