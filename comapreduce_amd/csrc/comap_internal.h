@@ -110,10 +110,11 @@ struct SlideSeg {
 };
 
 // Sliding-median plan.  slide: k_med_slide over `segs` (windows up to ~12k);
-// otherwise the global-sort path (jobs, per-job sorted-key segments, chunk table, buffers).
+// otherwise the global-sort path (jobs, per-job sorted-key segments, k_med_walk
+// segments in `segs`, buffers).
 struct MedPlan {
     bool slide = false;
-    SlideSeg *segs = nullptr;    // dev [nsegs]
+    SlideSeg *segs = nullptr;    // dev [nsegs] k_med_slide or k_med_walk segments
     int32_t nsegs = 0;
     int32_t kper = 0;
     int32_t w = 0, lc = 0, nwmax = 0, njobs = 0;
@@ -121,12 +122,12 @@ struct MedPlan {
     int64_t nchunks = 0;
     MedJob *jobs = nullptr;      // dev [njobs]
     int32_t *seg = nullptr;      // dev [njobs+1] segment offsets
-    int64_t *chunks = nullptr;   // dev [nchunks][2] (job, i0)
     uint64_t *k0 = nullptr, *k1 = nullptr;
     int32_t *v0 = nullptr, *v1 = nullptr;
     int32_t *rank = nullptr;     // dev [nitems] position -> sorted index
     bool key32 = true;           // sort 32-bit proxies + exact run fix-up (else u64 keys)
     int32_t *redo = nullptr;     // dev [3][njobs]: segment re-sort flags, begin, end
+    void *krange = nullptr;      // dev [njobs][2] u64: per-series key min, max (proxy scaling)
     void *temp = nullptr;
     size_t temp_bytes = 0;
 };

@@ -6,20 +6,23 @@
 // a pure function of its multiset; even w averages s[w/2-1] and s[w/2] as
 // (hi + lo) / 2 in f64, the order Mediator::getMedian uses (Mediator.h:91-99).
 //
-// 1. k_med_keys: every series (job) contributes the Ns = n_out + w - 1 values
-//    its windows touch, as 32-bit order-preserving keys of the value rounded to
-//    f32 (a monotone map, so the f64 order only differs inside runs of equal
-//    proxies) + positions.
+// 1. k_med_range + k_med_keys: every series (job) contributes the Ns = n_out + w - 1
+//    values its windows touch, as 32-bit order-preserving proxies -- the value's u64
+//    key relative to the series' smallest, scaled so the series' key range spans 32
+//    bits (a monotone map, so the f64 order only differs inside runs of equal
+//    proxies, which need keys within range / 2^32 of each other) + positions.
 // 2. rocprim segmented radix sort (4 digit passes instead of 8); k_med_fix then
 //    re-sorts every run of equal proxies by the exact u64 key of the f64 value
 //    (runs are a few elements on real data).  A segment with a run longer than
 //    kFixRun is flagged and re-sorted whole on 64-bit keys (a second segmented
 //    sort over the flagged segments only -- the others are passed as empty).
 //    k_med_rank inverts the permutation (rank of every position).
-// 3. k_med_walk, one workgroup per chunk of L = 128 consecutive outputs:
+// 3. k_med_walk, one workgroup per segment of up to 4 chunks of L = 128 consecutive
+//    outputs, chunk by chunk:
 //    a. the chunk's union window U = positions [c, c+w+L-1) is marked in an
-//       LDS bitmap indexed by rank (coalesced reads of rank[]), together with
-//       its "zone" Z (offsets < L-1 or >= w: excluded by some output's window);
+//       LDS bitmap indexed by rank (built once per segment from coalesced reads
+//       of rank[], then slid: L positions leave and L enter per chunk), together
+//       with its "zone" Z (offsets < L-1 or >= w: excluded by some output's window);
 //       word popcount prefixes turn a rank into its index within U;
 //    b. the zone entries, in rank order, form the list E = (U index, offset);
 //    c. lane k walks E (4 entries per wave-uniform LDS read): from q = r, every
@@ -53,6 +56,18 @@ __device__ __forceinline__ double val_of(uint64_t k)
     return __longlong_as_double(b);
 }
 
+// index into j.src of the virtual series' element at pos (see xprime)
+__device__ __forceinline__ int64_t src_index(const MedJob &j, int64_t pos, int h)
+{
+    const int64_t n = j.n;
+    if (j.mode == 0) return pos < h ? 0 : (pos >= n ? n - 1 : pos);
+    if (pos < 0) pos = 0;
+    if (pos < n) return n - 1 - pos;
+    if (pos < 2 * n) return pos - n;
+    const int64_t q = 3 * n - 1 - pos;
+    return q < 0 ? 0 : q;
+}
+
 // virtual series x'(pos), pos relative to the start of the (virtual) series
 __device__ __forceinline__ double xprime(const MedJob &j, int64_t pos, int h)
 {
@@ -70,17 +85,53 @@ __device__ __forceinline__ double xprime(const MedJob &j, int64_t pos, int h)
     return j.src[q < 0 ? 0 : q];
 }
 
-// order-preserving 32-bit proxy: the key of the value rounded to f32 (monotone non-decreasing in v)
-__device__ __forceinline__ uint32_t key32_of(double v)
+// Per-series range of the u64 keys (kr[2j] = min, kr[2j+1] = max), one workgroup per series.
+__global__ void __launch_bounds__(256) k_med_range(const MedJob *__restrict__ jobs, const int32_t *__restrict__ seg,
+                                                   int32_t njobs, int32_t w, unsigned long long *__restrict__ kr)
 {
-    const uint32_t b = __float_as_uint((float)v);
-    return (b >> 31) ? ~b : (b | 0x80000000u);
+    __shared__ unsigned long long s_lo[4], s_hi[4];
+    const int jb = blockIdx.x;
+    if (jb >= njobs) return;
+    const MedJob job = jobs[jb];
+    const int32_t s0 = seg[jb], ns = seg[jb + 1] - s0;
+    const int h = w / 2;
+    const int64_t base = job.out_lo - h;
+    unsigned long long lo = ~0ull, hi = 0ull;
+    for (int i = threadIdx.x; i < ns; i += blockDim.x) {
+        const unsigned long long k = key_of(xprime(job, base + i, h));
+        lo = k < lo ? k : lo;
+        hi = k > hi ? k : hi;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long a = __shfl_xor(lo, o, 64), b = __shfl_xor(hi, o, 64);
+        lo = a < lo ? a : lo;
+        hi = b > hi ? b : hi;
+    }
+    if ((threadIdx.x & 63) == 0) { s_lo[threadIdx.x >> 6] = lo; s_hi[threadIdx.x >> 6] = hi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int v = 1; v < 4; ++v) {
+            lo = s_lo[v] < lo ? s_lo[v] : lo;
+            hi = s_hi[v] > hi ? s_hi[v] : hi;
+        }
+        kr[2 * jb] = lo;
+        kr[2 * jb + 1] = hi;
+    }
+}
+
+// Order-preserving 32-bit proxy of a u64 key: its offset from the series' smallest key,
+// scaled so the series' key range spans 32 bits (monotone non-decreasing in the key;
+// two values share a proxy only when their keys are within range / 2^32).
+__device__ __forceinline__ uint32_t key32_of(uint64_t k, uint64_t kmin, int shift)
+{
+    return (uint32_t)((k - kmin) >> shift);
 }
 
 template <typename K>
 __global__ void __launch_bounds__(256) k_med_keys(const MedJob *__restrict__ jobs, const int32_t *__restrict__ seg,
                                                   int32_t njobs, int32_t w, K *__restrict__ keys,
-                                                  int32_t *__restrict__ vals)
+                                                  int32_t *__restrict__ vals, const unsigned long long *__restrict__ kr)
 {
     const int jb = blockIdx.y;
     if (jb >= njobs) return;
@@ -88,10 +139,18 @@ __global__ void __launch_bounds__(256) k_med_keys(const MedJob *__restrict__ job
     const int32_t s0 = seg[jb], ns = seg[jb + 1] - s0;
     const int h = w / 2;
     const int64_t base = job.out_lo - h;
+    uint64_t kmin = 0;
+    int shift = 0;
+    if constexpr (sizeof(K) == 4) {
+        kmin = kr[2 * jb];
+        const uint64_t range = kr[2 * jb + 1] - kmin;
+        const int bits = range ? 64 - __clzll((long long)range) : 0;
+        shift = bits > 32 ? bits - 32 : 0;
+    }
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += gridDim.x * blockDim.x) {
-        const double v = xprime(job, base + i, h);
-        if constexpr (sizeof(K) == 4) keys[s0 + i] = key32_of(v);
-        else keys[s0 + i] = key_of(v);
+        const uint64_t k = key_of(xprime(job, base + i, h));
+        if constexpr (sizeof(K) == 4) keys[s0 + i] = key32_of(k, kmin, shift);
+        else keys[s0 + i] = k;
         vals[s0 + i] = i;
     }
 }
@@ -119,6 +178,14 @@ __global__ void __launch_bounds__(256) k_med_fix(const MedJob *__restrict__ jobs
         const MedJob job = jobs[jb];
         const int64_t base = job.out_lo - h;
         const int n = e - i;
+        // the common run: one source element seen at several positions (reflection
+        // padding, medfilt edges) -- equal values, already in position order (stable sort)
+        {
+            const int64_t si = src_index(job, base + svals[s0 + i], h);
+            bool same = true;
+            for (int t = 1; t < n && same; ++t) same = src_index(job, base + svals[s0 + i + t], h) == si;
+            if (same) continue;
+        }
         auto before = [](uint64_t ka, int32_t pa, uint64_t kb, int32_t pb) { return ka < kb || (ka == kb && pa < pb); };
         if (n <= 8) {
             // the common case: a register-resident odd-even transposition sort (padded to 8)
@@ -202,139 +269,168 @@ __global__ void __launch_bounds__(256) k_med_rank(const int32_t *__restrict__ se
         rank[s0 + svals[s0 + i]] = i;
 }
 
+// One workgroup per walk segment: S consecutive chunks of LT outputs of one job.  The
+// union-window bitmap U is built once for the segment's first chunk and then slid:
+// moving to the next chunk clears the LT positions that leave and sets the LT that
+// enter (3 LT rank reads per chunk instead of w + LT - 1).
 template <int LT>   // threads = outputs per chunk
-__global__ void __launch_bounds__(LT) k_med_walk(const MedJob *__restrict__ jobs, const int64_t *__restrict__ chunks,
+__global__ void __launch_bounds__(LT) k_med_walk(const MedJob *__restrict__ jobs, const SlideSeg *__restrict__ wsegs,
                                                  const int32_t *__restrict__ seg, const int32_t *__restrict__ svals,
                                                  const int32_t *__restrict__ rank, int32_t w, int32_t nwmax)
 {
-    constexpr int kWalkThreads = LT;
-    const int lc = LT;
     // LDS: E (16-B aligned for 4-entry reads) | U bitmap | Z bitmap | U word prefixes | scans
     extern __shared__ __align__(16) unsigned char smem[];
     uint32_t *E = reinterpret_cast<uint32_t *>(smem);
-    uint32_t *Ub = E + (2 * kWalkThreads + 16);
+    uint32_t *Ub = E + (2 * LT + 16);
     uint32_t *Zb = Ub + nwmax;
     int32_t *Up = reinterpret_cast<int32_t *>(Zb + nwmax);
     int *scanU = Up + nwmax;
-    int *scanZ = scanU + kWalkThreads;
+    int *scanZ = scanU + LT;
     __shared__ int s_ne;
 
     const int tid = threadIdx.x;
-    const int jb = (int)chunks[2 * blockIdx.x];
+    const int lane = tid & 63, wv = tid >> 6;
+    const SlideSeg sg = wsegs[blockIdx.x];
+    const int jb = sg.job;
     const MedJob job = jobs[jb];
     if (job.gate && *job.gate <= 0.0) return;
-    const int64_t i0 = chunks[2 * blockIdx.x + 1];
-    const int L = (int)min((int64_t)lc, job.out_hi - i0);
-    const int M = w + L - 1;
-    const int c0 = (int)(i0 - job.out_lo);          // chunk offset inside the series' position space
     const int32_t s0 = seg[jb], ns = seg[jb + 1] - s0;
     const int nw = (ns + 31) >> 5;
-
-    // ---- a. bitmaps of the union window and its zone, indexed by rank
-    for (int i = tid; i < nw; i += kWalkThreads) { Ub[i] = 0u; Zb[i] = 0u; }
-    __syncthreads();
-    for (int i = tid; i < M; i += kWalkThreads) {
-        const int r = rank[s0 + c0 + i];
-        const uint32_t bit = 1u << (r & 31);
-        atomicOr(&Ub[r >> 5], bit);
-        if ((i < L - 1) | (i >= w)) atomicOr(&Zb[r >> 5], bit);
-    }
-    __syncthreads();
-    // per-thread contiguous word ranges; prefix sums of set bits
-    const int wpt = (nw + kWalkThreads - 1) / kWalkThreads;
+    const int32_t *rk = rank + s0;                 // rank of series position p
+    const int32_t *sv = svals + s0;                // position of rank r
+    const int h = w / 2;
+    const int64_t base = job.out_lo - h;
+    const int r_lo = (w % 2 == 0) ? (w / 2 - 1) : (w / 2);
+    const int wpt = (nw + LT - 1) / LT;            // per-thread contiguous word ranges
     const int wb = min(nw, tid * wpt), we = min(nw, wb + wpt);
-    int cu = 0, cz = 0;
-    for (int k = wb; k < we; ++k) { cu += __popc(Ub[k]); cz += __popc(Zb[k]); }
-    scanU[tid] = cu;
-    scanZ[tid] = cz;
-    __syncthreads();
-    for (int off = 1; off < kWalkThreads; off <<= 1) {
-        const int vu = (tid >= off) ? scanU[tid - off] : 0;
-        const int vz = (tid >= off) ? scanZ[tid - off] : 0;
-        __syncthreads();
-        scanU[tid] += vu;
-        scanZ[tid] += vz;
-        __syncthreads();
-    }
-    // ---- b. word prefixes and the zone list E in rank order
-    int u = scanU[tid] - cu, z = scanZ[tid] - cz;
-    if (tid == kWalkThreads - 1) s_ne = scanZ[tid];
-    for (int k = wb; k < we; ++k) {
-        const uint32_t ub = Ub[k];
-        Up[k] = u;
-        uint32_t zb = Zb[k];
-        while (zb) {
-            const int b = __builtin_ctz(zb);
-            const int r = 32 * k + b;
-            const int ui = u + __popc(ub & ((1u << b) - 1u));
-            const int p = svals[s0 + r] - c0;
-            E[z++] = ((uint32_t)ui << 16) | (uint32_t)p;
-            zb &= zb - 1u;
-        }
-        u += __popc(ub);
-    }
-    __syncthreads();
-    const int ne = s_ne;
-    if (tid < 16) E[ne + tid] = 0xffffffffu;   // sentinels: index 0xffff > any q
-    __syncthreads();
 
-    // ---- c. walk
-    if (tid < L) {
-        const int k = tid;
-        const int r_lo = (w % 2 == 0) ? (w / 2 - 1) : (w / 2);
-        int q = r_lo;
-        int j = 0;
-        int jstop = 0;
-        for (;;) {
-            const uint4 v = *reinterpret_cast<const uint4 *>(E + j);
-            const uint32_t es[4] = {v.x, v.y, v.z, v.w};
-            bool stop = false;
+    int64_t i0 = sg.o0;
+    int L = (int)min((int64_t)LT, sg.o1 - i0);
+    int c0 = (int)(i0 - job.out_lo);               // chunk offset inside the series' position space
+    // ---- a0. U of the first chunk: positions [c0, c0 + w + L - 1)
+    for (int i = tid; i < nw; i += LT) Ub[i] = 0u;
+    __syncthreads();
+    for (int i = tid; i < w + L - 1; i += LT) {
+        const int r = rk[c0 + i];
+        atomicOr(&Ub[r >> 5], 1u << (r & 31));
+    }
+    for (;;) {
+        const int M = w + L - 1;
+        // ---- a. zone Z: offsets < L-1 or >= w (excluded by some output's window)
+        for (int i = tid; i < nw; i += LT) Zb[i] = 0u;
+        __syncthreads();
+        if (tid < L - 1) {
+            const int r = rk[c0 + tid];
+            atomicOr(&Zb[r >> 5], 1u << (r & 31));
+            const int r2 = rk[c0 + w + tid];
+            atomicOr(&Zb[r2 >> 5], 1u << (r2 & 31));
+        }
+        __syncthreads();
+        int cu = 0, cz = 0;
+        for (int k = wb; k < we; ++k) { cu += __popc(Ub[k]); cz += __popc(Zb[k]); }
+        // inclusive scans of (cu, cz): within each wave by shuffles, then across waves
+        int iu = cu, iz = cz;
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                if (!stop) {
-                    const uint32_t e = es[t];
-                    if ((int)(e >> 16) > q) {
-                        stop = true;
-                        jstop = j + t;
-                    } else {
-                        const int pp = (int)(e & 0xffff);
-                        q += (pp < k) | (pp >= k + w);
+        for (int off = 1; off < 64; off <<= 1) {
+            const int yu = __shfl_up(iu, off, 64), yz = __shfl_up(iz, off, 64);
+            if (lane >= off) { iu += yu; iz += yz; }
+        }
+        if (lane == 63) { scanU[wv] = iu; scanZ[wv] = iz; }
+        __syncthreads();
+        int bu = 0, bz = 0, tz = 0;
+        for (int v = 0; v < LT / 64; ++v) {
+            if (v < wv) { bu += scanU[v]; bz += scanZ[v]; }
+            tz += scanZ[v];
+        }
+        // ---- b. word prefixes and the zone list E in rank order
+        int u = bu + iu - cu, z = bz + iz - cz;
+        for (int k = wb; k < we; ++k) {
+            const uint32_t ub = Ub[k];
+            Up[k] = u;
+            uint32_t zb = Zb[k];
+            while (zb) {
+                const int b = __builtin_ctz(zb);
+                const int ui = u + __popc(ub & ((1u << b) - 1u));
+                const int p = sv[32 * k + b] - c0;
+                E[z++] = ((uint32_t)ui << 16) | (uint32_t)p;
+                zb &= zb - 1u;
+            }
+            u += __popc(ub);
+        }
+        if (tid < 16) E[tz + tid] = 0xffffffffu;   // sentinels: index 0xffff > any q
+        __syncthreads();
+
+        // ---- c. walk
+        if (tid < L) {
+            const int k = tid;
+            int q = r_lo;
+            int j = 0;
+            int jstop = 0;
+            for (;;) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(E + j);
+                const uint32_t es[4] = {v.x, v.y, v.z, v.w};
+                bool stop = false;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    if (!stop) {
+                        const uint32_t e = es[t];
+                        if ((int)(e >> 16) > q) {
+                            stop = true;
+                            jstop = j + t;
+                        } else {
+                            const int pp = (int)(e & 0xffff);
+                            q += (pp < k) | (pp >= k + w);
+                        }
                     }
                 }
+                if (stop) break;
+                j += 4;
             }
-            if (stop) break;
-            j += 4;
+            // U index -> rank: the last word whose prefix is <= q holds it
+            auto select = [&](int qi) -> int {
+                int lo = 0, hi = nw - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (Up[mid] <= qi) lo = mid; else hi = mid - 1;
+                }
+                uint32_t bits = Ub[lo];
+                for (int t = qi - Up[lo]; t > 0; --t) bits &= bits - 1u;
+                return 32 * lo + __builtin_ctz(bits);
+            };
+            auto value = [&](int qi) -> double { return xprime(job, base + sv[select(qi)], h); };
+            const int q1 = q;
+            const double v1 = value(q1);
+            double out;
+            if (w % 2 == 0) {
+                q = q1 + 1;
+                for (j = jstop;; ++j) {
+                    const uint32_t e = E[j];
+                    if ((int)(e >> 16) > q) break;
+                    const int pp = (int)(e & 0xffff);
+                    q += (pp < k) | (pp >= k + w);
+                }
+                out = (value(q) + v1) / 2.0;
+            } else {
+                out = v1;
+            }
+            job.dst[i0 + k - job.out_lo] = out;
         }
-        // U index -> rank: the last word whose prefix is <= q holds it
-        auto select = [&](int qi) -> int {
-            int lo = 0, hi = nw - 1;
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (Up[mid] <= qi) lo = mid; else hi = mid - 1;
-            }
-            uint32_t bits = Ub[lo];
-            for (int t = qi - Up[lo]; t > 0; --t) bits &= bits - 1u;
-            return 32 * lo + __builtin_ctz(bits);
-        };
-        const int h = w / 2;
-        const int64_t base = job.out_lo - h;
-        auto value = [&](int qi) -> double { return xprime(job, base + svals[s0 + select(qi)], h); };
-        const int q1 = q;
-        const double v1 = value(q1);
-        double out;
-        if (w % 2 == 0) {
-            q = q1 + 1;
-            for (j = jstop;; ++j) {
-                const uint32_t e = E[j];
-                if ((int)(e >> 16) > q) break;
-                const int pp = (int)(e & 0xffff);
-                q += (pp < k) | (pp >= k + w);
-            }
-            out = (value(q) + v1) / 2.0;
-        } else {
-            out = v1;
+        // ---- next chunk: positions [c0, c0 + L) leave, [c0 + M, c0 + L + w + L1 - 1) enter
+        const int64_t i1 = i0 + L;
+        if (i1 >= sg.o1) break;
+        const int L1 = (int)min((int64_t)LT, sg.o1 - i1);
+        __syncthreads();          // the walk's reads of Ub / Up / E are done
+        if (tid < L) {
+            const int r = rk[c0 + tid];
+            atomicAnd(&Ub[r >> 5], ~(1u << (r & 31)));
         }
-        job.dst[i0 + k - job.out_lo] = out;
+        if (tid < L1) {
+            const int r = rk[c0 + M + tid];
+            atomicOr(&Ub[r >> 5], 1u << (r & 31));
+        }
+        i0 = i1;
+        c0 += L;
+        L = L1;
     }
 }
 
@@ -669,38 +765,51 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
         }
     }
     std::vector<int32_t> seg(jobs.size() + 1, 0);
-    std::vector<int64_t> chunks;
-    int64_t nsmax = 0;
+    int64_t nsmax = 0, nchunks = 0;
     for (size_t j = 0; j < jobs.size(); ++j) {
         const int64_t nout = jobs[j].out_hi - jobs[j].out_lo;
         const int64_t ns = nout > 0 ? nout + w - 1 : 0;
         if ((int64_t)seg[j] + ns >= (1ll << 31)) return comap_fail(ctx, -1, "median plan too large");
         seg[j + 1] = seg[j] + (int32_t)ns;
         nsmax = std::max(nsmax, ns);
-        for (int64_t i0 = jobs[j].out_lo; i0 < jobs[j].out_hi; i0 += mp->lc) {
-            chunks.push_back((int64_t)j);
-            chunks.push_back(i0);
+        if (nout > 0) nchunks += (nout + mp->lc - 1) / mp->lc;
+    }
+    // walk segments of up to S chunks per workgroup (the bitmaps slide from chunk to
+    // chunk); measured at w = 6000: C2 (107k chunks) S = 4 best, a C3 shard (13k) S = 1-2
+    const char *senv = getenv("COMAP_MEDIAN_S");
+    int64_t S = senv ? atoll(senv) : std::min<int64_t>(4, std::max<int64_t>(1, nchunks / 16384));
+    S = std::max<int64_t>(1, S);
+    std::vector<SlideSeg> wsegs;
+    for (size_t j = 0; j < jobs.size(); ++j) {
+        const int64_t span = S * mp->lc;
+        for (int64_t o = jobs[j].out_lo; o < jobs[j].out_hi; o += span) {
+            SlideSeg sg;
+            sg.job = (int32_t)j; sg.pad_ = 0; sg.o0 = o; sg.o1 = std::min(jobs[j].out_hi, o + span);
+            wsegs.push_back(sg);
         }
     }
     mp->nwmax = (int32_t)((nsmax + 31) / 32);
     mp->njobs = (int32_t)jobs.size();
     mp->nitems = seg.back();
-    mp->nchunks = (int64_t)chunks.size() / 2;
+    mp->nchunks = nchunks;
+    mp->nsegs = (int32_t)wsegs.size();
     hipStream_t st = ctx->stream;
     auto alloc = [&](void **p, size_t b) { return hipMalloc(p, b ? b : 8); };
     COMAP_CHECK(ctx, alloc((void **)&mp->jobs, sizeof(MedJob) * jobs.size()));
     COMAP_CHECK(ctx, alloc((void **)&mp->seg, 4 * seg.size()));
-    COMAP_CHECK(ctx, alloc((void **)&mp->chunks, 8 * chunks.size()));
+    COMAP_CHECK(ctx, alloc((void **)&mp->segs, sizeof(SlideSeg) * wsegs.size()));
     COMAP_CHECK(ctx, alloc((void **)&mp->k0, 8 * (size_t)mp->nitems));
     COMAP_CHECK(ctx, alloc((void **)&mp->k1, 8 * (size_t)mp->nitems));
     COMAP_CHECK(ctx, alloc((void **)&mp->v0, 4 * (size_t)mp->nitems));
     COMAP_CHECK(ctx, alloc((void **)&mp->v1, 4 * (size_t)mp->nitems));
     COMAP_CHECK(ctx, alloc((void **)&mp->rank, 4 * (size_t)mp->nitems));
     COMAP_CHECK(ctx, alloc((void **)&mp->redo, 4 * 3 * jobs.size()));   // flags | begin | end
+    COMAP_CHECK(ctx, alloc((void **)&mp->krange, 16 * jobs.size()));    // per-series key min, max
     COMAP_CHECK(ctx, hipMemcpyAsync(mp->jobs, jobs.data(), sizeof(MedJob) * jobs.size(), hipMemcpyHostToDevice, st));
     COMAP_CHECK(ctx, hipMemcpyAsync(mp->seg, seg.data(), 4 * seg.size(), hipMemcpyHostToDevice, st));
-    if (!chunks.empty())
-        COMAP_CHECK(ctx, hipMemcpyAsync(mp->chunks, chunks.data(), 8 * chunks.size(), hipMemcpyHostToDevice, st));
+    if (!wsegs.empty())
+        COMAP_CHECK(ctx, hipMemcpyAsync(mp->segs, wsegs.data(), sizeof(SlideSeg) * wsegs.size(), hipMemcpyHostToDevice,
+                                        st));
     size_t tb = 0, tb32 = 0;
     COMAP_CHECK(ctx, seg_sort(nullptr, tb, mp->k0, mp->k1, mp->v0, mp->v1, (int)mp->nitems, mp->njobs, mp->seg,
                               mp->seg + 1, st));
@@ -720,7 +829,7 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
 
 void comap_median_plan_free(MedPlan *mp)
 {
-    void *b[] = {mp->jobs, mp->seg, mp->chunks, mp->k0, mp->k1, mp->v0, mp->v1, mp->rank, mp->temp, mp->segs, mp->redo};
+    void *b[] = {mp->jobs, mp->seg, mp->k0, mp->k1, mp->v0, mp->v1, mp->rank, mp->temp, mp->segs, mp->redo, mp->krange};
     for (void *p : b)
         if (p) (void)hipFree(p);
     *mp = MedPlan();
@@ -746,7 +855,10 @@ int comap_median_run(comap_ctx *ctx, MedPlan *mp, hipStream_t st)
     if (mp->key32) {
         uint32_t *k0 = (uint32_t *)mp->k0, *k1 = (uint32_t *)mp->k1;
         int32_t *flag = mp->redo, *beg = mp->redo + mp->njobs, *end = beg + mp->njobs;
-        k_med_keys<uint32_t><<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, k0, mp->v0);
+        unsigned long long *kr = (unsigned long long *)mp->krange;
+        k_med_range<<<mp->njobs, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, kr);
+        COMAP_LAUNCH_CHECK(ctx);
+        k_med_keys<uint32_t><<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, k0, mp->v0, kr);
         COMAP_LAUNCH_CHECK(ctx);
         COMAP_CHECK(ctx, seg_sort(mp->temp, tb, (const uint32_t *)k0, k1, mp->v0, mp->v1, (int)mp->nitems, mp->njobs,
                                   mp->seg, mp->seg + 1, st));
@@ -760,7 +872,7 @@ int comap_median_run(comap_ctx *ctx, MedPlan *mp, hipStream_t st)
         COMAP_CHECK(ctx, seg_sort(mp->temp, tb, (const uint64_t *)mp->k0, mp->k1, mp->v0, mp->v1, (int)mp->nitems,
                                   mp->njobs, beg, end, st));
     } else {
-        k_med_keys<uint64_t><<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, mp->k0, mp->v0);
+        k_med_keys<uint64_t><<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, mp->k0, mp->v0, nullptr);
         COMAP_LAUNCH_CHECK(ctx);
         COMAP_CHECK(ctx, seg_sort(mp->temp, tb, (const uint64_t *)mp->k0, mp->k1, mp->v0, mp->v1, (int)mp->nitems,
                                   mp->njobs, mp->seg, mp->seg + 1, st));
@@ -768,12 +880,15 @@ int comap_median_run(comap_ctx *ctx, MedPlan *mp, hipStream_t st)
     k_med_rank<<<g1, 256, 0, st>>>(mp->seg, mp->njobs, mp->v1, mp->rank);
     COMAP_LAUNCH_CHECK(ctx);
     const size_t sm = walk_smem(mp->nwmax, mp->lc);
+#define COMAP_WALK(LT) k_med_walk<LT><<<mp->nsegs, LT, sm, st>>>(mp->jobs, mp->segs, mp->seg, mp->v1, mp->rank, mp->w, \
+                                                                 mp->nwmax)
     switch (mp->lc) {
-    case 64: k_med_walk<64><<<mp->nchunks, 64, sm, st>>>(mp->jobs, mp->chunks, mp->seg, mp->v1, mp->rank, mp->w, mp->nwmax); break;
-    case 128: k_med_walk<128><<<mp->nchunks, 128, sm, st>>>(mp->jobs, mp->chunks, mp->seg, mp->v1, mp->rank, mp->w, mp->nwmax); break;
-    case 512: k_med_walk<512><<<mp->nchunks, 512, sm, st>>>(mp->jobs, mp->chunks, mp->seg, mp->v1, mp->rank, mp->w, mp->nwmax); break;
-    default: k_med_walk<256><<<mp->nchunks, 256, sm, st>>>(mp->jobs, mp->chunks, mp->seg, mp->v1, mp->rank, mp->w, mp->nwmax); break;
+    case 64: COMAP_WALK(64); break;
+    case 128: COMAP_WALK(128); break;
+    case 512: COMAP_WALK(512); break;
+    default: COMAP_WALK(256); break;
     }
+#undef COMAP_WALK
     COMAP_LAUNCH_CHECK(ctx);
     return 0;
 }

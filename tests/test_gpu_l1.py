@@ -77,15 +77,18 @@ def test_medfilt_long_series_split(path, monkeypatch):
     assert np.array_equal(got, oracle.medfilt(z, 400)[y.size:2 * y.size])
 
 
-@pytest.mark.parametrize('key32,lc', [('1', '128'), ('0', '128'), ('1', '64'), ('1', '256'), ('1', '512')])
-def test_medfilt_sort_proxy_runs(key32, lc, monkeypatch):
+@pytest.mark.parametrize('key32,lc,S', [('1', '128', ''), ('0', '128', ''), ('1', '64', ''), ('1', '256', ''),
+                                        ('1', '512', ''), ('1', '128', '1'), ('1', '128', '3'), ('1', '64', '16')])
+def test_medfilt_sort_proxy_runs(key32, lc, S, monkeypatch):
     """Global-sort path with 32-bit proxy keys: values that round to the same
     f32 but differ in f64 (short runs: fixed in place; runs > 32: the segment is
     re-sorted on u64 keys), signed zeros and negative values; u64-key path and
-    the 64/256/512-output walk chunks for comparison."""
+    the 64/256/512-output walk chunks and 1..16 chunks per walk workgroup for comparison."""
     monkeypatch.setenv('COMAP_MEDIAN_PATH', 'sort')
     monkeypatch.setenv('COMAP_MEDIAN_KEY32', key32)
     monkeypatch.setenv('COMAP_MEDIAN_L', lc)
+    if S:
+        monkeypatch.setenv('COMAP_MEDIAN_S', S)      # chunks per walk workgroup (bitmaps slid between them)
     from comapreduce_amd.tools.medfilt import medfilt, medfilt_batch
     rng = np.random.default_rng(12)
     n = 20000
@@ -94,7 +97,9 @@ def test_medfilt_sort_proxy_runs(key32, lc, monkeypatch):
     long_ = np.round(rng.standard_normal(n), 1) + eps            # runs of hundreds -> segment re-sort
     flat = 1.0 + rng.integers(0, 40, n) * 2.0 ** -45              # one proxy for the whole series
     zeros = np.where(rng.random(n) < 0.5, 0.0, -0.0) * (rng.random(n) < 0.9) + (rng.random(n) < 0.1) * -1e-300
-    for x, w in ((short, 6000), (long_, 6000), (flat, 401), (zeros, 400), (short[:7000], 7000)):
+    cluster = rng.standard_normal(n) * 1e6                          # wide range: coarse proxy buckets ...
+    cluster[rng.choice(n, 300, replace=False)] = 1.0 + np.arange(300) * 1e-12   # ... one holds a 300-run
+    for x, w in ((short, 6000), (long_, 6000), (flat, 401), (zeros, 400), (short[:7000], 7000), (cluster, 6000)):
         assert np.array_equal(medfilt(x.copy(), w), oracle.medfilt(x.copy(), w)), (w, x[:3])
     series = [short, long_[:9000], flat[:6500]]
     got = medfilt_batch(series, 6000, reflect=True)
