@@ -42,6 +42,7 @@
 
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 
 struct comap_destriper {
     comap_ctx *ctx = nullptr;
@@ -71,6 +72,11 @@ struct comap_destriper {
     int32_t *hrow = nullptr;       // [nh] pixel rows with entries (the CG bin skips empty rows)
     int64_t nh = 0;
     int32_t *perm = nullptr;       // [NO] internal offset position -> caller's offset (NULL: identity)
+    // COMAP_DS_BIN=lds (measurement variant): LDS-privatised scatter-add bin over pixel
+    // tiles of bin_tile pixels, needing each pixel-major entry's pixel
+    int bin_mode = 0;
+    int bin_tile = 256;
+    int32_t *ppix = nullptr;       // [nnzp] pixel of each pixel-major entry (bin_mode 1)
     int32_t *flags_host = nullptr; // pinned [2 + 2 nb]
     double *thr_host = nullptr;    // pinned [1]
     hipStream_t cs = nullptr;      // CG stream (graph capture needs a non-default stream)
@@ -571,6 +577,64 @@ __global__ void __launch_bounds__(256) k_ds_bin(const int64_t *__restrict__ prow
     }
 }
 
+// The north_star's formulation of the same bin, kept as a measured alternative
+// (COMAP_DS_BIN=lds): one workgroup per tile of TP consecutive pixels privatises the
+// tile's NB-band numerators in LDS; its threads stream the tile's entries (coalesced,
+// in pixel-major order) and scatter-add s_e x_o(e) with LDS f64 atomics, then write the
+// tile out with the same base / hdiv post-processing.  The add order within a pixel is
+// not fixed (results vary in the last bits run to run).
+template <int NB>
+__global__ void __launch_bounds__(256) k_ds_bin_lds(const int64_t *__restrict__ prow, const int32_t *__restrict__ poff,
+                                                    const double *__restrict__ pw, const int32_t *__restrict__ ppix,
+                                                    const double *__restrict__ x, int64_t npix, int TP,
+                                                    const double *__restrict__ base, const double *__restrict__ hdiv,
+                                                    double *__restrict__ num, const int32_t *__restrict__ flags)
+{
+    extern __shared__ double tacc[];   // [TP][NB]
+    if (cg_done(flags)) return;
+    const int64_t P0 = (int64_t)blockIdx.x * TP, P1 = min(npix, P0 + TP);
+    const int nt = (int)(P1 - P0) * NB;
+    for (int i = threadIdx.x; i < nt; i += 256) tacc[i] = 0.0;
+    __syncthreads();
+    const int64_t e1 = prow[P1];
+    constexpr int U = 4;
+    for (int64_t e = prow[P0] + threadIdx.x; e < e1; e += 256 * U) {
+        int32_t o[U], q[U];
+        double a[U][NB], xv[U][NB];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t k = e + u * 256;
+            const bool in = k < e1;
+            o[u] = in ? poff[k] : 0;
+            q[u] = in ? ppix[k] - (int32_t)P0 : -1;
+            if (in) {
+                ldb<NB>(pw + k * NB, a[u]);
+            } else {
+#pragma unroll
+                for (int b = 0; b < NB; ++b) a[u][b] = 0.0;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) ldb<NB>(x + (int64_t)o[u] * NB, xv[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (q[u] >= 0) {
+#pragma unroll
+                for (int b = 0; b < NB; ++b)
+                    __hip_atomic_fetch_add(&tacc[q[u] * NB + b], a[u][b] * xv[u][b], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nt; i += 256) {
+        const int64_t g = P0 * NB + i;
+        double s = tacc[i];
+        if (base) s = base[g] - s;
+        else if (hdiv) { const double hv = hdiv[g]; s = hv != 0.0 ? s / hv : s; }
+        num[g] = s;
+    }
+}
+
 // y_o = ws_o x_o - sum_e s_e m_p(e) per band  (x == NULL: y_o = tw_o - ..., the b vector).
 // G lanes per offset (G = 16 for L <= 64: 256/G offsets per block sweep); each lane issues
 // kProjU entry loads then kProjU map gathers before its fmas; m = num / h, or num itself
@@ -888,6 +952,13 @@ template <int NB>
 void launch_bin_nb(const comap_destriper *d, hipStream_t st, const double *x, const double *base, const double *hdiv,
                    double *num, const int32_t *flags, bool hit_rows)
 {
+    if (d->bin_mode == 1) {
+        const int TP = d->bin_tile;
+        const unsigned g = (unsigned)std::max<int64_t>(1, (d->npix + TP - 1) / TP);
+        k_ds_bin_lds<NB><<<g, 256, sizeof(double) * TP * NB, st>>>(d->prow, d->poff, d->pw, d->ppix, x, d->npix, TP,
+                                                                  base, hdiv, num, flags);
+        return;
+    }
     const int64_t np = hit_rows ? d->nh : d->npix;
     const int32_t *rows = hit_rows ? d->hrow : nullptr;
     const int64_t mean = np ? d->nnzp / np : 0;
@@ -1091,6 +1162,16 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     rc |= dalloc(ctx, &d->poff, d->nnzp);
     rc |= dalloc(ctx, &d->pw, d->nnzp * NB);
     if (rc) return -2;
+    {
+        const char *bm = getenv("COMAP_DS_BIN");
+        if (bm && !strcmp(bm, "lds")) {
+            const char *tp = getenv("COMAP_DS_TILE");
+            d->bin_mode = 1;
+            d->bin_tile = tp ? std::max(32, std::min(4096, atoi(tp))) : 256;
+            if (dalloc(ctx, &d->ppix, d->nnzp)) return -2;
+            COMAP_CHECK(ctx, hipMemcpyAsync(d->ppix, k1, 4 * (size_t)d->nnzp, hipMemcpyDeviceToDevice, st));
+        }
+    }
     COMAP_NB_SWITCH(nb, k_pixel_entries<NB><<<grid_for(d->nnzp), 256, 0, st>>>(v1, d->nnzp, eoff, d->ow, d->poff,
                                                                                 d->pw));
     COMAP_LAUNCH_CHECK(ctx);
@@ -1119,7 +1200,7 @@ extern "C" int comap_destripe_destroy(comap_destriper *d)
     COMAP_DEVICE_GUARD(d->ctx);
     if (d->cs) (void)hipStreamSynchronize(d->cs);
     void *b[] = {d->orow, d->opix, d->ow, d->ws, d->tw, d->prow, d->poff, d->pw, d->h, d->hits, d->nnum, d->part, d->scal,
-                 d->cg, d->flags, d->hrow, d->perm};
+                 d->cg, d->flags, d->hrow, d->perm, d->ppix};
     for (void *p : b)
         if (p) (void)hipFree(p);
     if (d->flags_host) (void)hipHostFree(d->flags_host);
