@@ -1238,8 +1238,9 @@ __global__ void __launch_bounds__(256) k_scan_weights(const int32_t *__restrict_
 // F-ordered (strides (4, 4 n)), so its float32 nanmean reduces each channel
 // SEQUENTIALLY: s = ((0 + x0) + x1) + ... in float32 with NaN -> 0, then
 // float32(double(s) / count).  gain = double(float32(th - tc)) / (t_hot - 2.73)
-// and tsys = tc / gain in float64 (t_hot is an np.float64).  One thread per
-// channel row; a block's 256 rows read the same columns, so each cache line
+// and tsys = tc / gain in float64 (t_hot is an np.float64).  Two threads per
+// channel row -- the hot and the cold mean are independent sequential sums -- so a
+// block is 128 rows x 2 sides; its rows read the same columns, so each cache line
 // is fetched once and re-used from L1 for the next 15 columns.
 __global__ void __launch_bounds__(256) k_vane(const float *__restrict__ tod, int64_t T, int F,
                                               int64_t vstart, const int32_t *__restrict__ hot,
@@ -1247,21 +1248,22 @@ __global__ void __launch_bounds__(256) k_vane(const float *__restrict__ tod, int
                                               const int64_t *__restrict__ coff, double t_hot,
                                               double *__restrict__ tsys, double *__restrict__ gain)
 {
-    const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;   // (f*4+b)*1024 + c
-    if (row >= (int64_t)F * kBC) return;
-    const int fb = (int)(row / kChannels);                          // uniform: 1024 % 256 == 0
+    __shared__ float s_cold[128];
+    const int side = threadIdx.x >> 7;                               // wave-uniform: 0 hot, 1 cold
+    const int64_t row = (int64_t)blockIdx.x * 128 + (threadIdx.x & 127);   // (f*4+b)*1024 + c
+    const bool live = row < (int64_t)F * kBC;
+    const int fb = live ? (int)(row / kChannels) : 0;               // uniform: 1024 % 128 == 0
     const float *p = tod + row * T + vstart;
     const int64_t h0 = hoff[fb], h1 = hoff[fb + 1], k0 = coff[fb], k1 = coff[fb + 1];
-    if (h1 == h0) return;   // no hot/cold found (RuntimeError path): leave zeros
-    float mean[2];
-    for (int side = 0; side < 2; ++side) {
+    float mean = 0.f;
+    if (live && h1 != h0) {
         const int32_t *idx = side == 0 ? hot : cold;
         const int64_t j0 = side == 0 ? h0 : k0, j1 = side == 0 ? h1 : k1;
         float s = 0.f;
         int64_t cnt = 0;
-        // the adds stay sequential (numpy's order); the loads are issued 8 at a time
+        // the adds stay sequential (numpy's order); the loads are issued kV at a time
         // (one at a time the row's ~900 gathers made this a latency chain)
-        constexpr int kV = 8;
+        constexpr int kV = 16;
         int64_t j = j0;
         for (; j + kV <= j1; j += kV) {
             float x[kV];
@@ -1280,12 +1282,16 @@ __global__ void __launch_bounds__(256) k_vane(const float *__restrict__ tod, int
             s += ok ? x : 0.f;
             cnt += ok;
         }
-        mean[side] = (float)((double)s / (double)cnt);   // empty list: nanmean([]) -> NaN
+        mean = (float)((double)s / (double)cnt);   // empty list: nanmean([]) -> NaN
     }
-    const float d = mean[0] - mean[1];
+    if (side == 1) s_cold[threadIdx.x & 127] = mean;
+    __syncthreads();
+    if (side == 1 || !live || h1 == h0) return;   // no hot/cold found (RuntimeError path): leave zeros
+    const float mc = s_cold[threadIdx.x];
+    const float d = mean - mc;
     const double g = (double)d / (t_hot - 2.73);
     gain[row] = g;
-    tsys[row] = (double)mean[1] / g;
+    tsys[row] = (double)mc / g;
 }
 
 // ------------------------------------------------------------------ generic channel binning
@@ -1908,7 +1914,7 @@ extern "C" int comap_l1_vane(comap_l1_plan *p, int64_t vstart, int64_t vlen, con
     COMAP_CHECK(ctx, hipMemsetAsync(tsys, 0, (size_t)FB * kChannels * 8, st));
     COMAP_CHECK(ctx, hipMemsetAsync(gain, 0, (size_t)FB * kChannels * 8, st));
     const int64_t rows = (int64_t)FB * kChannels;
-    PROF(p, KV_VANE, k_vane<<<(rows + 255) / 256, 256, 0, st>>>(p->tod, p->T, p->F, vstart, dh, dho, dc, dco, t_hot,
+    PROF(p, KV_VANE, k_vane<<<(rows + 127) / 128, 256, 0, st>>>(p->tod, p->T, p->F, vstart, dh, dho, dc, dco, t_hot,
                                                             tsys, gain));
     COMAP_LAUNCH_CHECK(ctx);
     return 0;
