@@ -259,14 +259,23 @@ __global__ void __launch_bounds__(256) k_med_redo(const MedJob *__restrict__ job
     }
 }
 
-__global__ void __launch_bounds__(256) k_med_rank(const int32_t *__restrict__ seg, int32_t njobs,
-                                                  const int32_t *__restrict__ svals, int32_t *__restrict__ rank)
+// rank[position] = sorted index, and sval[sorted index] = the value (so the walk's
+// final lookup is one load)
+__global__ void __launch_bounds__(256) k_med_rank(const MedJob *__restrict__ jobs, const int32_t *__restrict__ seg,
+                                                  int32_t njobs, int32_t w, const int32_t *__restrict__ svals,
+                                                  int32_t *__restrict__ rank, double *__restrict__ sval)
 {
     const int jb = blockIdx.y;
     if (jb >= njobs) return;
+    const MedJob job = jobs[jb];
     const int32_t s0 = seg[jb], ns = seg[jb + 1] - s0;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += gridDim.x * blockDim.x)
-        rank[s0 + svals[s0 + i]] = i;
+    const int h = w / 2;
+    const int64_t base = job.out_lo - h;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += gridDim.x * blockDim.x) {
+        const int32_t p = svals[s0 + i];
+        rank[s0 + p] = i;
+        sval[s0 + i] = xprime(job, base + p, h);
+    }
 }
 
 // One workgroup per walk segment: S consecutive chunks of LT outputs of one job.  The
@@ -275,18 +284,18 @@ __global__ void __launch_bounds__(256) k_med_rank(const int32_t *__restrict__ se
 // enter (3 LT rank reads per chunk instead of w + LT - 1).
 template <int LT>   // threads = outputs per chunk
 __global__ void __launch_bounds__(LT) k_med_walk(const MedJob *__restrict__ jobs, const SlideSeg *__restrict__ wsegs,
-                                                 const int32_t *__restrict__ seg, const int32_t *__restrict__ svals,
+                                                 const int32_t *__restrict__ seg, const double *__restrict__ sval,
                                                  const int32_t *__restrict__ rank, int32_t w, int32_t nwmax)
 {
-    // LDS: E (16-B aligned for 4-entry reads) | U bitmap | Z bitmap | U word prefixes | scans
+    // LDS: E (16-B aligned for 4-entry reads) | U bitmap | Z bitmap | U, Z word prefixes | scans
     extern __shared__ __align__(16) unsigned char smem[];
     uint32_t *E = reinterpret_cast<uint32_t *>(smem);
     uint32_t *Ub = E + (2 * LT + 16);
     uint32_t *Zb = Ub + nwmax;
     int32_t *Up = reinterpret_cast<int32_t *>(Zb + nwmax);
-    int *scanU = Up + nwmax;
+    int32_t *Zp = Up + nwmax;
+    int *scanU = Zp + nwmax;
     int *scanZ = scanU + LT;
-    __shared__ int s_ne;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6;
@@ -297,9 +306,7 @@ __global__ void __launch_bounds__(LT) k_med_walk(const MedJob *__restrict__ jobs
     const int32_t s0 = seg[jb], ns = seg[jb + 1] - s0;
     const int nw = (ns + 31) >> 5;
     const int32_t *rk = rank + s0;                 // rank of series position p
-    const int32_t *sv = svals + s0;                // position of rank r
-    const int h = w / 2;
-    const int64_t base = job.out_lo - h;
+    const double *sv = sval + s0;                  // value of rank r
     const int r_lo = (w % 2 == 0) ? (w / 2 - 1) : (w / 2);
     const int wpt = (nw + LT - 1) / LT;            // per-thread contiguous word ranges
     const int wb = min(nw, tid * wpt), we = min(nw, wb + wpt);
@@ -319,11 +326,12 @@ __global__ void __launch_bounds__(LT) k_med_walk(const MedJob *__restrict__ jobs
         // ---- a. zone Z: offsets < L-1 or >= w (excluded by some output's window)
         for (int i = tid; i < nw; i += LT) Zb[i] = 0u;
         __syncthreads();
+        int zr0 = -1, zr1 = -1;                   // this thread's zone entries: offsets tid and w + tid
         if (tid < L - 1) {
-            const int r = rk[c0 + tid];
-            atomicOr(&Zb[r >> 5], 1u << (r & 31));
-            const int r2 = rk[c0 + w + tid];
-            atomicOr(&Zb[r2 >> 5], 1u << (r2 & 31));
+            zr0 = rk[c0 + tid];
+            atomicOr(&Zb[zr0 >> 5], 1u << (zr0 & 31));
+            zr1 = rk[c0 + w + tid];
+            atomicOr(&Zb[zr1 >> 5], 1u << (zr1 & 31));
         }
         __syncthreads();
         int cu = 0, cz = 0;
@@ -342,20 +350,27 @@ __global__ void __launch_bounds__(LT) k_med_walk(const MedJob *__restrict__ jobs
             if (v < wv) { bu += scanU[v]; bz += scanZ[v]; }
             tz += scanZ[v];
         }
-        // ---- b. word prefixes and the zone list E in rank order
+        // ---- b. word prefixes; each zone entry's place in rank order (its Z prefix) and
+        //         its union index (its U prefix) -> the zone list E, sorted by rank
         int u = bu + iu - cu, z = bz + iz - cz;
         for (int k = wb; k < we; ++k) {
-            const uint32_t ub = Ub[k];
             Up[k] = u;
-            uint32_t zb = Zb[k];
-            while (zb) {
-                const int b = __builtin_ctz(zb);
-                const int ui = u + __popc(ub & ((1u << b) - 1u));
-                const int p = sv[32 * k + b] - c0;
-                E[z++] = ((uint32_t)ui << 16) | (uint32_t)p;
-                zb &= zb - 1u;
+            Zp[k] = z;
+            u += __popc(Ub[k]);
+            z += __popc(Zb[k]);
+        }
+        __syncthreads();
+        if (tid < L - 1) {
+            const int rr[2] = {zr0, zr1};
+            const int pp[2] = {tid, w + tid};
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const int r = rr[t], k = r >> 5;
+                const uint32_t below = (1u << (r & 31)) - 1u;
+                const int ui = Up[k] + __popc(Ub[k] & below);
+                const int zi = Zp[k] + __popc(Zb[k] & below);
+                E[zi] = ((uint32_t)ui << 16) | (uint32_t)pp[t];
             }
-            u += __popc(ub);
         }
         if (tid < 16) E[tz + tid] = 0xffffffffu;   // sentinels: index 0xffff > any q
         __syncthreads();
@@ -397,7 +412,7 @@ __global__ void __launch_bounds__(LT) k_med_walk(const MedJob *__restrict__ jobs
                 for (int t = qi - Up[lo]; t > 0; --t) bits &= bits - 1u;
                 return 32 * lo + __builtin_ctz(bits);
             };
-            auto value = [&](int qi) -> double { return xprime(job, base + sv[select(qi)], h); };
+            auto value = [&](int qi) -> double { return sv[select(qi)]; };
             const int q1 = q;
             const double v1 = value(q1);
             double out;
@@ -667,7 +682,7 @@ hipError_t seg_sort(void *tmp, size_t &tb, const K *k0, K *k1, const int32_t *v0
                                                               beg, end, 0u, 8u * (unsigned)sizeof(K), st);
 }
 
-size_t walk_smem(int nwmax, int lt) { return 4 * (2 * (size_t)lt + 16) + 12 * (size_t)nwmax + 8 * (size_t)lt + 64; }
+size_t walk_smem(int nwmax, int lt) { return 4 * (2 * (size_t)lt + 16) + 16 * (size_t)nwmax + 8 * (size_t)lt + 64; }
 
 }  // namespace
 
@@ -877,10 +892,12 @@ int comap_median_run(comap_ctx *ctx, MedPlan *mp, hipStream_t st)
         COMAP_CHECK(ctx, seg_sort(mp->temp, tb, (const uint64_t *)mp->k0, mp->k1, mp->v0, mp->v1, (int)mp->nitems,
                                   mp->njobs, mp->seg, mp->seg + 1, st));
     }
-    k_med_rank<<<g1, 256, 0, st>>>(mp->seg, mp->njobs, mp->v1, mp->rank);
+    // k0 (sort keys) is free now: it holds the values in sorted order for the walk
+    double *sval = (double *)mp->k0;
+    k_med_rank<<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, mp->v1, mp->rank, sval);
     COMAP_LAUNCH_CHECK(ctx);
     const size_t sm = walk_smem(mp->nwmax, mp->lc);
-#define COMAP_WALK(LT) k_med_walk<LT><<<mp->nsegs, LT, sm, st>>>(mp->jobs, mp->segs, mp->seg, mp->v1, mp->rank, mp->w, \
+#define COMAP_WALK(LT) k_med_walk<LT><<<mp->nsegs, LT, sm, st>>>(mp->jobs, mp->segs, mp->seg, sval, mp->rank, mp->w, \
                                                                  mp->nwmax)
     switch (mp->lc) {
     case 64: COMAP_WALK(64); break;
