@@ -126,6 +126,7 @@ struct MedPlan {
     int32_t *v0 = nullptr, *v1 = nullptr;
     int32_t *rank = nullptr;     // dev [nitems] position -> sorted index
     bool key32 = true;           // sort 32-bit proxies + exact run fix-up (else u64 keys)
+    bool wide = false;           // segmented sort with 1024-thread workgroups (few series)
     int32_t *redo = nullptr;     // dev [3][njobs]: segment re-sort flags, begin, end
     void *krange = nullptr;      // dev [njobs][2] u64: per-series key min, max (proxy scaling)
     void *temp = nullptr;

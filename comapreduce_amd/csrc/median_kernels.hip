@@ -674,10 +674,18 @@ size_t slide_smem(int w)
 #endif
 using SegSortConfig = rocprim::segmented_radix_sort_config<COMAP_SORT_RB, rocprim::kernel_config<256, COMAP_SORT_IPT>,
                                                            rocprim::DisabledWarpSortConfig, false>;
+// few segments (a C3 shard: ~100 series for 256 CUs): the sort runs one workgroup per
+// segment, so wider workgroups finish each segment in fewer tiles per digit pass
+using SegSortConfigWide = rocprim::segmented_radix_sort_config<8, rocprim::kernel_config<1024, 8>,
+                                                               rocprim::DisabledWarpSortConfig, false>;
 template <typename K>
 hipError_t seg_sort(void *tmp, size_t &tb, const K *k0, K *k1, const int32_t *v0, int32_t *v1, int n, int nseg,
-                    const int32_t *beg, const int32_t *end, hipStream_t st)
+                    const int32_t *beg, const int32_t *end, hipStream_t st, bool wide = false)
 {
+    if (wide)
+        return rocprim::segmented_radix_sort_pairs<SegSortConfigWide>(tmp, tb, k0, k1, v0, v1, (unsigned)n,
+                                                                      (unsigned)nseg, beg, end, 0u,
+                                                                      8u * (unsigned)sizeof(K), st);
     return rocprim::segmented_radix_sort_pairs<SegSortConfig>(tmp, tb, k0, k1, v0, v1, (unsigned)n, (unsigned)nseg,
                                                               beg, end, 0u, 8u * (unsigned)sizeof(K), st);
 }
@@ -825,11 +833,15 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
     if (!wsegs.empty())
         COMAP_CHECK(ctx, hipMemcpyAsync(mp->segs, wsegs.data(), sizeof(SlideSeg) * wsegs.size(), hipMemcpyHostToDevice,
                                         st));
+    {
+        const char *wenv = getenv("COMAP_SORT_WIDE");   // 0 / 1; default: wide below 512 series
+        mp->wide = wenv ? atoi(wenv) != 0 : mp->njobs < 512;
+    }
     size_t tb = 0, tb32 = 0;
     COMAP_CHECK(ctx, seg_sort(nullptr, tb, mp->k0, mp->k1, mp->v0, mp->v1, (int)mp->nitems, mp->njobs, mp->seg,
-                              mp->seg + 1, st));
+                              mp->seg + 1, st, mp->wide));
     COMAP_CHECK(ctx, seg_sort(nullptr, tb32, (const uint32_t *)mp->k0, (uint32_t *)mp->k1, mp->v0, mp->v1,
-                              (int)mp->nitems, mp->njobs, mp->seg, mp->seg + 1, st));
+                              (int)mp->nitems, mp->njobs, mp->seg, mp->seg + 1, st, mp->wide));
     tb = std::max(tb, tb32);
     mp->temp_bytes = tb;
     COMAP_CHECK(ctx, alloc(&mp->temp, tb));
@@ -876,7 +888,7 @@ int comap_median_run(comap_ctx *ctx, MedPlan *mp, hipStream_t st)
         k_med_keys<uint32_t><<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, k0, mp->v0, kr);
         COMAP_LAUNCH_CHECK(ctx);
         COMAP_CHECK(ctx, seg_sort(mp->temp, tb, (const uint32_t *)k0, k1, mp->v0, mp->v1, (int)mp->nitems, mp->njobs,
-                                  mp->seg, mp->seg + 1, st));
+                                  mp->seg, mp->seg + 1, st, mp->wide));
         COMAP_CHECK(ctx, hipMemsetAsync(flag, 0, 4 * (size_t)mp->njobs, st));
         k_med_fix<<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, k1, mp->v1, flag);
         COMAP_LAUNCH_CHECK(ctx);
@@ -885,12 +897,12 @@ int comap_median_run(comap_ctx *ctx, MedPlan *mp, hipStream_t st)
         COMAP_LAUNCH_CHECK(ctx);
         tb = mp->temp_bytes;
         COMAP_CHECK(ctx, seg_sort(mp->temp, tb, (const uint64_t *)mp->k0, mp->k1, mp->v0, mp->v1, (int)mp->nitems,
-                                  mp->njobs, beg, end, st));
+                                  mp->njobs, beg, end, st, mp->wide));
     } else {
         k_med_keys<uint64_t><<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, mp->k0, mp->v0, nullptr);
         COMAP_LAUNCH_CHECK(ctx);
         COMAP_CHECK(ctx, seg_sort(mp->temp, tb, (const uint64_t *)mp->k0, mp->k1, mp->v0, mp->v1, (int)mp->nitems,
-                                  mp->njobs, mp->seg, mp->seg + 1, st));
+                                  mp->njobs, mp->seg, mp->seg + 1, st, mp->wide));
     }
     // k0 (sort keys) is free now: it holds the values in sorted order for the walk
     double *sval = (double *)mp->k0;
