@@ -210,6 +210,7 @@ struct comap_l1_plan {
     double *dw = nullptr;              // [U*4][1024][4] (alpha, kg, kr, ko) of each listed channel
     // per-kernel HIP-event timing (comap_l1_profile)
     bool prof_on = false;
+    int prof_level = 2;                // 1: streaming passes only, 2: every kernel
     std::vector<hipEvent_t> prof_pool;
     std::vector<std::pair<int, int>> prof_rec;   // (kernel id, index of start event)
     double prof_ms[32] = {0};

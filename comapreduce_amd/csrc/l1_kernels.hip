@@ -1355,9 +1355,12 @@ __global__ void __launch_bounds__(256) k_channel_bin(const float *__restrict__ t
 
 // ================================================================== host side
 // HIP events around each launch on the plan's stream (comap_l1_profile)
-static int prof_begin(comap_l1_plan *p, hipStream_t st)
+static int prof_begin(comap_l1_plan *p, int id, hipStream_t st)
 {
     if (!p->prof_on) return -1;
+    // level 1: the three streaming passes only (a bench's timed region: an event pair
+    // costs a few us of gap, too much around every small kernel)
+    if (p->prof_level == 1 && id != KV_MOMENTS && id != KV_BAND_SUMS && id != KV_REGRESS) return -1;
     const int idx = (int)p->prof_rec.size() * 2;
     while ((int)p->prof_pool.size() < idx + 2) {
         hipEvent_t e;
@@ -1377,7 +1380,7 @@ static void prof_end(comap_l1_plan *p, int id, int idx, hipStream_t st)
 
 #define PROF_ON(p, id, st, ...)              \
     do {                                     \
-        const int _pi = prof_begin(p, st);   \
+        const int _pi = prof_begin(p, id, st); \
         __VA_ARGS__;                         \
         prof_end(p, id, _pi, st);            \
     } while (0)
@@ -1387,6 +1390,7 @@ extern "C" int comap_l1_profile(comap_l1_plan *p, int32_t enable)
 {
     if (!p) return -1;
     p->prof_on = enable != 0;
+    p->prof_level = enable >= 2 ? 2 : 1;
     return 0;
 }
 

@@ -312,9 +312,11 @@ class GPUObservation:
     # unless a NaN regression coefficient needs it
     STREAMING = ('moments', 'band_sums', 'regress')
 
-    def profile(self, enable: bool = True):
-        """Record HIP events around every kernel launch of this plan."""
-        N.check(N.lib().comap_l1_profile(self.plan, int(enable)), self.ctx, 'comap_l1_profile')
+    def profile(self, enable=True):
+        """Record HIP events around every kernel launch of this plan (True / 2), around
+        the three streaming passes only (1), or not at all (False / 0)."""
+        level = 2 if enable is True else int(enable)
+        N.check(N.lib().comap_l1_profile(self.plan, level), self.ctx, 'comap_l1_profile')
 
     def profile_collect(self):
         """{kernel: (total_ms, launches)} since the last collect (synchronises)."""

@@ -141,7 +141,8 @@ int comap_l1_channel_bin(comap_l1_plan *plan, int32_t bin_size, const double *we
 int comap_l1_debug_fetch(comap_l1_plan *plan, int32_t what, double *out_host, int64_t n);
 
 /* Per-kernel timing with HIP events recorded on the launching stream around
- * every launch.  collect synchronises, returns per-kernel total ms and launch
+ * every launch (enable = 2) or around the three streaming passes only (enable =
+ * 1: moments, band sums, regress).  collect synchronises, returns per-kernel total ms and launch
  * counts (ids: 0 vane, 1 moments/pass A, 2 atmos fit, 3 coef B, 4 band sums/
  * pass B, 5 sliding median, 6 series sums, 7 regress/pass C, 8 gain weights,
  * 9 coef D, 10 legacy pass D, 11 scan weights, 12 unused, 13 finish) and resets. */
