@@ -25,6 +25,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 using namespace comap;
 
@@ -197,6 +198,9 @@ __global__ void __launch_bounds__(256) k_unit_sums(const int32_t *__restrict__ u
 #ifndef COMAP_A_ALD
 #define COMAP_A_ALD 0   // >0: aligned 16-B loads + lane shuffle, COMAP_A_ALD groups per trip; measured at C2: 2 -> 17.0 ms, 4 -> 22.3 ms vs 8.85 off (parity green)
 #endif
+#ifndef COMAP_A_LDSAIR
+#define COMAP_A_LDSAIR 0   // 1: airmass groups staged through LDS once per block per trip
+#endif
 #ifndef COMAP_A_BADSUM
 // 1: a row's non-finite flag is !isfinite(sum d) -- NaN/Inf propagate through the f64
 // sum and f32 samples cannot overflow it (|x| < 3.4e38, n < 2^31), so the flag is exact
@@ -305,7 +309,50 @@ __global__ void __launch_bounds__(256) k_moments(const float *__restrict__ tod, 
         }
     }
 #endif
-#if COMAP_AUNR > 1
+#if COMAP_AUNR > 1 && COMAP_A_LDSAIR
+    // the block's 4 waves walk the same samples of 16 rows: each trip's airmass groups are
+    // read from L2 once per block into LDS (double-buffered, one barrier per trip) instead
+    // of once per wave.  Trips are block-uniform (whole trips only; the rest below).
+    static_assert(COMAP_AUNR * 64 == 256, "one airmass group of 4 samples per thread");
+    __shared__ double4 air[2][COMAP_AUNR * 64];
+    {
+        int par = 0;
+        for (int kb = hg; kb + 64 * COMAP_AUNR <= n4; kb += 64 * COMAP_AUNR, par ^= 1) {
+            f32x4u xs[COMAP_AUNR][kCPW];
+#pragma unroll
+            for (int j = 0; j < COMAP_AUNR; ++j)
+#pragma unroll
+                for (int r = 0; r < kCPW; ++r) xs[j][r] = ld4a(row0 + (int64_t)r * T + 4 * (kb + 64 * j + lane));
+            {
+                const double *q = a + 4 * (kb + (int)threadIdx.x);
+                air[par][threadIdx.x] = make_double4(q[0], q[1], q[2], q[3]);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < COMAP_AUNR; ++j) {
+                const double4 av = air[par][64 * j + lane];
+                const double a0 = av.x, a1 = av.y, a2 = av.z, a3 = av.w;
+                const double v = a0 - a2;
+#pragma unroll
+                for (int r = 0; r < kCPW; ++r) {
+                    const f32x4u x = xs[j][r];
+                    const double x0 = x.x, x1 = x.y, x2 = x.z, x3 = x.w;
+                    if (!COMAP_A_BADSUM) bad[r] += !isfinite(x.x) + !isfinite(x.y) + !isfinite(x.z) + !isfinite(x.w);
+                    sd[r] += (x0 + x1) + (x2 + x3);
+                    sad[r] = fma(a0, x0, sad[r]);
+                    sad[r] = fma(a1, x1, sad[r]);
+                    sad[r] = fma(a2, x2, sad[r]);
+                    sad[r] = fma(a3, x3, sad[r]);
+                    const double uu = x0 - x2;
+                    su[r] += uu;
+                    suu[r] = fma(uu, uu, suu[r]);
+                    suv[r] = fma(uu, v, suv[r]);
+                }
+            }
+            k = kb + 64 * COMAP_AUNR + lane;
+        }
+    }
+#elif COMAP_AUNR > 1
     // COMAP_AUNR sample groups per lane per trip: every row load of the trip is issued
     // before any is accumulated (same per-lane summation order as the plain loop)
     for (; k + 64 * (COMAP_AUNR - 1) < n4; k += 64 * COMAP_AUNR) {
@@ -356,6 +403,201 @@ __global__ void __launch_bounds__(256) k_moments(const float *__restrict__ tod, 
         const double s0 = wave_sum(sd[r]), s1 = wave_sum(sad[r]), s2 = wave_sum(su[r]);
         const double s3 = wave_sum(suu[r]), s4 = wave_sum(suv[r]);
         const int nb = COMAP_A_BADSUM ? (int)!isfinite(s0) : (int)wave_sum((double)bad[r]);
+        tot += nb;
+        if (lane == 0) {
+            const int64_t idx = (int64_t)u * kBC + b * kChannels + c0 + r;
+            mom[idx] = s0;
+            mom[UC + idx] = s1;
+            mom[2 * UC + idx] = s2;
+            mom[3 * UC + idx] = s3;
+            mom[4 * UC + idx] = s4;
+            rowbad[idx] = nb;
+        }
+    }
+    if (lane == 0 && tot) atomicAdd(nan_count, tot);
+}
+
+// Pass A on 16-B aligned chunks (T % 4 == 0, so every row of a unit shares the
+// residue R = t0 mod 4).  Chunk j of a row = scan samples s = 4j - R .. 4j - R + 3.
+// A stride-4 pair (s, s + 2), s = 4k, has its first sample at element R of chunk k
+// and its second at element R + 2 of chunk k (R < 2) or element R - 2 of chunk k + 1
+// (R >= 2).  For R >= 2 the lane of chunk j takes pair j - 1 and gets element R of
+// chunk j - 1 from the lane below by one DPP row shift (wave_shr:1); lane 0 gets it
+// from the previous group's lane 63 (readlane carry), so every load is aligned and
+// no load is repeated.  The airmass pair term is shifted the same way.  The chunks
+// that are not whole scan samples with a whole pair (at most one at the head and
+// fewer than 64 at the tail) go through a per-sample / per-pair loop.
+#ifndef COMAP_AGRP
+#define COMAP_AGRP 2   // chunk groups per lane per trip (loads in flight = COMAP_AGRP x kCPW)
+#endif
+#ifndef COMAP_A_SCHED
+#define COMAP_A_SCHED 0
+#endif
+constexpr int kDppWaveShr1 = 0x138;
+
+__device__ __forceinline__ int dpp_shr1(int old, int v)
+{
+    return __builtin_amdgcn_update_dpp(old, v, kDppWaveShr1, 0xf, 0xf, false);
+}
+
+__device__ __forceinline__ double dpp_shr1(double old, double v)
+{
+    const int2 o = __builtin_bit_cast(int2, old), x = __builtin_bit_cast(int2, v);
+    return __builtin_bit_cast(double, make_int2(dpp_shr1(o.x, x.x), dpp_shr1(o.y, x.y)));
+}
+
+__device__ __forceinline__ double readlane63(double v)
+{
+    const int2 x = __builtin_bit_cast(int2, v);
+    return __builtin_bit_cast(double, make_int2(__builtin_amdgcn_readlane(x.x, 63), __builtin_amdgcn_readlane(x.y, 63)));
+}
+
+struct MomRow {
+    double sd, sad, su, suu, suv;
+    int bad;
+};
+
+template <int R, int G>
+__device__ __forceinline__ void moments_trip(const float *__restrict__ rb, const double *__restrict__ ab, int64_t T,
+                                             int j, int lane, MomRow (&m)[kCPW], float (&pc)[kCPW], double &apc)
+{
+    f32x4a xs[G][kCPW];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int r = 0; r < kCPW; ++r) xs[g][r] = ld4al(rb + (int64_t)r * T + 4 * (j + 64 * g + lane));
+    // R >= 2: the pair's first sample from the lane below (chunk j - 1), all groups first
+    float pa[G][kCPW];
+    if constexpr (R >= 2) {
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int r = 0; r < kCPW; ++r) {
+                const int e = __float_as_int(xs[g][r][R]);
+                pa[g][r] = __int_as_float(dpp_shr1(__float_as_int(pc[r]), e));
+                pc[r] = __int_as_float(__builtin_amdgcn_readlane(e, 63));
+            }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const double *ap = ab + 4 * (j + 64 * g + lane);
+        const double a0 = ap[0], a1 = ap[1], a2 = ap[2], a3 = ap[3];
+        const double ae[4] = {a0, a1, a2, a3};
+        double v;
+        if constexpr (R < 2) {
+            v = ae[R] - ae[R + 2];
+        } else {
+            const double ap_ = dpp_shr1(apc, ae[R]);
+            apc = readlane63(ae[R]);
+            v = ap_ - ae[R - 2];
+        }
+#pragma unroll
+        for (int r = 0; r < kCPW; ++r) {
+            const f32x4a x = xs[g][r];
+            const float pb = x[R < 2 ? R + 2 : R - 2];
+            const float pa_ = R < 2 ? x[R < 2 ? R : 0] : pa[g][r];
+            const double x0 = x.x, x1 = x.y, x2 = x.z, x3 = x.w;
+            m[r].bad += !isfinite(x.x) + !isfinite(x.y) + !isfinite(x.z) + !isfinite(x.w);
+            m[r].sd += (x0 + x1) + (x2 + x3);
+            m[r].sad = fma(a0, x0, m[r].sad);
+            m[r].sad = fma(a1, x1, m[r].sad);
+            m[r].sad = fma(a2, x2, m[r].sad);
+            m[r].sad = fma(a3, x3, m[r].sad);
+            const double uu = (double)pa_ - (double)pb;
+            m[r].su += uu;
+            m[r].suu = fma(uu, uu, m[r].suu);
+            m[r].suv = fma(uu, v, m[r].suv);
+        }
+#if COMAP_A_SCHED
+        __builtin_amdgcn_sched_barrier(0);   // keep the groups' conversions from all being hoisted
+#endif
+    }
+}
+
+template <int R>
+__device__ __forceinline__ void moments_rows_al(const float *__restrict__ row0, const double *__restrict__ a, int64_t T,
+                                                int n, int lane, MomRow (&m)[kCPW])
+{
+    const float *rb = row0 - R;           // chunk 0, 16-B aligned
+    const double *ab = a - R;
+    const int n4 = n >> 2;
+    const int jA = R > 0 ? 1 : 0;
+    int jB = min((n + R) >> 2, R < 2 ? n4 : n4 + 1);
+    if (jB < jA) jB = jA;
+    float pc[kCPW] = {};                  // R >= 2: element R of the chunk before the group's lane 0
+    double apc = 0.0;
+    if constexpr (R >= 2) {
+#pragma unroll
+        for (int r = 0; r < kCPW; ++r) pc[r] = row0[(int64_t)r * T + 4 * (jA - 1)];
+        apc = a[4 * (jA - 1)];
+    }
+    int j = jA;
+    for (; j + 64 * COMAP_AGRP <= jB; j += 64 * COMAP_AGRP) moments_trip<R, COMAP_AGRP>(rb, ab, T, j, lane, m, pc, apc);
+    for (; j + 64 <= jB; j += 64) moments_trip<R, 1>(rb, ab, T, j, lane, m, pc, apc);
+    // leftovers: samples [0, 4 jA - R) and [4 j - R, n); pairs [0, kA) and [kB, n4)
+    const int hs = min(n, 4 * jA - R), ts = max(hs, 4 * j - R);
+    auto sample = [&](int s) {
+        const double at = a[s];
+#pragma unroll
+        for (int r = 0; r < kCPW; ++r) {
+            const float xf = row0[(int64_t)r * T + s];
+            m[r].bad += !isfinite(xf);
+            m[r].sd += (double)xf;
+            m[r].sad = fma(at, (double)xf, m[r].sad);
+        }
+    };
+    for (int s = lane; s < hs; s += 64) sample(s);
+    for (int s = ts + lane; s < n; s += 64) sample(s);
+    const int kA = min(n4, R < 2 ? jA : jA - 1), kB = max(kA, R < 2 ? j : j - 1);
+    auto pair = [&](int k) {
+        const double v = a[4 * k] - a[4 * k + 2];
+#pragma unroll
+        for (int r = 0; r < kCPW; ++r) {
+            const float *q = row0 + (int64_t)r * T + 4 * k;
+            const double uu = (double)q[0] - (double)q[2];
+            m[r].su += uu;
+            m[r].suu = fma(uu, uu, m[r].suu);
+            m[r].suv = fma(uu, v, m[r].suv);
+        }
+    };
+    for (int k = lane; k < kA; k += 64) pair(k);
+    for (int k = kB + lane; k < n4; k += 64) pair(k);
+}
+
+#ifndef COMAP_A_WPE
+#define COMAP_A_WPE 3   // waves per SIMD the register allocation must allow
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COMAP_A_WPE))) k_moments_al(const float *__restrict__ tod, const double *__restrict__ A,
+                                                    const int32_t *__restrict__ units, int64_t T,
+                                                    double *__restrict__ mom, int64_t UC, int32_t *nan_count,
+                                                    int32_t *__restrict__ rowbad)
+{
+    const int wid = uniform(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int groups_per_band = kChannels / (4 * kCPW);
+    int bid = blockIdx.x;
+    const int g = bid % groups_per_band; bid /= groups_per_band;
+    const int b = bid % kBands;
+    const int u = bid / kBands;
+    const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
+    const int c0 = g * 4 * kCPW + wid * kCPW;
+    const float *row0 = tod + ((int64_t)(f * kBands + b) * kChannels + c0) * T + t0;
+    const double *a = A + (int64_t)f * T + t0;
+    MomRow m[kCPW];
+#pragma unroll
+    for (int r = 0; r < kCPW; ++r) { m[r].sd = m[r].sad = m[r].su = m[r].suu = m[r].suv = 0.0; m[r].bad = 0; }
+    switch (t0 & 3) {
+    case 0: moments_rows_al<0>(row0, a, T, n, lane, m); break;
+    case 1: moments_rows_al<1>(row0, a, T, n, lane, m); break;
+    case 2: moments_rows_al<2>(row0, a, T, n, lane, m); break;
+    default: moments_rows_al<3>(row0, a, T, n, lane, m); break;
+    }
+    int tot = 0;
+#pragma unroll
+    for (int r = 0; r < kCPW; ++r) {
+        const double s0 = wave_sum(m[r].sd), s1 = wave_sum(m[r].sad), s2 = wave_sum(m[r].su);
+        const double s3 = wave_sum(m[r].suu), s4 = wave_sum(m[r].suv);
+        const int nb = (int)wave_sum((double)m[r].bad);
         tot += nb;
         if (lane == 0) {
             const int64_t idx = (int64_t)u * kBC + b * kChannels + c0 + r;
@@ -742,6 +984,99 @@ __global__ void __launch_bounds__(256) k_band_sums(const float *__restrict__ tod
                 const int tl = 256 * g + 4 * lane + e;
                 sg_out[(int64_t)f * T + t0 + r0 + o] = (sg[0][tl] + sg[1][tl]) + (sg[2][tl] + sg[3][tl]);
             }
+        }
+}
+
+// Pass B, one band per block (COMAP_B1): the block's kTile / (256 J) waves cover
+// consecutive 256 J-sample pieces of ONE 1024-sample tile of one band, so each
+// listed channel row is read as one 4 KB run by the whole block while a wave holds
+// only 4 J samples x 4 sums (J = 1: 32 accumulator VGPRs instead of 128, more waves
+// per SIMD).  Per sample the channel order and the FMAs are those of k_band_sums
+// (bit-identical outputs); the gain template is written per band (sgb [F][4][T])
+// and summed over the bands in k_finish in k_band_sums' order.
+#ifndef COMAP_B1
+#define COMAP_B1 0
+#endif
+#ifndef COMAP_KJB1
+#define COMAP_KJB1 1
+#endif
+#ifndef COMAP_BB1
+#define COMAP_BB1 8
+#endif
+template <int J, int BB>
+__global__ void __launch_bounds__(kTile / (4 * J)) k_band_sums1(const float *__restrict__ tod, const double *__restrict__ A,
+                                                          const int32_t *__restrict__ units,
+                                                          const int32_t *__restrict__ tiles, int64_t tile0, int64_t T,
+                                                          const int32_t *__restrict__ dlist,
+                                                          const int32_t *__restrict__ dcnt,
+                                                          const double *__restrict__ dw,
+                                                          const double *__restrict__ bsum, double *__restrict__ mb,
+                                                          double *__restrict__ sr_out, double *__restrict__ so_out,
+                                                          double *__restrict__ sgb)
+{
+    const int b = blockIdx.x % kBands;
+    const int tile = (int)(tile0 + blockIdx.x / kBands);
+    const int u = tiles[2 * tile];
+    const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
+    const int wbase = tiles[2 * tile + 1] + 256 * J * (int)(threadIdx.x >> 6);
+    if (wbase >= n) return;                                     // whole wave past the scan end
+    const int lane = threadIdx.x & 63;
+    const int rl = wbase + 4 * lane;                            // this lane's first sample
+    const int nv0 = n - rl;
+    const float *base = tod + (int64_t)(f * kBands + b) * kChannels * T + t0 + rl;
+    const int ub = u * kBands + b;
+    double am[4 * J], ag[4 * J], ar[4 * J], ao[4 * J];
+#pragma unroll
+    for (int i = 0; i < 4 * J; ++i) am[i] = ag[i] = ar[i] = ao[i] = 0.0;
+    const int32_t *lst = dlist + (int64_t)ub * kChannels;
+    const double *wl = dw + 4 * (int64_t)ub * kChannels;
+    const int cnt = dcnt[ub];
+    auto fma4 = [&](const double *__restrict__ w, const f32x4u (&r)[J]) {
+        const double wa = w[0], wg = w[1], wr = w[2], wo = w[3];
+#pragma unroll
+        for (int g = 0; g < J; ++g)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int i = 4 * g + e;
+                const double x = (double)r[g][e];
+                am[i] = fma(wa, x, am[i]);
+                ag[i] = fma(wg, x, ag[i]);
+                ar[i] = fma(wr, x, ar[i]);
+                ao[i] = fma(wo, x, ao[i]);
+            }
+    };
+    auto run = [&](auto full) {
+        constexpr bool FULL = decltype(full)::value;
+        int j = 0;
+        for (; j + BB <= cnt; j += BB) {
+            f32x4u r[BB][J];
+#pragma unroll
+            for (int q = 0; q < BB; ++q) load_raw<J, FULL>(base + (int64_t)lst[j + q] * T, nv0, r[q]);
+#pragma unroll
+            for (int q = 0; q < BB; ++q) fma4(wl + 4 * (j + q), r[q]);
+        }
+        for (; j < cnt; ++j) {
+            f32x4u r[J];
+            load_raw<J, FULL>(base + (int64_t)lst[j] * T, nv0, r);
+            fma4(wl + 4 * j, r);
+        }
+    };
+    if (n - wbase >= 256 * J) run(std::true_type{});
+    else run(std::false_type{});
+    const double *bs = bsum + 4 * (int64_t)ub;
+    const double beta = bs[0], gamma = bs[1], cn = bs[2];
+    const int64_t rowo = (int64_t)(f * kBands + b) * T + t0 + rl;
+    const double *a = A + (int64_t)f * T + t0 + rl;
+#pragma unroll
+    for (int g = 0; g < J; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int i = 4 * g + e, o = 256 * g + e;
+            if (o >= nv0 || rl + o < 0) continue;   // before the scan: aligned-tile lead-in
+            mb[rowo + o] = cn > 0 ? (am[i] - beta - gamma * a[o]) / cn : NAN;
+            sr_out[rowo + o] = ar[i];
+            so_out[rowo + o] = ao[i];
+            sgb[rowo + o] = ag[i];
         }
 }
 
@@ -1169,7 +1504,8 @@ __global__ void __launch_bounds__(256) k_finish(const int32_t *__restrict__ unit
                                                 int64_t T, const double *__restrict__ A,
                                                 const double *__restrict__ mf, const double *__restrict__ dsum,
                                                 double *__restrict__ tod_out, double *__restrict__ orig_out,
-                                                double *__restrict__ dG, const int32_t *__restrict__ flag)
+                                                double *__restrict__ dG, const int32_t *__restrict__ flag,
+                                                const double *__restrict__ sgb)
 {
     if (*flag != 0) return;                          // mismatch: the legacy passes produce the outputs
     const int u = tiles[2 * blockIdx.x];
@@ -1180,7 +1516,13 @@ __global__ void __launch_bounds__(256) k_finish(const int32_t *__restrict__ unit
         if (r >= n) break;
         const int64_t t = t0 + r;
         const double a = A[(int64_t)f * T + t];
-        double m[kBands], g = dG[(int64_t)f * T + t];
+        double m[kBands], g;
+        if (sgb) {   // k_band_sums1: per-band gain template sums, added in k_band_sums' order
+            const double *q = sgb + (int64_t)f * kBands * T + t;
+            g = (q[0] + q[T]) + (q[2 * T] + q[3 * T]);
+        } else {
+            g = dG[(int64_t)f * T + t];
+        }
 #pragma unroll
         for (int b = 0; b < kBands; ++b) {
             m[b] = mf[(int64_t)(f * kBands + b) * T + t];
@@ -1443,6 +1785,11 @@ extern "C" int comap_l1_plan_create(comap_ctx *ctx, const comap_obs_desc *d, com
     p->ctx = ctx;
     p->F = d->n_feeds; p->S = d->n_scans; p->U = d->n_units; p->T = d->n_samples;
     p->tod = d->tod; p->el = d->el;
+    // pass A on aligned chunks (opt-in, COMAP_A_DPP=1; measured slower) needs 16-B aligned rows
+    {
+        const char *e = getenv("COMAP_A_DPP");
+        p->moments_aligned = p->T % 4 == 0 && (reinterpret_cast<uintptr_t>(p->tod) & 15) == 0 && e && e[0] == '1';
+    }
     p->units_h.assign(d->units_host, d->units_host + 4 * (size_t)d->n_units);
     for (int u = 0; u < p->U; ++u) {
         const int32_t *q = &p->units_h[4 * u];
@@ -1491,6 +1838,11 @@ extern "C" int comap_l1_plan_create(comap_ctx *ctx, const comap_obs_desc *d, com
     rc |= dalloc(ctx, &p->dsum, 16 * (size_t)p->U * kBands);
     rc |= dalloc(ctx, &p->xreg, 2 * (size_t)UC);
     rc |= dalloc(ctx, &p->dG, (size_t)p->F * p->T);
+    {   // pass B with one band per block (COMAP_B1, env overrides): per-band gain template sums
+        int b1 = COMAP_B1;
+        if (const char *e = getenv("COMAP_B1")) b1 = atoi(e);
+        if (b1) rc |= dalloc(ctx, &p->sgb, (size_t)p->F * kBands * p->T);
+    }
     rc |= dalloc(ctx, &p->rowbad, UC);
     rc |= dalloc(ctx, &p->ubs, 4 * (size_t)p->U * kBands);
     rc |= dalloc(ctx, &p->fitsum, 2 * (size_t)UC);
@@ -1563,7 +1915,7 @@ extern "C" int comap_l1_plan_destroy(comap_l1_plan *p)
     void *bufs[] = {p->units, p->tiles, p->tiles_b, p->airmass, p->unit_sums, p->mom,
                     p->nan_count, p->alpha, p->nf, p->bsum, p->mb, p->mf, p->ssum, p->sdm, p->gw,
                     p->gmode, p->kap, p->dsum, p->xreg, p->dG, p->rowbad, p->ubs, p->fitsum, p->oa,
-                    p->flag, p->dlist, p->dcnt, p->dw, p->nanpos, p->nanpos_n, p->vane_dev};
+                    p->flag, p->dlist, p->dcnt, p->dw, p->nanpos, p->nanpos_n, p->vane_dev, p->sgb};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (int g = 0; g < comap_l1_plan::kMaxGroups; ++g) {
@@ -1590,8 +1942,12 @@ static int launch_moments(comap_l1_plan *p)
     const int64_t UC = (int64_t)p->U * kBC;
     COMAP_CHECK(ctx, hipMemsetAsync(p->nan_count, 0, 4, ctx->stream));
     const int64_t grid = (int64_t)p->U * kBands * (kChannels / (4 * kCPW));
-    PROF(p, KV_MOMENTS, k_moments<<<grid, 256, 0, ctx->stream>>>(p->tod, p->airmass, p->units, p->T, p->mom, UC,
-                                                                 p->nan_count, p->rowbad));
+    if (p->moments_aligned)
+        PROF(p, KV_MOMENTS, k_moments_al<<<grid, 256, 0, ctx->stream>>>(p->tod, p->airmass, p->units, p->T, p->mom, UC,
+                                                                        p->nan_count, p->rowbad));
+    else
+        PROF(p, KV_MOMENTS, k_moments<<<grid, 256, 0, ctx->stream>>>(p->tod, p->airmass, p->units, p->T, p->mom, UC,
+                                                                     p->nan_count, p->rowbad));
     COMAP_LAUNCH_CHECK(ctx);
     COMAP_CHECK(ctx, hipMemcpyAsync(p->nan_host, p->nan_count, 4, hipMemcpyDeviceToHost, ctx->stream));
     COMAP_CHECK(ctx, hipEventRecord(p->mom_event, ctx->stream));
@@ -1835,9 +2191,14 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
     for (int g = 0; g < p->ngroups; ++g) {
         const int64_t t0 = p->grpb_tile0[g], nt = p->grpb_tile0[g + 1] - t0;
         const int ub0 = p->grp_u0[g] * kBands, nub = (p->grp_u0[g + 1] - p->grp_u0[g]) * kBands;
-        PROF(p, KV_BAND_SUMS, k_band_sums<<<kSubB * nt, 256, 0, st>>>(p->tod, p->airmass, p->units, p->tiles_b, t0,
-                                                                    p->T, p->dlist, p->dcnt, p->dw, p->bsum,
-                                                                    p->mb, tod_out, orig_out, p->dG));
+        if (p->sgb)
+            PROF(p, KV_BAND_SUMS, (k_band_sums1<COMAP_KJB1, COMAP_BB1><<<kBands * nt, kTile / (4 * COMAP_KJB1), 0, st>>>(
+                                      p->tod, p->airmass, p->units, p->tiles_b, t0, p->T, p->dlist, p->dcnt, p->dw,
+                                      p->bsum, p->mb, tod_out, orig_out, p->sgb)));
+        else
+            PROF(p, KV_BAND_SUMS, k_band_sums<<<kSubB * nt, 256, 0, st>>>(p->tod, p->airmass, p->units, p->tiles_b, t0,
+                                                                        p->T, p->dlist, p->dcnt, p->dw, p->bsum,
+                                                                        p->mb, tod_out, orig_out, p->dG));
         COMAP_LAUNCH_CHECK(ctx);
         COMAP_CHECK(ctx, hipEventRecord(p->ev_b[g], st));
         COMAP_CHECK(ctx, hipStreamWaitEvent(side, p->ev_b[g], 0));
@@ -1867,7 +2228,7 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
                                                                 p->flag));
     COMAP_LAUNCH_CHECK(ctx);
     PROF(p, KV_FINISH, k_finish<<<p->n_tiles, 256, 0, st>>>(p->units, p->tiles, p->T, p->airmass, p->mf, p->dsum,
-                                                            tod_out, orig_out, p->dG, p->flag));
+                                                            tod_out, orig_out, p->dG, p->flag, p->sgb));
     COMAP_LAUNCH_CHECK(ctx);
     PROF(p, KV_SCAN_WEIGHTS, k_scan_weights<<<UB, 256, 0, st>>>(p->units, p->T, tod_out, w_out));
     COMAP_LAUNCH_CHECK(ctx);

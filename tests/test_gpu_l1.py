@@ -324,3 +324,25 @@ def test_nan_fill_leaves_raw_cube(golden_dir):
     again = A.Level1AveragingGainCorrection(level2=l2)
     assert again(data, l2)
     assert np.array_equal(again.tod_cleaned, np.asarray(l2['averaged_tod/tod']), equal_nan=True)
+
+
+def test_scan_alignment_residues_vs_oracle():
+    """Pass A reads 16-B aligned chunks and forms the stride-4 pairs of
+    normalise_data across lanes when t0 mod 4 >= 2 (k_moments_al): scans starting
+    at every residue mod 4, with every length residue and one short scan (no median
+    band), against oracle.l1.reduce_level1 (Level1Averaging.py:642-679)."""
+    import oracle.l1 as ol1
+    T = 59_000
+    gen = synthetic.generate_level1(synthetic.SyntheticConfig(n_feeds=1, n_samples=T, obs_id=21))
+    st = np.zeros(T, dtype=np.int64)
+    for a, b in ((1500, 15502), (16502, 29500), (30500, 43503), (44503, 57503), (58200, 58707)):
+        st[a:b] = 1
+    gen['data']['hk/antenna0/deTracker/lissajous_status'] = st
+    edges = synthetic.scan_edges_from_status(st)
+    assert sorted({int(s) % 4 for s, _ in edges}) == [0, 1, 2, 3]
+    assert sorted({int(e - s) % 4 for s, e in edges}) == [0, 1, 2, 3]
+    l2 = _reduce(level1_from_dict(gen))
+    ref = ol1.reduce_level1(gen['data'])
+    assert np.asarray(l2['averaged_tod/scan_edges']).tolist() == np.asarray(ref['averaged_tod/scan_edges']).tolist()
+    for k in KEYS[2:]:
+        assert relmax(l2[k], ref[k]) < RTOL, k
