@@ -199,7 +199,7 @@ __global__ void __launch_bounds__(256) k_unit_sums(const int32_t *__restrict__ u
 #define COMAP_A_ALD 0   // >0: aligned 16-B loads + lane shuffle, COMAP_A_ALD groups per trip; measured at C2: 2 -> 17.0 ms, 4 -> 22.3 ms vs 8.85 off (parity green)
 #endif
 #ifndef COMAP_A_LDSAIR
-#define COMAP_A_LDSAIR 0   // 1: airmass groups staged through LDS once per block per trip
+#define COMAP_A_LDSAIR 1   // airmass groups staged through LDS once per block per trip; measured at C2: 8.86 -> 8.65 ms
 #endif
 #ifndef COMAP_A_BADSUM
 // 1: a row's non-finite flag is !isfinite(sum d) -- NaN/Inf propagate through the f64
@@ -1119,6 +1119,12 @@ __global__ void __launch_bounds__(256) k_series_sums(int ub0, const int32_t *__r
 #ifndef COMAP_RPW
 #define COMAP_RPW 8
 #endif
+#ifndef COMAP_C_LDSMF
+#define COMAP_C_LDSMF 0   // 1: median-filter groups staged through LDS once per block per 4 trips (measured no faster: 7.89 vs 7.93 ms)
+#endif
+#ifndef COMAP_C_LDSUNR
+#define COMAP_C_LDSUNR 1   // trips unrolled per staged run (loads in flight = COMAP_C_LDSUNR x kRPW)
+#endif
 #ifndef COMAP_CUNR
 #define COMAP_CUNR 1   // sample groups per lane per trip in pass C; measured at C2: 1 -> 7.90 ms, 2 -> 8.07, (RPW 4) 2 -> 8.64, 4 -> 8.39
 #endif
@@ -1135,22 +1141,38 @@ __global__ void __launch_bounds__(256) k_regress(int ub0, const float *__restric
     const int u = ub / kBands, b = ub % kBands;
     const int cnt = dcnt[ub];
     const int j0 = g * 4 * kRPW + wid * kRPW;
-    if (j0 >= cnt || bsum[4 * (int64_t)ub + 3] <= 0) return;
+    if (bsum[4 * (int64_t)ub + 3] <= 0) return;      // band skipped by median_filter (block-uniform)
+#if COMAP_C_LDSMF
+    if (g * 4 * kRPW >= cnt) return;                   // whole block past the list
+    const bool live = j0 < cnt;                        // else: only helps stage the block's mf
+#else
+    if (j0 >= cnt) return;
+#endif
     const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
     const int32_t *lst = dlist + (int64_t)ub * kChannels;
     const float *band = tod + (int64_t)(f * kBands + b) * kChannels * T + t0;
     const float *row[kRPW];
+#if COMAP_C_LDSMF
+    const int jw = live ? j0 : 0;
+#else
+    const int jw = j0;
+#endif
 #pragma unroll
-    for (int r = 0; r < kRPW; ++r) row[r] = band + (int64_t)lst[j0 + r < cnt ? j0 + r : j0] * T;   // pad: re-read
+    for (int r = 0; r < kRPW; ++r) row[r] = band + (int64_t)lst[jw + r < cnt ? jw + r : jw] * T;   // pad: re-read
     const double *m = mf + (int64_t)(f * kBands + b) * T + t0;
     double acc[kRPW];
 #pragma unroll
     for (int r = 0; r < kRPW; ++r) acc[r] = 0.0;
 #if COMAP_ALIGN_C
-    // peel the samples before the first 128-B boundary of row 0 (every row of the
-    // band shares it when T is a multiple of 32), so each wave load covers 8 whole lines
-    const int head = (int)min((int64_t)n, (-(int64_t)(row[0] - tod)) & 31);
+    // peel the samples before the first 128-B boundary of the list's first row (every row
+    // of the band shares it when T is a multiple of 32), so each wave load covers 8 whole
+    // lines; block-uniform in any case
+    const int head = (int)min((int64_t)n, (-(int64_t)(band + (int64_t)lst[0] * T - tod)) & 31);
+#if COMAP_C_LDSMF
+    if (live && lane < head) {
+#else
     if (lane < head) {
+#endif
 #pragma unroll
         for (int r = 0; r < kRPW; ++r) acc[r] = fma(m[lane], (double)row[r][lane], acc[r]);
     }
@@ -1186,6 +1208,42 @@ __global__ void __launch_bounds__(256) k_regress(int ub0, const float *__restric
             }
         }
     }
+#endif
+#if COMAP_C_LDSMF
+    // the block's 4 waves walk the same samples of one (unit, band): each run of 4 trips'
+    // median-filter groups is read from L2 once per block into LDS (double-buffered,
+    // one barrier per 4 trips) instead of once per wave.  Block-uniform trips; waves
+    // whose rows are all padding still take part in the staging.
+    __shared__ double4 mfs[2][256];
+    {
+        int par = 0;
+        for (int kb = 0; kb + 256 <= n4; kb += 256, par ^= 1) {
+            {
+                const double *q = m + 4 * (kb + (int)threadIdx.x);
+                mfs[par][threadIdx.x] = make_double4(q[0], q[1], q[2], q[3]);
+            }
+            __syncthreads();
+            if (live) {
+#pragma unroll COMAP_C_LDSUNR
+                for (int i = 0; i < 4; ++i) {
+                    const int kk = kb + 64 * i + lane;
+                    const double4 mv = mfs[par][64 * i + lane];
+#pragma unroll
+                    for (int r = 0; r < kRPW; ++r) {
+                        const f32x4u x = ld4(row[r] + 4 * kk);
+                        double s = acc[r];
+                        s = fma(mv.x, (double)x.x, s);
+                        s = fma(mv.y, (double)x.y, s);
+                        s = fma(mv.z, (double)x.z, s);
+                        s = fma(mv.w, (double)x.w, s);
+                        acc[r] = s;
+                    }
+                }
+            }
+            k = kb + 256 + lane;
+        }
+    }
+    if (!live) return;
 #endif
     for (; k < n4; k += 64) {
         const double m0 = m[4 * k], m1 = m[4 * k + 1], m2 = m[4 * k + 2], m3 = m[4 * k + 3];
