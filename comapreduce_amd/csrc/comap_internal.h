@@ -127,6 +127,9 @@ struct MedPlan {
     int32_t *rank = nullptr;     // dev [nitems] position -> sorted index
     bool key32 = true;           // sort 32-bit proxies + exact run fix-up (else u64 keys)
     bool wide = false;           // segmented sort with 1024-thread workgroups (few series)
+    bool wm = false;             // walk = wavelet-matrix range order statistics (k_med_wm)
+    int32_t wmL = 0;             // wavelet-matrix levels (bits of the largest rank)
+    size_t wm_smem = 0;          // its dynamic LDS bytes
     int32_t *redo = nullptr;     // dev [3][njobs]: segment re-sort flags, begin, end
     void *krange = nullptr;      // dev [njobs][2] u64: per-series key min, max (proxy scaling)
     void *temp = nullptr;

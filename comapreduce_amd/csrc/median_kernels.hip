@@ -449,6 +449,136 @@ __global__ void __launch_bounds__(LT) k_med_walk(const MedJob *__restrict__ jobs
     }
 }
 
+// ------------------------------------------------------------------ wavelet-matrix walk
+// k_med_wm: one workgroup per segment of consecutive outputs [o0, o1) of one job.  The
+// ranks of the segment's positions P = [c0, c0 + ns), ns = (o1 - o0) + w - 1, are a
+// sequence of L-bit integers; output k needs the r_lo-th (and for even w the next)
+// smallest rank among positions [k, k + w) of it -- a range order statistic.  The
+// workgroup builds the sequence's wavelet matrix in LDS (Claude & Navarro): level l
+// (from the top bit down) holds bit l of every element of the current sequence, packed
+// 32 to a word with the count of zeros before the word, and the next level's sequence
+// is the stable partition of this one by that bit (zeros first).  A query then walks
+// the L levels, each narrowing the range with two rank0 lookups (one LDS read each);
+// the two middle order statistics share their path until the level where they part.
+// Same ranks as the bitmap walk, so the same (bit-exact) values.
+constexpr int kWmThreads = 1024;
+
+__device__ __forceinline__ int wm_rank0(const uint64_t *__restrict__ lv, int i)
+{
+    const uint64_t e = lv[i >> 5];
+    return (int)(e >> 32) + __popc(~(uint32_t)e & ((1u << (i & 31)) - 1u));
+}
+
+__global__ void __launch_bounds__(kWmThreads) k_med_wm(const MedJob *__restrict__ jobs,
+                                                       const SlideSeg *__restrict__ wsegs,
+                                                       const int32_t *__restrict__ seg, const double *__restrict__ sval,
+                                                       const int32_t *__restrict__ rank, int32_t w, int32_t L)
+{
+    extern __shared__ __align__(16) unsigned char smem[];
+    __shared__ int wtot[kWmThreads / 64];
+    __shared__ int zt[32];
+    const SlideSeg sg = wsegs[blockIdx.x];
+    const MedJob job = jobs[sg.job];
+    if (job.gate && *job.gate <= 0.0) return;
+    const int32_t s0 = seg[sg.job];
+    const int c0 = (int)(sg.o0 - job.out_lo);
+    const int nout = (int)(sg.o1 - sg.o0);
+    const int ns = nout + w - 1;
+    const int nw = (ns + 31) >> 5;                 // <= kWmThreads (plan)
+    const int ld = nw + 1;                         // words per level (+ the total-zeros entry)
+    uint64_t *lev = reinterpret_cast<uint64_t *>(smem);                 // [L][ld]
+    uint16_t *S = reinterpret_cast<uint16_t *>(lev + (size_t)L * ld);   // [nw * 32]
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint16_t pad = (uint16_t)((1u << L) - 1u);   // padding sorts last at every level
+    for (int i = tid; i < nw * 32; i += kWmThreads) S[i] = i < ns ? (uint16_t)rank[s0 + c0 + i] : pad;
+    __syncthreads();
+    const bool own = tid < nw;
+    for (int l = L - 1; l >= 0; --l) {
+        uint16_t v[32];
+        uint32_t bits = 0;
+        if (own) {
+            const uint4 *p = reinterpret_cast<const uint4 *>(S + 32 * tid);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint4 x = p[q];
+                const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    v[8 * q + 2 * t] = (uint16_t)(xw[t] & 0xffffu);
+                    v[8 * q + 2 * t + 1] = (uint16_t)(xw[t] >> 16);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 32; ++j) bits |= (uint32_t)((v[j] >> l) & 1u) << j;
+        }
+        const int z = own ? 32 - __popc(bits) : 0;
+        int incl = z;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) wtot[wv] = incl;
+        __syncthreads();
+        int before = 0, Z = 0;
+#pragma unroll
+        for (int u = 0; u < kWmThreads / 64; ++u) {
+            const int t = wtot[u];
+            before += u < wv ? t : 0;
+            Z += t;
+        }
+        const int zpre = before + incl - z;
+        uint64_t *lv = lev + (size_t)l * ld;
+        if (own) lv[tid] = ((uint64_t)(uint32_t)zpre << 32) | bits;
+        if (tid == 0) { lv[nw] = (uint64_t)(uint32_t)Z << 32; zt[l] = Z; }
+        __syncthreads();                           // every read of S (and wtot) is done
+        if (own && l > 0) {
+            const int opre = 32 * tid - zpre;      // ones before this word
+#pragma unroll
+            for (int j = 0; j < 32; ++j) {
+                const uint32_t below = (1u << j) - 1u;
+                const int dst = ((bits >> j) & 1u) ? Z + opre + __popc(bits & below) : zpre + __popc(~bits & below);
+                S[dst] = v[j];
+            }
+        }
+        __syncthreads();
+    }
+    const bool two = (w % 2) == 0;
+    const int r_lo = two ? (w / 2 - 1) : (w / 2);
+    const double *sv = sval + s0;
+    for (int k = tid; k < nout; k += kWmThreads) {
+        int a = k, b = k + w, r = r_lo;
+        int a2 = 0, b2 = 0, r2 = 0;
+        uint32_t v1 = 0, v2 = 0;
+        bool split = false;
+        for (int l = L - 1; l >= 0; --l) {
+            const uint64_t *lv = lev + (size_t)l * ld;
+            const int Z = zt[l];
+            if (split) {                           // the upper statistic on its own path
+                const int za = wm_rank0(lv, a2), zb = wm_rank0(lv, b2), nz = zb - za;
+                if (r2 < nz) { a2 = za; b2 = zb; }
+                else { r2 -= nz; a2 = Z + a2 - za; b2 = Z + b2 - zb; v2 |= 1u << l; }
+            }
+            const int za = wm_rank0(lv, a), zb = wm_rank0(lv, b), nz = zb - za;
+            if (two && !split && r < nz && r + 1 >= nz) {   // the two part here: upper = first one
+                split = true;
+                a2 = Z + a - za; b2 = Z + b - zb; r2 = 0; v2 = v1 | (1u << l);
+                a = za; b = zb;
+            } else if (r < nz) {
+                a = za; b = zb;
+            } else {
+                r -= nz; a = Z + a - za; b = Z + b - zb; v1 |= 1u << l;
+            }
+        }
+        const double lo = sv[v1];
+        double out = lo;
+        if (two) out = (sv[split ? v2 : v1] + lo) / 2.0;
+        job.dst[sg.o0 + k - job.out_lo] = out;
+    }
+}
+
+size_t wm_smem(int L, int nw) { return (size_t)L * (nw + 1) * 8 + (size_t)nw * 64; }
+
 // ------------------------------------------------------------------ sliding sorted window
 // k_med_slide: one workgroup walks a segment of a series chunk by chunk
 // (kSlideL outputs per chunk), keeping the chunk's union window U sorted in
@@ -769,10 +899,14 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
     const int64_t kMinSegs = ms ? atoll(ms) : 0;   // measured: splitting costs more than it fills (off)
     int64_t total_out = 0;
     for (const MedJob &j : jobs_in) total_out += std::max<int64_t>(0, j.out_hi - j.out_lo);
-    int64_t max_out = kMaxOut;
+    // the walk: wavelet matrix (default) or the bitmap walk (COMAP_MEDIAN_WALK=bitmap);
+    // the wavelet matrix keeps ranks in 16 bits, so sub-jobs stay within 65536 positions
+    const char *walk_env = getenv("COMAP_MEDIAN_WALK");
+    mp->wm = !(walk_env && !strcmp(walk_env, "bitmap")) && w <= 16384;
+    int64_t max_out = mp->wm ? std::min<int64_t>(kMaxOut, 65536 - (int64_t)w + 1) : kMaxOut;
     if (kMinSegs > 0 && total_out > 0) {
         const int64_t want = (total_out + kMinSegs - 1) / kMinSegs;
-        max_out = std::min<int64_t>(kMaxOut, std::max<int64_t>(4 * (int64_t)kWalkThreads,
+        max_out = std::min<int64_t>(max_out, std::max<int64_t>(4 * (int64_t)kWalkThreads,
                                                                (want + mp->lc - 1) / mp->lc * mp->lc));
     }
     std::vector<MedJob> jobs;
@@ -812,6 +946,38 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
             wsegs.push_back(sg);
         }
     }
+    if (mp->wm) {
+        // wavelet-matrix segments: short enough that L levels of (nw + 1) words plus the
+        // 16-bit sequence fit the LDS budget, and enough of them to fill the chip
+        int L = 1;
+        while ((int64_t)1 << L < nsmax) ++L;
+        const int64_t budget = 150 * 1024;
+        const int64_t nwcap = std::min<int64_t>(kWmThreads, (budget - 8 * L) / (8 * L + 64));
+        const int64_t seg_cap = nwcap * 32 - (w - 1);
+        const char *te = getenv("COMAP_MEDIAN_WMSEGS");
+        const int64_t target = te ? std::max(1, atoi(te)) : 512;
+        if (L > 16 || seg_cap < 1) {
+            mp->wm = false;
+        } else {
+            wsegs.clear();
+            size_t smax = 0;
+            for (size_t j = 0; j < jobs.size(); ++j) {
+                const int64_t nout = jobs[j].out_hi - jobs[j].out_lo;
+                if (nout <= 0) continue;
+                const int64_t want = total_out > 0 ? (nout * target + total_out - 1) / total_out : 1;
+                const int64_t nseg = std::max<int64_t>((nout + seg_cap - 1) / seg_cap, std::max<int64_t>(1, want));
+                const int64_t len = (nout + nseg - 1) / nseg;
+                for (int64_t o = jobs[j].out_lo; o < jobs[j].out_hi; o += len) {
+                    SlideSeg sg;
+                    sg.job = (int32_t)j; sg.pad_ = 0; sg.o0 = o; sg.o1 = std::min(jobs[j].out_hi, o + len);
+                    wsegs.push_back(sg);
+                    smax = std::max(smax, wm_smem(L, (int)((sg.o1 - sg.o0 + w - 1 + 31) / 32)));
+                }
+            }
+            mp->wmL = L;
+            mp->wm_smem = smax;
+        }
+    }
     mp->nwmax = (int32_t)((nsmax + 31) / 32);
     mp->njobs = (int32_t)jobs.size();
     mp->nitems = seg.back();
@@ -847,6 +1013,12 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
     tb = std::max(tb, tb32);
     mp->temp_bytes = tb;
     COMAP_CHECK(ctx, alloc(&mp->temp, tb));
+    if (mp->wm) {
+        COMAP_CHECK(ctx, hipFuncSetAttribute((const void *)k_med_wm, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)std::max<size_t>(mp->wm_smem, 16)));
+        COMAP_CHECK(ctx, hipStreamSynchronize(st));   // host vectors go out of scope
+        return 0;
+    }
     const size_t sm = walk_smem(mp->nwmax, mp->lc);
     if (sm > 160 * 1024) return comap_fail(ctx, -1, "median plan: LDS budget exceeded");
     const void *wk = mp->lc == 64 ? (const void *)k_med_walk<64> : mp->lc == 128 ? (const void *)k_med_walk<128>
@@ -910,6 +1082,13 @@ int comap_median_run(comap_ctx *ctx, MedPlan *mp, hipStream_t st)
     double *sval = (double *)mp->k0;
     k_med_rank<<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, mp->v1, mp->rank, sval);
     COMAP_LAUNCH_CHECK(ctx);
+    if (mp->wm) {
+        if (mp->nsegs > 0)
+            k_med_wm<<<mp->nsegs, kWmThreads, mp->wm_smem, st>>>(mp->jobs, mp->segs, mp->seg, sval, mp->rank, mp->w,
+                                                                 mp->wmL);
+        COMAP_LAUNCH_CHECK(ctx);
+        return 0;
+    }
     const size_t sm = walk_smem(mp->nwmax, mp->lc);
 #define COMAP_WALK(LT) k_med_walk<LT><<<mp->nsegs, LT, sm, st>>>(mp->jobs, mp->segs, mp->seg, sval, mp->rank, mp->w, \
                                                                  mp->nwmax)

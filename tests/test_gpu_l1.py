@@ -50,11 +50,18 @@ def test_medfilt_dropin_bit_exact(meta, golden_dir):
         assert np.array_equal(x, g[f'medfilt_{seed}_{n}_{w}']), (seed, n, w)
 
 
-@pytest.mark.parametrize('path', ['slide', 'sort'])
+def _median_path(path, monkeypatch):
+    """'slide': the sliding sorted window; 'sort': global sort + wavelet-matrix walk
+    (the default); 'bitmap': global sort + the chunked bitmap walk."""
+    monkeypatch.setenv('COMAP_MEDIAN_PATH', 'slide' if path == 'slide' else 'sort')
+    monkeypatch.setenv('COMAP_MEDIAN_WALK', 'bitmap' if path == 'bitmap' else 'wm')
+
+
+@pytest.mark.parametrize('path', ['slide', 'sort', 'bitmap'])
 def test_medfilt_dropin_ties_and_edges(path, monkeypatch):
-    """Both device median paths: the sliding sorted window (windows up to ~12k)
-    and the global-sort path (every window; forced with COMAP_MEDIAN_PATH=sort)."""
-    monkeypatch.setenv('COMAP_MEDIAN_PATH', path)
+    """Every device median path: the sliding sorted window (windows up to ~12k)
+    and the global-sort path (every window) with either walk."""
+    _median_path(path, monkeypatch)
     from comapreduce_amd.tools.medfilt import medfilt
     rng = np.random.default_rng(9)
     for n, w in [(6000, 6000), (12000, 6000), (7681, 7681), (513, 400), (2048, 2), (100, 1), (3000, 5),
@@ -63,10 +70,10 @@ def test_medfilt_dropin_ties_and_edges(path, monkeypatch):
         assert np.array_equal(medfilt(x.copy(), w), oracle.medfilt(x.copy(), w)), (n, w)
 
 
-@pytest.mark.parametrize('path', ['slide', 'sort'])
+@pytest.mark.parametrize('path', ['slide', 'sort', 'bitmap'])
 def test_medfilt_long_series_split(path, monkeypatch):
     """Series longer than one median sub-job / segment are split internally."""
-    monkeypatch.setenv('COMAP_MEDIAN_PATH', path)
+    _median_path(path, monkeypatch)
     from comapreduce_amd.tools.medfilt import medfilt, medfilt_batch
     rng = np.random.default_rng(10)
     x = np.round(rng.standard_normal(150_001), 2)
@@ -77,15 +84,24 @@ def test_medfilt_long_series_split(path, monkeypatch):
     assert np.array_equal(got, oracle.medfilt(z, 400)[y.size:2 * y.size])
 
 
-@pytest.mark.parametrize('key32,lc,S', [('1', '128', ''), ('0', '128', ''), ('1', '64', ''), ('1', '256', ''),
+@pytest.mark.parametrize('key32,lc,S', [('1', 'wm', ''), ('0', 'wm', ''), ('1', 'wm', '7'), ('1', '128', ''),
+                                        ('0', '128', ''), ('1', '64', ''), ('1', '256', ''),
                                         ('1', '512', ''), ('1', '128', '1'), ('1', '128', '3'), ('1', '64', '16')])
 def test_medfilt_sort_proxy_runs(key32, lc, S, monkeypatch):
     """Global-sort path with 32-bit proxy keys: values that round to the same
     f32 but differ in f64 (short runs: fixed in place; runs > 32: the segment is
-    re-sorted on u64 keys), signed zeros and negative values; u64-key path and
-    the 64/256/512-output walk chunks and 1..16 chunks per walk workgroup for comparison."""
+    re-sorted on u64 keys), signed zeros and negative values; u64-key path; the
+    wavelet-matrix walk (one or several segments per series), and the bitmap walk with
+    64/256/512-output chunks and 1..16 chunks per walk workgroup for comparison."""
     monkeypatch.setenv('COMAP_MEDIAN_PATH', 'sort')
     monkeypatch.setenv('COMAP_MEDIAN_KEY32', key32)
+    if lc == 'wm':
+        monkeypatch.setenv('COMAP_MEDIAN_WALK', 'wm')
+        if S:
+            monkeypatch.setenv('COMAP_MEDIAN_WMSEGS', S)   # segments to fill the chip (splits every series)
+        lc, S = '128', ''
+    else:
+        monkeypatch.setenv('COMAP_MEDIAN_WALK', 'bitmap')
     monkeypatch.setenv('COMAP_MEDIAN_L', lc)
     if S:
         monkeypatch.setenv('COMAP_MEDIAN_S', S)      # chunks per walk workgroup (bitmaps slid between them)
