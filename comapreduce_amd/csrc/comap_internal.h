@@ -130,6 +130,8 @@ struct MedPlan {
     bool wm = false;             // walk = wavelet-matrix range order statistics (k_med_wm)
     int32_t wmL = 0;             // wavelet-matrix levels (bits of the largest rank)
     size_t wm_smem = 0;          // its dynamic LDS bytes
+    int32_t *slo = nullptr;      // dev [njobs] first source index of each job (wavelet-matrix walk: the
+                                 // sort segments hold the distinct sources a job reads, not positions)
     int32_t *redo = nullptr;     // dev [3][njobs]: segment re-sort flags, begin, end
     void *krange = nullptr;      // dev [njobs][2] u64: per-series key min, max (proxy scaling)
     void *temp = nullptr;

@@ -85,9 +85,45 @@ __device__ __forceinline__ double xprime(const MedJob &j, int64_t pos, int h)
     return j.src[q < 0 ? 0 : q];
 }
 
+// Source-index interval [lo, hi) that virtual positions [p0, p1) of a job read (src_index
+// is monotone on each piece and the pieces meet, so the set is one interval: its ends
+// are at the range ends or at the piece boundaries)
+__host__ __device__ inline void src_interval(const MedJob &j, int64_t p0, int64_t p1, int h, int64_t &lo, int64_t &hi)
+{
+    const int64_t n = j.n;
+    auto src = [&](int64_t pos) -> int64_t {
+        if (j.mode == 0) return pos < h ? 0 : (pos >= n ? n - 1 : pos);
+        if (pos < 0) pos = 0;
+        if (pos < n) return n - 1 - pos;
+        if (pos < 2 * n) return pos - n;
+        const int64_t q = 3 * n - 1 - pos;
+        return q < 0 ? 0 : q;
+    };
+    int64_t a = src(p0), b = a;
+    const int64_t pts[6] = {p1 - 1, (int64_t)h - 1, n - 1, n, 2 * n - 1, 2 * n};
+    for (int t = 0; t < 6; ++t)
+        if (pts[t] >= p0 && pts[t] < p1) {
+            const int64_t v = src(pts[t]);
+            a = v < a ? v : a;
+            b = v > b ? v : b;
+        }
+    lo = a;
+    hi = b + 1;
+}
+
+// Element i of job jb's sort segment: with per-job source offsets (slo, the distinct-
+// source layout of the wavelet-matrix walk) source slo[jb] + i, else virtual position
+// base + i.
+__device__ __forceinline__ double seg_elem(const MedJob &job, const int32_t *__restrict__ slo, int jb, int64_t base,
+                                           int h, int64_t i)
+{
+    return slo ? job.src[slo[jb] + i] : xprime(job, base + i, h);
+}
+
 // Per-series range of the u64 keys (kr[2j] = min, kr[2j+1] = max), one workgroup per series.
 __global__ void __launch_bounds__(256) k_med_range(const MedJob *__restrict__ jobs, const int32_t *__restrict__ seg,
-                                                   int32_t njobs, int32_t w, unsigned long long *__restrict__ kr)
+                                                   int32_t njobs, int32_t w, unsigned long long *__restrict__ kr,
+                                                   const int32_t *__restrict__ slo)
 {
     __shared__ unsigned long long s_lo[4], s_hi[4];
     const int jb = blockIdx.x;
@@ -98,7 +134,7 @@ __global__ void __launch_bounds__(256) k_med_range(const MedJob *__restrict__ jo
     const int64_t base = job.out_lo - h;
     unsigned long long lo = ~0ull, hi = 0ull;
     for (int i = threadIdx.x; i < ns; i += blockDim.x) {
-        const unsigned long long k = key_of(xprime(job, base + i, h));
+        const unsigned long long k = key_of(seg_elem(job, slo, jb, base, h, i));
         lo = k < lo ? k : lo;
         hi = k > hi ? k : hi;
     }
@@ -131,7 +167,8 @@ __device__ __forceinline__ uint32_t key32_of(uint64_t k, uint64_t kmin, int shif
 template <typename K>
 __global__ void __launch_bounds__(256) k_med_keys(const MedJob *__restrict__ jobs, const int32_t *__restrict__ seg,
                                                   int32_t njobs, int32_t w, K *__restrict__ keys,
-                                                  int32_t *__restrict__ vals, const unsigned long long *__restrict__ kr)
+                                                  int32_t *__restrict__ vals, const unsigned long long *__restrict__ kr,
+                                                  const int32_t *__restrict__ slo)
 {
     const int jb = blockIdx.y;
     if (jb >= njobs) return;
@@ -148,7 +185,7 @@ __global__ void __launch_bounds__(256) k_med_keys(const MedJob *__restrict__ job
         shift = bits > 32 ? bits - 32 : 0;
     }
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += gridDim.x * blockDim.x) {
-        const uint64_t k = key_of(xprime(job, base + i, h));
+        const uint64_t k = key_of(seg_elem(job, slo, jb, base, h, i));
         if constexpr (sizeof(K) == 4) keys[s0 + i] = key32_of(k, kmin, shift);
         else keys[s0 + i] = k;
         vals[s0 + i] = i;
@@ -162,7 +199,8 @@ constexpr int kFixRun = 32;   // longest run of equal proxies k_med_fix re-sorts
 // the order the 64-bit sort gives.  Longer runs flag the segment for the full re-sort.
 __global__ void __launch_bounds__(256) k_med_fix(const MedJob *__restrict__ jobs, const int32_t *__restrict__ seg,
                                                  int32_t njobs, int32_t w, const uint32_t *__restrict__ skeys,
-                                                 int32_t *__restrict__ svals, int32_t *__restrict__ redo)
+                                                 int32_t *__restrict__ svals, int32_t *__restrict__ redo,
+                                                 const int32_t *__restrict__ slo)
 {
     const int jb = blockIdx.y;
     if (jb >= njobs) return;
@@ -178,12 +216,13 @@ __global__ void __launch_bounds__(256) k_med_fix(const MedJob *__restrict__ jobs
         const MedJob job = jobs[jb];
         const int64_t base = job.out_lo - h;
         const int n = e - i;
-        // the common run: one source element seen at several positions (reflection
-        // padding, medfilt edges) -- equal values, already in position order (stable sort)
+        // the common run: equal values (one source element seen at several positions --
+        // reflection padding, medfilt edges -- or equal samples): their relative order
+        // cannot change any order statistic's value
         {
-            const int64_t si = src_index(job, base + svals[s0 + i], h);
+            const uint64_t k0 = key_of(seg_elem(job, slo, jb, base, h, svals[s0 + i]));
             bool same = true;
-            for (int t = 1; t < n && same; ++t) same = src_index(job, base + svals[s0 + i + t], h) == si;
+            for (int t = 1; t < n && same; ++t) same = key_of(seg_elem(job, slo, jb, base, h, svals[s0 + i + t])) == k0;
             if (same) continue;
         }
         auto before = [](uint64_t ka, int32_t pa, uint64_t kb, int32_t pb) { return ka < kb || (ka == kb && pa < pb); };
@@ -195,7 +234,7 @@ __global__ void __launch_bounds__(256) k_med_fix(const MedJob *__restrict__ jobs
             for (int t = 0; t < 8; ++t) {
                 if (t < n) {
                     pp[t] = svals[s0 + i + t];
-                    kk[t] = key_of(xprime(job, base + pp[t], h));
+                    kk[t] = key_of(seg_elem(job, slo, jb, base, h, pp[t]));
                 } else {
                     kk[t] = ~0ull;
                     pp[t] = 0x7fffffff;
@@ -220,7 +259,7 @@ __global__ void __launch_bounds__(256) k_med_fix(const MedJob *__restrict__ jobs
         int32_t rp[kFixRun];
         for (int t = 0; t < n; ++t) {
             const int32_t p = svals[s0 + i + t];
-            const uint64_t kk = key_of(xprime(job, base + p, h));
+            const uint64_t kk = key_of(seg_elem(job, slo, jb, base, h, p));
             int u = t;
             while (u > 0 && (rk[u - 1] > kk || (rk[u - 1] == kk && rp[u - 1] > p))) {
                 rk[u] = rk[u - 1];
@@ -239,7 +278,8 @@ __global__ void __launch_bounds__(256) k_med_fix(const MedJob *__restrict__ jobs
 __global__ void __launch_bounds__(256) k_med_redo(const MedJob *__restrict__ jobs, const int32_t *__restrict__ seg,
                                                   int32_t njobs, int32_t w, const int32_t *__restrict__ redo,
                                                   uint64_t *__restrict__ keys, int32_t *__restrict__ vals,
-                                                  int32_t *__restrict__ beg, int32_t *__restrict__ end)
+                                                  int32_t *__restrict__ beg, int32_t *__restrict__ end,
+                                                  const int32_t *__restrict__ slo)
 {
     const int jb = blockIdx.y;
     if (jb >= njobs) return;
@@ -254,7 +294,7 @@ __global__ void __launch_bounds__(256) k_med_redo(const MedJob *__restrict__ job
     const int h = w / 2;
     const int64_t base = job.out_lo - h;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += gridDim.x * blockDim.x) {
-        keys[s0 + i] = key_of(xprime(job, base + i, h));
+        keys[s0 + i] = key_of(seg_elem(job, slo, jb, base, h, i));
         vals[s0 + i] = i;
     }
 }
@@ -471,8 +511,9 @@ __device__ __forceinline__ int wm_rank0(const uint64_t *__restrict__ lv, int i)
 
 __global__ void __launch_bounds__(kWmThreads) k_med_wm(const MedJob *__restrict__ jobs,
                                                        const SlideSeg *__restrict__ wsegs,
-                                                       const int32_t *__restrict__ seg, const double *__restrict__ sval,
-                                                       const int32_t *__restrict__ rank, int32_t w, int32_t L)
+                                                       const int32_t *__restrict__ seg,
+                                                       const int32_t *__restrict__ sidx,
+                                                       const int32_t *__restrict__ slo, int32_t w, int32_t L)
 {
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int wtot[kWmThreads / 64];
@@ -480,17 +521,32 @@ __global__ void __launch_bounds__(kWmThreads) k_med_wm(const MedJob *__restrict_
     const SlideSeg sg = wsegs[blockIdx.x];
     const MedJob job = jobs[sg.job];
     if (job.gate && *job.gate <= 0.0) return;
-    const int32_t s0 = seg[sg.job];
+    // the job's sort segment: its distinct sources [sl, sl + nu) in sorted order (sidx holds
+    // source - sl); u(s) = sorted index of source s, so u order refines value order
+    const int32_t s0 = seg[sg.job], nu = seg[sg.job + 1] - s0, sl = slo[sg.job];
     const int c0 = (int)(sg.o0 - job.out_lo);
     const int nout = (int)(sg.o1 - sg.o0);
     const int ns = nout + w - 1;
     const int nw = (ns + 31) >> 5;                 // <= kWmThreads (plan)
     const int ld = nw + 1;                         // words per level (+ the total-zeros entry)
+    const int h = w / 2;
+    const int64_t base = job.out_lo - h;           // virtual position of sort element 0
     uint64_t *lev = reinterpret_cast<uint64_t *>(smem);                 // [L][ld]
-    uint16_t *S = reinterpret_cast<uint16_t *>(lev + (size_t)L * ld);   // [nw * 32]
+    const size_t lbytes = max((size_t)L * ld * 8, (size_t)nw * 64 + 16);
+    uint16_t *S = reinterpret_cast<uint16_t *>(smem + lbytes);          // [nw * 32]
+    uint16_t *uinv = reinterpret_cast<uint16_t *>(smem);                // [b - a], before the levels
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint16_t pad = (uint16_t)((1u << L) - 1u);   // padding sorts last at every level
-    for (int i = tid; i < nw * 32; i += kWmThreads) S[i] = i < ns ? (uint16_t)rank[s0 + c0 + i] : pad;
+    // sequence: u of the source every segment position reads
+    int64_t a, b;
+    src_interval(job, base + c0, base + c0 + ns, h, a, b);
+    for (int i = tid; i < nu; i += kWmThreads) {
+        const int64_t sidx_i = sl + sidx[s0 + i];
+        if (sidx_i >= a && sidx_i < b) uinv[sidx_i - a] = (uint16_t)i;
+    }
+    __syncthreads();
+    for (int i = tid; i < nw * 32; i += kWmThreads)
+        S[i] = i < ns ? uinv[src_index(job, base + c0 + i, h) - a] : pad;
     __syncthreads();
     const bool own = tid < nw;
     for (int l = L - 1; l >= 0; --l) {
@@ -545,7 +601,8 @@ __global__ void __launch_bounds__(kWmThreads) k_med_wm(const MedJob *__restrict_
     }
     const bool two = (w % 2) == 0;
     const int r_lo = two ? (w / 2 - 1) : (w / 2);
-    const double *sv = sval + s0;
+    const int32_t *sp = sidx + s0;
+    auto value = [&](uint32_t u) { return job.src[sl + sp[u]]; };   // value of sorted index u
     for (int k = tid; k < nout; k += kWmThreads) {
         int a = k, b = k + w, r = r_lo;
         int a2 = 0, b2 = 0, r2 = 0;
@@ -570,14 +627,16 @@ __global__ void __launch_bounds__(kWmThreads) k_med_wm(const MedJob *__restrict_
                 r -= nz; a = Z + a - za; b = Z + b - zb; v1 |= 1u << l;
             }
         }
-        const double lo = sv[v1];
+        const double lo = value(v1);
         double out = lo;
-        if (two) out = (sv[split ? v2 : v1] + lo) / 2.0;
+        if (two) out = (value(split ? v2 : v1) + lo) / 2.0;
         job.dst[sg.o0 + k - job.out_lo] = out;
     }
 }
 
-size_t wm_smem(int L, int nw) { return (size_t)L * (nw + 1) * 8 + (size_t)nw * 64; }
+// LDS of a wavelet-matrix segment: the level words (whose space first holds the 16-bit
+// source -> sorted-index table, at most one entry per position) + the 16-bit sequence
+size_t wm_smem(int L, int nw) { return std::max<size_t>((size_t)L * (nw + 1) * 8, (size_t)nw * 64 + 16) + (size_t)nw * 64; }
 
 // ------------------------------------------------------------------ sliding sorted window
 // k_med_slide: one workgroup walks a segment of a series chunk by chunk
@@ -922,14 +981,26 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
             jobs.push_back(sj);
         }
     }
-    std::vector<int32_t> seg(jobs.size() + 1, 0);
-    int64_t nsmax = 0, nchunks = 0;
+    // sort segments: the Ns = n_out + w - 1 virtual positions of each job (bitmap walk), or
+    // for the wavelet-matrix walk the distinct source elements those positions read
+    // (reflection padding and medfilt's edge repeats read some sources several times;
+    // equal values need no order between them, so each source is sorted once)
+    std::vector<int32_t> seg(jobs.size() + 1, 0), slo(jobs.size(), 0);
+    int64_t nsmax = 0, numax = 0, nchunks = 0;
     for (size_t j = 0; j < jobs.size(); ++j) {
         const int64_t nout = jobs[j].out_hi - jobs[j].out_lo;
         const int64_t ns = nout > 0 ? nout + w - 1 : 0;
-        if ((int64_t)seg[j] + ns >= (1ll << 31)) return comap_fail(ctx, -1, "median plan too large");
-        seg[j + 1] = seg[j] + (int32_t)ns;
+        int64_t ne = ns;
+        if (mp->wm && ns > 0) {
+            int64_t a = 0, b = 0;
+            src_interval(jobs[j], jobs[j].out_lo - w / 2, jobs[j].out_lo - w / 2 + ns, w / 2, a, b);
+            slo[j] = (int32_t)a;
+            ne = b - a;
+        }
+        if ((int64_t)seg[j] + ne >= (1ll << 31)) return comap_fail(ctx, -1, "median plan too large");
+        seg[j + 1] = seg[j] + (int32_t)ne;
         nsmax = std::max(nsmax, ns);
+        numax = std::max(numax, ne);
         if (nout > 0) nchunks += (nout + mp->lc - 1) / mp->lc;
     }
     // walk segments of up to S chunks per workgroup (the bitmaps slide from chunk to
@@ -950,14 +1021,14 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
         // wavelet-matrix segments: short enough that L levels of (nw + 1) words plus the
         // 16-bit sequence fit the LDS budget, and enough of them to fill the chip
         int L = 1;
-        while ((int64_t)1 << L < nsmax) ++L;
+        while ((int64_t)1 << L < numax) ++L;
         const int64_t budget = 150 * 1024;
-        const int64_t nwcap = std::min<int64_t>(kWmThreads, (budget - 8 * L) / (8 * L + 64));
+        const int64_t nwcap = std::min<int64_t>(kWmThreads, (budget - 8 * L) / (std::max(8 * L, 64) + 64));
         const int64_t seg_cap = nwcap * 32 - (w - 1);
         const char *te = getenv("COMAP_MEDIAN_WMSEGS");
         const int64_t target = te ? std::max(1, atoi(te)) : 512;
         if (L > 16 || seg_cap < 1) {
-            mp->wm = false;
+            return comap_fail(ctx, -1, "median plan: wavelet-matrix walk does not fit (use COMAP_MEDIAN_WALK=bitmap)");
         } else {
             wsegs.clear();
             size_t smax = 0;
@@ -994,6 +1065,10 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
     COMAP_CHECK(ctx, alloc((void **)&mp->v1, 4 * (size_t)mp->nitems));
     COMAP_CHECK(ctx, alloc((void **)&mp->rank, 4 * (size_t)mp->nitems));
     COMAP_CHECK(ctx, alloc((void **)&mp->redo, 4 * 3 * jobs.size()));   // flags | begin | end
+    if (mp->wm) {
+        COMAP_CHECK(ctx, alloc((void **)&mp->slo, 4 * jobs.size()));
+        COMAP_CHECK(ctx, hipMemcpyAsync(mp->slo, slo.data(), 4 * slo.size(), hipMemcpyHostToDevice, st));
+    }
     COMAP_CHECK(ctx, alloc((void **)&mp->krange, 16 * jobs.size()));    // per-series key min, max
     COMAP_CHECK(ctx, hipMemcpyAsync(mp->jobs, jobs.data(), sizeof(MedJob) * jobs.size(), hipMemcpyHostToDevice, st));
     COMAP_CHECK(ctx, hipMemcpyAsync(mp->seg, seg.data(), 4 * seg.size(), hipMemcpyHostToDevice, st));
@@ -1030,7 +1105,8 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
 
 void comap_median_plan_free(MedPlan *mp)
 {
-    void *b[] = {mp->jobs, mp->seg, mp->k0, mp->k1, mp->v0, mp->v1, mp->rank, mp->temp, mp->segs, mp->redo, mp->krange};
+    void *b[] = {mp->jobs, mp->seg, mp->k0, mp->k1, mp->v0, mp->v1, mp->rank, mp->temp, mp->segs, mp->redo, mp->krange,
+                 mp->slo};
     for (void *p : b)
         if (p) (void)hipFree(p);
     *mp = MedPlan();
@@ -1057,38 +1133,39 @@ int comap_median_run(comap_ctx *ctx, MedPlan *mp, hipStream_t st)
         uint32_t *k0 = (uint32_t *)mp->k0, *k1 = (uint32_t *)mp->k1;
         int32_t *flag = mp->redo, *beg = mp->redo + mp->njobs, *end = beg + mp->njobs;
         unsigned long long *kr = (unsigned long long *)mp->krange;
-        k_med_range<<<mp->njobs, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, kr);
+        k_med_range<<<mp->njobs, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, kr, mp->slo);
         COMAP_LAUNCH_CHECK(ctx);
-        k_med_keys<uint32_t><<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, k0, mp->v0, kr);
+        k_med_keys<uint32_t><<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, k0, mp->v0, kr, mp->slo);
         COMAP_LAUNCH_CHECK(ctx);
         COMAP_CHECK(ctx, seg_sort(mp->temp, tb, (const uint32_t *)k0, k1, mp->v0, mp->v1, (int)mp->nitems, mp->njobs,
                                   mp->seg, mp->seg + 1, st, mp->wide));
         COMAP_CHECK(ctx, hipMemsetAsync(flag, 0, 4 * (size_t)mp->njobs, st));
-        k_med_fix<<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, k1, mp->v1, flag);
+        k_med_fix<<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, k1, mp->v1, flag, mp->slo);
         COMAP_LAUNCH_CHECK(ctx);
         // the flagged segments (if any) again on exact 64-bit keys; the rest are empty ranges
-        k_med_redo<<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, flag, mp->k0, mp->v0, beg, end);
+        k_med_redo<<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, flag, mp->k0, mp->v0, beg, end, mp->slo);
         COMAP_LAUNCH_CHECK(ctx);
         tb = mp->temp_bytes;
         COMAP_CHECK(ctx, seg_sort(mp->temp, tb, (const uint64_t *)mp->k0, mp->k1, mp->v0, mp->v1, (int)mp->nitems,
                                   mp->njobs, beg, end, st, mp->wide));
     } else {
-        k_med_keys<uint64_t><<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, mp->k0, mp->v0, nullptr);
+        k_med_keys<uint64_t><<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, mp->k0, mp->v0, nullptr,
+                                                 mp->slo);
         COMAP_LAUNCH_CHECK(ctx);
         COMAP_CHECK(ctx, seg_sort(mp->temp, tb, (const uint64_t *)mp->k0, mp->k1, mp->v0, mp->v1, (int)mp->nitems,
                                   mp->njobs, mp->seg, mp->seg + 1, st, mp->wide));
+    }
+    if (mp->wm) {   // the wavelet-matrix walk reads the sorted positions directly
+        if (mp->nsegs > 0)
+            k_med_wm<<<mp->nsegs, kWmThreads, mp->wm_smem, st>>>(mp->jobs, mp->segs, mp->seg, mp->v1, mp->slo, mp->w,
+                                                                 mp->wmL);
+        COMAP_LAUNCH_CHECK(ctx);
+        return 0;
     }
     // k0 (sort keys) is free now: it holds the values in sorted order for the walk
     double *sval = (double *)mp->k0;
     k_med_rank<<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, mp->v1, mp->rank, sval);
     COMAP_LAUNCH_CHECK(ctx);
-    if (mp->wm) {
-        if (mp->nsegs > 0)
-            k_med_wm<<<mp->nsegs, kWmThreads, mp->wm_smem, st>>>(mp->jobs, mp->segs, mp->seg, sval, mp->rank, mp->w,
-                                                                 mp->wmL);
-        COMAP_LAUNCH_CHECK(ctx);
-        return 0;
-    }
     const size_t sm = walk_smem(mp->nwmax, mp->lc);
 #define COMAP_WALK(LT) k_med_walk<LT><<<mp->nsegs, LT, sm, st>>>(mp->jobs, mp->segs, mp->seg, sval, mp->rank, mp->w, \
                                                                  mp->nwmax)
