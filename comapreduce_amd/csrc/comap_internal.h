@@ -126,6 +126,7 @@ struct MedPlan {
     int32_t *v0 = nullptr, *v1 = nullptr;
     int32_t *rank = nullptr;     // dev [nitems] position -> sorted index
     bool key32 = true;           // sort 32-bit proxies + exact run fix-up (else u64 keys)
+    int32_t pbits = 32;          // significant proxy bits (radix-sort digit passes = pbits / 8)
     bool wide = false;           // segmented sort with 1024-thread workgroups (few series)
     bool wm = false;             // walk = wavelet-matrix range order statistics (k_med_wm)
     int32_t wmL = 0;             // wavelet-matrix levels (bits of the largest rank)

@@ -168,7 +168,7 @@ template <typename K>
 __global__ void __launch_bounds__(256) k_med_keys(const MedJob *__restrict__ jobs, const int32_t *__restrict__ seg,
                                                   int32_t njobs, int32_t w, K *__restrict__ keys,
                                                   int32_t *__restrict__ vals, const unsigned long long *__restrict__ kr,
-                                                  const int32_t *__restrict__ slo)
+                                                  const int32_t *__restrict__ slo, int pbits = 32)
 {
     const int jb = blockIdx.y;
     if (jb >= njobs) return;
@@ -182,7 +182,7 @@ __global__ void __launch_bounds__(256) k_med_keys(const MedJob *__restrict__ job
         kmin = kr[2 * jb];
         const uint64_t range = kr[2 * jb + 1] - kmin;
         const int bits = range ? 64 - __clzll((long long)range) : 0;
-        shift = bits > 32 ? bits - 32 : 0;
+        shift = bits > pbits ? bits - pbits : 0;
     }
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += gridDim.x * blockDim.x) {
         const uint64_t k = key_of(seg_elem(job, slo, jb, base, h, i));
@@ -870,14 +870,14 @@ using SegSortConfigWide = rocprim::segmented_radix_sort_config<8, rocprim::kerne
                                                                rocprim::DisabledWarpSortConfig, false>;
 template <typename K>
 hipError_t seg_sort(void *tmp, size_t &tb, const K *k0, K *k1, const int32_t *v0, int32_t *v1, int n, int nseg,
-                    const int32_t *beg, const int32_t *end, hipStream_t st, bool wide = false)
+                    const int32_t *beg, const int32_t *end, hipStream_t st, bool wide = false,
+                    unsigned end_bit = 8u * (unsigned)sizeof(K))
 {
     if (wide)
         return rocprim::segmented_radix_sort_pairs<SegSortConfigWide>(tmp, tb, k0, k1, v0, v1, (unsigned)n,
-                                                                      (unsigned)nseg, beg, end, 0u,
-                                                                      8u * (unsigned)sizeof(K), st);
+                                                                      (unsigned)nseg, beg, end, 0u, end_bit, st);
     return rocprim::segmented_radix_sort_pairs<SegSortConfig>(tmp, tb, k0, k1, v0, v1, (unsigned)n, (unsigned)nseg,
-                                                              beg, end, 0u, 8u * (unsigned)sizeof(K), st);
+                                                              beg, end, 0u, end_bit, st);
 }
 
 size_t walk_smem(int nwmax, int lt) { return 4 * (2 * (size_t)lt + 16) + 16 * (size_t)nwmax + 8 * (size_t)lt + 64; }
@@ -943,6 +943,11 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
     if (mp->lc != 64 && mp->lc != 256 && mp->lc != 512) mp->lc = 128;
     const char *k32 = getenv("COMAP_MEDIAN_KEY32");           // 0: sort the full u64 keys directly
     mp->key32 = !(k32 && !strcmp(k32, "0"));
+    // proxy bits: the series' key range is scaled onto this many bits and the radix sort
+    // runs bits / 8 digit passes; fewer bits = one pass less but more proxy collisions
+    // for k_med_fix (measured at C2: 24 bits 1.18 ms of median, 32 bits 1.00 ms)
+    const char *pb = getenv("COMAP_MEDIAN_PBITS");
+    mp->pbits = pb ? std::min(32, std::max(8, atoi(pb) / 8 * 8)) : 32;
     if (w < 1 || w > kMaxWindow) return comap_fail(ctx, -1, "median window must be 1 <= w <= 32768");
     const char *force = getenv("COMAP_MEDIAN_PATH");         // "sort" / "slide": test both paths
     const int mcap = w + kSlideL - 1;
@@ -1135,10 +1140,11 @@ int comap_median_run(comap_ctx *ctx, MedPlan *mp, hipStream_t st)
         unsigned long long *kr = (unsigned long long *)mp->krange;
         k_med_range<<<mp->njobs, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, kr, mp->slo);
         COMAP_LAUNCH_CHECK(ctx);
-        k_med_keys<uint32_t><<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, k0, mp->v0, kr, mp->slo);
+        k_med_keys<uint32_t><<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, k0, mp->v0, kr, mp->slo,
+                                                 mp->pbits);
         COMAP_LAUNCH_CHECK(ctx);
         COMAP_CHECK(ctx, seg_sort(mp->temp, tb, (const uint32_t *)k0, k1, mp->v0, mp->v1, (int)mp->nitems, mp->njobs,
-                                  mp->seg, mp->seg + 1, st, mp->wide));
+                                  mp->seg, mp->seg + 1, st, mp->wide, (unsigned)mp->pbits));
         COMAP_CHECK(ctx, hipMemsetAsync(flag, 0, 4 * (size_t)mp->njobs, st));
         k_med_fix<<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, k1, mp->v1, flag, mp->slo);
         COMAP_LAUNCH_CHECK(ctx);
