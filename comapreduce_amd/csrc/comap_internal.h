@@ -129,6 +129,7 @@ struct MedPlan {
     int32_t pbits = 32;          // significant proxy bits (radix-sort digit passes = pbits / 8)
     bool wide = false;           // segmented sort with 1024-thread workgroups (few series)
     bool wm = false;             // walk = wavelet-matrix range order statistics (k_med_wm)
+    bool wmq = false;            // ... on 2-bit digits (k_med_wm4: half the levels)
     int32_t wmL = 0;             // wavelet-matrix levels (bits of the largest rank)
     size_t wm_smem = 0;          // its dynamic LDS bytes
     int32_t *slo = nullptr;      // dev [njobs] first source index of each job (wavelet-matrix walk: the
