@@ -82,12 +82,13 @@ int comap_row_nanmedian(comap_ctx *ctx, const float *tod, const int64_t *rows_ho
     int64_t *drows = nullptr;
     int32_t *dseg = nullptr;
     uint32_t *k0 = nullptr, *k1 = nullptr;
-    void *tmp = nullptr;
-    COMAP_CHECK(ctx, hipMalloc((void **)&drows, 16 * (size_t)nrows));
-    COMAP_CHECK(ctx, hipMalloc((void **)&dseg, 4 * (size_t)(nrows + 1)));
-    COMAP_CHECK(ctx, hipMalloc((void **)&k0, 4 * (size_t)(items ? items : 1)));
-    COMAP_CHECK(ctx, hipMalloc((void **)&k1, 4 * (size_t)(items ? items : 1)));
-    COMAP_CHECK(ctx, hipMalloc(&tmp, tb ? tb : 8));
+    char *tmp = nullptr;
+    DevTemps tmps(st);   // freed on every return path, after the queued work
+    COMAP_CHECK(ctx, tmps.alloc(&drows, 2 * (size_t)nrows));
+    COMAP_CHECK(ctx, tmps.alloc(&dseg, (size_t)nrows + 1));
+    COMAP_CHECK(ctx, tmps.alloc(&k0, (size_t)items));
+    COMAP_CHECK(ctx, tmps.alloc(&k1, (size_t)items));
+    COMAP_CHECK(ctx, tmps.alloc(&tmp, tb ? tb : 8));
     COMAP_CHECK(ctx, hipMemcpyAsync(drows, rows_host, 16 * (size_t)nrows, hipMemcpyHostToDevice, st));
     COMAP_CHECK(ctx, hipMemcpyAsync(dseg, seg.data(), 4 * (size_t)(nrows + 1), hipMemcpyHostToDevice, st));
     for (int r0 = 0; r0 < nrows; r0 += 65535) {
@@ -100,6 +101,5 @@ int comap_row_nanmedian(comap_ctx *ctx, const float *tod, const int64_t *rows_ho
     k_row_median<<<(nrows + 255) / 256, 256, 0, st>>>(k1, dseg, nrows, med_dev);
     COMAP_LAUNCH_CHECK(ctx);
     COMAP_CHECK(ctx, hipStreamSynchronize(st));
-    (void)hipFree(drows); (void)hipFree(dseg); (void)hipFree(k0); (void)hipFree(k1); (void)hipFree(tmp);
     return 0;
 }

@@ -168,10 +168,11 @@ extern "C" int comap_power_spectra(comap_ctx *ctx, const double *tod, int32_t n_
     ScanJob *djobs = nullptr;
     int rc = 0;
     std::vector<ScanJob> jobs(n_rows);
-    COMAP_CHECK(ctx, hipMalloc((void **)&buf, in_bytes));
-    COMAP_CHECK(ctx, hipMalloc((void **)&X, cx_bytes));
-    COMAP_CHECK(ctx, hipMalloc((void **)&djobs, sizeof(ScanJob) * (size_t)n_rows * n_scans));
-    if (mask) COMAP_CHECK(ctx, hipMalloc((void **)&prev, 4 * (size_t)n_rows * nmax));
+    DevTemps tmps(st);   // freed on every return path, after the queued work
+    COMAP_CHECK(ctx, tmps.alloc(&buf, in_bytes / 8));
+    COMAP_CHECK(ctx, tmps.alloc(&X, cx_bytes / 16));
+    COMAP_CHECK(ctx, tmps.alloc(&djobs, (size_t)n_rows * n_scans));
+    if (mask) COMAP_CHECK(ctx, tmps.alloc(&prev, (size_t)n_rows * nmax));
     for (int k = 0; k < n_scans && rc == 0; ++k) {
         const int64_t s = edges[2 * k];
         const int n = (int)(edges[2 * k + 1] - s);
@@ -204,10 +205,5 @@ extern "C" int comap_power_spectra(comap_ctx *ctx, const double *tod, int32_t n_
         if (hipStreamSynchronize(st) != hipSuccess && rc == 0) rc = comap_fail(ctx, -2, "power spectra failed");
         hipfftDestroy(plan);
     }
-    (void)hipStreamSynchronize(st);
-    (void)hipFree(buf);
-    (void)hipFree(X);
-    (void)hipFree(djobs);
-    if (prev) (void)hipFree(prev);
     return rc;
 }

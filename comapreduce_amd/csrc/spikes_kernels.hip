@@ -195,12 +195,13 @@ extern "C" int comap_spikes(comap_ctx *ctx, const double *tod, int32_t n_rows, i
             if (e > s) { jobs.push_back(r); jobs.push_back(s); jobs.push_back(e - s); }
         }
     const int nj = (int)jobs.size() / 3;
-    COMAP_CHECK(ctx, hipMalloc((void **)&comp, 8 * (size_t)n_rows * T));
-    COMAP_CHECK(ctx, hipMalloc((void **)&mf, 8 * (size_t)n_rows * T));
-    COMAP_CHECK(ctx, hipMalloc((void **)&rms, 8 * (size_t)n_rows));
-    COMAP_CHECK(ctx, hipMalloc((void **)&cnt, 8 * (size_t)n_rows));
-    COMAP_CHECK(ctx, hipMalloc((void **)&gate, 8 * (size_t)(nj + 1)));
-    COMAP_CHECK(ctx, hipMalloc((void **)&djobs, 8 * (size_t)(jobs.size() + 1)));
+    DevTemps tmps(st);   // freed on every return path, after the queued work
+    COMAP_CHECK(ctx, tmps.alloc(&comp, (size_t)n_rows * T));
+    COMAP_CHECK(ctx, tmps.alloc(&mf, (size_t)n_rows * T));
+    COMAP_CHECK(ctx, tmps.alloc(&rms, (size_t)n_rows));
+    COMAP_CHECK(ctx, tmps.alloc(&cnt, (size_t)n_rows));
+    COMAP_CHECK(ctx, tmps.alloc(&gate, (size_t)nj + 1));
+    COMAP_CHECK(ctx, tmps.alloc(&djobs, jobs.size() + 1));
     COMAP_CHECK(ctx, hipMemsetAsync(mask, 0, (size_t)n_rows * T, st));
     if (nj) COMAP_CHECK(ctx, hipMemcpyAsync(djobs, jobs.data(), 8 * jobs.size(), hipMemcpyHostToDevice, st));
     k_compact_nonzero<<<n_rows, 1024, 0, st>>>(tod, T, comp, cnt);
@@ -240,8 +241,5 @@ extern "C" int comap_spikes(comap_ctx *ctx, const double *tod, int32_t n_rows, i
         if (!rc && e != hipSuccess) rc = comap_fail(ctx, -2, hipGetErrorString(e));
         comap_median_plan_free(&mp);
     }
-    (void)hipStreamSynchronize(st);
-    (void)hipFree(comp); (void)hipFree(mf); (void)hipFree(rms); (void)hipFree(cnt); (void)hipFree(gate);
-    (void)hipFree(djobs);
     return rc;
 }
