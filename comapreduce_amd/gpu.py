@@ -37,6 +37,10 @@ def to_device(x, dtype, device):
     if isinstance(x, torch.Tensor):
         t = x.to(device=device, dtype=dtype)
         return t.contiguous()
+    if hasattr(x, 'read_flat'):      # a lazy HDF5 dataset (pipeline/h5file.py): staged from the file
+        if x.dtype == np.dtype(str(dtype).replace('torch.', '')):
+            return upload(x, device)
+        x = x[...]
     a = np.ascontiguousarray(to_host(x))
     if a.nbytes >= UPLOAD_MIN_BYTES and a.dtype == np.dtype(str(dtype).replace('torch.', '')):
         return upload(a, device)
@@ -51,16 +55,23 @@ def upload(a, device, chunk_bytes=UPLOAD_CHUNK, threads=8):
     """Host array -> device tensor through two pinned staging buffers: host threads
     fill one buffer (np.copyto releases the GIL) while the DMA engine drains the
     other on a copy stream, so a Level-1 cube moves at the PCIe rate instead of a
-    pageable copy's.  Synchronises before returning."""
+    pageable copy's.  ``a`` may also be a lazy HDF5 dataset (``read_flat``): the
+    native file layer then reads each flat element range straight into the
+    staging buffer (the ctypes call releases the GIL, so the copy of the
+    previous buffer proceeds meanwhile).  Synchronises before returning."""
     from concurrent.futures import ThreadPoolExecutor
     torch = _torch()
     dev = torch.device(device) if not isinstance(device, int) else torch.device('cuda', device)
-    a = np.ascontiguousarray(a)
-    src = a.reshape(-1)
-    out = torch.empty(a.shape, dtype=getattr(torch, str(a.dtype)), device=dev)
+    lazy = hasattr(a, 'read_flat')
+    if not lazy:
+        a = np.ascontiguousarray(a)
+    src = None if lazy else a.reshape(-1)
+    out = torch.empty(tuple(a.shape), dtype=getattr(torch, str(a.dtype)), device=dev)
     dst = out.view(-1)
-    n = src.size
-    per = max(1, chunk_bytes // a.itemsize)
+    n = int(np.prod(a.shape, dtype=np.int64))
+    if n == 0:
+        return out
+    per = max(1, chunk_bytes // a.dtype.itemsize)
     bufs = [torch.empty(min(per, n), dtype=out.dtype, pin_memory=True) for _ in range(2 if n > per else 1)]
     views = [b.numpy() for b in bufs]
     done = [None] * len(bufs)
@@ -71,9 +82,12 @@ def upload(a, device, chunk_bytes=UPLOAD_CHUNK, threads=8):
             m = min(per, n - off)
             if done[k] is not None:
                 done[k].synchronize()                      # staging buffer k drained
-            step = (m + threads - 1) // threads
-            list(pool.map(lambda s: np.copyto(views[k][s:min(s + step, m)], src[off + s:off + min(s + step, m)]),
-                          range(0, m, step)))
+            if lazy:
+                a.read_flat(off, views[k][:m])
+            else:
+                step = (m + threads - 1) // threads
+                list(pool.map(lambda s: np.copyto(views[k][s:min(s + step, m)], src[off + s:off + min(s + step, m)]),
+                              range(0, m, step)))
             with torch.cuda.stream(stream):
                 dst[off:off + m].copy_(bufs[k][:m], non_blocking=True)
                 done[k] = torch.cuda.Event()

@@ -8,9 +8,13 @@ feature bit decoding, the pre/post-2022 vane temperature).  Datasets may be
 NumPy arrays (host) or torch CUDA tensors (device-resident observations, as
 bench.py uses); the GPU stages accept both.
 
-HDF5 I/O uses h5py when importable.  h5py is absent from this image, so
-``write_data_file``/``read_data_file`` fall back to ``.npz`` containers with
-the same dataset paths (Level-1/Level-2 wire formats are SURVEY §8f row 2).
+HDF5 I/O (the Level-1 / Level-2 wire format) goes through
+the native file layer ``pipeline/h5file.py`` -> ``libcomap_h5.so``
+(include/comap_h5.h, libhdf5): files are real HDF5, readable by h5py and the
+reference.  ``large_datasets`` stay lazy on read (an ``H5Dataset``, as the
+reference keeps the h5py Dataset), so a Level-1 cube is staged from the file
+straight into pinned buffers on its way to the GPU.  A filename ending in
+``.npz`` selects NumPy containers with the same dataset paths instead.
 """
 from __future__ import annotations
 
@@ -24,10 +28,7 @@ from datetime import datetime, timedelta
 import numpy as np
 from scipy.interpolate import interp1d
 
-try:  # optional
-    import h5py  # type: ignore
-except ImportError:  # pragma: no cover - h5py is not in this image
-    h5py = None
+from . import h5file
 
 CALIBRATOR_LIST = ('TauA', 'CasA', 'CygA', 'jupiter', 'sun', 'saturn', 'moon')  # Tools/Coordinates.py:7-15
 MJD_EPOCH = datetime(1858, 11, 17)
@@ -53,6 +54,18 @@ class HDF5Data:
     _data: dict = field(default_factory=dict, repr=False)
     _attrs: dict = field(default_factory=dict, repr=False)
     _source: str = ''
+    hdf5_file: object = field(default=None, repr=False)   # the open H5File (lazy datasets read from it)
+
+    def __del__(self):
+        self.close()
+
+    def close(self):
+        f, self.hdf5_file = getattr(self, 'hdf5_file', None), None
+        if f is not None:
+            try:
+                f.close()
+            except Exception:  # pragma: no cover
+                pass
 
     def __setitem__(self, key, item):
         self._data[key] = item
@@ -89,9 +102,11 @@ class HDF5Data:
 
     # ---------------------------------------------------------------- I/O
     def read_data_file(self, filename: str) -> None:
+        """DataHandling.py:101-108, 168-179: every object's attributes, every
+        dataset read whole except ``large_datasets`` (kept lazy)."""
         logging.info(f'{self.name}: READING {filename}')
         self._source = filename
-        if filename.endswith('.npz') or h5py is None:
+        if filename.endswith('.npz'):
             with np.load(filename, allow_pickle=False) as z:
                 for k in z.files:
                     if k == '__attrs__':
@@ -100,35 +115,44 @@ class HDF5Data:
                 if '__attrs__' in z.files:
                     self._attrs.update(json.loads(str(z['__attrs__'])))
             return
-        with h5py.File(filename, 'r') as h:  # pragma: no cover
-            def visit(name, node):
-                for a, v in node.attrs.items():
-                    self._attrs.setdefault(name, {})[a] = v
-                if isinstance(node, h5py.Dataset):
-                    self._data[name] = node[...]
-            h.visititems(visit)
+        self.close()
+        f = h5file.H5File(filename, 'r')
+        self.hdf5_file = f
+        for name, kind in f.visit():
+            a = f.attrs(name)
+            if a:
+                self._attrs.setdefault(name, {}).update(a)
+            if kind != 'dataset':
+                continue
+            try:
+                self._data[name] = f.dataset(name) if name in self.large_datasets else f.read(name)
+            except h5file.H5Error as e:       # a type this layer does not map (e.g. compound)
+                logging.warning(f'{self.name}: skipping {name}: {e}')
 
     def write_data_file(self, filename: str) -> None:
+        """DataHandling.py:110-139: append to an existing file (replacing the
+        datasets written), skip ``large_datasets``, then the attributes."""
         logging.info(f'{self.name}: WRITING {filename}')
-        out = {k.replace('/', '|'): to_host(v) for k, v in self._data.items()
-               if k not in self.large_datasets and v is not None}
-        if h5py is None or filename.endswith('.npz'):
-            path = filename if filename.endswith('.npz') else filename + '.npz'
+        out = {k: to_host(v) for k, v in self._data.items() if k not in self.large_datasets and v is not None}
+        if filename.endswith('.npz'):
             attrs = {k: {a: (v.tolist() if hasattr(v, 'tolist') else v) for a, v in d.items()}
                      for k, d in self._attrs.items()}
-            np.savez(path, __attrs__=json.dumps(attrs, default=str), **out)
+            np.savez(filename, __attrs__=json.dumps(attrs, default=str),
+                     **{k.replace('/', '|'): v for k, v in out.items()})
             return
-        mode = 'a' if os.path.exists(filename) else 'w'  # pragma: no cover
-        with h5py.File(filename, mode) as h:
+        if self.hdf5_file is not None and os.path.abspath(self.hdf5_file.filename) == os.path.abspath(filename):
+            self.close()                      # lazy datasets of this file are read before it is rewritten
+        with h5file.H5File(filename, 'a' if os.path.exists(filename) else 'w') as h:
             for k, v in out.items():
-                k = k.replace('|', '/')
-                if k in h:
-                    del h[k]
-                h.create_dataset(k, data=v)
+                h.write(k, v)
             for p, d in self._attrs.items():
-                g = h.require_group(p) if p not in h else h[p]
+                if p not in h:
+                    h.require_group(p)
                 for a, v in d.items():
-                    g.attrs[a] = v
+                    h.set_attr(p, a, v)
+        if self.hdf5_file is None:
+            self.hdf5_file = h5file.H5File(filename, 'r')
+            self._source = filename
 
 
 class RepointEdges:

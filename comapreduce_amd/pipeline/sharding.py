@@ -110,7 +110,10 @@ def slice_feeds(data: COMAPLevel1, f_lo: int, f_hi: int, unit_filter=None) -> CO
     within the slice, scan) restricts the device reduction to those units."""
     out = COMAPLevel1(overwrite=data.overwrite, large_datasets=list(data.large_datasets))
     for k, v in data.items():
-        out[k] = v[f_lo:f_hi] if k in FEED_AXIS_PATHS else v
+        if k in FEED_AXIS_PATHS:
+            out[k] = v.rows(f_lo, f_hi) if hasattr(v, 'rows') else v[f_lo:f_hi]   # file-backed: stays lazy
+        else:
+            out[k] = v
     for p, a in data.items(attr=True):
         for k, v in a.items():
             out.set_attrs(p, k, v)

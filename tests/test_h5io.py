@@ -1,0 +1,232 @@
+"""The native HDF5 file layer (include/comap_h5.h, pipeline/h5file.py) and the
+HDF5Data read/write contract on top of it (reference DataHandling.py:101-179).
+
+Pinned two ways, independent of our own reader: (1) tests/golden/ref_gains.hd5
+is the h5py-written data file the reference ships (comancpipeline/data/gains.hd5,
+read by its Data.py:70-72) -- our reads equal the raw little-endian bytes the
+HDF5 tools' ``h5dump -b`` writes out; (2) files we write are listed by ``h5ls``
+and dumped by ``h5dump`` with the types h5py uses (bool enum, vlen UTF-8 str,
+NULLPAD bytes).  CPU only."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from comapreduce_amd.pipeline import h5file as H
+from comapreduce_amd.pipeline.datahandling import COMAPLevel1, COMAPLevel2, HDF5Data
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+H5TOOLS = '/opt/conda/bin'
+
+pytestmark = pytest.mark.skipif(not H.available(), reason='libcomap_h5.so not built (no libhdf5 headers)')
+
+
+def _tool(name):
+    p = os.path.join(H5TOOLS, name)
+    if not os.path.exists(p):
+        pytest.skip(f'{name} not available')
+    return p
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, 'include', 'comap_h5.h')).read()
+    src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+    return sorted(set(re.findall(r'\b(comap_h5_[a-z0-9_]+)\s*\(', src)))
+
+
+def test_every_header_symbol_exported():
+    L = H.lib()
+    assert L.comap_h5_version().startswith(b'comap_h5 (HDF5 1.')
+    missing = [f for f in header_functions() if not hasattr(L, f)]
+    assert not missing, missing
+    assert set(header_functions()) == set(H.EXPORTED)
+
+
+def test_reads_reference_h5py_file(golden_dir, tmp_path):
+    path = os.path.join(golden_dir, 'ref_gains.hd5')
+    with H.H5File(path) as f:
+        assert f.visit() == [('taua', 'group'), ('taua/errors', 'dataset'), ('taua/gains', 'dataset'),
+                             ('taua/obsids', 'dataset')]
+        for name in ('taua/errors', 'taua/gains', 'taua/obsids'):
+            ours = f.read(name)
+            out = tmp_path / (name.replace('/', '_') + '.bin')
+            subprocess.run([_tool('h5dump'), '-d', '/' + name, '-b', 'LE', '-o', str(out), path], check=True,
+                           capture_output=True)
+            ref = np.fromfile(out, dtype='<f8').reshape(ours.shape)
+            assert ours.dtype == np.float64
+            assert np.array_equal(ours, ref, equal_nan=True), name
+        # hyperslab and flat ranges of the same data
+        g = f.read('taua/gains')
+        d = f.dataset('taua/gains')
+        assert d.shape == (521, 20, 8)
+        assert np.array_equal(d[17:400:3, 5, ::-2], g[17:400:3, 5, ::-2], equal_nan=True)
+        flat = g.reshape(-1)
+        for off, n in ((0, flat.size), (7, 1), (159, 161), (160 * 3 - 5, 1000), (flat.size - 3, 3)):
+            o = np.empty(n)
+            d.read_flat(off, o)
+            assert np.array_equal(o, flat[off:off + n], equal_nan=True), (off, n)
+
+
+def test_written_file_is_plain_hdf5(tmp_path):
+    p = str(tmp_path / 'w.h5')
+    rng = np.random.default_rng(0)
+    tod = rng.standard_normal((2, 4, 8, 33)).astype(np.float32)
+    with H.H5File(p, 'w') as f:
+        f.write('spectrometer/tod', tod)
+        f.write('spectrometer/feeds', np.array([1, 20], dtype=np.int64))
+        f.write('flags/mask', np.array([True, False, True]))
+        f.write('meta/name', np.array([b'ab', b'c']))
+        f.write('meta/unicode', np.array(['héllo', 'x']))
+        f.write('meta/scalar', 2.5)
+        f.write('meta/empty', np.zeros((0, 3)))
+        f.require_group('comap')
+        f.set_attr('comap', 'source', 'co2_7,TauA')
+        f.set_attr('comap', 'obsid', 12345)
+        f.set_attr('comap', 'arr', np.arange(3.0))
+        f.set_attr('comap', 'flag', np.bool_(True))
+        f.set_attr('comap', 'raw', b'xyz')
+        f.set_attr('spectrometer/tod', 'units', 'K')
+    ls = subprocess.run([_tool('h5ls'), '-r', p], check=True, capture_output=True, text=True).stdout
+    for line in ('/spectrometer/tod', 'Dataset {2, 4, 8, 33}', '/flags/mask', '/meta/empty', 'Dataset {0, 3}'):
+        assert line in ls, ls
+    dump = subprocess.run([_tool('h5dump'), '-H', '-A', p], check=True, capture_output=True, text=True).stdout
+    assert '"FALSE"            0;' in dump and '"TRUE"             1;' in dump      # h5py's bool enum
+    assert 'STRSIZE H5T_VARIABLE;' in dump and 'CSET H5T_CSET_UTF8;' in dump      # str
+    assert 'STRPAD H5T_STR_NULLPAD;' in dump                                       # bytes
+    assert 'DATASPACE  SCALAR' in dump
+    out = tmp_path / 'tod.bin'
+    subprocess.run([_tool('h5dump'), '-d', '/spectrometer/tod', '-b', 'LE', '-o', str(out), p], check=True,
+                   capture_output=True)
+    assert np.array_equal(np.fromfile(out, dtype='<f4').reshape(tod.shape), tod)
+    with H.H5File(p) as f:
+        assert np.array_equal(f.read('spectrometer/tod'), tod)
+        assert f.read('flags/mask').dtype == np.bool_
+        assert list(f.read('meta/name')) == [b'ab', b'c']
+        assert list(f.read('meta/unicode')) == ['héllo', 'x']
+        assert f.read('meta/scalar').shape == () and float(f.read('meta/scalar')) == 2.5
+        assert f.read('meta/empty').shape == (0, 3)
+        a = f.attrs('comap')
+        assert a['source'] == 'co2_7,TauA' and isinstance(a['source'], str)
+        assert a['obsid'] == 12345 and a['obsid'].dtype == np.int64
+        assert np.array_equal(a['arr'], np.arange(3.0))
+        assert a['flag'] is np.True_ or a['flag'] == True   # noqa: E712
+        assert a['raw'] == b'xyz'
+        assert f.attr('spectrometer/tod', 'units') == 'K'
+
+
+def test_append_replaces_and_errors_are_raised(tmp_path):
+    p = str(tmp_path / 'a.h5')
+    with H.H5File(p, 'w') as f:
+        f.write('x/y', np.arange(5))
+    with H.H5File(p, 'a') as f:
+        f.write('x/y', np.arange(3.0))           # replaced, other type and shape
+        f.write('x/z', np.ones(2))
+        assert 'x/y' in f and 'x/q' not in f and 'nope/deeper' not in f
+    with H.H5File(p) as f:
+        assert np.array_equal(f.read('x/y'), np.arange(3.0))
+        with pytest.raises(H.H5Error, match='no dataset'):
+            f.read('x/missing')
+        with pytest.raises(H.H5Error):
+            f.write('x/w', np.ones(2))           # read-only file
+        with pytest.raises(IndexError):
+            f.dataset('x/y')[5]
+    with pytest.raises(H.H5Error, match='cannot open'):
+        H.H5File(str(tmp_path / 'missing.h5'))
+
+
+def _level1_dict():
+    from comapreduce_amd import synthetic
+    return synthetic.generate_level1(synthetic.SyntheticConfig(n_feeds=2, n_samples=3000, obs_id=5))
+
+
+def test_hdf5data_roundtrip_lazy_large_dataset(tmp_path):
+    """write_data_file / read_data_file (DataHandling.py:101-179): every dataset and
+    attribute comes back; ``large_datasets`` stay lazy and slice like the array."""
+    gen = _level1_dict()
+    p = str(tmp_path / 'comap-0000005.hd5')
+    src = HDF5Data(name='writer')                 # no large_datasets: the cube is written too
+    for k, v in gen['data'].items():
+        src[k] = v
+    for path, a in gen['attrs'].items():
+        for k, v in a.items():
+            src.set_attrs(path, k, v)
+    src.write_data_file(p)
+    d = COMAPLevel1(overwrite=False, large_datasets=['spectrometer/tod'])
+    d.read_data_file(p)
+    assert set(d.keys()) == set(gen['data'])
+    tod = d['spectrometer/tod']
+    assert isinstance(tod, H.H5Dataset) and tod.shape == gen['data']['spectrometer/tod'].shape
+    assert np.array_equal(tod[1, 2, 10:20, 100:140], gen['data']['spectrometer/tod'][1, 2, 10:20, 100:140])
+    for k, v in gen['data'].items():
+        if k != 'spectrometer/tod':
+            assert np.array_equal(np.asarray(d[k]), np.asarray(v)), k
+    for path, a in gen['attrs'].items():
+        for k, v in a.items():
+            got = d.attrs(path, k)
+            assert (got == v) if isinstance(v, str) else np.array_equal(got, v), (path, k)
+    # the reference's derived properties work on the file-backed object
+    assert d.obsid == int(gen['attrs']['comap']['obsid'])
+    assert np.array_equal(np.asarray(d.scan_edges), np.asarray(level1_scan_edges(gen)))
+    d.close()
+
+
+def level1_scan_edges(gen):
+    from comapreduce_amd.pipeline.datahandling import level1_from_dict
+    return level1_from_dict(gen).scan_edges
+
+
+def test_level2_append_across_stages(tmp_path):
+    """Runner.run_tod writes Level-2 after every stage into the same file
+    (Running.py:151-153): later writes append and replace, COMAPLevel2 reopens it."""
+    p = str(tmp_path / 'Level2_obs.hd5')
+    l2 = COMAPLevel2(filename=p)
+    l2['vane/system_temperature'] = np.full((1, 2, 4, 8), 40.0)
+    l2.set_attrs('comap', 'obsid', 7)
+    l2.write_data_file(p)
+    l2['averaged_tod/tod'] = np.zeros((2, 4, 10))
+    l2['vane/system_temperature'] = np.full((1, 2, 4, 8), 41.0)
+    l2.write_data_file(p)
+    again = COMAPLevel2(filename=p)
+    assert set(again.groups) == {'averaged_tod', 'vane'}
+    assert float(np.asarray(again['vane/system_temperature']).max()) == 41.0
+    assert again.obsid == 7
+    ls = subprocess.run([_tool('h5ls'), '-r', p], check=True, capture_output=True, text=True).stdout
+    assert '/averaged_tod/tod' in ls and '/vane/system_temperature' in ls
+
+
+def test_npz_container_still_selected_by_suffix(tmp_path):
+    p = str(tmp_path / 'x.npz')
+    h = HDF5Data()
+    h['a/b'] = np.arange(4)
+    h.set_attrs('a', 'k', 3)
+    h.write_data_file(p)
+    g = HDF5Data()
+    g.read_data_file(p)
+    assert np.array_equal(g['a/b'], np.arange(4)) and g.attrs('a', 'k') == 3
+
+
+def test_feed_rows_view_reads_only_its_range(tmp_path):
+    """A shard of a file-backed cube (sharding.slice_feeds) is a lazy row view:
+    its flat ranges are the shard's own elements."""
+    from comapreduce_amd.pipeline.sharding import slice_feeds
+    p = str(tmp_path / 'c.h5')
+    x = np.random.default_rng(1).standard_normal((5, 4, 3, 11)).astype(np.float32)
+    with H.H5File(p, 'w') as f:
+        f.write('spectrometer/tod', x)
+        f.write('spectrometer/feeds', np.arange(1, 6))
+    d = COMAPLevel1(overwrite=False, large_datasets=['spectrometer/tod'])
+    d.read_data_file(p)
+    part = slice_feeds(d, 1, 4)
+    v = part['spectrometer/tod']
+    assert isinstance(v, H.H5Rows) and v.shape == (3, 4, 3, 11)
+    flat = x[1:4].reshape(-1)
+    for off, n in ((0, flat.size), (5, 40), (131, 1), (flat.size - 7, 7)):
+        o = np.empty(n, np.float32)
+        v.read_flat(off, o)
+        assert np.array_equal(o, flat[off:off + n])
+    assert np.array_equal(np.asarray(v), x[1:4])
+    assert np.array_equal(v.rows(1, 2)[0, 2], x[2, 2])
+    assert np.array_equal(np.asarray(part['spectrometer/feeds']), np.arange(2, 5))
+    d.close()
