@@ -230,3 +230,22 @@ def test_feed_rows_view_reads_only_its_range(tmp_path):
     assert np.array_equal(v.rows(1, 2)[0, 2], x[2, 2])
     assert np.array_equal(np.asarray(part['spectrometer/feeds']), np.arange(2, 5))
     d.close()
+
+
+def test_flat_reads_of_a_large_contiguous_dataset(tmp_path):
+    """Ranges >= 8 MB of a contiguous dataset in a read-only file take the
+    multi-threaded pread path (comap_h5_read_flat); the same ranges from a file
+    opened for writing go through H5Dread: both equal the array."""
+    p = str(tmp_path / 'big.h5')
+    x = np.random.default_rng(2).standard_normal((3, 4, 64, 9001)).astype(np.float32)   # 27.6 MB
+    with H.H5File(p, 'w') as f:
+        f.write('spectrometer/tod', x)
+    flat = x.reshape(-1)
+    cases = ((0, flat.size), (12345, 3_000_001), (flat.size - 2_500_000, 2_500_000))
+    for mode in ('r', 'a'):
+        with H.H5File(p, mode) as f:
+            d = f.dataset('spectrometer/tod')
+            for off, n in cases:
+                o = np.empty(n, np.float32)
+                d.read_flat(off, o)
+                assert np.array_equal(o, flat[off:off + n]), (mode, off, n)
