@@ -208,6 +208,11 @@ struct comap_l1_plan {
     char *vane_pinned = nullptr, *vane_dev = nullptr;
     size_t vane_cap = 0;
     hipEvent_t vane_ev = nullptr;
+    // the vane kernel runs on the side stream beside pass A: it waits only for the main
+    // stream's work up to pass A's launch (pre_a_ev), and the main stream waits for it
+    // (vane_done) before anything queued after the vane call
+    hipEvent_t pre_a_ev = nullptr, vane_done = nullptr;
+    bool pre_a_valid = false;          // pre_a_ev marks the cube as final (no fill/restore since)
     double *ubs = nullptr;             // [U*4][4] fit normal-equation sums n, SA, SAA per (unit, band)
     double *fitsum = nullptr;          // [2][U*4096] masked Sd, SAd (select_time path)
     double *oa = nullptr;              // [U*4096][2] offset/slope L1AGC subtracts

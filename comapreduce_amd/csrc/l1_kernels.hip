@@ -1985,6 +1985,8 @@ extern "C" int comap_l1_plan_destroy(comap_l1_plan *p)
     if (p->nan_host) (void)hipHostFree(p->nan_host);
     if (p->mom_event) (void)hipEventDestroy(p->mom_event);
     if (p->vane_ev) (void)hipEventDestroy(p->vane_ev);
+    if (p->pre_a_ev) (void)hipEventDestroy(p->pre_a_ev);
+    if (p->vane_done) (void)hipEventDestroy(p->vane_done);
     if (p->vane_pinned) (void)hipHostFree(p->vane_pinned);
     for (hipEvent_t e : p->prof_pool) (void)hipEventDestroy(e);
     delete p;
@@ -1998,6 +2000,9 @@ static int launch_moments(comap_l1_plan *p)
 {
     comap_ctx *ctx = p->ctx;
     const int64_t UC = (int64_t)p->U * kBC;
+    if (!p->pre_a_ev) COMAP_CHECK(ctx, hipEventCreateWithFlags(&p->pre_a_ev, hipEventDisableTiming));
+    COMAP_CHECK(ctx, hipEventRecord(p->pre_a_ev, ctx->stream));
+    p->pre_a_valid = true;
     COMAP_CHECK(ctx, hipMemsetAsync(p->nan_count, 0, 4, ctx->stream));
     const int64_t grid = (int64_t)p->U * kBands * (kChannels / (4 * kCPW));
     if (p->moments_aligned)
@@ -2066,6 +2071,7 @@ extern "C" int comap_l1_atmosphere(comap_l1_plan *p, const int32_t *const_el_uni
 {
     if (!p || !fit) return -1;
     COMAP_DEVICE_GUARD(p->ctx);
+    p->pre_a_valid = false;            // a later vane call orders itself after this stage
     comap_ctx *ctx = p->ctx;
     hipStream_t st = ctx->stream;
     int rc = p->prefetched ? wait_moments(p) : run_moments(p);   // pass A, unless comap_l1_prefetch ran it
@@ -2203,6 +2209,7 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
 {
     if (!p || !fit || !tsys0 || !gain0 || !tod_out || !orig_out || !w_out) return -1;
     COMAP_DEVICE_GUARD(p->ctx);
+    p->pre_a_valid = false;            // the NaN fill below writes the cube
     comap_ctx *ctx = p->ctx;
     int rc = 0;
     if (!p->moments_valid && (rc = run_moments(p))) return rc;
@@ -2313,6 +2320,18 @@ extern "C" int comap_l1_vane(comap_l1_plan *p, int64_t vstart, int64_t vlen, con
     const size_t off_c = (size_t)nh * 4, off_ho = (off_c + (size_t)nc * 4 + 15) & ~(size_t)15;
     const size_t off_co = off_ho + (size_t)(FB + 1) * 8, bytes = off_co + (size_t)(FB + 1) * 8;
     hipStream_t st = ctx->stream;
+    // COMAP_VANE_SIDE=1: k_vane (it reads ~1% of the cube) on the side stream beside pass A
+    // (queued by comap_l1_prefetch before the host search) instead of behind it.  Measured
+    // at C2: 27.16 vs 27.09 ms per step -- its scattered row reads slow pass A by as much
+    // as they hide (the kernel itself 0.23 -> 0.59 ms) -- so it stays on the main stream.
+    static const bool use_side = getenv("COMAP_VANE_SIDE") && getenv("COMAP_VANE_SIDE")[0] == '1';
+    hipStream_t vs = (use_side && p->side) ? p->side : st;
+    if (vs != st) {
+        if (!p->pre_a_ev) COMAP_CHECK(ctx, hipEventCreateWithFlags(&p->pre_a_ev, hipEventDisableTiming));
+        if (!p->vane_done) COMAP_CHECK(ctx, hipEventCreateWithFlags(&p->vane_done, hipEventDisableTiming));
+        if (!p->pre_a_valid) COMAP_CHECK(ctx, hipEventRecord(p->pre_a_ev, st));   // no prefetch: the stream's tail
+        COMAP_CHECK(ctx, hipStreamWaitEvent(vs, p->pre_a_ev, 0));
+    }
     if (!p->vane_ev) COMAP_CHECK(ctx, hipEventCreateWithFlags(&p->vane_ev, hipEventDisableTiming));
     else COMAP_CHECK(ctx, hipEventSynchronize(p->vane_ev));   // the previous call's upload has run
     if (bytes > p->vane_cap) {
@@ -2328,18 +2347,22 @@ extern "C" int comap_l1_vane(comap_l1_plan *p, int64_t vstart, int64_t vlen, con
     std::memcpy(p->vane_pinned + off_c, cold_h, (size_t)nc * 4);
     std::memcpy(p->vane_pinned + off_ho, hoff_h, (size_t)(FB + 1) * 8);
     std::memcpy(p->vane_pinned + off_co, coff_h, (size_t)(FB + 1) * 8);
-    COMAP_CHECK(ctx, hipMemcpyAsync(p->vane_dev, p->vane_pinned, bytes, hipMemcpyHostToDevice, st));
-    COMAP_CHECK(ctx, hipEventRecord(p->vane_ev, st));
+    COMAP_CHECK(ctx, hipMemcpyAsync(p->vane_dev, p->vane_pinned, bytes, hipMemcpyHostToDevice, vs));
+    COMAP_CHECK(ctx, hipEventRecord(p->vane_ev, vs));
     const int32_t *dh = (const int32_t *)p->vane_dev;
     const int32_t *dc = (const int32_t *)(p->vane_dev + off_c);
     const int64_t *dho = (const int64_t *)(p->vane_dev + off_ho);
     const int64_t *dco = (const int64_t *)(p->vane_dev + off_co);
-    COMAP_CHECK(ctx, hipMemsetAsync(tsys, 0, (size_t)FB * kChannels * 8, st));
-    COMAP_CHECK(ctx, hipMemsetAsync(gain, 0, (size_t)FB * kChannels * 8, st));
+    COMAP_CHECK(ctx, hipMemsetAsync(tsys, 0, (size_t)FB * kChannels * 8, vs));
+    COMAP_CHECK(ctx, hipMemsetAsync(gain, 0, (size_t)FB * kChannels * 8, vs));
     const int64_t rows = (int64_t)FB * kChannels;
-    PROF(p, KV_VANE, k_vane<<<(rows + 127) / 128, 256, 0, st>>>(p->tod, p->T, p->F, vstart, dh, dho, dc, dco, t_hot,
-                                                            tsys, gain));
+    PROF_ON(p, KV_VANE, vs, k_vane<<<(rows + 127) / 128, 256, 0, vs>>>(p->tod, p->T, p->F, vstart, dh, dho, dc, dco,
+                                                                      t_hot, tsys, gain));
     COMAP_LAUNCH_CHECK(ctx);
+    if (vs != st) {
+        COMAP_CHECK(ctx, hipEventRecord(p->vane_done, vs));
+        COMAP_CHECK(ctx, hipStreamWaitEvent(st, p->vane_done, 0));
+    }
     return 0;
 }
 
@@ -2385,6 +2408,7 @@ extern "C" int comap_l1_channel_bin(comap_l1_plan *p, int32_t bin_size, const do
 {
     if (!p || !weights || !gain || !wsum || !avg || !stddev) return -1;
     COMAP_DEVICE_GUARD(p->ctx);
+    p->pre_a_valid = false;
     comap_ctx *ctx = p->ctx;
     if (bin_size < 1 || kChannels % bin_size) return comap_fail(ctx, -1, "bin_size must divide 1024");
     const int64_t ntile = (p->T + kTile - 1) / kTile;
