@@ -44,6 +44,22 @@ def torch_allreduce(t):
     return t
 
 
+def compact_pixels(pix, npix, allreduce):
+    """(pixel ids relabelled onto the union over ranks of the hit pixels, int32 with
+    -1 kept; the union's pixel ids, increasing).  Pixel npix - 1 is always in the
+    union (the off-map m[-1] reads of Destriper.py:206-213 then land on the union's
+    last slot).  pix: int64 torch tensor on any device; allreduce sums in place."""
+    import torch
+    hit = torch.zeros(npix, dtype=torch.int32, device=pix.device)
+    hit[pix[pix >= 0]] = 1
+    hit[npix - 1] = 1
+    allreduce(hit)
+    keep = hit > 0
+    cid = torch.cumsum(keep.to(torch.int64), 0) - 1
+    comp = torch.where(pix >= 0, cid[pix.clamp(min=0)], torch.full_like(pix, -1))
+    return comp.to(torch.int32), torch.nonzero(keep).reshape(-1)
+
+
 def cg_solve(ops, allreduce, threshold=1e-6, niter=100, h=None, nnum=None):
     """Distributed CG for the destriper offsets.
 
@@ -383,8 +399,39 @@ class DeviceDestriper:
     {'x': [n_bands, N/L], 'iters': [per band], 'maps': {k: [n_bands, npix]}}."""
 
     def __init__(self, pixels, tod, weights, offset_length, npix, device=None, keep=None):
+        self.npix_full, self.hit_index = int(npix), None
+        d = _dist()
+        if d is not None and d.get_world_size() > 1 and os.environ.get('COMAP_DS_COMPACT', '1') != '0':
+            pixels, npix = self._compact(pixels, int(npix), device)
         self.ops = DeviceOps(pixels, tod, weights, offset_length, npix, device, keep)
         self.multi = np.ndim(tod) == 2 if not hasattr(tod, 'dim') else tod.dim() == 2
+
+    def _compact(self, pixels, npix, device):
+        """Across ranks the map numerator is all-reduced every CG iteration
+        (Destriper.py:183-204); only pixels some rank's samples hit can be non-zero.
+        Relabel the pixels onto that union, in increasing pixel order, so every
+        all-reduce carries the hit pixels only ("compact to hit pixels").
+        The relabelling is monotone, and pixel npix - 1 is always kept (off-map
+        samples read m[-1], Destriper.py:206-213): the per-pixel sums, the offsets'
+        spatial order and hence every iterate are unchanged, bit for bit.  Maps are
+        expanded back to npix in solve()."""
+        import torch
+        dev = torch.device('cuda', N.current_device() if device is None else int(device))
+        pix = pixels.to(device=dev, dtype=torch.int64).reshape(-1) if isinstance(pixels, torch.Tensor) else \
+            torch.from_numpy(np.ascontiguousarray(pixels, dtype=np.int64)).to(dev).reshape(-1)
+        if pix.numel() and int(pix.max().item()) >= npix:
+            raise IndexError(f'pixel index {int(pix.max().item())} out of range for a map of {npix} pixels')
+        comp, self.hit_index = compact_pixels(pix, npix, torch_allreduce)
+        return comp, int(self.hit_index.numel())
+
+    def _expand(self, v):
+        """[n_hit * nb] interleaved map on the compacted pixels -> [npix * nb]."""
+        if self.hit_index is None:
+            return v
+        nb = self.ops.nb
+        out = self.ops.torch.zeros((self.npix_full, nb), dtype=v.dtype, device=v.device)
+        out[self.hit_index] = v.reshape(-1, nb)
+        return out.reshape(-1)
 
     def nnz(self):
         return self.ops.nnz()
@@ -410,6 +457,7 @@ class DeviceDestriper:
             ops.div_map(nnum, h, maps['naive'])
             it = it[:ops.n_bands]
             x = ops.natural(x)
+            maps = {k: self._expand(v) for k, v in maps.items()}
         if not self.multi:
             maps['map2'] = maps['weight']
             return {'x': x, 'iters': it[0], 'maps': maps}
