@@ -196,6 +196,7 @@ struct comap_l1_plan {
     double *xreg = nullptr;            // [U*4096][2] regression x0,x1 (debug)
     double *dG = nullptr;              // [F][T]
     double *sgb = nullptr;             // [F][4][T] per-band gain template sums (pass B one band per block)
+    int32_t b1 = 0;                    // pass B variant (COMAP_B1): 0 k_band_sums, else k_band_sums1 layout
     // NaN / calibrator paths
     int32_t *rowbad = nullptr;         // [U*4096] non-finite samples per row (pass A)
     int32_t nan_total = 0;             // total from the last pass A

@@ -1003,22 +1003,31 @@ __global__ void __launch_bounds__(256) k_band_sums(const float *__restrict__ tod
 #ifndef COMAP_BB1
 #define COMAP_BB1 8
 #endif
-template <int J, int BB>
-__global__ void __launch_bounds__(kTile / (4 * J)) k_band_sums1(const float *__restrict__ tod, const double *__restrict__ A,
-                                                          const int32_t *__restrict__ units,
-                                                          const int32_t *__restrict__ tiles, int64_t tile0, int64_t T,
-                                                          const int32_t *__restrict__ dlist,
-                                                          const int32_t *__restrict__ dcnt,
-                                                          const double *__restrict__ dw,
-                                                          const double *__restrict__ bsum, double *__restrict__ mb,
-                                                          double *__restrict__ sr_out, double *__restrict__ so_out,
-                                                          double *__restrict__ sgb)
+// TPB > 1: the block's waves cover TPB consecutive tiles of the band (COMAP_B1=2/4/8:
+// a block then reads TPB x 4 KB of each listed row, TPB times fewer distinct rows in
+// flight across the chip for the same number of resident waves).
+template <int J, int BB, int TPB = 1>
+__global__ void __launch_bounds__(kTile / (4 * J) * TPB) k_band_sums1(const float *__restrict__ tod,
+                                                                const double *__restrict__ A,
+                                                                const int32_t *__restrict__ units,
+                                                                const int32_t *__restrict__ tiles, int64_t tile0,
+                                                                int64_t ntiles, int64_t T,
+                                                                const int32_t *__restrict__ dlist,
+                                                                const int32_t *__restrict__ dcnt,
+                                                                const double *__restrict__ dw,
+                                                                const double *__restrict__ bsum, double *__restrict__ mb,
+                                                                double *__restrict__ sr_out, double *__restrict__ so_out,
+                                                                double *__restrict__ sgb)
 {
+    constexpr int kWpt = kTile / (256 * J);                    // waves per tile
     const int b = blockIdx.x % kBands;
-    const int tile = (int)(tile0 + blockIdx.x / kBands);
+    const int w = uniform((int)(threadIdx.x >> 6));
+    const int64_t tl = (int64_t)(blockIdx.x / kBands) * TPB + w / kWpt;
+    if (tl >= ntiles) return;
+    const int tile = (int)(tile0 + tl);
     const int u = tiles[2 * tile];
     const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
-    const int wbase = tiles[2 * tile + 1] + 256 * J * (int)(threadIdx.x >> 6);
+    const int wbase = tiles[2 * tile + 1] + 256 * J * (w % kWpt);
     if (wbase >= n) return;                                     // whole wave past the scan end
     const int lane = threadIdx.x & 63;
     const int rl = wbase + 4 * lane;                            // this lane's first sample
@@ -1900,6 +1909,7 @@ extern "C" int comap_l1_plan_create(comap_ctx *ctx, const comap_obs_desc *d, com
         int b1 = COMAP_B1;
         if (const char *e = getenv("COMAP_B1")) b1 = atoi(e);
         if (b1) rc |= dalloc(ctx, &p->sgb, (size_t)p->F * kBands * p->T);
+        p->b1 = b1;
     }
     rc |= dalloc(ctx, &p->rowbad, UC);
     rc |= dalloc(ctx, &p->ubs, 4 * (size_t)p->U * kBands);
@@ -2256,11 +2266,21 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
     for (int g = 0; g < p->ngroups; ++g) {
         const int64_t t0 = p->grpb_tile0[g], nt = p->grpb_tile0[g + 1] - t0;
         const int ub0 = p->grp_u0[g] * kBands, nub = (p->grp_u0[g + 1] - p->grp_u0[g]) * kBands;
-        if (p->sgb)
-            PROF(p, KV_BAND_SUMS, (k_band_sums1<COMAP_KJB1, COMAP_BB1><<<kBands * nt, kTile / (4 * COMAP_KJB1), 0, st>>>(
-                                      p->tod, p->airmass, p->units, p->tiles_b, t0, p->T, p->dlist, p->dcnt, p->dw,
-                                      p->bsum, p->mb, tod_out, orig_out, p->sgb)));
-        else
+        if (p->sgb) {
+            // COMAP_B1 = 1: J = COMAP_KJB1 samples groups per lane, one tile per block; 2 / 4: J = 4,
+            // 2 / 4 tiles per block; 8: J = 2, 4 tiles per block
+#define B1_LAUNCH(J, BB, TPB)                                                                                  \
+    PROF(p, KV_BAND_SUMS, (k_band_sums1<J, BB, TPB><<<kBands * ((nt + TPB - 1) / TPB), kTile / (4 * J) * TPB, 0, st>>>( \
+                              p->tod, p->airmass, p->units, p->tiles_b, t0, nt, p->T, p->dlist, p->dcnt, p->dw,   \
+                              p->bsum, p->mb, tod_out, orig_out, p->sgb)))
+            switch (p->b1) {
+            case 2: B1_LAUNCH(4, 2, 2); break;
+            case 4: B1_LAUNCH(4, 2, 4); break;
+            case 8: B1_LAUNCH(2, 4, 4); break;
+            default: B1_LAUNCH(COMAP_KJB1, COMAP_BB1, 1); break;
+            }
+#undef B1_LAUNCH
+        } else
             PROF(p, KV_BAND_SUMS, k_band_sums<<<kSubB * nt, 256, 0, st>>>(p->tod, p->airmass, p->units, p->tiles_b, t0,
                                                                         p->T, p->dlist, p->dcnt, p->dw, p->bsum,
                                                                         p->mb, tod_out, orig_out, p->dG));

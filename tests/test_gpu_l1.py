@@ -363,3 +363,16 @@ def test_scan_alignment_residues_vs_oracle():
     assert np.asarray(l2['averaged_tod/scan_edges']).tolist() == np.asarray(ref['averaged_tod/scan_edges']).tolist()
     for k in KEYS[2:]:
         assert relmax(l2[k], ref[k]) < RTOL, k
+
+
+@pytest.mark.parametrize('b1', ['1', '2', '4', '8'])
+def test_pass_b_layouts_bit_identical(f3_gen, b1, monkeypatch):
+    """Pass B variants (COMAP_B1: one band per block, 1 / 2 / 4 consecutive tiles per
+    block, per-band gain template sums added in k_finish in k_band_sums' band order)
+    give the default kernel's Level-2 outputs bit for bit: per sample the channel
+    order and the FMAs are the same."""
+    ref = _reduce(level1_from_dict(f3_gen))
+    monkeypatch.setenv('COMAP_B1', b1)
+    got = _reduce(level1_from_dict(f3_gen))
+    for k in KEYS:
+        assert np.array_equal(np.asarray(got[k]), np.asarray(ref[k]), equal_nan=True), (b1, k)
