@@ -70,6 +70,7 @@ struct comap_destriper {
     double *cg = nullptr;          // [(4 NO + npix) nb]: x, r, p, q | num
     int32_t *flags = nullptr;      // [2 + 2 nb]
     int32_t *hrow = nullptr;       // [nh] pixel rows with entries (the CG bin skips empty rows)
+    int64_t *hprow = nullptr;      // [nh + 1] their entry ranges: hprow[i] = prow[hrow[i]] (no empty row between)
     int64_t nh = 0;
     int32_t *perm = nullptr;       // [NO] internal offset position -> caller's offset (NULL: identity)
     // COMAP_DS_BIN=lds (measurement variant): LDS-privatised scatter-add bin over pixel
@@ -531,14 +532,15 @@ __global__ void __launch_bounds__(256) k_ds_bin(const int64_t *__restrict__ prow
     const int sub = threadIdx.x & (kBinLanes - 1);
     const int64_t step = (int64_t)gridDim.x * blockDim.x / kBinLanes;
     const int64_t lb = xcd_block(blockIdx.x, gridDim.x);
-    // rows != NULL: only the listed (non-empty) rows, npix = their count
+    // rows != NULL: only the listed (non-empty) rows, npix = their count, and prow holds
+    // their entry ranges (hprow: row i spans [prow[i], prow[i + 1]), no dependent row load)
     for (int64_t i = (lb * blockDim.x + threadIdx.x) / kBinLanes; i < npix; i += step) {
         const int64_t p = rows ? (int64_t)rows[i] : i;
         double s[NB];
 #pragma unroll
         for (int b = 0; b < NB; ++b) s[b] = 0.0;
-        const int64_t e1 = prow[p + 1];
-        for (int64_t k = prow[p] + sub; k < e1; k += kBinLanes * kBinU) {
+        const int64_t e1 = prow[i + 1];
+        for (int64_t k = prow[i] + sub; k < e1; k += kBinLanes * kBinU) {
             int32_t o[kBinU];
             double a[kBinU][NB], xv[kBinU][NB];
 #pragma unroll
@@ -961,15 +963,16 @@ void launch_bin_nb(const comap_destriper *d, hipStream_t st, const double *x, co
     }
     const int64_t np = hit_rows ? d->nh : d->npix;
     const int32_t *rows = hit_rows ? d->hrow : nullptr;
+    const int64_t *rp = hit_rows ? d->hprow : d->prow;
     const int64_t mean = np ? d->nnzp / np : 0;
     const int lanes = mean >= 24 ? 16 : (mean >= 10 ? 8 : 4);
     const unsigned g = grid_for(np * lanes, 65536);
     if (lanes == 16)
-        k_ds_bin<16, NB><<<g, 256, 0, st>>>(d->prow, d->poff, d->pw, x, np, base, hdiv, num, flags, rows);
+        k_ds_bin<16, NB><<<g, 256, 0, st>>>(rp, d->poff, d->pw, x, np, base, hdiv, num, flags, rows);
     else if (lanes == 8)
-        k_ds_bin<8, NB><<<g, 256, 0, st>>>(d->prow, d->poff, d->pw, x, np, base, hdiv, num, flags, rows);
+        k_ds_bin<8, NB><<<g, 256, 0, st>>>(rp, d->poff, d->pw, x, np, base, hdiv, num, flags, rows);
     else
-        k_ds_bin<4, NB><<<g, 256, 0, st>>>(d->prow, d->poff, d->pw, x, np, base, hdiv, num, flags, rows);
+        k_ds_bin<4, NB><<<g, 256, 0, st>>>(rp, d->poff, d->pw, x, np, base, hdiv, num, flags, rows);
 }
 
 void launch_bin(const comap_destriper *d, hipStream_t st, const double *x, const double *base, const double *hdiv,
@@ -1151,12 +1154,15 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         COMAP_CHECK(ctx, hipMemcpyAsync(ph.data(), d->prow, 8 * (size_t)(npix + 1), hipMemcpyDeviceToHost, st));
         COMAP_CHECK(ctx, hipStreamSynchronize(st));
         std::vector<int32_t> hr;
+        std::vector<int64_t> hp;
         for (int64_t q = 0; q < npix; ++q)
-            if (ph[q + 1] > ph[q]) hr.push_back((int32_t)q);
+            if (ph[q + 1] > ph[q]) { hr.push_back((int32_t)q); hp.push_back(ph[q]); }
+        hp.push_back(ph[npix]);
         d->nh = (int64_t)hr.size();
-        if (dalloc(ctx, &d->hrow, hr.size())) return -2;
+        if (dalloc(ctx, &d->hrow, hr.size()) || dalloc(ctx, &d->hprow, hp.size())) return -2;
         if (!hr.empty())
             COMAP_CHECK(ctx, hipMemcpyAsync(d->hrow, hr.data(), 4 * hr.size(), hipMemcpyHostToDevice, st));
+        COMAP_CHECK(ctx, hipMemcpyAsync(d->hprow, hp.data(), 8 * hp.size(), hipMemcpyHostToDevice, st));
         COMAP_CHECK(ctx, hipStreamSynchronize(st));
     }
     rc |= dalloc(ctx, &d->poff, d->nnzp);
@@ -1200,7 +1206,7 @@ extern "C" int comap_destripe_destroy(comap_destriper *d)
     COMAP_DEVICE_GUARD(d->ctx);
     if (d->cs) (void)hipStreamSynchronize(d->cs);
     void *b[] = {d->orow, d->opix, d->ow, d->ws, d->tw, d->prow, d->poff, d->pw, d->h, d->hits, d->nnum, d->part, d->scal,
-                 d->cg, d->flags, d->hrow, d->perm, d->ppix};
+                 d->cg, d->flags, d->hrow, d->hprow, d->perm, d->ppix};
     for (void *p : b)
         if (p) (void)hipFree(p);
     if (d->flags_host) (void)hipHostFree(d->flags_host);
