@@ -62,6 +62,12 @@ _SIGS = {
     'comap_destripe_dist_project': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     'comap_destripe_dist_update': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     'comap_destripe_dist_direction': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    'comap_destripe_dist_parts': (c_int32, []),
+    'comap_destripe_dist_project_parts': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                                  c_void_p]),
+    'comap_destripe_dist_update_fused': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                                 c_void_p, c_void_p, c_void_p]),
+    'comap_destripe_dist_direction_fused': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     'comap_destripe_create_bands': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32,
                                             c_int64, c_int32, ctypes.POINTER(c_void_p)]),
     'comap_destripe_destroy': (c_int, [c_void_p]),

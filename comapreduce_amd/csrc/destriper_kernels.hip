@@ -191,7 +191,8 @@ __device__ __forceinline__ double block_final_sum(const double *__restrict__ par
 // same per-band order and result, with every band's loads in flight together.
 // red: 4 NB doubles.
 template <int NB>
-__device__ __forceinline__ void block_final_sums(const double *__restrict__ part, int n, double *red, double (&out)[NB])
+__device__ __forceinline__ void block_final_sums(const double *__restrict__ part, int n, double *red, double (&out)[NB],
+                                                 int64_t stride = kPartMax)
 {
     double acc[NB];
 #pragma unroll
@@ -203,7 +204,7 @@ __device__ __forceinline__ void block_final_sums(const double *__restrict__ part
 #pragma unroll
         for (int b = 0; b < NB; ++b)
 #pragma unroll
-            for (int k = 0; k < kB; ++k) v[b][k] = part[(int64_t)b * kPartMax + i + k * 256];
+            for (int k = 0; k < kB; ++k) v[b][k] = part[(int64_t)b * stride + i + k * 256];
 #pragma unroll
         for (int b = 0; b < NB; ++b)
 #pragma unroll
@@ -211,7 +212,7 @@ __device__ __forceinline__ void block_final_sums(const double *__restrict__ part
     }
     for (; i < n; i += 256) {
 #pragma unroll
-        for (int b = 0; b < NB; ++b) acc[b] += part[(int64_t)b * kPartMax + i];
+        for (int b = 0; b < NB; ++b) acc[b] += part[(int64_t)b * stride + i];
     }
 #pragma unroll
     for (int b = 0; b < NB; ++b) acc[b] = wave_sum(acc[b]);
@@ -223,6 +224,17 @@ __device__ __forceinline__ void block_final_sums(const double *__restrict__ part
     __syncthreads();
 #pragma unroll
     for (int b = 0; b < NB; ++b) out[b] = (red[4 * b] + red[4 * b + 1]) + (red[4 * b + 2] + red[4 * b + 3]);
+}
+
+// Partial slots [used, stride) of every band set to 0 (by one block).  The multi-rank
+// partial buffers (stride kDistParts) are all-reduced in place, so a rank whose grid
+// is smaller than another's must clear the slots it does not write each time.
+template <int NB>
+__device__ __forceinline__ void zero_tail(double *__restrict__ part, int64_t stride, int64_t used)
+{
+    for (int64_t t = used + threadIdx.x; t < stride; t += blockDim.x)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) part[(int64_t)b * stride + t] = 0.0;
 }
 
 // Block partial (4 waves) of a per-thread accumulator; thread 0 writes *out.
@@ -238,7 +250,7 @@ __device__ __forceinline__ void block_partial(double acc, double *red, double *o
 // block_partial of NB accumulators with one pair of barriers; band b's partial goes to
 // part[b kPartMax] (same value as block_partial per band).  red: 4 NB doubles.
 template <int NB>
-__device__ __forceinline__ void block_partials(double (&acc)[NB], double *red, double *part)
+__device__ __forceinline__ void block_partials(double (&acc)[NB], double *red, double *part, int64_t stride = kPartMax)
 {
 #pragma unroll
     for (int b = 0; b < NB; ++b) acc[b] = wave_sum(acc[b]);
@@ -251,7 +263,7 @@ __device__ __forceinline__ void block_partials(double (&acc)[NB], double *red, d
     if (threadIdx.x == 0) {
 #pragma unroll
         for (int b = 0; b < NB; ++b)
-            part[(int64_t)b * kPartMax] = (red[4 * b] + red[4 * b + 1]) + (red[4 * b + 2] + red[4 * b + 3]);
+            part[(int64_t)b * stride] = (red[4 * b] + red[4 * b + 1]) + (red[4 * b + 2] + red[4 * b + 3]);
     }
 }
 
@@ -648,7 +660,8 @@ __global__ void __launch_bounds__(256) k_ds_project(const int64_t *__restrict__ 
                                                     const double *__restrict__ tw, const double *__restrict__ x,
                                                     const double *__restrict__ num, const double *__restrict__ h,
                                                     int64_t NO, int64_t npix, double *__restrict__ y,
-                                                    double *__restrict__ dot_part, const int32_t *__restrict__ flags)
+                                                    double *__restrict__ dot_part, const int32_t *__restrict__ flags,
+                                                    int64_t pstride = kPartMax)
 {
     __shared__ double red[4 * NB];
     if (cg_done(flags)) return;
@@ -724,7 +737,8 @@ __global__ void __launch_bounds__(256) k_ds_project(const int64_t *__restrict__ 
         }
     }
     if (dot_part) {
-        block_partials<NB>(acc, red, dot_part + blockIdx.x);
+        block_partials<NB>(acc, red, dot_part + blockIdx.x, pstride);
+        if (pstride < kPartMax && blockIdx.x == 0) zero_tail<NB>(dot_part, pstride, gridDim.x);
     }
 }
 
@@ -854,13 +868,13 @@ __global__ void __launch_bounds__(256) k_cg_update_fused(double *__restrict__ sc
                                                          int npq, double *__restrict__ x, double *__restrict__ r,
                                                          const double *__restrict__ p, const double *__restrict__ q,
                                                          int64_t n, double *__restrict__ part_rr,
-                                                         const int32_t *__restrict__ flags)
+                                                         const int32_t *__restrict__ flags, int64_t pstride = kPartMax)
 {
     __shared__ double red[4 * NB];
     if (cg_done(flags)) return;
     double pq[NB], rr[NB], a[NB], acc[NB];
     bool live[NB];
-    block_final_sums<NB>(part_pq, npq, red, pq);
+    block_final_sums<NB>(part_pq, npq, red, pq, pstride);
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
         rr[b] = scal[3 * NB + b];
@@ -870,7 +884,8 @@ __global__ void __launch_bounds__(256) k_cg_update_fused(double *__restrict__ sc
     }
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         update_row<NB>(x + i * NB, r + i * NB, p + i * NB, q + i * NB, a, live, acc);
-    block_partials<NB>(acc, red, part_rr + blockIdx.x);
+    block_partials<NB>(acc, red, part_rr + blockIdx.x, pstride);
+    if (pstride < kPartMax && blockIdx.x == 0) zero_tail<NB>(part_rr, pstride, gridDim.x);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
 #pragma unroll
         for (int b = 0; b < NB; ++b)
@@ -881,13 +896,13 @@ __global__ void __launch_bounds__(256) k_cg_update_fused(double *__restrict__ sc
 template <int NB>
 __global__ void __launch_bounds__(256) k_cg_direction_fused(double *__restrict__ scal, const double *__restrict__ part_rr,
                                                             int nrr, double *__restrict__ p, const double *__restrict__ r,
-                                                            int64_t n, int32_t *flags)
+                                                            int64_t n, int32_t *flags, int64_t pstride = kPartMax)
 {
     __shared__ double red[4 * NB];
     if (flags[0]) return;
     double rrn[NB], beta[NB];
     bool live[NB];
-    block_final_sums<NB>(part_rr, nrr, red, rrn);
+    block_final_sums<NB>(part_rr, nrr, red, rrn, pstride);
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
         beta[b] = rrn[b] / scal[NB + b];
@@ -991,30 +1006,30 @@ inline unsigned project_grid(int64_t NO, int L)
 // k_ds_project with the lane group sized to the offset length; returns its grid (= partials).
 template <int NB>
 unsigned launch_project_nb(const comap_destriper *d, hipStream_t st, const double *x, const double *num,
-                           const double *h, double *y, double *part, const int32_t *flags)
+                           const double *h, double *y, double *part, const int32_t *flags, int64_t pstride)
 {
     const unsigned pg = project_grid(d->NO, d->L);
     switch (project_lanes(d->L)) {
     case 16:
         k_ds_project<16, NB><<<pg, 256, 0, st>>>(d->orow, d->opix, d->ow, d->ws, d->tw, x, num, h, d->NO, d->npix, y,
-                                                 part, flags);
+                                                 part, flags, pstride);
         break;
     case 32:
         k_ds_project<32, NB><<<pg, 256, 0, st>>>(d->orow, d->opix, d->ow, d->ws, d->tw, x, num, h, d->NO, d->npix, y,
-                                                 part, flags);
+                                                 part, flags, pstride);
         break;
     default:
         k_ds_project<64, NB><<<pg, 256, 0, st>>>(d->orow, d->opix, d->ow, d->ws, d->tw, x, num, h, d->NO, d->npix, y,
-                                                 part, flags);
+                                                 part, flags, pstride);
     }
     return pg;
 }
 
 unsigned launch_project(const comap_destriper *d, hipStream_t st, const double *x, const double *num,
-                        const double *h, double *y, double *part, const int32_t *flags)
+                        const double *h, double *y, double *part, const int32_t *flags, int64_t pstride = kPartMax)
 {
     unsigned pg = 0;
-    COMAP_NB_SWITCH(d->nb, pg = launch_project_nb<NB>(d, st, x, num, h, y, part, flags));
+    COMAP_NB_SWITCH(d->nb, pg = launch_project_nb<NB>(d, st, x, num, h, y, part, flags, pstride));
     return pg;
 }
 
@@ -1379,6 +1394,51 @@ extern "C" int comap_destripe_dist_direction(comap_destriper *d, double *scal, d
     COMAP_NB_SWITCH(nb, k_cg_direction<NB><<<grid_for(d->NO), 256, 0, ctx->stream>>>(scal + 3 * nb, scal + nb, p, r,
                                                                                       d->NO, flags);
                     k_cg_check<NB><<<1, 64, 0, ctx->stream>>>(scal, flags));
+    COMAP_LAUNCH_CHECK(ctx);
+    return 0;
+}
+
+// Partial-sum variant of the multi-rank pieces: the native solve's kernels, with the p.q
+// and r.r block partials (one slot per block, kDistParts per band, zero beyond the grid)
+// all-reduced between them instead of final sums.  Adding the zero slots changes no bit,
+// so on one rank the iterates equal comap_destripe_solve's.
+constexpr int kDistParts = 1024;   // >= kProjBlocks, kUpdBlocks
+static_assert(kDistParts >= kProjBlocks && kDistParts >= kUpdBlocks, "partial slots");
+
+extern "C" int32_t comap_destripe_dist_parts(void) { return kDistParts; }
+
+extern "C" int comap_destripe_dist_project_parts(comap_destriper *d, const double *p, const double *num,
+                                                 const double *h, double *q, double *pq_part, const int32_t *flags)
+{
+    if (!d || !p || !num || !h || !q || !pq_part || !flags) return -1;
+    COMAP_DEVICE_GUARD(d->ctx);
+    comap_ctx *ctx = d->ctx;
+    launch_project(d, ctx->stream, p, num, h, q, pq_part, flags, kDistParts);
+    COMAP_LAUNCH_CHECK(ctx);
+    return 0;
+}
+
+extern "C" int comap_destripe_dist_update_fused(comap_destriper *d, double *scal, const double *pq_part, double *x,
+                                                double *r, const double *p, const double *q, double *rr_part,
+                                                const int32_t *flags)
+{
+    if (!d || !scal || !pq_part || !x || !r || !p || !q || !rr_part || !flags) return -1;
+    COMAP_DEVICE_GUARD(d->ctx);
+    comap_ctx *ctx = d->ctx;
+    COMAP_NB_SWITCH(d->nb, k_cg_update_fused<NB><<<upd_grid(d->NO), 256, 0, ctx->stream>>>(
+                               scal, pq_part, kDistParts, x, r, p, q, d->NO, rr_part, flags, kDistParts));
+    COMAP_LAUNCH_CHECK(ctx);
+    return 0;
+}
+
+extern "C" int comap_destripe_dist_direction_fused(comap_destriper *d, double *scal, const double *rr_part, double *p,
+                                                   const double *r, int32_t *flags)
+{
+    if (!d || !scal || !rr_part || !p || !r || !flags) return -1;
+    COMAP_DEVICE_GUARD(d->ctx);
+    comap_ctx *ctx = d->ctx;
+    COMAP_NB_SWITCH(d->nb, k_cg_direction_fused<NB><<<grid_for(d->NO, kDirBlocks), 256, 0, ctx->stream>>>(
+                               scal, rr_part, kDistParts, p, r, d->NO, flags, kDistParts));
     COMAP_LAUNCH_CHECK(ctx);
     return 0;
 }

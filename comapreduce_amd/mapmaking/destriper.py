@@ -129,23 +129,50 @@ def cg_solve_batched(ops, allreduce, threshold=1e-6, niter=100, batch=16):
     ops.dot(r, r, scal[0:nb])
     allreduce(scal[0:nb])
     scal[nb:2 * nb].copy_(scal[0:nb])
+    scal[3 * nb:4 * nb].copy_(scal[0:nb])
     scal[4 * nb] = float(threshold)
     flags = torch.zeros(2 + 2 * nb, dtype=torch.int32, device=ops.dev)
+    iteration = _dist_iteration(ops, allreduce, p, num, h, q, scal, flags, x, r)
     enq = 0
     while enq < niter:
         k = min(batch, niter - enq)
         for _ in range(k):
-            ops.dist_bin(p, num, flags)
-            allreduce(num)
-            ops.dist_project(p, num, h, q, scal, flags)
-            allreduce(scal[2 * nb:3 * nb])
-            ops.dist_update(scal, x, r, p, q, flags)
-            allreduce(scal[3 * nb:4 * nb])
-            ops.dist_direction(scal, p, r, flags)
+            iteration()
         enq += k
         if int(flags[0].item()):
             break
     return x, [int(v) for v in flags[2 + nb:2 + 2 * nb].tolist()], h, nnum
+
+
+def _dist_iteration(ops, allreduce, p, num, h, q, scal, flags, x, r):
+    """One multi-rank CG iteration as a no-argument callable: by default the native
+    solve's 4 kernels with the p.q / r.r block partials all-reduced
+    (comap_destripe_dist_*_parts / _fused); COMAP_DS_DIST_FUSED=0 (and operator
+    objects without them, e.g. the oracle's) use the 7-launch pieces that all-reduce
+    final sums."""
+    nb = ops.nb
+    if hasattr(ops, 'dist_parts') and os.environ.get('COMAP_DS_DIST_FUSED', '0') != '0':
+        pq_part, rr_part = ops.dist_parts()
+
+        def fused():
+            ops.dist_bin(p, num, flags)
+            allreduce(num)
+            ops.dist_project_parts(p, num, h, q, pq_part, flags)
+            allreduce(pq_part)
+            ops.dist_update_fused(scal, pq_part, x, r, p, q, rr_part, flags)
+            allreduce(rr_part)
+            ops.dist_direction_fused(scal, rr_part, p, r, flags)
+        return fused
+
+    def pieces():
+        ops.dist_bin(p, num, flags)
+        allreduce(num)
+        ops.dist_project(p, num, h, q, scal, flags)
+        allreduce(scal[2 * nb:3 * nb])
+        ops.dist_update(scal, x, r, p, q, flags)
+        allreduce(scal[3 * nb:4 * nb])
+        ops.dist_direction(scal, p, r, flags)
+    return pieces
 
 
 def cg_solve_graph(ops, allreduce, threshold=1e-6, niter=100, batch=16):
@@ -169,17 +196,10 @@ def cg_solve_graph(ops, allreduce, threshold=1e-6, niter=100, batch=16):
     ops.dot(r, r, scal[0:nb])
     allreduce(scal[0:nb])
     scal[nb:2 * nb].copy_(scal[0:nb])
+    scal[3 * nb:4 * nb].copy_(scal[0:nb])
     scal[4 * nb] = float(threshold)
     flags = torch.zeros(2 + 2 * nb, dtype=torch.int32, device=ops.dev)
-
-    def iteration():
-        ops.dist_bin(p, num, flags)
-        allreduce(num)
-        ops.dist_project(p, num, h, q, scal, flags)
-        allreduce(scal[2 * nb:3 * nb])
-        ops.dist_update(scal, x, r, p, q, flags)
-        allreduce(scal[3 * nb:4 * nb])
-        ops.dist_direction(scal, p, r, flags)
+    iteration = _dist_iteration(ops, allreduce, p, num, h, q, scal, flags, x, r)
 
     nfull = niter // batch
     graph = None
@@ -374,6 +394,30 @@ class DeviceOps:
     def dist_direction(self, scal, p, r, flags):
         self._c('comap_destripe_dist_direction', self.h, self._s(scal, 4 * self.nb + 1), self._v(p), self._v(r),
                 self._f(flags))
+
+    # ---- the same iteration with block partials all-reduced (4 launches, as the native solve)
+    def dist_parts(self):
+        """Zeroed [nb * comap_destripe_dist_parts()] partial buffers for p.q and r.r."""
+        n = int(N.lib().comap_destripe_dist_parts()) * self.nb
+        return self.zeros(n), self.zeros(n)
+
+    def _pp(self, t):
+        n = int(N.lib().comap_destripe_dist_parts()) * self.nb
+        if t.numel() < n or t.dtype != self.torch.float64:
+            raise ValueError(f'partial buffer must be float64 with >= {n} values')
+        return N.dptr(t)
+
+    def dist_project_parts(self, p, num, h, q, pq_part, flags):
+        self._c('comap_destripe_dist_project_parts', self.h, self._v(p), self._m(num), self._m(h), self._v(q),
+                self._pp(pq_part), self._f(flags))
+
+    def dist_update_fused(self, scal, pq_part, x, r, p, q, rr_part, flags):
+        self._c('comap_destripe_dist_update_fused', self.h, self._s(scal, 4 * self.nb + 1), self._pp(pq_part),
+                self._v(x), self._v(r), self._v(p), self._v(q), self._pp(rr_part), self._f(flags))
+
+    def dist_direction_fused(self, scal, rr_part, p, r, flags):
+        self._c('comap_destripe_dist_direction_fused', self.h, self._s(scal, 4 * self.nb + 1), self._pp(rr_part),
+                self._v(p), self._v(r), self._f(flags))
 
     def div_map(self, num, h, out):
         self._c('comap_destripe_div_map', self.h, self._m(num), self._m(h), self._m(out))

@@ -259,6 +259,24 @@ int comap_destripe_dist_update(comap_destriper *d, double *scal_dev, double *x_d
                                const double *p_dev, const double *q_dev, const int32_t *flags_dev);
 int comap_destripe_dist_direction(comap_destriper *d, double *scal_dev, double *p_dev, const double *r_dev,
                                   int32_t *flags_dev);
+/* The same iteration with the block PARTIALS of p.q and r.r all-reduced instead of
+ * their sums, so no final-sum launches: the native solve's 4 kernels per iteration.
+ * pq_part_dev / rr_part_dev f64 [NB][comap_destripe_dist_parts()], zeroed by the
+ * caller before the first iteration (a rank writes its own blocks' slots; every rank
+ * re-sums all slots in one fixed order, so the scalars agree across ranks).  scal as
+ * above, with rr_new[NB] initialised to rr0 (the current r.r):
+ *   dist_project_parts   q = F^T W (F p - m[p]); p.q partials -> all-reduce pq_part
+ *   dist_update_fused    pq = sum(pq_part); x, r; r.r partials -> all-reduce rr_part
+ *   dist_direction_fused rr_new = sum(rr_part); p = r + (rr_new/rr) p; stop test */
+int32_t comap_destripe_dist_parts(void);
+int comap_destripe_dist_project_parts(comap_destriper *d, const double *p_dev, const double *num_dev,
+                                      const double *h_dev, double *q_dev, double *pq_part_dev,
+                                      const int32_t *flags_dev);
+int comap_destripe_dist_update_fused(comap_destriper *d, double *scal_dev, const double *pq_part_dev, double *x_dev,
+                                     double *r_dev, const double *p_dev, const double *q_dev, double *rr_part_dev,
+                                     const int32_t *flags_dev);
+int comap_destripe_dist_direction_fused(comap_destriper *d, double *scal_dev, const double *rr_part_dev,
+                                        double *p_dev, const double *r_dev, int32_t *flags_dev);
 /* out = num/h (num where h == 0); h_dev == NULL uses the local weight map */
 int comap_destripe_div_map(comap_destriper *d, const double *num_dev, const double *h_dev, double *out_dev);
 /* Whole single-rank destriper_iteration (no collectives) for every band: CG

@@ -187,6 +187,50 @@ def test_two_ranks_compacted_map_allreduce_bit_identical(nb):
     assert np.count_nonzero(res[0][1][0][3]['hits']) < 0.2 * big * big * (4 if nb == 4 else 1)
 
 
+def _uneven_rank(rank, world, port, p, t, w, frac, q):
+    import torch
+    import torch.distributed as dist
+    from comapreduce_amd.mapmaking.destriper import DeviceDestriper
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    no = t.shape[-1] // L
+    cut = int(no * frac) * L
+    lo, hi = (0, cut) if rank == 0 else (cut, t.shape[-1])
+    res = DeviceDestriper(p[lo:hi], t[..., lo:hi], w[..., lo:hi], L, NPIX, device=0).solve(1e-6, 100)
+    q.put((rank, res['x'].cpu().numpy(), res['iters'], {k: v.cpu().numpy() for k, v in res['maps'].items()}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('nb', [1, 4])
+def test_two_ranks_uneven_split_matches_single_rank(nb):
+    """The multi-rank CG all-reduces the p.q / r.r block partials (native kernels, no
+    final-sum launches); ranks with different grids (80 / 20 % of the offsets) must
+    clear the partial slots they do not write.  Offsets and maps == the single-rank
+    native solve to 1e-9, same iteration counts."""
+    import torch.multiprocessing as mp
+    from comapreduce_amd.mapmaking.destriper import DeviceDestriper
+    p, tods, ws, _ = _bands_problem(4)
+    t, w = (tods, ws) if nb == 4 else (tods[0], ws[0])
+    ref = DeviceDestriper(p, t, w, L, NPIX).solve(1e-6, 100)
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = 29300 + os.getpid() % 190
+    procs = [ctx.Process(target=_uneven_rank, args=(r, 2, port, p, t, w, 0.8, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=240) for _ in range(2)], key=lambda r: r[0])
+    for pr in procs:
+        pr.join(timeout=60)
+    assert res[0][2] == res[1][2] == ref['iters']
+    x = np.concatenate([res[0][1], res[1][1]], axis=-1)
+    assert rel(x, ref['x'].cpu().numpy()) < 1e-9
+    for k in ('map', 'naive', 'weight', 'hits'):
+        assert rel(res[0][3][k], ref['maps'][k].cpu().numpy()) < 1e-9, k
+
+
 # ---------------------------------------------------------------- batched bands
 def _bands_problem(nb=4, seed=11):
     """The golden problem's pointing with nb sidebands: per-band tod and weight
