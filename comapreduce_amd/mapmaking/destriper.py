@@ -151,7 +151,7 @@ def _dist_iteration(ops, allreduce, p, num, h, q, scal, flags, x, r):
     objects without them, e.g. the oracle's) use the 7-launch pieces that all-reduce
     final sums."""
     nb = ops.nb
-    if hasattr(ops, 'dist_parts') and os.environ.get('COMAP_DS_DIST_FUSED', '0') != '0':
+    if hasattr(ops, 'dist_parts') and os.environ.get('COMAP_DS_DIST_FUSED', '1') != '0':
         pq_part, rr_part = ops.dist_parts()
 
         def fused():
