@@ -249,3 +249,92 @@ def test_flat_reads_of_a_large_contiguous_dataset(tmp_path):
                 o = np.empty(n, np.float32)
                 d.read_flat(off, o)
                 assert np.array_equal(o, flat[off:off + n]), (mode, off, n)
+
+
+H5PY = '/opt/conda/bin/python3.9'   # a separate interpreter of this image with h5py 3.3.0 (not importable here)
+
+
+def _h5py(code):
+    if not os.path.exists(H5PY):
+        pytest.skip('no interpreter with h5py')
+    r = subprocess.run([H5PY, '-c', code], capture_output=True, text=True, timeout=120)
+    if r.returncode != 0 and 'No module named' in r.stderr:
+        pytest.skip('h5py not importable by ' + H5PY)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return r.stdout
+
+
+def test_h5py_reads_our_level2_file(tmp_path):
+    """Interop with h5py itself (3.3.0, run by the image's conda interpreter): a
+    Level-2 file written by HDF5Data.write_data_file reads back in h5py with the
+    same datasets, dtypes, values and attribute types h5py would have written."""
+    p = str(tmp_path / 'Level2_x.hd5')
+    rng = np.random.default_rng(4)
+    l2 = COMAPLevel2(filename=p)
+    tod = rng.standard_normal((2, 4, 100))
+    l2['averaged_tod/tod'] = tod
+    l2['averaged_tod/scan_edges'] = np.array([[0, 50], [50, 100]])
+    l2['spikes/spike_mask'] = rng.random((2, 4, 100)) < 0.1
+    l2.set_attrs('comap', 'source', 'co2_7,TauA')
+    l2.set_attrs('comap', 'obsid', 12345)
+    l2.set_attrs('comap', 'TauA_calibration_factor_band0', np.arange(20.0))
+    l2.write_data_file(p)
+    np.save(str(tmp_path / 'tod.npy'), tod)
+    out = _h5py(f"""
+import h5py, numpy as np
+with h5py.File({p!r}, 'r') as h:
+    t = h['averaged_tod/tod']
+    assert t.dtype == np.float64 and t.shape == (2, 4, 100)
+    assert np.array_equal(t[...], np.load({str(tmp_path / 'tod.npy')!r}))
+    assert h['averaged_tod/scan_edges'].dtype == np.int64
+    assert h['spikes/spike_mask'].dtype == np.bool_
+    a = h['comap'].attrs
+    assert a['source'] == 'co2_7,TauA' and isinstance(a['source'], str)
+    assert a['obsid'] == 12345
+    assert np.array_equal(a['TauA_calibration_factor_band0'], np.arange(20.0))
+print('ok')
+""")
+    assert out.strip() == 'ok'
+
+
+def test_we_read_h5py_written_level1_file(tmp_path):
+    """The other direction: a Level-1-shaped file written by h5py (vlen str, bytes,
+    bool, int and float attributes; a chunked + gzip-compressed and a contiguous
+    dataset) reads through HDF5Data with h5py's values; the lazy cube stages by
+    flat ranges from the compressed (H5Dread) and contiguous (pread) layouts."""
+    p = str(tmp_path / 'comap-0001234-h5py.hd5')
+    _h5py(f"""
+import h5py, numpy as np
+rng = np.random.default_rng(5)
+with h5py.File({p!r}, 'w') as h:
+    h.create_dataset('spectrometer/tod', data=rng.standard_normal((2, 4, 8, 5000)).astype(np.float32))
+    h.create_dataset('spectrometer/band_average', data=rng.standard_normal((2, 4, 5000)).astype(np.float32),
+                     chunks=(1, 4, 1000), compression='gzip')
+    h.create_dataset('spectrometer/feeds', data=np.array([1, 20]))
+    h.create_dataset('spectrometer/flags', data=np.array([True, False]))
+    g = h.require_group('comap')
+    g.attrs['source'] = 'co2_7,TauA'
+    g.attrs['obsid'] = 1234
+    g.attrs['raw'] = np.bytes_(b'abc')
+    g.attrs['flag'] = np.bool_(True)
+    g.attrs['vec'] = np.arange(3.0)
+    np.save({str(tmp_path / 'tod.npy')!r}, h['spectrometer/tod'][...])
+    np.save({str(tmp_path / 'ba.npy')!r}, h['spectrometer/band_average'][...])
+""")
+    d = COMAPLevel1(overwrite=False, large_datasets=['spectrometer/tod', 'spectrometer/band_average'])
+    d.read_data_file(p)
+    tod, ba = np.load(str(tmp_path / 'tod.npy')), np.load(str(tmp_path / 'ba.npy'))
+    for name, ref in (('spectrometer/tod', tod), ('spectrometer/band_average', ba)):
+        v = d[name]
+        assert isinstance(v, H.H5Dataset) and v.shape == ref.shape
+        assert np.array_equal(v[...], ref)
+        flat = ref.reshape(-1)
+        o = np.empty(flat.size - 7, np.float32)
+        v.read_flat(7, o)
+        assert np.array_equal(o, flat[7:])
+    assert np.array_equal(np.asarray(d['spectrometer/feeds']), [1, 20])
+    assert np.asarray(d['spectrometer/flags']).dtype == np.bool_
+    a = d.attrs('comap')
+    assert a['source'] == 'co2_7,TauA' and d.obsid == 1234
+    assert a['raw'] == b'abc' and bool(a['flag']) and np.array_equal(a['vec'], np.arange(3.0))
+    d.close()
