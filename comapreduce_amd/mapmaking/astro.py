@@ -10,8 +10,9 @@ psi]`` in degrees, ``get_rotation_matrix`` negating the latitude angle,
 (-pi, pi]).  ``sun_radec`` is the Astronomical Almanac low-precision solar
 ephemeris (~0.01 deg, 1950-2050) referred to the J2000 equinox; astropy's
 ``get_sun`` (GCRS) differs by ~arcsec-arcmin, which only moves samples that
-sit exactly on the reference's 10-degree Sun cut.  Both are parity UNPINNED
-against healpy/astropy; the golden harness uses these same
+sit exactly on the reference's 10-degree Sun cut (measured: within 0.007 deg of
+astropy 4.3.1's get_sun, tests/test_astro_golden.py).  healpy is absent, so the
+Rotator is pinned to healpy's source only; the golden harness uses these same
 functions as its stand-ins, so everything downstream of them is pinned.
 """
 from __future__ import annotations
