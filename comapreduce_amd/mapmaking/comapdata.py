@@ -146,6 +146,29 @@ def read_pixels(f, datasize, offset_length, selected_feeds, map_info):
     return pixels
 
 
+def read_pixels_healpix(f, datasize, offset_length, selected_feeds, map_info, nside=4096):
+    """COMAPData.read_pixels_healpix (COMAPData.py:429-469): healpy.ang2pix RING
+    pixels (nside 4096) of every scan sample (galactic for a GLON map), rows in
+    the file's feed order (the reference does not remap them to the output
+    order as read_pixels does; with every selected feed present they coincide)."""
+    from . import healpix
+    fi, oi = GetFeeds(f['spectrometer/feeds'], selected_feeds)
+    wcs = map_info['wcs']
+    edges = f['averaged_tod/scan_edges']
+    lens = scan_lengths(edges, offset_length)
+    cols = np.concatenate([np.arange(s, s + n) for (s, _), n in zip(edges, lens)]) if lens else np.zeros(0, int)
+    x = f['spectrometer/pixel_pointing/pixel_ra'][fi][:, cols]
+    y = f['spectrometer/pixel_pointing/pixel_dec'][fi][:, cols]
+    if 'GLON' in wcs.ctype[0]:
+        gb, gl = astro.Rotator(coord=['C', 'G'])((90 - y.ravel()) * np.pi / 180., x.ravel() * np.pi / 180.)
+        x, y = gl * 180. / np.pi, (np.pi / 2 - gb) * 180. / np.pi
+    p = healpix.ang2pix(nside, (90 - np.ravel(y)) * np.pi / 180., np.ravel(x) * np.pi / 180).reshape(len(fi), cols.size)
+    pixels = np.zeros((len(oi), datasize))
+    n = min(len(oi), len(fi))
+    pixels[:n, :cols.size] = p[:n]
+    return pixels
+
+
 class _FilePrep:
     """get_tod (COMAPData.py:247-380) split in two: ``collect`` builds the
     per-feed arrays and queues median-filter series; ``finish`` subtracts the
@@ -239,10 +262,9 @@ def read_comap_data(filelist, map_info, feed_weights=None, iband=0, use_gain_fil
     feedid, obsids)``.  ``store`` (tests) maps filename -> (datasets, attrs);
     ``device``: the rank's GPU for the batched median (default: torch's
     current device)."""
-    if healpix:
-        raise NotImplementedError('HEALPix pixelisation (read_pixels_healpix) is not built yet')
     (tod,), (weights,), pointing, az, el, ra, dec, feedid, obsids = _read_uncut(
-        filelist, map_info, (iband,), use_gain_filter, offset_length, feeds, calibration, calibrator, store, device)
+        filelist, map_info, (iband,), use_gain_filter, offset_length, feeds, calibration, calibrator, store, device,
+        healpix)
     mask = ~np.isfinite(tod)
     tod[mask] = 0
     weights[mask] = 0
@@ -251,11 +273,14 @@ def read_comap_data(filelist, map_info, feed_weights=None, iband=0, use_gain_fil
     az, el, ra, dec, feedid, obsids = az[keep], el[keep], ra[keep], dec[keep], feedid[keep], obsids[keep]
     weights[~np.isfinite(weights)] = 0
     remapping_array = find_unique_values(np.unique(pointing))
+    if healpix:      # COMAPData.py:572-573: pixel ids -> positions in the union over ranks
+        from .healpix import index_replace
+        pointing = index_replace(remapping_array, pointing)
     return tod, weights, pointing, remapping_array.astype(int), az, el, ra, dec, feedid, obsids
 
 
 def _read_uncut(filelist, map_info, bands, use_gain_filter, offset_length, feeds, calibration, calibrator, store,
-                device):
+                device, healpix=False):
     """Per-band tod / weights (lists) and the band-independent vectors of
     read_comap_data before its NaN and empty-offset cuts.  Every band's
     400-sample high-pass series of every file go through ONE batched device
@@ -268,7 +293,7 @@ def _read_uncut(filelist, map_info, bands, use_gain_filter, offset_length, feeds
     queue, preps, pix = [], [], []
     for fn, f, info in zip(filelist, files, sizes):
         ds = int(info['datasize'])
-        pix.append(read_pixels(f, ds, offset_length, feeds, map_info))
+        pix.append((read_pixels_healpix if healpix else read_pixels)(f, ds, offset_length, feeds, map_info))
         preps.append([_FilePrep(f, ds, offset_length, feeds, use_gain_filter, b, calibration, calibrator, queue)
                       for b in bands])
     filtered = medfilt_batch(queue, MEDFILT_STEP, reflect=True, device=device)
@@ -311,11 +336,9 @@ def read_comap_data_bands(filelist, map_info, bands=(0, 1, 2, 3), use_gain_filte
 
     Returns dict: tod, weights [nb, N]; keep uint8 [nb, N/L]; pointing, az, el,
     ra, dec, feedid, obsids [N]; remapping_array (unique pixels of the union)."""
-    if healpix:
-        raise NotImplementedError('HEALPix pixelisation (read_pixels_healpix) is not built yet')
     tods, wts, pointing, az, el, ra, dec, feedid, obsids = _read_uncut(
         filelist, map_info, tuple(bands), use_gain_filter, offset_length, feeds, calibration, calibrator, store,
-        device)
+        device, healpix)
     keeps = []
     for t, w in zip(tods, wts):
         bad = ~np.isfinite(t)
@@ -333,4 +356,7 @@ def read_comap_data_bands(filelist, map_info, bands=(0, 1, 2, 3), use_gain_filte
            'az': az[sel], 'el': el[sel], 'ra': ra[sel], 'dec': dec[sel], 'feedid': feedid[sel],
            'obsids': obsids[sel]}
     out['remapping_array'] = find_unique_values(np.unique(pointing)).astype(int)
+    if healpix:
+        from .healpix import index_replace
+        out['pointing'] = index_replace(out['remapping_array'], pointing)
     return out

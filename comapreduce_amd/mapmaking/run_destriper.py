@@ -52,6 +52,34 @@ def write_map(prefix, maps, map_info, output_dir, iband, postfix=''):
         write_image_hdus(fname, images, cards)
 
 
+def write_map_healpix(prefix, maps, remapping_array, map_info, output_dir, iband, postfix='', nside=4096):
+    """run_destriper.write_map_healpix (run_destriper.py:53-77): per map set a
+    partial HEALPix file of (map, naive, sqrt(1/weight)) on the union pixels."""
+    from .healpix import UNSEEN, nside2npix, write_map_partial
+    os.makedirs(output_dir, exist_ok=True)
+    for k, v in maps.items():
+        m = np.zeros((3, nside2npix(nside))) + UNSEEN
+        m[0, remapping_array] = v['map']
+        m[1, remapping_array] = v['naive']
+        with np.errstate(divide='ignore'):
+            m[2, remapping_array] = np.sqrt(1. / v['weight'])
+        fname = '{}/{}_{}_Band{:02d}.fits'.format(output_dir, k, prefix, iband)
+        write_map_partial(fname, m, nside)
+
+
+def _healpix_edges(pointing):
+    """run_destriper.py:159-161: pixel_edges = arange(max over ranks of pointing + 1)."""
+    import torch.distributed as dist
+    mx = int(np.max(pointing)) if np.size(pointing) else -1
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        import torch
+        dev = torch.device('cuda', torch.cuda.current_device()) if dist.get_backend() == 'nccl' else 'cpu'
+        t = torch.tensor([mx], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        mx = int(t.item())
+    return np.arange(mx + 1, dtype=int)
+
+
 def main(filelistname, offset_length=50, feed_weights=None, prefix='fg9', output_dir='maps/fg9/', obsid_cuts=[],
          feeds=[1, 2, 3, 5, 6, 9, 11, 12, 13, 14, 15, 16, 17, 18, 19], nxpix=480, nypix=480,
          crval=['05:32:00.3', '+12:30:28.0'], crpix=[240, 240], ctype=['RA---CAR', 'DEC--CAR'],
@@ -88,20 +116,21 @@ def main(filelistname, offset_length=50, feed_weights=None, prefix='fg9', output
     if source in CALIBRATORS:
         offset_length = 250
         threshold = 1
-    if healpix:
-        raise NotImplementedError('HEALPix maps (write_map_healpix) are not built yet')
     out = {}
     if batch_bands and len(bands) > 1:
         r = COMAPData.read_comap_data_bands(filelist, map_info, bands=bands, offset_length=offset_length, feeds=feeds,
                                             use_gain_filter=use_gain_filter, calibration=calibration,
                                             calibrator=calibrator, healpix=healpix, store=store, device=device)
-        pixel_edges = np.arange(nxpix * nypix)
+        pixel_edges = _healpix_edges(r['pointing']) if healpix else np.arange(nxpix * nypix)
         res = run_destriper_bands(r['pointing'], r['tod'], r['weights'], offset_length, pixel_edges, keep=r['keep'],
                                   threshold=threshold, niter=niter, device=device)
         for iband, maps in zip(bands, res):
             maps = {'All': maps['All']}
             if rank == 0:
-                write_map(prefix, maps, map_info, output_dir, iband)
+                if healpix:
+                    write_map_healpix(prefix, maps, r['remapping_array'], map_info, output_dir, iband)
+                else:
+                    write_map(prefix, maps, map_info, output_dir, iband)
             out[iband] = maps
         return out
     for iband in bands:
@@ -109,12 +138,15 @@ def main(filelistname, offset_length=50, feed_weights=None, prefix='fg9', output
             filelist, map_info, feed_weights=feed_weights, offset_length=offset_length, iband=iband, feeds=feeds,
             use_gain_filter=use_gain_filter, calibration=calibration, calibrator=calibrator, healpix=healpix,
             store=store, device=device)
-        pixel_edges = np.arange(nxpix * nypix)
+        pixel_edges = _healpix_edges(pointing) if healpix else np.arange(nxpix * nypix)
         maps = run_destriper(pointing, tod, weights, offset_length, pixel_edges, az, el, ra, dec, feedid, obsids,
                              obsid_cuts, threshold=threshold, niter=niter, chi2_cutoff=20,
                              device=device)
         if rank == 0:
-            write_map(prefix, maps, map_info, output_dir, iband)
+            if healpix:
+                write_map_healpix(prefix, maps, remap, map_info, output_dir, iband)
+            else:
+                write_map(prefix, maps, map_info, output_dir, iband)
         out[iband] = maps
     return out
 

@@ -107,3 +107,46 @@ def test_run_destriper_main_bands_batched(tmp_path):
         scale = np.max(np.abs(ref['map'][fin]))
         assert np.max(np.abs(got['map'][fin] - ref['map'][fin])) <= 1e-6 * scale, b
         assert os.path.exists(tmp_path / f'All_t_Band{b:02d}.fits')
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('batch', [False, True])
+def test_run_destriper_main_healpix(tmp_path, batch):
+    """healpix=True: RING nside-4096 pixels (read_pixels_healpix, COMAPData.py:429-469),
+    compacted to the union of hit pixels (:572-573), pixel_edges = arange(max + 1)
+    (run_destriper.py:159-161), partial HEALPix files (write_map_healpix, :53-77).
+    The data prep is otherwise unchanged (tod / weights equal the CAR read's), and the
+    maps equal the oracle destriper on the compact pointing; the file holds the union
+    pixels with (map, naive, sqrt(1/weight)).  healpy parity itself is unpinned."""
+    import comapdata_case as cc
+    from comapreduce_amd.mapmaking import comapdata as CD, healpix as H
+    from comapreduce_amd.mapmaking.run_destriper import main
+    from oracle import destriper as od
+    store, names = cc.store()
+    names = names[:2]
+    m = cc.CASES['car']['map']
+    geo = dict(nxpix=m['nxpix'], nypix=m['nypix'], crval=m['crval'], crpix=m['crpix'], ctype=m['ctype'],
+               cdelt=m['cdelt'])
+    bands = (0, 1) if batch else (0,)
+    out = main(names, offset_length=50, prefix='h', output_dir=str(tmp_path), feeds=cc.FEEDS,
+               use_gain_filter=True, calibration=False, threshold=1e-6, niter=50, bands=bands, store=store,
+               healpix=True, batch_bands=batch, **geo)
+    mi = CD.map_info_from(m['crval'], m['cdelt'], m['crpix'], m['ctype'], m['nxpix'], m['nypix'])
+    for b in bands:
+        tod_c, w_c, _, _, *_ = CD.read_comap_data(names, mi, iband=b, offset_length=50, feeds=cc.FEEDS, store=store)
+        tod, w, pix, remap, *_ = CD.read_comap_data(names, mi, iband=b, offset_length=50, feeds=cc.FEEDS,
+                                                    store=store, healpix=True)
+        assert np.array_equal(tod, tod_c) and np.array_equal(w, w_c)
+        assert pix.min() >= 0 and pix.max() < remap.size and np.all(np.diff(remap) > 0)
+        assert remap.max() < H.nside2npix(4096)
+        ref, _, _ = od.destriper_iteration(pix, tod, w, 50, remap.size, threshold=1e-6, niter=50)
+        got = out[b]['All']
+        for k in ('weight', 'hits', 'naive'):
+            assert np.array_equal(np.nan_to_num(got[k]), np.nan_to_num(ref[k])), (b, k)
+        fin = np.isfinite(ref['map']) & (ref['weight'] > 0)
+        assert np.max(np.abs(got['map'][fin] - ref['map'][fin])) <= 1e-6 * np.max(np.abs(ref['map'][fin]))
+        hdr, rec = H.read_map_partial(str(tmp_path / f'All_h_Band{b:02d}.fits'))
+        assert hdr['NSIDE'] == 4096 and hdr['ORDERING'] == 'RING'
+        assert np.array_equal(rec['PIXEL'], remap)
+        assert np.array_equal(rec['TEMPERATURE'], got['map'], equal_nan=True)
+        assert np.array_equal(rec['Q_POLARISATION'], got['naive'], equal_nan=True)
