@@ -915,12 +915,36 @@ __device__ __forceinline__ void band_fma(BandAcc &a, const double *__restrict__ 
         }
 }
 
+#ifndef COMAP_B_PREF
+#define COMAP_B_PREF 0   // 1: the next batch's channel ids are loaded before this batch's rows
+#endif
 template <bool FULL>
 __device__ __forceinline__ void band_sums(const float *__restrict__ base, int64_t T, int nv0,
                                           const int32_t *__restrict__ lst, const double *__restrict__ wl, int cnt,
                                           BandAcc &a)
 {
     int j = 0;
+#if COMAP_B_PREF
+    // the row addresses of batch j + 1 depend on list loads: issue them one batch ahead
+    // so each batch's row loads start without waiting for its channel ids
+    int32_t cur[kBB], nxt[kBB];
+    if (kBB <= cnt) {
+#pragma unroll
+        for (int q = 0; q < kBB; ++q) cur[q] = lst[q];
+    }
+    for (; j + kBB <= cnt; j += kBB) {
+        const bool more = j + 2 * kBB <= cnt;
+#pragma unroll
+        for (int q = 0; q < kBB; ++q) nxt[q] = more ? lst[j + kBB + q] : 0;
+        f32x4u r[kBB][kJB];
+#pragma unroll
+        for (int q = 0; q < kBB; ++q) load_raw<kJB, FULL>(base + (int64_t)cur[q] * T, nv0, r[q]);
+#pragma unroll
+        for (int q = 0; q < kBB; ++q) band_fma(a, wl + 4 * (j + q), r[q]);
+#pragma unroll
+        for (int q = 0; q < kBB; ++q) cur[q] = nxt[q];
+    }
+#else
     for (; j + kBB <= cnt; j += kBB) {
         f32x4u r[kBB][kJB];
 #pragma unroll
@@ -928,6 +952,7 @@ __device__ __forceinline__ void band_sums(const float *__restrict__ base, int64_
 #pragma unroll
         for (int q = 0; q < kBB; ++q) band_fma(a, wl + 4 * (j + q), r[q]);
     }
+#endif
     for (; j < cnt; ++j) {
         f32x4u r[kJB];
         load_raw<kJB, FULL>(base + (int64_t)lst[j] * T, nv0, r);
