@@ -236,8 +236,9 @@ class GPUObservation:
         nV = ev.shape[0]
         if nV == 0:
             return None, None
-        tsys = torch.zeros((nV, self.F, N_BANDS, N_CHANNELS), dtype=torch.float64, device=self.tdev)
-        gain = torch.zeros_like(tsys)
+        # comap_l1_vane zeroes both before its kernel writes them (no-vane rows stay 0)
+        tsys = torch.empty((nV, self.F, N_BANDS, N_CHANNELS), dtype=torch.float64, device=self.tdev)
+        gain = torch.empty_like(tsys)
         self._bind()
         # The band-average windows are copied first (pinned, asynchronous), then pass A
         # (which does not depend on the vane) is queued behind them, so the host search
