@@ -915,6 +915,9 @@ __device__ __forceinline__ void band_fma(BandAcc &a, const double *__restrict__ 
         }
 }
 
+#ifndef COMAP_B_XCD
+#define COMAP_B_XCD 0   // 1: pass B tiles dealt to the XCDs in contiguous runs
+#endif
 #ifndef COMAP_B_PREF
 #define COMAP_B_PREF 0   // 1: the next batch's channel ids are loaded before this batch's rows
 #endif
@@ -972,7 +975,19 @@ __global__ void __launch_bounds__(256) k_band_sums(const float *__restrict__ tod
     __shared__ double sg[kBands][256 * kJB];
     const int b = uniform(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
+#if COMAP_B_XCD
+    // XCD-contiguous tiles: workgroups b, b + 8, ... share an XCD (round-robin dispatch),
+    // so logical block ids are dealt to the 8 XCDs in contiguous runs -- the blocks an XCD
+    // runs at once then read the same few units' rows (fewer distinct pages in its TLB)
+    int lbid;
+    {
+        const int nwg = (int)gridDim.x, q = nwg / 8, r = nwg % 8, x = (int)blockIdx.x % 8;
+        lbid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (int)blockIdx.x / 8;
+    }
+    const int tile = (int)(tile0 + lbid / kSubB), sub = lbid % kSubB;
+#else
     const int tile = (int)(tile0 + blockIdx.x / kSubB), sub = blockIdx.x % kSubB;
+#endif
     const int u = tiles[2 * tile], toff = tiles[2 * tile + 1] + 256 * kJB * sub;
     const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
     if (toff >= n) return;                          // whole block: past the scan end
