@@ -502,6 +502,10 @@ __global__ void __launch_bounds__(LT) k_med_walk(const MedJob *__restrict__ jobs
 // the two middle order statistics share their path until the level where they part.
 // Same ranks as the bitmap walk, so the same (bit-exact) values.
 constexpr int kWmThreads = 1024;
+#ifndef COMAP_WM_Q
+#define COMAP_WM_Q 2
+#endif
+constexpr int kWmQ = COMAP_WM_Q;   // outputs per thread walking the levels together
 
 __device__ __forceinline__ int wm_rank0(const uint64_t *__restrict__ lv, int i)
 {
@@ -603,34 +607,54 @@ __global__ void __launch_bounds__(kWmThreads) k_med_wm(const MedJob *__restrict_
     const int r_lo = two ? (w / 2 - 1) : (w / 2);
     const int32_t *sp = sidx + s0;
     auto value = [&](uint32_t u) { return job.src[sl + sp[u]]; };   // value of sorted index u
-    for (int k = tid; k < nout; k += kWmThreads) {
-        int a = k, b = k + w, r = r_lo;
-        int a2 = 0, b2 = 0, r2 = 0;
-        uint32_t v1 = 0, v2 = 0;
-        bool split = false;
+    // kWmQ outputs per thread walk the levels together: their rank lookups are
+    // independent, so each level's LDS reads of all of them are in flight at once
+    // (one output's walk is a chain of dependent LDS round trips)
+    struct Walk {
+        int a, b, r, a2, b2, r2;
+        uint32_t v1, v2;
+        bool split;
+    };
+    for (int k0 = tid; k0 < nout; k0 += kWmThreads * kWmQ) {
+        Walk q[kWmQ];
+#pragma unroll
+        for (int i = 0; i < kWmQ; ++i) {
+            const int k = k0 + i * kWmThreads;
+            const int ka = k < nout ? k : 0;           // idle slots walk output 0 (valid ranges)
+            q[i] = Walk{ka, ka + w, r_lo, 0, 0, 0, 0u, 0u, false};
+        }
         for (int l = L - 1; l >= 0; --l) {
             const uint64_t *lv = lev + (size_t)l * ld;
             const int Z = zt[l];
-            if (split) {                           // the upper statistic on its own path
-                const int za = wm_rank0(lv, a2), zb = wm_rank0(lv, b2), nz = zb - za;
-                if (r2 < nz) { a2 = za; b2 = zb; }
-                else { r2 -= nz; a2 = Z + a2 - za; b2 = Z + b2 - zb; v2 |= 1u << l; }
-            }
-            const int za = wm_rank0(lv, a), zb = wm_rank0(lv, b), nz = zb - za;
-            if (two && !split && r < nz && r + 1 >= nz) {   // the two part here: upper = first one
-                split = true;
-                a2 = Z + a - za; b2 = Z + b - zb; r2 = 0; v2 = v1 | (1u << l);
-                a = za; b = zb;
-            } else if (r < nz) {
-                a = za; b = zb;
-            } else {
-                r -= nz; a = Z + a - za; b = Z + b - zb; v1 |= 1u << l;
+#pragma unroll
+            for (int i = 0; i < kWmQ; ++i) {
+                Walk &t = q[i];
+                if (t.split) {                     // the upper statistic on its own path
+                    const int za = wm_rank0(lv, t.a2), zb = wm_rank0(lv, t.b2), nz = zb - za;
+                    if (t.r2 < nz) { t.a2 = za; t.b2 = zb; }
+                    else { t.r2 -= nz; t.a2 = Z + t.a2 - za; t.b2 = Z + t.b2 - zb; t.v2 |= 1u << l; }
+                }
+                const int za = wm_rank0(lv, t.a), zb = wm_rank0(lv, t.b), nz = zb - za;
+                if (two && !t.split && t.r < nz && t.r + 1 >= nz) {   // the two part here: upper = first one
+                    t.split = true;
+                    t.a2 = Z + t.a - za; t.b2 = Z + t.b - zb; t.r2 = 0; t.v2 = t.v1 | (1u << l);
+                    t.a = za; t.b = zb;
+                } else if (t.r < nz) {
+                    t.a = za; t.b = zb;
+                } else {
+                    t.r -= nz; t.a = Z + t.a - za; t.b = Z + t.b - zb; t.v1 |= 1u << l;
+                }
             }
         }
-        const double lo = value(v1);
-        double out = lo;
-        if (two) out = (value(split ? v2 : v1) + lo) / 2.0;
-        job.dst[sg.o0 + k - job.out_lo] = out;
+#pragma unroll
+        for (int i = 0; i < kWmQ; ++i) {
+            const int k = k0 + i * kWmThreads;
+            if (k >= nout) continue;
+            const double lo = value(q[i].v1);
+            double out = lo;
+            if (two) out = (value(q[i].split ? q[i].v2 : q[i].v1) + lo) / 2.0;
+            job.dst[sg.o0 + k - job.out_lo] = out;
+        }
     }
 }
 

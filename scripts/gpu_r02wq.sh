@@ -1,10 +1,13 @@
 #!/bin/bash
-# 4-ary wavelet-matrix median walk: median + L1 parity, bench wm4 vs wm2
+# Wavelet-matrix walk with 2 (default) / 1 / 4 outputs per thread walking the levels together.
+set -o pipefail
+TAG=${1:-r02wqq}
 mkdir -p gpurun_out
-export TMPDIR=/tmp
-timeout -k 10 500 python -u -m pytest tests/test_gpu_l1.py -m gpu -x -q --timeout 200 --timeout-method thread -k "medfilt or median or c1 or multi_feed or shards or residues" > gpurun_out/r02wq_pytest.log 2>&1 || exit $?
-B="--steps 8 --warmup 2 --no-destriper --no-e2e --no-cpu-baseline"
-timeout -k 10 200 python -u bench.py $B --check > gpurun_out/r02wq_wm4.log 2>&1 || exit $?
-COMAP_MEDIAN_WALK=wm2 timeout -k 10 200 python -u bench.py $B > gpurun_out/r02wq_wm2.log 2>&1 || exit $?
-timeout -k 10 200 python -u bench.py $B --shard-of 8 --steps 20 --warmup 3 > gpurun_out/r02wq_s8.log 2>&1 || exit $?
-COMAP_MEDIAN_WALK=wm2 timeout -k 10 200 python -u bench.py $B --shard-of 8 --steps 20 --warmup 3 > gpurun_out/r02wq_s8w2.log 2>&1 || exit $?
+timeout -k 10 400 python -u -m pytest tests/test_gpu_l1.py -x -q -m gpu --timeout 300 --timeout-method thread -k "medfilt or median or c1" > gpurun_out/${TAG}_pytest.log 2>&1 || exit $?
+L="--steps 10 --warmup 2 --no-destriper --no-e2e --no-cpu-baseline"
+timeout -k 10 200 python -u bench.py $L > gpurun_out/${TAG}_q2.log 2>&1 || exit $?
+COMAP_HIP_LIB=$PWD/exp/wq1/libcomap_hip.so timeout -k 10 200 python -u bench.py $L > gpurun_out/${TAG}_q1.log 2>&1 || exit $?
+COMAP_HIP_LIB=$PWD/exp/wq4/libcomap_hip.so timeout -k 10 200 python -u bench.py $L > gpurun_out/${TAG}_q4.log 2>&1 || exit $?
+timeout -k 10 200 python -u bench.py $L --shard-of 8 > gpurun_out/${TAG}_q2_s8.log 2>&1 || exit $?
+COMAP_HIP_LIB=$PWD/exp/wq1/libcomap_hip.so timeout -k 10 200 python -u bench.py $L --shard-of 8 > gpurun_out/${TAG}_q1_s8.log 2>&1 || exit $?
+COMAP_HIP_LIB=$PWD/exp/wq4/libcomap_hip.so timeout -k 10 200 python -u bench.py $L --shard-of 8 > gpurun_out/${TAG}_q4_s8.log 2>&1 || exit $?
