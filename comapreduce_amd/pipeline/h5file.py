@@ -339,8 +339,13 @@ class H5Dataset:
                 else:
                     hi = max(hi, lo)
                     start.append(lo); count.append(hi - lo); post.append(slice(None, None, st))
+            elif ax == 0 and np.ndim(k) == 1 and np.asarray(k).dtype.kind in 'iu':
+                # integer list on the leading axis (e.g. a feed selection): one hyperslab
+                # read per listed row, never the whole dataset
+                rows = [self[(int(i),) + tuple(key[1:])] for i in np.asarray(k)]
+                return np.stack(rows) if rows else np.empty((0,) + self[(0,) + tuple(key[1:])].shape, self.dtype)
             else:
-                a = np.asarray(self)[tuple(key)]   # fancy indexing: read, then index
+                a = np.asarray(self)[tuple(key)]   # other fancy indexing: read, then index
                 return a
         out = np.empty(tuple(count), dtype=self.dtype)
         if out.size:

@@ -338,3 +338,17 @@ with h5py.File({p!r}, 'w') as h:
     assert a['source'] == 'co2_7,TauA' and d.obsid == 1234
     assert a['raw'] == b'abc' and bool(a['flag']) and np.array_equal(a['vec'], np.arange(3.0))
     d.close()
+
+
+def test_lazy_dataset_feed_list_indexing(tmp_path):
+    """An integer list on the leading axis (the reference's d['...'][file_feed_index, :])
+    reads only the listed rows, in the listed order."""
+    p = str(tmp_path / 'f.h5')
+    x = np.random.default_rng(3).standard_normal((6, 5, 40)).astype(np.float32)
+    with H.H5File(p, 'w') as f:
+        f.write('spectrometer/pixel_pointing/pixel_ra', x)
+    with H.H5File(p) as f:
+        d = f.dataset('spectrometer/pixel_pointing/pixel_ra')
+        for sel in ([4, 0, 2], np.array([5]), [1, 1]):
+            assert np.array_equal(d[sel, 1:3, ::3], x[sel, 1:3, ::3])
+            assert np.array_equal(d[sel], x[sel])
