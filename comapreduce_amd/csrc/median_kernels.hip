@@ -1238,7 +1238,9 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
         const int64_t nwcap = std::min<int64_t>(kWmThreads, (budget - 8 * L) / (std::max(8 * L, 64) + 64));
         const int64_t seg_cap = nwcap * 32 - (w - 1);
         const char *te = getenv("COMAP_MEDIAN_WMSEGS");
-        const int64_t target = te ? std::max(1, atoi(te)) : 256;   // measured: C3 shard median 0.28 -> 0.25 ms (512 -> 256), C2 unchanged
+        // measured at the C3 shard (r02sw2): 1 / 64 -> 0.255 ms, 128 / 192 -> 0.218, 256 -> 0.265, 512 -> 0.28;
+        // C2 is cap-driven (>= 600 segments) and unchanged
+        const int64_t target = te ? std::max(1, atoi(te)) : 128;
         if (L > 16 || seg_cap < 1) {
             return comap_fail(ctx, -1, "median plan: wavelet-matrix walk does not fit (use COMAP_MEDIAN_WALK=bitmap)");
         } else {
