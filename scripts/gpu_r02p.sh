@@ -1,9 +1,9 @@
 #!/bin/bash
-# median walk: XCD-contiguous chunk order A/B (C2 and rank 0 of an 8-way split)
+# Full GPU suite + smoke + default bench at HEAD
+set -o pipefail
+TAG=${1:-r02p}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu_l1.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/r02p_pytest.log 2>&1 || exit $?
-for x in 0; do
-  COMAP_MEDIAN_XCD=$x timeout -k 10 200 python -u bench.py --steps 8 --warmup 2 --no-destriper --no-e2e --no-cpu-baseline > gpurun_out/r02p_c2_x$x.log 2>&1 || exit $?
-  COMAP_MEDIAN_XCD=$x timeout -k 10 200 python -u bench.py --shard-of 8 --steps 20 --warmup 3 --no-destriper --no-e2e --no-cpu-baseline > gpurun_out/r02p_s8_x$x.log 2>&1 || exit $?
-done
+timeout -k 10 700 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/${TAG}_pytest_gpu.log 2>&1 || exit $?
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || exit $?
+timeout -k 10 500 python -u bench.py > gpurun_out/${TAG}_bench.log 2>&1 || exit $?
