@@ -4,6 +4,8 @@ healpy is not in the image, so parity with it is unpinned; these tests pin the
 restatement to the scheme's own invariants: every pixel centre maps back to its
 pixel, known pixel centres, equal areas, ring ordering, the pole branches, and the
 partial-map file layout."""
+import os
+
 import numpy as np
 import pytest
 
@@ -74,3 +76,44 @@ def test_partial_map_file(tmp_path):
     assert np.array_equal(rec['PIXEL'], pix)
     assert np.array_equal(rec['TEMPERATURE'], m[0, pix]) and np.array_equal(rec['U_POLARISATION'], m[2, pix])
     assert (tmp_path / 'hp.fits').stat().st_size % 2880 == 0
+
+
+def _remap_rank(rank, world, port, pix, q):
+    import torch.distributed as dist
+    from comapreduce_amd.mapmaking.comapdata import find_unique_values
+    from comapreduce_amd.mapmaking.run_destriper import _healpix_edges
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    mine = pix[rank]
+    remap = find_unique_values(np.unique(mine))
+    pointing = H.index_replace(remap, mine)
+    edges = _healpix_edges(pointing)
+    q.put((rank, remap, pointing, edges))
+    dist.destroy_process_group()
+
+
+def test_multirank_healpix_remapping_gloo():
+    """COMAPData.py:570-574 + run_destriper.py:159-161 on 2 gloo ranks: every rank
+    gets the same union of hit pixels (find_unique_values), its pointing becomes
+    positions in that union, and pixel_edges spans the union on both ranks."""
+    import multiprocessing as mp
+    rng = np.random.default_rng(3)
+    npix = H.nside2npix(4096)
+    pix = [rng.integers(0, npix // 2, 5000), np.concatenate([rng.integers(npix // 4, npix, 3000), [npix - 1]])]
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = 27500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_remap_rank, args=(r, 2, port, pix, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=120) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    union = np.unique(np.concatenate(pix))
+    for r in range(2):
+        remap, pointing, edges = res[r]
+        assert np.array_equal(remap, union)
+        assert np.array_equal(union[pointing], pix[r])
+        assert np.array_equal(edges, np.arange(union.size))
