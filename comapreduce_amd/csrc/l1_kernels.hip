@@ -964,7 +964,15 @@ __device__ __forceinline__ void band_sums(const float *__restrict__ base, int64_
 }
 
 // Block = 4 waves (wave b = band b) on a 256 kJB-sample sub-tile of a 1024-sample tile.
-__global__ void __launch_bounds__(256) k_band_sums(const float *__restrict__ tod, const double *__restrict__ A,
+#ifndef COMAP_B_WPE
+#define COMAP_B_WPE 0   // >0: waves per SIMD the register allocation must allow (default: the compiler's 2)
+#endif
+#if COMAP_B_WPE
+#define COMAP_B_ATTR __attribute__((amdgpu_waves_per_eu(COMAP_B_WPE)))
+#else
+#define COMAP_B_ATTR
+#endif
+__global__ void __launch_bounds__(256) COMAP_B_ATTR k_band_sums(const float *__restrict__ tod, const double *__restrict__ A,
                                                    const int32_t *__restrict__ units, const int32_t *__restrict__ tiles,
                                                    int64_t tile0, int64_t T, const int32_t *__restrict__ dlist,
                                                    const int32_t *__restrict__ dcnt, const double *__restrict__ dw,
