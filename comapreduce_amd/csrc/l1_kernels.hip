@@ -208,7 +208,15 @@ __global__ void __launch_bounds__(256) k_unit_sums(const int32_t *__restrict__ u
 #define COMAP_A_BADSUM 0
 #endif
 constexpr int kCPW = COMAP_CPW;   // channel rows per wave
-__global__ void __launch_bounds__(256) k_moments(const float *__restrict__ tod, const double *__restrict__ A,
+#ifndef COMAP_AM_WPE
+#define COMAP_AM_WPE 0   // >0: waves per SIMD the register allocation must allow (default: the compiler's 3)
+#endif
+#if COMAP_AM_WPE
+#define COMAP_AM_ATTR __attribute__((amdgpu_waves_per_eu(COMAP_AM_WPE)))
+#else
+#define COMAP_AM_ATTR
+#endif
+__global__ void __launch_bounds__(256) COMAP_AM_ATTR k_moments(const float *__restrict__ tod, const double *__restrict__ A,
                                                  const int32_t *__restrict__ units, int64_t T,
                                                  double *__restrict__ mom, int64_t UC, int32_t *nan_count,
                                                  int32_t *__restrict__ rowbad)
