@@ -441,6 +441,9 @@ __global__ void __launch_bounds__(256) COMAP_AM_ATTR k_moments(const float *__re
 #ifndef COMAP_A_SCHED
 #define COMAP_A_SCHED 0
 #endif
+#ifndef COMAP_A_XLD
+#define COMAP_A_XLD 0   // 1: R >= 2 takes the pair's first sample by a second load, not a DPP shift
+#endif
 constexpr int kDppWaveShr1 = 0x138;
 
 __device__ __forceinline__ int dpp_shr1(int old, int v)
@@ -477,6 +480,13 @@ __device__ __forceinline__ void moments_trip(const float *__restrict__ rb, const
     // R >= 2: the pair's first sample from the lane below (chunk j - 1), all groups first
     float pa[G][kCPW];
     if constexpr (R >= 2) {
+#if COMAP_A_XLD
+        // the pair's first sample re-read from chunk j - 1 (same cache lines) instead of shifted in
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int r = 0; r < kCPW; ++r) pa[g][r] = rb[(int64_t)r * T + 4 * (j + 64 * g + lane - 1) + R];
+#else
 #pragma unroll
         for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -485,6 +495,7 @@ __device__ __forceinline__ void moments_trip(const float *__restrict__ rb, const
                 pa[g][r] = __int_as_float(dpp_shr1(__float_as_int(pc[r]), e));
                 pc[r] = __int_as_float(__builtin_amdgcn_readlane(e, 63));
             }
+#endif
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -495,9 +506,13 @@ __device__ __forceinline__ void moments_trip(const float *__restrict__ rb, const
         if constexpr (R < 2) {
             v = ae[R] - ae[R + 2];
         } else {
+#if COMAP_A_XLD
+            v = ab[4 * (j + 64 * g + lane - 1) + R] - ae[R - 2];
+#else
             const double ap_ = dpp_shr1(apc, ae[R]);
             apc = readlane63(ae[R]);
             v = ap_ - ae[R - 2];
+#endif
         }
 #pragma unroll
         for (int r = 0; r < kCPW; ++r) {
