@@ -444,6 +444,9 @@ __global__ void __launch_bounds__(256) COMAP_AM_ATTR k_moments(const float *__re
 #ifndef COMAP_A_XLD
 #define COMAP_A_XLD 0   // 1: R >= 2 takes the pair's first sample by a second load, not a DPP shift
 #endif
+#ifndef COMAP_A_ALDS
+#define COMAP_A_ALDS 0  // 1: each trip's airmass chunks staged through LDS once per block (as k_moments)
+#endif
 constexpr int kDppWaveShr1 = 0x138;
 
 __device__ __forceinline__ int dpp_shr1(int old, int v)
@@ -470,7 +473,8 @@ struct MomRow {
 
 template <int R, int G>
 __device__ __forceinline__ void moments_trip(const float *__restrict__ rb, const double *__restrict__ ab, int64_t T,
-                                             int j, int lane, MomRow (&m)[kCPW], float (&pc)[kCPW], double &apc)
+                                             int j, int lane, MomRow (&m)[kCPW], float (&pc)[kCPW], double &apc,
+                                             double4 (*sair)[64 * COMAP_AGRP], int &par)
 {
     f32x4a xs[G][kCPW];
 #pragma unroll
@@ -497,10 +501,26 @@ __device__ __forceinline__ void moments_trip(const float *__restrict__ rb, const
             }
 #endif
     }
+#if COMAP_A_ALDS
+    // the block's 4 waves walk the same chunks: the trip's airmass is read once per block
+    // (double-buffered, one barrier per trip; trips are block-uniform)
+    double4 *buf = sair[par];
+    par ^= 1;
+    if ((int)threadIdx.x < 64 * G) {
+        const double *q = ab + 4 * (j + (int)threadIdx.x);
+        buf[threadIdx.x] = make_double4(q[0], q[1], q[2], q[3]);
+    }
+    __syncthreads();
+#endif
 #pragma unroll
     for (int g = 0; g < G; ++g) {
+#if COMAP_A_ALDS
+        const double4 av = buf[64 * g + lane];
+        const double a0 = av.x, a1 = av.y, a2 = av.z, a3 = av.w;
+#else
         const double *ap = ab + 4 * (j + 64 * g + lane);
         const double a0 = ap[0], a1 = ap[1], a2 = ap[2], a3 = ap[3];
+#endif
         const double ae[4] = {a0, a1, a2, a3};
         double v;
         if constexpr (R < 2) {
@@ -539,8 +559,9 @@ __device__ __forceinline__ void moments_trip(const float *__restrict__ rb, const
 
 template <int R>
 __device__ __forceinline__ void moments_rows_al(const float *__restrict__ row0, const double *__restrict__ a, int64_t T,
-                                                int n, int lane, MomRow (&m)[kCPW])
+                                                int n, int lane, MomRow (&m)[kCPW], double4 (*sair)[64 * COMAP_AGRP])
 {
+    int par = 0;
     const float *rb = row0 - R;           // chunk 0, 16-B aligned
     const double *ab = a - R;
     const int n4 = n >> 2;
@@ -555,8 +576,8 @@ __device__ __forceinline__ void moments_rows_al(const float *__restrict__ row0, 
         apc = a[4 * (jA - 1)];
     }
     int j = jA;
-    for (; j + 64 * COMAP_AGRP <= jB; j += 64 * COMAP_AGRP) moments_trip<R, COMAP_AGRP>(rb, ab, T, j, lane, m, pc, apc);
-    for (; j + 64 <= jB; j += 64) moments_trip<R, 1>(rb, ab, T, j, lane, m, pc, apc);
+    for (; j + 64 * COMAP_AGRP <= jB; j += 64 * COMAP_AGRP) moments_trip<R, COMAP_AGRP>(rb, ab, T, j, lane, m, pc, apc, sair, par);
+    for (; j + 64 <= jB; j += 64) moments_trip<R, 1>(rb, ab, T, j, lane, m, pc, apc, sair, par);
     // leftovers: samples [0, 4 jA - R) and [4 j - R, n); pairs [0, kA) and [kB, n4)
     const int hs = min(n, 4 * jA - R), ts = max(hs, 4 * j - R);
     auto sample = [&](int s) {
@@ -609,11 +630,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COMAP_
     MomRow m[kCPW];
 #pragma unroll
     for (int r = 0; r < kCPW; ++r) { m[r].sd = m[r].sad = m[r].su = m[r].suu = m[r].suv = 0.0; m[r].bad = 0; }
+#if COMAP_A_ALDS
+    __shared__ double4 sair[2][64 * COMAP_AGRP];
+#else
+    double4 (*sair)[64 * COMAP_AGRP] = nullptr;
+#endif
     switch (t0 & 3) {
-    case 0: moments_rows_al<0>(row0, a, T, n, lane, m); break;
-    case 1: moments_rows_al<1>(row0, a, T, n, lane, m); break;
-    case 2: moments_rows_al<2>(row0, a, T, n, lane, m); break;
-    default: moments_rows_al<3>(row0, a, T, n, lane, m); break;
+    case 0: moments_rows_al<0>(row0, a, T, n, lane, m, sair); break;
+    case 1: moments_rows_al<1>(row0, a, T, n, lane, m, sair); break;
+    case 2: moments_rows_al<2>(row0, a, T, n, lane, m, sair); break;
+    default: moments_rows_al<3>(row0, a, T, n, lane, m, sair); break;
     }
     int tot = 0;
 #pragma unroll
