@@ -176,7 +176,6 @@ struct comap_l1_plan {
     double *unit_sums = nullptr;       // [U][8]: n, SA, SAA, Sv, Svv, N4
     double *mom = nullptr;             // [5][U*4096]: Sd, SAd, Su, Suu, Suv
     int32_t *nan_count = nullptr;      // [1]
-    bool moments_aligned = false;      // pass A runs k_moments_al (T % 4 == 0, 16-B aligned cube)
     bool moments_valid = false;
     bool moments_pending = false;      // pass A enqueued, NaN count not read back yet
     bool prefetched = false;           // comap_l1_prefetch launched pass A for the next atmosphere call
@@ -195,8 +194,6 @@ struct comap_l1_plan {
     double *dsum = nullptr;            // [U*4][16] per-band constants for pass D
     double *xreg = nullptr;            // [U*4096][2] regression x0,x1 (debug)
     double *dG = nullptr;              // [F][T]
-    double *sgb = nullptr;             // [F][4][T] per-band gain template sums (pass B one band per block)
-    int32_t b1 = 0;                    // pass B variant (COMAP_B1): 0 k_band_sums, else k_band_sums1 layout
     // NaN / calibrator paths
     int32_t *rowbad = nullptr;         // [U*4096] non-finite samples per row (pass A)
     int32_t nan_total = 0;             // total from the last pass A

@@ -340,7 +340,8 @@ bool valid(const comap_h5 *f) { return f && f->file >= 0; }
 constexpr int64_t kDirectMinBytes = 8ll << 20;     // below this one H5Dread is as fast
 constexpr int64_t kDirectPerThread = 32ll << 20;
 
-int direct_read(comap_h5 *f, hid_t d, hid_t ftype, hid_t mtype, int64_t elsize, int64_t offset, int64_t n, void *buf)
+int direct_read(comap_h5 *f, hid_t d, hid_t ftype, hid_t mtype, int64_t elsize, int64_t offset, int64_t n, void *buf,
+                std::string *err)
 {
     if (!f->readonly || n * elsize < kDirectMinBytes) return 0;
     Hid dcpl(H5Dget_create_plist(d));
@@ -357,14 +358,18 @@ int direct_read(comap_h5 *f, hid_t d, hid_t ftype, hid_t mtype, int64_t elsize, 
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
     const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)16, (int64_t)hw, bytes / kDirectPerThread}));
     const int64_t per = (bytes + nt - 1) / nt;
-    std::atomic<int> bad{0};
+    // errno is per thread and a short read sets none: each worker records its own
+    // failure (errno, or the file offset of an unexpected end of file)
+    std::vector<int> eno(nt, 0);
+    std::vector<int64_t> short_at(nt, -1);
     auto work = [&](int i) {
         int64_t lo = (int64_t)i * per, hi = std::min(bytes, lo + per);
         char *dst = static_cast<char *>(buf);
         while (lo < hi) {
             const ssize_t r = ::pread(f->fd, dst + lo, (size_t)std::min<int64_t>(hi - lo, 1ll << 30), start + lo);
             if (r < 0 && errno == EINTR) continue;
-            if (r <= 0) { bad = 1; return; }
+            if (r < 0) { eno[i] = errno; return; }
+            if (r == 0) { short_at[i] = start + lo; return; }
             lo += r;
         }
     };
@@ -372,7 +377,11 @@ int direct_read(comap_h5 *f, hid_t d, hid_t ftype, hid_t mtype, int64_t elsize, 
     for (int i = 1; i < nt; ++i) th.emplace_back(work, i);
     work(0);
     for (auto &t : th) t.join();
-    return bad ? -1 : 1;
+    for (int i = 0; i < nt; ++i) {
+        if (eno[i]) { *err = strerror(eno[i]); return -1; }
+        if (short_at[i] >= 0) { *err = "short read (end of file) at byte offset " + std::to_string(short_at[i]); return -1; }
+    }
+    return 1;
 }
 
 }  // namespace
@@ -529,8 +538,9 @@ int comap_h5_read_flat(comap_h5 *f, const char *path, int32_t dtype, int64_t els
     if (offset + n > n_elements(nd, dims)) return fail(std::string("flat range out of range in ") + path, -1);
     {
         Hid ft(H5Dget_type(d));
-        const int dr = ft.ok() ? direct_read(f, d, ft, mt, elsize, offset, n, buf) : 0;
-        if (dr < 0) return fail(std::string("pread ") + f->path + ": " + strerror(errno));
+        std::string err;
+        const int dr = ft.ok() ? direct_read(f, d, ft, mt, elsize, offset, n, buf, &err) : 0;
+        if (dr < 0) return fail(std::string("pread ") + f->path + ": " + err);
         if (dr > 0) return 0;
     }
     if (nd == 0) return H5Dread(d, mt, H5S_ALL, H5S_ALL, H5P_DEFAULT, buf) < 0 ? fail("read scalar") : 0;

@@ -3,23 +3,28 @@
 // The reference reduces each (feed, scan) with NumPy/SciPy
 // (comancpipeline/Analysis/Level1Averaging.py:792-872).  Here every step is a
 // weighted sum of the raw f32 cube d[f][b][c][t] with per-channel f64
-// coefficients, so the whole observation is four streaming passes over HBM:
+// coefficients, so the whole observation is three streaming passes over HBM:
 //
 //   pass A  k_moments      per channel, over t: sum d, sum A d, and the
 //                          stride-4 difference moments (atmosphere fit +
 //                          normalise_data rms)                  -> 4 B/samp·ch
-//   pass B  k_band_mean    per t, over the 993 median channels: band mean of
-//                          y = (d - o - a A)/rms                -> 4 B/samp·ch
-//           k_sliding_median (median_kernels.hip) on the band means
+//   pass B  k_band_sums    per t, over the listed median channels: the band
+//                          mean of y = (d - o - a A)/rms (median input) AND
+//                          every per-sample output sum (gain template, residual
+//                          and original band sums)              -> 4 B/samp·ch
+//           median_kernels.hip: the w = 6000 running median of the band means
 //   pass C  k_regress      per channel, over t: sum d mf        -> 4 B/samp·ch
-//   pass D  k_gain_avg     per t, over all 4096 channels: gain template sum
-//                          dG and both band averages            -> 4 B/samp·ch
+//
+// The regression enters the outputs only through per-band constants (k_finish);
+// k_gain_avg (the former pass D) runs only when a NaN regression coefficient
+// changes a channel weight (k_coef_d phase 1 flags it).
 //
 // Layout: time is contiguous (the reference's [F][B][C][T]); a wave reads
 // 64 lanes x 16 B of one channel row per instruction (coalesced).  Pass A/C
-// waves own 4 channel rows and share the airmass / median loads; pass B/D
-// workgroups own a 256-sample tile with one wave per band.  All arithmetic
-// is f64 (the reference upcasts to f64 at subtract_fitted_atmosphere).
+// waves own 4 / 8 channel rows and share the airmass / median loads; pass B
+// workgroups own a sub-tile of a 1024-sample tile with one wave per band.  All
+// arithmetic is f64 (the reference upcasts to f64 at subtract_fitted_atmosphere).
+// Variants measured slower are listed in DESIGN.md §3 (code in git history).
 #include "comap_internal.h"
 
 #include <cmath>
@@ -29,54 +34,17 @@
 
 using namespace comap;
 
-#ifndef COMAP_ALIGN_A
-#define COMAP_ALIGN_A 0      // pass A: peel to 128-B row alignment (measured slower: 9.27 -> 9.61 ms at C2)
-#endif
-#ifndef COMAP_ALIGN_C
-#define COMAP_ALIGN_C 1      // pass C: peel to 128-B row alignment (measured 8.98 -> 8.82 ms at C2)
-#endif
-#ifndef COMAP_ALIGN_B
-#define COMAP_ALIGN_B 1      // pass B: 128-B aligned tiles
-#endif
 #ifndef COMAP_GROUPS
 #define COMAP_GROUPS 1      // unit groups of the pass B / median / pass C pipeline (2 measured no faster with the sort-path median)
 #endif
 
 typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
-#ifndef COMAP_NT
-#define COMAP_NT 1   // measured at C2: pass B 9.55 -> 8.75 ms, pass C 8.86 -> 7.89 ms, pass A unchanged
-#endif
-// streaming load of 4 cube samples (COMAP_NT: non-temporal, no L2 allocation)
+// Streaming load of 4 cube samples, non-temporal: data read once never allocates in
+// L2, which keeps the airmass / median-filter rows every wave shares resident
+// (measured at C2: pass A 9.19 -> 8.82 ms, B 9.55 -> 8.75, C 8.86 -> 7.89).
 __device__ __forceinline__ f32x4u ld4(const float *p)
 {
-#if COMAP_NT
     return __builtin_nontemporal_load(reinterpret_cast<const f32x4u *>(p));
-#else
-    return *reinterpret_cast<const f32x4u *>(p);
-#endif
-}
-
-#ifndef COMAP_NT_A
-#define COMAP_NT_A COMAP_NT   // measured at C2 (AUNR=4): NT 8.82 ms, plain 9.19 ms
-#endif
-// pass A's cube loads (COMAP_NT_A selects non-temporal independently of B / C)
-__device__ __forceinline__ f32x4u ld4a(const float *p)
-{
-#if COMAP_NT_A
-    return __builtin_nontemporal_load(reinterpret_cast<const f32x4u *>(p));
-#else
-    return *reinterpret_cast<const f32x4u *>(p);
-#endif
-}
-
-typedef float f32x4a __attribute__((ext_vector_type(4)));   // 16-B aligned
-__device__ __forceinline__ f32x4a ld4al(const float *p)
-{
-#if COMAP_NT_A
-    return __builtin_nontemporal_load(reinterpret_cast<const f32x4a *>(p));
-#else
-    return *reinterpret_cast<const f32x4a *>(p);
-#endif
 }
 
 __device__ __forceinline__ double wave_sum(double v)
@@ -189,34 +157,15 @@ __global__ void __launch_bounds__(256) k_unit_sums(const int32_t *__restrict__ u
 // the stride-4 pairs u_k = d[4k]-d[4k+2]: Su, Suu, Suv (v_k = A[4k]-A[4k+2]).
 // normalise_data's rms for ANY atmosphere slope a follows in closed form:
 //   diff_k = u_k - a v_k  (the offset cancels).
-#ifndef COMAP_CPW
-#define COMAP_CPW 4   // measured at C2: 8 rows per wave 9.28 -> 10.13 ms
-#endif
-#ifndef COMAP_AUNR
-#define COMAP_AUNR 4  // sample groups per lane per trip (loads in flight = COMAP_AUNR x kCPW); measured at C2: 1 -> 9.39 ms, 2 -> 9.15, 4 -> 8.82, 8 -> 9.08
-#endif
-#ifndef COMAP_A_ALD
-#define COMAP_A_ALD 0   // >0: aligned 16-B loads + lane shuffle, COMAP_A_ALD groups per trip; measured at C2: 2 -> 17.0 ms, 4 -> 22.3 ms vs 8.85 off (parity green)
-#endif
-#ifndef COMAP_A_LDSAIR
-#define COMAP_A_LDSAIR 1   // airmass groups staged through LDS once per block per trip; measured at C2: 8.86 -> 8.65 ms
-#endif
-#ifndef COMAP_A_BADSUM
-// 1: a row's non-finite flag is !isfinite(sum d) -- NaN/Inf propagate through the f64
-// sum and f32 samples cannot overflow it (|x| < 3.4e38, n < 2^31), so the flag is exact
-// and rowbad / nan_count count flagged rows; 0: per-sample isfinite counts
-#define COMAP_A_BADSUM 0
-#endif
-constexpr int kCPW = COMAP_CPW;   // channel rows per wave
-#ifndef COMAP_AM_WPE
-#define COMAP_AM_WPE 0   // >0: waves per SIMD the register allocation must allow (default: the compiler's 3)
-#endif
-#if COMAP_AM_WPE
-#define COMAP_AM_ATTR __attribute__((amdgpu_waves_per_eu(COMAP_AM_WPE)))
-#else
-#define COMAP_AM_ATTR
-#endif
-__global__ void __launch_bounds__(256) COMAP_AM_ATTR k_moments(const float *__restrict__ tod, const double *__restrict__ A,
+// Wave shape and load depth by measurement at C2 (where the rejected
+// variants -- aligned loads with lane shifts, other wave shapes, forced occupancy --
+// are listed): 4 channel rows per wave (8: 9.28 -> 10.13 ms), 4 sample groups per
+// lane per trip with every row load issued before any is accumulated (1: 9.39 ms,
+// 2: 9.15, 4: 8.82, 8: 9.08), the trip's airmass staged once per block in LDS
+// (8.86 -> 8.65 ms).
+constexpr int kCPW = 4;    // channel rows per wave
+constexpr int kAUnr = 4;   // sample groups per lane per trip (loads in flight = kAUnr x kCPW)
+__global__ void __launch_bounds__(256) k_moments(const float *__restrict__ tod, const double *__restrict__ A,
                                                  const int32_t *__restrict__ units, int64_t T,
                                                  double *__restrict__ mom, int64_t UC, int32_t *nan_count,
                                                  int32_t *__restrict__ rowbad)
@@ -243,9 +192,9 @@ __global__ void __launch_bounds__(256) COMAP_AM_ATTR k_moments(const float *__re
         const double v = a0 - a2;
 #pragma unroll
         for (int r = 0; r < kCPW; ++r) {
-            const f32x4u x = ld4a(row0 + (int64_t)r * T + 4 * k);
+            const f32x4u x = ld4(row0 + (int64_t)r * T + 4 * k);
             const double x0 = x.x, x1 = x.y, x2 = x.z, x3 = x.w;
-            if (!COMAP_A_BADSUM) bad[r] += !isfinite(x.x) + !isfinite(x.y) + !isfinite(x.z) + !isfinite(x.w);
+            bad[r] += !isfinite(x.x) + !isfinite(x.y) + !isfinite(x.z) + !isfinite(x.w);
             sd[r] += (x0 + x1) + (x2 + x3);
             sad[r] = fma(a0, x0, sad[r]);
             sad[r] = fma(a1, x1, sad[r]);
@@ -257,87 +206,29 @@ __global__ void __launch_bounds__(256) COMAP_AM_ATTR k_moments(const float *__re
             suv[r] = fma(uu, v, suv[r]);
         }
     };
-    // groups of 4 stay on the scan's stride-4 pairs (normalise_data); when the row start
-    // is 16-B aligned, peel the groups before its first 128-B boundary so every wave
-    // load covers 8 whole lines
-    const int64_t idx0 = row0 - tod;
-    const int hg = (COMAP_ALIGN_A && (idx0 & 3) == 0) ? min(n4, (int)((-idx0) & 31) >> 2) : 0;
-    if (lane < hg) group(lane);
-    int k = hg + lane;
-#if COMAP_A_ALD
-    // Scan rows start 12 B into a 16-B chunk here (t0 = 3 mod 4), so the plain
-    // 16-B loads are misaligned.  Wave-uniform trips: lane l loads the aligned
-    // chunk l of the trip's row window, takes its neighbour's chunk by a lane
-    // shuffle (lane 63 loads chunk 64 itself) and assembles its 4 samples.
-    // Lane l still handles groups hg + l + 64 i in order (same sums).
-    for (int kb = hg; kb + 64 * COMAP_A_ALD <= n4; kb += 64 * COMAP_A_ALD, k += 64 * COMAP_A_ALD) {
-        f32x4a lo[COMAP_A_ALD][kCPW], ex[COMAP_A_ALD][kCPW];
-        int mis[kCPW];
-#pragma unroll
-        for (int r = 0; r < kCPW; ++r) mis[r] = uniform((int)((reinterpret_cast<uintptr_t>(row0 + (int64_t)r * T) >> 2) & 3));
-#pragma unroll
-        for (int j = 0; j < COMAP_A_ALD; ++j)
-#pragma unroll
-            for (int r = 0; r < kCPW; ++r) {
-                const float *q = row0 + (int64_t)r * T + 4 * (kb + 64 * j) - mis[r];
-                lo[j][r] = ld4al(q + 4 * lane);
-                ex[j][r] = lo[j][r];
-                if (lane == 63 && mis[r]) ex[j][r] = ld4al(q + 256);
-            }
-#pragma unroll
-        for (int j = 0; j < COMAP_A_ALD; ++j) {
-            const int kk = k + 64 * j;
-            const double a0 = a[4 * kk], a1 = a[4 * kk + 1], a2 = a[4 * kk + 2], a3 = a[4 * kk + 3];
-            const double v = a0 - a2;
-#pragma unroll
-            for (int r = 0; r < kCPW; ++r) {
-                const f32x4a L = lo[j][r];
-                f32x4a N;
-                N.x = __shfl_down(L.x, 1, 64); N.y = __shfl_down(L.y, 1, 64); N.z = __shfl_down(L.z, 1, 64);
-                if (lane == 63) { N.x = ex[j][r].x; N.y = ex[j][r].y; N.z = ex[j][r].z; }
-                float y0, y1, y2, y3;
-                switch (mis[r]) {
-                case 0: y0 = L.x; y1 = L.y; y2 = L.z; y3 = L.w; break;
-                case 1: y0 = L.y; y1 = L.z; y2 = L.w; y3 = N.x; break;
-                case 2: y0 = L.z; y1 = L.w; y2 = N.x; y3 = N.y; break;
-                default: y0 = L.w; y1 = N.x; y2 = N.y; y3 = N.z; break;
-                }
-                const double x0 = y0, x1 = y1, x2 = y2, x3 = y3;
-                if (!COMAP_A_BADSUM) bad[r] += !isfinite(y0) + !isfinite(y1) + !isfinite(y2) + !isfinite(y3);
-                sd[r] += (x0 + x1) + (x2 + x3);
-                sad[r] = fma(a0, x0, sad[r]);
-                sad[r] = fma(a1, x1, sad[r]);
-                sad[r] = fma(a2, x2, sad[r]);
-                sad[r] = fma(a3, x3, sad[r]);
-                const double uu = x0 - x2;
-                su[r] += uu;
-                suu[r] = fma(uu, uu, suu[r]);
-                suv[r] = fma(uu, v, suv[r]);
-            }
-        }
-    }
-#endif
-#if COMAP_AUNR > 1 && COMAP_A_LDSAIR
+    // groups of 4 stay on the scan's stride-4 pairs (normalise_data); the scans' rows
+    // start anywhere in a 16-B chunk, so the loads are unaligned
+    int k = lane;
     // the block's 4 waves walk the same samples of 16 rows: each trip's airmass groups are
     // read from L2 once per block into LDS (double-buffered, one barrier per trip) instead
     // of once per wave.  Trips are block-uniform (whole trips only; the rest below).
-    static_assert(COMAP_AUNR * 64 == 256, "one airmass group of 4 samples per thread");
-    __shared__ double4 air[2][COMAP_AUNR * 64];
+    static_assert(kAUnr * 64 == 256, "one airmass group of 4 samples per thread");
+    __shared__ double4 air[2][kAUnr * 64];
     {
         int par = 0;
-        for (int kb = hg; kb + 64 * COMAP_AUNR <= n4; kb += 64 * COMAP_AUNR, par ^= 1) {
-            f32x4u xs[COMAP_AUNR][kCPW];
+        for (int kb = 0; kb + 64 * kAUnr <= n4; kb += 64 * kAUnr, par ^= 1) {
+            f32x4u xs[kAUnr][kCPW];
 #pragma unroll
-            for (int j = 0; j < COMAP_AUNR; ++j)
+            for (int j = 0; j < kAUnr; ++j)
 #pragma unroll
-                for (int r = 0; r < kCPW; ++r) xs[j][r] = ld4a(row0 + (int64_t)r * T + 4 * (kb + 64 * j + lane));
+                for (int r = 0; r < kCPW; ++r) xs[j][r] = ld4(row0 + (int64_t)r * T + 4 * (kb + 64 * j + lane));
             {
                 const double *q = a + 4 * (kb + (int)threadIdx.x);
                 air[par][threadIdx.x] = make_double4(q[0], q[1], q[2], q[3]);
             }
             __syncthreads();
 #pragma unroll
-            for (int j = 0; j < COMAP_AUNR; ++j) {
+            for (int j = 0; j < kAUnr; ++j) {
                 const double4 av = air[par][64 * j + lane];
                 const double a0 = av.x, a1 = av.y, a2 = av.z, a3 = av.w;
                 const double v = a0 - a2;
@@ -345,7 +236,7 @@ __global__ void __launch_bounds__(256) COMAP_AM_ATTR k_moments(const float *__re
                 for (int r = 0; r < kCPW; ++r) {
                     const f32x4u x = xs[j][r];
                     const double x0 = x.x, x1 = x.y, x2 = x.z, x3 = x.w;
-                    if (!COMAP_A_BADSUM) bad[r] += !isfinite(x.x) + !isfinite(x.y) + !isfinite(x.z) + !isfinite(x.w);
+                    bad[r] += !isfinite(x.x) + !isfinite(x.y) + !isfinite(x.z) + !isfinite(x.w);
                     sd[r] += (x0 + x1) + (x2 + x3);
                     sad[r] = fma(a0, x0, sad[r]);
                     sad[r] = fma(a1, x1, sad[r]);
@@ -357,41 +248,9 @@ __global__ void __launch_bounds__(256) COMAP_AM_ATTR k_moments(const float *__re
                     suv[r] = fma(uu, v, suv[r]);
                 }
             }
-            k = kb + 64 * COMAP_AUNR + lane;
+            k = kb + 64 * kAUnr + lane;
         }
     }
-#elif COMAP_AUNR > 1
-    // COMAP_AUNR sample groups per lane per trip: every row load of the trip is issued
-    // before any is accumulated (same per-lane summation order as the plain loop)
-    for (; k + 64 * (COMAP_AUNR - 1) < n4; k += 64 * COMAP_AUNR) {
-        f32x4u xs[COMAP_AUNR][kCPW];
-#pragma unroll
-        for (int j = 0; j < COMAP_AUNR; ++j)
-#pragma unroll
-            for (int r = 0; r < kCPW; ++r) xs[j][r] = ld4a(row0 + (int64_t)r * T + 4 * (k + 64 * j));
-#pragma unroll
-        for (int j = 0; j < COMAP_AUNR; ++j) {
-            const int kk = k + 64 * j;
-            const double a0 = a[4 * kk], a1 = a[4 * kk + 1], a2 = a[4 * kk + 2], a3 = a[4 * kk + 3];
-            const double v = a0 - a2;
-#pragma unroll
-            for (int r = 0; r < kCPW; ++r) {
-                const f32x4u x = xs[j][r];
-                const double x0 = x.x, x1 = x.y, x2 = x.z, x3 = x.w;
-                if (!COMAP_A_BADSUM) bad[r] += !isfinite(x.x) + !isfinite(x.y) + !isfinite(x.z) + !isfinite(x.w);
-                sd[r] += (x0 + x1) + (x2 + x3);
-                sad[r] = fma(a0, x0, sad[r]);
-                sad[r] = fma(a1, x1, sad[r]);
-                sad[r] = fma(a2, x2, sad[r]);
-                sad[r] = fma(a3, x3, sad[r]);
-                const double uu = x0 - x2;
-                su[r] += uu;
-                suu[r] = fma(uu, uu, suu[r]);
-                suv[r] = fma(uu, v, suv[r]);
-            }
-        }
-    }
-#endif
     for (; k < n4; k += 64) group(k);
     // tail samples n4*4 .. n-1 (at most 3)
     const int tt = 4 * n4 + lane;
@@ -400,7 +259,7 @@ __global__ void __launch_bounds__(256) COMAP_AM_ATTR k_moments(const float *__re
 #pragma unroll
         for (int r = 0; r < kCPW; ++r) {
             const float xf = row0[(int64_t)r * T + tt];
-            if (!COMAP_A_BADSUM) bad[r] += !isfinite(xf);
+            bad[r] += !isfinite(xf);
             sd[r] += (double)xf;
             sad[r] = fma(at, (double)xf, sad[r]);
         }
@@ -410,243 +269,7 @@ __global__ void __launch_bounds__(256) COMAP_AM_ATTR k_moments(const float *__re
     for (int r = 0; r < kCPW; ++r) {
         const double s0 = wave_sum(sd[r]), s1 = wave_sum(sad[r]), s2 = wave_sum(su[r]);
         const double s3 = wave_sum(suu[r]), s4 = wave_sum(suv[r]);
-        const int nb = COMAP_A_BADSUM ? (int)!isfinite(s0) : (int)wave_sum((double)bad[r]);
-        tot += nb;
-        if (lane == 0) {
-            const int64_t idx = (int64_t)u * kBC + b * kChannels + c0 + r;
-            mom[idx] = s0;
-            mom[UC + idx] = s1;
-            mom[2 * UC + idx] = s2;
-            mom[3 * UC + idx] = s3;
-            mom[4 * UC + idx] = s4;
-            rowbad[idx] = nb;
-        }
-    }
-    if (lane == 0 && tot) atomicAdd(nan_count, tot);
-}
-
-// Pass A on 16-B aligned chunks (T % 4 == 0, so every row of a unit shares the
-// residue R = t0 mod 4).  Chunk j of a row = scan samples s = 4j - R .. 4j - R + 3.
-// A stride-4 pair (s, s + 2), s = 4k, has its first sample at element R of chunk k
-// and its second at element R + 2 of chunk k (R < 2) or element R - 2 of chunk k + 1
-// (R >= 2).  For R >= 2 the lane of chunk j takes pair j - 1 and gets element R of
-// chunk j - 1 from the lane below by one DPP row shift (wave_shr:1); lane 0 gets it
-// from the previous group's lane 63 (readlane carry), so every load is aligned and
-// no load is repeated.  The airmass pair term is shifted the same way.  The chunks
-// that are not whole scan samples with a whole pair (at most one at the head and
-// fewer than 64 at the tail) go through a per-sample / per-pair loop.
-#ifndef COMAP_AGRP
-#define COMAP_AGRP 2   // chunk groups per lane per trip (loads in flight = COMAP_AGRP x kCPW)
-#endif
-#ifndef COMAP_A_SCHED
-#define COMAP_A_SCHED 0
-#endif
-#ifndef COMAP_A_XLD
-#define COMAP_A_XLD 0   // 1: R >= 2 takes the pair's first sample by a second load, not a DPP shift
-#endif
-#ifndef COMAP_A_ALDS
-#define COMAP_A_ALDS 0  // 1: each trip's airmass chunks staged through LDS once per block (as k_moments)
-#endif
-constexpr int kDppWaveShr1 = 0x138;
-
-__device__ __forceinline__ int dpp_shr1(int old, int v)
-{
-    return __builtin_amdgcn_update_dpp(old, v, kDppWaveShr1, 0xf, 0xf, false);
-}
-
-__device__ __forceinline__ double dpp_shr1(double old, double v)
-{
-    const int2 o = __builtin_bit_cast(int2, old), x = __builtin_bit_cast(int2, v);
-    return __builtin_bit_cast(double, make_int2(dpp_shr1(o.x, x.x), dpp_shr1(o.y, x.y)));
-}
-
-__device__ __forceinline__ double readlane63(double v)
-{
-    const int2 x = __builtin_bit_cast(int2, v);
-    return __builtin_bit_cast(double, make_int2(__builtin_amdgcn_readlane(x.x, 63), __builtin_amdgcn_readlane(x.y, 63)));
-}
-
-struct MomRow {
-    double sd, sad, su, suu, suv;
-    int bad;
-};
-
-template <int R, int G>
-__device__ __forceinline__ void moments_trip(const float *__restrict__ rb, const double *__restrict__ ab, int64_t T,
-                                             int j, int lane, MomRow (&m)[kCPW], float (&pc)[kCPW], double &apc,
-                                             double4 (*sair)[64 * COMAP_AGRP], int &par)
-{
-    f32x4a xs[G][kCPW];
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-        for (int r = 0; r < kCPW; ++r) xs[g][r] = ld4al(rb + (int64_t)r * T + 4 * (j + 64 * g + lane));
-    // R >= 2: the pair's first sample from the lane below (chunk j - 1), all groups first
-    float pa[G][kCPW];
-    if constexpr (R >= 2) {
-#if COMAP_A_XLD
-        // the pair's first sample re-read from chunk j - 1 (same cache lines) instead of shifted in
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int r = 0; r < kCPW; ++r) pa[g][r] = rb[(int64_t)r * T + 4 * (j + 64 * g + lane - 1) + R];
-#else
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int r = 0; r < kCPW; ++r) {
-                const int e = __float_as_int(xs[g][r][R]);
-                pa[g][r] = __int_as_float(dpp_shr1(__float_as_int(pc[r]), e));
-                pc[r] = __int_as_float(__builtin_amdgcn_readlane(e, 63));
-            }
-#endif
-    }
-#if COMAP_A_ALDS
-    // the block's 4 waves walk the same chunks: the trip's airmass is read once per block
-    // (double-buffered, one barrier per trip; trips are block-uniform)
-    double4 *buf = sair[par];
-    par ^= 1;
-    if ((int)threadIdx.x < 64 * G) {
-        const double *q = ab + 4 * (j + (int)threadIdx.x);
-        buf[threadIdx.x] = make_double4(q[0], q[1], q[2], q[3]);
-    }
-    __syncthreads();
-#endif
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-#if COMAP_A_ALDS
-        const double4 av = buf[64 * g + lane];
-        const double a0 = av.x, a1 = av.y, a2 = av.z, a3 = av.w;
-#else
-        const double *ap = ab + 4 * (j + 64 * g + lane);
-        const double a0 = ap[0], a1 = ap[1], a2 = ap[2], a3 = ap[3];
-#endif
-        const double ae[4] = {a0, a1, a2, a3};
-        double v;
-        if constexpr (R < 2) {
-            v = ae[R] - ae[R + 2];
-        } else {
-#if COMAP_A_XLD
-            v = ab[4 * (j + 64 * g + lane - 1) + R] - ae[R - 2];
-#else
-            const double ap_ = dpp_shr1(apc, ae[R]);
-            apc = readlane63(ae[R]);
-            v = ap_ - ae[R - 2];
-#endif
-        }
-#pragma unroll
-        for (int r = 0; r < kCPW; ++r) {
-            const f32x4a x = xs[g][r];
-            const float pb = x[R < 2 ? R + 2 : R - 2];
-            const float pa_ = R < 2 ? x[R < 2 ? R : 0] : pa[g][r];
-            const double x0 = x.x, x1 = x.y, x2 = x.z, x3 = x.w;
-            m[r].bad += !isfinite(x.x) + !isfinite(x.y) + !isfinite(x.z) + !isfinite(x.w);
-            m[r].sd += (x0 + x1) + (x2 + x3);
-            m[r].sad = fma(a0, x0, m[r].sad);
-            m[r].sad = fma(a1, x1, m[r].sad);
-            m[r].sad = fma(a2, x2, m[r].sad);
-            m[r].sad = fma(a3, x3, m[r].sad);
-            const double uu = (double)pa_ - (double)pb;
-            m[r].su += uu;
-            m[r].suu = fma(uu, uu, m[r].suu);
-            m[r].suv = fma(uu, v, m[r].suv);
-        }
-#if COMAP_A_SCHED
-        __builtin_amdgcn_sched_barrier(0);   // keep the groups' conversions from all being hoisted
-#endif
-    }
-}
-
-template <int R>
-__device__ __forceinline__ void moments_rows_al(const float *__restrict__ row0, const double *__restrict__ a, int64_t T,
-                                                int n, int lane, MomRow (&m)[kCPW], double4 (*sair)[64 * COMAP_AGRP])
-{
-    int par = 0;
-    const float *rb = row0 - R;           // chunk 0, 16-B aligned
-    const double *ab = a - R;
-    const int n4 = n >> 2;
-    const int jA = R > 0 ? 1 : 0;
-    int jB = min((n + R) >> 2, R < 2 ? n4 : n4 + 1);
-    if (jB < jA) jB = jA;
-    float pc[kCPW] = {};                  // R >= 2: element R of the chunk before the group's lane 0
-    double apc = 0.0;
-    if constexpr (R >= 2) {
-#pragma unroll
-        for (int r = 0; r < kCPW; ++r) pc[r] = row0[(int64_t)r * T + 4 * (jA - 1)];
-        apc = a[4 * (jA - 1)];
-    }
-    int j = jA;
-    for (; j + 64 * COMAP_AGRP <= jB; j += 64 * COMAP_AGRP) moments_trip<R, COMAP_AGRP>(rb, ab, T, j, lane, m, pc, apc, sair, par);
-    for (; j + 64 <= jB; j += 64) moments_trip<R, 1>(rb, ab, T, j, lane, m, pc, apc, sair, par);
-    // leftovers: samples [0, 4 jA - R) and [4 j - R, n); pairs [0, kA) and [kB, n4)
-    const int hs = min(n, 4 * jA - R), ts = max(hs, 4 * j - R);
-    auto sample = [&](int s) {
-        const double at = a[s];
-#pragma unroll
-        for (int r = 0; r < kCPW; ++r) {
-            const float xf = row0[(int64_t)r * T + s];
-            m[r].bad += !isfinite(xf);
-            m[r].sd += (double)xf;
-            m[r].sad = fma(at, (double)xf, m[r].sad);
-        }
-    };
-    for (int s = lane; s < hs; s += 64) sample(s);
-    for (int s = ts + lane; s < n; s += 64) sample(s);
-    const int kA = min(n4, R < 2 ? jA : jA - 1), kB = max(kA, R < 2 ? j : j - 1);
-    auto pair = [&](int k) {
-        const double v = a[4 * k] - a[4 * k + 2];
-#pragma unroll
-        for (int r = 0; r < kCPW; ++r) {
-            const float *q = row0 + (int64_t)r * T + 4 * k;
-            const double uu = (double)q[0] - (double)q[2];
-            m[r].su += uu;
-            m[r].suu = fma(uu, uu, m[r].suu);
-            m[r].suv = fma(uu, v, m[r].suv);
-        }
-    };
-    for (int k = lane; k < kA; k += 64) pair(k);
-    for (int k = kB + lane; k < n4; k += 64) pair(k);
-}
-
-#ifndef COMAP_A_WPE
-#define COMAP_A_WPE 3   // waves per SIMD the register allocation must allow
-#endif
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COMAP_A_WPE))) k_moments_al(const float *__restrict__ tod, const double *__restrict__ A,
-                                                    const int32_t *__restrict__ units, int64_t T,
-                                                    double *__restrict__ mom, int64_t UC, int32_t *nan_count,
-                                                    int32_t *__restrict__ rowbad)
-{
-    const int wid = uniform(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const int groups_per_band = kChannels / (4 * kCPW);
-    int bid = blockIdx.x;
-    const int g = bid % groups_per_band; bid /= groups_per_band;
-    const int b = bid % kBands;
-    const int u = bid / kBands;
-    const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
-    const int c0 = g * 4 * kCPW + wid * kCPW;
-    const float *row0 = tod + ((int64_t)(f * kBands + b) * kChannels + c0) * T + t0;
-    const double *a = A + (int64_t)f * T + t0;
-    MomRow m[kCPW];
-#pragma unroll
-    for (int r = 0; r < kCPW; ++r) { m[r].sd = m[r].sad = m[r].su = m[r].suu = m[r].suv = 0.0; m[r].bad = 0; }
-#if COMAP_A_ALDS
-    __shared__ double4 sair[2][64 * COMAP_AGRP];
-#else
-    double4 (*sair)[64 * COMAP_AGRP] = nullptr;
-#endif
-    switch (t0 & 3) {
-    case 0: moments_rows_al<0>(row0, a, T, n, lane, m, sair); break;
-    case 1: moments_rows_al<1>(row0, a, T, n, lane, m, sair); break;
-    case 2: moments_rows_al<2>(row0, a, T, n, lane, m, sair); break;
-    default: moments_rows_al<3>(row0, a, T, n, lane, m, sair); break;
-    }
-    int tot = 0;
-#pragma unroll
-    for (int r = 0; r < kCPW; ++r) {
-        const double s0 = wave_sum(m[r].sd), s1 = wave_sum(m[r].sad), s2 = wave_sum(m[r].su);
-        const double s3 = wave_sum(m[r].suu), s4 = wave_sum(m[r].suv);
-        const int nb = (int)wave_sum((double)m[r].bad);
+        const int nb = (int)wave_sum((double)bad[r]);
         tot += nb;
         if (lane == 0) {
             const int64_t idx = (int64_t)u * kBC + b * kChannels + c0 + r;
@@ -934,14 +557,8 @@ __device__ __forceinline__ void load_raw(const float *__restrict__ p, int nv0, f
 
 // 4 groups x 4 samples per lane: a wave reads 4 KB of a channel row per load
 // pair (measured: 1 KB 10.6 ms, 2 KB 9.9 ms, 4 KB 9.45 ms at C2)
-#ifndef COMAP_KJB
-#define COMAP_KJB 4
-#endif
-#ifndef COMAP_BB
-#define COMAP_BB 2   // measured at C2: 2 -> 8.76 ms, 4 -> 8.98
-#endif
-constexpr int kJB = COMAP_KJB;             // groups of 4 samples per lane
-constexpr int kBB = COMAP_BB;              // channel-list entries per load batch
+constexpr int kJB = 4;                     // groups of 4 samples per lane
+constexpr int kBB = 2;                     // channel-list entries per load batch (4: 8.76 -> 8.98 ms at C2)
 constexpr int kSubB = kTile / (256 * kJB); // pass-B blocks per 1024-sample tile
 
 struct BandAcc {
@@ -964,39 +581,12 @@ __device__ __forceinline__ void band_fma(BandAcc &a, const double *__restrict__ 
         }
 }
 
-#ifndef COMAP_B_XCD
-#define COMAP_B_XCD 0   // 1: pass B tiles dealt to the XCDs in contiguous runs
-#endif
-#ifndef COMAP_B_PREF
-#define COMAP_B_PREF 0   // 1: the next batch's channel ids are loaded before this batch's rows
-#endif
 template <bool FULL>
 __device__ __forceinline__ void band_sums(const float *__restrict__ base, int64_t T, int nv0,
                                           const int32_t *__restrict__ lst, const double *__restrict__ wl, int cnt,
                                           BandAcc &a)
 {
     int j = 0;
-#if COMAP_B_PREF
-    // the row addresses of batch j + 1 depend on list loads: issue them one batch ahead
-    // so each batch's row loads start without waiting for its channel ids
-    int32_t cur[kBB], nxt[kBB];
-    if (kBB <= cnt) {
-#pragma unroll
-        for (int q = 0; q < kBB; ++q) cur[q] = lst[q];
-    }
-    for (; j + kBB <= cnt; j += kBB) {
-        const bool more = j + 2 * kBB <= cnt;
-#pragma unroll
-        for (int q = 0; q < kBB; ++q) nxt[q] = more ? lst[j + kBB + q] : 0;
-        f32x4u r[kBB][kJB];
-#pragma unroll
-        for (int q = 0; q < kBB; ++q) load_raw<kJB, FULL>(base + (int64_t)cur[q] * T, nv0, r[q]);
-#pragma unroll
-        for (int q = 0; q < kBB; ++q) band_fma(a, wl + 4 * (j + q), r[q]);
-#pragma unroll
-        for (int q = 0; q < kBB; ++q) cur[q] = nxt[q];
-    }
-#else
     for (; j + kBB <= cnt; j += kBB) {
         f32x4u r[kBB][kJB];
 #pragma unroll
@@ -1004,7 +594,6 @@ __device__ __forceinline__ void band_sums(const float *__restrict__ base, int64_
 #pragma unroll
         for (int q = 0; q < kBB; ++q) band_fma(a, wl + 4 * (j + q), r[q]);
     }
-#endif
     for (; j < cnt; ++j) {
         f32x4u r[kJB];
         load_raw<kJB, FULL>(base + (int64_t)lst[j] * T, nv0, r);
@@ -1013,15 +602,7 @@ __device__ __forceinline__ void band_sums(const float *__restrict__ base, int64_
 }
 
 // Block = 4 waves (wave b = band b) on a 256 kJB-sample sub-tile of a 1024-sample tile.
-#ifndef COMAP_B_WPE
-#define COMAP_B_WPE 0   // >0: waves per SIMD the register allocation must allow (default: the compiler's 2)
-#endif
-#if COMAP_B_WPE
-#define COMAP_B_ATTR __attribute__((amdgpu_waves_per_eu(COMAP_B_WPE)))
-#else
-#define COMAP_B_ATTR
-#endif
-__global__ void __launch_bounds__(256) COMAP_B_ATTR k_band_sums(const float *__restrict__ tod, const double *__restrict__ A,
+__global__ void __launch_bounds__(256) k_band_sums(const float *__restrict__ tod, const double *__restrict__ A,
                                                    const int32_t *__restrict__ units, const int32_t *__restrict__ tiles,
                                                    int64_t tile0, int64_t T, const int32_t *__restrict__ dlist,
                                                    const int32_t *__restrict__ dcnt, const double *__restrict__ dw,
@@ -1032,19 +613,7 @@ __global__ void __launch_bounds__(256) COMAP_B_ATTR k_band_sums(const float *__r
     __shared__ double sg[kBands][256 * kJB];
     const int b = uniform(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-#if COMAP_B_XCD
-    // XCD-contiguous tiles: workgroups b, b + 8, ... share an XCD (round-robin dispatch),
-    // so logical block ids are dealt to the 8 XCDs in contiguous runs -- the blocks an XCD
-    // runs at once then read the same few units' rows (fewer distinct pages in its TLB)
-    int lbid;
-    {
-        const int nwg = (int)gridDim.x, q = nwg / 8, r = nwg % 8, x = (int)blockIdx.x % 8;
-        lbid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (int)blockIdx.x / 8;
-    }
-    const int tile = (int)(tile0 + lbid / kSubB), sub = lbid % kSubB;
-#else
     const int tile = (int)(tile0 + blockIdx.x / kSubB), sub = blockIdx.x % kSubB;
-#endif
     const int u = tiles[2 * tile], toff = tiles[2 * tile + 1] + 256 * kJB * sub;
     const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
     if (toff >= n) return;                          // whole block: past the scan end
@@ -1084,108 +653,6 @@ __global__ void __launch_bounds__(256) COMAP_B_ATTR k_band_sums(const float *__r
         }
 }
 
-// Pass B, one band per block (COMAP_B1): the block's kTile / (256 J) waves cover
-// consecutive 256 J-sample pieces of ONE 1024-sample tile of one band, so each
-// listed channel row is read as one 4 KB run by the whole block while a wave holds
-// only 4 J samples x 4 sums (J = 1: 32 accumulator VGPRs instead of 128, more waves
-// per SIMD).  Per sample the channel order and the FMAs are those of k_band_sums
-// (bit-identical outputs); the gain template is written per band (sgb [F][4][T])
-// and summed over the bands in k_finish in k_band_sums' order.
-#ifndef COMAP_B1
-#define COMAP_B1 0
-#endif
-#ifndef COMAP_KJB1
-#define COMAP_KJB1 1
-#endif
-#ifndef COMAP_BB1
-#define COMAP_BB1 8
-#endif
-// TPB > 1: the block's waves cover TPB consecutive tiles of the band (COMAP_B1=2/4/8:
-// a block then reads TPB x 4 KB of each listed row, TPB times fewer distinct rows in
-// flight across the chip for the same number of resident waves).
-template <int J, int BB, int TPB = 1>
-__global__ void __launch_bounds__(kTile / (4 * J) * TPB) k_band_sums1(const float *__restrict__ tod,
-                                                                const double *__restrict__ A,
-                                                                const int32_t *__restrict__ units,
-                                                                const int32_t *__restrict__ tiles, int64_t tile0,
-                                                                int64_t ntiles, int64_t T,
-                                                                const int32_t *__restrict__ dlist,
-                                                                const int32_t *__restrict__ dcnt,
-                                                                const double *__restrict__ dw,
-                                                                const double *__restrict__ bsum, double *__restrict__ mb,
-                                                                double *__restrict__ sr_out, double *__restrict__ so_out,
-                                                                double *__restrict__ sgb)
-{
-    constexpr int kWpt = kTile / (256 * J);                    // waves per tile
-    const int b = blockIdx.x % kBands;
-    const int w = uniform((int)(threadIdx.x >> 6));
-    const int64_t tl = (int64_t)(blockIdx.x / kBands) * TPB + w / kWpt;
-    if (tl >= ntiles) return;
-    const int tile = (int)(tile0 + tl);
-    const int u = tiles[2 * tile];
-    const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
-    const int wbase = tiles[2 * tile + 1] + 256 * J * (w % kWpt);
-    if (wbase >= n) return;                                     // whole wave past the scan end
-    const int lane = threadIdx.x & 63;
-    const int rl = wbase + 4 * lane;                            // this lane's first sample
-    const int nv0 = n - rl;
-    const float *base = tod + (int64_t)(f * kBands + b) * kChannels * T + t0 + rl;
-    const int ub = u * kBands + b;
-    double am[4 * J], ag[4 * J], ar[4 * J], ao[4 * J];
-#pragma unroll
-    for (int i = 0; i < 4 * J; ++i) am[i] = ag[i] = ar[i] = ao[i] = 0.0;
-    const int32_t *lst = dlist + (int64_t)ub * kChannels;
-    const double *wl = dw + 4 * (int64_t)ub * kChannels;
-    const int cnt = dcnt[ub];
-    auto fma4 = [&](const double *__restrict__ w, const f32x4u (&r)[J]) {
-        const double wa = w[0], wg = w[1], wr = w[2], wo = w[3];
-#pragma unroll
-        for (int g = 0; g < J; ++g)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int i = 4 * g + e;
-                const double x = (double)r[g][e];
-                am[i] = fma(wa, x, am[i]);
-                ag[i] = fma(wg, x, ag[i]);
-                ar[i] = fma(wr, x, ar[i]);
-                ao[i] = fma(wo, x, ao[i]);
-            }
-    };
-    auto run = [&](auto full) {
-        constexpr bool FULL = decltype(full)::value;
-        int j = 0;
-        for (; j + BB <= cnt; j += BB) {
-            f32x4u r[BB][J];
-#pragma unroll
-            for (int q = 0; q < BB; ++q) load_raw<J, FULL>(base + (int64_t)lst[j + q] * T, nv0, r[q]);
-#pragma unroll
-            for (int q = 0; q < BB; ++q) fma4(wl + 4 * (j + q), r[q]);
-        }
-        for (; j < cnt; ++j) {
-            f32x4u r[J];
-            load_raw<J, FULL>(base + (int64_t)lst[j] * T, nv0, r);
-            fma4(wl + 4 * j, r);
-        }
-    };
-    if (n - wbase >= 256 * J) run(std::true_type{});
-    else run(std::false_type{});
-    const double *bs = bsum + 4 * (int64_t)ub;
-    const double beta = bs[0], gamma = bs[1], cn = bs[2];
-    const int64_t rowo = (int64_t)(f * kBands + b) * T + t0 + rl;
-    const double *a = A + (int64_t)f * T + t0 + rl;
-#pragma unroll
-    for (int g = 0; g < J; ++g)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int i = 4 * g + e, o = 256 * g + e;
-            if (o >= nv0 || rl + o < 0) continue;   // before the scan: aligned-tile lead-in
-            mb[rowo + o] = cn > 0 ? (am[i] - beta - gamma * a[o]) / cn : NAN;
-            sr_out[rowo + o] = ar[i];
-            so_out[rowo + o] = ao[i];
-            sgb[rowo + o] = ag[i];
-        }
-}
-
 // ------------------------------------------------------------------ series sums for pass C
 // ss[ub] = {sum mf, sum mf^2, sum A mf}; zeroes mf of skipped bands.
 __global__ void __launch_bounds__(256) k_series_sums(int ub0, const int32_t *__restrict__ units, const double *__restrict__ A,
@@ -1222,19 +689,9 @@ __global__ void __launch_bounds__(256) k_series_sums(int ub0, const int32_t *__r
 // A: a wave owns kRPW entries of the (unit, band)'s channel list and walks
 // the scan 4 samples per lane, sharing the mf loads between its rows.  Bands
 // the median filter skipped need no regression and are not read.
-#ifndef COMAP_RPW
-#define COMAP_RPW 8
-#endif
-#ifndef COMAP_C_LDSMF
-#define COMAP_C_LDSMF 0   // 1: median-filter groups staged through LDS once per block per 4 trips (measured no faster: 7.89 vs 7.93 ms)
-#endif
-#ifndef COMAP_C_LDSUNR
-#define COMAP_C_LDSUNR 1   // trips unrolled per staged run (loads in flight = COMAP_C_LDSUNR x kRPW)
-#endif
-#ifndef COMAP_CUNR
-#define COMAP_CUNR 1   // sample groups per lane per trip in pass C; measured at C2: 1 -> 7.90 ms, 2 -> 8.07, (RPW 4) 2 -> 8.64, 4 -> 8.39
-#endif
-constexpr int kRPW = COMAP_RPW;
+// (measured at C2 and rejected: 4 or 16 rows per wave, 2-4 sample groups per trip,
+// the median-filter groups staged through LDS -- DESIGN §3)
+constexpr int kRPW = 8;
 constexpr int kRegBlocks = kChannels / (4 * kRPW);   // blocks per (unit, band)
 __global__ void __launch_bounds__(256) k_regress(int ub0, const float *__restrict__ tod, const double *__restrict__ mf,
                                                  const int32_t *__restrict__ units, int64_t T,
@@ -1248,37 +705,22 @@ __global__ void __launch_bounds__(256) k_regress(int ub0, const float *__restric
     const int cnt = dcnt[ub];
     const int j0 = g * 4 * kRPW + wid * kRPW;
     if (bsum[4 * (int64_t)ub + 3] <= 0) return;      // band skipped by median_filter (block-uniform)
-#if COMAP_C_LDSMF
-    if (g * 4 * kRPW >= cnt) return;                   // whole block past the list
-    const bool live = j0 < cnt;                        // else: only helps stage the block's mf
-#else
     if (j0 >= cnt) return;
-#endif
     const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
     const int32_t *lst = dlist + (int64_t)ub * kChannels;
     const float *band = tod + (int64_t)(f * kBands + b) * kChannels * T + t0;
     const float *row[kRPW];
-#if COMAP_C_LDSMF
-    const int jw = live ? j0 : 0;
-#else
-    const int jw = j0;
-#endif
 #pragma unroll
-    for (int r = 0; r < kRPW; ++r) row[r] = band + (int64_t)lst[jw + r < cnt ? jw + r : jw] * T;   // pad: re-read
+    for (int r = 0; r < kRPW; ++r) row[r] = band + (int64_t)lst[j0 + r < cnt ? j0 + r : j0] * T;   // pad: re-read
     const double *m = mf + (int64_t)(f * kBands + b) * T + t0;
     double acc[kRPW];
 #pragma unroll
     for (int r = 0; r < kRPW; ++r) acc[r] = 0.0;
-#if COMAP_ALIGN_C
     // peel the samples before the first 128-B boundary of the list's first row (every row
     // of the band shares it when T is a multiple of 32), so each wave load covers 8 whole
     // lines; block-uniform in any case
     const int head = (int)min((int64_t)n, (-(int64_t)(band + (int64_t)lst[0] * T - tod)) & 31);
-#if COMAP_C_LDSMF
-    if (live && lane < head) {
-#else
     if (lane < head) {
-#endif
 #pragma unroll
         for (int r = 0; r < kRPW; ++r) acc[r] = fma(m[lane], (double)row[r][lane], acc[r]);
     }
@@ -1286,71 +728,8 @@ __global__ void __launch_bounds__(256) k_regress(int ub0, const float *__restric
     for (int r = 0; r < kRPW; ++r) row[r] += head;
     m += head;
     const int nb = n - head;
-#else
-    const int nb = n;
-#endif
     const int n4 = nb >> 2;
     int k = lane;
-#if COMAP_CUNR > 1
-    // COMAP_CUNR sample groups per trip, all row loads issued first (per-lane order unchanged)
-    for (; k + 64 * (COMAP_CUNR - 1) < n4; k += 64 * COMAP_CUNR) {
-        f32x4u xs[COMAP_CUNR][kRPW];
-#pragma unroll
-        for (int j = 0; j < COMAP_CUNR; ++j)
-#pragma unroll
-            for (int r = 0; r < kRPW; ++r) xs[j][r] = ld4(row[r] + 4 * (k + 64 * j));
-#pragma unroll
-        for (int j = 0; j < COMAP_CUNR; ++j) {
-            const int kk = k + 64 * j;
-            const double m0 = m[4 * kk], m1 = m[4 * kk + 1], m2 = m[4 * kk + 2], m3 = m[4 * kk + 3];
-#pragma unroll
-            for (int r = 0; r < kRPW; ++r) {
-                double s = acc[r];
-                s = fma(m0, (double)xs[j][r].x, s);
-                s = fma(m1, (double)xs[j][r].y, s);
-                s = fma(m2, (double)xs[j][r].z, s);
-                s = fma(m3, (double)xs[j][r].w, s);
-                acc[r] = s;
-            }
-        }
-    }
-#endif
-#if COMAP_C_LDSMF
-    // the block's 4 waves walk the same samples of one (unit, band): each run of 4 trips'
-    // median-filter groups is read from L2 once per block into LDS (double-buffered,
-    // one barrier per 4 trips) instead of once per wave.  Block-uniform trips; waves
-    // whose rows are all padding still take part in the staging.
-    __shared__ double4 mfs[2][256];
-    {
-        int par = 0;
-        for (int kb = 0; kb + 256 <= n4; kb += 256, par ^= 1) {
-            {
-                const double *q = m + 4 * (kb + (int)threadIdx.x);
-                mfs[par][threadIdx.x] = make_double4(q[0], q[1], q[2], q[3]);
-            }
-            __syncthreads();
-            if (live) {
-#pragma unroll COMAP_C_LDSUNR
-                for (int i = 0; i < 4; ++i) {
-                    const int kk = kb + 64 * i + lane;
-                    const double4 mv = mfs[par][64 * i + lane];
-#pragma unroll
-                    for (int r = 0; r < kRPW; ++r) {
-                        const f32x4u x = ld4(row[r] + 4 * kk);
-                        double s = acc[r];
-                        s = fma(mv.x, (double)x.x, s);
-                        s = fma(mv.y, (double)x.y, s);
-                        s = fma(mv.z, (double)x.z, s);
-                        s = fma(mv.w, (double)x.w, s);
-                        acc[r] = s;
-                    }
-                }
-            }
-            k = kb + 256 + lane;
-        }
-    }
-    if (!live) return;
-#endif
     for (; k < n4; k += 64) {
         const double m0 = m[4 * k], m1 = m[4 * k + 1], m2 = m[4 * k + 2], m3 = m[4 * k + 3];
 #pragma unroll
@@ -1668,8 +1047,7 @@ __global__ void __launch_bounds__(256) k_finish(const int32_t *__restrict__ unit
                                                 int64_t T, const double *__restrict__ A,
                                                 const double *__restrict__ mf, const double *__restrict__ dsum,
                                                 double *__restrict__ tod_out, double *__restrict__ orig_out,
-                                                double *__restrict__ dG, const int32_t *__restrict__ flag,
-                                                const double *__restrict__ sgb)
+                                                double *__restrict__ dG, const int32_t *__restrict__ flag)
 {
     if (*flag != 0) return;                          // mismatch: the legacy passes produce the outputs
     const int u = tiles[2 * blockIdx.x];
@@ -1680,13 +1058,7 @@ __global__ void __launch_bounds__(256) k_finish(const int32_t *__restrict__ unit
         if (r >= n) break;
         const int64_t t = t0 + r;
         const double a = A[(int64_t)f * T + t];
-        double m[kBands], g;
-        if (sgb) {   // k_band_sums1: per-band gain template sums, added in k_band_sums' order
-            const double *q = sgb + (int64_t)f * kBands * T + t;
-            g = (q[0] + q[T]) + (q[2 * T] + q[3 * T]);
-        } else {
-            g = dG[(int64_t)f * T + t];
-        }
+        double m[kBands], g = dG[(int64_t)f * T + t];
 #pragma unroll
         for (int b = 0; b < kBands; ++b) {
             m[b] = mf[(int64_t)(f * kBands + b) * T + t];
@@ -1949,11 +1321,6 @@ extern "C" int comap_l1_plan_create(comap_ctx *ctx, const comap_obs_desc *d, com
     p->ctx = ctx;
     p->F = d->n_feeds; p->S = d->n_scans; p->U = d->n_units; p->T = d->n_samples;
     p->tod = d->tod; p->el = d->el;
-    // pass A on aligned chunks (opt-in, COMAP_A_DPP=1; measured slower) needs 16-B aligned rows
-    {
-        const char *e = getenv("COMAP_A_DPP");
-        p->moments_aligned = p->T % 4 == 0 && (reinterpret_cast<uintptr_t>(p->tod) & 15) == 0 && e && e[0] == '1';
-    }
     p->units_h.assign(d->units_host, d->units_host + 4 * (size_t)d->n_units);
     for (int u = 0; u < p->U; ++u) {
         const int32_t *q = &p->units_h[4 * u];
@@ -1970,7 +1337,9 @@ extern "C" int comap_l1_plan_create(comap_ctx *ctx, const comap_obs_desc *d, com
     std::vector<int32_t> tiles_b;
     std::vector<int64_t> tub(p->U + 1, 0);
     for (int u = 0; u < p->U; ++u) {
-        const int shift = (COMAP_ALIGN_B && p->T % 32 == 0) ? (p->units_h[4 * u + 2] & 31) : 0;
+        // pass B tiles start on 128-B boundaries (up to 31 samples before the scan, read from
+        // the same row and never written): PMC bytes 56.9 -> 55.3 GB, time -2.5% at C2
+        const int shift = (p->T % 32 == 0) ? (p->units_h[4 * u + 2] & 31) : 0;
         for (int t = -shift; t < p->units_h[4 * u + 3]; t += kTile) { tiles_b.push_back(u); tiles_b.push_back(t); }
         tub[u + 1] = (int64_t)tiles_b.size() / 2;
     }
@@ -2002,12 +1371,6 @@ extern "C" int comap_l1_plan_create(comap_ctx *ctx, const comap_obs_desc *d, com
     rc |= dalloc(ctx, &p->dsum, 16 * (size_t)p->U * kBands);
     rc |= dalloc(ctx, &p->xreg, 2 * (size_t)UC);
     rc |= dalloc(ctx, &p->dG, (size_t)p->F * p->T);
-    {   // pass B with one band per block (COMAP_B1, env overrides): per-band gain template sums
-        int b1 = COMAP_B1;
-        if (const char *e = getenv("COMAP_B1")) b1 = atoi(e);
-        if (b1) rc |= dalloc(ctx, &p->sgb, (size_t)p->F * kBands * p->T);
-        p->b1 = b1;
-    }
     rc |= dalloc(ctx, &p->rowbad, UC);
     rc |= dalloc(ctx, &p->ubs, 4 * (size_t)p->U * kBands);
     rc |= dalloc(ctx, &p->fitsum, 2 * (size_t)UC);
@@ -2080,7 +1443,7 @@ extern "C" int comap_l1_plan_destroy(comap_l1_plan *p)
     void *bufs[] = {p->units, p->tiles, p->tiles_b, p->airmass, p->unit_sums, p->mom,
                     p->nan_count, p->alpha, p->nf, p->bsum, p->mb, p->mf, p->ssum, p->sdm, p->gw,
                     p->gmode, p->kap, p->dsum, p->xreg, p->dG, p->rowbad, p->ubs, p->fitsum, p->oa,
-                    p->flag, p->dlist, p->dcnt, p->dw, p->nanpos, p->nanpos_n, p->vane_dev, p->sgb};
+                    p->flag, p->dlist, p->dcnt, p->dw, p->nanpos, p->nanpos_n, p->vane_dev};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (int g = 0; g < comap_l1_plan::kMaxGroups; ++g) {
@@ -2112,11 +1475,7 @@ static int launch_moments(comap_l1_plan *p)
     p->pre_a_valid = true;
     COMAP_CHECK(ctx, hipMemsetAsync(p->nan_count, 0, 4, ctx->stream));
     const int64_t grid = (int64_t)p->U * kBands * (kChannels / (4 * kCPW));
-    if (p->moments_aligned)
-        PROF(p, KV_MOMENTS, k_moments_al<<<grid, 256, 0, ctx->stream>>>(p->tod, p->airmass, p->units, p->T, p->mom, UC,
-                                                                        p->nan_count, p->rowbad));
-    else
-        PROF(p, KV_MOMENTS, k_moments<<<grid, 256, 0, ctx->stream>>>(p->tod, p->airmass, p->units, p->T, p->mom, UC,
+    PROF(p, KV_MOMENTS, k_moments<<<grid, 256, 0, ctx->stream>>>(p->tod, p->airmass, p->units, p->T, p->mom, UC,
                                                                      p->nan_count, p->rowbad));
     COMAP_LAUNCH_CHECK(ctx);
     COMAP_CHECK(ctx, hipMemcpyAsync(p->nan_host, p->nan_count, 4, hipMemcpyDeviceToHost, ctx->stream));
@@ -2363,21 +1722,6 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
     for (int g = 0; g < p->ngroups; ++g) {
         const int64_t t0 = p->grpb_tile0[g], nt = p->grpb_tile0[g + 1] - t0;
         const int ub0 = p->grp_u0[g] * kBands, nub = (p->grp_u0[g + 1] - p->grp_u0[g]) * kBands;
-        if (p->sgb) {
-            // COMAP_B1 = 1: J = COMAP_KJB1 samples groups per lane, one tile per block; 2 / 4: J = 4,
-            // 2 / 4 tiles per block; 8: J = 2, 4 tiles per block
-#define B1_LAUNCH(J, BB, TPB)                                                                                  \
-    PROF(p, KV_BAND_SUMS, (k_band_sums1<J, BB, TPB><<<kBands * ((nt + TPB - 1) / TPB), kTile / (4 * J) * TPB, 0, st>>>( \
-                              p->tod, p->airmass, p->units, p->tiles_b, t0, nt, p->T, p->dlist, p->dcnt, p->dw,   \
-                              p->bsum, p->mb, tod_out, orig_out, p->sgb)))
-            switch (p->b1) {
-            case 2: B1_LAUNCH(4, 2, 2); break;
-            case 4: B1_LAUNCH(4, 2, 4); break;
-            case 8: B1_LAUNCH(2, 4, 4); break;
-            default: B1_LAUNCH(COMAP_KJB1, COMAP_BB1, 1); break;
-            }
-#undef B1_LAUNCH
-        } else
             PROF(p, KV_BAND_SUMS, k_band_sums<<<kSubB * nt, 256, 0, st>>>(p->tod, p->airmass, p->units, p->tiles_b, t0,
                                                                         p->T, p->dlist, p->dcnt, p->dw, p->bsum,
                                                                         p->mb, tod_out, orig_out, p->dG));
@@ -2410,7 +1754,7 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
                                                                 p->flag));
     COMAP_LAUNCH_CHECK(ctx);
     PROF(p, KV_FINISH, k_finish<<<p->n_tiles, 256, 0, st>>>(p->units, p->tiles, p->T, p->airmass, p->mf, p->dsum,
-                                                            tod_out, orig_out, p->dG, p->flag, p->sgb));
+                                                            tod_out, orig_out, p->dG, p->flag));
     COMAP_LAUNCH_CHECK(ctx);
     PROF(p, KV_SCAN_WEIGHTS, k_scan_weights<<<UB, 256, 0, st>>>(p->units, p->T, tod_out, w_out));
     COMAP_LAUNCH_CHECK(ctx);

@@ -488,7 +488,16 @@ class DeviceDestriper:
         else:
             # COMAP_DS_GRAPH=1: the captured-graph driver (one launch per 16 iterations);
             # default: the eager batched driver (7 host calls per iteration, 16 per check)
-            solver = cg_solve_graph if os.environ.get('COMAP_DS_GRAPH') == '1' else cg_solve_batched
+            # (graph capture of a collective needs RCCL: with any other backend, e.g. the gloo
+            # rehearsals, the eager driver runs instead)
+            solver = cg_solve_batched
+            if os.environ.get('COMAP_DS_GRAPH') == '1':
+                if d.get_backend() == 'nccl':
+                    solver = cg_solve_graph
+                else:
+                    import warnings
+                    warnings.warn(f'COMAP_DS_GRAPH=1 needs the nccl (RCCL) backend, not {d.get_backend()}: '
+                                  'using the eager CG driver')
             x, it, h, nnum = solver(ops, torch_allreduce, threshold, niter)
             _, hits, _ = ops.local_maps()
             torch_allreduce(hits)

@@ -56,8 +56,9 @@ class HDF5Data:
     _source: str = ''
     hdf5_file: object = field(default=None, repr=False)   # the open H5File (lazy datasets read from it)
 
-    def __del__(self):
-        self.close()
+    # No __del__ closing the file: lazy H5Dataset / H5Rows views handed to other
+    # containers (sharding.slice_feeds) hold the H5File themselves, and it closes
+    # in its own __del__ once the last of them is gone.
 
     def close(self):
         f, self.hdf5_file = getattr(self, 'hdf5_file', None), None
@@ -140,8 +141,23 @@ class HDF5Data:
             np.savez(filename, __attrs__=json.dumps(attrs, default=str),
                      **{k.replace('/', '|'): v for k, v in out.items()})
             return
-        if self.hdf5_file is not None and os.path.abspath(self.hdf5_file.filename) == os.path.abspath(filename):
-            self.close()                      # lazy datasets of this file are read before it is rewritten
+        src = self.hdf5_file
+        same = src is not None and os.path.abspath(src.filename) == os.path.abspath(filename)
+        if same:
+            # HDF5 cannot open a file for writing while it is open read-only: close the
+            # handle for the write, then re-open it on the same H5File object so every
+            # lazy view of it (large_datasets here, H5Rows in shards) reads again
+            src.close()
+        try:
+            self._write_h5(filename, out)
+        finally:
+            if same:
+                src.reopen()
+        if self.hdf5_file is None:
+            self.hdf5_file = h5file.H5File(filename, 'r')
+            self._source = filename
+
+    def _write_h5(self, filename, out):
         with h5file.H5File(filename, 'a' if os.path.exists(filename) else 'w') as h:
             for k, v in out.items():
                 h.write(k, v)
@@ -150,9 +166,6 @@ class HDF5Data:
                     h.require_group(p)
                 for a, v in d.items():
                     h.set_attr(p, a, v)
-        if self.hdf5_file is None:
-            self.hdf5_file = h5file.H5File(filename, 'r')
-            self._source = filename
 
 
 class RepointEdges:

@@ -168,6 +168,18 @@ class H5File:
         if h:
             _check(lib().comap_h5_close(h), f'close {self.filename}')
 
+    def reopen(self):
+        """Re-open a closed read-only file on the same object, so every lazy
+        dataset / row view taken from it (here or in a shard) works again after
+        the file was closed for a rewrite (HDF5Data.write_data_file)."""
+        if self._h:
+            return
+        if self.mode != 'r':
+            raise H5Error(f'{self.filename}: only read-only files are re-opened')
+        h = c_void_p()
+        _check(lib().comap_h5_open(_b(self.filename), 0, ctypes.byref(h)), f'open {self.filename}')
+        self._h = h
+
     def __enter__(self):
         return self
 

@@ -60,7 +60,7 @@ def main():
                       'fetch_size_kb': fetch.get(k), 'write_size_kb': write.get(k)}
     json.dump(traffic, open(os.path.join(here, f'{tag}_traffic.json'), 'w'), indent=1)
     if latest:
-        json.dump({k: v['hbm_bytes_per_launch'] for k, v in traffic.items()},
+        json.dump(dict({k: v['hbm_bytes_per_launch'] for k, v in traffic.items()}, _source=tag),
                   open(os.path.join(here, 'traffic_latest.json'), 'w'), indent=1)
     print(json.dumps(traffic, indent=1))
 

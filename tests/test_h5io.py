@@ -232,6 +232,45 @@ def test_feed_rows_view_reads_only_its_range(tmp_path):
     d.close()
 
 
+def test_shard_view_outlives_its_parent(tmp_path):
+    """A shard's lazy rows keep the file open after the parent container is
+    dropped (the H5File closes with its last view, not with the parent)."""
+    import gc
+    from comapreduce_amd.pipeline.sharding import slice_feeds
+    p = str(tmp_path / 'c.h5')
+    x = np.random.default_rng(3).standard_normal((4, 4, 2, 9)).astype(np.float32)
+    with H.H5File(p, 'w') as f:
+        f.write('spectrometer/tod', x)
+        f.write('spectrometer/feeds', np.arange(1, 5))
+    d = COMAPLevel1(overwrite=False, large_datasets=['spectrometer/tod'])
+    d.read_data_file(p)
+    part = slice_feeds(d, 2, 4)
+    del d
+    gc.collect()
+    assert np.array_equal(np.asarray(part['spectrometer/tod']), x[2:4])
+
+
+def test_write_back_to_source_keeps_lazy_datasets(tmp_path):
+    """write_data_file onto the file the object was read from: the lazy cube (and a
+    shard's rows of it) still read afterwards, and the new datasets are in the file."""
+    from comapreduce_amd.pipeline.sharding import slice_feeds
+    p = str(tmp_path / 'c.h5')
+    x = np.random.default_rng(4).standard_normal((3, 4, 2, 7)).astype(np.float32)
+    with H.H5File(p, 'w') as f:
+        f.write('spectrometer/tod', x)
+        f.write('spectrometer/feeds', np.arange(1, 4))
+    d = COMAPLevel1(overwrite=False, large_datasets=['spectrometer/tod'])
+    d.read_data_file(p)
+    part = slice_feeds(d, 1, 3)
+    d['extra/values'] = np.arange(5.0)
+    d.write_data_file(p)
+    assert np.array_equal(np.asarray(d['spectrometer/tod'][:]), x)
+    assert np.array_equal(np.asarray(part['spectrometer/tod']), x[1:3])
+    with H.H5File(p, 'r') as f:
+        assert np.array_equal(f.read('extra/values'), np.arange(5.0))
+        assert np.array_equal(f.read('spectrometer/tod'), x)     # large datasets are not rewritten
+
+
 def test_flat_reads_of_a_large_contiguous_dataset(tmp_path):
     """Ranges >= 8 MB of a contiguous dataset in a read-only file take the
     multi-threaded pread path (comap_h5_read_flat); the same ranges from a file
