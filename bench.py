@@ -262,48 +262,87 @@ def c4_map_info():
                          ['RA---CAR', 'DEC--CAR'], 480, 480)
 
 
+def _timed_solve(prob, threshold, niter):
+    import torch
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = prob.solve(threshold=threshold, niter=niter)
+    torch.cuda.synchronize()
+    return res, time.perf_counter() - t0
+
+
+def _timed_setup(*args, **kw):
+    """DeviceDestriper set-up on device-resident inputs (comap_destripe_create_bands:
+    spatial order, offset rows, pixel-major transpose, sample-level maps)."""
+    import torch
+    from comapreduce_amd.mapmaking import destriper as D
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    prob = D.DeviceDestriper(*args, **kw)
+    torch.cuda.synchronize()
+    return prob, time.perf_counter() - t0
+
+
+def operator_bytes(prob, NO, n_bands):
+    """HBM bytes one CG iteration of the batched operator must move: the
+    offset-major and pixel-major entries streamed once each (4 B index + 8 NB B
+    weights), 13 offset vectors of 8 NB B (bin gather source excluded as cache
+    resident, like SURVEY's map; project x / ws / y, update x r p q in + x r out,
+    direction p r in + p out)."""
+    nb = 4 if n_bands == 3 else n_bands
+    nnz, nnzp = prob.nnz()
+    return (nnz + nnzp) * (4 + 8 * nb) + 8 * (NO + 1) + 13 * NO * 8 * nb
+
+
+def _iters(res):
+    it = res['iters']
+    return max(it) if isinstance(it, (list, tuple)) else it
+
+
 def destriper_leg(level2, data, niter, device, want_cpu=False):
     """C4: COMAPData.read_comap_data (host prep + batched device w=400 median) on this
     observation's Level-2 output (band 0, 19 feeds, L = 50, 480x480 CAR), then the
-    device destriper's CG iterations / s (single rank, threshold 0: no early exit)."""
+    device destriper: set-up on device-resident inputs, the reference's own stopping
+    rule (threshold 1e-6, run_destriper.py:96-97, Destriper.py:134-141) timed to
+    convergence with the final maps, and CG iterations / s over a fixed niter with
+    early exit disabled (single rank)."""
     import torch
     from comapreduce_amd.mapmaking import comapdata as CD
-    from comapreduce_amd.mapmaking import destriper as D
+    dev = torch.device('cuda', device)
     store = level2_store(level2, data, obsid=int(data.obsid) if data.obsid > 0 else 1)
     t0 = time.perf_counter()
     tod, w, pix = CD.read_comap_data(list(store), c4_map_info(), iband=0, offset_length=50, store=store,
                                      device=device)[:3]
     prep = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    prob = D.DeviceDestriper(pix, tod, w, 50, 480 * 480, device=device)
-    torch.cuda.synchronize()
-    setup = time.perf_counter() - t0
+    td, wd, pd = (torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (tod, w, pix.astype(np.int32)))
+    _timed_setup(pd, td, wd, 50, 480 * 480, device=device)        # warm (module load, first allocations)
+    prob, setup = _timed_setup(pd, td, wd, 50, 480 * 480, device=device)
     prob.solve(threshold=0.0, niter=3)   # warm
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    res = prob.solve(threshold=0.0, niter=niter)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    conv, conv_s = _timed_solve(prob, 1e-6, 100)
+    res, dt = _timed_solve(prob, 0.0, niter)
     out = {'config': 'C4: read_comap_data (band 0, 19 feeds) -> destriper, L=50, 480x480 CAR, '
                      f'{niter} CG iterations (no early exit), single rank',
            'cg_iters_per_s': res['iters'] / dt, 'iters': res['iters'], 'n_samples': int(tod.size),
-           'n_offsets': int(tod.size // 50), 'prep_s': prep, 'setup_s': setup, 'nnz': prob.nnz()}
+           'n_offsets': int(tod.size // 50), 'prep_s': prep, 'setup_ms': setup * 1e3, 'nnz': prob.nnz(),
+           'converged': {'threshold': 1e-6, 'iters': conv['iters'], 'solve_ms': conv_s * 1e3,
+                         'setup_plus_solve_ms': (setup + conv_s) * 1e3}}
     # all 4 sidebands: one batched read (one device median call) and ONE batched solve
     t0 = time.perf_counter()
     r = CD.read_comap_data_bands(list(store), c4_map_info(), bands=(0, 1, 2, 3), offset_length=50, store=store,
                                  device=device)
     prep4 = time.perf_counter() - t0
-    prob4 = D.DeviceDestriper(r['pointing'], r['tod'], r['weights'], 50, 480 * 480, device=device, keep=r['keep'])
+    t4, w4, p4, k4 = (torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+                      for a in (r['tod'], r['weights'], r['pointing'].astype(np.int32), r['keep']))
+    prob4, setup4 = _timed_setup(p4, t4, w4, 50, 480 * 480, device=device, keep=k4)
     prob4.solve(threshold=0.0, niter=3)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    res4 = prob4.solve(threshold=0.0, niter=niter)
-    torch.cuda.synchronize()
-    dt4 = time.perf_counter() - t0
+    conv4, conv4_s = _timed_solve(prob4, 1e-6, 100)
+    res4, dt4 = _timed_solve(prob4, 0.0, niter)
     it4 = max(res4['iters'])
     out['bands4'] = {'config': 'C4, all 4 sidebands batched (read_comap_data_bands -> one batched solve)',
                      'band_iters_per_s': 4 * it4 / dt4, 'cg_iters_per_s': it4 / dt4, 'iters': res4['iters'],
-                     'n_samples_union': int(r['pointing'].size), 'prep_s': prep4}
+                     'n_samples_union': int(r['pointing'].size), 'prep_s': prep4, 'setup_ms': setup4 * 1e3,
+                     'converged': {'threshold': 1e-6, 'iters': conv4['iters'], 'solve_ms': conv4_s * 1e3,
+                                   'setup_plus_solve_ms': (setup4 + conv4_s) * 1e3}}
     if want_cpu:
         out['cpu_port'] = cpu_destriper_port(tod, w, pix, 50, 480 * 480)
     return out
@@ -323,20 +362,15 @@ def destriper_c5_leg(n_obs, niter, device, world, rank, n_bands=1):
     L, npix = 50, 480 * 480
     pix, tod, w = synthetic.destriper_inputs_device(n_obs, offset_length=L, device=device, seed=1000 + rank,
                                                     n_bands=n_bands)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    prob = D.DeviceDestriper(pix, tod, w, L, npix, device=device)
-    torch.cuda.synchronize()
-    setup = time.perf_counter() - t0
+    prob, setup = _timed_setup(pix, tod, w, L, npix, device=device)
     prob.solve(threshold=0.0, niter=3)   # warm (graph capture, RCCL communicators)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    res = prob.solve(threshold=0.0, niter=niter)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    conv, conv_s = _timed_solve(prob, 1e-6, 100)
+    if world > 1:
+        dist.barrier()
+    res, dt = _timed_solve(prob, 0.0, niter)
     if world > 1:
         e = torch.tensor([dt], device='cuda', dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -347,13 +381,21 @@ def destriper_c5_leg(n_obs, niter, device, world, rank, n_bands=1):
     algo = DESTRIPER_BYTES_PER_SAMPLE * N + DESTRIPER_BYTES_PER_OFFSET * NO     # per band-iteration
     ms = dt / it * 1e3
     ms_band = ms / n_bands
+    op_bytes = operator_bytes(prob, NO, n_bands)
     return {'config': f'C5: {n_obs} obs x 19 feeds x 180000 samples per GPU, {n_bands} band(s) per solve, L={L}, '
                       f'480x480 CAR, {niter} CG iterations (no early exit), {world} rank(s)',
             'cg_iters_per_s': it / dt, 'band_iters_per_s': n_bands * it / dt, 'ms_per_iter': ms,
             'ms_per_band_iter': ms_band, 'iters': res['iters'],
-            'n_samples_per_gpu': N, 'n_offsets_per_gpu': NO, 'nnz': prob.nnz(), 'setup_s': setup,
+            'n_samples_per_gpu': N, 'n_offsets_per_gpu': NO, 'nnz': prob.nnz(), 'setup_ms': setup * 1e3,
+            'converged': {'threshold': 1e-6, 'iters': conv['iters'], 'solve_ms': conv_s * 1e3,
+                          'setup_plus_solve_ms': (setup + conv_s) * 1e3},
             'algo_bytes_per_band_iter_per_gpu': algo, 'achieved_GBs_per_gpu': algo / (ms_band * 1e-3) / 1e9,
-            'roofline_frac': algo / (ms_band * 1e-3) / 1e9 / HBM_PEAK_GBS}
+            'roofline_frac_survey_equiv': algo / (ms_band * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            'roofline_frac_survey_equiv_note': 'SURVEY §8(d) per-band bytes (24 B/sample + 80 B/offset) x bands: '
+                                               'the batched operator shares the pixel stream between bands and '
+                                               'folds samples into entries, so it never moves these bytes',
+            'operator_bytes_per_iter': op_bytes,
+            'operator_roofline_frac': op_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
 def e2e_leg(F, T, device):

@@ -237,16 +237,6 @@ __device__ __forceinline__ void zero_tail(double *__restrict__ part, int64_t str
         for (int b = 0; b < NB; ++b) part[(int64_t)b * stride + t] = 0.0;
 }
 
-// Block partial (4 waves) of a per-thread accumulator; thread 0 writes *out.
-__device__ __forceinline__ void block_partial(double acc, double *red, double *out)
-{
-    acc = wave_sum(acc);
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
-    __syncthreads();
-    if (threadIdx.x == 0) *out = (red[0] + red[1]) + (red[2] + red[3]);
-}
-
 // block_partial of NB accumulators with one pair of barriers; band b's partial goes to
 // part[b kPartMax] (same value as block_partial per band).  red: 4 NB doubles.
 template <int NB>
@@ -267,105 +257,7 @@ __device__ __forceinline__ void block_partials(double (&acc)[NB], double *red, d
     }
 }
 
-// One wave per offset: lane l owns samples l, l + 64, ... (K per lane, L <= 64 K).
-// Unique pixels in first-occurrence order, weights summed per band in sample order;
-// an entry is kept when any band's sum is non-zero.  pass 0 counts (and sums
-// ws = sum w, tw = sum w tod per band), pass 1 fills.  w, tod: [NB][N] band-major.
-template <int K, int NB>
-__global__ void __launch_bounds__(256) k_ds_entries(const int32_t *__restrict__ pix, const double *__restrict__ w,
-                                                    const double *__restrict__ tod, int64_t N, int64_t NO, int L,
-                                                    int pass, int64_t *__restrict__ cnt,
-                                                    const int64_t *__restrict__ orow, int32_t *__restrict__ opix,
-                                                    double *__restrict__ ow, double *__restrict__ ws,
-                                                    double *__restrict__ tw)
-{
-    const int lane = threadIdx.x & 63;
-    const int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (o >= NO) return;
-    int32_t p[K];
-    double wi[K][NB], gsum[K][NB];
-    bool first[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const int sidx = lane + 64 * k;
-        const bool in = sidx < L;
-        p[k] = in ? pix[o * L + sidx] : -2;
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            wi[k][b] = in ? w[(int64_t)b * N + o * L + sidx] : 0.0;
-            gsum[k][b] = 0.0;
-        }
-        first[k] = in;
-    }
-    // every sample in order (chunk kk, lane j): first occurrence and the in-order group sums
-#pragma unroll
-    for (int kk = 0; kk < K; ++kk)
-        for (int j = 0; j < 64; ++j) {
-            const int32_t pj = __shfl(p[kk], j, 64);
-            double wj[NB];
-#pragma unroll
-            for (int b = 0; b < NB; ++b) wj[b] = __shfl(wi[kk][b], j, 64);
-#pragma unroll
-            for (int k = 0; k < K; ++k)
-                if (pj == p[k]) {
-                    if (j + 64 * kk < lane + 64 * k) first[k] = false;
-#pragma unroll
-                    for (int b = 0; b < NB; ++b) gsum[k][b] += wj[b];
-                }
-        }
-    unsigned long long m[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        bool any = false;
-#pragma unroll
-        for (int b = 0; b < NB; ++b) any |= gsum[k][b] != 0.0;
-        m[k] = __ballot(first[k] && any);
-    }
-    if (pass == 0) {
-        int64_t c = 0;
-#pragma unroll
-        for (int k = 0; k < K; ++k) c += __popcll(m[k]);
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            double sw = 0.0, st = 0.0;
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                sw += wi[k][b];
-                if (lane + 64 * k < L) st += wi[k][b] * tod[(int64_t)b * N + o * L + lane + 64 * k];
-            }
-            sw = wave_sum(sw);
-            st = wave_sum(st);
-            if (lane == 0) { ws[o * NB + b] = sw; tw[o * NB + b] = st; }
-        }
-        if (lane == 0) cnt[o] = c;
-        return;
-    }
-    int base = 0;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        if ((m[k] >> lane) & 1ull) {
-            const int64_t e = orow[o] + base + __popcll(m[k] & ((1ull << lane) - 1ull));
-            opix[e] = p[k];
-#pragma unroll
-            for (int b = 0; b < NB; ++b) ow[e * NB + b] = gsum[k][b];
-        }
-        base += __popcll(m[k]);
-    }
-}
-
-template <int NB>
-void launch_entries(int L, unsigned blocks, hipStream_t st, const int32_t *pix, const double *w, const double *tod,
-                    int64_t N, int64_t NO, int pass, int64_t *cnt, const int64_t *orow, int32_t *opix, double *ow,
-                    double *ws, double *tw)
-{
-    if (L <= 64)
-        k_ds_entries<1, NB><<<blocks, 256, 0, st>>>(pix, w, tod, N, NO, L, pass, cnt, orow, opix, ow, ws, tw);
-    else if (L <= 128)
-        k_ds_entries<2, NB><<<blocks, 256, 0, st>>>(pix, w, tod, N, NO, L, pass, cnt, orow, opix, ow, ws, tw);
-    else
-        k_ds_entries<4, NB><<<blocks, 256, 0, st>>>(pix, w, tod, N, NO, L, pass, cnt, orow, opix, ow, ws, tw);
-}
-
+// ---------------------------------------------------------------- set-up (comap_destripe_create_bands)
 // Processing order of the offsets.  In time order the offsets in flight at once
 // cover the whole scan pattern, so the projection's map gathers (npix x 8 NB bytes,
 // 7.4 MB for 4 bands at 480^2) miss the 4 MB XCD L2s.  Sorting offsets by the pixel
@@ -373,50 +265,177 @@ void launch_entries(int L, unsigned blocks, hipStream_t st, const int32_t *pix, 
 // of map rows, and puts offsets that cross the same pixels next to each other in the
 // CG vectors (the bin's x gathers).  Key: that pixel (npix when the offset is all
 // off-map); a stable sort keeps time order among equal keys.
-__global__ void k_offset_keys(const int64_t *__restrict__ orow, const int32_t *__restrict__ opix, int64_t NO,
-                              int64_t npix, int32_t *__restrict__ key, int32_t *__restrict__ val)
+__global__ void k_offset_keys(const int32_t *__restrict__ pix, int64_t NO, int L, int64_t npix,
+                              int32_t *__restrict__ key, int32_t *__restrict__ val)
 {
     for (int64_t o = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; o < NO; o += (int64_t)gridDim.x * blockDim.x) {
         int32_t k = (int32_t)npix;
-        for (int64_t e = orow[o]; e < orow[o + 1]; ++e)
-            if (opix[e] >= 0) { k = opix[e]; break; }
+        for (int j = 0; j < L; ++j) {
+            const int32_t p = pix[o * L + j];
+            if (p >= 0) { k = p; break; }
+        }
         key[o] = k;
         val[o] = (int32_t)o;
     }
 }
 
-__global__ void k_perm_counts(const int64_t *__restrict__ orow, const int32_t *__restrict__ perm, int64_t NO,
-                              int64_t *__restrict__ cnt)
+// Offset rows of the sparse operator, one wave per row k (offset o = perm[k]): lane l
+// holds samples l, l + 64, ... (K per lane, L <= 64 K).  The distinct pixels of the
+// offset are found in first-occurrence order by a leader loop (the first pending
+// sample leads, one ballot per chunk collects every sample with its pixel), so the
+// work is one short scalar loop per distinct pixel instead of an L x L compare.  The
+// group's head lane then sums its samples' weights per band in sample order (the
+// reference's binValues order within the offset; the offset's rows are L1-resident
+// after the coalesced loads).  An entry is kept when any band's sum is non-zero.
+//   FILL = false: cnt[k] (kept entries), ws / tw (sum w, sum w tod per band: lane
+//                 order, then a fixed butterfly), and per sample the sort key of the
+//                 sample-level maps (pixel, npix when not binned), its index, and the
+//                 packed payload {w_b, tod_b w_b} [N][2 NB] (the product rounded, as
+//                 binValues(weights = tod * w) rounds it).
+//   FILL = true:  the row's entries at orow[k]: pixel (-1 = off-map), weights, and the
+//                 pixel-major transpose's key / entry id / row.
+// w, tod: band-major [NB][N].
+template <int K, int NB, bool FILL>
+__global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix, const double *__restrict__ w,
+                                                 const double *__restrict__ tod, int64_t N, int64_t NO, int L,
+                                                 int64_t npix, const int32_t *__restrict__ perm,
+                                                 int64_t *__restrict__ cnt, double *__restrict__ ws,
+                                                 double *__restrict__ tw, double *__restrict__ payload,
+                                                 int32_t *__restrict__ skey, int32_t *__restrict__ sval,
+                                                 const int64_t *__restrict__ orow, int32_t *__restrict__ opix,
+                                                 double *__restrict__ ow, int32_t *__restrict__ ekey,
+                                                 int32_t *__restrict__ eval, int32_t *__restrict__ eoff)
 {
-    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < NO; k += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t o = perm[k];
-        cnt[k] = orow[o + 1] - orow[o];
-    }
-}
-
-// new offset k = old offset perm[k]: one wave copies its entry row
-template <int NB>
-__global__ void __launch_bounds__(256) k_perm_entries(const int64_t *__restrict__ orow, const int32_t *__restrict__ opix,
-                                                      const double *__restrict__ ow, const double *__restrict__ ws,
-                                                      const double *__restrict__ tw, const int32_t *__restrict__ perm,
-                                                      int64_t NO, const int64_t *__restrict__ orow2,
-                                                      int32_t *__restrict__ opix2, double *__restrict__ ow2,
-                                                      double *__restrict__ ws2, double *__restrict__ tw2)
-{
+#pragma clang fp contract(off)
     const int lane = threadIdx.x & 63;
     const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (k >= NO) return;
-    const int64_t o = perm[k];
-    const int64_t e0 = orow[o], n = orow[o + 1] - e0, f0 = orow2[k];
-    for (int64_t j = lane; j < n; j += 64) {
-        opix2[f0 + j] = opix[e0 + j];
+    const int64_t o = perm ? (int64_t)perm[k] : k;
+    const int64_t base = o * L;
+    constexpr int32_t kNone = INT32_MIN;    // lanes past the offset's end (real pixels are >= -1)
+    int32_t q[K];
+    unsigned long long rem[K];
 #pragma unroll
-        for (int b = 0; b < NB; ++b) ow2[(f0 + j) * NB + b] = ow[(e0 + j) * NB + b];
+    for (int m = 0; m < K; ++m) {
+        const int j = lane + 64 * m;
+        q[m] = j < L ? pix[base + j] : kNone;
+        rem[m] = __ballot(j < L);
     }
-    if (lane < NB) {
-        ws2[k * NB + lane] = ws[o * NB + lane];
-        tw2[k * NB + lane] = tw[o * NB + lane];
+    // leader loop: head lanes and their members (per chunk of the leader)
+    bool head[K];
+    unsigned long long mem[K][K];
+#pragma unroll
+    for (int m = 0; m < K; ++m) {
+        head[m] = false;
+#pragma unroll
+        for (int c = 0; c < K; ++c) mem[m][c] = 0ull;
     }
+#pragma unroll
+    for (int m = 0; m < K; ++m) {
+        while (rem[m]) {
+            const int ld = __ffsll((long long)rem[m]) - 1;
+            const int32_t pl = __shfl(q[m], ld, 64);
+            unsigned long long mm[K];
+#pragma unroll
+            for (int c = 0; c < K; ++c) {
+                mm[c] = c < m ? 0ull : __ballot(q[c] == pl);
+                rem[c] &= ~mm[c];
+            }
+            if (lane == ld) {
+                head[m] = true;
+#pragma unroll
+                for (int c = 0; c < K; ++c) mem[m][c] = mm[c];
+            }
+        }
+    }
+    // per head: the group's in-order weight sums per band
+    double gs[K][NB];
+    bool keepe[K];
+#pragma unroll
+    for (int m = 0; m < K; ++m) {
+        bool any = false;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            double s = 0.0;
+            if (head[m]) {
+#pragma unroll
+                for (int c = 0; c < K; ++c)
+                    for (unsigned long long bits = mem[m][c]; bits; bits &= bits - 1)
+                        s += w[(int64_t)b * N + base + 64 * c + (__ffsll((long long)bits) - 1)];
+            }
+            gs[m][b] = s;
+            any |= s != 0.0;
+        }
+        keepe[m] = head[m] && any;
+    }
+    if constexpr (!FILL) {
+        int64_t c0 = 0;
+#pragma unroll
+        for (int m = 0; m < K; ++m) c0 += __popcll(__ballot(keepe[m]));
+        double wi[K][NB], ti[K][NB];
+#pragma unroll
+        for (int m = 0; m < K; ++m) {
+            const int j = lane + 64 * m;
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                wi[m][b] = j < L ? w[(int64_t)b * N + base + j] : 0.0;
+                ti[m][b] = j < L ? tod[(int64_t)b * N + base + j] : 0.0;
+            }
+            if (j < L) {
+                const int64_t i = base + j;
+                double pl[2 * NB];
+#pragma unroll
+                for (int b = 0; b < NB; ++b) { pl[b] = wi[m][b]; pl[NB + b] = ti[m][b] * wi[m][b]; }
+                stb<2 * NB>(payload + i * 2 * NB, pl);
+                skey[i] = (q[m] >= 0 && q[m] < npix) ? q[m] : (int32_t)npix;
+                sval[i] = (int32_t)i;
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            double sw = 0.0, st = 0.0;
+#pragma unroll
+            for (int m = 0; m < K; ++m) {
+                sw += wi[m][b];
+                if (lane + 64 * m < L) st = fma(wi[m][b], ti[m][b], st);   // fused, as before the rewrite
+            }
+            sw = wave_sum(sw);
+            st = wave_sum(st);
+            if (lane == 0) { ws[k * NB + b] = sw; tw[k * NB + b] = st; }
+        }
+        if (lane == 0) cnt[k] = c0;
+    } else {
+        int64_t e = orow[k];
+#pragma unroll
+        for (int m = 0; m < K; ++m) {
+            const unsigned long long bm = __ballot(keepe[m]);
+            if (keepe[m]) {
+                const int64_t ei = e + __popcll(bm & ((1ull << lane) - 1ull));
+                opix[ei] = q[m];
+#pragma unroll
+                for (int b = 0; b < NB; ++b) ow[ei * NB + b] = gs[m][b];
+                ekey[ei] = (q[m] >= 0 && q[m] < npix) ? q[m] : (int32_t)npix;
+                eval[ei] = (int32_t)ei;
+                eoff[ei] = (int32_t)k;
+            }
+            e += __popcll(bm);
+        }
+    }
+}
+
+template <int NB, bool FILL>
+void launch_rows(int L, hipStream_t st, const int32_t *pix, const double *w, const double *tod, int64_t N,
+                 int64_t NO, int64_t npix, const int32_t *perm, int64_t *cnt, double *ws, double *tw, double *payload,
+                 int32_t *skey, int32_t *sval, const int64_t *orow, int32_t *opix, double *ow, int32_t *ekey,
+                 int32_t *eval, int32_t *eoff)
+{
+    const unsigned blocks = (unsigned)((NO + 3) / 4);
+#define COMAP_ROWS(K) k_ds_rows<K, NB, FILL><<<blocks, 256, 0, st>>>(pix, w, tod, N, NO, L, npix, perm, cnt, ws, tw, \
+                                                                      payload, skey, sval, orow, opix, ow, ekey, eval, eoff)
+    if (L <= 64) COMAP_ROWS(1);
+    else if (L <= 128) COMAP_ROWS(2);
+    else COMAP_ROWS(4);
+#undef COMAP_ROWS
 }
 
 // x_out[perm[k]] = x[k] per band (internal offset order -> the caller's)
@@ -431,21 +450,6 @@ __global__ void k_unpermute(const double *__restrict__ x, const int32_t *__restr
     }
 }
 
-// keys for the pixel-major transpose: pixel of each offset-major entry (npix for off-map)
-__global__ void k_entry_keys(const int64_t *__restrict__ orow, int64_t NO, const int32_t *__restrict__ opix,
-                             int64_t npix, int32_t *__restrict__ key, int32_t *__restrict__ val,
-                             int32_t *__restrict__ eoff)
-{
-    for (int64_t o = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; o < NO; o += (int64_t)gridDim.x * blockDim.x) {
-        for (int64_t e = orow[o]; e < orow[o + 1]; ++e) {
-            const int32_t p = opix[e];
-            key[e] = (p >= 0 && p < npix) ? p : (int32_t)npix;
-            val[e] = (int32_t)e;
-            eoff[e] = (int32_t)o;
-        }
-    }
-}
-
 __device__ __forceinline__ int64_t lb32(const int32_t *a, int64_t n, int64_t v)
 {
     int64_t lo = 0, hi = n;
@@ -456,61 +460,100 @@ __device__ __forceinline__ int64_t lb32(const int32_t *a, int64_t n, int64_t v)
     return lo;
 }
 
+// row[p] = first sorted position with key >= p, p in [0, npix]
 __global__ void k_rowptr(const int32_t *__restrict__ skey, int64_t n, int64_t npix, int64_t *__restrict__ row)
 {
     for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p <= npix; p += (int64_t)gridDim.x * blockDim.x)
         row[p] = lb32(skey, n, p);
 }
 
+// pixel-major entries: sorted position k < nnzp (= prow[npix], read on the device) takes
+// offset-major entry sval[k] (entries of one pixel come from spatially adjacent rows)
 template <int NB>
-__global__ void k_pixel_entries(const int32_t *__restrict__ sval, int64_t nnzp, const int32_t *__restrict__ eoff,
-                                const double *__restrict__ ow, int32_t *__restrict__ poff, double *__restrict__ pw)
+__global__ void k_pixel_entries(const int32_t *__restrict__ sval, const int64_t *__restrict__ nnzp_dev,
+                                const int32_t *__restrict__ eoff, const double *__restrict__ ow,
+                                int32_t *__restrict__ poff, double *__restrict__ pw)
 {
+    const int64_t nnzp = *nnzp_dev;
     for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < nnzp; k += (int64_t)gridDim.x * blockDim.x) {
         const int32_t e = sval[k];
         poff[k] = eoff[e];
-#pragma unroll
-        for (int b = 0; b < NB; ++b) pw[k * NB + b] = ow[(int64_t)e * NB + b];
+        double v[NB];
+        ldb<NB>(ow + (int64_t)e * NB, v);
+        stb<NB>(pw + k * NB, v);
     }
 }
 
-// sample-level maps in binValues order (stable pixel sort keeps sample order)
-__global__ void k_sample_keys(const int32_t *__restrict__ pix, int64_t N, int64_t npix, int32_t *__restrict__ key,
-                              int32_t *__restrict__ val)
+// Non-empty pixel rows for the CG bin: flag, exclusive scan, then the compact list with
+// each row's entry range (hprow[i] = prow[hrow[i]], hprow[nh] = nnzp) and nh itself.
+__global__ void k_hit_flags(const int64_t *__restrict__ prow, int64_t npix, int32_t *__restrict__ flag)
 {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t p = pix[i];
-        key[i] = (p >= 0 && p < npix) ? p : (int32_t)npix;
-        val[i] = (int32_t)i;
-    }
+    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x)
+        flag[p] = prow[p + 1] > prow[p] ? 1 : 0;
 }
 
-// h = sum w, hits = sum 1, nnum = sum tod w per pixel and band, over the samples
-// of the offsets the band keeps (keep [NB][NO], NULL = all)
-template <int NB>
-__global__ void k_sample_maps(const int32_t *__restrict__ skey, const int32_t *__restrict__ sval, int64_t N,
-                              int64_t npix, int L, const double *__restrict__ w, const double *__restrict__ tod,
-                              const uint8_t *__restrict__ keep, double *__restrict__ h, double *__restrict__ hits,
-                              double *__restrict__ nnum)
+__global__ void k_hit_rows(const int64_t *__restrict__ prow, const int32_t *__restrict__ flag,
+                           const int32_t *__restrict__ pos, int64_t npix, int32_t *__restrict__ hrow,
+                           int64_t *__restrict__ hprow, int64_t *__restrict__ counts)
 {
-#pragma clang fp contract(off)   // binValues(weights=z*w): the product is rounded before the add
-    const int64_t NO = N / L;
     for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t lo = lb32(skey, N, p), hi = lb32(skey, N, p + 1);
+        if (flag[p]) { hrow[pos[p]] = (int32_t)p; hprow[pos[p]] = prow[p]; }
+        if (p == npix - 1) {
+            const int64_t nh = (int64_t)pos[p] + flag[p];
+            hprow[nh] = prow[npix];
+            counts[0] = prow[npix];   // nnzp
+            counts[1] = nh;
+        }
+    }
+}
+
+// Sample-level maps in binValues order: h = sum w, hits = sum 1, nnum = sum tod w per
+// pixel and band, over the samples of the offsets the band keeps (keep [NB][NO], NULL =
+// all), each pixel's samples added one after the other in sample order (the stable
+// pixel sort keeps it) -- the reference's sequential loop, bit for bit.  One thread per
+// pixel walks its run of the sorted sample ids, with kSU packed payloads (64 B for 4
+// bands: one cache line per sample, not 2 NB) in flight before the ordered adds.
+constexpr int kSU = 8;
+template <int NB>
+__global__ void __launch_bounds__(256) k_sample_walk(const int64_t *__restrict__ srow, const int32_t *__restrict__ sval,
+                                                     const double *__restrict__ payload, int64_t npix, int L, int64_t NO,
+                                                     const uint8_t *__restrict__ keep, double *__restrict__ h,
+                                                     double *__restrict__ hits, double *__restrict__ nnum)
+{
+    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t lo = srow[p], hi = srow[p + 1];
         double sh[NB], sc[NB], sn[NB];
 #pragma unroll
         for (int b = 0; b < NB; ++b) sh[b] = sc[b] = sn[b] = 0.0;
-        for (int64_t k = lo; k < hi; ++k) {
-            const int32_t i = sval[k];
-            const int64_t o = i / L;
+        for (int64_t k = lo; k < hi; k += kSU) {
+            int32_t i[kSU];
 #pragma unroll
-            for (int b = 0; b < NB; ++b) {
-                if (keep && !keep[(int64_t)b * NO + o]) continue;
-                const double wi = w[(int64_t)b * N + i];
-                sh[b] += wi;
-                sn[b] += tod[(int64_t)b * N + i] * wi;
-                sc[b] += 1.0;
+            for (int u = 0; u < kSU; ++u) i[u] = k + u < hi ? sval[k + u] : -1;
+            double pl[kSU][2 * NB];
+            bool in[kSU][NB];
+#pragma unroll
+            for (int u = 0; u < kSU; ++u) {
+                if (i[u] >= 0) {
+                    ldb<2 * NB>(payload + (int64_t)i[u] * 2 * NB, pl[u]);
+                    const int64_t o = i[u] / L;
+#pragma unroll
+                    for (int b = 0; b < NB; ++b) in[u][b] = !keep || keep[(int64_t)b * NO + o];
+                } else {
+#pragma unroll
+                    for (int b = 0; b < 2 * NB; ++b) pl[u][b] = 0.0;
+#pragma unroll
+                    for (int b = 0; b < NB; ++b) in[u][b] = false;
+                }
             }
+#pragma unroll
+            for (int u = 0; u < kSU; ++u)
+#pragma unroll
+                for (int b = 0; b < NB; ++b)
+                    if (in[u][b]) {
+                        sh[b] += pl[u][b];
+                        sn[b] += pl[u][NB + b];
+                        sc[b] += 1.0;
+                    }
         }
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
@@ -1058,8 +1101,34 @@ struct ProblemOwner {
     }
 };
 
+// One device allocation carved into the set-up's scratch arrays (256-B aligned), so the
+// set-up makes one hipMalloc / hipFree pair for its temporaries instead of one per array.
+struct Arena {
+    char *base = nullptr;
+    size_t used = 0, cap = 0;
+    template <typename T>
+    T *take(size_t n)
+    {
+        const size_t b = (sizeof(T) * (n ? n : 1) + 255) & ~(size_t)255;
+        T *p = reinterpret_cast<T *>(base + used);
+        used += b;
+        return p;
+    }
+    template <typename T>
+    static size_t bytes(size_t n) { return (sizeof(T) * (n ? n : 1) + 255) & ~(size_t)255; }
+};
+
 }  // namespace
 
+// Set-up of the constant operator (pointing and weights do not change during CG):
+//   1. spatial offset order: first on-map pixel per offset, stable radix sort -> perm
+//   2. k_ds_rows count pass: kept entries per row, ws / tw, the sample sort keys and
+//      the packed sample payload; scan -> orow; nnz back to the host (sync 1)
+//   3. k_ds_rows fill pass: the offset-major entries + the transpose's keys
+//   4. pixel-major transpose: stable radix sort of the entries by pixel, row pointers,
+//      gathered entry weights, the non-empty row list
+//   5. sample-level maps: stable radix sort of the samples by pixel, ordered walk
+//   nnzp and the non-empty row count back to the host (sync 2).
 extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, const double *tod, const double *w,
                                            const uint8_t *keep, int64_t N, int32_t L, int64_t npix, int32_t nb,
                                            comap_destriper **out)
@@ -1074,136 +1143,119 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     hipStream_t st = ctx->stream;
     auto *d = new comap_destriper();
     d->ctx = ctx; d->N = N; d->L = L; d->NO = N / L; d->npix = npix; d->nb = nb;
+    const int64_t NO = d->NO;
     const size_t NB = (size_t)nb;
     ProblemOwner own{d};   // frees d on every early return; released at the end
-    DevTemps tmp;          // this call's scratch, freed on every return
     int rc = 0;
-    rc |= dalloc(ctx, &d->orow, d->NO + 1);
-    rc |= dalloc(ctx, &d->ws, d->NO * NB);
-    rc |= dalloc(ctx, &d->tw, d->NO * NB);
+    rc |= dalloc(ctx, &d->orow, NO + 1);
+    rc |= dalloc(ctx, &d->ws, NO * NB);
+    rc |= dalloc(ctx, &d->tw, NO * NB);
     rc |= dalloc(ctx, &d->prow, npix + 1);
     rc |= dalloc(ctx, &d->h, npix * NB);
     rc |= dalloc(ctx, &d->hits, npix * NB);
     rc |= dalloc(ctx, &d->nnum, npix * NB);
     rc |= dalloc(ctx, &d->part, 2 * NB * (size_t)kPartMax);   // [0, NB kPartMax): p.q / dots, then r.r of the fused CG
     rc |= dalloc(ctx, &d->scal, 4 * NB + 4);
+    rc |= dalloc(ctx, &d->hrow, npix);
+    rc |= dalloc(ctx, &d->hprow, npix + 1);
+    const char *ord = getenv("COMAP_DS_ORDER");          // 0: keep the offsets in time order
+    const bool spatial = !(ord && ord[0] == '0');
+    if (spatial) rc |= dalloc(ctx, &d->perm, NO);
     if (rc) return -2;
-    // ---- offset-major entries
-    int64_t *cnt = nullptr;
-    COMAP_CHECK(ctx, tmp.alloc(&cnt, d->NO + 1));
-    const unsigned gblocks = (unsigned)((d->NO + 3) / 4);
-    COMAP_NB_SWITCH(nb, launch_entries<NB>(L, gblocks, st, pix, w, tod, N, d->NO, 0, cnt, nullptr, nullptr, nullptr,
-                                           d->ws, d->tw));
+    int end_bit = 1;
+    while ((1ll << end_bit) <= npix) ++end_bit;
+    // ---- scratch: sizes first (hipcub temp storage for the largest sort / scan), one allocation
+    size_t sort_tb = 0, scan_tb = 0, scan32_tb = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tb, (int32_t *)nullptr, (int32_t *)nullptr,
+                                             (int32_t *)nullptr, (int32_t *)nullptr, (int)N, 0, end_bit, st);
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tb, (int64_t *)nullptr, (int64_t *)nullptr, (int)(NO + 1), st);
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan32_tb, (int32_t *)nullptr, (int32_t *)nullptr, (int)npix, st);
+    const size_t cub_tb = std::max({sort_tb, scan_tb, scan32_tb});
+    Arena ar;
+    ar.cap = Arena::bytes<char>(cub_tb) + Arena::bytes<int64_t>(NO + 1) + 8 * Arena::bytes<int32_t>(N) +
+             Arena::bytes<double>((size_t)N * 2 * NB) + Arena::bytes<int64_t>(npix + 1) +
+             2 * Arena::bytes<int32_t>(npix) + Arena::bytes<int64_t>(2) + Arena::bytes<int32_t>(N);
+    COMAP_CHECK(ctx, hipMalloc((void **)&ar.base, ar.cap));
+    struct ArenaFree {
+        Arena *a;
+        hipStream_t s;
+        ~ArenaFree()
+        {
+            (void)hipStreamSynchronize(s);
+            (void)hipFree(a->base);
+        }
+    } arena_free{&ar, st};
+    char *cub_tmp = ar.take<char>(cub_tb);
+    int64_t *cnt = ar.take<int64_t>(NO + 1);
+    int32_t *skey = ar.take<int32_t>(N), *sval = ar.take<int32_t>(N);      // samples by pixel (sort in)
+    int32_t *skey2 = ar.take<int32_t>(N), *sval2 = ar.take<int32_t>(N);    // (sort out)
+    int32_t *ekey = ar.take<int32_t>(N), *eval = ar.take<int32_t>(N);      // entries by pixel (nnz <= N)
+    int32_t *ekey2 = ar.take<int32_t>(N), *eval2 = ar.take<int32_t>(N);
+    int32_t *eoff = ar.take<int32_t>(N);
+    double *payload = ar.take<double>((size_t)N * 2 * NB);
+    int64_t *srow = ar.take<int64_t>(npix + 1);
+    int32_t *hflag = ar.take<int32_t>(npix), *hpos = ar.take<int32_t>(npix);
+    int64_t *counts = ar.take<int64_t>(2);
+    // ---- 1. spatial processing order of the offsets
+    if (spatial) {
+        k_offset_keys<<<grid_for(NO), 256, 0, st>>>(pix, NO, L, npix, ekey, eval);
+        COMAP_LAUNCH_CHECK(ctx);
+        COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(cub_tmp, sort_tb, ekey, ekey2, eval, d->perm, (int)NO, 0,
+                                                            end_bit, st));
+    }
+    // ---- 2. count pass
+    COMAP_NB_SWITCH(nb, (launch_rows<NB, false>(L, st, pix, w, tod, N, NO, npix, d->perm, cnt, d->ws, d->tw, payload,
+                                                skey, sval, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr)));
     COMAP_LAUNCH_CHECK(ctx);
-    size_t scan_tb = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tb, cnt, d->orow, (int)(d->NO + 1), st);
-    char *scan_tmp = nullptr;
-    COMAP_CHECK(ctx, tmp.alloc(&scan_tmp, scan_tb));
-    COMAP_CHECK(ctx, hipMemsetAsync(cnt + d->NO, 0, 8, st));
-    COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_tb, cnt, d->orow, (int)(d->NO + 1), st));
-    COMAP_CHECK(ctx, hipMemcpyAsync(&d->nnz, d->orow + d->NO, 8, hipMemcpyDeviceToHost, st));
+    COMAP_CHECK(ctx, hipMemsetAsync(cnt + NO, 0, 8, st));
+    COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(cub_tmp, scan_tb, cnt, d->orow, (int)(NO + 1), st));
+    COMAP_CHECK(ctx, hipMemcpyAsync(&d->nnz, d->orow + NO, 8, hipMemcpyDeviceToHost, st));
     COMAP_CHECK(ctx, hipStreamSynchronize(st));
     rc |= dalloc(ctx, &d->opix, d->nnz);
     rc |= dalloc(ctx, &d->ow, d->nnz * NB);
+    rc |= dalloc(ctx, &d->poff, d->nnz);          // nnzp <= nnz (off-map entries are not binned)
+    rc |= dalloc(ctx, &d->pw, d->nnz * NB);
     if (rc) return -2;
-    COMAP_NB_SWITCH(nb, launch_entries<NB>(L, gblocks, st, pix, w, tod, N, d->NO, 1, nullptr, d->orow, d->opix, d->ow,
-                                           nullptr, nullptr));
+    // ---- 3. fill pass
+    COMAP_NB_SWITCH(nb, (launch_rows<NB, true>(L, st, pix, w, tod, N, NO, npix, d->perm, nullptr, nullptr, nullptr,
+                                               nullptr, nullptr, nullptr, d->orow, d->opix, d->ow, ekey, eval, eoff)));
     COMAP_LAUNCH_CHECK(ctx);
-    const int64_t sortn = std::max<int64_t>(d->nnz, N);
-    int32_t *k0 = nullptr, *k1 = nullptr, *v0 = nullptr, *v1 = nullptr, *eoff = nullptr;
-    COMAP_CHECK(ctx, tmp.alloc(&k0, sortn));
-    COMAP_CHECK(ctx, tmp.alloc(&k1, sortn));
-    COMAP_CHECK(ctx, tmp.alloc(&v0, sortn));
-    COMAP_CHECK(ctx, tmp.alloc(&v1, sortn));
-    COMAP_CHECK(ctx, tmp.alloc(&eoff, d->nnz));
-    int end_bit = 1;
-    while ((1ll << (end_bit)) <= npix) ++end_bit;
-    size_t tb = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k0, k1, v0, v1, (int)sortn, 0, end_bit, st);
-    char *sort_tmp = nullptr;
-    COMAP_CHECK(ctx, tmp.alloc(&sort_tmp, tb));
-    // ---- spatial processing order of the offsets (COMAP_DS_ORDER=0 keeps time order)
-    const char *ord = getenv("COMAP_DS_ORDER");
-    if (!(ord && ord[0] == '0')) {
-        k_offset_keys<<<grid_for(d->NO), 256, 0, st>>>(d->orow, d->opix, d->NO, npix, k0, v0);
-        COMAP_LAUNCH_CHECK(ctx);
-        if (dalloc(ctx, &d->perm, d->NO)) return -2;
-        COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(sort_tmp, tb, k0, k1, v0, d->perm, (int)d->NO, 0, end_bit,
-                                                            st));
-        int64_t *orow2 = nullptr, *cnt2 = nullptr;
-        int32_t *opix2 = nullptr;
-        double *ow2 = nullptr, *ws2 = nullptr, *tw2 = nullptr;
-        if (dalloc(ctx, &orow2, d->NO + 1) || dalloc(ctx, &opix2, d->nnz) || dalloc(ctx, &ow2, d->nnz * NB) ||
-            dalloc(ctx, &ws2, d->NO * NB) || dalloc(ctx, &tw2, d->NO * NB)) {
-            for (void *q : {(void *)orow2, (void *)opix2, (void *)ow2, (void *)ws2, (void *)tw2})
-                if (q) (void)hipFree(q);
-            return -2;
-        }
-        // the new arrays replace the old ones now (comap_destripe_destroy frees whatever d holds)
-        std::swap(d->orow, orow2);
-        std::swap(d->opix, opix2);
-        std::swap(d->ow, ow2);
-        std::swap(d->ws, ws2);
-        std::swap(d->tw, tw2);
-        DevTemps old(st);   // the time-ordered arrays, freed once the copies below have run
-        old.p = {(void *)orow2, (void *)opix2, (void *)ow2, (void *)ws2, (void *)tw2};
-        COMAP_CHECK(ctx, tmp.alloc(&cnt2, d->NO + 1));
-        k_perm_counts<<<grid_for(d->NO), 256, 0, st>>>(orow2, d->perm, d->NO, cnt2);
-        COMAP_LAUNCH_CHECK(ctx);
-        COMAP_CHECK(ctx, hipMemsetAsync(cnt2 + d->NO, 0, 8, st));
-        COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_tb, cnt2, d->orow,
-                                                          (int)(d->NO + 1), st));
-        COMAP_NB_SWITCH(nb, k_perm_entries<NB><<<gblocks, 256, 0, st>>>(orow2, opix2, ow2, ws2, tw2, d->perm, d->NO,
-                                                                         d->orow, d->opix, d->ow, d->ws, d->tw));
-        COMAP_LAUNCH_CHECK(ctx);
-    }
-    // ---- pixel-major transpose (stable radix sort keeps offset order within a pixel)
-    k_entry_keys<<<grid_for(d->NO), 256, 0, st>>>(d->orow, d->NO, d->opix, npix, k0, v0, eoff);
+    // ---- 4. pixel-major transpose (stable: offset order within a pixel)
+    COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(cub_tmp, sort_tb, ekey, ekey2, eval, eval2, (int)d->nnz, 0,
+                                                        end_bit, st));
+    k_rowptr<<<grid_for(npix + 1), 256, 0, st>>>(ekey2, d->nnz, npix, d->prow);
     COMAP_LAUNCH_CHECK(ctx);
-    COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(sort_tmp, tb, k0, k1, v0, v1, (int)d->nnz, 0, end_bit, st));
-    k_rowptr<<<grid_for(npix + 1), 256, 0, st>>>(k1, d->nnz, npix, d->prow);
+    COMAP_NB_SWITCH(nb, k_pixel_entries<NB><<<grid_for(d->nnz, 8192), 256, 0, st>>>(eval2, d->prow + npix, eoff, d->ow,
+                                                                                     d->poff, d->pw));
     COMAP_LAUNCH_CHECK(ctx);
-    COMAP_CHECK(ctx, hipMemcpyAsync(&d->nnzp, d->prow + npix, 8, hipMemcpyDeviceToHost, st));
-    {
-        std::vector<int64_t> ph(npix + 1);
-        COMAP_CHECK(ctx, hipMemcpyAsync(ph.data(), d->prow, 8 * (size_t)(npix + 1), hipMemcpyDeviceToHost, st));
-        COMAP_CHECK(ctx, hipStreamSynchronize(st));
-        std::vector<int32_t> hr;
-        std::vector<int64_t> hp;
-        for (int64_t q = 0; q < npix; ++q)
-            if (ph[q + 1] > ph[q]) { hr.push_back((int32_t)q); hp.push_back(ph[q]); }
-        hp.push_back(ph[npix]);
-        d->nh = (int64_t)hr.size();
-        if (dalloc(ctx, &d->hrow, hr.size()) || dalloc(ctx, &d->hprow, hp.size())) return -2;
-        if (!hr.empty())
-            COMAP_CHECK(ctx, hipMemcpyAsync(d->hrow, hr.data(), 4 * hr.size(), hipMemcpyHostToDevice, st));
-        COMAP_CHECK(ctx, hipMemcpyAsync(d->hprow, hp.data(), 8 * hp.size(), hipMemcpyHostToDevice, st));
-        COMAP_CHECK(ctx, hipStreamSynchronize(st));
-    }
-    rc |= dalloc(ctx, &d->poff, d->nnzp);
-    rc |= dalloc(ctx, &d->pw, d->nnzp * NB);
-    if (rc) return -2;
+    k_hit_flags<<<grid_for(npix), 256, 0, st>>>(d->prow, npix, hflag);
+    COMAP_LAUNCH_CHECK(ctx);
+    COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(cub_tmp, scan32_tb, hflag, hpos, (int)npix, st));
+    k_hit_rows<<<grid_for(npix), 256, 0, st>>>(d->prow, hflag, hpos, npix, d->hrow, d->hprow, counts);
+    COMAP_LAUNCH_CHECK(ctx);
     {
         const char *bm = getenv("COMAP_DS_BIN");
         if (bm && !strcmp(bm, "lds")) {
             const char *tp = getenv("COMAP_DS_TILE");
             d->bin_mode = 1;
             d->bin_tile = tp ? std::max(32, std::min(4096, atoi(tp))) : 256;
-            if (dalloc(ctx, &d->ppix, d->nnzp)) return -2;
-            COMAP_CHECK(ctx, hipMemcpyAsync(d->ppix, k1, 4 * (size_t)d->nnzp, hipMemcpyDeviceToDevice, st));
+            if (dalloc(ctx, &d->ppix, d->nnz)) return -2;
+            COMAP_CHECK(ctx, hipMemcpyAsync(d->ppix, ekey2, 4 * (size_t)d->nnz, hipMemcpyDeviceToDevice, st));
         }
     }
-    COMAP_NB_SWITCH(nb, k_pixel_entries<NB><<<grid_for(d->nnzp), 256, 0, st>>>(v1, d->nnzp, eoff, d->ow, d->poff,
-                                                                                d->pw));
+    // ---- 5. sample-level maps (binValues order)
+    COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(cub_tmp, sort_tb, skey, skey2, sval, sval2, (int)N, 0, end_bit,
+                                                        st));
+    k_rowptr<<<grid_for(npix + 1), 256, 0, st>>>(skey2, N, npix, srow);
     COMAP_LAUNCH_CHECK(ctx);
-    // ---- sample-level maps (binValues order)
-    k_sample_keys<<<grid_for(N), 256, 0, st>>>(pix, N, npix, k0, v0);
+    COMAP_NB_SWITCH(nb, k_sample_walk<NB><<<grid_for(npix), 256, 0, st>>>(srow, sval2, payload, npix, L, NO, keep,
+                                                                          d->h, d->hits, d->nnum));
     COMAP_LAUNCH_CHECK(ctx);
-    COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(sort_tmp, tb, k0, k1, v0, v1, (int)N, 0, end_bit, st));
-    COMAP_NB_SWITCH(nb, k_sample_maps<NB><<<grid_for(npix), 256, 0, st>>>(k1, v1, N, npix, L, w, tod, keep, d->h,
-                                                                           d->hits, d->nnum));
-    COMAP_LAUNCH_CHECK(ctx);
+    int64_t hc[2] = {0, 0};
+    COMAP_CHECK(ctx, hipMemcpyAsync(hc, counts, 16, hipMemcpyDeviceToHost, st));
     COMAP_CHECK(ctx, hipStreamSynchronize(st));
+    d->nnzp = hc[0];
+    d->nh = hc[1];
     own.d = nullptr;
     *out = d;
     return 0;
