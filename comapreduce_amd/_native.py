@@ -85,6 +85,13 @@ _SIGS = {
     'comap_destripe_div_map': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     'comap_destripe_solve': (c_int, [c_void_p, c_double, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
                                      c_void_p, P_int32]),
+    'comap_prep_auto_rms': (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int32, c_int64, c_void_p]),
+    'comap_prep_percentiles': (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int32, c_int64,
+                                       c_void_p]),
+    'comap_prep_gather': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    'comap_prep_highpass': (c_int, [c_void_p, c_void_p, c_void_p, c_int32, c_int32]),
+    'comap_prep_cut': (c_int, [c_void_p, c_void_p, c_int32, c_int64, c_int32, c_void_p, c_void_p, c_int64,
+                               P_int64]),
 }
 
 EXPORTED = tuple(_SIGS)

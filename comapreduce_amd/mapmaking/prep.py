@@ -1,0 +1,274 @@
+"""Destriper data prep on the GPU (COMAPData.read_comap_data).
+
+Drives the ``comap_prep_*`` kernels (csrc/prep_kernels.hip) over a rank's
+Level-2 files: per file, one launch each for the auto_rms weights of every
+(feed, band), the az / el percentiles of every feed, and the per-sample gather
+(tod / cal, weight cuts, Sun distance, pixel ids); then one batched
+running-median high-pass over every (file, feed, scan, band) segment and one
+NaN / empty-offset cut with compaction.  Host work is per-file metadata only
+(scan table, feed mapping, calibration factors, the Sun's position and the
+WCS constants).  Inputs may be NumPy arrays (uploaded) or torch CUDA tensors
+(used in place: the Level-2 outputs of the device reduction).
+
+Reference: comancpipeline/MapMaking/COMAPData.py:72-117 (median_filter,
+transform_to_1d), 205-236 (auto_rms, Sun-centric coordinates, haversine),
+247-380 (get_tod), 383-427 (read_pixels), 471-577 (read_comap_data).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from .. import _native as N
+from . import astro
+
+MEDFILT_STEP = 400
+CALIBRATORS = ('TauA', 'CasA', 'CygA', 'jupiter')
+P = ctypes.c_void_p
+
+
+class PrepFile(ctypes.Structure):
+    """comap_prep_file (include/comap_hip.h)."""
+    _fields_ = [('tod', P), ('tod_feed_stride', ctypes.c_int64), ('tod_band_stride', ctypes.c_int64),
+                ('az', P), ('el', P), ('ra', P), ('dec', P), ('point_stride', ctypes.c_int64),
+                ('spike', P), ('spike_feed_stride', ctypes.c_int64), ('spike_band_stride', ctypes.c_int64),
+                ('n_rows', ctypes.c_int32), ('n_scans', ctypes.c_int32), ('datasize', ctypes.c_int64),
+                ('scans', P), ('row_src', P), ('pix_src', P), ('row_feed', P), ('row_cal', P), ('row_w', P),
+                ('row_pct', P), ('bands', ctypes.c_int32 * 4), ('n_bands', ctypes.c_int32),
+                ('sun_rot', ctypes.c_double * 9), ('obsid', ctypes.c_int64), ('pixels', P)]
+
+
+class PrepWCS(ctypes.Structure):
+    """comap_prep_wcs (include/comap_hip.h)."""
+    _fields_ = [('proj', ctypes.c_int32), ('galactic', ctypes.c_int32), ('eul', ctypes.c_double * 5),
+                ('crpix', ctypes.c_double * 2), ('cdelt', ctypes.c_double * 2), ('nx', ctypes.c_int64),
+                ('ny', ctypes.c_int64), ('gal_rot', ctypes.c_double * 9)]
+
+
+class PrepOut(ctypes.Structure):
+    """comap_prep_out (include/comap_hip.h)."""
+    _fields_ = [('tod', P), ('w', P), ('band_stride', ctypes.c_int64), ('az', P), ('el', P), ('ra', P),
+                ('dec', P), ('feedid', P), ('obsid', P), ('pix', P), ('offset', ctypes.c_int64)]
+
+
+class FlatArrays:
+    """read_comap_data's flat vectors on the device: tod / weights [nb, n], the rest [n]."""
+
+    def __init__(self, torch, dev, nb, n):
+        f64 = dict(dtype=torch.float64, device=dev)
+        self.tod = torch.zeros((nb, n), **f64)
+        self.w = torch.zeros((nb, n), **f64)
+        self.az, self.el, self.ra, self.dec = (torch.zeros(n, **f64) for _ in range(4))
+        self.feedid = torch.zeros(n, dtype=torch.int64, device=dev)
+        self.obsid = torch.zeros(n, dtype=torch.int64, device=dev)
+        self.pix = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.n = n
+
+    def struct(self, offset=0):
+        d = N.dptr
+        return PrepOut(d(self.tod), d(self.w), self.n, d(self.az), d(self.el), d(self.ra), d(self.dec),
+                       d(self.feedid), d(self.obsid), d(self.pix), int(offset))
+
+
+def wcs_struct(map_info):
+    """The CelestialWCS constants (mapmaking/wcs.py) for the device transform."""
+    w = map_info['wcs']
+    proj = {'CAR': 0, 'SIN': 1, 'TAN': 2}[w.proj]
+    gal = astro.Rotator(coord=['C', 'G']).mat if 'GLON' in w.ctype[0] else np.identity(3)
+    return PrepWCS(proj, int('GLON' in w.ctype[0]), (ctypes.c_double * 5)(*[float(v) for v in w.eul]),
+                   (ctypes.c_double * 2)(*w.crpix), (ctypes.c_double * 2)(*w.cdelt), int(map_info['nxpix']),
+                   int(map_info['nypix']), (ctypes.c_double * 9)(*np.asarray(gal, dtype=np.float64).ravel()))
+
+
+def _feed_rows(file_feeds, selected_feeds):
+    from .comapdata import GetFeeds
+    return GetFeeds(file_feeds, selected_feeds)
+
+
+def prep_flat(files, filelist, map_info, bands, use_gain_filter, offset_length, feeds, calibration, calibrator,
+              device, healpix=False):
+    """read_comap_data's vectors for every band in ``bands`` before the NaN and
+    empty-offset cuts (get_tod + read_pixels for every file, high-pass included).
+    Returns FlatArrays on the device."""
+    import torch
+    from .comapdata import countDataSize, feed_is_bad, get_scan_edges, scan_lengths
+    dev = torch.device('cuda', N.current_device() if device is None else int(device))
+    c = N.ctx(dev.index)
+    N.bind_stream(c, dev)
+    lib = N.lib()
+    L = int(offset_length)
+    nb = len(bands)
+    if not 1 <= nb <= 4:
+        raise ValueError('1 to 4 bands per prep call')
+    sizes = [countDataSize(f, len(feeds), L) for f in files]
+    out = FlatArrays(torch, dev, nb, sum(i['N'] for i in sizes))
+    wcs = None if healpix else wcs_struct(map_info)
+    segs = []
+    keep_alive = []
+    last = 0
+    for fn, f, info in zip(filelist, files, sizes):
+        ds = int(info['datasize'])
+        file_feeds = np.asarray(_host(f['spectrometer/feeds'])).astype(np.int64)
+        fi, oi = _feed_rows(file_feeds, feeds)
+        nrow = len(oi)
+        edges = np.asarray(_host(get_scan_edges(f)), dtype=np.int64).reshape(-1, 2)
+        lens = scan_lengths(edges, L)
+        obsid = int(os.path.basename(fn).split('-')[1])
+        if len(edges) == 0 or nrow == 0 or ds == 0:
+            # get_tod returns zeros; read_pixels leaves its zero rows (COMAPData.py:294-296)
+            if nrow * ds:
+                out.obsid[last:last + nrow * ds] = obsid
+            last += nrow * ds
+            continue
+        source = f.attrs('comap')['source'].split(',')[0]
+        calib = source in CALIBRATORS
+        dname = 'averaged_tod/tod' if (use_gain_filter and not calib) else 'averaged_tod/tod_original'
+        tod = _dev(torch, f[dname], dev, torch.float64)
+        F, B, T = tod.shape
+        bad = f.attrs('comap')['bad_observation']
+        if calibration:
+            cal = np.zeros((20, 4))
+            for b in range(4):
+                cal[:, b] = f.attrs('comap')[f'{calibrator}_calibration_factor_band{b}']
+        else:
+            cal = np.ones((F, B))
+        row_src = np.full(nrow, -1, np.int32)
+        row_feed = np.zeros(nrow, np.int64)
+        row_cal = np.ones((nrow, 4))
+        for ff, of in zip(fi, oi):
+            if feed_is_bad(bad[file_feeds[ff]]):
+                continue
+            row_src[of] = ff
+            row_feed[of] = file_feeds[ff]
+            for k, b in enumerate(bands):
+                row_cal[of, k] = cal[ff, b]
+        pix_src = np.full(nrow, -1, np.int32)
+        n = min(len(oi), len(fi))
+        pix_src[:n] = np.asarray(fi)[np.asarray(oi)[:n]]
+        az, el, ra, dec = (_dev(torch, f[f'spectrometer/pixel_pointing/pixel_{k}'], dev, torch.float64)
+                           for k in ('az', 'el', 'ra', 'dec'))
+        spike = f['spikes/spike_mask'] if 'spikes/spike_mask' in f else None
+        if spike is not None and len(_shape_of(spike)) == 1:     # COMAPData.py:268-269
+            spike = None
+        spike_d = None
+        if spike is not None:
+            spike_d = _spike_mask(torch, spike, dev, (F, B, T))
+        live = np.flatnonzero(row_src >= 0)
+        # weights: 1 / auto_rms(tod_file)^2 per (row, band) (COMAPData.py:320)
+        rms_rows = np.array([row_src[r] * B + b for r in live for b in bands], dtype=np.int32)
+        rms_scale = np.array([row_cal[r, k] for r in live for k in range(nb)], dtype=np.float64)
+        rms = torch.empty(max(1, rms_rows.size), dtype=torch.float64, device=dev)
+        rr, rs = _dev_np(torch, rms_rows, dev), _dev_np(torch, rms_scale, dev)
+        N.check(lib.comap_prep_auto_rms(c, N.dptr(tod), T, N.dptr(rr), N.dptr(rs), int(rms_rows.size), T,
+                                        N.dptr(rms)), c, 'comap_prep_auto_rms')
+        row_w = torch.ones((nrow, 4), dtype=torch.float64, device=dev)
+        if live.size:
+            row_w[torch.as_tensor(live, device=dev), :nb] = (1.0 / (rms * rms)).reshape(live.size, nb)
+        # az / el percentile band per row (COMAPData.py:338-346)
+        pct = torch.zeros((max(1, live.size), 4), dtype=torch.float64, device=dev)
+        pr = _dev_np(torch, row_src[live].astype(np.int32), dev)
+        N.check(lib.comap_prep_percentiles(c, N.dptr(az), N.dptr(el), T, N.dptr(pr), int(live.size), T,
+                                           N.dptr(pct)), c, 'comap_prep_percentiles')
+        row_pct = torch.zeros((nrow, 4), dtype=torch.float64, device=dev)
+        if live.size:
+            row_pct[torch.as_tensor(live, device=dev)] = pct[:live.size]
+        colstart = np.concatenate(([0], np.cumsum(lens)[:-1])).astype(np.int64)
+        scans = np.stack([edges[:, 0], np.asarray(lens, np.int64), colstart], axis=1).astype(np.int64)
+        if scans.shape[0] > 64:
+            raise ValueError('at most 64 scans per file')
+        mjd0 = float(np.asarray(_host(f['spectrometer/MJD'])).reshape(-1)[0])
+        sra, sdec = astro.sun_radec(mjd0)
+        rot = astro.Rotator(rot=[sra, sdec], inv=True).mat
+        pixels = None
+        if healpix:
+            from .comapdata import read_pixels_healpix
+            pixels = _dev_np(torch, np.asarray(read_pixels_healpix(f, ds, L, feeds, map_info)).astype(np.int64), dev)
+        dsc, drs, dps, drf, drc = (_dev_np(torch, a, dev) for a in (scans, row_src, pix_src, row_feed, row_cal))
+        bands4 = (ctypes.c_int32 * 4)(*(list(bands) + [0] * (4 - nb)))
+        pf = PrepFile(N.dptr(tod), B * T, T, N.dptr(az), N.dptr(el), N.dptr(ra), N.dptr(dec), T,
+                      None if spike_d is None else N.dptr(spike_d), B * T, T, nrow, int(scans.shape[0]), ds,
+                      N.dptr(dsc), N.dptr(drs), N.dptr(dps), N.dptr(drf), N.dptr(drc), N.dptr(row_w),
+                      N.dptr(row_pct), bands4, nb, (ctypes.c_double * 9)(*np.asarray(rot).ravel()), obsid,
+                      None if pixels is None else N.dptr(pixels))
+        o = out.struct(last)
+        N.check(lib.comap_prep_gather(c, ctypes.byref(pf), None if wcs is None else ctypes.byref(wcs),
+                                      ctypes.byref(o)), c, 'comap_prep_gather')
+        keep_alive.append((tod, az, el, ra, dec, spike_d, rr, rs, rms, row_w, pct, pr, row_pct, pixels, dsc, drs,
+                           dps, drf, drc))
+        if not calib:      # high-pass of each scan's non-zero samples (COMAPData.py:353-360)
+            for r in live:
+                for (s0, _), nl, cs in zip(edges, lens, colstart):
+                    if nl <= 0:
+                        continue
+                    for k in range(nb):
+                        segs.append((k * out.n + last + r * ds + cs, nl))
+        last += nrow * ds
+    if segs:
+        sd = _dev_np(torch, np.asarray(segs, dtype=np.int64), dev)
+        N.check(lib.comap_prep_highpass(c, N.dptr(out.tod), N.dptr(sd), len(segs), MEDFILT_STEP), c,
+                'comap_prep_highpass')
+    torch.cuda.current_stream(dev).synchronize()
+    del keep_alive
+    return out
+
+
+def cut_flat(flat, nb, offset_length, device=None):
+    """NaN -> 0 and the empty-offset cut (COMAPData.py:550-568) for every band, the
+    union of kept offsets compacted.  Returns (FlatArrays of the kept samples,
+    keep uint8 [nb, kept offsets] -- band b's own cut)."""
+    import torch
+    dev = flat.tod.device
+    c = N.ctx(dev.index)
+    N.bind_stream(c, dev)
+    L = int(offset_length)
+    out = FlatArrays(torch, dev, nb, flat.n)
+    cap = flat.n // L
+    keep = torch.zeros((nb, max(cap, 1)), dtype=torch.uint8, device=dev)
+    nk = ctypes.c_int64(0)
+    N.check(N.lib().comap_prep_cut(c, ctypes.byref(flat.struct()), nb, flat.n, L, ctypes.byref(out.struct()),
+                                   N.dptr(keep), max(cap, 1), ctypes.byref(nk)), c, 'comap_prep_cut')
+    n = int(nk.value) * L
+    cut = FlatArrays.__new__(FlatArrays)
+    cut.tod, cut.w = out.tod[:, :n], out.w[:, :n]
+    cut.az, cut.el, cut.ra, cut.dec = out.az[:n], out.el[:n], out.ra[:n], out.dec[:n]
+    cut.feedid, cut.obsid, cut.pix, cut.n = out.feedid[:n], out.obsid[:n], out.pix[:n], n
+    return cut, keep[:, :int(nk.value)]
+
+
+# ---------------------------------------------------------------- helpers
+def _host(x):
+    if hasattr(x, 'detach'):
+        return x.detach().cpu().numpy()
+    return np.asarray(x)
+
+
+def _shape_of(x):
+    return tuple(x.shape)
+
+
+def _dev(torch, x, dev, dtype):
+    if isinstance(x, torch.Tensor):
+        return x.to(device=dev, dtype=dtype).contiguous()
+    return torch.from_numpy(np.ascontiguousarray(np.asarray(x), dtype=np.dtype(str(dtype).split('.')[-1]))).to(dev)
+
+
+def _dev_np(torch, a, dev):
+    a = np.ascontiguousarray(a)
+    if a.size == 0:
+        a = np.zeros(1, dtype=a.dtype)
+    return torch.from_numpy(a).to(dev)
+
+
+def _spike_mask(torch, spike, dev, shape):
+    """spikes/spike_mask as a 0/1 byte mask (the reference indexes the weights with
+    it: a bool mask selects, an integer array would list positions)."""
+    if isinstance(spike, torch.Tensor):
+        if spike.dtype != torch.bool:
+            raise TypeError('spikes/spike_mask must be boolean')
+        return spike.to(device=dev, dtype=torch.uint8).contiguous()
+    s = np.asarray(spike)
+    if s.dtype != bool:
+        raise TypeError('spikes/spike_mask must be boolean')
+    return torch.from_numpy(np.ascontiguousarray(s.astype(np.uint8))).to(dev)

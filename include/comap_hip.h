@@ -14,6 +14,8 @@
  *                            + Analysis/GainSubtraction.py:17-209
  *   comap_l1_channel_bin     Analysis/Level1Averaging.py:249-321 (Level1Averaging)
  *   comap_destripe_*         MapMaking/Destriper.py:85-263,402-503
+ *   comap_prep_*             MapMaking/COMAPData.py:72-117,205-236,247-427,471-577
+ *                            (read_comap_data / get_tod / read_pixels)
  *
  * Conventions
  *   - Plain C types only; no C++ exceptions cross this boundary.
@@ -289,6 +291,75 @@ int comap_destripe_div_map(comap_destriper *d, const double *num_dev, const doub
 int comap_destripe_solve(comap_destriper *d, double threshold, int32_t niter, double *x_dev,
                          double *map_dev, double *naive_dev, double *weight_dev,
                          double *hits_dev, int32_t *iters_out);
+
+/* ------------------------------------------------------------ destriper data prep (COMAPData.py) */
+/* One Level-2 file's inputs to comap_prep_gather (device pointers).  Output row r
+ * (0 <= r < n_rows = len(output_feed_index)) takes its tod / weights / az / el /
+ * Sun coordinates from file feed row row_src[r] (-1: a bad feed, the row stays 0,
+ * COMAPData.py:306-315) and its pointing from file feed row pix_src[r] (read_pixels'
+ * row mapping, :423-424; -1: pixel 0).  Columns are the concatenated scans:
+ * scans[s] = {first sample, N_s = floor((end - start) / L) L, first column}. */
+typedef struct comap_prep_file {
+    const double *tod;            /* [F][B][T] averaged_tod/tod or tod_original */
+    int64_t tod_feed_stride, tod_band_stride;
+    const double *az, *el, *ra, *dec;   /* [F][T] spectrometer/pixel_pointing/pixel_* */
+    int64_t point_stride;
+    const uint8_t *spike;         /* [F][B][T] spikes/spike_mask (0 / 1), or NULL */
+    int64_t spike_feed_stride, spike_band_stride;
+    int32_t n_rows, n_scans;      /* n_scans <= 64 */
+    int64_t datasize;             /* columns per output row */
+    const int64_t *scans;         /* [n_scans][3] */
+    const int32_t *row_src, *pix_src;   /* [n_rows] */
+    const int64_t *row_feed;      /* [n_rows] feed id written to feedid */
+    const double *row_cal;        /* [n_rows][4] calibration factor per output band */
+    const double *row_w;          /* [n_rows][4] 1 / auto_rms^2 per output band */
+    const double *row_pct;        /* [n_rows][4] az 10 / 90, el 10 / 90 percentiles */
+    int32_t bands[4];             /* file band of output band k */
+    int32_t n_bands;              /* 1..4 */
+    double sun_rot[9];            /* healpy Rotator(rot=[sun ra, sun dec], inv=True) matrix */
+    int64_t obsid;
+    const int64_t *pixels;        /* [n_rows][datasize] precomputed pixel ids (HEALPix) or NULL */
+} comap_prep_file;
+/* CelestialWCS world -> pixel (CAR / SIN / TAN), transform_to_1d (COMAPData.py:83-117) */
+typedef struct comap_prep_wcs {
+    int32_t proj;                 /* 0 CAR, 1 SIN, 2 TAN */
+    int32_t galactic;             /* 1: J2000 -> galactic first (gal_rot, COMAPData.py:411-415) */
+    double eul[5];                /* wcslib celestial Euler angles: lng0, 90 - lat_p, phi_p, cos, sin */
+    double crpix[2], cdelt[2];
+    int64_t nx, ny;
+    double gal_rot[9];
+} comap_prep_wcs;
+/* Flat outputs (read_comap_data's vectors); a file's block starts at `offset` */
+typedef struct comap_prep_out {
+    double *tod, *w;              /* [n_bands][band_stride] */
+    int64_t band_stride;
+    double *az, *el, *ra, *dec;   /* ra = Sun distance (deg), dec = Sun-centric colatitude (rad) */
+    int64_t *feedid, *obsid;
+    int32_t *pix;
+    int64_t offset;
+} comap_prep_out;
+/* rms_dev[r] = COMAPData.auto_rms(x_r / scale[r]) (COMAPData.py:205-208), x_r =
+ * x_dev + rows[r] * row_stride (n values): NumPy's nanstd, bit for bit. */
+int comap_prep_auto_rms(comap_ctx *ctx, const double *x_dev, int64_t row_stride, const int32_t *rows_dev,
+                        const double *scale_dev, int32_t nrows, int64_t n, double *rms_dev);
+/* pct_dev[r] = np.percentile(az[good], (10, 90)), np.percentile(el[good], (10, 90)),
+ * good = isfinite(az) (COMAPData.py:338-346), bit for bit. */
+int comap_prep_percentiles(comap_ctx *ctx, const double *az_dev, const double *el_dev, int64_t row_stride,
+                           const int32_t *rows_dev, int32_t nrows, int64_t n, double *pct_dev);
+/* get_tod + read_pixels of one file into the flat outputs (COMAPData.py:247-427),
+ * before the high-pass; `wcs` may be NULL when f->pixels is given. */
+int comap_prep_gather(comap_ctx *ctx, const comap_prep_file *f, const comap_prep_wcs *wcs,
+                      const comap_prep_out *out);
+/* x[seg] -= median_filter(x[seg][keep], w) on keep = non-zero finite samples of each
+ * segment seg_dev[k] = {element offset, length} (COMAPData.py:72-81, 353-360).
+ * Synchronises (segment lengths size the median plan). */
+int comap_prep_highpass(comap_ctx *ctx, double *x_dev, const int64_t *seg_dev, int32_t nseg, int32_t w);
+/* NaN -> 0, keep[b][o] = any weight of offset o in band b non-zero, the union of kept
+ * offsets compacted into `out` (COMAPData.py:550-568).  Synchronises; *n_kept_out =
+ * kept offsets; keep_out_dev [n_bands][n_kept_cap]. */
+int comap_prep_cut(comap_ctx *ctx, const comap_prep_out *in, int32_t n_bands, int64_t n_samples,
+                   int32_t offset_length, const comap_prep_out *out, uint8_t *keep_out_dev,
+                   int64_t n_kept_cap, int64_t *n_kept_out);
 
 #ifdef __cplusplus
 }

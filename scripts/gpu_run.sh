@@ -10,11 +10,13 @@
 TAG=$1; shift
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+NSTEP=0
 for step in "$@"; do
+  NSTEP=$((NSTEP + 1))
   name=${step%%=*}; arg=${step#*=}; [ "$arg" = "$step" ] && arg=""
   case $name in
     tests) timeout -k 10 900 python -u -m pytest ${arg:-tests -m gpu} -x -v --timeout 400 --timeout-method thread \
-             > gpurun_out/${TAG}_pytest.log 2>&1 ;;
+             > gpurun_out/${TAG}_pytest${NSTEP}.log 2>&1 ;;
     bench) timeout -k 10 420 python -u bench.py ${arg:---steps 5 --warmup 2 --check} > gpurun_out/${TAG}_bench.log 2>&1 ;;
     prof)  timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_trace -o run \
              -- python3 bench.py ${arg:---steps 2 --warmup 1 --no-cpu-baseline} > gpurun_out/${TAG}_prof.log 2>&1 ;;
