@@ -7,17 +7,24 @@ is in this image.  ``Rotator`` below restates healpy's matrix construction
 psi]`` in degrees, ``get_rotation_matrix`` negating the latitude angle,
 ``get_coordconv_matrix`` for 'C'->'G', ``inv`` transposing) and its
 ``__call__(theta, phi)`` (ang2vec -> matrix -> vec2ang with phi in
-(-pi, pi]).  ``sun_radec`` is the Astronomical Almanac low-precision solar
-ephemeris (~0.01 deg, 1950-2050) referred to the J2000 equinox; astropy's
-``get_sun`` (GCRS) differs by ~arcsec-arcmin, which only moves samples that
-sit exactly on the reference's 10-degree Sun cut (measured: within 0.007 deg of
-astropy 4.3.1's get_sun, tests/test_astro_golden.py).  healpy is absent, so the
-Rotator is pinned to healpy's source only; the golden harness uses these same
-functions as its stand-ins, so everything downstream of them is pinned.
+(-pi, pi]).  ``sun_radec`` evaluates a Chebyshev table of the Sun's
+apparent geocentric direction fitted to astropy 4.3.1's ``get_sun`` (erfa
+epv00 + aberration, GCRS; the reference's pinned version) by
+tests/golden/make_sun_table.py and shipped as data (``sun_table.npz``, UTC MJD
+2018-01-01 .. 2036-01-01, fit residual 1.5e-10 deg); outside that range it falls
+back to the Astronomical Almanac low-precision ephemeris (~0.007 deg from
+get_sun), which only moves samples within that distance of the reference's
+10-degree Sun cut.  healpy is absent, so the Rotator is pinned to healpy's source
+only; the golden harness uses these same functions as its stand-ins, so
+everything downstream of them is pinned.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
+
+_SUN_TABLE = None
 
 
 def euler_matrix_zyx(a1, a2, a3):
@@ -67,8 +74,17 @@ class Rotator:
         return np.array([np.arccos(z / r), np.arctan2(y, x)])
 
 
-def sun_radec(mjd):
-    """Apparent solar RA/Dec (deg) referred to the J2000 equinox."""
+def _sun_table():
+    global _SUN_TABLE
+    if _SUN_TABLE is None:
+        with np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'sun_table.npz')) as z:
+            _SUN_TABLE = (float(z['mjd0']), float(z['seg_days']), np.array(z['coef']))
+    return _SUN_TABLE
+
+
+def sun_radec_almanac(mjd):
+    """Apparent solar RA/Dec (deg) referred to the J2000 equinox: the Astronomical
+    Almanac's low-precision formulae (~0.01 deg, 1950-2050)."""
     n = float(mjd) + 2400000.5 - 2451545.0
     L = 280.460 + 0.9856474 * n
     g = np.deg2rad(357.528 + 0.9856003 * n)
@@ -78,6 +94,21 @@ def sun_radec(mjd):
     lr = np.deg2rad(lam)
     ra = np.rad2deg(np.arctan2(np.cos(eps) * np.sin(lr), np.cos(lr))) % 360.0
     dec = np.rad2deg(np.arcsin(np.sin(eps) * np.sin(lr)))
+    return ra, dec
+
+
+def sun_radec(mjd):
+    """get_sun(Time(mjd, format='mjd')).ra.deg / .dec.deg (COMAPData.py:215-218):
+    the Chebyshev table of astropy 4.3.1's get_sun inside its range (UTC MJD), the
+    almanac outside it."""
+    mjd0, seg, coef = _sun_table()
+    k = int(np.floor((float(mjd) - mjd0) / seg))
+    if not 0 <= k < coef.shape[0]:
+        return sun_radec_almanac(mjd)
+    t = 2.0 * (float(mjd) - (mjd0 + seg * k)) / seg - 1.0
+    x, y, z = np.polynomial.chebyshev.chebval(t, coef[k].T)
+    ra = np.rad2deg(np.arctan2(y, x)) % 360.0
+    dec = np.rad2deg(np.arcsin(z / np.sqrt(x * x + y * y + z * z)))
     return ra, dec
 
 

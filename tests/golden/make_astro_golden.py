@@ -11,6 +11,7 @@ carries in a separate conda interpreter (not importable by the pipeline's Python
   including the map edges -- COMAPData.transform_to_1d calls wcs_world2pix(x, y, 0).
 * The Sun: astropy.coordinates.get_sun(Time(mjd, format='mjd')).ra/.dec in degrees
   (COMAPData.py:194, 218).
+* astropy's Sun at six more dates, for the 10-degree Sun-cut boundary test.
 * J2000 equatorial (FK5) -> galactic by astropy, for the GLON-CAR branch
   (the reference rotates with healpy's Rotator(coord=['C','G']), COMAPData.py:411-415;
   healpy is not in the image, so this pins that rotation to astropy's frames).
@@ -85,6 +86,13 @@ def main():
     out['sun_mjd'] = mjd
     out['sun_ra'] = np.asarray(sun.ra.deg)
     out['sun_dec'] = np.asarray(sun.dec.deg)
+    # the Sun at six dates for the 10-degree Sun-cut boundary test (COMAPData.py:326-335;
+    # tests/test_astro_golden.py places points 1e-6 .. 1e-2 deg from the cut around it)
+    cut_mjd = 58300.0 + np.array([0.0, 211.37, 512.9, 1300.25, 2111.6, 3650.01])
+    csun = get_sun(Time(cut_mjd, format='mjd'))
+    out['suncut_mjd'] = cut_mjd
+    out['suncut_sun_ra'] = np.asarray(csun.ra.deg)
+    out['suncut_sun_dec'] = np.asarray(csun.dec.deg)
     ra = rng.uniform(0, 360, 2000)
     dec = np.degrees(np.arcsin(rng.uniform(-1, 1, 2000)))
     g = SkyCoord(ra=ra * u.deg, dec=dec * u.deg, frame=FK5(equinox='J2000')).galactic
