@@ -61,6 +61,23 @@ struct comap_destriper {
     int64_t *prow = nullptr;   // [npix+1]
     int32_t *poff = nullptr;   // [nnzp]
     double *pw = nullptr;      // [nnzp][nb]
+    // count form (cf): every offset's non-zero sample weights in band b equal one value
+    // wbar[o][b] (COMAP's weights are per (feed, band, file), cuts set 0), so an entry
+    // stores the number of non-zero-weight samples per band (uint8) instead of the f64
+    // sums: s_e = wbar_o c_e.  opix / poff + ocnt / pcnt replace ow / pw (4 + NB bytes per
+    // entry instead of 4 + 8 NB); the bin gathers pt = wbar o x (written by the direction
+    // kernel, or by k_scale), the projection multiplies its row sum by wbar_o.
+    bool cf = false;
+    // launch shapes (defaults: the measured best; COMAP_DS_BL / BU / PG / PU / PB override)
+    int bin_lanes = 0;         // lanes per pixel row (0: by the mean row length)
+    int bin_u = 4;             // entry loads in flight per bin lane
+    int proj_lanes = 0;        // lanes per offset row (0: by L)
+    int proj_u = 4;            // entry loads in flight per projection lane
+    int64_t proj_blocks = 1024;   // projection grid cap (its p.q partials are re-summed by every update block)
+    uint8_t *ocnt = nullptr;   // [nnz][nb]
+    uint8_t *pcnt = nullptr;   // [nnzp][nb]
+    double *wbar = nullptr;    // [NO][nb]
+    double *pt = nullptr;      // [NO][nb] scaled bin input (CG direction / scratch)
     // sample-level maps (local), [npix][nb]
     double *h = nullptr, *hits = nullptr, *nnum = nullptr;
     // reduction scratch
@@ -73,11 +90,6 @@ struct comap_destriper {
     int64_t *hprow = nullptr;      // [nh + 1] their entry ranges: hprow[i] = prow[hrow[i]] (no empty row between)
     int64_t nh = 0;
     int32_t *perm = nullptr;       // [NO] internal offset position -> caller's offset (NULL: identity)
-    // COMAP_DS_BIN=lds (measurement variant): LDS-privatised scatter-add bin over pixel
-    // tiles of bin_tile pixels, needing each pixel-major entry's pixel
-    int bin_mode = 0;
-    int bin_tile = 256;
-    int32_t *ppix = nullptr;       // [nnzp] pixel of each pixel-major entry (bin_mode 1)
     int32_t *flags_host = nullptr; // pinned [2 + 2 nb]
     double *thr_host = nullptr;    // pinned [1]
     hipStream_t cs = nullptr;      // CG stream (graph capture needs a non-default stream)
@@ -92,8 +104,6 @@ constexpr int kUpdBlocks = 1024;  // CG update grid cap: its r.r partials are re
 constexpr int kProjBlocks = 1024; // k_ds_project grid cap: its p.q partials are re-summed by every update block
 constexpr int kDirBlocks = 1024;  // CG direction grid cap
 constexpr int kPartMax = 8192;     // >= every reduction grid below
-constexpr int kBinU = 4;           // entry loads in flight per lane (k_ds_bin)
-constexpr int kProjU = 4;          // entry loads in flight per lane (k_ds_project)
 constexpr int kCgBatch = 16;       // CG iterations per replayed graph (one host check per batch)
 
 typedef double d2v __attribute__((ext_vector_type(2)));
@@ -135,6 +145,29 @@ __device__ __forceinline__ void stb(double *__restrict__ p, const double (&v)[NB
     } else {
 #pragma unroll
         for (int b = 0; b < NB; ++b) p[b] = v[b];
+    }
+}
+
+// Entry coefficients of NB bands: the f64 weight sums (full form) or the uint8
+// non-zero-sample counts (count form, CF), as doubles.
+template <int NB, bool CF>
+__device__ __forceinline__ void ld_coef(const void *__restrict__ base, int64_t k, double (&a)[NB])
+{
+    if constexpr (CF) {
+        const uint8_t *c = reinterpret_cast<const uint8_t *>(base) + k * NB;
+        if constexpr (NB == 4) {
+            const uint32_t v = *reinterpret_cast<const uint32_t *>(c);
+#pragma unroll
+            for (int b = 0; b < 4; ++b) a[b] = (double)((v >> (8 * b)) & 0xffu);
+        } else if constexpr (NB == 2) {
+            const uint32_t v = *reinterpret_cast<const uint16_t *>(c);
+            a[0] = (double)(v & 0xffu);
+            a[1] = (double)(v >> 8);
+        } else {
+            a[0] = (double)c[0];
+        }
+    } else {
+        ldb<NB>(reinterpret_cast<const double *>(base) + k * NB, a);
     }
 }
 
@@ -295,16 +328,18 @@ __global__ void k_offset_keys(const int32_t *__restrict__ pix, int64_t NO, int L
 //   FILL = true:  the row's entries at orow[k]: pixel (-1 = off-map), weights, and the
 //                 pixel-major transpose's key / entry id / row.
 // w, tod: band-major [NB][N].
-template <int K, int NB, bool FILL>
+template <int K, int NB, bool FILL, bool CF>
 __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix, const double *__restrict__ w,
                                                  const double *__restrict__ tod, int64_t N, int64_t NO, int L,
                                                  int64_t npix, const int32_t *__restrict__ perm,
                                                  int64_t *__restrict__ cnt, double *__restrict__ ws,
                                                  double *__restrict__ tw, double *__restrict__ payload,
                                                  int32_t *__restrict__ skey, int32_t *__restrict__ sval,
+                                                 double *__restrict__ wbar, int32_t *__restrict__ nonuni,
                                                  const int64_t *__restrict__ orow, int32_t *__restrict__ opix,
-                                                 double *__restrict__ ow, int32_t *__restrict__ ekey,
-                                                 int32_t *__restrict__ eval, int32_t *__restrict__ eoff)
+                                                 double *__restrict__ ow, uint8_t *__restrict__ ocnt,
+                                                 int32_t *__restrict__ ekey, int32_t *__restrict__ eval,
+                                                 int32_t *__restrict__ eoff)
 {
 #pragma clang fp contract(off)
     const int lane = threadIdx.x & 63;
@@ -348,8 +383,10 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
             }
         }
     }
-    // per head: the group's in-order weight sums per band
+    // per head: the group's in-order weight sums per band (and, for the count form, its
+    // number of non-zero-weight samples)
     double gs[K][NB];
+    int gc[K][NB];
     bool keepe[K];
 #pragma unroll
     for (int m = 0; m < K; ++m) {
@@ -357,13 +394,18 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
             double s = 0.0;
+            int nz = 0;
             if (head[m]) {
 #pragma unroll
                 for (int c = 0; c < K; ++c)
-                    for (unsigned long long bits = mem[m][c]; bits; bits &= bits - 1)
-                        s += w[(int64_t)b * N + base + 64 * c + (__ffsll((long long)bits) - 1)];
+                    for (unsigned long long bits = mem[m][c]; bits; bits &= bits - 1) {
+                        const double v = w[(int64_t)b * N + base + 64 * c + (__ffsll((long long)bits) - 1)];
+                        s += v;
+                        nz += v != 0.0;
+                    }
             }
             gs[m][b] = s;
+            gc[m][b] = nz;
             any |= s != 0.0;
         }
         keepe[m] = head[m] && any;
@@ -394,14 +436,34 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
             double sw = 0.0, st = 0.0;
+            // count-form test: the offset's non-zero weights in band b are one finite value
+            double mn = INFINITY, mx = -INFINITY;
+            bool bad = false;
 #pragma unroll
             for (int m = 0; m < K; ++m) {
                 sw += wi[m][b];
                 if (lane + 64 * m < L) st = fma(wi[m][b], ti[m][b], st);   // fused, as before the rewrite
+                const double v = wi[m][b];
+                if (v != 0.0) {
+                    bad |= !isfinite(v);
+                    mn = fmin(mn, v);
+                    mx = fmax(mx, v);
+                }
             }
             sw = wave_sum(sw);
             st = wave_sum(st);
-            if (lane == 0) { ws[k * NB + b] = sw; tw[k * NB + b] = st; }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                mn = fmin(mn, __shfl_xor(mn, o, 64));
+                mx = fmax(mx, __shfl_xor(mx, o, 64));
+            }
+            bad = __ballot(bad) != 0ull;
+            if (lane == 0) {
+                ws[k * NB + b] = sw;
+                tw[k * NB + b] = st;
+                wbar[k * NB + b] = mx == -INFINITY ? 0.0 : mx;
+                if (bad || (mx != -INFINITY && mn != mx)) nonuni[0] = 1;
+            }
         }
         if (lane == 0) cnt[k] = c0;
     } else {
@@ -412,8 +474,13 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
             if (keepe[m]) {
                 const int64_t ei = e + __popcll(bm & ((1ull << lane) - 1ull));
                 opix[ei] = q[m];
+                if constexpr (CF) {
 #pragma unroll
-                for (int b = 0; b < NB; ++b) ow[ei * NB + b] = gs[m][b];
+                    for (int b = 0; b < NB; ++b) ocnt[ei * NB + b] = (uint8_t)gc[m][b];
+                } else {
+#pragma unroll
+                    for (int b = 0; b < NB; ++b) ow[ei * NB + b] = gs[m][b];
+                }
                 ekey[ei] = (q[m] >= 0 && q[m] < npix) ? q[m] : (int32_t)npix;
                 eval[ei] = (int32_t)ei;
                 eoff[ei] = (int32_t)k;
@@ -423,15 +490,16 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
     }
 }
 
-template <int NB, bool FILL>
+template <int NB, bool FILL, bool CF>
 void launch_rows(int L, hipStream_t st, const int32_t *pix, const double *w, const double *tod, int64_t N,
                  int64_t NO, int64_t npix, const int32_t *perm, int64_t *cnt, double *ws, double *tw, double *payload,
-                 int32_t *skey, int32_t *sval, const int64_t *orow, int32_t *opix, double *ow, int32_t *ekey,
-                 int32_t *eval, int32_t *eoff)
+                 int32_t *skey, int32_t *sval, double *wbar, int32_t *nonuni, const int64_t *orow, int32_t *opix,
+                 double *ow, uint8_t *ocnt, int32_t *ekey, int32_t *eval, int32_t *eoff)
 {
     const unsigned blocks = (unsigned)((NO + 3) / 4);
-#define COMAP_ROWS(K) k_ds_rows<K, NB, FILL><<<blocks, 256, 0, st>>>(pix, w, tod, N, NO, L, npix, perm, cnt, ws, tw, \
-                                                                      payload, skey, sval, orow, opix, ow, ekey, eval, eoff)
+#define COMAP_ROWS(K) k_ds_rows<K, NB, FILL, CF><<<blocks, 256, 0, st>>>(pix, w, tod, N, NO, L, npix, perm, cnt, ws, \
+                                                                          tw, payload, skey, sval, wbar, nonuni, orow, \
+                                                                          opix, ow, ocnt, ekey, eval, eoff)
     if (L <= 64) COMAP_ROWS(1);
     else if (L <= 128) COMAP_ROWS(2);
     else COMAP_ROWS(4);
@@ -472,15 +540,37 @@ __global__ void k_rowptr(const int32_t *__restrict__ skey, int64_t n, int64_t np
 template <int NB>
 __global__ void k_pixel_entries(const int32_t *__restrict__ sval, const int64_t *__restrict__ nnzp_dev,
                                 const int32_t *__restrict__ eoff, const double *__restrict__ ow,
-                                int32_t *__restrict__ poff, double *__restrict__ pw)
+                                const uint8_t *__restrict__ ocnt, int32_t *__restrict__ poff, double *__restrict__ pw,
+                                uint8_t *__restrict__ pcnt)
 {
     const int64_t nnzp = *nnzp_dev;
     for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < nnzp; k += (int64_t)gridDim.x * blockDim.x) {
         const int32_t e = sval[k];
         poff[k] = eoff[e];
-        double v[NB];
-        ldb<NB>(ow + (int64_t)e * NB, v);
-        stb<NB>(pw + k * NB, v);
+        if (ocnt) {
+#pragma unroll
+            for (int b = 0; b < NB; ++b) pcnt[k * NB + b] = ocnt[(int64_t)e * NB + b];
+        } else {
+            double v[NB];
+            ldb<NB>(ow + (int64_t)e * NB, v);
+            stb<NB>(pw + k * NB, v);
+        }
+    }
+}
+
+// xs = wbar o x per band (the count form's bin input); gated by the CG stop flags
+template <int NB>
+__global__ void k_scale(const double *__restrict__ wbar, const double *__restrict__ x, int64_t NO,
+                        double *__restrict__ xs, const int32_t *__restrict__ flags)
+{
+    if (cg_done(flags)) return;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < NO; i += (int64_t)gridDim.x * blockDim.x) {
+        double a[NB], v[NB];
+        ldb<NB>(wbar + i * NB, a);
+        ldb<NB>(x + i * NB, v);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) v[b] *= a[b];
+        stb<NB>(xs + i * NB, v);
     }
 }
 
@@ -576,9 +666,9 @@ __device__ __forceinline__ double map_value(const double *num, const double *h, 
 // entries), lane-strided; each lane issues kBinU entry loads, then kBinU gathers of the
 // NB-band x vectors, before its fmas (in entry order, so the sum is the plain
 // lane-strided one), then a kBinLanes-lane reduction.
-template <int kBinLanes, int NB>
+template <int kBinLanes, int NB, bool CF, int kBinU>
 __global__ void __launch_bounds__(256) k_ds_bin(const int64_t *__restrict__ prow, const int32_t *__restrict__ poff,
-                                                const double *__restrict__ pw, const double *__restrict__ x,
+                                                const void *__restrict__ pw, const double *__restrict__ x,
                                                 int64_t npix, const double *__restrict__ base,
                                                 const double *__restrict__ hdiv, double *__restrict__ num,
                                                 const int32_t *__restrict__ flags, const int32_t *__restrict__ rows = nullptr)
@@ -603,7 +693,7 @@ __global__ void __launch_bounds__(256) k_ds_bin(const int64_t *__restrict__ prow
                 const bool in = k + u * kBinLanes < e1;
                 o[u] = in ? poff[k + u * kBinLanes] : 0;
                 if (in) {
-                    ldb<NB>(pw + (k + u * kBinLanes) * NB, a[u]);
+                    ld_coef<NB, CF>(pw, k + u * kBinLanes, a[u]);
                 } else {
 #pragma unroll
                     for (int b = 0; b < NB; ++b) a[u][b] = 0.0;
@@ -634,72 +724,15 @@ __global__ void __launch_bounds__(256) k_ds_bin(const int64_t *__restrict__ prow
     }
 }
 
-// The north_star's formulation of the same bin, kept as a measured alternative
-// (COMAP_DS_BIN=lds): one workgroup per tile of TP consecutive pixels privatises the
-// tile's NB-band numerators in LDS; its threads stream the tile's entries (coalesced,
-// in pixel-major order) and scatter-add s_e x_o(e) with LDS f64 atomics, then write the
-// tile out with the same base / hdiv post-processing.  The add order within a pixel is
-// not fixed (results vary in the last bits run to run).
-template <int NB>
-__global__ void __launch_bounds__(256) k_ds_bin_lds(const int64_t *__restrict__ prow, const int32_t *__restrict__ poff,
-                                                    const double *__restrict__ pw, const int32_t *__restrict__ ppix,
-                                                    const double *__restrict__ x, int64_t npix, int TP,
-                                                    const double *__restrict__ base, const double *__restrict__ hdiv,
-                                                    double *__restrict__ num, const int32_t *__restrict__ flags)
-{
-    extern __shared__ double tacc[];   // [TP][NB]
-    if (cg_done(flags)) return;
-    const int64_t P0 = (int64_t)blockIdx.x * TP, P1 = min(npix, P0 + TP);
-    const int nt = (int)(P1 - P0) * NB;
-    for (int i = threadIdx.x; i < nt; i += 256) tacc[i] = 0.0;
-    __syncthreads();
-    const int64_t e1 = prow[P1];
-    constexpr int U = 4;
-    for (int64_t e = prow[P0] + threadIdx.x; e < e1; e += 256 * U) {
-        int32_t o[U], q[U];
-        double a[U][NB], xv[U][NB];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t k = e + u * 256;
-            const bool in = k < e1;
-            o[u] = in ? poff[k] : 0;
-            q[u] = in ? ppix[k] - (int32_t)P0 : -1;
-            if (in) {
-                ldb<NB>(pw + k * NB, a[u]);
-            } else {
-#pragma unroll
-                for (int b = 0; b < NB; ++b) a[u][b] = 0.0;
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) ldb<NB>(x + (int64_t)o[u] * NB, xv[u]);
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (q[u] >= 0) {
-#pragma unroll
-                for (int b = 0; b < NB; ++b)
-                    __hip_atomic_fetch_add(&tacc[q[u] * NB + b], a[u][b] * xv[u][b], __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < nt; i += 256) {
-        const int64_t g = P0 * NB + i;
-        double s = tacc[i];
-        if (base) s = base[g] - s;
-        else if (hdiv) { const double hv = hdiv[g]; s = hv != 0.0 ? s / hv : s; }
-        num[g] = s;
-    }
-}
-
 // y_o = ws_o x_o - sum_e s_e m_p(e) per band  (x == NULL: y_o = tw_o - ..., the b vector).
 // G lanes per offset (G = 16 for L <= 64: 256/G offsets per block sweep); each lane issues
 // kProjU entry loads then kProjU map gathers before its fmas; m = num / h, or num itself
 // when h == NULL (k_ds_bin already divided).  Block partials of y.x per band
 // (dot_part + b kPartMax, when dot_part != NULL).
-template <int G, int NB>
+template <int G, int NB, bool CF, int kProjU>
 __global__ void __launch_bounds__(256) k_ds_project(const int64_t *__restrict__ orow, const int32_t *__restrict__ opix,
-                                                    const double *__restrict__ ow, const double *__restrict__ ws,
+                                                    const void *__restrict__ ow, const double *__restrict__ wbar,
+                                                    const double *__restrict__ ws,
                                                     const double *__restrict__ tw, const double *__restrict__ x,
                                                     const double *__restrict__ num, const double *__restrict__ h,
                                                     int64_t NO, int64_t npix, double *__restrict__ y,
@@ -719,15 +752,31 @@ __global__ void __launch_bounds__(256) k_ds_project(const int64_t *__restrict__ 
     const int64_t s0 = xcd_block(blockIdx.x, gridDim.x) * per, s1 = min(s0 + per, sweeps);
     for (int64_t o0 = s0 * kPer; o0 < s1 * kPer; o0 += kPer) {
 #else
+    // the row bounds of the next sweep are loaded before this sweep's entries (one less
+    // dependent load per sweep)
+    int64_t nb0 = 0, nb1 = 0;
+    {
+        const int64_t o = (int64_t)blockIdx.x * kPer + threadIdx.x / G;
+        if (o < NO) { nb0 = orow[o]; nb1 = orow[o + 1]; }
+    }
     for (int64_t o0 = (int64_t)blockIdx.x * kPer; o0 < NO; o0 += (int64_t)gridDim.x * kPer) {
 #endif
         const int64_t o = o0 + threadIdx.x / G;
         const bool valid = o < NO;
-        const int64_t e1 = valid ? orow[o + 1] : 0;
+#if COMAP_DS_XCD
+        const int64_t e0 = valid ? orow[o] : 0, e1 = valid ? orow[o + 1] : 0;
+#else
+        const int64_t e0 = nb0, e1 = nb1;
+        {
+            const int64_t on = o + (int64_t)gridDim.x * kPer;
+            nb0 = nb1 = 0;
+            if (on < NO) { nb0 = orow[on]; nb1 = orow[on + 1]; }
+        }
+#endif
         double g[NB];
 #pragma unroll
         for (int b = 0; b < NB; ++b) g[b] = 0.0;
-        for (int64_t e = (valid ? orow[o] : 0) + sub; e < e1; e += G * kProjU) {
+        for (int64_t e = e0 + sub; e < e1; e += G * kProjU) {
             int32_t q[kProjU];
             double a[kProjU][NB], mv[kProjU][NB];
 #pragma unroll
@@ -736,7 +785,7 @@ __global__ void __launch_bounds__(256) k_ds_project(const int64_t *__restrict__ 
                 const int32_t pp = in ? opix[e + u * G] : 0;
                 q[u] = pp >= 0 ? pp : (int32_t)(npix - 1);   // m[-1] for off-map samples
                 if (in) {
-                    ldb<NB>(ow + (e + u * G) * NB, a[u]);
+                    ld_coef<NB, CF>(ow, e + u * G, a[u]);
                 } else {
 #pragma unroll
                     for (int b = 0; b < NB; ++b) a[u][b] = 0.0;
@@ -770,6 +819,12 @@ __global__ void __launch_bounds__(256) k_ds_project(const int64_t *__restrict__ 
             } else {
 #pragma unroll
                 for (int b = 0; b < NB; ++b) xo[b] = 0.0;
+            }
+            if constexpr (CF) {   // the row's sum of counts x m, times the offset's weight
+                double wb[NB];
+                ldb<NB>(wbar + o * NB, wb);
+#pragma unroll
+                for (int b = 0; b < NB; ++b) g[b] *= wb[b];
             }
 #pragma unroll
             for (int b = 0; b < NB; ++b) {
@@ -841,10 +896,12 @@ __device__ __forceinline__ void update_row(double *__restrict__ x, double *__res
     stb<NB>(r, rv);
 }
 
-// p = r + beta p for the live bands of one offset
+// p = r + beta p for the live bands of one offset; wbar != NULL (count form): also
+// pt = wbar o p, the next bin's input
 template <int NB>
 __device__ __forceinline__ void direction_row(double *__restrict__ p, const double *__restrict__ r,
-                                              const double (&beta)[NB], const bool (&live)[NB])
+                                              const double (&beta)[NB], const bool (&live)[NB],
+                                              const double *__restrict__ wbar = nullptr, double *__restrict__ pt = nullptr)
 {
     double pv[NB], rv[NB];
     ldb<NB>(p, pv);
@@ -853,6 +910,13 @@ __device__ __forceinline__ void direction_row(double *__restrict__ p, const doub
     for (int b = 0; b < NB; ++b)
         if (live[b]) pv[b] = rv[b] + beta[b] * pv[b];
     stb<NB>(p, pv);
+    if (wbar) {
+        double a[NB];
+        ldb<NB>(wbar, a);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) pv[b] *= a[b];
+        stb<NB>(pt, pv);
+    }
 }
 
 // x += a p ; r -= a q ; a = rr / pq per band (bands already stopped are left alone);
@@ -939,7 +1003,9 @@ __global__ void __launch_bounds__(256) k_cg_update_fused(double *__restrict__ sc
 template <int NB>
 __global__ void __launch_bounds__(256) k_cg_direction_fused(double *__restrict__ scal, const double *__restrict__ part_rr,
                                                             int nrr, double *__restrict__ p, const double *__restrict__ r,
-                                                            int64_t n, int32_t *flags, int64_t pstride = kPartMax)
+                                                            int64_t n, int32_t *flags, int64_t pstride = kPartMax,
+                                                            const double *__restrict__ wbar = nullptr,
+                                                            double *__restrict__ pt = nullptr)
 {
     __shared__ double red[4 * NB];
     if (flags[0]) return;
@@ -952,7 +1018,8 @@ __global__ void __launch_bounds__(256) k_cg_direction_fused(double *__restrict__
         live[b] = !flags[2 + b];
     }
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        direction_row<NB>(p + i * NB, r + i * NB, beta, live);
+        direction_row<NB>(p + i * NB, r + i * NB, beta, live, wbar ? wbar + i * NB : nullptr,
+                          wbar ? pt + i * NB : nullptr);
     // block 0 only, after its own sweep: a band that stops here never reads p again.
     // scal[NB+b] is left alone -- other blocks may still be reading it for beta; the
     // fused update takes rr from scal[3NB+b] and rewrites scal[NB+b] itself.
@@ -1007,72 +1074,100 @@ inline unsigned upd_grid(int64_t NO) { return grid_for(NO, kUpdBlocks); }
 // hold ~5 entries per pixel: 16 lanes per row would leave most lanes idle and
 // need several latency-bound grid sweeps); one sweep over all rows.
 // hit_rows: only the non-empty rows (d->hrow; the caller's num must hold 0 on the
-// empty rows, as the CG's own map buffer does).
-template <int NB>
-void launch_bin_nb(const comap_destriper *d, hipStream_t st, const double *x, const double *base, const double *hdiv,
-                   double *num, const int32_t *flags, bool hit_rows)
+// empty rows, as the CG's own map buffer does).  Count form: x must already be
+// scaled (wbar o x, x_scaled) or is scaled into d->pt first.
+template <int NB, bool CF, int U>
+void launch_bin_u(const comap_destriper *d, hipStream_t st, const double *x, const double *base, const double *hdiv,
+                  double *num, const int32_t *flags, bool hit_rows)
 {
-    if (d->bin_mode == 1) {
-        const int TP = d->bin_tile;
-        const unsigned g = (unsigned)std::max<int64_t>(1, (d->npix + TP - 1) / TP);
-        k_ds_bin_lds<NB><<<g, 256, sizeof(double) * TP * NB, st>>>(d->prow, d->poff, d->pw, d->ppix, x, d->npix, TP,
-                                                                  base, hdiv, num, flags);
-        return;
-    }
     const int64_t np = hit_rows ? d->nh : d->npix;
     const int32_t *rows = hit_rows ? d->hrow : nullptr;
     const int64_t *rp = hit_rows ? d->hprow : d->prow;
     const int64_t mean = np ? d->nnzp / np : 0;
-    const int lanes = mean >= 24 ? 16 : (mean >= 10 ? 8 : 4);
+    const int lanes = d->bin_lanes ? d->bin_lanes : (mean >= 24 ? 16 : (mean >= 10 ? 8 : 4));
     const unsigned g = grid_for(np * lanes, 65536);
-    if (lanes == 16)
-        k_ds_bin<16, NB><<<g, 256, 0, st>>>(rp, d->poff, d->pw, x, np, base, hdiv, num, flags, rows);
-    else if (lanes == 8)
-        k_ds_bin<8, NB><<<g, 256, 0, st>>>(rp, d->poff, d->pw, x, np, base, hdiv, num, flags, rows);
-    else
-        k_ds_bin<4, NB><<<g, 256, 0, st>>>(rp, d->poff, d->pw, x, np, base, hdiv, num, flags, rows);
+    const void *co = CF ? (const void *)d->pcnt : (const void *)d->pw;
+#define COMAP_BIN(LN) k_ds_bin<LN, NB, CF, U><<<g, 256, 0, st>>>(rp, d->poff, co, x, np, base, hdiv, num, flags, rows)
+    switch (lanes) {
+    case 64: COMAP_BIN(64); break;
+    case 32: COMAP_BIN(32); break;
+    case 16: COMAP_BIN(16); break;
+    case 8: COMAP_BIN(8); break;
+    default: COMAP_BIN(4);
+    }
+#undef COMAP_BIN
+}
+
+template <int NB, bool CF>
+void launch_bin_cf(const comap_destriper *d, hipStream_t st, const double *x, const double *base, const double *hdiv,
+                   double *num, const int32_t *flags, bool hit_rows)
+{
+    if (d->bin_u == 8) launch_bin_u<NB, CF, 8>(d, st, x, base, hdiv, num, flags, hit_rows);
+    else launch_bin_u<NB, CF, 4>(d, st, x, base, hdiv, num, flags, hit_rows);
 }
 
 void launch_bin(const comap_destriper *d, hipStream_t st, const double *x, const double *base, const double *hdiv,
-                double *num, const int32_t *flags, bool hit_rows = false)
+                double *num, const int32_t *flags, bool hit_rows = false, bool x_scaled = false)
 {
-    COMAP_NB_SWITCH(d->nb, launch_bin_nb<NB>(d, st, x, base, hdiv, num, flags, hit_rows));
+    if (d->cf && !x_scaled) {
+        COMAP_NB_SWITCH(d->nb, k_scale<NB><<<grid_for(d->NO), 256, 0, st>>>(d->wbar, x, d->NO, d->pt, flags));
+        x = d->pt;
+    }
+    if (d->cf) {
+        COMAP_NB_SWITCH(d->nb, (launch_bin_cf<NB, true>(d, st, x, base, hdiv, num, flags, hit_rows)));
+    } else {
+        COMAP_NB_SWITCH(d->nb, (launch_bin_cf<NB, false>(d, st, x, base, hdiv, num, flags, hit_rows)));
+    }
 }
 
-inline int project_lanes(int L) { return L <= 64 ? 16 : (L <= 128 ? 32 : 64); }
-inline unsigned project_grid(int64_t NO, int L)
+inline int project_lanes(const comap_destriper *d)
 {
-    const int64_t per = 256 / project_lanes(L);
-    return (unsigned)std::max<int64_t>(1, std::min<int64_t>((NO + per - 1) / per, kProjBlocks));
+    if (d->proj_lanes) return d->proj_lanes;
+    return d->L <= 64 ? 16 : (d->L <= 128 ? 32 : 64);
+}
+inline unsigned project_grid(const comap_destriper *d, int64_t cap)
+{
+    const int64_t per = 256 / project_lanes(d);
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>((d->NO + per - 1) / per, std::min<int64_t>(cap, d->proj_blocks)));
 }
 
 // k_ds_project with the lane group sized to the offset length; returns its grid (= partials).
-template <int NB>
-unsigned launch_project_nb(const comap_destriper *d, hipStream_t st, const double *x, const double *num,
+template <int NB, bool CF, int U>
+unsigned launch_project_u(const comap_destriper *d, hipStream_t st, const double *x, const double *num,
+                          const double *h, double *y, double *part, const int32_t *flags, int64_t pstride)
+{
+    const unsigned pg = project_grid(d, pstride);
+    const void *co = CF ? (const void *)d->ocnt : (const void *)d->ow;
+#define COMAP_PROJ(G) k_ds_project<G, NB, CF, U><<<pg, 256, 0, st>>>(d->orow, d->opix, co, d->wbar, d->ws, d->tw, x, \
+                                                                     num, h, d->NO, d->npix, y, part, flags, pstride)
+    switch (project_lanes(d)) {
+    case 4: COMAP_PROJ(4); break;
+    case 8: COMAP_PROJ(8); break;
+    case 16: COMAP_PROJ(16); break;
+    case 32: COMAP_PROJ(32); break;
+    default: COMAP_PROJ(64);
+    }
+#undef COMAP_PROJ
+    return pg;
+}
+
+template <int NB, bool CF>
+unsigned launch_project_cf(const comap_destriper *d, hipStream_t st, const double *x, const double *num,
                            const double *h, double *y, double *part, const int32_t *flags, int64_t pstride)
 {
-    const unsigned pg = project_grid(d->NO, d->L);
-    switch (project_lanes(d->L)) {
-    case 16:
-        k_ds_project<16, NB><<<pg, 256, 0, st>>>(d->orow, d->opix, d->ow, d->ws, d->tw, x, num, h, d->NO, d->npix, y,
-                                                 part, flags, pstride);
-        break;
-    case 32:
-        k_ds_project<32, NB><<<pg, 256, 0, st>>>(d->orow, d->opix, d->ow, d->ws, d->tw, x, num, h, d->NO, d->npix, y,
-                                                 part, flags, pstride);
-        break;
-    default:
-        k_ds_project<64, NB><<<pg, 256, 0, st>>>(d->orow, d->opix, d->ow, d->ws, d->tw, x, num, h, d->NO, d->npix, y,
-                                                 part, flags, pstride);
-    }
-    return pg;
+    return d->proj_u == 8 ? launch_project_u<NB, CF, 8>(d, st, x, num, h, y, part, flags, pstride)
+                          : launch_project_u<NB, CF, 4>(d, st, x, num, h, y, part, flags, pstride);
 }
 
 unsigned launch_project(const comap_destriper *d, hipStream_t st, const double *x, const double *num,
                         const double *h, double *y, double *part, const int32_t *flags, int64_t pstride = kPartMax)
 {
     unsigned pg = 0;
-    COMAP_NB_SWITCH(d->nb, pg = launch_project_nb<NB>(d, st, x, num, h, y, part, flags, pstride));
+    if (d->cf) {
+        COMAP_NB_SWITCH(d->nb, (pg = launch_project_cf<NB, true>(d, st, x, num, h, y, part, flags, pstride)));
+    } else {
+        COMAP_NB_SWITCH(d->nb, (pg = launch_project_cf<NB, false>(d, st, x, num, h, y, part, flags, pstride)));
+    }
     return pg;
 }
 
@@ -1150,6 +1245,8 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     rc |= dalloc(ctx, &d->orow, NO + 1);
     rc |= dalloc(ctx, &d->ws, NO * NB);
     rc |= dalloc(ctx, &d->tw, NO * NB);
+    rc |= dalloc(ctx, &d->wbar, NO * NB);
+    rc |= dalloc(ctx, &d->pt, NO * NB);
     rc |= dalloc(ctx, &d->prow, npix + 1);
     rc |= dalloc(ctx, &d->h, npix * NB);
     rc |= dalloc(ctx, &d->hits, npix * NB);
@@ -1174,7 +1271,8 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     Arena ar;
     ar.cap = Arena::bytes<char>(cub_tb) + Arena::bytes<int64_t>(NO + 1) + 8 * Arena::bytes<int32_t>(N) +
              Arena::bytes<double>((size_t)N * 2 * NB) + Arena::bytes<int64_t>(npix + 1) +
-             2 * Arena::bytes<int32_t>(npix) + Arena::bytes<int64_t>(2) + Arena::bytes<int32_t>(N);
+             2 * Arena::bytes<int32_t>(npix) + Arena::bytes<int64_t>(2) + Arena::bytes<int32_t>(N) +
+             Arena::bytes<int32_t>(1);
     COMAP_CHECK(ctx, hipMalloc((void **)&ar.base, ar.cap));
     struct ArenaFree {
         Arena *a;
@@ -1196,6 +1294,7 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     int64_t *srow = ar.take<int64_t>(npix + 1);
     int32_t *hflag = ar.take<int32_t>(npix), *hpos = ar.take<int32_t>(npix);
     int64_t *counts = ar.take<int64_t>(2);
+    int32_t *nonuni = ar.take<int32_t>(1);
     // ---- 1. spatial processing order of the offsets
     if (spatial) {
         k_offset_keys<<<grid_for(NO), 256, 0, st>>>(pix, NO, L, npix, ekey, eval);
@@ -1203,22 +1302,56 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(cub_tmp, sort_tb, ekey, ekey2, eval, d->perm, (int)NO, 0,
                                                             end_bit, st));
     }
-    // ---- 2. count pass
-    COMAP_NB_SWITCH(nb, (launch_rows<NB, false>(L, st, pix, w, tod, N, NO, npix, d->perm, cnt, d->ws, d->tw, payload,
-                                                skey, sval, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr)));
+    // ---- 2. count pass (+ the count-form test: non-zero weights uniform per offset and band)
+    COMAP_CHECK(ctx, hipMemsetAsync(nonuni, 0, 4, st));
+    COMAP_NB_SWITCH(nb, (launch_rows<NB, false, false>(L, st, pix, w, tod, N, NO, npix, d->perm, cnt, d->ws, d->tw,
+                                                       payload, skey, sval, d->wbar, nonuni, nullptr, nullptr, nullptr,
+                                                       nullptr, nullptr, nullptr, nullptr)));
     COMAP_LAUNCH_CHECK(ctx);
     COMAP_CHECK(ctx, hipMemsetAsync(cnt + NO, 0, 8, st));
     COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(cub_tmp, scan_tb, cnt, d->orow, (int)(NO + 1), st));
+    int32_t nonuni_h = 0;
     COMAP_CHECK(ctx, hipMemcpyAsync(&d->nnz, d->orow + NO, 8, hipMemcpyDeviceToHost, st));
+    COMAP_CHECK(ctx, hipMemcpyAsync(&nonuni_h, nonuni, 4, hipMemcpyDeviceToHost, st));
     COMAP_CHECK(ctx, hipStreamSynchronize(st));
+    {
+        const char *cfe = getenv("COMAP_DS_CF");             // 0: always the f64 entry weights
+        d->cf = !nonuni_h && L <= 255 && !(cfe && cfe[0] == '0');
+        // launch-shape overrides (measurement knobs; invalid values keep the defaults)
+        auto env_int = [](const char *k, int dflt, std::initializer_list<int> ok) {
+            const char *v = getenv(k);
+            if (!v) return dflt;
+            const int x = atoi(v);
+            for (int o : ok)
+                if (x == o) return x;
+            return dflt;
+        };
+        d->bin_lanes = env_int("COMAP_DS_BL", 0, {4, 8, 16, 32, 64});
+        d->bin_u = env_int("COMAP_DS_BU", 4, {4, 8});
+        d->proj_lanes = env_int("COMAP_DS_PG", 0, {4, 8, 16, 32, 64});
+        d->proj_u = env_int("COMAP_DS_PU", 4, {4, 8});
+        d->proj_blocks = env_int("COMAP_DS_PB", kProjBlocks, {256, 512, 1024, 2048, 4096, 8192});
+    }
     rc |= dalloc(ctx, &d->opix, d->nnz);
-    rc |= dalloc(ctx, &d->ow, d->nnz * NB);
     rc |= dalloc(ctx, &d->poff, d->nnz);          // nnzp <= nnz (off-map entries are not binned)
-    rc |= dalloc(ctx, &d->pw, d->nnz * NB);
+    if (d->cf) {
+        rc |= dalloc(ctx, &d->ocnt, d->nnz * NB);
+        rc |= dalloc(ctx, &d->pcnt, d->nnz * NB);
+    } else {
+        rc |= dalloc(ctx, &d->ow, d->nnz * NB);
+        rc |= dalloc(ctx, &d->pw, d->nnz * NB);
+    }
     if (rc) return -2;
     // ---- 3. fill pass
-    COMAP_NB_SWITCH(nb, (launch_rows<NB, true>(L, st, pix, w, tod, N, NO, npix, d->perm, nullptr, nullptr, nullptr,
-                                               nullptr, nullptr, nullptr, d->orow, d->opix, d->ow, ekey, eval, eoff)));
+    if (d->cf) {
+        COMAP_NB_SWITCH(nb, (launch_rows<NB, true, true>(L, st, pix, w, tod, N, NO, npix, d->perm, nullptr, nullptr,
+                                                         nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, d->orow,
+                                                         d->opix, nullptr, d->ocnt, ekey, eval, eoff)));
+    } else {
+        COMAP_NB_SWITCH(nb, (launch_rows<NB, true, false>(L, st, pix, w, tod, N, NO, npix, d->perm, nullptr, nullptr,
+                                                          nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, d->orow,
+                                                          d->opix, d->ow, nullptr, ekey, eval, eoff)));
+    }
     COMAP_LAUNCH_CHECK(ctx);
     // ---- 4. pixel-major transpose (stable: offset order within a pixel)
     COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(cub_tmp, sort_tb, ekey, ekey2, eval, eval2, (int)d->nnz, 0,
@@ -1226,23 +1359,13 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     k_rowptr<<<grid_for(npix + 1), 256, 0, st>>>(ekey2, d->nnz, npix, d->prow);
     COMAP_LAUNCH_CHECK(ctx);
     COMAP_NB_SWITCH(nb, k_pixel_entries<NB><<<grid_for(d->nnz, 8192), 256, 0, st>>>(eval2, d->prow + npix, eoff, d->ow,
-                                                                                     d->poff, d->pw));
+                                                                                     d->ocnt, d->poff, d->pw, d->pcnt));
     COMAP_LAUNCH_CHECK(ctx);
     k_hit_flags<<<grid_for(npix), 256, 0, st>>>(d->prow, npix, hflag);
     COMAP_LAUNCH_CHECK(ctx);
     COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(cub_tmp, scan32_tb, hflag, hpos, (int)npix, st));
     k_hit_rows<<<grid_for(npix), 256, 0, st>>>(d->prow, hflag, hpos, npix, d->hrow, d->hprow, counts);
     COMAP_LAUNCH_CHECK(ctx);
-    {
-        const char *bm = getenv("COMAP_DS_BIN");
-        if (bm && !strcmp(bm, "lds")) {
-            const char *tp = getenv("COMAP_DS_TILE");
-            d->bin_mode = 1;
-            d->bin_tile = tp ? std::max(32, std::min(4096, atoi(tp))) : 256;
-            if (dalloc(ctx, &d->ppix, d->nnz)) return -2;
-            COMAP_CHECK(ctx, hipMemcpyAsync(d->ppix, ekey2, 4 * (size_t)d->nnz, hipMemcpyDeviceToDevice, st));
-        }
-    }
     // ---- 5. sample-level maps (binValues order)
     COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(cub_tmp, sort_tb, skey, skey2, sval, sval2, (int)N, 0, end_bit,
                                                         st));
@@ -1273,7 +1396,7 @@ extern "C" int comap_destripe_destroy(comap_destriper *d)
     COMAP_DEVICE_GUARD(d->ctx);
     if (d->cs) (void)hipStreamSynchronize(d->cs);
     void *b[] = {d->orow, d->opix, d->ow, d->ws, d->tw, d->prow, d->poff, d->pw, d->h, d->hits, d->nnum, d->part, d->scal,
-                 d->cg, d->flags, d->hrow, d->hprow, d->perm, d->ppix};
+                 d->cg, d->flags, d->hrow, d->hprow, d->perm, d->ocnt, d->pcnt, d->wbar, d->pt};
     for (void *p : b)
         if (p) (void)hipFree(p);
     if (d->flags_host) (void)hipHostFree(d->flags_host);
@@ -1287,6 +1410,11 @@ extern "C" int comap_destripe_destroy(comap_destriper *d)
 
 extern "C" int64_t comap_destripe_n_offsets(const comap_destriper *d) { return d ? d->NO : -1; }
 extern "C" int32_t comap_destripe_n_bands(const comap_destriper *d) { return d ? d->nb : -1; }
+
+extern "C" int32_t comap_destripe_entry_bytes(const comap_destriper *d)
+{
+    return d ? (d->cf ? 4 + d->nb : 4 + 8 * d->nb) : -1;
+}
 
 extern "C" int comap_destripe_nnz(const comap_destriper *d, int64_t *nnz_offset_major, int64_t *nnz_pixel_major)
 {
@@ -1504,7 +1632,8 @@ static void enqueue_iteration(comap_destriper *d, hipStream_t st)
     double *x = d->cg, *r = x + n, *p = r + n, *q = p + n, *num = q + n;
     const int32_t *flags = d->flags;
     // the bin writes the map m = (W p) / h itself, so the projection gathers one array
-    launch_bin(d, st, p, nullptr, d->h, num, flags, true);   // empty rows of num stay 0
+    // (count form: it bins pt = wbar o p, which the previous direction kernel wrote)
+    launch_bin(d, st, d->cf ? d->pt : p, nullptr, d->h, num, flags, true, d->cf);   // empty rows of num stay 0
     // 4 launches per iteration: the p.q / r.r finals and the stop test are folded into
     // the update and direction kernels (same arithmetic and order as k_dot_final + k_cg_check)
     const unsigned pg = launch_project(d, st, p, num, nullptr, q, d->part, flags);
@@ -1512,9 +1641,9 @@ static void enqueue_iteration(comap_destriper *d, hipStream_t st)
     COMAP_NB_SWITCH(d->nb,
                     k_cg_update_fused<NB><<<upd_grid(d->NO), 256, 0, st>>>(d->scal, d->part, (int)pg, x, r, p, q,
                                                                            d->NO, part_rr, flags);
-                    k_cg_direction_fused<NB><<<grid_for(d->NO, kDirBlocks), 256, 0, st>>>(d->scal, part_rr,
-                                                                                          (int)upd_grid(d->NO), p, r,
-                                                                                          d->NO, d->flags));
+                    k_cg_direction_fused<NB><<<grid_for(d->NO, kDirBlocks), 256, 0, st>>>(
+                        d->scal, part_rr, (int)upd_grid(d->NO), p, r, d->NO, d->flags, kPartMax,
+                        d->cf ? d->wbar : nullptr, d->cf ? d->pt : nullptr));
 }
 
 // CG state, stream and the kCgBatch-iteration graph, created on first use.
@@ -1568,6 +1697,10 @@ extern "C" int comap_destripe_solve(comap_destriper *d, double threshold, int32_
     launch_project(d, st, nullptr, d->nnum, d->h, r, nullptr, nullptr);
     COMAP_LAUNCH_CHECK(ctx);
     COMAP_CHECK(ctx, hipMemcpyAsync(p, r, 8 * n, hipMemcpyDeviceToDevice, st));
+    if (d->cf) {   // the first bin's input pt = wbar o p (later ones come from the direction kernel)
+        COMAP_NB_SWITCH(nb, k_scale<NB><<<grid_for(d->NO), 256, 0, st>>>(d->wbar, p, d->NO, d->pt, nullptr));
+        COMAP_LAUNCH_CHECK(ctx);
+    }
     if ((rc = dot(d, st, r, r, d->scal, nullptr))) return rc;
     COMAP_CHECK(ctx, hipMemcpyAsync(d->scal + nb, d->scal, 8 * nb, hipMemcpyDeviceToDevice, st));
     COMAP_CHECK(ctx, hipMemcpyAsync(d->scal + 3 * nb, d->scal, 8 * nb, hipMemcpyDeviceToDevice, st));   // current rr

@@ -216,8 +216,10 @@ def read_comap_data_bands(filelist, map_info, bands=(0, 1, 2, 3), use_gain_filte
                           calibrator, device, healpix)
     cut, keep = prep.cut_flat(flat, len(bands), offset_length)
     del flat
+    mark = prep._Phases(torch, cut.tod.device)
     pointing = cut.pix.to(torch.int64)
     remapping_array = find_unique_values(torch.unique(pointing).cpu().numpy()).astype(int)
+    mark('unique')
     if healpix:      # COMAPData.py:572-573: pixel ids -> positions in the union over ranks
         ra_sorted = torch.as_tensor(np.sort(remapping_array), device=pointing.device)
         order = torch.as_tensor(np.argsort(remapping_array), device=pointing.device)
@@ -227,4 +229,5 @@ def read_comap_data_bands(filelist, map_info, bands=(0, 1, 2, 3), use_gain_filte
     if not device_outputs:
         out = {k: v.cpu().numpy() for k, v in out.items()}
     out['remapping_array'] = remapping_array
+    mark('outputs')
     return out

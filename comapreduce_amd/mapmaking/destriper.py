@@ -313,6 +313,10 @@ class DeviceOps:
         N.lib().comap_destripe_nnz(self.h, ctypes.byref(a), ctypes.byref(b))
         return int(a.value), int(b.value)
 
+    def entry_bytes(self):
+        """Bytes per operator entry: 4 + NB (count form) or 4 + 8 NB."""
+        return int(N.lib().comap_destripe_entry_bytes(self.h))
+
     # ---- vector helpers
     def zeros(self, n):
         return self.torch.zeros(n, dtype=self.torch.float64, device=self.dev)
@@ -479,6 +483,9 @@ class DeviceDestriper:
 
     def nnz(self):
         return self.ops.nnz()
+
+    def entry_bytes(self):
+        return self.ops.entry_bytes()
 
     def solve(self, threshold=1e-6, niter=100):
         d = _dist()

@@ -28,6 +28,28 @@ MEDFILT_STEP = 400
 CALIBRATORS = ('TauA', 'CasA', 'CygA', 'jupiter')
 P = ctypes.c_void_p
 
+# COMAP_PREP_PROFILE=1: device-synchronised wall time per prep phase (seconds) of the
+# last call, in ``last_phases`` (a measurement aid: the syncs cost a little)
+last_phases = {}
+
+
+class _Phases:
+    def __init__(self, torch, dev):
+        self.on = os.environ.get('COMAP_PREP_PROFILE') == '1'
+        self.torch, self.dev = torch, dev
+        if self.on:
+            import time
+            self.clock = time.perf_counter
+            torch.cuda.synchronize(dev)
+            self.t = self.clock()
+
+    def __call__(self, name):
+        if self.on:
+            self.torch.cuda.synchronize(self.dev)
+            now = self.clock()
+            last_phases[name] = last_phases.get(name, 0.0) + now - self.t
+            self.t = now
+
 
 class PrepFile(ctypes.Structure):
     """comap_prep_file (include/comap_hip.h)."""
@@ -102,8 +124,11 @@ def prep_flat(files, filelist, map_info, bands, use_gain_filter, offset_length, 
     nb = len(bands)
     if not 1 <= nb <= 4:
         raise ValueError('1 to 4 bands per prep call')
+    last_phases.clear()
+    mark = _Phases(torch, dev)
     sizes = [countDataSize(f, len(feeds), L) for f in files]
     out = FlatArrays(torch, dev, nb, sum(i['N'] for i in sizes))
+    mark('alloc')
     wcs = None if healpix else wcs_struct(map_info)
     segs = []
     keep_alive = []
@@ -127,6 +152,7 @@ def prep_flat(files, filelist, map_info, bands, use_gain_filter, offset_length, 
         dname = 'averaged_tod/tod' if (use_gain_filter and not calib) else 'averaged_tod/tod_original'
         tod = _dev(torch, f[dname], dev, torch.float64)
         F, B, T = tod.shape
+        mark('file_tod')
         bad = f.attrs('comap')['bad_observation']
         if calibration:
             cal = np.zeros((20, 4))
@@ -161,8 +187,10 @@ def prep_flat(files, filelist, map_info, bands, use_gain_filter, offset_length, 
         rms_scale = np.array([row_cal[r, k] for r in live for k in range(nb)], dtype=np.float64)
         rms = torch.empty(max(1, rms_rows.size), dtype=torch.float64, device=dev)
         rr, rs = _dev_np(torch, rms_rows, dev), _dev_np(torch, rms_scale, dev)
+        mark('file_meta')
         N.check(lib.comap_prep_auto_rms(c, N.dptr(tod), T, N.dptr(rr), N.dptr(rs), int(rms_rows.size), T,
                                         N.dptr(rms)), c, 'comap_prep_auto_rms')
+        mark('auto_rms')
         row_w = torch.ones((nrow, 4), dtype=torch.float64, device=dev)
         if live.size:
             row_w[torch.as_tensor(live, device=dev), :nb] = (1.0 / (rms * rms)).reshape(live.size, nb)
@@ -174,6 +202,7 @@ def prep_flat(files, filelist, map_info, bands, use_gain_filter, offset_length, 
         row_pct = torch.zeros((nrow, 4), dtype=torch.float64, device=dev)
         if live.size:
             row_pct[torch.as_tensor(live, device=dev)] = pct[:live.size]
+        mark('percentiles')
         colstart = np.concatenate(([0], np.cumsum(lens)[:-1])).astype(np.int64)
         scans = np.stack([edges[:, 0], np.asarray(lens, np.int64), colstart], axis=1).astype(np.int64)
         if scans.shape[0] > 64:
@@ -193,8 +222,10 @@ def prep_flat(files, filelist, map_info, bands, use_gain_filter, offset_length, 
                       N.dptr(row_pct), bands4, nb, (ctypes.c_double * 9)(*np.asarray(rot).ravel()), obsid,
                       None if pixels is None else N.dptr(pixels))
         o = out.struct(last)
+        mark('gather_tables')
         N.check(lib.comap_prep_gather(c, ctypes.byref(pf), None if wcs is None else ctypes.byref(wcs),
                                       ctypes.byref(o)), c, 'comap_prep_gather')
+        mark('gather')
         keep_alive.append((tod, az, el, ra, dec, spike_d, rr, rs, rms, row_w, pct, pr, row_pct, pixels, dsc, drs,
                            dps, drf, drc))
         if not calib:      # high-pass of each scan's non-zero samples (COMAPData.py:353-360)
@@ -205,11 +236,13 @@ def prep_flat(files, filelist, map_info, bands, use_gain_filter, offset_length, 
                     for k in range(nb):
                         segs.append((k * out.n + last + r * ds + cs, nl))
         last += nrow * ds
+    mark('segments')
     if segs:
         sd = _dev_np(torch, np.asarray(segs, dtype=np.int64), dev)
         N.check(lib.comap_prep_highpass(c, N.dptr(out.tod), N.dptr(sd), len(segs), MEDFILT_STEP), c,
                 'comap_prep_highpass')
     torch.cuda.current_stream(dev).synchronize()
+    mark('highpass')
     del keep_alive
     return out
 
@@ -226,7 +259,9 @@ def cut_flat(flat, nb, offset_length, device=None):
     out = FlatArrays(torch, dev, nb, flat.n)
     cap = flat.n // L
     keep = torch.zeros((nb, max(cap, 1)), dtype=torch.uint8, device=dev)
+    mark = _Phases(torch, dev)
     nk = ctypes.c_int64(0)
+    mark('cut_alloc')
     N.check(N.lib().comap_prep_cut(c, ctypes.byref(flat.struct()), nb, flat.n, L, ctypes.byref(out.struct()),
                                    N.dptr(keep), max(cap, 1), ctypes.byref(nk)), c, 'comap_prep_cut')
     n = int(nk.value) * L
@@ -234,6 +269,7 @@ def cut_flat(flat, nb, offset_length, device=None):
     cut.tod, cut.w = out.tod[:, :n], out.w[:, :n]
     cut.az, cut.el, cut.ra, cut.dec = out.az[:n], out.el[:n], out.ra[:n], out.dec[:n]
     cut.feedid, cut.obsid, cut.pix, cut.n = out.feedid[:n], out.obsid[:n], out.pix[:n], n
+    mark('cut')
     return cut, keep[:, :int(nk.value)]
 
 

@@ -219,6 +219,10 @@ int32_t comap_destripe_n_bands(const comap_destriper *d);
 /* x_out [N/L][NB] (caller's offset order) from x_internal (internal order); x_out != x_internal */
 int comap_destripe_offsets_natural(comap_destriper *d, const double *x_internal_dev, double *x_out_dev);
 int comap_destripe_nnz(const comap_destriper *d, int64_t *nnz_offset_major, int64_t *nnz_pixel_major);
+/* Bytes one sparse-operator entry holds: 4 + n_bands (count form: every offset's
+ * non-zero weights per band are one value, so an entry keeps uint8 sample counts;
+ * COMAP_DS_CF=0 disables it) or 4 + 8 n_bands (f64 weight sums). */
+int32_t comap_destripe_entry_bytes(const comap_destriper *d);
 /* Local (this rank) sample-level maps, summed in binValues order:
  * h = sum w, hits = sum 1, naive_num = sum w tod (any may be NULL). */
 int comap_destripe_local_maps(comap_destriper *d, double *h_dev, double *hits_dev, double *naive_num_dev);

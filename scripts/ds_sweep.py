@@ -1,0 +1,65 @@
+"""Launch-shape sweep of the destriper CG kernels at C5 (one process): the same
+synthetic problem (bench.destriper_c5_leg's inputs) solved for a fixed number of
+iterations under each COMAP_DS_* setting (read when a problem is created); prints
+one JSON line per (bands, setting) with ms per iteration and the iterate's checksum
+(so a variant that changes the answer beyond rounding shows).
+    python scripts/ds_sweep.py [n_obs] [iters] [bands ...]"""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+SETTINGS = [
+    {},
+    {'COMAP_DS_PG': '8'},
+    {'COMAP_DS_PG': '8', 'COMAP_DS_PU': '8'},
+    {'COMAP_DS_PG': '4', 'COMAP_DS_PU': '8'},
+    {'COMAP_DS_PB': '2048'},
+    {'COMAP_DS_PG': '8', 'COMAP_DS_PB': '2048'},
+    {'COMAP_DS_BU': '8'},
+    {'COMAP_DS_BL': '32'},
+    {'COMAP_DS_BL': '64'},
+    {'COMAP_DS_BL': '32', 'COMAP_DS_BU': '8'},
+    {'COMAP_DS_BL': '8', 'COMAP_DS_BU': '8'},
+]
+KEYS = ('COMAP_DS_PG', 'COMAP_DS_PU', 'COMAP_DS_PB', 'COMAP_DS_BU', 'COMAP_DS_BL')
+
+
+def main():
+    import torch
+    from comapreduce_amd import synthetic
+    from comapreduce_amd.mapmaking import destriper as D
+    n_obs = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    iters = int(sys.argv[2]) if len(sys.argv) > 2 else 40
+    bands = [int(b) for b in sys.argv[3:]] or [1, 4]
+    torch.cuda.set_device(0)
+    for nb in bands:
+        pix, tod, w = synthetic.destriper_inputs_device(n_obs, offset_length=50, device=0, seed=1000, n_bands=nb)
+        for st in SETTINGS:
+            for k in KEYS:
+                os.environ.pop(k, None)
+            os.environ.update(st)
+            prob = D.DeviceDestriper(pix, tod, w, 50, 480 * 480, device=0)
+            prob.solve(threshold=0.0, niter=3)
+            best = None
+            for _ in range(2):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                res = prob.solve(threshold=0.0, niter=iters)
+                torch.cuda.synchronize()
+                dt = (time.perf_counter() - t0) / iters * 1e3
+                best = dt if best is None else min(best, dt)
+            x = res['x']
+            print(json.dumps({'bands': nb, 'setting': st, 'ms_per_iter': best,
+                              'x_sum': float(x.double().sum()), 'x_abs': float(x.double().abs().sum())}), flush=True)
+            del prob, res
+        for k in KEYS:
+            os.environ.pop(k, None)
+        del pix, tod, w
+        torch.cuda.empty_cache()
+
+
+if __name__ == '__main__':
+    main()

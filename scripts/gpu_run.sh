@@ -7,6 +7,9 @@
 #         prof[=BENCH_ARGS]     rocprofv3 kernel trace + stats of bench.py
 #         pmc=COUNTERS[@BENCH_ARGS]  one rocprofv3 --pmc pass
 #         smoke                 __graft_entry__.smoke()
+#         py=SCRIPT ARGS        python3 SCRIPT ARGS (log gpurun_out/TAG_py<step>.log)
+#         dsprof[=ARGS]         rocprofv3 kernel trace + stats of scripts/ds_c5.py (default: 8 obs, 4 bands, 50 it)
+#         dspmc=COUNTERS[@ARGS] one rocprofv3 --pmc pass over scripts/ds_c5.py
 TAG=$1; shift
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -24,6 +27,13 @@ for step in "$@"; do
            d=gpurun_out/${TAG}_pmc_$(echo $cnt | tr ' ' '_' | cut -c1-40)
            timeout -s KILL 300 rocprofv3 --pmc $cnt --output-format csv -d $d -o run -- python3 bench.py $bargs \
              > $d.log 2>&1 ;;
+    dsprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_dstrace -o run \
+             -- python3 scripts/ds_c5.py ${arg:-8 4 50} > gpurun_out/${TAG}_dsprof.log 2>&1 ;;
+    dspmc) cnt=${arg%%@*}; dargs=${arg#*@}; [ "$dargs" = "$arg" ] && dargs="8 4 20"
+           d=gpurun_out/${TAG}_dspmc_$(echo $cnt | tr ' ' '_' | cut -c1-40)
+           timeout -s KILL 240 rocprofv3 --pmc $cnt --output-format csv -d $d -o run -- python3 scripts/ds_c5.py $dargs \
+             > $d.log 2>&1 ;;
+    py)    timeout -k 10 300 python3 -u $arg > gpurun_out/${TAG}_py${NSTEP}.log 2>&1 ;;
     smoke) timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/${TAG}_smoke.log 2>&1 ;;
     *) echo "unknown step $name"; exit 2 ;;
   esac

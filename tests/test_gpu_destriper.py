@@ -330,19 +330,28 @@ def test_graph_driver_captures_rccl_allreduce():
     assert itg == itb and same
 
 
-@pytest.mark.parametrize('tile,nb', [('256', 1), ('128', 4), ('1024', 2)])
-def test_lds_scatter_bin_variant_vs_oracle(tile, nb, monkeypatch):
-    """The LDS-privatised scatter-add bin (COMAP_DS_BIN=lds, the measured alternative to
-    the pixel-major gather) against the oracle: the same solve to 1e-9 (its add order
-    within a pixel is not fixed)."""
+@pytest.mark.parametrize('form,nb', [('count', 1), ('count', 4), ('count', 2), ('full', 1), ('full', 4),
+                                     ('nonuniform', 1), ('nonuniform', 4)])
+def test_entry_forms_vs_oracle(form, nb, monkeypatch):
+    """The operator's two entry forms against the oracle: the count form (uint8
+    non-zero-sample counts per band, s_e = wbar_o c_e; chosen when every offset's
+    non-zero weights are one value per band, as COMAP's per-(feed, band) weights with
+    zeroed cuts are), the f64 weight sums (COMAP_DS_CF=0), and weights that vary inside
+    an offset (the set-up falls back to the f64 form by itself).  Same solve to 1e-9,
+    weight / hits bit-exact, the same iteration counts."""
     import oracle.destriper as od
     from comapreduce_amd.mapmaking.destriper import DeviceDestriper
-    monkeypatch.setenv('COMAP_DS_BIN', 'lds')
-    monkeypatch.setenv('COMAP_DS_TILE', tile)
+    if form == 'full':
+        monkeypatch.setenv('COMAP_DS_CF', '0')
     p, tods, ws, keep = _bands_problem(max(nb, 2))
     tods, ws, keep = tods[:nb], ws[:nb], keep[:nb]
+    if form == 'nonuniform':
+        ws = ws * np.random.default_rng(5).uniform(0.5, 2.0, ws.shape)
+    want_bytes = 4 + nb if form == 'count' else 4 + 8 * nb
     if nb == 1:
-        res = DeviceDestriper(p, tods[0], ws[0], L, NPIX).solve(1e-6, 100)
+        dd = DeviceDestriper(p, tods[0], ws[0], L, NPIX)
+        assert dd.entry_bytes() == want_bytes
+        res = dd.solve(1e-6, 100)
         ref, xr, itr = od.destriper_iteration(p, tods[0], ws[0], L, NPIX, threshold=1e-6, niter=100)
         assert res['iters'] == itr
         assert rel(res['x'].cpu().numpy(), xr) < 1e-9
@@ -350,11 +359,14 @@ def test_lds_scatter_bin_variant_vs_oracle(tile, nb, monkeypatch):
         assert np.array_equal(m['weight'], ref['weight']) and np.array_equal(m['hits'], ref['hits'])
         assert rel(m['map'], ref['map']) < 1e-9
         return
-    res = DeviceDestriper(p, tods, ws, L, NPIX, keep=keep).solve(1e-6, 100)
+    dd = DeviceDestriper(p, tods, ws, L, NPIX, keep=keep)
+    assert dd.entry_bytes() == want_bytes
+    res = dd.solve(1e-6, 100)
     for b in range(nb):
         sel = np.repeat(keep[b], L)
         ref, xr, itr = od.destriper_iteration(p[sel], tods[b][sel], ws[b][sel], L, NPIX, threshold=1e-6, niter=100)
         assert res['iters'][b] == itr
         m = {k: v[b].cpu().numpy() for k, v in res['maps'].items()}
+        assert np.array_equal(m['weight'], ref['weight']) and np.array_equal(m['hits'], ref['hits'])
         assert rel(m['map'], ref['map']) < 1e-9, b
         assert rel(res['x'][b].cpu().numpy()[keep[b]], xr) < 1e-9, b
