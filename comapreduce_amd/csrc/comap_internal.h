@@ -50,25 +50,40 @@ struct DeviceGuard {
 // Device buffers owned by one call: freed on every return path (error returns
 // included).  With a stream, the destructor first waits for the work queued on
 // it (kernels may still read the buffers).
+// Process-wide stream-ordered pool for the current device's temporaries (created on
+// first use, release threshold unbounded): hipMallocFromPoolAsync / hipFreeAsync then
+// reuse cached memory instead of mapping and unmapping hundreds of MB per call
+// (the prep high-pass lost 1.8 ms per call to that, r03h).
+hipMemPool_t comap_tmp_pool();
+// Temporaries through a host-side cache of freed blocks (power-of-two size classes per
+// device) in front of that pool: a free is a list push, an allocation of a cached class a
+// list pop -- no HIP call.  hipFreeAsync of a median plan's 12 buffers still cost
+// 0.75-0.8 ms of host time per prep call (r03j).  Blocks are handed out again in stream
+// order: every user allocates and frees on one stream, or frees after a sync.
+hipError_t comap_tmp_alloc(void **p, size_t bytes, hipStream_t st);
+void comap_tmp_free(void *p);
+
 struct DevTemps {
     std::vector<void *> p;
     hipStream_t st = nullptr;
     explicit DevTemps(hipStream_t s = nullptr) : st(s) {}
     DevTemps(const DevTemps &) = delete;
     DevTemps &operator=(const DevTemps &) = delete;
+    // stream-ordered pool allocations (the context keeps the device pool's memory cached,
+    // comap_ctx_create): no page mapping per call; freed after the stream sync
     template <typename T>
     hipError_t alloc(T **out, size_t n)
     {
         void *q = nullptr;
-        const hipError_t e = hipMalloc(&q, sizeof(T) * (n ? n : 1));
+        const hipError_t e = comap_tmp_alloc(&q, sizeof(T) * (n ? n : 1), st);
         if (e == hipSuccess) p.push_back(q);
         *out = (T *)q;
         return e;
     }
     ~DevTemps()
     {
-        if (!p.empty() && st) (void)hipStreamSynchronize(st);
-        for (void *q : p) (void)hipFree(q);
+        if (!p.empty()) (void)hipStreamSynchronize(st);
+        for (void *q : p) comap_tmp_free(q);
     }
 };
 
@@ -138,6 +153,7 @@ struct MedPlan {
     void *krange = nullptr;      // dev [njobs][2] u64: per-series key min, max (proxy scaling)
     void *temp = nullptr;
     size_t temp_bytes = 0;
+    hipStream_t alloc_stream = nullptr;   // its buffers come from the device pool on this stream
 };
 
 int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jobs, int32_t w);
@@ -160,6 +176,10 @@ struct comap_l1_plan {
     // 4 KB row runs start on 128-B boundaries (the few samples before the scan are read
     // from the same row and never written out)
     int32_t *tiles_b = nullptr;        // dev [NTB][2] (unit, t_off)
+    // samples of each feed that no unit of this plan covers (scan gaps, and in a C3 shard
+    // the other ranks' units): (feed, t0, n); comap_l1_average zeroes the outputs there
+    int64_t *gaps = nullptr;           // dev [NG][3]
+    int64_t n_gaps = 0, max_gap = 0;
     // pass B -> median -> pass C software pipeline over unit groups (comap_l1_average):
     // group g = units [grp_u0[g], grp_u0[g+1]) = tiles [grp_tile0[g], grp_tile0[g+1]);
     // its sliding medians (one job per (unit, band)) run on the side stream

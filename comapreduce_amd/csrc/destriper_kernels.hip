@@ -74,6 +74,10 @@ struct comap_destriper {
     int proj_lanes = 0;        // lanes per offset row (0: by L)
     int proj_u = 4;            // entry loads in flight per projection lane
     int64_t proj_blocks = 1024;   // projection grid cap (its p.q partials are re-summed by every update block)
+    // comap_destripe_solve replays a captured graph of kCgBatch iterations only for small
+    // problems, whose 4 kernels per iteration run shorter than their host enqueue; larger
+    // ones enqueue eagerly (no capture: 0.4 ms at C4 that no replay won back)
+    int cg_graph = -1;          // -1: by size (COMAP_DS_CGGRAPH=0 / 1 overrides)
     uint8_t *ocnt = nullptr;   // [nnz][nb]
     uint8_t *pcnt = nullptr;   // [nnzp][nb]
     double *wbar = nullptr;    // [NO][nb]
@@ -170,6 +174,33 @@ __device__ __forceinline__ void ld_coef(const void *__restrict__ base, int64_t k
         ldb<NB>(reinterpret_cast<const double *>(base) + k * NB, a);
     }
 }
+
+// One entry's coefficients held in registers between its load and its use (the bin's
+// software pipeline): the count form keeps the packed uint8 counts (one dword for up to
+// 4 bands), the full form the NB doubles.
+template <int NB, bool CF>
+struct Coef;
+template <int NB>
+struct Coef<NB, true> {
+    uint32_t v = 0;
+    __device__ __forceinline__ void load(const void *__restrict__ base, int64_t k)
+    {
+        const uint8_t *c = reinterpret_cast<const uint8_t *>(base) + k * NB;
+        if constexpr (NB == 4) v = *reinterpret_cast<const uint32_t *>(c);
+        else if constexpr (NB == 2) v = *reinterpret_cast<const uint16_t *>(c);
+        else v = c[0];
+    }
+    __device__ __forceinline__ double get(int b) const { return (double)((v >> (8 * b)) & 0xffu); }
+};
+template <int NB>
+struct Coef<NB, false> {
+    double v[NB] = {};
+    __device__ __forceinline__ void load(const void *__restrict__ base, int64_t k)
+    {
+        ldb<NB>(reinterpret_cast<const double *>(base) + k * NB, v);
+    }
+    __device__ __forceinline__ double get(int b) const { return v[b]; }
+};
 
 // XCD-aware block order (bijective for any grid): blocks b and b + 8 share an XCD
 // (MI355X_MICROARCH.md, workgroup dispatch), so logical block ids are dealt to the 8
@@ -685,28 +716,39 @@ __global__ void __launch_bounds__(256) k_ds_bin(const int64_t *__restrict__ prow
 #pragma unroll
         for (int b = 0; b < NB; ++b) s[b] = 0.0;
         const int64_t e1 = prow[i + 1];
-        for (int64_t k = prow[i] + sub; k < e1; k += kBinLanes * kBinU) {
-            int32_t o[kBinU];
-            double a[kBinU][NB], xv[kBinU][NB];
+        // software pipeline: the next group's entry loads are issued before this group's
+        // x gathers are consumed, so a lane has one dependent latency per group, not two
+        int64_t k = prow[i] + sub;
+        int32_t o[kBinU];
+        Coef<NB, CF> a[kBinU];
 #pragma unroll
-            for (int u = 0; u < kBinU; ++u) {
-                const bool in = k + u * kBinLanes < e1;
-                o[u] = in ? poff[k + u * kBinLanes] : 0;
-                if (in) {
-                    ld_coef<NB, CF>(pw, k + u * kBinLanes, a[u]);
-                } else {
-#pragma unroll
-                    for (int b = 0; b < NB; ++b) a[u][b] = 0.0;
-                }
-            }
+        for (int u = 0; u < kBinU; ++u) {
+            const bool in = k + u * kBinLanes < e1;
+            o[u] = in ? poff[k + u * kBinLanes] : 0;
+            if (in) a[u].load(pw, k + u * kBinLanes);
+        }
+        while (k < e1) {
+            double xv[kBinU][NB];
 #pragma unroll
             for (int u = 0; u < kBinU; ++u) ldb<NB>(x + (int64_t)o[u] * NB, xv[u]);
+            const int64_t kn = k + kBinLanes * kBinU;
+            int32_t on[kBinU];
+            Coef<NB, CF> an[kBinU];
+#pragma unroll
+            for (int u = 0; u < kBinU; ++u) {
+                const bool in = kn + u * kBinLanes < e1;
+                on[u] = in ? poff[kn + u * kBinLanes] : 0;
+                if (in) an[u].load(pw, kn + u * kBinLanes);
+            }
 #pragma unroll
             for (int u = 0; u < kBinU; ++u)
                 if (k + u * kBinLanes < e1) {
 #pragma unroll
-                    for (int b = 0; b < NB; ++b) s[b] = fma(a[u][b], xv[u][b], s[b]);
+                    for (int b = 0; b < NB; ++b) s[b] = fma(a[u].get(b), xv[u][b], s[b]);
                 }
+#pragma unroll
+            for (int u = 0; u < kBinU; ++u) { o[u] = on[u]; a[u] = an[u]; }
+            k = kn;
         }
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
@@ -1120,10 +1162,17 @@ void launch_bin(const comap_destriper *d, hipStream_t st, const double *x, const
     }
 }
 
+// lanes per offset row: the fewest whose one pass of kProjU loads covers the mean row
+// (C5: 28 entries per offset -> 8 lanes, 32 offsets per block sweep; C4: 14 -> 4).
+// Measured at C5 (r03e, ms per CG iteration, 1 / 4 bands): 16 lanes 0.152 / 0.347,
+// 8 lanes 0.132 / 0.307; 8 loads per lane or a 2048-block grid: within noise or slower.
 inline int project_lanes(const comap_destriper *d)
 {
     if (d->proj_lanes) return d->proj_lanes;
-    return d->L <= 64 ? 16 : (d->L <= 128 ? 32 : 64);
+    const int64_t mean = d->NO ? (d->nnz + d->NO - 1) / d->NO : 0;
+    int g = 4;
+    while (g < 64 && g * d->proj_u < mean) g *= 2;
+    return g;
 }
 inline unsigned project_grid(const comap_destriper *d, int64_t cap)
 {
@@ -1273,14 +1322,14 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
              Arena::bytes<double>((size_t)N * 2 * NB) + Arena::bytes<int64_t>(npix + 1) +
              2 * Arena::bytes<int32_t>(npix) + Arena::bytes<int64_t>(2) + Arena::bytes<int32_t>(N) +
              Arena::bytes<int32_t>(1);
-    COMAP_CHECK(ctx, hipMalloc((void **)&ar.base, ar.cap));
+    COMAP_CHECK(ctx, comap_tmp_alloc((void **)&ar.base, ar.cap, st));
     struct ArenaFree {
         Arena *a;
         hipStream_t s;
         ~ArenaFree()
         {
             (void)hipStreamSynchronize(s);
-            (void)hipFree(a->base);
+            comap_tmp_free(a->base);
         }
     } arena_free{&ar, st};
     char *cub_tmp = ar.take<char>(cub_tb);
@@ -1331,6 +1380,7 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         d->proj_lanes = env_int("COMAP_DS_PG", 0, {4, 8, 16, 32, 64});
         d->proj_u = env_int("COMAP_DS_PU", 4, {4, 8});
         d->proj_blocks = env_int("COMAP_DS_PB", kProjBlocks, {256, 512, 1024, 2048, 4096, 8192});
+        d->cg_graph = env_int("COMAP_DS_CGGRAPH", -1, {0, 1});
     }
     rc |= dalloc(ctx, &d->opix, d->nnz);
     rc |= dalloc(ctx, &d->poff, d->nnz);          // nnzp <= nnz (off-map entries are not binned)
@@ -1646,10 +1696,19 @@ static void enqueue_iteration(comap_destriper *d, hipStream_t st)
                         d->cf ? d->wbar : nullptr, d->cf ? d->pt : nullptr));
 }
 
-// CG state, stream and the kCgBatch-iteration graph, created on first use.
+// graph replay pays when an iteration's kernels are shorter than enqueueing them
+// (~20 us of host time for 4 launches): below ~300k entries (C4's 4-band iteration of
+// 0.5 M entries already runs 34 us)
+static bool cg_use_graph(const comap_destriper *d)
+{
+    if (d->cg_graph >= 0) return d->cg_graph == 1;
+    return d->nnz + d->nnzp < 300000;
+}
+
+// CG state, stream and (small problems) the kCgBatch-iteration graph, created on first use.
 static int cg_setup(comap_destriper *d)
 {
-    if (d->batch) return 0;
+    if (d->batch || (d->cs && !cg_use_graph(d))) return 0;
     comap_ctx *ctx = d->ctx;
     const size_t nb = (size_t)d->nb;
     if (!d->cg && (dalloc(ctx, &d->cg, (4 * (size_t)d->NO + (size_t)d->npix) * nb) ||
@@ -1659,6 +1718,7 @@ static int cg_setup(comap_destriper *d)
     if (!d->thr_host) COMAP_CHECK(ctx, hipHostMalloc((void **)&d->thr_host, 8, hipHostMallocDefault));
     if (!d->cs) COMAP_CHECK(ctx, hipStreamCreateWithFlags(&d->cs, hipStreamNonBlocking));
     if (!d->ev) COMAP_CHECK(ctx, hipEventCreateWithFlags(&d->ev, hipEventDisableTiming));
+    if (!cg_use_graph(d)) return 0;
     hipGraph_t g = nullptr;
     COMAP_CHECK(ctx, hipStreamBeginCapture(d->cs, hipStreamCaptureModeThreadLocal));
     for (int i = 0; i < kCgBatch; ++i) enqueue_iteration(d, d->cs);
@@ -1707,7 +1767,7 @@ extern "C" int comap_destripe_solve(comap_destriper *d, double threshold, int32_
     for (int i = 0; i < 2 + 2 * nb; ++i) d->flags_host[i] = 0;
     for (int enq = 0; enq < niter;) {
         const int k = std::min(kCgBatch, niter - enq);
-        if (k == kCgBatch) {
+        if (k == kCgBatch && d->batch) {
             COMAP_CHECK(ctx, hipGraphLaunch(d->batch, st));
         } else {
             for (int i = 0; i < k; ++i) enqueue_iteration(d, st);

@@ -27,10 +27,12 @@
 // Variants measured slower are listed in DESIGN.md §3 (code in git history).
 #include "comap_internal.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
+#include <utility>
 
 using namespace comap;
 
@@ -1108,6 +1110,27 @@ __global__ void __launch_bounds__(256) k_scan_weights(const int32_t *__restrict_
     for (int t = threadIdx.x; t < n; t += blockDim.x) wo[t] = wt;
 }
 
+// ------------------------------------------------------------------ output gaps
+// The Level-2 outputs are 0 wherever no unit of the plan writes (between scans, and a
+// C3 shard's foreign units): zero exactly those samples of every (output, band) instead
+// of clearing the whole [3][F][4][T] buffer first.  gap g = (feed, t0, n); grid.y = gap.
+__global__ void __launch_bounds__(256) k_zero_gaps(const int64_t *__restrict__ gaps, int64_t T, int F,
+                                                   double *__restrict__ tod_out, double *__restrict__ orig_out,
+                                                   double *__restrict__ w_out)
+{
+    const int64_t *g = gaps + 3 * (int64_t)blockIdx.y;
+    const int64_t f = g[0], t0 = g[1], n = g[2];
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+#pragma unroll
+        for (int b = 0; b < kBands; ++b) {
+            const int64_t o = (f * kBands + b) * T + t0 + k;
+            tod_out[o] = 0.0;
+            orig_out[o] = 0.0;
+            w_out[o] = 0.0;
+        }
+    }
+}
+
 // ------------------------------------------------------------------ vane
 // system_temperature_from_tod (VaneCalibration.py:67-82): per channel nanmean
 // over the hot and cold samples of the vane event; one wave per channel row.
@@ -1343,8 +1366,27 @@ extern "C" int comap_l1_plan_create(comap_ctx *ctx, const comap_obs_desc *d, com
         for (int t = -shift; t < p->units_h[4 * u + 3]; t += kTile) { tiles_b.push_back(u); tiles_b.push_back(t); }
         tub[u + 1] = (int64_t)tiles_b.size() / 2;
     }
+    // uncovered samples per feed (the complement of the plan's units)
+    std::vector<int64_t> gaps;
+    {
+        std::vector<std::vector<std::pair<int64_t, int64_t>>> cov(p->F);
+        for (int u = 0; u < p->U; ++u)
+            cov[p->units_h[4 * u]].push_back({p->units_h[4 * u + 2], p->units_h[4 * u + 2] + p->units_h[4 * u + 3]});
+        for (int f = 0; f < p->F; ++f) {
+            std::sort(cov[f].begin(), cov[f].end());
+            int64_t t = 0;
+            for (auto &c : cov[f]) {
+                if (c.first > t) { gaps.push_back(f); gaps.push_back(t); gaps.push_back(c.first - t); }
+                t = std::max(t, c.second);
+            }
+            if (t < p->T) { gaps.push_back(f); gaps.push_back(t); gaps.push_back(p->T - t); }
+        }
+        p->n_gaps = (int64_t)gaps.size() / 3;
+        for (int64_t g = 0; g < p->n_gaps; ++g) p->max_gap = std::max(p->max_gap, gaps[3 * g + 2]);
+    }
     const int64_t UC = (int64_t)p->U * kBC;
     int rc = 0;
+    if (p->n_gaps) rc |= upload(ctx, (void **)&p->gaps, gaps.data(), gaps.size() * 8);
     rc |= dalloc(ctx, &p->flag, 1);
     rc |= dalloc(ctx, &p->dlist, (size_t)p->U * kBC);
     rc |= dalloc(ctx, &p->dcnt, (size_t)p->U * kBands);
@@ -1440,7 +1482,7 @@ extern "C" int comap_l1_plan_destroy(comap_l1_plan *p)
     if (!p) return 0;
     COMAP_DEVICE_GUARD(p->ctx);
     if (p->side) (void)hipStreamSynchronize(p->side);
-    void *bufs[] = {p->units, p->tiles, p->tiles_b, p->airmass, p->unit_sums, p->mom,
+    void *bufs[] = {p->units, p->tiles, p->tiles_b, p->gaps, p->airmass, p->unit_sums, p->mom,
                     p->nan_count, p->alpha, p->nf, p->bsum, p->mb, p->mf, p->ssum, p->sdm, p->gw,
                     p->gmode, p->kap, p->dsum, p->xreg, p->dG, p->rowbad, p->ubs, p->fitsum, p->oa,
                     p->flag, p->dlist, p->dcnt, p->dw, p->nanpos, p->nanpos_n, p->vane_dev};
@@ -1697,6 +1739,11 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
         for (int64_t i = 0; i < UC; ++i) ids[i] = i;
         COMAP_CHECK(ctx, tmp.alloc(&cmed, (size_t)UC));
         if ((rc = unit_row_medians(p, ids, cmed))) return rc;
+    }
+    if (p->n_gaps) {
+        const unsigned gx = (unsigned)std::min<int64_t>(64, (p->max_gap + 255) / 256);
+        k_zero_gaps<<<dim3(gx, (unsigned)p->n_gaps), 256, 0, st>>>(p->gaps, p->T, p->F, tod_out, orig_out, w_out);
+        COMAP_LAUNCH_CHECK(ctx);
     }
     k_gather_oa<<<(UC + 255) / 256, 256, 0, st>>>(p->units, fit, p->F, p->U, cmed, p->oa);
     COMAP_LAUNCH_CHECK(ctx);

@@ -1269,7 +1269,8 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
     mp->nchunks = nchunks;
     mp->nsegs = (int32_t)wsegs.size();
     hipStream_t st = ctx->stream;
-    auto alloc = [&](void **p, size_t b) { return hipMalloc(p, b ? b : 8); };
+    mp->alloc_stream = st;
+    auto alloc = [&](void **p, size_t b) { return comap_tmp_alloc(p, b ? b : 8, st); };
     COMAP_CHECK(ctx, alloc((void **)&mp->jobs, sizeof(MedJob) * jobs.size()));
     COMAP_CHECK(ctx, alloc((void **)&mp->seg, 4 * seg.size()));
     COMAP_CHECK(ctx, alloc((void **)&mp->segs, sizeof(SlideSeg) * wsegs.size()));
@@ -1322,8 +1323,7 @@ void comap_median_plan_free(MedPlan *mp)
 {
     void *b[] = {mp->jobs, mp->seg, mp->k0, mp->k1, mp->v0, mp->v1, mp->rank, mp->temp, mp->segs, mp->redo, mp->krange,
                  mp->slo};
-    for (void *p : b)
-        if (p) (void)hipFree(p);
+    for (void *p : b) comap_tmp_free(p);
     *mp = MedPlan();
 }
 

@@ -27,7 +27,10 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 namespace {
@@ -94,121 +97,161 @@ __device__ double pairwise_tree(int n, Leaf leaf)
     }
 }
 
-// One leaf of pw: values v(lo .. lo + n - 1), n <= 128.
+// rms[r] = nanstd(d) / sqrt(2), d_i = x[1 + i] / s - x[0] / s, i < m = N - 1, N = n // 2 * 2
+// (COMAPData.auto_rms with its tod[:-1:N] slice: COMAPData.py:205-208).  np.nanstd:
+// NaN -> 0, avg = sum / count, (d - avg)^2 with NaN -> 0, var = sum / count; both sums
+// are NumPy's pairwise sums: 0 + pw(b_0) + pw(b_1) + ... over 8192-value buffer blocks.
+// Spread over the chip: one wave per (series, buffer block) computes pw(b_k) -- a full
+// block is a balanced tree of 64 leaves of 128 values (lane l: leaf l, then a butterfly
+// in the tree's pairing); the last, partial block walks pw's recursion -- and a final
+// per-series step adds the block values in order.  PHASE 0 sums d (and counts the
+// non-NaN d); PHASE 1 re-derives avg from the phase-0 block values and sums (d - avg)^2.
+constexpr int kRmsWG = 512;   // one workgroup per (series, buffer block): 64 groups of 8 lanes
+
+// One pw leaf of n values at lo by the 8 lanes of a group (j = lane % 8): lane j sums the
+// values lo + j, lo + j + 8, ... below n - n % 8 (NumPy's accumulator r[j]), the group
+// combines ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)), then the n % 8 tail is added
+// in order; n < 8: a plain sequential sum.  The group's lane 0 holds the result.
 template <typename Val>
-__device__ __forceinline__ double pw_leaf(Val v, int64_t lo, int n)
+__device__ __forceinline__ double pw_leaf8(Val v, int64_t lo, int n, int j)
 {
 #pragma clang fp contract(off)
     if (n < 8) {
         double r = 0.0;
-        for (int i = 0; i < n; ++i) r += v(lo + i);
+        if (j == 0)
+            for (int i = 0; i < n; ++i) r += v(lo + i);
         return r;
     }
-    double r[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = v(lo + j);
-    int i = 8;
     const int n8 = n - n % 8;
-    for (; i < n8; i += 8) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) r[j] += v(lo + i + j);
-    }
-    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-    for (; i < n; ++i) res += v(lo + i);
-    return res;
+    double r = v(lo + j);
+    for (int i = 8; i < n8; i += 8) r += v(lo + i + j);
+    r = r + __shfl_xor(r, 1, 64);
+    r = r + __shfl_xor(r, 2, 64);
+    r = r + __shfl_xor(r, 4, 64);
+    if (j == 0)
+        for (int i = n8; i < n; ++i) r += v(lo + i);
+    return r;
 }
 
-constexpr int kRmsThreads = 256;
-constexpr int kRmsGroup = 16;                                  // buffer blocks per LDS round
-constexpr int kRmsLeafCap = kRmsGroup * (kPwBlock / 64) + 256;   // >= leaves of 16 blocks
-
-// np.sum over m values v(0 .. m-1) with NumPy's tree, by one 256-thread block: leaves
-// listed by thread 0, summed by all threads, folded by thread 0 in the tree's order.
-template <typename Val>
-__device__ double numpy_sum(Val v, int64_t m, int32_t *loff, int32_t *llen, double *lsum, int32_t *bleaf,
-                            double *bcast)
-{
-    double total = 0.0;   // thread 0's running value
-    const int64_t nblk = (m + kPwBlock - 1) / kPwBlock;
-    for (int64_t g0 = 0; g0 < nblk; g0 += kRmsGroup) {
-        const int gn = (int)std::min<int64_t>(kRmsGroup, nblk - g0);
-        if (threadIdx.x == 0) {
-            int nl = 0;
-            for (int g = 0; g < gn; ++g) {
-                const int64_t b0 = (g0 + g) * kPwBlock;
-                const int bn = (int)std::min<int64_t>(kPwBlock, m - b0);
-                bleaf[g] = nl;
-                pairwise_tree(bn, [&](int off, int len) {
-                    loff[nl] = (int32_t)(b0 - g0 * kPwBlock) + off;
-                    llen[nl] = len;
-                    ++nl;
-                    return 0.0;
-                });
-            }
-            bleaf[gn] = nl;
-        }
-        __syncthreads();
-        const int64_t base = g0 * kPwBlock;
-        for (int l = threadIdx.x; l < bleaf[gn]; l += blockDim.x) lsum[l] = pw_leaf(v, base + loff[l], llen[l]);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            for (int g = 0; g < gn; ++g) {
-                const int bn = (int)std::min<int64_t>(kPwBlock, m - (g0 + g) * kPwBlock);
-                int li = bleaf[g];
-                total += pairwise_tree(bn, [&](int, int) { return lsum[li++]; });
-            }
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) *bcast = total;
-    __syncthreads();
-    const double t = *bcast;
-    __syncthreads();
-    return t;
-}
-
-// rms[r] = nanstd(d) / sqrt(2), d_i = x[1 + i] / s - x[0] / s, i < N - 1, N = n // 2 * 2
-// (COMAPData.auto_rms with its tod[:-1:N] slice: COMAPData.py:205-208).  np.nanstd:
-// NaN -> 0, avg = sum / count, (d - avg)^2 with NaN -> 0, var = sum / count.
-__global__ void __launch_bounds__(kRmsThreads) k_prep_rms(const double *__restrict__ x, int64_t stride,
-                                                          const int32_t *__restrict__ rows,
-                                                          const double *__restrict__ scale, int64_t n,
-                                                          double *__restrict__ rms)
+template <int PHASE>
+__global__ void __launch_bounds__(kRmsWG) k_rms_blocks(const double *__restrict__ x, int64_t stride,
+                                                       const int32_t *__restrict__ rows,
+                                                       const double *__restrict__ scale, int64_t n, int32_t nrows,
+                                                       int32_t nblk, const double *__restrict__ part0,
+                                                       const int64_t *__restrict__ cnt0, double *__restrict__ part,
+                                                       int64_t *__restrict__ cnt)
 {
 #pragma clang fp contract(off)
-    __shared__ int32_t loff[kRmsLeafCap], llen[kRmsLeafCap];
-    __shared__ double lsum[kRmsLeafCap];
-    __shared__ int32_t bleaf[kRmsGroup + 1];
-    __shared__ double bc;
+    // a partial block's leaves: pw splits at multiples of 8, so there are at most 65
+    __shared__ int32_t loff[128], llen[128];
+    __shared__ double lsum[128];
+    __shared__ int nleaf;
     __shared__ unsigned long long cnt_s;
-    const int r = blockIdx.x;
+    const int64_t job = blockIdx.x;
+    const int r = (int)(job / nblk), k = (int)(job % nblk);
+    const int64_t m = n / 2 * 2 - 1;
     const double *xr = x + (int64_t)rows[r] * stride;
     const double s = scale[r];
-    const int64_t m = n / 2 * 2 - 1;
-    if (m <= 0) {
-        if (threadIdx.x == 0) rms[r] = NAN;
-        return;
-    }
     const double x0 = xr[0] / s;
-    auto d_at = [&](int64_t i) { return xr[1 + i] / s - x0; };
-    // count of non-NaN differences (exact integer sum)
-    if (threadIdx.x == 0) cnt_s = 0;
-    __syncthreads();
-    unsigned long long c = 0;
-    for (int64_t i = threadIdx.x; i < m; i += blockDim.x) c += !isnan(d_at(i));
-    atomicAdd(&cnt_s, c);
-    __syncthreads();
-    const double cnt = (double)cnt_s;
-    const double sum = numpy_sum([&](int64_t i) { const double d = d_at(i); return isnan(d) ? 0.0 : d; }, m, loff,
-                                 llen, lsum, bleaf, &bc);
-    const double avg = sum / cnt;
-    const double sq = numpy_sum([&](int64_t i) {
-        const double d = d_at(i);
+    double avg = 0.0;
+    if constexpr (PHASE == 1) {
+        double sum = 0.0;
+        int64_t c = 0;
+        for (int q = 0; q < nblk; ++q) { sum += part0[(int64_t)r * nblk + q]; c += cnt0[(int64_t)r * nblk + q]; }
+        avg = sum / (double)c;
+    }
+    auto v = [&](int64_t i) {
+        const double d = xr[1 + i] / s - x0;
         if (isnan(d)) return 0.0;
-        const double e = d - avg;
-        return e * e;
-    }, m, loff, llen, lsum, bleaf, &bc);
-    if (threadIdx.x == 0) rms[r] = sqrt(sq / cnt) / 1.4142135623730951;   // np.sqrt(2)
+        if constexpr (PHASE == 0) {
+            return d;
+        } else {
+            const double e = d - avg;
+            return e * e;
+        }
+    };
+    const int64_t b0 = (int64_t)k * kPwBlock;
+    const int bn = (int)std::min<int64_t>(kPwBlock, m - b0);
+    const bool full = bn == kPwBlock;
+    if (threadIdx.x == 0) {
+        cnt_s = 0;
+        int nl = 0;
+        if (!full)
+            pairwise_tree(bn, [&](int off, int len) {
+                loff[nl] = off;
+                llen[nl] = len;
+                ++nl;
+                return 0.0;
+            });
+        nleaf = full ? kPwBlock / kPwLeaf : nl;
+    }
+    __syncthreads();
+    const int g = threadIdx.x >> 3, j = threadIdx.x & 7;
+    unsigned long long c = 0;         // phase 0: non-NaN d (exact)
+    if (full) {
+        // one leaf per 8-lane group: lane j's 16 values (r[j]'s chain) loaded before any add
+        const int64_t lo = b0 + (int64_t)kPwLeaf * g;
+        double t[kPwLeaf / 8];
+#pragma unroll
+        for (int i = 0; i < kPwLeaf / 8; ++i) {
+            const double d = xr[1 + lo + 8 * i + j] / s - x0;
+            c += !isnan(d);
+            if (isnan(d)) {
+                t[i] = 0.0;
+            } else if constexpr (PHASE == 0) {
+                t[i] = d;
+            } else {
+                const double e = d - avg;
+                t[i] = e * e;
+            }
+        }
+        double r = t[0];
+#pragma unroll
+        for (int i = 1; i < kPwLeaf / 8; ++i) r += t[i];
+        r = r + __shfl_xor(r, 1, 64);
+        r = r + __shfl_xor(r, 2, 64);
+        r = r + __shfl_xor(r, 4, 64);
+        if (j == 0) lsum[g] = r;
+    } else {
+        if constexpr (PHASE == 0)
+            for (int i = threadIdx.x; i < bn; i += kRmsWG) c += !isnan(xr[1 + b0 + i] / s - x0);
+        for (int l = g; l < nleaf; l += kRmsWG / 8) {
+            const double t = pw_leaf8(v, b0 + loff[l], llen[l], j);
+            if (j == 0) lsum[l] = t;
+        }
+    }
+    if constexpr (PHASE == 0) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+        if ((threadIdx.x & 63) == 0) atomicAdd(&cnt_s, c);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double val;
+        if (full) {   // pw's balanced tree over the 64 leaves, level by level, left + right
+            for (int o = 1; o < 64; o <<= 1)
+                for (int i = 0; i < 64; i += 2 * o) lsum[i] = lsum[i] + lsum[i + o];
+            val = lsum[0];
+        } else {
+            int li = 0;
+            val = pairwise_tree(bn, [&](int, int) { return lsum[li++]; });
+        }
+        part[job] = val;
+        if constexpr (PHASE == 0) cnt[job] = (int64_t)cnt_s;
+    }
+}
+
+// rms[r] from the phase-1 block values: var = (0 + q_0 + q_1 + ...) / count
+__global__ void k_rms_final(int32_t nrows, int32_t nblk, int64_t n, const double *__restrict__ part1,
+                            const int64_t *__restrict__ cnt0, double *__restrict__ rms)
+{
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrows) return;
+    if (n / 2 * 2 - 1 <= 0) { rms[r] = NAN; return; }
+    double sq = 0.0;
+    int64_t c = 0;
+    for (int j = 0; j < nblk; ++j) { sq += part1[(int64_t)r * nblk + j]; c += cnt0[(int64_t)r * nblk + j]; }
+    rms[r] = sqrt(sq / (double)c) / 1.4142135623730951;   // np.sqrt(2)
 }
 
 // ---------------------------------------------------------------- percentiles
@@ -228,86 +271,61 @@ __device__ __forceinline__ double from_key(unsigned long long k)
 // v = az (which 0) or el (which 1) of row rows[r] (COMAPData.py:338-346).  NumPy's
 // 'linear' rule: virtual index (n - 1) q, gamma its fraction, lerp between the order
 // statistics at floor and floor + 1 (a + (b - a) g, or b - (b - a)(1 - g) for g >= 0.5);
-// a NaN among the values makes the result NaN.  The four order statistics come from
-// one block's radix select (8 passes of 8 bits over orderable u64 keys).
-constexpr int kPctThreads = 1024;
-__global__ void __launch_bounds__(kPctThreads) k_prep_pct(const double *__restrict__ az, const double *__restrict__ el,
-                                                          int64_t stride, const int32_t *__restrict__ rows, int64_t n,
-                                                          double *__restrict__ pct)
+// a NaN among the values makes the result NaN.  The order statistics come from one
+// device-wide sort of every (row, which) series at once: orderable u64 keys (excluded
+// samples last) sorted with their series id, then a stable sort by series id.
+// (A per-series radix select in one workgroup took 1.6-2.2 ms per file: 38 workgroups
+// and LDS-atomic histograms on nearly constant leading digits.)
+__global__ void k_pct_keys(const double *__restrict__ az, const double *__restrict__ el, int64_t stride,
+                           const int32_t *__restrict__ rows, int32_t nrows, int64_t n,
+                           unsigned long long *__restrict__ key, uint16_t *__restrict__ sid,
+                           unsigned long long *__restrict__ cnt)
 {
-#pragma clang fp contract(off)
-    __shared__ unsigned int hist[4][256];
-    __shared__ unsigned long long pre[4];
-    __shared__ long long rk[4];
-    __shared__ unsigned long long ngood_s, nnan_s;
-    const int r = blockIdx.x >> 1, which = blockIdx.x & 1;
+    const int sg = blockIdx.y;                       // series = 2 r + which
+    const int r = sg >> 1, which = sg & 1;
     const double *a = az + (int64_t)rows[r] * stride;
     const double *v = (which ? el : az) + (int64_t)rows[r] * stride;
-    if (threadIdx.x == 0) { ngood_s = 0; nnan_s = 0; }
-    __syncthreads();
     unsigned long long ng = 0, nn = 0;
-    for (int64_t t = threadIdx.x; t < n; t += blockDim.x) {
-        if (isfinite(a[t])) { ++ng; nn += isnan(v[t]); }
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
+        const bool good = isfinite(a[t]);
+        const double x = v[t];
+        ng += good;
+        nn += good && isnan(x);
+        key[(int64_t)sg * n + t] = good ? ord_key(x) : ~0ull;
+        sid[(int64_t)sg * n + t] = (uint16_t)sg;
     }
-    atomicAdd(&ngood_s, ng);
-    atomicAdd(&nnan_s, nn);
-    __syncthreads();
-    const int64_t cnt = (int64_t)ngood_s;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        ng += __shfl_xor(ng, o, 64);
+        nn += __shfl_xor(nn, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&cnt[2 * sg], ng);
+        atomicAdd(&cnt[2 * sg + 1], nn);
+    }
+}
+
+// sorted: series sg occupies [sg n, (sg + 1) n), its good samples first, ascending
+__global__ void k_pct_pick(const unsigned long long *__restrict__ sorted, const unsigned long long *__restrict__ cnt,
+                           int32_t nseries, int64_t n, double *__restrict__ pct)
+{
+#pragma clang fp contract(off)
+    const int sg = blockIdx.x * blockDim.x + threadIdx.x;
+    if (sg >= nseries) return;
+    const int r = sg >> 1, which = sg & 1;
     double *out = pct + 4 * (int64_t)r + 2 * which;
-    if (cnt == 0 || nnan_s > 0) {
-        if (threadIdx.x < 2) out[threadIdx.x] = NAN;
-        return;
-    }
+    const int64_t c = cnt ? (int64_t)cnt[2 * sg] : 0;
+    if (c == 0 || cnt[2 * sg + 1] > 0) { out[0] = NAN; out[1] = NAN; return; }
     const double q[2] = {0.1, 0.9};   // np.true_divide(10, 100), (90, 100)
-    double virt[2];
-    int64_t lo[2], hi[2];
     for (int k = 0; k < 2; ++k) {
-        virt[k] = (double)(cnt - 1) * q[k];
-        double prev = floor(virt[k]);
-        if (virt[k] >= (double)(cnt - 1)) prev = -1.0;   // _get_indexes: above the last index -> the last value
-        if (virt[k] < 0) prev = 0.0;
-        lo[k] = prev < 0 ? cnt - 1 : (int64_t)prev;
-        hi[k] = prev < 0 ? cnt - 1 : std::min<int64_t>(lo[k] + 1, cnt - 1);
-        virt[k] = virt[k] - prev;                        // gamma = virtual - previous index
-    }
-    if (threadIdx.x < 4) {
-        pre[threadIdx.x] = 0;
-        rk[threadIdx.x] = threadIdx.x == 0 ? lo[0] : threadIdx.x == 1 ? hi[0] : threadIdx.x == 2 ? lo[1] : hi[1];
-    }
-    unsigned long long mask = 0;
-    for (int pass = 7; pass >= 0; --pass) {
-        const int sh = 8 * pass;
-        for (int i = threadIdx.x; i < 4 * 256; i += blockDim.x) (&hist[0][0])[i] = 0;
-        __syncthreads();
-        unsigned long long p4[4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) p4[s] = pre[s];
-        for (int64_t t = threadIdx.x; t < n; t += blockDim.x) {
-            if (!isfinite(a[t])) continue;
-            const unsigned long long key = ord_key(v[t]);
-            const unsigned dg = (unsigned)(key >> sh) & 255u;
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-                if ((key & mask) == p4[s]) atomicAdd(&hist[s][dg], 1u);
-        }
-        __syncthreads();
-        if (threadIdx.x < 4) {
-            const int s = threadIdx.x;
-            long long before = 0;
-            int d = 0;
-            for (; d < 255; ++d) {
-                if (before + hist[s][d] > rk[s]) break;
-                before += hist[s][d];
-            }
-            rk[s] -= before;
-            pre[s] |= (unsigned long long)d << sh;
-        }
-        mask |= 255ull << sh;
-        __syncthreads();
-    }
-    if (threadIdx.x < 2) {
-        const int k = threadIdx.x;
-        const double av = from_key(pre[2 * k]), bv = from_key(pre[2 * k + 1]), g = virt[k];
+        const double virt = (double)(c - 1) * q[k];
+        double prev = floor(virt);
+        if (virt >= (double)(c - 1)) prev = -1.0;   // _get_indexes: above the last index -> the last value
+        if (virt < 0) prev = 0.0;
+        const int64_t lo = prev < 0 ? c - 1 : (int64_t)prev;
+        const int64_t hi = prev < 0 ? c - 1 : std::min<int64_t>(lo + 1, c - 1);
+        const double g = virt - prev;                // gamma = virtual - previous index
+        const double av = from_key(sorted[(int64_t)sg * n + lo]), bv = from_key(sorted[(int64_t)sg * n + hi]);
         const double diff = bv - av;
         double res = av + diff * g;
         if (g >= 0.5) res = bv - diff * (1.0 - g);
@@ -482,27 +500,29 @@ __global__ void k_seg_subtract(double *__restrict__ x, const int64_t *__restrict
 // ---------------------------------------------------------------- NaN and empty-offset cuts
 // per band: tod NaN / inf -> tod = w = 0 (COMAPData.py:550-552); keep[b][o] = any w != 0
 // over the offset (:554-557); kept[o] = any band keeps o
-__global__ void k_cut_flags(double *__restrict__ tod, double *__restrict__ w, int64_t band_stride, int nb, int64_t NO,
-                            int L, uint8_t *__restrict__ keep, int32_t *__restrict__ kept)
+// One wave per offset (lanes over its samples, coalesced): NaN tod -> tod = w = 0, then
+// keep[b][o] = any w != 0 in band b, kept[o] = any band keeps it.
+__global__ void __launch_bounds__(256) k_cut_flags(double *__restrict__ tod, double *__restrict__ w,
+                                                   int64_t band_stride, int nb, int64_t NO, int L,
+                                                   uint8_t *__restrict__ keep, int32_t *__restrict__ kept)
 {
-    for (int64_t o = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; o < NO; o += (int64_t)gridDim.x * blockDim.x) {
-        int any_band = 0;
-        for (int b = 0; b < nb; ++b) {
-            double *tp = tod + b * band_stride + o * L, *wp = w + b * band_stride + o * L;
-            int any = 0;
-            for (int j = 0; j < L; ++j) {
-                if (!isfinite(tp[j])) { tp[j] = 0.0; wp[j] = 0.0; }
-                any |= wp[j] != 0.0;
-            }
-            keep[b * NO + o] = (uint8_t)any;
-            any_band |= any;
+    const int lane = threadIdx.x & 63;
+    const int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (o >= NO) return;
+    int any_band = 0;
+    for (int b = 0; b < nb; ++b) {
+        double *tp = tod + b * band_stride + o * L, *wp = w + b * band_stride + o * L;
+        bool any = false;
+        for (int j = lane; j < L; j += 64) {
+            if (!isfinite(tp[j])) { tp[j] = 0.0; wp[j] = 0.0; }
+            any |= wp[j] != 0.0;
         }
-        kept[o] = any_band;
+        any = __ballot(any) != 0ull;
+        if (lane == 0) keep[b * NO + o] = (uint8_t)any;
+        any_band |= any;
     }
+    if (lane == 0) kept[o] = any_band;
 }
-
-// compaction of the kept offsets (L samples each) of every output array; non-finite
-// weights -> 0 after the cut (COMAPData.py:568)
 __global__ void k_cut_copy(const comap_prep_out in, comap_prep_out out, int nb, int64_t NO, int L,
                            const int32_t *__restrict__ kept, const int32_t *__restrict__ newo,
                            const uint8_t *__restrict__ keep, uint8_t *__restrict__ keep_out, int64_t NO_out)
@@ -536,7 +556,21 @@ extern "C" int comap_prep_auto_rms(comap_ctx *ctx, const double *x, int64_t row_
     if (!ctx || !x || !rows || !scale || !rms || nrows < 0 || n < 0) return -1;
     COMAP_DEVICE_GUARD(ctx);
     if (nrows == 0) return 0;
-    k_prep_rms<<<nrows, kRmsThreads, 0, ctx->stream>>>(x, row_stride, rows, scale, n, rms);
+    const int64_t m = n / 2 * 2 - 1;
+    const int32_t nblk = (int32_t)std::max<int64_t>(1, (m + kPwBlock - 1) / kPwBlock);
+    const size_t nj = (size_t)nrows * nblk;
+    // block values in the context scratch (stream-ordered: no allocation or sync per call)
+    void *sc = nullptr;
+    if (int rc = comap_scratch(ctx, 24 * nj, &sc)) return rc;
+    double *p0 = (double *)sc, *p1 = p0 + nj;
+    int64_t *c0 = (int64_t *)(p1 + nj);
+    if (m > 0) {
+        const unsigned g = (unsigned)nj;
+        k_rms_blocks<0><<<g, kRmsWG, 0, ctx->stream>>>(x, row_stride, rows, scale, n, nrows, nblk, nullptr, nullptr, p0,
+                                                      c0);
+        k_rms_blocks<1><<<g, kRmsWG, 0, ctx->stream>>>(x, row_stride, rows, scale, n, nrows, nblk, p0, c0, p1, nullptr);
+    }
+    k_rms_final<<<(nrows + 255) / 256, 256, 0, ctx->stream>>>(nrows, nblk, n, p1, c0, rms);
     COMAP_LAUNCH_CHECK(ctx);
     return 0;
 }
@@ -547,7 +581,42 @@ extern "C" int comap_prep_percentiles(comap_ctx *ctx, const double *az, const do
     if (!ctx || !az || !el || !rows || !pct || nrows < 0 || n < 0) return -1;
     COMAP_DEVICE_GUARD(ctx);
     if (nrows == 0) return 0;
-    k_prep_pct<<<2 * nrows, kPctThreads, 0, ctx->stream>>>(az, el, row_stride, rows, n, pct);
+    if (2 * (int64_t)nrows > 65535) return comap_fail(ctx, -1, "comap_prep_percentiles: too many rows");
+    hipStream_t st = ctx->stream;
+    const int ns = 2 * nrows;
+    const int64_t tot = (int64_t)ns * n;
+    if (tot >= (1ll << 31)) return comap_fail(ctx, -1, "comap_prep_percentiles: too many samples");
+    if (n == 0) {
+        k_pct_pick<<<(ns + 255) / 256, 256, 0, st>>>(nullptr, nullptr, ns, 0, pct);   // NaN: no good sample
+        COMAP_LAUNCH_CHECK(ctx);
+        return 0;
+    }
+    int sbits = 1;
+    while ((1 << sbits) < ns) ++sbits;
+    size_t tb1 = 0, tb2 = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb1, (unsigned long long *)nullptr, (unsigned long long *)nullptr,
+                                             (uint16_t *)nullptr, (uint16_t *)nullptr, (int)tot, 0, 64, st);
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, (uint16_t *)nullptr, (uint16_t *)nullptr,
+                                             (unsigned long long *)nullptr, (unsigned long long *)nullptr, (int)tot, 0,
+                                             sbits, st);
+    DevTemps tmp(st);
+    unsigned long long *k0 = nullptr, *k1 = nullptr, *cnt = nullptr;
+    uint16_t *s0 = nullptr, *s1 = nullptr;
+    char *tb = nullptr;
+    COMAP_CHECK(ctx, tmp.alloc(&k0, (size_t)tot));
+    COMAP_CHECK(ctx, tmp.alloc(&k1, (size_t)tot));
+    COMAP_CHECK(ctx, tmp.alloc(&s0, (size_t)tot));
+    COMAP_CHECK(ctx, tmp.alloc(&s1, (size_t)tot));
+    COMAP_CHECK(ctx, tmp.alloc(&cnt, 2 * (size_t)ns));
+    COMAP_CHECK(ctx, tmp.alloc(&tb, std::max(tb1, tb2)));
+    COMAP_CHECK(ctx, hipMemsetAsync(cnt, 0, 16 * (size_t)ns, st));
+    const dim3 g((unsigned)std::min<int64_t>(64, (n + 255) / 256), (unsigned)ns);
+    k_pct_keys<<<g, 256, 0, st>>>(az, el, row_stride, rows, nrows, n, k0, s0, cnt);
+    COMAP_LAUNCH_CHECK(ctx);
+    // by key, then (stable) by series: every series' keys end up contiguous and ascending
+    COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(tb, tb1, k0, k1, s0, s1, (int)tot, 0, 64, st));
+    COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(tb, tb2, s1, s0, k1, k0, (int)tot, 0, sbits, st));
+    k_pct_pick<<<(ns + 255) / 256, 256, 0, st>>>(k0, cnt, ns, n, pct);
     COMAP_LAUNCH_CHECK(ctx);
     return 0;
 }
@@ -621,14 +690,21 @@ extern "C" int comap_prep_highpass(comap_ctx *ctx, double *x, const int64_t *seg
     int rc = 0;
     if (!jobs.empty()) {
         MedPlan mp;
+        const bool prof = getenv("COMAP_PREP_PROFILE") && getenv("COMAP_PREP_PROFILE")[0] == '1';
+        auto now = [] { return std::chrono::steady_clock::now(); };
+        const auto t0 = now();
         rc = comap_median_plan(ctx, &mp, jobs, w);
+        const auto t1 = now();
         if (!rc) rc = comap_median_run(ctx, &mp);
-        if (!rc) {
-            // the plan's buffers are freed below: wait for the walk
-            const hipError_t e = hipStreamSynchronize(st);
-            if (e != hipSuccess) rc = comap_fail(ctx, -2, hipGetErrorString(e));
-        }
+        const auto t2 = now();
+        // the plan's buffers come from the stream-ordered pool: freed behind the walk, no sync
         comap_median_plan_free(&mp);
+        const auto t3 = now();
+        if (prof) {
+            auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+            fprintf(stderr, "[comap_prep_highpass] plan %.0f us, run enqueue %.0f us, free %.0f us (%zu jobs)\n",
+                    us(t0, t1), us(t1, t2), us(t2, t3), jobs.size());
+        }
         if (rc) return rc;
     }
     // short segments: np.nanmedian of their (finite) values -- a mean of the two middle
@@ -670,7 +746,7 @@ extern "C" int comap_prep_cut(comap_ctx *ctx, const comap_prep_out *in, int32_t 
     COMAP_CHECK(ctx, tmp.alloc(&keep, (size_t)nb * NO));
     COMAP_CHECK(ctx, tmp.alloc(&kept, (size_t)NO + 1));
     COMAP_CHECK(ctx, tmp.alloc(&newo, (size_t)NO + 1));
-    k_cut_flags<<<grid_for(NO), 256, 0, st>>>(in->tod, in->w, in->band_stride, nb, NO, L, keep, kept);
+    k_cut_flags<<<(unsigned)((NO + 3) / 4), 256, 0, st>>>(in->tod, in->w, in->band_stride, nb, NO, L, keep, kept);
     COMAP_LAUNCH_CHECK(ctx);
     size_t tb = 0;
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, kept, newo, (int)(NO + 1), st);

@@ -286,7 +286,9 @@ class GPUObservation:
         fit = to_device(fit_values, torch.float64, self.tdev)
         ts = to_device(tsys0, torch.float64, self.tdev)
         gn = to_device(gain0, torch.float64, self.tdev)
-        out = torch.zeros((3, self.F, N_BANDS, self.T), dtype=torch.float64, device=self.tdev)
+        # every sample is written by comap_l1_average (the units' by the reduction, the
+        # rest -- scan gaps, a shard's foreign units -- zeroed there)
+        out = torch.empty((3, self.F, N_BANDS, self.T), dtype=torch.float64, device=self.tdev)
         self._bind()
         N.check(N.lib().comap_l1_average(self.plan, N.dptr(fit), N.dptr(ts), N.dptr(gn), int(bool(calibrator)),
                                          N.dptr(out[0]), N.dptr(out[1]), N.dptr(out[2])), self.ctx,

@@ -218,7 +218,14 @@ def read_comap_data_bands(filelist, map_info, bands=(0, 1, 2, 3), use_gain_filte
     del flat
     mark = prep._Phases(torch, cut.tod.device)
     pointing = cut.pix.to(torch.int64)
-    remapping_array = find_unique_values(torch.unique(pointing).cpu().numpy()).astype(int)
+    if healpix:
+        local = torch.unique(pointing)
+    else:   # map pixels (and -1) are bounded by the map: a hit mask, no sort
+        hit = torch.zeros(int(map_info['nxpix']) * int(map_info['nypix']) + 1, dtype=torch.uint8,
+                          device=pointing.device)
+        hit[pointing + 1] = 1
+        local = torch.nonzero(hit).reshape(-1) - 1
+    remapping_array = find_unique_values(local.cpu().numpy()).astype(int)
     mark('unique')
     if healpix:      # COMAPData.py:572-573: pixel ids -> positions in the union over ranks
         ra_sorted = torch.as_tensor(np.sort(remapping_array), device=pointing.device)

@@ -444,15 +444,129 @@ class DeviceDestriper:
 
     One band ([N] tod/weights): solve() -> {'x': [N/L], 'iters': int,
     'maps': {k: [npix]}}.  Several bands ([n_bands, N], one batched system):
-    {'x': [n_bands, N/L], 'iters': [per band], 'maps': {k: [n_bands, npix]}}."""
+    {'x': [n_bands, N/L], 'iters': [per band], 'maps': {k: [n_bands, npix]}}.
+
+    Across ranks (torch.distributed initialised, world > 1) every rank passes its own
+    samples and gets its own offsets and the full maps.  The problem is either
+    sharded (each rank's operator, RCCL all-reduces every CG iteration) or gathered
+    to rank 0, which solves it alone and hands back each rank's offsets and the maps:
+    mapmaking/rankplan.py models both (COMAP_DS_RANKS=auto, the default) -- small
+    problems such as one observation (C4) are latency-bound across ranks and are
+    gathered, large ones (C5) sharded; COMAP_DS_RANKS=shard / gather forces one."""
 
     def __init__(self, pixels, tod, weights, offset_length, npix, device=None, keep=None):
         self.npix_full, self.hit_index = int(npix), None
-        d = _dist()
-        if d is not None and d.get_world_size() > 1 and os.environ.get('COMAP_DS_COMPACT', '1') != '0':
-            pixels, npix = self._compact(pixels, int(npix), device)
-        self.ops = DeviceOps(pixels, tod, weights, offset_length, npix, device, keep)
         self.multi = np.ndim(tod) == 2 if not hasattr(tod, 'dim') else tod.dim() == 2
+        self.gathered, self.plan = None, None
+        d = _dist()
+        if d is not None and d.get_world_size() > 1:
+            if self._choose_gather(d, pixels, tod, offset_length):
+                self._gather(d, pixels, tod, weights, keep, offset_length, npix, device)
+                return
+            if os.environ.get('COMAP_DS_COMPACT', '1') != '0':
+                pixels, npix = self._compact(pixels, int(npix), device)
+        self.ops = DeviceOps(pixels, tod, weights, offset_length, npix, device, keep)
+
+    # ---- rank policy
+    def _choose_gather(self, d, pixels, tod, offset_length):
+        import torch
+        from . import rankplan
+        policy = os.environ.get('COMAP_DS_RANKS', 'auto')
+        if policy == 'shard':
+            return False
+        n_local = int(pixels.numel()) if hasattr(pixels, 'numel') else int(np.size(pixels))
+        n_bands = (int(tod.shape[0]) if self.multi else 1)
+        dev = self._comm_device(d)
+        cnt = torch.tensor([n_local], dtype=torch.int64, device=dev)
+        parts = [torch.zeros_like(cnt) for _ in range(d.get_world_size())]
+        d.all_gather(parts, cnt)
+        self.counts = [int(c.item()) for c in parts]
+        if policy == 'gather':
+            return True
+        self.plan = rankplan.plan(sum(self.counts), n_bands, d.get_world_size())
+        return self.plan['mode'] == 'gather'
+
+    @staticmethod
+    def _comm_device(d):
+        import torch
+        return torch.device('cuda', torch.cuda.current_device()) if d.get_backend() == 'nccl' else torch.device('cpu')
+
+    def _gather(self, d, pixels, tod, weights, keep, offset_length, npix, device):
+        """Inputs of every rank to rank 0 (padded to the largest rank, in rank order);
+        rank 0 builds the single-rank operator on their concatenation."""
+        import torch
+        L = int(offset_length)
+        rank, world = d.get_rank(), d.get_world_size()
+        cdev = self._comm_device(d)
+        nbands = int(tod.shape[0]) if self.multi else 1
+        nmax = max(self.counts)
+
+        def as_t(a, dt):
+            t = a if isinstance(a, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(a))
+            return t.to(device=cdev, dtype=dt)
+
+        def gather(t, width):       # t [rows, n_local] -> root: list of [rows, width]
+            pad = torch.zeros((t.shape[0], width), dtype=t.dtype, device=cdev)
+            pad[:, :t.shape[1]] = t
+            parts = [torch.zeros_like(pad) for _ in range(world)] if rank == 0 else None
+            d.gather(pad, gather_list=parts, dst=0)
+            return parts
+
+        pix = gather(as_t(pixels, torch.int32).reshape(1, -1), nmax)
+        td = gather(as_t(tod, torch.float64).reshape(nbands, -1), nmax)
+        wd = gather(as_t(weights, torch.float64).reshape(nbands, -1), nmax)
+        kp = None
+        if keep is not None:
+            kp = gather(as_t(keep, torch.uint8).reshape(nbands, -1), nmax // L)
+        self.gathered = {'counts': self.counts, 'L': L}
+        if rank != 0:
+            self.ops = None
+            self._ref = (device, nbands)
+            return
+        dev = torch.device('cuda', N.current_device() if device is None else int(device))
+        cat = lambda parts, per: torch.cat([parts[r][:, :c // per] for r, c in enumerate(self.counts)], dim=1).to(dev)  # noqa: E731
+        p_all, t_all, w_all = cat(pix, 1).reshape(-1), cat(td, 1), cat(wd, 1)
+        k_all = cat(kp, L) if kp is not None else None
+        if not self.multi:
+            t_all, w_all = t_all.reshape(-1), w_all.reshape(-1)
+        self.ops = DeviceOps(p_all, t_all, w_all, L, npix, device, k_all)
+        self._ref = (device, nbands)
+
+    def _solve_gathered(self, d, threshold, niter):
+        """Rank 0 solves; iterations and maps are broadcast, each rank's offsets sent back."""
+        import torch
+        rank, world = d.get_rank(), d.get_world_size()
+        cdev = self._comm_device(d)
+        device, nbands = self._ref
+        nb = 4 if nbands == 3 else nbands
+        L, counts = self.gathered['L'], self.gathered['counts']
+        npix = self.npix_full
+        dev = torch.device('cuda', N.current_device() if device is None else int(device))
+        nomax = max(counts) // L
+        keys = ('map', 'naive', 'weight', 'hits')
+        if rank == 0:
+            x, it, maps = self.ops.solve_native(threshold, niter)
+            its = torch.tensor(list(it) + [0] * (4 - len(it)), dtype=torch.int64, device=cdev)
+            mp = torch.stack([maps[k] for k in keys]).to(cdev)
+            xv = x.reshape(-1, nb)
+            parts, o = [], 0
+            for c in counts:
+                pad = torch.zeros((nomax, nb), dtype=torch.float64, device=cdev)
+                pad[:c // L] = xv[o:o + c // L]
+                parts.append(pad)
+                o += c // L
+        else:
+            its = torch.zeros(4, dtype=torch.int64, device=cdev)
+            mp = torch.zeros((4, npix * nb), dtype=torch.float64, device=cdev)
+            parts = None
+        d.broadcast(its, src=0)
+        d.broadcast(mp, src=0)
+        mine = torch.zeros((nomax, nb), dtype=torch.float64, device=cdev)
+        d.scatter(mine, scatter_list=parts, src=0)
+        x = mine[:counts[rank] // L].reshape(-1).to(dev)
+        it = [int(v) for v in its.cpu()][:nbands]
+        maps = {k: mp[i].to(dev) for i, k in enumerate(keys)}
+        return x, it, maps, nb, nbands
 
     def _compact(self, pixels, npix, device):
         """Across ranks the map numerator is all-reduced every CG iteration
@@ -490,8 +604,12 @@ class DeviceDestriper:
     def solve(self, threshold=1e-6, niter=100):
         d = _dist()
         ops = self.ops
-        if d is None or d.get_world_size() == 1:
+        if self.gathered is not None:
+            x, it, maps, nb, nbands = self._solve_gathered(d, threshold, niter)
+            split = lambda v: v.reshape(-1, nb).t()[:nbands].contiguous()   # noqa: E731
+        elif d is None or d.get_world_size() == 1:
             x, it, maps = ops.solve_native(threshold, niter)
+            split = ops.split_bands
         else:
             # COMAP_DS_GRAPH=1: the captured-graph driver (one launch per 16 iterations);
             # default: the eager batched driver (7 host calls per iteration, 16 per check)
@@ -518,12 +636,28 @@ class DeviceDestriper:
             it = it[:ops.n_bands]
             x = ops.natural(x)
             maps = {k: self._expand(v) for k, v in maps.items()}
+            split = ops.split_bands
         if not self.multi:
             maps['map2'] = maps['weight']
             return {'x': x, 'iters': it[0], 'maps': maps}
-        maps = {k: ops.split_bands(v) for k, v in maps.items()}
+        maps = {k: split(v) for k, v in maps.items()}
         maps['map2'] = maps['weight']
-        return {'x': ops.split_bands(x), 'iters': it, 'maps': maps}
+        return {'x': split(x), 'iters': it, 'maps': maps}
+
+
+def maps_to_host(maps):
+    """{name: device tensor} -> {name: NumPy array}: one device-side stack and one copy
+    into pinned host memory (a pageable copy per map runs at a fraction of the link)."""
+    import torch
+    keys = list(maps)
+    if not keys:
+        return {}
+    flat = torch.stack([maps[k].reshape(-1) for k in keys])
+    host = torch.empty(flat.shape, dtype=flat.dtype, pin_memory=True)
+    host.copy_(flat, non_blocking=True)
+    torch.cuda.current_stream(flat.device).synchronize()
+    a = host.numpy()
+    return {k: a[i].reshape(tuple(maps[k].shape)) for i, k in enumerate(keys)}
 
 
 def run_destriper(_pointing, _tod, _weights, offset_length, pixel_edges, az=None, el=None, ra=None, dec=None,
@@ -546,8 +680,7 @@ def run_destriper(_pointing, _tod, _weights, offset_length, pixel_edges, az=None
     rank = d.get_rank() if d is not None else 0
     if rank != 0:
         return {'All': {'map': None, 'naive': None, 'weight': None, 'map2': None}}
-    maps = {k: v.cpu().numpy() for k, v in res['maps'].items()}
-    return {'All': maps}
+    return {'All': maps_to_host(res['maps'])}
 
 
 def run_destriper_bands(_pointing, _tods, _weights, offset_length, pixel_edges, keep=None, threshold=1e-6,
@@ -573,11 +706,12 @@ def run_destriper_bands(_pointing, _tods, _weights, offset_length, pixel_edges, 
     d = _dist()
     rank = d.get_rank() if d is not None else 0
     out = []
+    hm = maps_to_host(res['maps']) if rank == 0 else None
     for b in range(tods.shape[0]):
         if rank != 0:
             out.append({'All': {'map': None, 'naive': None, 'weight': None, 'map2': None}})
             continue
-        maps = {k: v[b].cpu().numpy() for k, v in res['maps'].items()}
+        maps = {k: v[b] for k, v in hm.items()}
         out.append({'All': maps, 'iters': res['iters'][b], 'offsets': res['x'][b].cpu().numpy()})
     return out
 

@@ -185,28 +185,36 @@ def prep_flat(files, filelist, map_info, bands, use_gain_filter, offset_length, 
         # weights: 1 / auto_rms(tod_file)^2 per (row, band) (COMAPData.py:320)
         rms_rows = np.array([row_src[r] * B + b for r in live for b in bands], dtype=np.int32)
         rms_scale = np.array([row_cal[r, k] for r in live for k in range(nb)], dtype=np.float64)
+        colstart = np.concatenate(([0], np.cumsum(lens)[:-1])).astype(np.int64)
+        scans = np.stack([edges[:, 0], np.asarray(lens, np.int64), colstart], axis=1).astype(np.int64)
+        if scans.shape[0] > 64:
+            raise ValueError('at most 64 scans per file')
+        # every per-file table in one host -> device copy
+        rr, rs, pr, dsc, drs, dps, drf, drc, dlive = _dev_pack(
+            torch, dev, (rms_rows, rms_scale, row_src[live].astype(np.int32), scans, row_src, pix_src, row_feed,
+                         row_cal, live.astype(np.int64)))
         rms = torch.empty(max(1, rms_rows.size), dtype=torch.float64, device=dev)
-        rr, rs = _dev_np(torch, rms_rows, dev), _dev_np(torch, rms_scale, dev)
         mark('file_meta')
         N.check(lib.comap_prep_auto_rms(c, N.dptr(tod), T, N.dptr(rr), N.dptr(rs), int(rms_rows.size), T,
                                         N.dptr(rms)), c, 'comap_prep_auto_rms')
         mark('auto_rms')
         row_w = torch.ones((nrow, 4), dtype=torch.float64, device=dev)
-        if live.size:
-            row_w[torch.as_tensor(live, device=dev), :nb] = (1.0 / (rms * rms)).reshape(live.size, nb)
+        wl = (1.0 / (rms[:rms_rows.size] * rms[:rms_rows.size])).reshape(live.size, nb)
+        if live.size == nrow:
+            row_w[:, :nb] = wl
+        elif live.size:
+            row_w[dlive, :nb] = wl
         # az / el percentile band per row (COMAPData.py:338-346)
         pct = torch.zeros((max(1, live.size), 4), dtype=torch.float64, device=dev)
-        pr = _dev_np(torch, row_src[live].astype(np.int32), dev)
         N.check(lib.comap_prep_percentiles(c, N.dptr(az), N.dptr(el), T, N.dptr(pr), int(live.size), T,
                                            N.dptr(pct)), c, 'comap_prep_percentiles')
-        row_pct = torch.zeros((nrow, 4), dtype=torch.float64, device=dev)
-        if live.size:
-            row_pct[torch.as_tensor(live, device=dev)] = pct[:live.size]
+        if live.size == nrow:
+            row_pct = pct
+        else:
+            row_pct = torch.zeros((nrow, 4), dtype=torch.float64, device=dev)
+            if live.size:
+                row_pct[dlive] = pct[:live.size]
         mark('percentiles')
-        colstart = np.concatenate(([0], np.cumsum(lens)[:-1])).astype(np.int64)
-        scans = np.stack([edges[:, 0], np.asarray(lens, np.int64), colstart], axis=1).astype(np.int64)
-        if scans.shape[0] > 64:
-            raise ValueError('at most 64 scans per file')
         mjd0 = float(np.asarray(_host(f['spectrometer/MJD'])).reshape(-1)[0])
         sra, sdec = astro.sun_radec(mjd0)
         rot = astro.Rotator(rot=[sra, sdec], inv=True).mat
@@ -214,7 +222,6 @@ def prep_flat(files, filelist, map_info, bands, use_gain_filter, offset_length, 
         if healpix:
             from .comapdata import read_pixels_healpix
             pixels = _dev_np(torch, np.asarray(read_pixels_healpix(f, ds, L, feeds, map_info)).astype(np.int64), dev)
-        dsc, drs, dps, drf, drc = (_dev_np(torch, a, dev) for a in (scans, row_src, pix_src, row_feed, row_cal))
         bands4 = (ctypes.c_int32 * 4)(*(list(bands) + [0] * (4 - nb)))
         pf = PrepFile(N.dptr(tod), B * T, T, N.dptr(az), N.dptr(el), N.dptr(ra), N.dptr(dec), T,
                       None if spike_d is None else N.dptr(spike_d), B * T, T, nrow, int(scans.shape[0]), ds,
@@ -227,7 +234,7 @@ def prep_flat(files, filelist, map_info, bands, use_gain_filter, offset_length, 
                                       ctypes.byref(o)), c, 'comap_prep_gather')
         mark('gather')
         keep_alive.append((tod, az, el, ra, dec, spike_d, rr, rs, rms, row_w, pct, pr, row_pct, pixels, dsc, drs,
-                           dps, drf, drc))
+                           dps, drf, drc, dlive))
         if not calib:      # high-pass of each scan's non-zero samples (COMAPData.py:353-360)
             for r in live:
                 for (s0, _), nl, cs in zip(edges, lens, colstart):
@@ -239,11 +246,13 @@ def prep_flat(files, filelist, map_info, bands, use_gain_filter, offset_length, 
     mark('segments')
     if segs:
         sd = _dev_np(torch, np.asarray(segs, dtype=np.int64), dev)
+        mark('highpass_upload')
         N.check(lib.comap_prep_highpass(c, N.dptr(out.tod), N.dptr(sd), len(segs), MEDFILT_STEP), c,
                 'comap_prep_highpass')
     torch.cuda.current_stream(dev).synchronize()
     mark('highpass')
     del keep_alive
+    mark('release')
     return out
 
 
@@ -288,6 +297,27 @@ def _dev(torch, x, dev, dtype):
     if isinstance(x, torch.Tensor):
         return x.to(device=dev, dtype=dtype).contiguous()
     return torch.from_numpy(np.ascontiguousarray(np.asarray(x), dtype=np.dtype(str(dtype).split('.')[-1]))).to(dev)
+
+
+def _dev_pack(torch, dev, arrays):
+    """Several small host arrays to the device in ONE copy (8-byte aligned segments of one
+    buffer); returns device tensors of the same dtypes and shapes (views of that buffer)."""
+    segs, off = [], 0
+    for a in arrays:
+        a = np.ascontiguousarray(a)
+        segs.append((a, off))
+        off += (a.nbytes + 7) // 8 * 8 or 8
+    buf = np.zeros(off, dtype=np.uint8)
+    for a, o in segs:
+        buf[o:o + a.nbytes] = a.view(np.uint8).reshape(-1)
+    d = torch.from_numpy(buf).to(dev)
+    out = []
+    for a, o in segs:
+        tdt = getattr(torch, str(a.dtype)) if str(a.dtype) != 'bool' else torch.bool
+        n = max(a.size, 1)
+        t = d[o:o + n * a.itemsize].view(tdt)
+        out.append(t[:a.size].reshape(a.shape) if a.size else t)
+    return out
 
 
 def _dev_np(torch, a, dev):

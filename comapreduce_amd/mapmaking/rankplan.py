@@ -1,0 +1,74 @@
+"""How many ranks a destriper problem should run on.
+
+Across ranks every CG iteration all-reduces the compacted map numerator and two
+block-partial vectors (Destriper.py:183-204 sums the map over MPI every matvec), so
+the per-iteration cost on n ranks is
+
+    t_iter(n) = a + b_NB * N / n + 3 * alpha(n) + map_bytes * 2 (n - 1) / n / beta
+
+(a: the 4 launches' latency floor; b_NB: the streaming part per sample for NB bands;
+N: the problem's total samples; alpha(n): one small RCCL all-reduce; beta: the ring's
+bus bandwidth), and the set-up costs s0_NB + s1_NB * N / n.  Gathering the inputs to
+one rank instead costs bytes / (gather bandwidth) once, then the single-rank times.
+plan() compares the two for the expected iteration count and returns the faster.
+
+The a / b / s constants are fitted to this build's single-GPU measurements (bench.py
+C4 and C5 legs, count-form operator, r03d: 1 band 22 / 152 us per iteration at
+1.76 M / 27.4 M samples, 4 bands 34 / 339 us; set-up 1.0 / 5.05 ms and 2.27 / 9.1 ms).
+alpha and beta are NOT measured here (the one-GPU box cannot run two RCCL ranks; a
+one-rank all-reduce costs 10 us of host enqueue, profiles/r03/r03n_rccl_one_rank.log):
+alpha(n) = 10 us + 2 (n - 1) x 1.5 us per ring hop and beta = 100 GB/s are modelling
+assumptions for 8 MI355X on xGMI (7 links x ~153 GB/s per GPU), to be replaced by the
+driver's multi-GPU measurement.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+
+@dataclass
+class CostModel:
+    a_us: float = 13.0                                   # per-iteration latency floor
+    b_us_per_msample: dict = field(default_factory=lambda: {1: 5.07, 2: 8.5, 4: 11.9})
+    setup0_ms: dict = field(default_factory=lambda: {1: 0.72, 2: 1.2, 4: 1.8})
+    setup1_ms_per_msample: dict = field(default_factory=lambda: {1: 0.158, 2: 0.21, 4: 0.267})
+    alpha0_us: float = 10.0                              # one all-reduce: enqueue / protocol floor
+    alpha_hop_us: float = 1.5                            # per ring step (2 (n - 1) steps)
+    beta_gbs: float = 100.0                              # all-reduce bus bandwidth
+    gather_gbs: float = 150.0                            # inputs gathered to one rank (7 links in parallel)
+
+    def alpha_us(self, n):
+        return 0.0 if n <= 1 else self.alpha0_us + 2 * (n - 1) * self.alpha_hop_us
+
+    def iter_us(self, n_samples, nb, n, map_bytes):
+        nb = 4 if nb == 3 else nb
+        t = self.a_us + self.b_us_per_msample[nb] * n_samples / 1e6 / n
+        if n > 1:
+            t += 3 * self.alpha_us(n) + map_bytes * 2 * (n - 1) / n / (self.beta_gbs * 1e3)
+        return t
+
+    def setup_ms(self, n_samples, nb, n):
+        nb = 4 if nb == 3 else nb
+        return self.setup0_ms[nb] + self.setup1_ms_per_msample[nb] * n_samples / 1e6 / n
+
+
+def input_bytes(n_samples, nb, offset_length=50):
+    """Bytes of one problem's inputs: int32 pixel + f64 tod and weight per band and
+    sample, the uint8 keep mask per band and offset."""
+    return n_samples * (4 + 16 * nb) + nb * n_samples // max(offset_length, 1)
+
+
+def plan(n_samples, nb, world, n_hit_pixels=31_000, iters=25, model=None):
+    """Shard (every rank solves its own samples, RCCL all-reduces per iteration) or
+    gather (the inputs go to rank 0, which solves alone).  Returns a dict with the
+    choice and both modelled times (ms), plus the per-iteration model for 1/2/4/8 ranks."""
+    m = model or CostModel()
+    nbb = 4 if nb == 3 else nb
+    map_bytes = 8 * nbb * n_hit_pixels
+    t_shard = m.setup_ms(n_samples, nb, world) + iters * m.iter_us(n_samples, nb, world, map_bytes) / 1e3
+    t_gather = (input_bytes(n_samples, nbb) * (world - 1) / world / (m.gather_gbs * 1e6) +
+                m.setup_ms(n_samples, nb, 1) + iters * m.iter_us(n_samples, nb, 1, map_bytes) / 1e3)
+    per_iter = {n: m.iter_us(n_samples, nb, n, map_bytes) for n in (1, 2, 4, 8)}
+    mode = 'gather' if world > 1 and t_gather < t_shard else 'shard'
+    return {'mode': mode, 'shard_ms': t_shard, 'gather_ms': t_gather, 'iters': iters,
+            'iter_us_by_ranks': per_iter}

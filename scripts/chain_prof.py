@@ -24,8 +24,9 @@ def main():
     level2 = bench.reduce_step(data, 0)
     dev = torch.device('cuda', 0)
     out = {}
+    pointing = bench.pointing_device(data, dev)
     for rep in range(3):
-        store = bench.level2_store_device(level2, data, 1, dev)
+        store = bench.level2_store_device(level2, data, 1, dev, pointing)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         r = CD.read_comap_data_bands(list(store), bench.c4_map_info(), bands=(0, 1, 2, 3), offset_length=50,

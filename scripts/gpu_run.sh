@@ -8,6 +8,7 @@
 #         pmc=COUNTERS[@BENCH_ARGS]  one rocprofv3 --pmc pass
 #         smoke                 __graft_entry__.smoke()
 #         py=SCRIPT ARGS        python3 SCRIPT ARGS (log gpurun_out/TAG_py<step>.log)
+#         pyprof=SCRIPT ARGS    the same under rocprofv3 --kernel-trace --stats (gpurun_out/TAG_pyprof<step>/)
 #         dsprof[=ARGS]         rocprofv3 kernel trace + stats of scripts/ds_c5.py (default: 8 obs, 4 bands, 50 it)
 #         dspmc=COUNTERS[@ARGS] one rocprofv3 --pmc pass over scripts/ds_c5.py
 TAG=$1; shift
@@ -33,6 +34,8 @@ for step in "$@"; do
            d=gpurun_out/${TAG}_dspmc_$(echo $cnt | tr ' ' '_' | cut -c1-40)
            timeout -s KILL 240 rocprofv3 --pmc $cnt --output-format csv -d $d -o run -- python3 scripts/ds_c5.py $dargs \
              > $d.log 2>&1 ;;
+    pyprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_pyprof${NSTEP} \
+              -o run -- python3 $arg > gpurun_out/${TAG}_pyprof${NSTEP}.log 2>&1 ;;
     py)    timeout -k 10 300 python3 -u $arg > gpurun_out/${TAG}_py${NSTEP}.log 2>&1 ;;
     smoke) timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/${TAG}_smoke.log 2>&1 ;;
     *) echo "unknown step $name"; exit 2 ;;

@@ -97,6 +97,7 @@ def _gloo_rank(rank, world, port, p, t, w, q):
     from comapreduce_amd.mapmaking.destriper import DeviceDestriper
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
+    os.environ['COMAP_DS_RANKS'] = 'shard'    # the sharded CG (small problems are gathered by default)
     torch.cuda.set_device(0)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     no = t.size // L
@@ -142,6 +143,7 @@ def _compact_rank(rank, world, port, p, t, w, npix, q):
     from comapreduce_amd.mapmaking.destriper import DeviceDestriper
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
+    os.environ['COMAP_DS_RANKS'] = 'shard'    # the sharded CG (small problems are gathered by default)
     torch.cuda.set_device(0)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     no = t.shape[-1] // L
@@ -193,6 +195,7 @@ def _uneven_rank(rank, world, port, p, t, w, frac, q):
     from comapreduce_amd.mapmaking.destriper import DeviceDestriper
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
+    os.environ['COMAP_DS_RANKS'] = 'shard'    # the sharded CG (small problems are gathered by default)
     torch.cuda.set_device(0)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     no = t.shape[-1] // L
@@ -229,6 +232,60 @@ def test_two_ranks_uneven_split_matches_single_rank(nb):
     assert rel(x, ref['x'].cpu().numpy()) < 1e-9
     for k in ('map', 'naive', 'weight', 'hits'):
         assert rel(res[0][3][k], ref['maps'][k].cpu().numpy()) < 1e-9, k
+
+
+def _gather_rank(rank, world, port, p, t, w, keep, policy, q):
+    import torch
+    import torch.distributed as dist
+    from comapreduce_amd.mapmaking.destriper import DeviceDestriper
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    os.environ['COMAP_DS_RANKS'] = policy
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    no = t.shape[-1] // L
+    lo, hi = (no * rank // world), (no * (rank + 1) // world)
+    k = None if keep is None else keep[:, lo:hi]
+    prob = DeviceDestriper(p[lo * L:hi * L], t[..., lo * L:hi * L], w[..., lo * L:hi * L], L, NPIX, device=0, keep=k)
+    res = prob.solve(1e-6, 100)
+    q.put((rank, prob.gathered is not None, None if prob.plan is None else prob.plan['mode'], res['x'].cpu().numpy(),
+           res['iters'], {kk: v.cpu().numpy() for kk, v in res['maps'].items()}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('nb,policy', [(1, 'auto'), (4, 'auto'), (3, 'gather')])
+def test_two_ranks_gathered_solve_equals_single_rank(nb, policy):
+    """A problem the rank model (mapmaking/rankplan.py) finds latency-bound across ranks
+    -- the golden pointing, 40k samples -- is gathered to rank 0 and solved there alone:
+    every rank's offsets and the maps equal the single-rank native solve bit for bit
+    (same operator, same order), on 2 gloo ranks; 3 bands exercise the padded band."""
+    import torch.multiprocessing as mp
+    from comapreduce_amd.mapmaking.destriper import DeviceDestriper
+    p, tods, ws, keep = _bands_problem(4)
+    if nb == 1:
+        t, w, keep = tods[0], ws[0], None
+    else:
+        t, w, keep = tods[:nb], ws[:nb], keep[:nb].astype(np.uint8)
+    ref = DeviceDestriper(p, t, w, L, NPIX, keep=keep).solve(1e-6, 100)
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = 29100 + os.getpid() % 190
+    procs = [ctx.Process(target=_gather_rank, args=(r, 2, port, p, t, w, keep, policy, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=240) for _ in range(2)], key=lambda r: r[0])
+    for pr in procs:
+        pr.join(timeout=60)
+    for rank, gathered, mode, x, it, maps in res:
+        assert gathered, rank
+        if policy == 'auto':
+            assert mode == 'gather'
+        assert it == ref['iters']
+        for k in ('map', 'naive', 'weight', 'hits'):
+            assert np.array_equal(maps[k], ref['maps'][k].cpu().numpy()), (rank, k)
+    x = np.concatenate([res[0][3], res[1][3]], axis=-1)
+    assert np.array_equal(x, ref['x'].cpu().numpy())
 
 
 # ---------------------------------------------------------------- batched bands
