@@ -95,7 +95,7 @@ struct comap_destriper {
     int64_t nh = 0;
     int32_t *perm = nullptr;       // [NO] internal offset position -> caller's offset (NULL: identity)
     int32_t *flags_host = nullptr; // pinned [2 + 2 nb]
-    double *thr_host = nullptr;    // pinned [1]
+    double *thr_host = nullptr;    // pinned [1 + 4 nb]: threshold, then a copy of scal's rr0 .. rr_new
     hipStream_t cs = nullptr;      // CG stream (graph capture needs a non-default stream)
     hipEvent_t ev = nullptr;
     hipGraphExec_t batch = nullptr;   // kCgBatch iterations
@@ -370,7 +370,7 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
                                                  const int64_t *__restrict__ orow, int32_t *__restrict__ opix,
                                                  double *__restrict__ ow, uint8_t *__restrict__ ocnt,
                                                  int32_t *__restrict__ ekey, int32_t *__restrict__ eval,
-                                                 int32_t *__restrict__ eoff)
+                                                 int32_t *__restrict__ eoff, uint64_t *__restrict__ epay)
 {
 #pragma clang fp contract(off)
     const int lane = threadIdx.x & 63;
@@ -381,12 +381,20 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
     constexpr int32_t kNone = INT32_MIN;    // lanes past the offset's end (real pixels are >= -1)
     int32_t q[K];
     unsigned long long rem[K];
+    // the offset's weights, staged in LDS by coalesced loads: the group sums below read
+    // their members from here instead of one dependent global load per member (the count
+    // pass took 3.2 ms at C5 with 4 bands, 80 % of its wave cycles waiting)
+    __shared__ double wsh[4][K * 64 * NB];
+    double *wl = wsh[threadIdx.x >> 6];
 #pragma unroll
     for (int m = 0; m < K; ++m) {
         const int j = lane + 64 * m;
         q[m] = j < L ? pix[base + j] : kNone;
         rem[m] = __ballot(j < L);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) wl[(64 * m + lane) * NB + b] = j < L ? w[(int64_t)b * N + base + j] : 0.0;
     }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // the staged weights, before other lanes read them
     // leader loop: head lanes and their members (per chunk of the leader)
     bool head[K];
     unsigned long long mem[K][K];
@@ -430,7 +438,7 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
 #pragma unroll
                 for (int c = 0; c < K; ++c)
                     for (unsigned long long bits = mem[m][c]; bits; bits &= bits - 1) {
-                        const double v = w[(int64_t)b * N + base + 64 * c + (__ffsll((long long)bits) - 1)];
+                        const double v = wl[(64 * c + (__ffsll((long long)bits) - 1)) * NB + b];
                         s += v;
                         nz += v != 0.0;
                     }
@@ -451,7 +459,7 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
             const int j = lane + 64 * m;
 #pragma unroll
             for (int b = 0; b < NB; ++b) {
-                wi[m][b] = j < L ? w[(int64_t)b * N + base + j] : 0.0;
+                wi[m][b] = wl[(64 * m + lane) * NB + b];
                 ti[m][b] = j < L ? tod[(int64_t)b * N + base + j] : 0.0;
             }
             if (j < L) {
@@ -506,8 +514,15 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
                 const int64_t ei = e + __popcll(bm & ((1ull << lane) - 1ull));
                 opix[ei] = q[m];
                 if constexpr (CF) {
+                    // the transpose sorts (pixel, offset << 32 | counts) pairs: its pixel-major
+                    // entries come out of the sort whole, no gather by entry id
+                    uint32_t pk = 0;
 #pragma unroll
-                    for (int b = 0; b < NB; ++b) ocnt[ei * NB + b] = (uint8_t)gc[m][b];
+                    for (int b = 0; b < NB; ++b) {
+                        ocnt[ei * NB + b] = (uint8_t)gc[m][b];
+                        pk |= (uint32_t)gc[m][b] << (8 * b);
+                    }
+                    epay[ei] = ((uint64_t)(uint32_t)k << 32) | pk;
                 } else {
 #pragma unroll
                     for (int b = 0; b < NB; ++b) ow[ei * NB + b] = gs[m][b];
@@ -525,12 +540,12 @@ template <int NB, bool FILL, bool CF>
 void launch_rows(int L, hipStream_t st, const int32_t *pix, const double *w, const double *tod, int64_t N,
                  int64_t NO, int64_t npix, const int32_t *perm, int64_t *cnt, double *ws, double *tw, double *payload,
                  int32_t *skey, int32_t *sval, double *wbar, int32_t *nonuni, const int64_t *orow, int32_t *opix,
-                 double *ow, uint8_t *ocnt, int32_t *ekey, int32_t *eval, int32_t *eoff)
+                 double *ow, uint8_t *ocnt, int32_t *ekey, int32_t *eval, int32_t *eoff, uint64_t *epay = nullptr)
 {
     const unsigned blocks = (unsigned)((NO + 3) / 4);
 #define COMAP_ROWS(K) k_ds_rows<K, NB, FILL, CF><<<blocks, 256, 0, st>>>(pix, w, tod, N, NO, L, npix, perm, cnt, ws, \
                                                                           tw, payload, skey, sval, wbar, nonuni, orow, \
-                                                                          opix, ow, ocnt, ekey, eval, eoff)
+                                                                          opix, ow, ocnt, ekey, eval, eoff, epay)
     if (L <= 64) COMAP_ROWS(1);
     else if (L <= 128) COMAP_ROWS(2);
     else COMAP_ROWS(4);
@@ -586,6 +601,22 @@ __global__ void k_pixel_entries(const int32_t *__restrict__ sval, const int64_t 
             ldb<NB>(ow + (int64_t)e * NB, v);
             stb<NB>(pw + k * NB, v);
         }
+    }
+}
+
+// count form: pixel-major entries straight from the sorted (offset << 32 | counts) values
+template <int NB>
+__global__ void k_pixel_entries_cf(const uint64_t *__restrict__ pay, const int64_t *__restrict__ nnzp_dev,
+                                   int32_t *__restrict__ poff, uint8_t *__restrict__ pcnt)
+{
+    const int64_t nnzp = *nnzp_dev;
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < nnzp; k += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t v = pay[k];
+        poff[k] = (int32_t)(v >> 32);
+        const uint32_t c = (uint32_t)v;
+        if constexpr (NB == 4) *reinterpret_cast<uint32_t *>(pcnt + k * 4) = c;
+        else if constexpr (NB == 2) *reinterpret_cast<uint16_t *>(pcnt + k * 2) = (uint16_t)c;
+        else pcnt[k] = (uint8_t)c;
     }
 }
 
@@ -788,67 +819,76 @@ __global__ void __launch_bounds__(256) k_ds_project(const int64_t *__restrict__ 
     double acc[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) acc[b] = 0.0;
-#if COMAP_DS_XCD
-    // each logical block takes a contiguous run of offset sweeps (time-contiguous samples)
-    const int64_t sweeps = (NO + kPer - 1) / kPer, per = (sweeps + gridDim.x - 1) / gridDim.x;
-    const int64_t s0 = xcd_block(blockIdx.x, gridDim.x) * per, s1 = min(s0 + per, sweeps);
-    for (int64_t o0 = s0 * kPer; o0 < s1 * kPer; o0 += kPer) {
-#else
-    // the row bounds of the next sweep are loaded before this sweep's entries (one less
-    // dependent load per sweep)
-    int64_t nb0 = 0, nb1 = 0;
-    {
-        const int64_t o = (int64_t)blockIdx.x * kPer + threadIdx.x / G;
-        if (o < NO) { nb0 = orow[o]; nb1 = orow[o + 1]; }
-    }
-    for (int64_t o0 = (int64_t)blockIdx.x * kPer; o0 < NO; o0 += (int64_t)gridDim.x * kPer) {
-#endif
-        const int64_t o = o0 + threadIdx.x / G;
-        const bool valid = o < NO;
-#if COMAP_DS_XCD
-        const int64_t e0 = valid ? orow[o] : 0, e1 = valid ? orow[o + 1] : 0;
-#else
-        const int64_t e0 = nb0, e1 = nb1;
-        {
-            const int64_t on = o + (int64_t)gridDim.x * kPer;
-            nb0 = nb1 = 0;
-            if (on < NO) { nb0 = orow[on]; nb1 = orow[on + 1]; }
+    // Software pipeline over the block's sweeps (kPer offsets each): while this sweep's
+    // map gathers are in flight, the next sweep's first pass of entries (and the row
+    // bounds of the one after) are already being loaded -- a lane waits on one dependent
+    // latency per sweep instead of three.  Rows longer than one pass (G kProjU entries)
+    // finish with plain passes.
+    const int64_t stride = (int64_t)gridDim.x * kPer;
+    int64_t o = (int64_t)blockIdx.x * kPer + threadIdx.x / G;
+    int64_t b0 = 0, b1 = 0, nb0 = 0, nb1 = 0;
+    if (o < NO) { b0 = orow[o]; b1 = orow[o + 1]; }
+    if (o + stride < NO) { nb0 = orow[o + stride]; nb1 = orow[o + stride + 1]; }
+    int32_t cq[kProjU];
+    Coef<NB, CF> ca[kProjU];
+    auto load_pass = [&](int64_t e, int64_t e1, int32_t (&q)[kProjU], Coef<NB, CF> (&a)[kProjU]) {
+#pragma unroll
+        for (int u = 0; u < kProjU; ++u) {
+            const bool in = e + u * G < e1;
+            const int32_t pp = in ? opix[e + u * G] : (int32_t)(npix - 1);
+            q[u] = pp >= 0 ? pp : (int32_t)(npix - 1);   // m[-1] for off-map samples
+            if (in) a[u].load(ow, e + u * G);
+            else a[u] = Coef<NB, CF>();
         }
-#endif
+    };
+    auto gather = [&](const int32_t (&q)[kProjU], double (&mv)[kProjU][NB]) {
+#pragma unroll
+        for (int u = 0; u < kProjU; ++u) {
+            if (h) {
+#pragma unroll
+                for (int b = 0; b < NB; ++b) mv[u][b] = map_value(num, h, (int64_t)q[u] * NB + b);
+            } else {
+                ldb<NB>(num + (int64_t)q[u] * NB, mv[u]);
+            }
+        }
+    };
+    load_pass(b0 + sub, b1, cq, ca);
+    for (; o - threadIdx.x / G < NO; o += stride) {
+        const bool valid = o < NO;
+        const int64_t e0 = b0, e1 = b1;
         double g[NB];
 #pragma unroll
         for (int b = 0; b < NB; ++b) g[b] = 0.0;
-        for (int64_t e = e0 + sub; e < e1; e += G * kProjU) {
+        double mv[kProjU][NB];
+        gather(cq, mv);
+        // next sweep: its first pass of entries, and the row bounds of the sweep after it
+        int32_t nq[kProjU];
+        Coef<NB, CF> na[kProjU];
+        load_pass(nb0 + sub, nb1, nq, na);
+        b0 = nb0; b1 = nb1;
+        nb0 = nb1 = 0;
+        if (o + 2 * stride < NO) { nb0 = orow[o + 2 * stride]; nb1 = orow[o + 2 * stride + 1]; }
+#pragma unroll
+        for (int u = 0; u < kProjU; ++u)
+            if (e0 + sub + u * G < e1) {
+#pragma unroll
+                for (int b = 0; b < NB; ++b) g[b] = fma(ca[u].get(b), mv[u][b], g[b]);
+            }
+        for (int64_t e = e0 + sub + G * kProjU; e < e1; e += G * kProjU) {   // long rows
             int32_t q[kProjU];
-            double a[kProjU][NB], mv[kProjU][NB];
-#pragma unroll
-            for (int u = 0; u < kProjU; ++u) {
-                const bool in = e + u * G < e1;
-                const int32_t pp = in ? opix[e + u * G] : 0;
-                q[u] = pp >= 0 ? pp : (int32_t)(npix - 1);   // m[-1] for off-map samples
-                if (in) {
-                    ld_coef<NB, CF>(ow, e + u * G, a[u]);
-                } else {
-#pragma unroll
-                    for (int b = 0; b < NB; ++b) a[u][b] = 0.0;
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < kProjU; ++u) {
-                if (h) {
-#pragma unroll
-                    for (int b = 0; b < NB; ++b) mv[u][b] = map_value(num, h, (int64_t)q[u] * NB + b);
-                } else {
-                    ldb<NB>(num + (int64_t)q[u] * NB, mv[u]);
-                }
-            }
+            Coef<NB, CF> a[kProjU];
+            load_pass(e, e1, q, a);
+            double mw[kProjU][NB];
+            gather(q, mw);
 #pragma unroll
             for (int u = 0; u < kProjU; ++u)
                 if (e + u * G < e1) {
 #pragma unroll
-                    for (int b = 0; b < NB; ++b) g[b] = fma(a[u][b], mv[u][b], g[b]);
+                    for (int b = 0; b < NB; ++b) g[b] = fma(a[u].get(b), mw[u][b], g[b]);
                 }
         }
+#pragma unroll
+        for (int u = 0; u < kProjU; ++u) { cq[u] = nq[u]; ca[u] = na[u]; }
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
 #pragma unroll
@@ -1314,14 +1354,17 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     size_t sort_tb = 0, scan_tb = 0, scan32_tb = 0;
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tb, (int32_t *)nullptr, (int32_t *)nullptr,
                                              (int32_t *)nullptr, (int32_t *)nullptr, (int)N, 0, end_bit, st);
+    size_t sort64_tb = 0;   // the count form's transpose: (pixel, u64 offset|counts) pairs
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort64_tb, (int32_t *)nullptr, (int32_t *)nullptr,
+                                             (uint64_t *)nullptr, (uint64_t *)nullptr, (int)N, 0, end_bit, st);
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tb, (int64_t *)nullptr, (int64_t *)nullptr, (int)(NO + 1), st);
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan32_tb, (int32_t *)nullptr, (int32_t *)nullptr, (int)npix, st);
-    const size_t cub_tb = std::max({sort_tb, scan_tb, scan32_tb});
+    const size_t cub_tb = std::max({sort_tb, sort64_tb, scan_tb, scan32_tb});
     Arena ar;
     ar.cap = Arena::bytes<char>(cub_tb) + Arena::bytes<int64_t>(NO + 1) + 8 * Arena::bytes<int32_t>(N) +
              Arena::bytes<double>((size_t)N * 2 * NB) + Arena::bytes<int64_t>(npix + 1) +
              2 * Arena::bytes<int32_t>(npix) + Arena::bytes<int64_t>(2) + Arena::bytes<int32_t>(N) +
-             Arena::bytes<int32_t>(1);
+             Arena::bytes<int32_t>(1) + 2 * Arena::bytes<uint64_t>(N);
     COMAP_CHECK(ctx, comap_tmp_alloc((void **)&ar.base, ar.cap, st));
     struct ArenaFree {
         Arena *a;
@@ -1344,6 +1387,7 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     int32_t *hflag = ar.take<int32_t>(npix), *hpos = ar.take<int32_t>(npix);
     int64_t *counts = ar.take<int64_t>(2);
     int32_t *nonuni = ar.take<int32_t>(1);
+    uint64_t *epay = ar.take<uint64_t>(N), *epay2 = ar.take<uint64_t>(N);   // count form: offset << 32 | counts
     // ---- 1. spatial processing order of the offsets
     if (spatial) {
         k_offset_keys<<<grid_for(NO), 256, 0, st>>>(pix, NO, L, npix, ekey, eval);
@@ -1396,7 +1440,7 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     if (d->cf) {
         COMAP_NB_SWITCH(nb, (launch_rows<NB, true, true>(L, st, pix, w, tod, N, NO, npix, d->perm, nullptr, nullptr,
                                                          nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, d->orow,
-                                                         d->opix, nullptr, d->ocnt, ekey, eval, eoff)));
+                                                         d->opix, nullptr, d->ocnt, ekey, eval, eoff, epay)));
     } else {
         COMAP_NB_SWITCH(nb, (launch_rows<NB, true, false>(L, st, pix, w, tod, N, NO, npix, d->perm, nullptr, nullptr,
                                                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, d->orow,
@@ -1404,12 +1448,23 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     }
     COMAP_LAUNCH_CHECK(ctx);
     // ---- 4. pixel-major transpose (stable: offset order within a pixel)
-    COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(cub_tmp, sort_tb, ekey, ekey2, eval, eval2, (int)d->nnz, 0,
-                                                        end_bit, st));
+    if (d->cf) {
+        COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(cub_tmp, sort64_tb, ekey, ekey2, epay, epay2, (int)d->nnz,
+                                                            0, end_bit, st));
+    } else {
+        COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(cub_tmp, sort_tb, ekey, ekey2, eval, eval2, (int)d->nnz, 0,
+                                                            end_bit, st));
+    }
     k_rowptr<<<grid_for(npix + 1), 256, 0, st>>>(ekey2, d->nnz, npix, d->prow);
     COMAP_LAUNCH_CHECK(ctx);
-    COMAP_NB_SWITCH(nb, k_pixel_entries<NB><<<grid_for(d->nnz, 8192), 256, 0, st>>>(eval2, d->prow + npix, eoff, d->ow,
-                                                                                     d->ocnt, d->poff, d->pw, d->pcnt));
+    if (d->cf) {
+        COMAP_NB_SWITCH(nb, k_pixel_entries_cf<NB><<<grid_for(d->nnz, 8192), 256, 0, st>>>(epay2, d->prow + npix,
+                                                                                            d->poff, d->pcnt));
+    } else {
+        COMAP_NB_SWITCH(nb, k_pixel_entries<NB><<<grid_for(d->nnz, 8192), 256, 0, st>>>(eval2, d->prow + npix, eoff,
+                                                                                         d->ow, d->ocnt, d->poff, d->pw,
+                                                                                         d->pcnt));
+    }
     COMAP_LAUNCH_CHECK(ctx);
     k_hit_flags<<<grid_for(npix), 256, 0, st>>>(d->prow, npix, hflag);
     COMAP_LAUNCH_CHECK(ctx);
@@ -1715,7 +1770,7 @@ static int cg_setup(comap_destriper *d)
                    dalloc(ctx, &d->flags, 2 + 2 * nb)))
         return -2;
     if (!d->flags_host) COMAP_CHECK(ctx, hipHostMalloc((void **)&d->flags_host, 4 * (2 + 2 * nb), hipHostMallocDefault));
-    if (!d->thr_host) COMAP_CHECK(ctx, hipHostMalloc((void **)&d->thr_host, 8, hipHostMallocDefault));
+    if (!d->thr_host) COMAP_CHECK(ctx, hipHostMalloc((void **)&d->thr_host, 8 * (1 + 4 * nb), hipHostMallocDefault));
     if (!d->cs) COMAP_CHECK(ctx, hipStreamCreateWithFlags(&d->cs, hipStreamNonBlocking));
     if (!d->ev) COMAP_CHECK(ctx, hipEventCreateWithFlags(&d->ev, hipEventDisableTiming));
     if (!cg_use_graph(d)) return 0;
@@ -1765,8 +1820,16 @@ extern "C" int comap_destripe_solve(comap_destriper *d, double threshold, int32_
     COMAP_CHECK(ctx, hipMemcpyAsync(d->scal + nb, d->scal, 8 * nb, hipMemcpyDeviceToDevice, st));
     COMAP_CHECK(ctx, hipMemcpyAsync(d->scal + 3 * nb, d->scal, 8 * nb, hipMemcpyDeviceToDevice, st));   // current rr
     for (int i = 0; i < 2 + 2 * nb; ++i) d->flags_host[i] = 0;
+    // Batches of kCgBatch iterations between host checks; after the first, the next batch
+    // is sized from each running band's convergence rate over the last batch (delta =
+    // rr / rr0 falls geometrically), so a solve that needs 2 more iterations does not
+    // enqueue 14 no-op ones (4 launches each).  The iterates are unchanged: every
+    // kernel still stops on the device flags.
+    double *hs = d->thr_host + 1;                       // rr0 [nb] | rr [nb] | pq [nb] | rr_new [nb]
+    std::vector<double> prev_delta(nb, -1.0);
+    int next = kCgBatch;
     for (int enq = 0; enq < niter;) {
-        const int k = std::min(kCgBatch, niter - enq);
+        const int k = std::min(next, niter - enq);
         if (k == kCgBatch && d->batch) {
             COMAP_CHECK(ctx, hipGraphLaunch(d->batch, st));
         } else {
@@ -1775,8 +1838,23 @@ extern "C" int comap_destripe_solve(comap_destriper *d, double threshold, int32_
         }
         enq += k;
         COMAP_CHECK(ctx, hipMemcpyAsync(d->flags_host, d->flags, 4 * (2 + 2 * nb), hipMemcpyDeviceToHost, st));
+        COMAP_CHECK(ctx, hipMemcpyAsync(hs, d->scal, 8 * 4 * (size_t)nb, hipMemcpyDeviceToHost, st));
         COMAP_CHECK(ctx, hipStreamSynchronize(st));
         if (d->flags_host[0]) break;
+        next = kCgBatch;
+        if (threshold > 0) {
+            int est = 0;
+            for (int b = 0; b < nb; ++b) {
+                if (d->flags_host[2 + b]) continue;
+                const double delta = hs[3 * nb + b] / hs[b];
+                const double pd = prev_delta[b] > 0 ? prev_delta[b] : 1.0;
+                prev_delta[b] = delta;
+                if (!(delta > 0) || !(delta < pd)) { est = kCgBatch; break; }
+                const double need = std::log(threshold / delta) / (std::log(delta / pd) / k);
+                est = std::max(est, (int)std::ceil(std::max(need, 0.0)) + 1);
+            }
+            next = std::max(1, std::min(kCgBatch, est));
+        }
     }
     if (iters_out)
         for (int b = 0; b < nb; ++b) iters_out[b] = d->flags_host[2 + nb + b];

@@ -405,26 +405,6 @@ __global__ void k_fit_from_median(const int32_t *__restrict__ units, const int32
     o[kChannels + c] = 0.0;
 }
 
-// per (unit, channel) offset/slope L1AGC subtracts: the unit's scan fit, or
-// (nanmedian, 0) for calibrator sources (remove_atmosphere, :647-648)
-__global__ void k_gather_oa(const int32_t *__restrict__ units, const double *__restrict__ fit, int F, int U,
-                            const float *__restrict__ med, double *__restrict__ oa)
-{
-    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (i >= (int64_t)U * kBC) return;
-    const int u = (int)(i / kBC), bc = (int)(i % kBC);
-    const int f = units[4 * u], s = units[4 * u + 1];
-    const int b = bc / kChannels, c = bc % kChannels;
-    if (med) {
-        oa[2 * i] = (double)med[i];
-        oa[2 * i + 1] = 0.0;
-    } else {
-        const double *o = fit + (((int64_t)s * F + f) * kBands + b) * 2 * kChannels;
-        oa[2 * i] = o[c];
-        oa[2 * i + 1] = o[kChannels + c];
-    }
-}
-
 // ------------------------------------------------------------------ atmosphere fit
 // AtmosphereRemoval.fit_atmosphere (Level1Averaging.py:197-227): the
 // block-diagonal spsolve is an independent 2x2 normal-equation solve per
@@ -457,22 +437,31 @@ __global__ void k_atmos_fit(const int32_t *__restrict__ units, const double *__r
 // normalise_data (Level1Averaging.py:667-679): rms from the pass-A moments for
 // the fit slope a; pass-B coefficients alpha_c = 1/rms on the median
 // channels; per (unit, band): beta = sum alpha o, gamma = sum alpha a, N.
+// Also gathers the (unit, channel) offsets / slopes L1AGC subtracts (k_gather_oa's job:
+// the unit's scan fit, or (nanmedian, 0) for calibrators) into oa for k_coef_d, and
+// block 0 clears the pass-D mismatch flag -- two launches fewer per step.
 __global__ void __launch_bounds__(256) k_coef_b(const int32_t *__restrict__ units, const double *__restrict__ us,
                                                 const double *__restrict__ mom, int64_t UC,
-                                                const double *__restrict__ oa,
+                                                const double *__restrict__ fit, int F, const float *__restrict__ med,
+                                                double *__restrict__ oa,
                                                 double *__restrict__ alpha, double *__restrict__ nf,
-                                                double *__restrict__ bsum)
+                                                double *__restrict__ bsum, int32_t *__restrict__ flag)
 {
     __shared__ double red[4];
     const int ub = blockIdx.x;
     const int u = ub / kBands, b = ub % kBands;
     const int n = units[4 * u + 3];
+    if (ub == 0 && threadIdx.x == 0) *flag = 0;
+    const int fu = units[4 * u], su = units[4 * u + 1];
+    const double *fo = fit + (((int64_t)su * F + fu) * kBands + b) * 2 * kChannels;
     const double *q = us + 8 * (int64_t)u;
     const double sv = q[3], svv = q[4], n4 = q[5];
     double beta = 0, gamma = 0, cnt = 0;
     for (int c = threadIdx.x; c < kChannels; c += blockDim.x) {
         const int64_t i = (int64_t)u * kBC + b * kChannels + c;
-        const double o = oa[2 * i], a = oa[2 * i + 1];
+        const double o = med ? (double)med[i] : fo[c], a = med ? 0.0 : fo[kChannels + c];
+        oa[2 * i] = o;
+        oa[2 * i + 1] = a;
         double rms = NAN;
         if (n4 > 0 && isfinite(o) && isfinite(a)) {
             const double su = mom[2 * UC + i], suu = mom[3 * UC + i], suv = mom[4 * UC + i];
@@ -1187,7 +1176,12 @@ __global__ void __launch_bounds__(256) k_vane(const float *__restrict__ tod, int
     }
     if (side == 1) s_cold[threadIdx.x & 127] = mean;
     __syncthreads();
-    if (side == 1 || !live || h1 == h0) return;   // no hot/cold found (RuntimeError path): leave zeros
+    if (side == 1 || !live) return;
+    if (h1 == h0) {                                // no hot/cold found (RuntimeError path): zeros
+        gain[row] = 0.0;
+        tsys[row] = 0.0;
+        return;
+    }
     const float mc = s_cold[threadIdx.x];
     const float d = mean - mc;
     const double g = (double)d / (t_hot - 2.73);
@@ -1745,14 +1739,11 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
         k_zero_gaps<<<dim3(gx, (unsigned)p->n_gaps), 256, 0, st>>>(p->gaps, p->T, p->F, tod_out, orig_out, w_out);
         COMAP_LAUNCH_CHECK(ctx);
     }
-    k_gather_oa<<<(UC + 255) / 256, 256, 0, st>>>(p->units, fit, p->F, p->U, cmed, p->oa);
-    COMAP_LAUNCH_CHECK(ctx);
-    PROF(p, KV_COEF_B, k_coef_b<<<UB, 256, 0, st>>>(p->units, p->unit_sums, p->mom, UC, p->oa, p->alpha, p->nf,
-                                                    p->bsum));
+    PROF(p, KV_COEF_B, k_coef_b<<<UB, 256, 0, st>>>(p->units, p->unit_sums, p->mom, UC, fit, p->F, cmed, p->oa,
+                                                    p->alpha, p->nf, p->bsum, p->flag));
     COMAP_LAUNCH_CHECK(ctx);
     PROF(p, KV_GAIN_WEIGHTS, k_gain_weights<<<p->F, 1024, 0, st>>>(tsys0, p->gw, p->gmode));
     COMAP_LAUNCH_CHECK(ctx);
-    COMAP_CHECK(ctx, hipMemsetAsync(p->flag, 0, 4, st));
     auto coef_d = [&](int phase) {
         k_coef_d<<<UB, 256, 0, st>>>(p->units, p->unit_sums, p->mom, UC, p->oa, p->alpha, p->nf, p->bsum, p->ssum,
                                      p->sdm, tsys0, gain0, p->gw, p->gmode, calibrator, p->kap, p->dsum, p->xreg,
@@ -1861,8 +1852,6 @@ extern "C" int comap_l1_vane(comap_l1_plan *p, int64_t vstart, int64_t vlen, con
     const int32_t *dc = (const int32_t *)(p->vane_dev + off_c);
     const int64_t *dho = (const int64_t *)(p->vane_dev + off_ho);
     const int64_t *dco = (const int64_t *)(p->vane_dev + off_co);
-    COMAP_CHECK(ctx, hipMemsetAsync(tsys, 0, (size_t)FB * kChannels * 8, vs));
-    COMAP_CHECK(ctx, hipMemsetAsync(gain, 0, (size_t)FB * kChannels * 8, vs));
     const int64_t rows = (int64_t)FB * kChannels;
     PROF_ON(p, KV_VANE, vs, k_vane<<<(rows + 127) / 128, 256, 0, vs>>>(p->tod, p->T, p->F, vstart, dh, dho, dc, dco,
                                                                       t_hot, tsys, gain));

@@ -121,9 +121,10 @@ __device__ __forceinline__ double seg_elem(const MedJob &job, const int32_t *__r
 }
 
 // Per-series range of the u64 keys (kr[2j] = min, kr[2j+1] = max), one workgroup per series.
+// (also clears the job's re-sort flag for k_med_fix: no separate memset launch)
 __global__ void __launch_bounds__(256) k_med_range(const MedJob *__restrict__ jobs, const int32_t *__restrict__ seg,
                                                    int32_t njobs, int32_t w, unsigned long long *__restrict__ kr,
-                                                   const int32_t *__restrict__ slo)
+                                                   const int32_t *__restrict__ slo, int32_t *__restrict__ flag = nullptr)
 {
     __shared__ unsigned long long s_lo[4], s_hi[4];
     const int jb = blockIdx.x;
@@ -153,6 +154,7 @@ __global__ void __launch_bounds__(256) k_med_range(const MedJob *__restrict__ jo
         }
         kr[2 * jb] = lo;
         kr[2 * jb + 1] = hi;
+        if (flag) flag[jb] = 0;
     }
 }
 
@@ -1348,14 +1350,13 @@ int comap_median_run(comap_ctx *ctx, MedPlan *mp, hipStream_t st)
         uint32_t *k0 = (uint32_t *)mp->k0, *k1 = (uint32_t *)mp->k1;
         int32_t *flag = mp->redo, *beg = mp->redo + mp->njobs, *end = beg + mp->njobs;
         unsigned long long *kr = (unsigned long long *)mp->krange;
-        k_med_range<<<mp->njobs, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, kr, mp->slo);
+        k_med_range<<<mp->njobs, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, kr, mp->slo, flag);
         COMAP_LAUNCH_CHECK(ctx);
         k_med_keys<uint32_t><<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, k0, mp->v0, kr, mp->slo,
                                                  mp->pbits);
         COMAP_LAUNCH_CHECK(ctx);
         COMAP_CHECK(ctx, seg_sort(mp->temp, tb, (const uint32_t *)k0, k1, mp->v0, mp->v1, (int)mp->nitems, mp->njobs,
                                   mp->seg, mp->seg + 1, st, mp->wide, (unsigned)mp->pbits));
-        COMAP_CHECK(ctx, hipMemsetAsync(flag, 0, 4 * (size_t)mp->njobs, st));
         k_med_fix<<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, k1, mp->v1, flag, mp->slo);
         COMAP_LAUNCH_CHECK(ctx);
         // the flagged segments (if any) again on exact 64-bit keys; the rest are empty ranges

@@ -188,7 +188,7 @@ def read_comap_data(filelist, map_info, feed_weights=None, iband=0, use_gain_fil
 
 def read_comap_data_bands(filelist, map_info, bands=(0, 1, 2, 3), use_gain_filter=True, offset_length=50,
                           feeds=[i + 1 for i in range(19)], calibration=False, calibrator='TauA', healpix=False,
-                          store=None, device=None, device_outputs=False):
+                          store=None, device=None, device_outputs=False, pointing=None):
     """read_comap_data for several bands at once, for the batched destriper
     (run_destriper.py:146-189 calls read_comap_data once per band on the same
     files; only tod and weights depend on the band).  One device prep for all
@@ -206,14 +206,15 @@ def read_comap_data_bands(filelist, map_info, bands=(0, 1, 2, 3), use_gain_filte
     Returns dict: tod, weights [nb, N]; keep uint8 [nb, N/L]; pointing, az, el,
     ra, dec, feedid, obsids [N]; remapping_array (unique pixels of the union).
     NumPy arrays, or torch CUDA tensors with device_outputs (remapping_array
-    stays NumPy)."""
+    stays NumPy).  ``pointing``: prep.precompute_pointing's result for these files
+    (the az / el percentiles computed ahead, e.g. beside the Level-1 reduction)."""
     import torch
     from . import prep
     open_file = _opener(store)
     bands = tuple(int(b) for b in bands)
     files = [open_file(fn) for fn in filelist]
     flat = prep.prep_flat(files, filelist, map_info, bands, use_gain_filter, offset_length, feeds, calibration,
-                          calibrator, device, healpix)
+                          calibrator, device, healpix, pointing)
     cut, keep = prep.cut_flat(flat, len(bands), offset_length)
     del flat
     mark = prep._Phases(torch, cut.tod.device)

@@ -109,8 +109,51 @@ def _feed_rows(file_feeds, selected_feeds):
     return GetFeeds(file_feeds, selected_feeds)
 
 
+def _live_rows(f, feeds):
+    """(file feed rows read for each output row, -1 = skipped) for the feeds read_comap_data
+    keeps (COMAPData.py:300-318: flag bits other than 0 and 5 drop a feed)."""
+    from .comapdata import feed_is_bad
+    file_feeds = np.asarray(_host(f['spectrometer/feeds'])).astype(np.int64)
+    fi, oi = _feed_rows(file_feeds, feeds)
+    bad = f.attrs('comap')['bad_observation']
+    row_src = np.full(len(oi), -1, np.int32)
+    for ff, of in zip(fi, oi):
+        if not feed_is_bad(bad[file_feeds[ff]]):
+            row_src[of] = ff
+    return row_src
+
+
+def precompute_pointing(files, filelist, feeds, device=None):
+    """The pointing-only part of the data prep -- the az / el percentile bands of every
+    kept feed row (COMAPData.py:338-346) -- enqueued on the caller's current stream, so
+    it can run beside other work (bench.py's chain: beside the Level-1 reduction's
+    tail, on a side stream).  Pass the result to read_comap_data_bands(pointing=...).
+    Returns {filename: (row_src, row_pct [rows, 4] device tensor, event, inputs)}."""
+    import torch
+    dev = torch.device('cuda', N.current_device() if device is None else int(device))
+    c = N.ctx(dev.index)
+    N.bind_stream(c, dev)
+    out = {}
+    for fn, f in zip(filelist, files):
+        row_src = _live_rows(f, feeds)
+        live = np.flatnonzero(row_src >= 0)
+        if live.size == 0:
+            continue
+        az = _dev(torch, f['spectrometer/pixel_pointing/pixel_az'], dev, torch.float64)
+        el = _dev(torch, f['spectrometer/pixel_pointing/pixel_el'], dev, torch.float64)
+        T = int(az.shape[-1])
+        pr, = _dev_pack(torch, dev, (row_src[live].astype(np.int32),))
+        pct = torch.zeros((live.size, 4), dtype=torch.float64, device=dev)
+        N.check(N.lib().comap_prep_percentiles(c, N.dptr(az), N.dptr(el), T, N.dptr(pr), int(live.size), T,
+                                               N.dptr(pct)), c, 'comap_prep_percentiles')
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        out[fn] = (row_src, pct, ev, (az, el, pr))
+    return out
+
+
 def prep_flat(files, filelist, map_info, bands, use_gain_filter, offset_length, feeds, calibration, calibrator,
-              device, healpix=False):
+              device, healpix=False, pointing=None):
     """read_comap_data's vectors for every band in ``bands`` before the NaN and
     empty-offset cuts (get_tod + read_pixels for every file, high-pass included).
     Returns FlatArrays on the device."""
@@ -204,10 +247,16 @@ def prep_flat(files, filelist, map_info, bands, use_gain_filter, offset_length, 
             row_w[:, :nb] = wl
         elif live.size:
             row_w[dlive, :nb] = wl
-        # az / el percentile band per row (COMAPData.py:338-346)
-        pct = torch.zeros((max(1, live.size), 4), dtype=torch.float64, device=dev)
-        N.check(lib.comap_prep_percentiles(c, N.dptr(az), N.dptr(el), T, N.dptr(pr), int(live.size), T,
-                                           N.dptr(pct)), c, 'comap_prep_percentiles')
+        # az / el percentile band per row (COMAPData.py:338-346), or the precomputed one
+        pre = pointing.get(fn) if pointing else None
+        if pre is not None and np.array_equal(pre[0], row_src):
+            torch.cuda.current_stream(dev).wait_event(pre[2])
+            pct = pre[1]
+            pct.record_stream(torch.cuda.current_stream(dev))   # allocated on the precompute's stream
+        else:
+            pct = torch.zeros((max(1, live.size), 4), dtype=torch.float64, device=dev)
+            N.check(lib.comap_prep_percentiles(c, N.dptr(az), N.dptr(el), T, N.dptr(pr), int(live.size), T,
+                                               N.dptr(pct)), c, 'comap_prep_percentiles')
         if live.size == nrow:
             row_pct = pct
         else:

@@ -119,7 +119,8 @@ int comap_l1_atmosphere(comap_l1_plan *plan, const int32_t *const_el_units_host,
  * NaN samples inside the units are replaced IN PLACE in the device cube by
  * their channel's scan nanmedian (fill_bad_data) before the reduction.
  * Outputs dev f64 [F][4][T]: tod (gain-subtracted residual), tod_original,
- * weights.  Samples outside the units are left untouched (caller zeroes). */
+ * weights.  Samples no unit of the plan covers (scan gaps, a C3 shard's foreign
+ * units) are set to 0 here, so the outputs may be allocated uninitialised. */
 int comap_l1_average(comap_l1_plan *plan, const double *fit_values_dev,
                      const double *tsys0_dev, const double *gain0_dev, int32_t calibrator,
                      double *tod_out_dev, double *orig_out_dev, double *weights_out_dev);
