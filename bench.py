@@ -449,6 +449,35 @@ def chain_leg(data, device, l1_bytes, reps=3):
     with a device sync at every phase boundary gives the phase breakdown.  Roofline: the
     L1 passes' design bytes + the operator bytes of every CG iteration, over the wall."""
     import torch
+    chain = chain_fn(data, device)
+    chain(False)                                   # warm the prep / set-up paths
+    phases = chain(True)
+    walls = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        info = chain(False)
+        torch.cuda.synchronize()
+        walls.append((time.perf_counter() - t0) * 1e3)
+        assert np.isfinite(info['maps']['map']).all(), 'chain maps not finite'
+    wall = sorted(walls)[len(walls) // 2]
+    algo = l1_bytes + info['op_bytes'] * max(info['iters'])
+    return {'config': 'north_star chain, 1 GPU: C2 resident cube -> vane + atmosphere + L1AveragingGainCorrection -> '
+                      'read_comap_data_bands (4 sidebands, device prep) -> batched destriper to threshold 1e-6 '
+                      '(max 100 it), L=50, 480x480 CAR -> 4 bands of maps on the host',
+            'reps': reps, 'wall_ms': wall, 'wall_ms_all': walls, 'iters': info['iters'],
+            'phases_synced_ms': {k: v for k, v in phases.items() if k.endswith('_ms')},
+            'phases_note': 'one extra chain with a device sync at every phase boundary (no overlap)',
+            'algo_bytes': algo, 'achieved_GBs': algo / (wall * 1e-3) / 1e9,
+            'roofline_frac': algo / (wall * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            'roofline_note': 'algorithmic bytes = the 3 L1 streaming passes (design bytes) + the batched operator '
+                             'bytes x CG iterations; prep, set-up and map copy move ~1.5 GB and count as overhead'}
+
+
+def chain_fn(data, device):
+    """The chain of chain_leg as a callable ``chain(sync) -> info`` (sync: a device
+    sync and a wall-clock mark at every phase boundary)."""
+    import torch
     from comapreduce_amd.mapmaking import comapdata as CD
     from comapreduce_amd.mapmaking import destriper as D
     from comapreduce_amd.mapmaking import prep as P
@@ -479,37 +508,14 @@ def chain_leg(data, device, l1_bytes, reps=3):
         prob = D.DeviceDestriper(r['pointing'].to(torch.int32), r['tod'], r['weights'], 50, 480 * 480,
                                  device=device, keep=r['keep'])
         mark('setup_ms')
-        res = prob.solve(threshold=1e-6, niter=100)
-        mark('solve_ms')
-        maps = D.maps_to_host(res['maps'])
-        mark('maps_to_host_ms')
-        assert all(np.isfinite(maps['map']).ravel()), 'chain maps not finite'
+        res = prob.solve(threshold=1e-6, niter=100, to_host=True)    # maps copied to the host
+        mark('solve_and_maps_ms')
+        ph['maps'] = res['maps']           # checked by the caller, outside the timed region
         ph['iters'] = res['iters']
         ph['op_bytes'] = operator_bytes(prob, int(r['tod'].shape[1]) // 50, 4)
         ph['n_samples_union'] = int(r['tod'].shape[1])
         return ph
-
-    chain(False)                                   # warm the prep / set-up paths
-    phases = chain(True)
-    walls = []
-    for _ in range(reps):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        info = chain(False)
-        torch.cuda.synchronize()
-        walls.append((time.perf_counter() - t0) * 1e3)
-    wall = sorted(walls)[len(walls) // 2]
-    algo = l1_bytes + info['op_bytes'] * max(info['iters'])
-    return {'config': 'north_star chain, 1 GPU: C2 resident cube -> vane + atmosphere + L1AveragingGainCorrection -> '
-                      'read_comap_data_bands (4 sidebands, device prep) -> batched destriper to threshold 1e-6 '
-                      '(max 100 it), L=50, 480x480 CAR -> 4 bands of maps on the host',
-            'reps': reps, 'wall_ms': wall, 'wall_ms_all': walls, 'iters': info['iters'],
-            'phases_synced_ms': {k: v for k, v in phases.items() if k.endswith('_ms')},
-            'phases_note': 'one extra chain with a device sync at every phase boundary (no overlap)',
-            'algo_bytes': algo, 'achieved_GBs': algo / (wall * 1e-3) / 1e9,
-            'roofline_frac': algo / (wall * 1e-3) / 1e9 / HBM_PEAK_GBS,
-            'roofline_note': 'algorithmic bytes = the 3 L1 streaming passes (design bytes) + the batched operator '
-                             'bytes x CG iterations; prep, set-up and map copy move ~1.5 GB and count as overhead'}
+    return chain
 
 
 def e2e_leg(F, T, device):

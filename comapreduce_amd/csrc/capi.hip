@@ -106,6 +106,93 @@ void comap_tmp_free(void *p)
     c.live.erase(it);
 }
 
+namespace {
+struct PinnedCache {
+    std::mutex mu;
+    std::map<size_t, std::vector<void *>> free;
+    std::map<void *, size_t> live;
+};
+PinnedCache &pinned_cache()
+{
+    static PinnedCache *c = new PinnedCache();
+    return *c;
+}
+struct StreamPool {
+    std::mutex mu;
+    std::map<int, std::vector<hipStream_t>> idle;
+    std::map<hipStream_t, int> dev_of;
+};
+StreamPool &stream_pool()
+{
+    static StreamPool *s = new StreamPool();
+    return *s;
+}
+}  // namespace
+
+hipError_t comap_pinned_alloc(void **p, size_t bytes)
+{
+    const size_t cls = tmp_class(bytes ? bytes : 1);
+    PinnedCache &c = pinned_cache();
+    {
+        std::lock_guard<std::mutex> lock(c.mu);
+        auto it = c.free.find(cls);
+        if (it != c.free.end() && !it->second.empty()) {
+            *p = it->second.back();
+            it->second.pop_back();
+            c.live[*p] = cls;
+            return hipSuccess;
+        }
+    }
+    const hipError_t e = hipHostMalloc(p, cls, hipHostMallocDefault);
+    if (e == hipSuccess) {
+        std::lock_guard<std::mutex> lock(c.mu);
+        c.live[*p] = cls;
+    }
+    return e;
+}
+
+void comap_pinned_free(void *p)
+{
+    if (!p) return;
+    PinnedCache &c = pinned_cache();
+    std::lock_guard<std::mutex> lock(c.mu);
+    auto it = c.live.find(p);
+    if (it == c.live.end()) return;
+    c.free[it->second].push_back(p);
+    c.live.erase(it);
+}
+
+hipError_t comap_stream_acquire(hipStream_t *s)
+{
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    StreamPool &sp = stream_pool();
+    {
+        std::lock_guard<std::mutex> lock(sp.mu);
+        auto &v = sp.idle[dev];
+        if (!v.empty()) {
+            *s = v.back();
+            v.pop_back();
+            return hipSuccess;
+        }
+    }
+    const hipError_t e = hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    if (e == hipSuccess) {
+        std::lock_guard<std::mutex> lock(sp.mu);
+        sp.dev_of[*s] = dev;
+    }
+    return e;
+}
+
+void comap_stream_release(hipStream_t s)
+{
+    if (!s) return;
+    StreamPool &sp = stream_pool();
+    std::lock_guard<std::mutex> lock(sp.mu);
+    auto it = sp.dev_of.find(s);
+    if (it != sp.dev_of.end()) sp.idle[it->second].push_back(s);
+}
+
 int comap_scratch(comap_ctx *ctx, size_t bytes, void **out)
 {
     if (bytes > ctx->scratch_bytes) {

@@ -62,6 +62,15 @@ hipMemPool_t comap_tmp_pool();
 // order: every user allocates and frees on one stream, or frees after a sync.
 hipError_t comap_tmp_alloc(void **p, size_t bytes, hipStream_t st);
 void comap_tmp_free(void *p);
+// Small pinned host blocks (CG flag / scalar read-back) through the same kind of cache:
+// hipHostMalloc costs 0.1-0.3 ms a call, once per destriper problem before this (r03l).
+hipError_t comap_pinned_alloc(void **p, size_t bytes);
+void comap_pinned_free(void *p);
+// Non-blocking streams for the current device, reused across objects (a problem's CG
+// stream): hipStreamCreate / hipStreamDestroy per destriper problem cost ~0.1 ms and a
+// device sync.  Released streams must be idle (the caller synchronised them).
+hipError_t comap_stream_acquire(hipStream_t *s);
+void comap_stream_release(hipStream_t s);
 
 struct DevTemps {
     std::vector<void *> p;

@@ -1260,10 +1260,14 @@ unsigned launch_project(const comap_destriper *d, hipStream_t st, const double *
     return pg;
 }
 
+// a problem's persistent buffers come from the cached device pool (comap_tmp_alloc) in
+// the context stream's order; comap_destripe_destroy returns them after a device sync
 template <typename T>
 int dalloc(comap_ctx *ctx, T **p, size_t n)
 {
-    COMAP_CHECK(ctx, hipMalloc((void **)p, sizeof(T) * (n ? n : 1)));
+    void *q = nullptr;
+    COMAP_CHECK(ctx, comap_tmp_alloc(&q, sizeof(T) * (n ? n : 1), ctx->stream));
+    *p = (T *)q;
     return 0;
 }
 
@@ -1499,16 +1503,17 @@ extern "C" int comap_destripe_destroy(comap_destriper *d)
 {
     if (!d) return 0;
     COMAP_DEVICE_GUARD(d->ctx);
-    if (d->cs) (void)hipStreamSynchronize(d->cs);
+    // every stream that may still read the buffers (the CG stream, the caller's) is idle
+    // after a device sync; the blocks then go back to the caches
+    (void)hipDeviceSynchronize();
     void *b[] = {d->orow, d->opix, d->ow, d->ws, d->tw, d->prow, d->poff, d->pw, d->h, d->hits, d->nnum, d->part, d->scal,
                  d->cg, d->flags, d->hrow, d->hprow, d->perm, d->ocnt, d->pcnt, d->wbar, d->pt};
-    for (void *p : b)
-        if (p) (void)hipFree(p);
-    if (d->flags_host) (void)hipHostFree(d->flags_host);
-    if (d->thr_host) (void)hipHostFree(d->thr_host);
+    for (void *p : b) comap_tmp_free(p);
+    comap_pinned_free(d->flags_host);
+    comap_pinned_free(d->thr_host);
     if (d->batch) (void)hipGraphExecDestroy(d->batch);
     if (d->ev) (void)hipEventDestroy(d->ev);
-    if (d->cs) (void)hipStreamDestroy(d->cs);
+    comap_stream_release(d->cs);
     delete d;
     return 0;
 }
@@ -1769,9 +1774,9 @@ static int cg_setup(comap_destriper *d)
     if (!d->cg && (dalloc(ctx, &d->cg, (4 * (size_t)d->NO + (size_t)d->npix) * nb) ||
                    dalloc(ctx, &d->flags, 2 + 2 * nb)))
         return -2;
-    if (!d->flags_host) COMAP_CHECK(ctx, hipHostMalloc((void **)&d->flags_host, 4 * (2 + 2 * nb), hipHostMallocDefault));
-    if (!d->thr_host) COMAP_CHECK(ctx, hipHostMalloc((void **)&d->thr_host, 8 * (1 + 4 * nb), hipHostMallocDefault));
-    if (!d->cs) COMAP_CHECK(ctx, hipStreamCreateWithFlags(&d->cs, hipStreamNonBlocking));
+    if (!d->flags_host) COMAP_CHECK(ctx, comap_pinned_alloc((void **)&d->flags_host, 4 * (2 + 2 * nb)));
+    if (!d->thr_host) COMAP_CHECK(ctx, comap_pinned_alloc((void **)&d->thr_host, 8 * (1 + 4 * nb)));
+    if (!d->cs) COMAP_CHECK(ctx, comap_stream_acquire(&d->cs));
     if (!d->ev) COMAP_CHECK(ctx, hipEventCreateWithFlags(&d->ev, hipEventDisableTiming));
     if (!cg_use_graph(d)) return 0;
     hipGraph_t g = nullptr;

@@ -1,19 +1,58 @@
 """The north_star chain leg (bench.chain_leg) alone, with the device prep's phase
 breakdown (COMAP_PREP_PROFILE=1) and the destriper's first-solve vs repeat-solve
 time, for kernel traces of the chain's non-L1 part:
-    python scripts/chain_prof.py [feeds]"""
+    python scripts/chain_prof.py [feeds]
+    python scripts/chain_prof.py --cprofile OUT.txt   (host cProfile of one unsynced chain)"""
 import json
 import os
 import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ.setdefault('COMAP_PREP_PROFILE', '1')
+if '--cprofile' not in sys.argv:
+    os.environ.setdefault('COMAP_PREP_PROFILE', '1')
 import bench  # noqa: E402
+
+
+def host_profile(path):
+    """cProfile one unsynced chain (after two warm ones): where the host spends the
+    wall clock the GPU timeline does not account for."""
+    import cProfile
+    import io
+    import pstats
+    import torch
+    torch.cuda.set_device(0)
+    data, sh = bench.build_observation(19, 180_000, obs_id=1, device=0)
+    chain = bench.chain_fn(data, 0)
+    for _ in range(2):
+        chain(False)
+    torch.cuda.synchronize()
+    walls = []
+    pr = cProfile.Profile()
+    for i in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if i == 2:
+            pr.enable()
+        chain(False)
+        torch.cuda.synchronize()
+        if i == 2:
+            pr.disable()
+        walls.append((time.perf_counter() - t0) * 1e3)
+    buf = io.StringIO()
+    st = pstats.Stats(pr, stream=buf)
+    st.sort_stats('cumulative').print_stats(60)
+    st.sort_stats('tottime').print_stats(40)
+    with open(path, 'w') as f:
+        f.write(f'walls_ms {walls}\n')
+        f.write(buf.getvalue())
+    print(json.dumps({'walls_ms': walls}), flush=True)
 
 
 def main():
     import torch
+    if len(sys.argv) > 2 and sys.argv[1] == '--cprofile':
+        return host_profile(sys.argv[2])
     from comapreduce_amd.mapmaking import comapdata as CD
     from comapreduce_amd.mapmaking import destriper as D
     from comapreduce_amd.mapmaking import prep

@@ -427,3 +427,26 @@ def test_entry_forms_vs_oracle(form, nb, monkeypatch):
         assert np.array_equal(m['weight'], ref['weight']) and np.array_equal(m['hits'], ref['hits'])
         assert rel(m['map'], ref['map']) < 1e-9, b
         assert rel(res['x'][b].cpu().numpy()[keep[b]], xr) < 1e-9, b
+
+
+@pytest.mark.parametrize('nb', [1, 3, 4])
+def test_solve_to_host_equals_device_maps(nb):
+    """solve(to_host=True) -- naive / weight / hits copied during the CG on a copy
+    stream, the map after it -- returns bit for bit what solve() + maps_to_host do."""
+    from comapreduce_amd.mapmaking.destriper import DeviceDestriper, maps_to_host
+    p, tods, ws, keep = _bands_problem(max(nb, 2))
+    if nb == 1:
+        args = (p, tods[0], ws[0], L, NPIX)
+        kw = {}
+    else:
+        args = (p, tods[:nb], ws[:nb], L, NPIX)
+        kw = {'keep': keep[:nb]}
+    dev = DeviceDestriper(*args, **kw).solve(1e-6, 100)
+    want = maps_to_host(dev['maps'])
+    got = DeviceDestriper(*args, **kw).solve(1e-6, 100, to_host=True)
+    assert got['iters'] == dev['iters']
+    assert np.array_equal(got['x'].cpu().numpy(), dev['x'].cpu().numpy())
+    assert set(got['maps']) == set(want)
+    for k, v in want.items():
+        assert got['maps'][k].shape == v.shape, k
+        assert np.array_equal(got['maps'][k], v), k
