@@ -452,6 +452,7 @@ def chain_leg(data, device, l1_bytes, reps=3):
     chain = chain_fn(data, device)
     chain(False)                                   # warm the prep / set-up paths
     phases = chain(True)
+    phases.pop('maps')
     walls = []
     for _ in range(reps):
         torch.cuda.synchronize()
@@ -459,7 +460,10 @@ def chain_leg(data, device, l1_bytes, reps=3):
         info = chain(False)
         torch.cuda.synchronize()
         walls.append((time.perf_counter() - t0) * 1e3)
-        assert np.isfinite(info['maps']['map']).all(), 'chain maps not finite'
+        # the job's output is consumed (checked) before the next job starts, so its pinned
+        # host block returns to torch's host cache; a map set still held when the next
+        # solve starts costs that solve a fresh 29 MB pinned allocation (~2.5 ms)
+        assert np.isfinite(info.pop('maps')['map']).all(), 'chain maps not finite'
     wall = sorted(walls)[len(walls) // 2]
     algo = l1_bytes + info['op_bytes'] * max(info['iters'])
     return {'config': 'north_star chain, 1 GPU: C2 resident cube -> vane + atmosphere + L1AveragingGainCorrection -> '

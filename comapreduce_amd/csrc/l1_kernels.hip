@@ -842,7 +842,6 @@ __global__ void __launch_bounds__(256) k_coef_d(const int32_t *__restrict__ unit
     __shared__ double red[4];
     __shared__ double s_kap[4][kChannels];     // alpha, kg, kr, ko (phase 0 channel list)
     const int ub = blockIdx.x;
-    if (phase == 2 && *flag == 0) return;          // legacy path only runs after a fused-path mismatch
     const int u = ub / kBands, b = ub % kBands;
     const int f = units[4 * u];
     const double *q = us + 8 * (int64_t)u;
@@ -1030,10 +1029,50 @@ __global__ void __launch_bounds__(256) k_gain_avg(const float *__restrict__ tod,
         }
 }
 
+// averaged_tod/weights = 1/auto_rms(residual)^2 per (band, scan)
+// (Level1Averaging.py:512-518, 867): nanstd of odd-even differences, ddof 0, over the
+// unit's n samples of one band, by one 256-thread block.
+__device__ __forceinline__ void scan_weight_band(const double *__restrict__ r, int n, double *__restrict__ wo,
+                                                 double *red)
+{
+    const int np = n / 2;
+    double s = 0, cnt = 0;
+    for (int k = threadIdx.x; k < np; k += blockDim.x) {
+        const double d = r[2 * k + 1] - r[2 * k];
+        if (!isnan(d)) { s += d; cnt += 1.0; }
+    }
+    s = block_sum256(s, red);
+    cnt = block_sum256(cnt, red);
+    const double mean = s / cnt;
+    double v = 0;
+    for (int k = threadIdx.x; k < np; k += blockDim.x) {
+        const double d = r[2 * k + 1] - r[2 * k];
+        if (!isnan(d)) v += (d - mean) * (d - mean);
+    }
+    v = block_sum256(v, red);
+    const double rms = sqrt(v / cnt) / sqrt(2.0);
+    const double wt = 1.0 / (rms * rms);
+    for (int t = threadIdx.x; t < n; t += blockDim.x) wo[t] = wt;
+}
+
+__global__ void __launch_bounds__(256) k_scan_weights(const int32_t *__restrict__ units, int64_t T,
+                                                      const double *__restrict__ tod_out, double *__restrict__ w_out)
+{
+    __shared__ double red[4];
+    const int ub = blockIdx.x;
+    const int u = ub / kBands, b = ub % kBands;
+    const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
+    const int64_t o = (int64_t)(f * kBands + b) * T + t0;
+    scan_weight_band(tod_out + o, n, w_out + o, red);
+}
+
 // Applies the per-band constants of k_coef_d phase 1 to the fused sums:
 //   dG    = Sg + sum_b (Dg0_b + A Dg1_b + mf_b Dg2_b)
 //   tod_b = (Sr_b + Dr0 + A Dr1 + mf Dr2 - dG SKr) / SW
 //   orig_b = (So_b + Do0 + A Do1 + mf Do2) / SWo
+// (Merging k_gain_avg into this kernel behind the flag branch -- one launch fewer --
+// cost far more than the launch: the pass-D body's registers and 32 KB of LDS ride on
+// every finish block, 103 -> 1448 us at C2, r03s2; reverted.)
 __global__ void __launch_bounds__(256) k_finish(const int32_t *__restrict__ units, const int32_t *__restrict__ tiles,
                                                 int64_t T, const double *__restrict__ A,
                                                 const double *__restrict__ mf, const double *__restrict__ dsum,
@@ -1065,38 +1104,6 @@ __global__ void __launch_bounds__(256) k_finish(const int32_t *__restrict__ unit
             orig_out[o] = (orig_out[o] + d[6] + a * d[7] + m[b] * d[8]) / d[11];
         }
     }
-}
-
-// ------------------------------------------------------------------ scan weights
-// averaged_tod/weights = 1/auto_rms(residual)^2 per (band, scan)
-// (Level1Averaging.py:512-518, 867): nanstd of odd-even differences, ddof 0.
-__global__ void __launch_bounds__(256) k_scan_weights(const int32_t *__restrict__ units, int64_t T,
-                                                      const double *__restrict__ tod_out, double *__restrict__ w_out)
-{
-    __shared__ double red[4];
-    const int ub = blockIdx.x;
-    const int u = ub / kBands, b = ub % kBands;
-    const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
-    const double *r = tod_out + (int64_t)(f * kBands + b) * T + t0;
-    const int np = n / 2;
-    double s = 0, cnt = 0;
-    for (int k = threadIdx.x; k < np; k += blockDim.x) {
-        const double d = r[2 * k + 1] - r[2 * k];
-        if (!isnan(d)) { s += d; cnt += 1.0; }
-    }
-    s = block_sum256(s, red);
-    cnt = block_sum256(cnt, red);
-    const double mean = s / cnt;
-    double v = 0;
-    for (int k = threadIdx.x; k < np; k += blockDim.x) {
-        const double d = r[2 * k + 1] - r[2 * k];
-        if (!isnan(d)) v += (d - mean) * (d - mean);
-    }
-    v = block_sum256(v, red);
-    const double rms = sqrt(v / cnt) / sqrt(2.0);
-    const double wt = 1.0 / (rms * rms);
-    double *wo = w_out + (int64_t)(f * kBands + b) * T + t0;
-    for (int t = threadIdx.x; t < n; t += blockDim.x) wo[t] = wt;
 }
 
 // ------------------------------------------------------------------ output gaps
@@ -1756,7 +1763,9 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
     // (regression sums) are software-pipelined over the unit groups on two streams:
     //   main: B0 B1 .. | wait M0: C0 | wait M1: C1 ..     side: wait B0: M0 | wait B1: M1 ..
     // so each group's median (latency-bound) runs under the next group's streaming pass.
-    hipStream_t side = p->side;
+    // one group: the median stays on the main stream -- the two cross-stream event hops
+    // cost ~20 us each at the C3 shard (r03s2 trace) and there is nothing to overlap
+    hipStream_t side = p->ngroups > 1 ? p->side : st;
     for (int g = 0; g < p->ngroups; ++g) {
         const int64_t t0 = p->grpb_tile0[g], nt = p->grpb_tile0[g + 1] - t0;
         const int ub0 = p->grp_u0[g] * kBands, nub = (p->grp_u0[g + 1] - p->grp_u0[g]) * kBands;
@@ -1764,18 +1773,20 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
                                                                         p->T, p->dlist, p->dcnt, p->dw, p->bsum,
                                                                         p->mb, tod_out, orig_out, p->dG));
         COMAP_LAUNCH_CHECK(ctx);
-        COMAP_CHECK(ctx, hipEventRecord(p->ev_b[g], st));
-        COMAP_CHECK(ctx, hipStreamWaitEvent(side, p->ev_b[g], 0));
+        if (side != st) {
+            COMAP_CHECK(ctx, hipEventRecord(p->ev_b[g], st));
+            COMAP_CHECK(ctx, hipStreamWaitEvent(side, p->ev_b[g], 0));
+        }
         PROF_ON(p, KV_MEDIAN, side, rc = comap_median_run(ctx, &p->medg[g], side));
         if (rc) return rc;
         PROF_ON(p, KV_SERIES_SUMS, side, k_series_sums<<<nub, 256, 0, side>>>(ub0, p->units, p->airmass, p->T,
                                                                              p->bsum, p->mf, p->ssum));
         COMAP_LAUNCH_CHECK(ctx);
-        COMAP_CHECK(ctx, hipEventRecord(p->ev_m[g], side));
+        if (side != st) COMAP_CHECK(ctx, hipEventRecord(p->ev_m[g], side));
     }
     for (int g = 0; g < p->ngroups; ++g) {
         const int ub0 = p->grp_u0[g] * kBands, nub = (p->grp_u0[g + 1] - p->grp_u0[g]) * kBands;
-        COMAP_CHECK(ctx, hipStreamWaitEvent(st, p->ev_m[g], 0));
+        if (side != st) COMAP_CHECK(ctx, hipStreamWaitEvent(st, p->ev_m[g], 0));
         PROF(p, KV_REGRESS, k_regress<<<nub * kRegBlocks, 256, 0, st>>>(ub0, p->tod, p->mf, p->units, p->T, p->bsum,
                                                                        p->dlist, p->dcnt, p->sdm));
         COMAP_LAUNCH_CHECK(ctx);
@@ -1783,10 +1794,10 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
     // phase 1: regression solve, per-band constants, kappa re-check
     PROF(p, KV_COEF_D, coef_d(1));
     COMAP_LAUNCH_CHECK(ctx);
-    // legacy pass D: exits at once unless phase 1 found a kappa that depends on the regression
-    // (a NaN regression coefficient), in which case it recomputes the outputs exactly
-    PROF(p, KV_COEF_D, coef_d(2));
-    COMAP_LAUNCH_CHECK(ctx);
+    // legacy pass D: exits at once unless phase 1 found a kappa that depends on the
+    // regression (a NaN regression coefficient), in which case it recomputes the outputs
+    // exactly from phase 1's constants (a former separate phase-2 k_coef_d launch
+    // recomputed what phase 1 had already written: dropped)
     PROF(p, KV_GAIN_AVG, k_gain_avg<<<p->n_tiles, 256, 0, st>>>(p->tod, p->airmass, p->units, p->tiles, p->T, UC,
                                                                 p->kap, p->dsum, p->mf, tod_out, orig_out, p->dG,
                                                                 p->flag));
