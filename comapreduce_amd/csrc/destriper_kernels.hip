@@ -355,7 +355,10 @@ __global__ void k_offset_keys(const int32_t *__restrict__ pix, int64_t NO, int L
 //                 order, then a fixed butterfly), and per sample the sort key of the
 //                 sample-level maps (pixel, npix when not binned), its index, and the
 //                 packed payload {w_b, tod_b w_b} [N][2 NB] (the product rounded, as
-//                 binValues(weights = tod * w) rounds it).
+//                 binValues(weights = tod * w) rounds it).  The row's kept entries
+//                 also go to slots [k L, k L + cnt[k]) of eval (pixel) / eoff (packed
+//                 uint8 counts), in entry order: the count form's fill is then a
+//                 compaction (k_ds_compact_cf) instead of a second leader loop.
 //   FILL = true:  the row's entries at orow[k]: pixel (-1 = off-map), weights, and the
 //                 pixel-major transpose's key / entry id / row.
 // w, tod: band-major [NB][N].
@@ -393,6 +396,17 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
         rem[m] = __ballot(j < L);
 #pragma unroll
         for (int b = 0; b < NB; ++b) wl[(64 * m + lane) * NB + b] = j < L ? w[(int64_t)b * N + base + j] : 0.0;
+    }
+    // count pass: the offset's tod loads go out with the pixels and weights, so their
+    // latency hides under the leader loop instead of following it
+    double ti[K][NB];
+    if constexpr (!FILL) {
+#pragma unroll
+        for (int m = 0; m < K; ++m) {
+            const int j = lane + 64 * m;
+#pragma unroll
+            for (int b = 0; b < NB; ++b) ti[m][b] = j < L ? tod[(int64_t)b * N + base + j] : 0.0;
+        }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // the staged weights, before other lanes read them
     // leader loop: head lanes and their members (per chunk of the leader)
@@ -453,15 +467,12 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
         int64_t c0 = 0;
 #pragma unroll
         for (int m = 0; m < K; ++m) c0 += __popcll(__ballot(keepe[m]));
-        double wi[K][NB], ti[K][NB];
+        double wi[K][NB];
 #pragma unroll
         for (int m = 0; m < K; ++m) {
             const int j = lane + 64 * m;
 #pragma unroll
-            for (int b = 0; b < NB; ++b) {
-                wi[m][b] = wl[(64 * m + lane) * NB + b];
-                ti[m][b] = j < L ? tod[(int64_t)b * N + base + j] : 0.0;
-            }
+            for (int b = 0; b < NB; ++b) wi[m][b] = wl[(64 * m + lane) * NB + b];
             if (j < L) {
                 const int64_t i = base + j;
                 double pl[2 * NB];
@@ -505,6 +516,22 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
             }
         }
         if (lane == 0) cnt[k] = c0;
+        if (eval) {
+            int64_t r0 = k * L;
+#pragma unroll
+            for (int m = 0; m < K; ++m) {
+                const unsigned long long bm = __ballot(keepe[m]);
+                if (keepe[m]) {
+                    const int64_t si = r0 + __popcll(bm & ((1ull << lane) - 1ull));
+                    uint32_t pk = 0;
+#pragma unroll
+                    for (int b = 0; b < NB; ++b) pk |= (uint32_t)(gc[m][b] & 255) << (8 * b);
+                    eval[si] = q[m];
+                    eoff[si] = (int32_t)pk;
+                }
+                r0 += __popcll(bm);
+            }
+        }
     } else {
         int64_t e = orow[k];
 #pragma unroll
@@ -513,26 +540,48 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
             if (keepe[m]) {
                 const int64_t ei = e + __popcll(bm & ((1ull << lane) - 1ull));
                 opix[ei] = q[m];
-                if constexpr (CF) {
-                    // the transpose sorts (pixel, offset << 32 | counts) pairs: its pixel-major
-                    // entries come out of the sort whole, no gather by entry id
-                    uint32_t pk = 0;
+                // (the count form's fill is k_ds_compact_cf over the count pass's slots)
 #pragma unroll
-                    for (int b = 0; b < NB; ++b) {
-                        ocnt[ei * NB + b] = (uint8_t)gc[m][b];
-                        pk |= (uint32_t)gc[m][b] << (8 * b);
-                    }
-                    epay[ei] = ((uint64_t)(uint32_t)k << 32) | pk;
-                } else {
-#pragma unroll
-                    for (int b = 0; b < NB; ++b) ow[ei * NB + b] = gs[m][b];
-                }
+                for (int b = 0; b < NB; ++b) ow[ei * NB + b] = gs[m][b];
                 ekey[ei] = (q[m] >= 0 && q[m] < npix) ? q[m] : (int32_t)npix;
                 eval[ei] = (int32_t)ei;
                 eoff[ei] = (int32_t)k;
             }
             e += __popcll(bm);
         }
+    }
+}
+
+// Count-form fill: row k's kept entries, left by the count pass in slots
+// [k L, k L + cnt_k) (pixel, packed uint8 counts per band), copied to the CSR rows at
+// orow[k] with the transpose's sort pairs (pixel key, offset << 32 | counts) -- the
+// same entries, in the same order, as the leader-loop fill pass wrote (1.2 ms of the
+// C5 4-band set-up, r03l).  One wave per row.
+template <int NB>
+__global__ void __launch_bounds__(256) k_ds_compact_cf(const int64_t *__restrict__ orow, int64_t NO, int L,
+                                                       int64_t npix, const int32_t *__restrict__ spx,
+                                                       const int32_t *__restrict__ spk, int32_t *__restrict__ opix,
+                                                       uint8_t *__restrict__ ocnt, int32_t *__restrict__ ekey,
+                                                       uint64_t *__restrict__ epay)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (k >= NO) return;
+    const int64_t e0 = orow[k], c = orow[k + 1] - e0;
+    for (int64_t r = lane; r < c; r += 64) {
+        const int32_t q = spx[k * L + r];
+        const uint32_t pk = (uint32_t)spk[k * L + r];
+        const int64_t ei = e0 + r;
+        opix[ei] = q;
+        if constexpr (NB == 4) {
+            *reinterpret_cast<uint32_t *>(ocnt + ei * 4) = pk;
+        } else if constexpr (NB == 2) {
+            *reinterpret_cast<uint16_t *>(ocnt + ei * 2) = (uint16_t)pk;
+        } else {
+            ocnt[ei] = (uint8_t)pk;
+        }
+        epay[ei] = ((uint64_t)(uint32_t)k << 32) | pk;
+        ekey[ei] = (q >= 0 && q < npix) ? q : (int32_t)npix;
     }
 }
 
@@ -662,57 +711,58 @@ __global__ void k_hit_rows(const int64_t *__restrict__ prow, const int32_t *__re
 // Sample-level maps in binValues order: h = sum w, hits = sum 1, nnum = sum tod w per
 // pixel and band, over the samples of the offsets the band keeps (keep [NB][NO], NULL =
 // all), each pixel's samples added one after the other in sample order (the stable
-// pixel sort keeps it) -- the reference's sequential loop, bit for bit.  One thread per
-// pixel walks its run of the sorted sample ids, with kSU packed payloads (64 B for 4
-// bands: one cache line per sample, not 2 NB) in flight before the ordered adds.
-constexpr int kSU = 8;
+// pixel sort keeps it) -- the reference's sequential loop, bit for bit.
+// One wave per pixel: per chunk of 64 of its samples every lane gathers one sample's
+// packed payload (64 B for 4 bands) and keep mask into LDS, then lanes 0 .. 3 NB - 1
+// each run one of the 3 NB ordered sums (h, nnum, hits per band) over the chunk.  The
+// thread-per-pixel walk this replaces kept 8 gathers in flight per pixel, so the most
+// hit pixel (thousands of samples) set the kernel time: 545 us on the chain's 3.4 M
+// samples, 690 us at C5 (r03s2, r03l).
 template <int NB>
 __global__ void __launch_bounds__(256) k_sample_walk(const int64_t *__restrict__ srow, const int32_t *__restrict__ sval,
                                                      const double *__restrict__ payload, int64_t npix, int L, int64_t NO,
                                                      const uint8_t *__restrict__ keep, double *__restrict__ h,
                                                      double *__restrict__ hits, double *__restrict__ nnum)
 {
-    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x) {
+    __shared__ double spl[4][64 * 2 * NB];
+    __shared__ uint32_t smk[4][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    double *pl = spl[wv];
+    uint32_t *mk = smk[wv];
+    const int kind = lane / NB, b = lane % NB;     // this lane's ordered sum (lanes < 3 NB)
+    const int col = kind == 2 ? 0 : kind * NB + b;
+    for (int64_t p = (int64_t)blockIdx.x * 4 + wv; p < npix; p += (int64_t)gridDim.x * 4) {
         const int64_t lo = srow[p], hi = srow[p + 1];
-        double sh[NB], sc[NB], sn[NB];
+        double acc = 0.0;
+        for (int64_t c = lo; c < hi; c += 64) {
+            const int n = (int)((hi - c) < 64 ? (hi - c) : 64);
+            if (lane < n) {
+                const int32_t i = sval[c + lane];
+                double v[2 * NB];
+                ldb<2 * NB>(payload + (int64_t)i * 2 * NB, v);
 #pragma unroll
-        for (int b = 0; b < NB; ++b) sh[b] = sc[b] = sn[b] = 0.0;
-        for (int64_t k = lo; k < hi; k += kSU) {
-            int32_t i[kSU];
+                for (int q = 0; q < 2 * NB; ++q) pl[lane * 2 * NB + q] = v[q];
+                const int64_t o = i / L;
+                uint32_t m = 0;
 #pragma unroll
-            for (int u = 0; u < kSU; ++u) i[u] = k + u < hi ? sval[k + u] : -1;
-            double pl[kSU][2 * NB];
-            bool in[kSU][NB];
-#pragma unroll
-            for (int u = 0; u < kSU; ++u) {
-                if (i[u] >= 0) {
-                    ldb<2 * NB>(payload + (int64_t)i[u] * 2 * NB, pl[u]);
-                    const int64_t o = i[u] / L;
-#pragma unroll
-                    for (int b = 0; b < NB; ++b) in[u][b] = !keep || keep[(int64_t)b * NO + o];
+                for (int bb = 0; bb < NB; ++bb) m |= (uint32_t)(!keep || keep[(int64_t)bb * NO + o]) << bb;
+                mk[lane] = m;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // the chunk, before other lanes read it
+            if (lane < 3 * NB) {
+                if (kind == 2) {
+                    for (int t = 0; t < n; ++t) acc = ((mk[t] >> b) & 1u) ? acc + 1.0 : acc;
                 } else {
-#pragma unroll
-                    for (int b = 0; b < 2 * NB; ++b) pl[u][b] = 0.0;
-#pragma unroll
-                    for (int b = 0; b < NB; ++b) in[u][b] = false;
+#pragma unroll 8
+                    for (int t = 0; t < n; ++t) {
+                        const double v = pl[t * 2 * NB + col];
+                        acc = ((mk[t] >> b) & 1u) ? acc + v : acc;
+                    }
                 }
             }
-#pragma unroll
-            for (int u = 0; u < kSU; ++u)
-#pragma unroll
-                for (int b = 0; b < NB; ++b)
-                    if (in[u][b]) {
-                        sh[b] += pl[u][b];
-                        sn[b] += pl[u][NB + b];
-                        sc[b] += 1.0;
-                    }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // read before the next chunk overwrites
         }
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            h[p * NB + b] = sh[b];
-            hits[p * NB + b] = sc[b];
-            nnum[p * NB + b] = sn[b];
-        }
+        if (lane < 3 * NB) (kind == 0 ? h : kind == 1 ? nnum : hits)[p * NB + b] = acc;
     }
 }
 
@@ -1401,9 +1451,11 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     }
     // ---- 2. count pass (+ the count-form test: non-zero weights uniform per offset and band)
     COMAP_CHECK(ctx, hipMemsetAsync(nonuni, 0, 4, st));
+    // (eval / eoff: the count-form fill's entry slots, unused by the f64 path until its
+    // own fill pass overwrites them)
     COMAP_NB_SWITCH(nb, (launch_rows<NB, false, false>(L, st, pix, w, tod, N, NO, npix, d->perm, cnt, d->ws, d->tw,
                                                        payload, skey, sval, d->wbar, nonuni, nullptr, nullptr, nullptr,
-                                                       nullptr, nullptr, nullptr, nullptr)));
+                                                       nullptr, nullptr, eval, eoff)));
     COMAP_LAUNCH_CHECK(ctx);
     COMAP_CHECK(ctx, hipMemsetAsync(cnt + NO, 0, 8, st));
     COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(cub_tmp, scan_tb, cnt, d->orow, (int)(NO + 1), st));
@@ -1442,9 +1494,8 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     if (rc) return -2;
     // ---- 3. fill pass
     if (d->cf) {
-        COMAP_NB_SWITCH(nb, (launch_rows<NB, true, true>(L, st, pix, w, tod, N, NO, npix, d->perm, nullptr, nullptr,
-                                                         nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, d->orow,
-                                                         d->opix, nullptr, d->ocnt, ekey, eval, eoff, epay)));
+        COMAP_NB_SWITCH(nb, (k_ds_compact_cf<NB><<<(unsigned)((NO + 3) / 4), 256, 0, st>>>(
+                                d->orow, NO, L, npix, eval, eoff, d->opix, d->ocnt, ekey, epay)));
     } else {
         COMAP_NB_SWITCH(nb, (launch_rows<NB, true, false>(L, st, pix, w, tod, N, NO, npix, d->perm, nullptr, nullptr,
                                                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, d->orow,
@@ -1480,7 +1531,8 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
                                                         st));
     k_rowptr<<<grid_for(npix + 1), 256, 0, st>>>(skey2, N, npix, srow);
     COMAP_LAUNCH_CHECK(ctx);
-    COMAP_NB_SWITCH(nb, k_sample_walk<NB><<<grid_for(npix), 256, 0, st>>>(srow, sval2, payload, npix, L, NO, keep,
+    COMAP_NB_SWITCH(nb, k_sample_walk<NB><<<(unsigned)std::min<int64_t>((npix + 3) / 4, 65536), 256, 0, st>>>(
+                            srow, sval2, payload, npix, L, NO, keep,
                                                                           d->h, d->hits, d->nnum));
     COMAP_LAUNCH_CHECK(ctx);
     int64_t hc[2] = {0, 0};

@@ -285,18 +285,20 @@ def prep_flat(files, filelist, map_info, bands, use_gain_filter, offset_length, 
         keep_alive.append((tod, az, el, ra, dec, spike_d, rr, rs, rms, row_w, pct, pr, row_pct, pixels, dsc, drs,
                            dps, drf, drc, dlive))
         if not calib:      # high-pass of each scan's non-zero samples (COMAPData.py:353-360)
-            for r in live:
-                for (s0, _), nl, cs in zip(edges, lens, colstart):
-                    if nl <= 0:
-                        continue
-                    for k in range(nb):
-                        segs.append((k * out.n + last + r * ds + cs, nl))
+            # (row, scan, band) order, as the per-segment loop appended them
+            sl = np.flatnonzero(np.asarray(lens) > 0)
+            if sl.size and live.size:
+                st0 = (last + live[:, None, None] * ds + colstart[sl][None, :, None]
+                       + np.arange(nb)[None, None, :] * out.n)
+                ln = np.broadcast_to(np.asarray(lens, np.int64)[sl][None, :, None], st0.shape)
+                segs.append(np.stack([st0.reshape(-1), ln.reshape(-1)], axis=1))
         last += nrow * ds
     mark('segments')
     if segs:
-        sd = _dev_np(torch, np.asarray(segs, dtype=np.int64), dev)
+        sd = _dev_np(torch, np.concatenate(segs).astype(np.int64), dev)
+        n_segs = int(sd.shape[0])
         mark('highpass_upload')
-        N.check(lib.comap_prep_highpass(c, N.dptr(out.tod), N.dptr(sd), len(segs), MEDFILT_STEP), c,
+        N.check(lib.comap_prep_highpass(c, N.dptr(out.tod), N.dptr(sd), n_segs, MEDFILT_STEP), c,
                 'comap_prep_highpass')
     torch.cuda.current_stream(dev).synchronize()
     mark('highpass')
