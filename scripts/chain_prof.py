@@ -2,19 +2,20 @@
 breakdown (COMAP_PREP_PROFILE=1) and the destriper's first-solve vs repeat-solve
 time, for kernel traces of the chain's non-L1 part:
     python scripts/chain_prof.py [feeds]
-    python scripts/chain_prof.py --cprofile OUT.txt   (host cProfile of one unsynced chain)"""
+    python scripts/chain_prof.py --cprofile OUT.txt   (host cProfile of one unsynced chain)
+    python scripts/chain_prof.py --plain              (3 unsynced chains, for a kernel trace)"""
 import json
 import os
 import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-if '--cprofile' not in sys.argv:
+if '--cprofile' not in sys.argv and '--plain' not in sys.argv:
     os.environ.setdefault('COMAP_PREP_PROFILE', '1')
 import bench  # noqa: E402
 
 
-def host_profile(path):
+def host_profile(path, profile=True):
     """cProfile one unsynced chain (after two warm ones): where the host spends the
     wall clock the GPU timeline does not account for."""
     import cProfile
@@ -32,13 +33,16 @@ def host_profile(path):
     for i in range(3):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        if i == 2:
+        if i == 2 and profile:
             pr.enable()
         chain(False)
         torch.cuda.synchronize()
-        if i == 2:
+        if i == 2 and profile:
             pr.disable()
         walls.append((time.perf_counter() - t0) * 1e3)
+    if not profile:
+        print(json.dumps({'walls_ms': walls}), flush=True)
+        return
     buf = io.StringIO()
     st = pstats.Stats(pr, stream=buf)
     st.sort_stats('cumulative').print_stats(60)
@@ -53,6 +57,8 @@ def main():
     import torch
     if len(sys.argv) > 2 and sys.argv[1] == '--cprofile':
         return host_profile(sys.argv[2])
+    if len(sys.argv) > 1 and sys.argv[1] == '--plain':
+        return host_profile(None, profile=False)
     from comapreduce_amd.mapmaking import comapdata as CD
     from comapreduce_amd.mapmaking import destriper as D
     from comapreduce_amd.mapmaking import prep
