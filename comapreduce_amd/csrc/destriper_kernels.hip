@@ -421,8 +421,10 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
 #pragma unroll
     for (int m = 0; m < K; ++m) {
         while (rem[m]) {
-            const int ld = __ffsll((long long)rem[m]) - 1;
-            const int32_t pl = __shfl(q[m], ld, 64);
+            // the leader's pixel by v_readlane (rem is wave-uniform): no LDS round trip
+            // (ds_bpermute) on this loop's dependent chain
+            const int ld = __builtin_amdgcn_readfirstlane(__ffsll((long long)rem[m]) - 1);
+            const int32_t pl = __builtin_amdgcn_readlane(q[m], ld);
             unsigned long long mm[K];
 #pragma unroll
             for (int c = 0; c < K; ++c) {
@@ -443,24 +445,31 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
     bool keepe[K];
 #pragma unroll
     for (int m = 0; m < K; ++m) {
-        bool any = false;
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
-            double s = 0.0;
-            int nz = 0;
-            if (head[m]) {
-#pragma unroll
-                for (int c = 0; c < K; ++c)
-                    for (unsigned long long bits = mem[m][c]; bits; bits &= bits - 1) {
-                        const double v = wl[(64 * c + (__ffsll((long long)bits) - 1)) * NB + b];
-                        s += v;
-                        nz += v != 0.0;
-                    }
-            }
-            gs[m][b] = s;
-            gc[m][b] = nz;
-            any |= s != 0.0;
+            gs[m][b] = 0.0;
+            gc[m][b] = 0;
         }
+        if (head[m]) {
+            // members in sample order, all bands per member (one NB-wide LDS read each);
+            // every band's sum keeps the member order
+#pragma unroll
+            for (int c = 0; c < K; ++c)
+                for (unsigned long long bits = mem[m][c]; bits; bits &= bits - 1) {
+                    const double *src = wl + (64 * c + (__ffsll((long long)bits) - 1)) * NB;
+                    double v[NB];
+#pragma unroll
+                    for (int b = 0; b < NB; ++b) v[b] = src[b];
+#pragma unroll
+                    for (int b = 0; b < NB; ++b) {
+                        gs[m][b] += v[b];
+                        gc[m][b] += v[b] != 0.0;
+                    }
+                }
+        }
+        bool any = false;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) any |= gs[m][b] != 0.0;
         keepe[m] = head[m] && any;
     }
     if constexpr (!FILL) {
