@@ -36,6 +36,8 @@ _SIGS = {
     'comap_set_stream': (c_int, [c_void_p, c_void_p]),
     'comap_synchronize': (c_int, [c_void_p]),
     'comap_version': (ctypes.c_char_p, []),
+    'comap_host_alloc': (c_int, [ctypes.c_size_t, ctypes.POINTER(c_void_p)]),
+    'comap_host_free': (None, [c_void_p]),
     'comap_medfilt_f64': (c_int, [c_void_p, P_double, c_int64, c_int32]),
     'comap_medfilt_batch_f64': (c_int, [c_void_p, P_double, P_int64, c_int32, c_int32, c_int32, P_double]),
     'comap_bin_values_f64': (c_int, [c_void_p, P_double, c_int64, P_int64, P_double, P_int64, c_int64]),
@@ -170,3 +172,36 @@ def dptr(t):
 
 def hptr(a, ctype):
     return a.ctypes.data_as(ctypes.POINTER(ctype))
+
+
+class _HostBlock:
+    """A cached page-locked block (comap_host_alloc) exposed to NumPy; it returns to
+    the cache when the last array viewing it is gone."""
+
+    def __init__(self, shape, dtype):
+        import numpy as np
+        dt = np.dtype(dtype)
+        nbytes = max(int(np.prod(shape)) * dt.itemsize, 1)
+        p = c_void_p()
+        rc = lib().comap_host_alloc(nbytes, ctypes.byref(p))
+        if rc:
+            raise MemoryError(f'comap_host_alloc({nbytes}) failed ({rc})')
+        self.ptr = p.value
+        self.__array_interface__ = {'shape': tuple(int(s) for s in shape), 'typestr': dt.str,
+                                    'data': (self.ptr, False), 'version': 3}
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                lib().comap_host_free(c_void_p(self.ptr))
+                self.ptr = None
+        except Exception:  # pragma: no cover (interpreter shutdown)
+            pass
+
+
+def host_empty(shape, dtype='float64'):
+    """Uninitialised page-locked NumPy array from the library's host cache (torch copies
+    into it asynchronously: it is pinned memory)."""
+    import numpy as np
+    return np.asarray(_HostBlock(shape, dtype))
+

@@ -212,6 +212,15 @@ int comap_scratch(comap_ctx *ctx, size_t bytes, void **out)
 
 extern "C" const char *comap_version(void) { return "comap_hip gfx950 " __DATE__; }
 
+extern "C" int comap_host_alloc(size_t bytes, void **out)
+{
+    if (!out) return -1;
+    *out = nullptr;
+    return comap_pinned_alloc(out, bytes) == hipSuccess ? 0 : -2;
+}
+
+extern "C" void comap_host_free(void *p) { comap_pinned_free(p); }
+
 extern "C" int comap_ctx_create(int device, comap_ctx **out)
 {
     if (!out) return -1;
