@@ -155,9 +155,24 @@ __global__ void __launch_bounds__(kRmsWG) k_rms_blocks(const double *__restrict_
     const double x0 = xr[0] / s;
     double avg = 0.0;
     if constexpr (PHASE == 1) {
+        // numpy's sum over its 8192-element buffer blocks: 0 + b_0 + b_1 + ..., in order;
+        // the block values are loaded 8 at a time before their adds (no load per add)
         double sum = 0.0;
         int64_t c = 0;
-        for (int q = 0; q < nblk; ++q) { sum += part0[(int64_t)r * nblk + q]; c += cnt0[(int64_t)r * nblk + q]; }
+        const double *pp = part0 + (int64_t)r * nblk;
+        const int64_t *cp = cnt0 + (int64_t)r * nblk;
+        for (int q0 = 0; q0 < nblk; q0 += 8) {
+            double pv[8];
+            int64_t cv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                pv[u] = q0 + u < nblk ? pp[q0 + u] : 0.0;
+                cv[u] = q0 + u < nblk ? cp[q0 + u] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (q0 + u < nblk) { sum += pv[u]; c += cv[u]; }
+        }
         avg = sum / (double)c;
     }
     auto v = [&](int64_t i) {
@@ -226,17 +241,26 @@ __global__ void __launch_bounds__(kRmsWG) k_rms_blocks(const double *__restrict_
         if ((threadIdx.x & 63) == 0) atomicAdd(&cnt_s, c);
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        double val;
-        if (full) {   // pw's balanced tree over the 64 leaves, level by level, left + right
-            for (int o = 1; o < 64; o <<= 1)
-                for (int i = 0; i < 64; i += 2 * o) lsum[i] = lsum[i] + lsum[i + o];
-            val = lsum[0];
-        } else {
-            int li = 0;
-            val = pairwise_tree(bn, [&](int, int) { return lsum[li++]; });
+    if (full) {
+        // pw's balanced tree over the 64 leaves, level by level, left + right: lane i of
+        // wave 0 holds leaf i, and at level o lane i (i % 2o == 0) adds lane i + o's
+        // value -- the serial loop's additions in the same pairs, as 6 shuffles instead
+        // of 63 dependent LDS read-modify-writes on one thread
+        if (threadIdx.x < 64) {
+            double v = lsum[threadIdx.x];
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const double w = __shfl_down(v, o, 64);
+                if ((threadIdx.x & (2 * o - 1)) == 0) v = v + w;
+            }
+            if (threadIdx.x == 0) {
+                part[job] = v;
+                if constexpr (PHASE == 0) cnt[job] = (int64_t)cnt_s;
+            }
         }
-        part[job] = val;
+    } else if (threadIdx.x == 0) {
+        int li = 0;
+        part[job] = pairwise_tree(bn, [&](int, int) { return lsum[li++]; });
         if constexpr (PHASE == 0) cnt[job] = (int64_t)cnt_s;
     }
 }

@@ -11,6 +11,7 @@
 #         pyprof=SCRIPT ARGS    the same under rocprofv3 --kernel-trace --stats (gpurun_out/TAG_pyprof<step>/)
 #         dsprof[=ARGS]         rocprofv3 kernel trace + stats of scripts/ds_c5.py (default: 8 obs, 4 bands, 50 it)
 #         dspmc=COUNTERS[@ARGS] one rocprofv3 --pmc pass over scripts/ds_c5.py
+#         pypmc=COUNTERS@SCRIPT ARGS  one rocprofv3 --pmc pass over python3 SCRIPT ARGS
 TAG=$1; shift
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -36,6 +37,9 @@ for step in "$@"; do
              > $d.log 2>&1 ;;
     pyprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_pyprof${NSTEP} \
               -o run -- python3 $arg > gpurun_out/${TAG}_pyprof${NSTEP}.log 2>&1 ;;
+    pypmc) cnt=${arg%%@*}; sargs=${arg#*@}
+           d=gpurun_out/${TAG}_pypmc${NSTEP}
+           timeout -s KILL 240 rocprofv3 --pmc $cnt --output-format csv -d $d -o run -- python3 $sargs > $d.log 2>&1 ;;
     py)    timeout -k 10 300 python3 -u $arg > gpurun_out/${TAG}_py${NSTEP}.log 2>&1 ;;
     smoke) timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/${TAG}_smoke.log 2>&1 ;;
     *) echo "unknown step $name"; exit 2 ;;
