@@ -53,48 +53,49 @@ inline unsigned grid_for(int64_t n, int64_t cap = 4096)
 constexpr int kPwBlock = 8192;
 constexpr int kPwLeaf = 128;
 
-// Post-order walk of pw's recursion over [0, n): leaf(off, len) is called for the
-// leaves left to right and returns the leaf's value; returns left + right at every
-// internal node.  Explicit stack (depth <= 8 for n <= 8192).
-template <typename Leaf>
-__device__ double pairwise_tree(int n, Leaf leaf)
+// NumPy's pairwise sum (pw) of n <= 8192 values as a static plan, built on the host once
+// per call (every series' last, partial buffer block has the same length): its leaves
+// (<= 128 values, left to right) and its internal nodes in post-order, node = left +
+// right.  Nodes 0 .. nleaf-1 are the leaves, nleaf + t the t-th internal node; the root
+// is the last node.  (A device-side walk of the recursion on one thread kept its stack
+// in scratch memory: ~0.19 ms per rms pass, all of it in the 76 partial blocks, r03s9.)
+constexpr int kPwMaxLeaves = 80;   // pw splits at multiples of 8: <= 65 leaves below 8192
+struct PwPlan {
+    int16_t nleaf, ntri;
+    int16_t loff[kPwMaxLeaves], llen[kPwMaxLeaves];
+    uint8_t tri[3 * kPwMaxLeaves];   // (dst, left, right) node ids
+};
+
+static int pw_plan_rec(PwPlan &p, std::vector<int> &kids, int off, int n)
 {
-    int so[24], sn[24], sst[24];
-    double sv[24];
-    int sp = 0;
-    so[0] = 0; sn[0] = n; sst[0] = 0;
-    double v = 0.0;
-    bool have = false;   // v holds the value of the node just finished
-    while (true) {
-        if (!have) {
-            if (sn[sp] <= kPwLeaf) {
-                v = leaf(so[sp], sn[sp]);
-                have = true;
-                if (sp == 0) return v;
-                --sp;
-                continue;
-            }
-            int n2 = sn[sp] / 2;
-            n2 -= n2 % 8;
-            so[sp + 1] = so[sp]; sn[sp + 1] = n2; sst[sp + 1] = 0;
-            sst[sp] = 0;
-            ++sp;
-        } else {
-            int n2 = sn[sp] / 2;
-            n2 -= n2 % 8;
-            if (sst[sp] == 0) {   // left child done: keep it, walk the right child
-                sv[sp] = v;
-                sst[sp] = 1;
-                have = false;
-                so[sp + 1] = so[sp] + n2; sn[sp + 1] = sn[sp] - n2; sst[sp + 1] = 0;
-                ++sp;
-            } else {              // right child done
-                v = sv[sp] + v;
-                if (sp == 0) return v;
-                --sp;
-            }
-        }
+    if (n <= kPwLeaf) {
+        const int id = p.nleaf++;
+        p.loff[id] = (int16_t)off;
+        p.llen[id] = (int16_t)n;
+        return -1 - id;                        // leaf id, encoded negative until renumbering
     }
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    const int a = pw_plan_rec(p, kids, off, n2);
+    const int b = pw_plan_rec(p, kids, off + n2, n - n2);
+    kids.push_back(a);
+    kids.push_back(b);
+    return (int)kids.size() / 2 - 1;           // internal node index (post-order)
+}
+
+static PwPlan pw_plan(int n)
+{
+    PwPlan p{};
+    std::vector<int> kids;
+    pw_plan_rec(p, kids, 0, n);
+    p.ntri = (int16_t)(kids.size() / 2);
+    auto id = [&](int v) { return v < 0 ? -1 - v : p.nleaf + v; };
+    for (int t = 0; t < p.ntri; ++t) {
+        p.tri[3 * t] = (uint8_t)(p.nleaf + t);
+        p.tri[3 * t + 1] = (uint8_t)id(kids[2 * t]);
+        p.tri[3 * t + 2] = (uint8_t)id(kids[2 * t + 1]);
+    }
+    return p;
 }
 
 // rms[r] = nanstd(d) / sqrt(2), d_i = x[1 + i] / s - x[0] / s, i < m = N - 1, N = n // 2 * 2
@@ -139,13 +140,11 @@ __global__ void __launch_bounds__(kRmsWG) k_rms_blocks(const double *__restrict_
                                                        const double *__restrict__ scale, int64_t n, int32_t nrows,
                                                        int32_t nblk, const double *__restrict__ part0,
                                                        const int64_t *__restrict__ cnt0, double *__restrict__ part,
-                                                       int64_t *__restrict__ cnt)
+                                                       int64_t *__restrict__ cnt, const PwPlan plan)
 {
 #pragma clang fp contract(off)
-    // a partial block's leaves: pw splits at multiples of 8, so there are at most 65
-    __shared__ int32_t loff[128], llen[128];
-    __shared__ double lsum[128];
-    __shared__ int nleaf;
+    // leaf sums, then (partial block) the plan's internal nodes
+    __shared__ double lsum[2 * kPwMaxLeaves];
     __shared__ unsigned long long cnt_s;
     const int64_t job = blockIdx.x;
     const int r = (int)(job / nblk), k = (int)(job % nblk);
@@ -188,18 +187,7 @@ __global__ void __launch_bounds__(kRmsWG) k_rms_blocks(const double *__restrict_
     const int64_t b0 = (int64_t)k * kPwBlock;
     const int bn = (int)std::min<int64_t>(kPwBlock, m - b0);
     const bool full = bn == kPwBlock;
-    if (threadIdx.x == 0) {
-        cnt_s = 0;
-        int nl = 0;
-        if (!full)
-            pairwise_tree(bn, [&](int off, int len) {
-                loff[nl] = off;
-                llen[nl] = len;
-                ++nl;
-                return 0.0;
-            });
-        nleaf = full ? kPwBlock / kPwLeaf : nl;
-    }
+    if (threadIdx.x == 0) cnt_s = 0;
     __syncthreads();
     const int g = threadIdx.x >> 3, j = threadIdx.x & 7;
     unsigned long long c = 0;         // phase 0: non-NaN d (exact)
@@ -230,8 +218,8 @@ __global__ void __launch_bounds__(kRmsWG) k_rms_blocks(const double *__restrict_
     } else {
         if constexpr (PHASE == 0)
             for (int i = threadIdx.x; i < bn; i += kRmsWG) c += !isnan(xr[1 + b0 + i] / s - x0);
-        for (int l = g; l < nleaf; l += kRmsWG / 8) {
-            const double t = pw_leaf8(v, b0 + loff[l], llen[l], j);
+        for (int l = g; l < plan.nleaf; l += kRmsWG / 8) {
+            const double t = pw_leaf8(v, b0 + plan.loff[l], plan.llen[l], j);
             if (j == 0) lsum[l] = t;
         }
     }
@@ -259,8 +247,9 @@ __global__ void __launch_bounds__(kRmsWG) k_rms_blocks(const double *__restrict_
             }
         }
     } else if (threadIdx.x == 0) {
-        int li = 0;
-        part[job] = pairwise_tree(bn, [&](int, int) { return lsum[li++]; });
+        for (int t = 0; t < plan.ntri; ++t)
+            lsum[plan.tri[3 * t]] = lsum[plan.tri[3 * t + 1]] + lsum[plan.tri[3 * t + 2]];
+        part[job] = lsum[plan.nleaf + plan.ntri - 1];
         if constexpr (PHASE == 0) cnt[job] = (int64_t)cnt_s;
     }
 }
@@ -590,9 +579,11 @@ extern "C" int comap_prep_auto_rms(comap_ctx *ctx, const double *x, int64_t row_
     int64_t *c0 = (int64_t *)(p1 + nj);
     if (m > 0) {
         const unsigned g = (unsigned)nj;
+        const PwPlan plan = pw_plan((int)(m - (int64_t)(nblk - 1) * kPwBlock));   // the last block's tree
         k_rms_blocks<0><<<g, kRmsWG, 0, ctx->stream>>>(x, row_stride, rows, scale, n, nrows, nblk, nullptr, nullptr, p0,
-                                                      c0);
-        k_rms_blocks<1><<<g, kRmsWG, 0, ctx->stream>>>(x, row_stride, rows, scale, n, nrows, nblk, p0, c0, p1, nullptr);
+                                                      c0, plan);
+        k_rms_blocks<1><<<g, kRmsWG, 0, ctx->stream>>>(x, row_stride, rows, scale, n, nrows, nblk, p0, c0, p1, nullptr,
+                                                      plan);
     }
     k_rms_final<<<(nrows + 255) / 256, 256, 0, ctx->stream>>>(nrows, nblk, n, p1, c0, rms);
     COMAP_LAUNCH_CHECK(ctx);
