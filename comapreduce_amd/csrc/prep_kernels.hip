@@ -31,6 +31,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 namespace {
@@ -703,7 +704,16 @@ extern "C" int comap_prep_highpass(comap_ctx *ctx, double *x, const int64_t *seg
         }
     }
     int rc = 0;
-    if (!jobs.empty()) {
+    // w <= kMedChunkMaxW (the reference's 400): one workgroup per 256 outputs sorts its
+    // union window in LDS (comap_median_chunked); COMAP_PREP_MEDIAN=plan: the general
+    // sort + wavelet-matrix plan.  Both give the exact order statistics.
+    const char *pm = getenv("COMAP_PREP_MEDIAN");
+    const bool chunked = w <= kMedChunkMaxW && !(pm && std::string(pm) == "plan");
+    if (!jobs.empty() && chunked) {
+        MedJob *dj = nullptr;
+        COMAP_CHECK(ctx, tmp.alloc(&dj, jobs.size()));
+        if ((rc = comap_median_chunked(ctx, jobs, w, st, dj))) return rc;
+    } else if (!jobs.empty()) {
         MedPlan mp;
         const bool prof = getenv("COMAP_PREP_PROFILE") && getenv("COMAP_PREP_PROFILE")[0] == '1';
         auto now = [] { return std::chrono::steady_clock::now(); };
