@@ -1189,8 +1189,10 @@ __global__ void __launch_bounds__(kMcOut) k_med_chunk(const MedJob *__restrict__
     const uint32_t lo_p = (uint32_t)tid, span = (uint32_t)w;  // window [tid, tid + w) of the union
     // walk the sorted positions 4 at a time (independent LDS reads, no per-element wait)
     int c = 0, j = 0, jl = -1, jh = -1;
+    uint4 vn = *reinterpret_cast<const uint4 *>(xp);
     for (; jh < 0; j += 4) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(xp + j);
+        const uint4 v = vn;                      // this group; the next one's read in flight
+        if (j + 4 < kMcSort) vn = *reinterpret_cast<const uint4 *>(xp + j + 4);
         const uint32_t pv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int u = 0; u < 4; ++u) {

@@ -704,11 +704,11 @@ extern "C" int comap_prep_highpass(comap_ctx *ctx, double *x, const int64_t *seg
         }
     }
     int rc = 0;
-    // w <= kMedChunkMaxW (the reference's 400): one workgroup per 256 outputs sorts its
-    // union window in LDS (comap_median_chunked); COMAP_PREP_MEDIAN=plan: the general
-    // sort + wavelet-matrix plan.  Both give the exact order statistics.
+    // COMAP_PREP_MEDIAN=chunked (w <= kMedChunkMaxW): one workgroup per 256 outputs sorts
+    // its union window in LDS (comap_median_chunked); default: the general sort +
+    // wavelet-matrix plan.  Both give the exact order statistics.
     const char *pm = getenv("COMAP_PREP_MEDIAN");
-    const bool chunked = w <= kMedChunkMaxW && !(pm && std::string(pm) == "plan");
+    const bool chunked = w <= kMedChunkMaxW && pm && std::string(pm) == "chunked";
     if (!jobs.empty() && chunked) {
         MedJob *dj = nullptr;
         COMAP_CHECK(ctx, tmp.alloc(&dj, jobs.size()));

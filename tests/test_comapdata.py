@@ -163,10 +163,7 @@ def test_gpu_highpass_chunked_median_equals_plan(w, monkeypatch):
     sd = torch.as_tensor(segs, device='cuda')
     outs = {}
     for mode in ('plan', 'chunked'):
-        if mode == 'plan':
-            monkeypatch.setenv('COMAP_PREP_MEDIAN', 'plan')
-        else:
-            monkeypatch.delenv('COMAP_PREP_MEDIAN', raising=False)
+        monkeypatch.setenv('COMAP_PREP_MEDIAN', mode)
         xd = torch.as_tensor(x, device='cuda')
         N.check(N.lib().comap_prep_highpass(c, N.dptr(xd), N.dptr(sd), len(lens), w), c, 'highpass')
         outs[mode] = xd.cpu().numpy()
