@@ -169,14 +169,6 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
 void comap_median_plan_free(MedPlan *mp);
 int comap_median_run(comap_ctx *ctx, MedPlan *mp, hipStream_t stream);
 inline int comap_median_run(comap_ctx *ctx, MedPlan *mp) { return comap_median_run(ctx, mp, ctx->stream); }
-// Small windows (w <= kMedChunkMaxW): the same outputs as a plan + run, by one workgroup
-// per chunk of 256 consecutive outputs that sorts the chunk's union window in LDS and
-// reads every output's order statistics off it (no plan, no device-wide sort).
-constexpr int kMedChunkMaxW = 769;
-// dev_jobs: caller-owned device room for jobs.size() MedJob (alive until the stream has
-// run the kernel, e.g. the caller's DevTemps).
-int comap_median_chunked(comap_ctx *ctx, const std::vector<MedJob> &jobs, int32_t w, hipStream_t stream,
-                         MedJob *dev_jobs);
 
 // ------------------------------------------------------------------ L1 plan
 struct comap_l1_plan {

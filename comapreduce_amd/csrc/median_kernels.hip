@@ -1093,123 +1093,6 @@ hipError_t seg_sort(void *tmp, size_t &tb, const K *k0, K *k1, const int32_t *v0
 
 size_t walk_smem(int nwmax, int lt) { return 4 * (2 * (size_t)lt + 16) + 16 * (size_t)nwmax + 8 * (size_t)lt + 64; }
 
-// ---------------------------------------------------------------- small windows
-// One workgroup per chunk of kMcOut consecutive outputs of one job: the chunk's union
-// window (kMcOut + w - 1 virtual positions) is sorted in LDS by the f64 value's
-// order-preserving u64 key (bitonic, padded to kMcSort), then output k walks the sorted
-// keys counting the ones whose position lies in its own window [k, k + w) until it has
-// the r_lo-th (and, for even w, the next) -- the exact order statistics, so the output
-// equals the sort + wavelet-matrix path's bit for bit: lo, or (hi + lo) / 2.
-constexpr int kMcOut = 256;
-constexpr int kMcSort = 1024;
-static_assert(kMcOut + kMedChunkMaxW - 1 <= kMcSort, "chunk union must fit the LDS sort");
-
-// Bitonic compare-exchange of element i (key k, pos p) with its partner i ^ s holding
-// (pk, pp): the lower index keeps the smaller key in an ascending run (the larger in a
-// descending one).  Equal keys keep their own element on both sides.
-__device__ __forceinline__ void mc_cx(int i, int s, int size, unsigned long long &k, uint32_t &p,
-                                      unsigned long long pk, uint32_t pp)
-{
-    const bool lower = (i & s) == 0, up = (i & size) == 0;
-    const bool take = (lower == up) ? (pk < k) : (pk > k);
-    if (take) { k = pk; p = pp; }
-}
-
-__global__ void __launch_bounds__(kMcOut) k_med_chunk(const MedJob *__restrict__ jobs, int32_t w)
-{
-    constexpr int kSlots = kMcSort / kMcOut;     // elements per thread: i = slot * kMcOut + tid
-    __shared__ unsigned long long xk[kMcSort];
-    __shared__ __align__(16) uint32_t xp[kMcSort];
-    const MedJob job = jobs[blockIdx.y];
-    const int64_t o0 = job.out_lo + (int64_t)blockIdx.x * kMcOut;
-    if (o0 >= job.out_hi) return;
-    if (job.gate && *job.gate <= 0) return;
-    const int h = w / 2;
-    const int U = kMcOut + w - 1;
-    const int64_t base = o0 - h;                 // virtual position of union element 0
-    const int tid = threadIdx.x;
-    unsigned long long k[kSlots];
-    uint32_t p[kSlots];
-#pragma unroll
-    for (int q = 0; q < kSlots; ++q) {
-        const int i = q * kMcOut + tid;
-        k[q] = i < U ? key_of(xprime(job, base + i, h)) : ~0ull;    // padding sorts last
-        p[q] = i < U ? (uint32_t)i : 0xffffu;                        // and is in no window
-    }
-    // bitonic sort, ascending by key, in registers: partners 256 or more apart are in the
-    // same thread (another slot), partners under 64 apart in the same wave (shuffles);
-    // only strides 64 and 128 go through LDS (7 of the 55 steps)
-    // (fully unrolled: every stride is a constant, so the slot indices k[q | qs] are
-    // static -- a runtime stride put k[] / p[] in scratch memory: 2.0 ms, r03t6)
-#pragma unroll
-    for (int size = 2; size <= kMcSort; size <<= 1) {
-#pragma unroll
-        for (int s = size >> 1; s > 0; s >>= 1) {
-            if (s >= kMcOut) {
-                const int qs = s / kMcOut;
-#pragma unroll
-                for (int q = 0; q < kSlots; ++q) {
-                    if (q & qs) continue;
-                    const int i = q * kMcOut + tid;
-                    unsigned long long ka = k[q], kb = k[q | qs];
-                    uint32_t pa = p[q], pb = p[q | qs];
-                    const bool up = (i & size) == 0;
-                    if ((ka > kb) == up && ka != kb) {
-                        k[q] = kb; k[q | qs] = ka;
-                        p[q] = pb; p[q | qs] = pa;
-                    }
-                }
-            } else if (s < 64) {
-#pragma unroll
-                for (int q = 0; q < kSlots; ++q) {
-                    const unsigned long long pk = __shfl_xor(k[q], s, 64);
-                    const uint32_t pp = __shfl_xor(p[q], s, 64);
-                    mc_cx(q * kMcOut + tid, s, size, k[q], p[q], pk, pp);
-                }
-            } else {
-#pragma unroll
-                for (int q = 0; q < kSlots; ++q) { xk[q * kMcOut + tid] = k[q]; xp[q * kMcOut + tid] = p[q]; }
-                __syncthreads();
-#pragma unroll
-                for (int q = 0; q < kSlots; ++q) {
-                    const int i = q * kMcOut + tid;
-                    mc_cx(i, s, size, k[q], p[q], xk[i ^ s], xp[i ^ s]);
-                }
-                __syncthreads();
-            }
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < kSlots; ++q) { xk[q * kMcOut + tid] = k[q]; xp[q * kMcOut + tid] = p[q]; }
-    __syncthreads();
-    const int64_t t = o0 + tid;                  // this thread's output
-    if (t >= job.out_hi) return;
-    const bool two = (w % 2) == 0;
-    const int r_lo = two ? (w / 2 - 1) : (w / 2);
-    const uint32_t lo_p = (uint32_t)tid, span = (uint32_t)w;  // window [tid, tid + w) of the union
-    // walk the sorted positions 4 at a time (independent LDS reads, no per-element wait)
-    int c = 0, j = 0, jl = -1, jh = -1;
-    uint4 vn = *reinterpret_cast<const uint4 *>(xp);
-    for (; jh < 0; j += 4) {
-        const uint4 v = vn;                      // this group; the next one's read in flight
-        if (j + 4 < kMcSort) vn = *reinterpret_cast<const uint4 *>(xp + j + 4);
-        const uint32_t pv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if (pv[u] - lo_p < span) {           // in the window (unsigned: below lo_p wraps)
-                if (c == r_lo) jl = j + u;
-                else if (c == r_lo + 1) { if (jh < 0) jh = j + u; }
-                ++c;
-            }
-        }
-        if (!two && jl >= 0) break;
-    }
-    const double lo = val_of(xk[jl]);
-    double out = lo;
-    if (two) out = (val_of(xk[jh]) + lo) / 2.0;
-    job.dst[t - job.out_lo] = out;
-}
-
 }  // namespace
 
 // ------------------------------------------------------------------ plan
@@ -1518,25 +1401,6 @@ int comap_median_run(comap_ctx *ctx, MedPlan *mp, hipStream_t st)
     default: COMAP_WALK(256); break;
     }
 #undef COMAP_WALK
-    COMAP_LAUNCH_CHECK(ctx);
-    return 0;
-}
-
-int comap_median_chunked(comap_ctx *ctx, const std::vector<MedJob> &jobs, int32_t w, hipStream_t st,
-                         MedJob *dj)
-{
-    if (jobs.empty()) return 0;
-    if (!dj) return -1;
-    if (w < 1 || w > kMedChunkMaxW) return comap_fail(ctx, -1, "comap_median_chunked: window out of range");
-    int64_t maxc = 0;
-    for (const MedJob &j : jobs) {
-        if (j.out_lo < 0 || j.out_hi < j.out_lo) return comap_fail(ctx, -1, "comap_median_chunked: bad job range");
-        maxc = std::max<int64_t>(maxc, (j.out_hi - j.out_lo + kMcOut - 1) / kMcOut);
-    }
-    if (maxc == 0) return 0;
-    if (maxc > 0x7fffffff || jobs.size() > 65535) return comap_fail(ctx, -1, "comap_median_chunked: grid too large");
-    COMAP_CHECK(ctx, hipMemcpyAsync(dj, jobs.data(), sizeof(MedJob) * jobs.size(), hipMemcpyHostToDevice, st));
-    k_med_chunk<<<dim3((unsigned)maxc, (unsigned)jobs.size()), kMcOut, 0, st>>>(dj, w);
     COMAP_LAUNCH_CHECK(ctx);
     return 0;
 }

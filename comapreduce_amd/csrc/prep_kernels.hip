@@ -704,16 +704,10 @@ extern "C" int comap_prep_highpass(comap_ctx *ctx, double *x, const int64_t *seg
         }
     }
     int rc = 0;
-    // COMAP_PREP_MEDIAN=chunked (w <= kMedChunkMaxW): one workgroup per 256 outputs sorts
-    // its union window in LDS (comap_median_chunked); default: the general sort +
-    // wavelet-matrix plan.  Both give the exact order statistics.
-    const char *pm = getenv("COMAP_PREP_MEDIAN");
-    const bool chunked = w <= kMedChunkMaxW && pm && std::string(pm) == "chunked";
-    if (!jobs.empty() && chunked) {
-        MedJob *dj = nullptr;
-        COMAP_CHECK(ctx, tmp.alloc(&dj, jobs.size()));
-        if ((rc = comap_median_chunked(ctx, jobs, w, st, dj))) return rc;
-    } else if (!jobs.empty()) {
+    // (a chunked small-window median -- one workgroup per 256 outputs bitonic-sorting its
+    // union window in registers / LDS -- matched this bit for bit but ran 1.9 ms against
+    // the plan's ~0.9 ms at the chain's 912 segments, r03t7: removed)
+    if (!jobs.empty()) {
         MedPlan mp;
         const bool prof = getenv("COMAP_PREP_PROFILE") && getenv("COMAP_PREP_PROFILE")[0] == '1';
         auto now = [] { return std::chrono::steady_clock::now(); };
