@@ -23,6 +23,8 @@ SETTINGS = [
     {'COMAP_DS_BL': '64'},
     {'COMAP_DS_BL': '32', 'COMAP_DS_BU': '8'},
     {'COMAP_DS_BL': '8', 'COMAP_DS_BU': '8'},
+    {'COMAP_DS_BL': '8'},
+    {'COMAP_DS_BL': '16'},
 ]
 KEYS = ('COMAP_DS_PG', 'COMAP_DS_PU', 'COMAP_DS_PB', 'COMAP_DS_BU', 'COMAP_DS_BL')
 
