@@ -38,6 +38,8 @@ _SIGS = {
     'comap_version': (ctypes.c_char_p, []),
     'comap_host_alloc': (c_int, [ctypes.c_size_t, ctypes.POINTER(c_void_p)]),
     'comap_host_free': (None, [c_void_p]),
+    'comap_cache_trim': (c_int, []),
+    'comap_cache_bytes': (c_int, [P_int64, P_int64, P_int64]),
     'comap_medfilt_f64': (c_int, [c_void_p, P_double, c_int64, c_int32]),
     'comap_medfilt_batch_f64': (c_int, [c_void_p, P_double, P_int64, c_int32, c_int32, c_int32, P_double]),
     'comap_bin_values_f64': (c_int, [c_void_p, P_double, c_int64, P_int64, P_double, P_int64, c_int64]),
@@ -197,6 +199,35 @@ class _HostBlock:
                 self.ptr = None
         except Exception:  # pragma: no cover (interpreter shutdown)
             pass
+
+
+def trim_caches():
+    """Return the library's cached device temporaries and page-locked blocks to the
+    system (comap_cache_trim) and torch's cached blocks too (torch.cuda.empty_cache)."""
+    import torch
+    lib().comap_cache_trim()
+    torch.cuda.empty_cache()
+
+
+def cache_bytes():
+    """{'device_cached', 'device_live', 'host_cached'} bytes of the library's caches
+    (current device)."""
+    v = [ctypes.c_int64(0) for _ in range(3)]
+    lib().comap_cache_bytes(*(ctypes.byref(x) for x in v))
+    return {k: int(x.value) for k, x in zip(('device_cached', 'device_live', 'host_cached'), v)}
+
+
+def retry_oom(fn, *args, **kw):
+    """fn(*args, **kw); on a device out-of-memory (torch's or a native call's) trim the
+    caches once and try again."""
+    import torch
+    try:
+        return fn(*args, **kw)
+    except (torch.OutOfMemoryError, NativeError) as e:
+        if isinstance(e, NativeError) and 'out of memory' not in str(e).lower():
+            raise
+        trim_caches()
+        return fn(*args, **kw)
 
 
 def host_empty(shape, dtype='float64'):

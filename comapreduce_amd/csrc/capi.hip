@@ -10,7 +10,9 @@
 #include "comap_internal.h"
 
 #include <map>
+#include <memory>
 #include <mutex>
+#include <tuple>
 #include <utility>
 #include <vector>
 
@@ -24,6 +26,28 @@ int comap_fail(comap_ctx *ctx, int code, const std::string &msg)
     if (ctx) ctx->err = msg;
     return code;
 }
+
+namespace {
+// Cached bytes above which a freed block goes back to the pool instead of the cache
+// (COMAP_TMP_CACHE_MB, default 16 GiB of device temporaries per device; the pool itself
+// keeps at most the same amount mapped between synchronisations).
+uint64_t tmp_cache_cap()
+{
+    static uint64_t cap = [] {
+        const char *e = getenv("COMAP_TMP_CACHE_MB");
+        return (uint64_t)(e ? atoll(e) : 16384) << 20;
+    }();
+    return cap;
+}
+uint64_t pinned_cache_cap()
+{
+    static uint64_t cap = [] {
+        const char *e = getenv("COMAP_PINNED_CACHE_MB");
+        return (uint64_t)(e ? atoll(e) : 2048) << 20;
+    }();
+    return cap;
+}
+}  // namespace
 
 hipMemPool_t comap_tmp_pool()
 {
@@ -45,7 +69,7 @@ hipMemPool_t comap_tmp_pool()
         (void)hipDeviceGetDefaultMemPool(&pool, dev);
     }
     if (pool) {
-        uint64_t keep = UINT64_MAX;
+        uint64_t keep = tmp_cache_cap();
         (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
     }
     pools[dev] = pool;
@@ -53,21 +77,60 @@ hipMemPool_t comap_tmp_pool()
 }
 
 namespace {
+// A freed block's last use: the stream it ran on and, unless the block was already idle,
+// an event recorded there after that use.  One event serves every block of one free call.
+struct LastUse {
+    hipStream_t st = nullptr;
+    std::shared_ptr<hipEvent_t> ev;      // null: idle (the caller synchronised)
+};
+struct TmpBlock {
+    void *p = nullptr;
+    LastUse use;
+};
 struct TmpCache {
     std::mutex mu;
-    std::map<std::pair<int, size_t>, std::vector<void *>> free;   // (device, class bytes) -> blocks
-    std::map<void *, std::pair<int, size_t>> live;                 // block -> (device, class bytes)
+    std::map<std::pair<int, size_t>, std::vector<TmpBlock>> free;   // (device, class bytes) -> blocks
+    std::map<void *, std::tuple<int, size_t, hipStream_t>> live;     // block -> (device, class, alloc stream)
+    std::map<int, uint64_t> cached;                                  // device -> bytes on the free lists
 };
 TmpCache &tmp_cache()
 {
     static TmpCache *c = new TmpCache();   // never destroyed: frees may run during exit
     return *c;
 }
+// 8 size classes per octave above 4 KiB: a request wastes at most 1/8 of its block
 size_t tmp_class(size_t b)
 {
-    size_t c = 4096;
-    while (c < b) c <<= 1;
-    return c;
+    if (b <= 4096) return 4096;
+    size_t top = 4096;
+    while ((top << 1) <= b) top <<= 1;
+    const size_t step = top / 8;
+    return (b + step - 1) / step * step;
+}
+bool capturing(hipStream_t st)
+{
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return st && hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+std::shared_ptr<hipEvent_t> record_use(hipStream_t st)
+{
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    if (hipEventRecord(e, st) != hipSuccess) {
+        (void)hipEventDestroy(e);
+        return nullptr;
+    }
+    return std::shared_ptr<hipEvent_t>(new hipEvent_t(e), [](hipEvent_t *q) {
+        (void)hipEventDestroy(*q);
+        delete q;
+    });
+}
+// the block's last use has completed, or is ordered before work that st enqueues next
+bool make_safe(const LastUse &u, hipStream_t st)
+{
+    if (!u.ev || u.st == st) return true;            // idle, or same stream: stream order
+    if (capturing(st)) return hipEventQuery(*u.ev) == hipSuccess;   // no cross-stream edge into a graph
+    return hipStreamWaitEvent(st, *u.ev, 0) == hipSuccess;
 }
 }  // namespace
 
@@ -80,30 +143,103 @@ hipError_t comap_tmp_alloc(void **p, size_t bytes, hipStream_t st)
     {
         std::lock_guard<std::mutex> lock(c.mu);
         auto it = c.free.find({dev, cls});
-        if (it != c.free.end() && !it->second.empty()) {
-            *p = it->second.back();
-            it->second.pop_back();
-            c.live[*p] = {dev, cls};
-            return hipSuccess;
+        if (it != c.free.end()) {
+            auto &v = it->second;
+            for (size_t i = v.size(); i-- > 0;) {
+                if (!make_safe(v[i].use, st)) continue;
+                *p = v[i].p;
+                v.erase(v.begin() + (std::ptrdiff_t)i);
+                c.cached[dev] -= cls;
+                c.live[*p] = {dev, cls, st};
+                return hipSuccess;
+            }
         }
     }
-    const hipError_t e = hipMallocFromPoolAsync(p, cls, comap_tmp_pool(), st);
+    hipError_t e = hipMallocFromPoolAsync(p, cls, comap_tmp_pool(), st);
+    if (e == hipErrorOutOfMemory) {       // cached blocks of other sizes hold the memory
+        (void)hipGetLastError();
+        comap_tmp_trim();
+        e = hipMallocFromPoolAsync(p, cls, comap_tmp_pool(), st);
+    }
     if (e == hipSuccess) {
         std::lock_guard<std::mutex> lock(c.mu);
-        c.live[*p] = {dev, cls};
+        c.live[*p] = {dev, cls, st};
     }
     return e;
 }
 
-void comap_tmp_free(void *p)
+void comap_tmp_free_on(void *const *ps, int n, hipStream_t st, bool idle)
 {
-    if (!p) return;
     TmpCache &c = tmp_cache();
-    std::lock_guard<std::mutex> lock(c.mu);
-    auto it = c.live.find(p);
-    if (it == c.live.end()) return;
-    c.free[it->second].push_back(p);
-    c.live.erase(it);
+    std::shared_ptr<hipEvent_t> ev;
+    bool recorded = false;
+    for (int i = 0; i < n; ++i) {
+        void *p = ps[i];
+        if (!p) continue;
+        std::unique_lock<std::mutex> lock(c.mu);
+        auto it = c.live.find(p);
+        if (it == c.live.end()) continue;
+        const int dev = std::get<0>(it->second);
+        const size_t cls = std::get<1>(it->second);
+        const hipStream_t use_st = st ? st : std::get<2>(it->second);
+        c.live.erase(it);
+        if (c.cached[dev] + cls > tmp_cache_cap()) {
+            lock.unlock();
+            DeviceGuard g(dev);
+            (void)hipFreeAsync(p, use_st);            // stream-ordered release to the pool
+            continue;
+        }
+        LastUse u;
+        u.st = use_st;
+        if (!idle) {
+            if (capturing(use_st)) {
+                // no event can be recorded into a capture: reuse stays on this stream only
+                u.ev = std::shared_ptr<hipEvent_t>(new hipEvent_t(nullptr), [](hipEvent_t *q) { delete q; });
+            } else {
+                if (!recorded) {
+                    lock.unlock();
+                    ev = record_use(use_st);
+                    recorded = true;
+                    lock.lock();
+                }
+                if (!ev) {                              // could not record: wait here instead
+                    lock.unlock();
+                    (void)hipStreamSynchronize(use_st);
+                    lock.lock();
+                }
+                u.ev = ev;
+            }
+        }
+        c.free[{dev, cls}].push_back({p, u});
+        c.cached[dev] += cls;
+    }
+}
+
+void comap_tmp_free(void *p) { comap_tmp_free_on(&p, 1, nullptr, false); }
+
+void comap_tmp_trim()
+{
+    TmpCache &c = tmp_cache();
+    std::map<std::pair<int, size_t>, std::vector<TmpBlock>> fl;
+    {
+        std::lock_guard<std::mutex> lock(c.mu);
+        fl.swap(c.free);
+        c.cached.clear();
+    }
+    std::map<int, bool> devs;
+    for (auto &kv : fl) {
+        DeviceGuard g(kv.first.first);
+        for (TmpBlock &b : kv.second) {
+            if (b.use.ev && *b.use.ev) (void)hipEventSynchronize(*b.use.ev);
+            else if (b.use.ev) (void)hipStreamSynchronize(b.use.st);
+            (void)hipFree(b.p);
+        }
+        devs[kv.first.first] = true;
+    }
+    for (auto &d : devs) {
+        DeviceGuard g(d.first);
+        (void)hipMemPoolTrimTo(comap_tmp_pool(), 0);
+    }
 }
 
 namespace {
@@ -111,6 +247,7 @@ struct PinnedCache {
     std::mutex mu;
     std::map<size_t, std::vector<void *>> free;
     std::map<void *, size_t> live;
+    uint64_t cached = 0;
 };
 PinnedCache &pinned_cache()
 {
@@ -139,6 +276,7 @@ hipError_t comap_pinned_alloc(void **p, size_t bytes)
         if (it != c.free.end() && !it->second.empty()) {
             *p = it->second.back();
             it->second.pop_back();
+            c.cached -= cls;
             c.live[*p] = cls;
             return hipSuccess;
         }
@@ -151,15 +289,67 @@ hipError_t comap_pinned_alloc(void **p, size_t bytes)
     return e;
 }
 
+// Host blocks are returned by their owner once no copy into or out of them is pending
+// (the Python side frees a result block when its last NumPy view is gone).
 void comap_pinned_free(void *p)
 {
     if (!p) return;
     PinnedCache &c = pinned_cache();
-    std::lock_guard<std::mutex> lock(c.mu);
+    std::unique_lock<std::mutex> lock(c.mu);
     auto it = c.live.find(p);
     if (it == c.live.end()) return;
-    c.free[it->second].push_back(p);
+    const size_t cls = it->second;
     c.live.erase(it);
+    if (c.cached + cls > pinned_cache_cap()) {
+        lock.unlock();
+        (void)hipHostFree(p);
+        return;
+    }
+    c.free[cls].push_back(p);
+    c.cached += cls;
+}
+
+void comap_pinned_trim()
+{
+    PinnedCache &c = pinned_cache();
+    std::map<size_t, std::vector<void *>> fl;
+    {
+        std::lock_guard<std::mutex> lock(c.mu);
+        fl.swap(c.free);
+        c.cached = 0;
+    }
+    for (auto &kv : fl)
+        for (void *p : kv.second) (void)hipHostFree(p);
+}
+
+extern "C" int comap_cache_trim(void)
+{
+    comap_tmp_trim();
+    comap_pinned_trim();
+    return 0;
+}
+
+extern "C" int comap_cache_bytes(int64_t *device_cached, int64_t *device_live, int64_t *host_cached)
+{
+    TmpCache &c = tmp_cache();
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    {
+        std::lock_guard<std::mutex> lock(c.mu);
+        if (device_cached) *device_cached = (int64_t)c.cached[dev];
+        if (device_live) {
+            int64_t s = 0;
+            for (auto &kv : c.live)
+                if (std::get<0>(kv.second) == dev) s += (int64_t)std::get<1>(kv.second);
+            *device_live = s;
+        }
+    }
+    if (host_cached) {
+        PinnedCache &pc = pinned_cache();
+        std::lock_guard<std::mutex> lock(pc.mu);
+        *host_cached = (int64_t)pc.cached;
+    }
+    return 0;
 }
 
 hipError_t comap_stream_acquire(hipStream_t *s)

@@ -55,17 +55,26 @@ struct DeviceGuard {
 // reuse cached memory instead of mapping and unmapping hundreds of MB per call
 // (the prep high-pass lost 1.8 ms per call to that, r03h).
 hipMemPool_t comap_tmp_pool();
-// Temporaries through a host-side cache of freed blocks (power-of-two size classes per
+// Temporaries through a host-side cache of freed blocks (8 size classes per octave, per
 // device) in front of that pool: a free is a list push, an allocation of a cached class a
-// list pop -- no HIP call.  hipFreeAsync of a median plan's 12 buffers still cost
-// 0.75-0.8 ms of host time per prep call (r03j).  Blocks are handed out again in stream
-// order: every user allocates and frees on one stream, or frees after a sync.
+// list pop -- no allocation call.  hipFreeAsync of a median plan's 12 buffers cost
+// 0.75-0.8 ms of host time per prep call (r03j).  Reuse is stream-safe: a free records
+// one event after the blocks' last use (on `st`, default the stream each block was
+// allocated on; none when `idle`, i.e. the caller synchronised), and a block handed out
+// on another stream makes that stream wait for the event first (same stream: stream
+// order suffices).  Cached bytes are capped (COMAP_TMP_CACHE_MB); comap_tmp_trim releases
+// every cached block (comap_cache_trim in the C ABI; also tried once on out-of-memory).
 hipError_t comap_tmp_alloc(void **p, size_t bytes, hipStream_t st);
 void comap_tmp_free(void *p);
-// Small pinned host blocks (CG flag / scalar read-back) through the same kind of cache:
-// hipHostMalloc costs 0.1-0.3 ms a call, once per destriper problem before this (r03l).
+void comap_tmp_free_on(void *const *ps, int n, hipStream_t st, bool idle);
+void comap_tmp_trim();
+// Small pinned host blocks (CG flag / scalar read-back, result blocks) through the same
+// kind of cache (capped by COMAP_PINNED_CACHE_MB): hipHostMalloc costs 0.1-0.3 ms a
+// call, once per destriper problem before this (r03l).  A block is freed by its owner
+// once no copy into or out of it is pending.
 hipError_t comap_pinned_alloc(void **p, size_t bytes);
 void comap_pinned_free(void *p);
+void comap_pinned_trim();
 // Non-blocking streams for the current device, reused across objects (a problem's CG
 // stream): hipStreamCreate / hipStreamDestroy per destriper problem cost ~0.1 ms and a
 // device sync.  Released streams must be idle (the caller synchronised them).
@@ -91,8 +100,9 @@ struct DevTemps {
     }
     ~DevTemps()
     {
-        if (!p.empty()) (void)hipStreamSynchronize(st);
-        for (void *q : p) comap_tmp_free(q);
+        if (p.empty()) return;
+        (void)hipStreamSynchronize(st);
+        comap_tmp_free_on(p.data(), (int)p.size(), st, true);
     }
 };
 
@@ -163,6 +173,7 @@ struct MedPlan {
     void *temp = nullptr;
     size_t temp_bytes = 0;
     hipStream_t alloc_stream = nullptr;   // its buffers come from the device pool on this stream
+    hipStream_t run_stream = nullptr;     // the stream of its last comap_median_run (their last use)
 };
 
 int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jobs, int32_t w);

@@ -1443,7 +1443,7 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         ~ArenaFree()
         {
             (void)hipStreamSynchronize(s);
-            comap_tmp_free(a->base);
+            comap_tmp_free_on((void *const *)&a->base, 1, s, true);
         }
     } arena_free{&ar, st};
     char *cub_tmp = ar.take<char>(cub_tb);
@@ -1577,7 +1577,7 @@ extern "C" int comap_destripe_destroy(comap_destriper *d)
     (void)hipDeviceSynchronize();
     void *b[] = {d->orow, d->opix, d->ow, d->ws, d->tw, d->prow, d->poff, d->pw, d->h, d->hits, d->nnum, d->part, d->scal,
                  d->cg, d->flags, d->hrow, d->hprow, d->perm, d->ocnt, d->pcnt, d->wbar, d->pt};
-    for (void *p : b) comap_tmp_free(p);
+    comap_tmp_free_on(b, (int)(sizeof(b) / sizeof(b[0])), nullptr, true);
     comap_pinned_free(d->flags_host);
     comap_pinned_free(d->thr_host);
     if (d->batch) (void)hipGraphExecDestroy(d->batch);

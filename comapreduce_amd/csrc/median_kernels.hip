@@ -1330,12 +1330,15 @@ void comap_median_plan_free(MedPlan *mp)
 {
     void *b[] = {mp->jobs, mp->seg, mp->k0, mp->k1, mp->v0, mp->v1, mp->rank, mp->temp, mp->segs, mp->redo, mp->krange,
                  mp->slo};
-    for (void *p : b) comap_tmp_free(p);
+    // the last use is the last walk (whose stream waited for the plan's uploads on the
+    // allocation stream): one event there guards every buffer's reuse
+    comap_tmp_free_on(b, (int)(sizeof(b) / sizeof(b[0])), mp->run_stream ? mp->run_stream : mp->alloc_stream, false);
     *mp = MedPlan();
 }
 
 int comap_median_run(comap_ctx *ctx, MedPlan *mp, hipStream_t st)
 {
+    mp->run_stream = st;
     if (mp->slide) {
         if (mp->nsegs == 0) return 0;
         const size_t sm = slide_smem(mp->w);

@@ -398,20 +398,34 @@ __device__ __forceinline__ int32_t wcs_pixel(const comap_prep_wcs &w, double lng
     return (int32_t)(py * (double)w.nx + px);
 }
 
+constexpr int kScanLds = 128;
+
 // One thread per output sample (row, column) of one file (get_tod COMAPData.py:306-376,
 // read_pixels :404-425): column -> (scan, sample) through the scan table.
 __global__ void __launch_bounds__(256) k_prep_gather(comap_prep_file f, comap_prep_wcs wc, comap_prep_out o)
 {
 #pragma clang fp contract(off)
-    __shared__ int64_t sc[3 * 64];
-    for (int i = threadIdx.x; i < 3 * f.n_scans; i += blockDim.x) sc[i] = f.scans[i];
-    __syncthreads();
+    // the scan of a column = the last scan whose first column is <= it (zero-length scans
+    // share the next scan's first column and are skipped); a file of up to kScanLds scans
+    // keeps its table in LDS, a longer one is binary-searched in global memory
+    __shared__ int64_t sc[3 * kScanLds];
+    const bool lds = f.n_scans <= kScanLds;
+    if (lds) {
+        for (int i = threadIdx.x; i < 3 * f.n_scans; i += blockDim.x) sc[i] = f.scans[i];
+        __syncthreads();
+    }
     const int64_t col = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     const int row = blockIdx.y;
     if (col >= f.datasize) return;
-    int s = 0;
-    while (s + 1 < f.n_scans && sc[3 * (s + 1) + 2] <= col) ++s;
-    const int64_t N = sc[3 * s + 1], j = col - sc[3 * s + 2], t = sc[3 * s] + j;
+    const int64_t *tab = lds ? sc : f.scans;
+    int lo = 0, hi = f.n_scans - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (tab[3 * mid + 2] <= col) lo = mid;
+        else hi = mid - 1;
+    }
+    const int s = lo;
+    const int64_t N = tab[3 * s + 1], j = col - tab[3 * s + 2], t = tab[3 * s] + j;
     const int64_t oi = o.offset + (int64_t)row * f.datasize + col;
     // pointing (read_pixels fills row i from the file row of output_feed_index[i])
     const int ps = f.pix_src[row];
@@ -500,6 +514,34 @@ __global__ void __launch_bounds__(256) k_seg_compact(const double *__restrict__ 
         if (threadIdx.x == 0) run += tot;
         __syncthreads();
     }
+}
+
+// Segments with 1 .. 2w median-input values: np.nanmedian of the values (COMAPData.py:79),
+// broadcast.  One workgroup per segment (the others exit at once): every value's rank =
+// the values below it plus the equal ones before it (the values are finite and non-zero),
+// so the sorted order needs no sort; even counts average the two middle values as
+// np.median does ((a + b) / 2).
+constexpr int kSmallSeg = 2048;
+__global__ void __launch_bounds__(256) k_seg_small_median(const double *__restrict__ vals,
+                                                          const int64_t *__restrict__ off,
+                                                          const int64_t *__restrict__ cnt, int64_t nmax,
+                                                          double *__restrict__ filt)
+{
+    const int64_t n = cnt[blockIdx.x];
+    if (n == 0 || n > nmax) return;
+    __shared__ double v[kSmallSeg], srt[kSmallSeg];
+    const int64_t o0 = off[blockIdx.x];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) v[i] = vals[o0 + i];
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const double x = v[i];
+        int r = 0;
+        for (int j = 0; j < n; ++j) r += (v[j] < x) || (v[j] == x && j < i);
+        srt[r] = x;
+    }
+    __syncthreads();
+    const double med = (n & 1) ? srt[n / 2] : (srt[n / 2 - 1] + srt[n / 2]) / 2.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) filt[o0 + i] = med;
 }
 
 __global__ void k_seg_subtract(double *__restrict__ x, const int64_t *__restrict__ seg, const int64_t *__restrict__ off,
@@ -642,7 +684,7 @@ extern "C" int comap_prep_gather(comap_ctx *ctx, const comap_prep_file *f, const
 {
     if (!ctx || !f || !out || (!wcs && !f->pixels)) return -1;
     COMAP_DEVICE_GUARD(ctx);
-    if (f->n_scans < 1 || f->n_scans > 64) return comap_fail(ctx, -1, "comap_prep_gather: 1 to 64 scans per file");
+    if (f->n_scans < 1) return comap_fail(ctx, -1, "comap_prep_gather: no scan in the file");
     if (f->n_bands < 1 || f->n_bands > 4) return comap_fail(ctx, -1, "comap_prep_gather: 1 to 4 bands");
     if (f->n_rows < 1 || f->datasize < 1) return 0;
     if (f->n_rows > 65535) return comap_fail(ctx, -1, "comap_prep_gather: too many rows");
@@ -685,9 +727,15 @@ extern "C" int comap_prep_highpass(comap_ctx *ctx, double *x, const int64_t *seg
     k_seg_compact<<<nseg, 256, 0, st>>>(x, seg_dev, off, vals, pos);
     COMAP_LAUNCH_CHECK(ctx);
     std::vector<MedJob> jobs;
-    std::vector<int> small;
+    std::vector<int> small;      // short segments the device kernel cannot hold (2w > kSmallSeg)
+    const int64_t nsmall_dev = 2 * (int64_t)w <= kSmallSeg ? 2 * (int64_t)w : 0;
+    bool any_small_dev = false;
     for (int k = 0; k < nseg; ++k) {
         if (c[k] == 0) continue;
+        if (c[k] <= nsmall_dev) {
+            any_small_dev = true;
+            continue;
+        }
         if (c[k] > 2 * (int64_t)w) {
             MedJob j;
             j.src = vals + o[k];
@@ -728,6 +776,10 @@ extern "C" int comap_prep_highpass(comap_ctx *ctx, double *x, const int64_t *seg
     }
     // short segments: np.nanmedian of their (finite) values -- a mean of the two middle
     // values for an even count -- broadcast (np.ones(n) * m)
+    if (any_small_dev) {
+        k_seg_small_median<<<nseg, 256, 0, st>>>(vals, off, cnt, nsmall_dev, filt);
+        COMAP_LAUNCH_CHECK(ctx);
+    }
     for (int k : small) {
         std::vector<double> v(c[k]);
         COMAP_CHECK(ctx, hipMemcpyAsync(v.data(), vals + o[k], 8 * v.size(), hipMemcpyDeviceToHost, st));

@@ -66,7 +66,8 @@ def upload(a, device, chunk_bytes=UPLOAD_CHUNK, threads=8):
     if not lazy:
         a = np.ascontiguousarray(a)
     src = None if lazy else a.reshape(-1)
-    out = torch.empty(tuple(a.shape), dtype=getattr(torch, str(a.dtype)), device=dev)
+    # the library's cached temporaries are outside torch's allocator: trim them if needed
+    out = N.retry_oom(torch.empty, tuple(a.shape), dtype=getattr(torch, str(a.dtype)), device=dev)
     dst = out.view(-1)
     n = int(np.prod(a.shape, dtype=np.int64))
     if n == 0:

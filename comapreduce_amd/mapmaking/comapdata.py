@@ -229,9 +229,13 @@ def read_comap_data_bands(filelist, map_info, bands=(0, 1, 2, 3), use_gain_filte
     remapping_array = find_unique_values(local.cpu().numpy()).astype(int)
     mark('unique')
     if healpix:      # COMAPData.py:572-573: pixel ids -> positions in the union over ranks
-        ra_sorted = torch.as_tensor(np.sort(remapping_array), device=pointing.device)
-        order = torch.as_tensor(np.argsort(remapping_array), device=pointing.device)
-        pointing = order[torch.searchsorted(ra_sorted, pointing)]
+        # index_replace (COMAPData.py:43-58) as written: the inverse sort permutation
+        # indexed by the searchsorted positions (the identity for np.unique's sorted union)
+        order = np.argsort(remapping_array)
+        inv = np.empty_like(order)
+        inv[order] = np.arange(order.size)
+        ra_sorted = torch.as_tensor(remapping_array[order], device=pointing.device)
+        pointing = torch.as_tensor(inv, device=pointing.device)[torch.searchsorted(ra_sorted, pointing)]
     out = {'tod': cut.tod, 'weights': cut.w, 'keep': keep, 'pointing': pointing, 'az': cut.az, 'el': cut.el,
            'ra': cut.ra, 'dec': cut.dec, 'feedid': cut.feedid, 'obsids': cut.obsid}
     if not device_outputs:

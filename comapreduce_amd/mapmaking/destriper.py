@@ -488,9 +488,10 @@ class DeviceDestriper:
     samples and gets its own offsets and the full maps.  The problem is either
     sharded (each rank's operator, RCCL all-reduces every CG iteration) or gathered
     to rank 0, which solves it alone and hands back each rank's offsets and the maps:
-    mapmaking/rankplan.py models both (COMAP_DS_RANKS=auto, the default) -- small
-    problems such as one observation (C4) are latency-bound across ranks and are
-    gathered, large ones (C5) sharded; COMAP_DS_RANKS=shard / gather forces one."""
+    mapmaking/rankplan.py models both (COMAP_DS_RANKS=auto: small problems such as one
+    observation (C4) are latency-bound across ranks and are gathered, large ones (C5)
+    sharded).  The default is COMAP_DS_RANKS=shard until a multi-GPU run replaces the
+    model's assumed all-reduce latency and bandwidth; gather forces the other."""
 
     def __init__(self, pixels, tod, weights, offset_length, npix, device=None, keep=None):
         self.npix_full, self.hit_index = int(npix), None
@@ -503,13 +504,15 @@ class DeviceDestriper:
                 return
             if os.environ.get('COMAP_DS_COMPACT', '1') != '0':
                 pixels, npix = self._compact(pixels, int(npix), device)
-        self.ops = DeviceOps(pixels, tod, weights, offset_length, npix, device, keep)
+        self.ops = N.retry_oom(DeviceOps, pixels, tod, weights, offset_length, npix, device, keep)
 
     # ---- rank policy
     def _choose_gather(self, d, pixels, tod, offset_length):
         import torch
         from . import rankplan
-        policy = os.environ.get('COMAP_DS_RANKS', 'auto')
+        # default 'shard': the rank model's all-reduce latency / ring bandwidth are assumptions
+        # until a multi-GPU run measures them (rankplan.py), so 'auto' is opt-in
+        policy = os.environ.get('COMAP_DS_RANKS', 'shard')
         if policy == 'shard':
             return False
         n_local = int(pixels.numel()) if hasattr(pixels, 'numel') else int(np.size(pixels))

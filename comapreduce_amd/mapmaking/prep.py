@@ -142,6 +142,9 @@ def precompute_pointing(files, filelist, feeds, device=None):
         az = _dev(torch, f['spectrometer/pixel_pointing/pixel_az'], dev, torch.float64)
         el = _dev(torch, f['spectrometer/pixel_pointing/pixel_el'], dev, torch.float64)
         T = int(az.shape[-1])
+        if az.dim() != 2 or tuple(el.shape) != tuple(az.shape) or int(row_src.max()) >= int(az.shape[0]):
+            raise ValueError(f'pixel_az / pixel_el shapes {tuple(az.shape)} / {tuple(el.shape)} do not cover '
+                             f'the file\'s {int(row_src.max()) + 1} feeds')
         pr, = _dev_pack(torch, dev, (row_src[live].astype(np.int32),))
         pct = torch.zeros((live.size, 4), dtype=torch.float64, device=dev)
         N.check(N.lib().comap_prep_percentiles(c, N.dptr(az), N.dptr(el), T, N.dptr(pr), int(live.size), T,
@@ -218,20 +221,30 @@ def prep_flat(files, filelist, map_info, bands, use_gain_filter, offset_length, 
         pix_src[:n] = np.asarray(fi)[np.asarray(oi)[:n]]
         az, el, ra, dec = (_dev(torch, f[f'spectrometer/pixel_pointing/pixel_{k}'], dev, torch.float64)
                            for k in ('az', 'el', 'ra', 'dec'))
+        # the kernels index these with the tod's strides: a mismatch would read out of
+        # bounds on the device (the reference raises an IndexError there)
+        for k, a in (('az', az), ('el', el), ('ra', ra), ('dec', dec)):
+            if tuple(a.shape) != (F, T):
+                raise ValueError(f'spectrometer/pixel_pointing/pixel_{k} has shape {tuple(a.shape)}, '
+                                 f'expected {(F, T)} (feeds x samples of {dname})')
+        if int(np.max(row_src, initial=-1)) >= F or int(np.max(pix_src, initial=-1)) >= F:
+            raise ValueError(f'spectrometer/feeds lists more feeds than {dname} holds ({F})')
+        if max(bands) >= B:
+            raise ValueError(f'band {max(bands)} requested from a tod of {B} bands')
         spike = f['spikes/spike_mask'] if 'spikes/spike_mask' in f else None
         if spike is not None and len(_shape_of(spike)) == 1:     # COMAPData.py:268-269
             spike = None
         spike_d = None
         if spike is not None:
             spike_d = _spike_mask(torch, spike, dev, (F, B, T))
+            if tuple(spike_d.shape) != (F, B, T):
+                raise ValueError(f'spikes/spike_mask has shape {tuple(spike_d.shape)}, expected {(F, B, T)}')
         live = np.flatnonzero(row_src >= 0)
         # weights: 1 / auto_rms(tod_file)^2 per (row, band) (COMAPData.py:320)
         rms_rows = np.array([row_src[r] * B + b for r in live for b in bands], dtype=np.int32)
         rms_scale = np.array([row_cal[r, k] for r in live for k in range(nb)], dtype=np.float64)
         colstart = np.concatenate(([0], np.cumsum(lens)[:-1])).astype(np.int64)
         scans = np.stack([edges[:, 0], np.asarray(lens, np.int64), colstart], axis=1).astype(np.int64)
-        if scans.shape[0] > 64:
-            raise ValueError('at most 64 scans per file')
         # every per-file table in one host -> device copy
         rr, rs, pr, dsc, drs, dps, drf, drc, dlive = _dev_pack(
             torch, dev, (rms_rows, rms_scale, row_src[live].astype(np.int32), scans, row_src, pix_src, row_feed,

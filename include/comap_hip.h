@@ -50,12 +50,21 @@ int comap_set_stream(comap_ctx *ctx, void *stream);
 int comap_synchronize(comap_ctx *ctx);
 /* Library build tag, e.g. "comap_hip gfx950 <date>" */
 const char *comap_version(void);
-/* Page-locked host memory from a process-wide cache (power-of-two size classes; a
- * freed block is kept for the next request of its class): result buffers of
- * device -> host copies that a caller keeps (the destriper's maps) without paying
- * hipHostMalloc (~2.5 ms for a 4-band map set) per solve.  0 or -2 (out of memory). */
+/* Page-locked host memory from a process-wide cache (8 size classes per octave; a
+ * freed block is kept for the next request of its class, up to COMAP_PINNED_CACHE_MB
+ * cached): result buffers of device -> host copies that a caller keeps (the
+ * destriper's maps) without paying hipHostMalloc (~2.5 ms for a 4-band map set) per
+ * solve.  0 or -2 (out of memory).  Free a block only when no copy into it is pending. */
 int comap_host_alloc(size_t bytes, void **out);
 void comap_host_free(void *p);
+/* The library keeps freed device temporaries (median plans, destriper problems) and
+ * page-locked blocks cached for reuse, outside torch's allocator, up to
+ * COMAP_TMP_CACHE_MB (default 16384) of device memory per device.  comap_cache_trim
+ * waits for the cached blocks' last uses and returns them all to the system (device
+ * pool trimmed to 0); comap_cache_bytes reports the current device's cached and live
+ * temporary bytes and the cached page-locked bytes (any pointer may be NULL). */
+int comap_cache_trim(void);
+int comap_cache_bytes(int64_t *device_cached, int64_t *device_live, int64_t *host_cached);
 
 /* ------------------------------------------------------------ drop-ins (host arrays) */
 /* In place, identical to medfilt.medfilt(x, w): out[i] = median of
@@ -317,7 +326,7 @@ typedef struct comap_prep_file {
     int64_t point_stride;
     const uint8_t *spike;         /* [F][B][T] spikes/spike_mask (0 / 1), or NULL */
     int64_t spike_feed_stride, spike_band_stride;
-    int32_t n_rows, n_scans;      /* n_scans <= 64 */
+    int32_t n_rows, n_scans;      /* any n_scans >= 1 (up to 128 held in LDS, more searched in HBM) */
     int64_t datasize;             /* columns per output row */
     const int64_t *scans;         /* [n_scans][3] */
     const int32_t *row_src, *pix_src;   /* [n_rows] */

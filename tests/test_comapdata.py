@@ -266,3 +266,52 @@ def test_nan_samples_do_not_abort_prep(case_store):
     moved = t != clean[0]
     assert t.size == clean[0].size and moved.any()
     assert np.unique(np.asarray(res[8])[moved]).size == 1                # only that feed's samples moved
+
+
+def _many_scans_store(case_store):
+    """File 13 of the golden scenario re-cut into 82 scans (> the 64 a scan table once
+    held): lengths cycle through 30 (shorter than L: no samples), 120 / 260 / 75 / 240
+    (short segments, np.nanmedian) and 900 (> 2 x 400: the running median)."""
+    store, names = case_store
+    ds, attrs = store[names[1]]
+    ds = dict(ds)
+    T = ds['averaged_tod/tod'].shape[-1]
+    edges, t = [], 100
+    cyc = (30, 120, 260, 900, 75, 240)
+    while True:
+        n = cyc[len(edges) % len(cyc)]
+        if t + n > T:
+            break
+        edges.append((t, t + n))
+        t += n + 20
+    ds['averaged_tod/scan_edges'] = np.asarray(edges, dtype=np.int64)
+    return {names[1]: (ds, attrs)}, [names[1]], len(edges)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', list(cc.CASES))
+def test_gpu_prep_many_scans_vs_oracle(case_store, name):
+    """read_comap_data on a file of 82 scans (COMAPData.py:350-360 loops over any number)
+    == the oracle, bit for bit except the Sun-centric trigonometric leaves."""
+    from oracle import comapdata as oc
+    store, names, S = _many_scans_store(case_store)
+    assert S > 64
+    case = cc.CASES[name]
+    ref = oc.read_comap_data(names, store, map_info(case['map']), feeds=cc.FEEDS, **case['kw'])
+    got = cd.read_comap_data(names, map_info(case['map']), feeds=cc.FEEDS, store=store, **case['kw'])
+    for k, a, b in zip(cc.OUTPUTS, got, ref):
+        a, b = np.asarray(a), np.asarray(b)
+        assert a.shape == b.shape, k
+        if k in TRIG:
+            assert np.max(np.abs(a - b)) <= 1e-12 * max(np.max(np.abs(b)), 1.0), k
+        else:
+            assert np.array_equal(a, b), k
+
+
+def test_oracle_many_scans_runs(case_store):
+    """The many-scan fixture is a real case for the oracle: several scans of each kind."""
+    from oracle import comapdata as oc
+    store, names, S = _many_scans_store(case_store)
+    case = cc.CASES['car']
+    res = oc.read_comap_data(names, store, map_info(case['map']), feeds=cc.FEEDS, **case['kw'])
+    assert S > 64 and res[0].size > 0 and res[0].size % 50 == 0

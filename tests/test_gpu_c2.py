@@ -224,6 +224,45 @@ def test_c4_four_bands_batched_vs_oracle(c4):
         assert rel(x[r['keep'][b].astype(bool)], xr) < 1e-5, b
 
 
+def test_chain_as_timed_vs_oracle(c2):
+    """The north_star chain exactly as bench.py times it (chain_fn: Level-2 left in HBM
+    by the three stages -> level2_store_device -> prep.precompute_pointing on a side
+    stream -> read_comap_data_bands(device_outputs=True, pointing=...) -> ONE batched
+    solve to the reference's stopping rule, threshold 1e-6 / at most 100 iterations,
+    maps copied to the host while the CG runs), run twice (the second run reuses the
+    process caches the timed runs use), against the oracle per band: read_comap_data
+    (COMAPData.py:471-577) on the host Level-2 of the same observation, then
+    destriper_iteration (Destriper.py:402-453, run_destriper.py:146-189).
+    weight / hits / naive bit-exact, map <= 1e-5 relative, equal iteration counts."""
+    from concurrent.futures import ThreadPoolExecutor
+    import bench
+    import oracle.destriper as od
+    from oracle import comapdata as oc
+    data, _, h = c2
+    chain = bench.chain_fn(data, 0)
+    runs = [chain(False), chain(False)]
+    for k in ('map', 'naive', 'weight', 'hits'):
+        assert np.array_equal(runs[0]['maps'][k], runs[1]['maps'][k]), k
+    assert runs[0]['iters'] == runs[1]['iters']
+    got, iters = runs[1]['maps'], runs[1]['iters']
+    assert got['map'].shape == (4, 480 * 480)
+    obsid = int(data.obsid) if data.obsid > 0 else 1
+    store = bench.level2_store(h, data, obsid=obsid)
+    npix = 480 * 480
+
+    def ref_band(b):
+        tb, wb, pb = oc.read_comap_data(list(store), store, bench.c4_map_info(), iband=b, offset_length=50)[:3]
+        return od.destriper_iteration(np.asarray(pb, np.int64), tb, wb, 50, npix, threshold=1e-6, niter=100)
+    with ThreadPoolExecutor(4) as ex:
+        refs = list(ex.map(ref_band, range(4)))
+    for b, (ref, _, itr) in enumerate(refs):
+        assert iters[b] == itr, (b, iters, itr)
+        assert 1 < itr < 100, itr                  # converged by the threshold, not the cap
+        for k in ('weight', 'hits', 'naive'):
+            assert np.array_equal(got[k][b], ref[k]), (b, k)
+        assert rel(got['map'][b], ref['map']) < 1e-5, b
+
+
 def test_c5_two_observations_two_bands_vs_oracle():
     """Reduced C5: 2 observations x 19 feeds x 180,000 samples (6.8 M samples, 137k
     offsets, 480x480 CAR), 2 sidebands batched, 12 CG iterations, against the oracle
@@ -278,3 +317,73 @@ def test_c5_bench_size_four_bands_vs_oracle():
             assert np.array_equal(got[k][b], ref[k]), (b, k)
         assert rel(got['map'][b], ref['map']) < 1e-5, b
         assert rel(x[b], xr) < 1e-5, b
+
+
+C5_ITERS = 30
+
+
+def _c5_shard_rank(rank, world, port, q):
+    """One rank of the sharded C5 solve: its 4 of the 8 observations (whole offsets), the
+    map numerator compacted to the union of hit pixels and all-reduced with the p.q / r.r
+    block partials every iteration (the path rankplan.plan() picks for C5)."""
+    import os
+    import torch
+    import torch.distributed as dist
+    from comapreduce_amd import synthetic
+    from comapreduce_amd.mapmaking.destriper import DeviceDestriper
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    os.environ['COMAP_DS_RANKS'] = 'shard'
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    L, npix = 50, 480 * 480
+    pix, tod, w = synthetic.destriper_inputs_device(8, offset_length=L, device=0, seed=1000, n_bands=4)
+    n = pix.numel()
+    lo, hi = n * rank // world, n * (rank + 1) // world        # 4 observations x 19 feeds each
+    prob = DeviceDestriper(pix[lo:hi].contiguous(), tod[:, lo:hi].contiguous(), w[:, lo:hi].contiguous(), L, npix,
+                           device=0)
+    res = prob.solve(threshold=1e-6, niter=C5_ITERS)
+    q.put((rank, res['x'].cpu().numpy(), res['iters'], {k: v.cpu().numpy() for k, v in res['maps'].items()},
+           int(prob.hit_index.numel()) if prob.hit_index is not None else -1))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_c5_two_ranks_sharded_field_scale():
+    """The sharded multi-rank solve at field scale (C5 per-GPU size: 8 obs x 19 feeds x
+    180k samples, 4 bands, 547k offsets, 480x480 CAR), split 4 + 4 observations over 2
+    gloo ranks sharing cuda:0 (Destriper.py:61-82, 183-204: partial maps and CG sums
+    over ranks).  Offsets and maps <= 1e-9 of the single-rank solve, hits bit-exact,
+    equal iteration counts; the compacted union covers only the hit pixels."""
+    import os
+    import torch
+    import torch.multiprocessing as mp
+    from comapreduce_amd import synthetic
+    from comapreduce_amd.mapmaking.destriper import DeviceDestriper
+    L, npix = 50, 480 * 480
+    pix, tod, w = synthetic.destriper_inputs_device(8, offset_length=L, device=0, seed=1000, n_bands=4)
+    ref = DeviceDestriper(pix, tod, w, L, npix, device=0).solve(threshold=1e-6, niter=C5_ITERS)
+    rx = ref['x'].cpu().numpy()
+    rm = {k: v.cpu().numpy() for k, v in ref['maps'].items()}
+    del pix, tod, w, ref
+    torch.cuda.empty_cache()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = 29100 + os.getpid() % 190
+    procs = [ctx.Process(target=_c5_shard_rank, args=(r, 2, port, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=600) for _ in range(2)], key=lambda r: r[0])
+    for pr in procs:
+        pr.join(timeout=120)
+    assert list(res[0][2]) == list(res[1][2]) == [C5_ITERS] * 4
+    x = np.concatenate([res[0][1], res[1][1]], axis=-1)
+    assert x.shape == rx.shape == (4, 8 * 19 * 180_000 // L)
+    assert rel(x, rx) < 1e-9
+    for k in ('map', 'naive', 'weight', 'hits'):
+        assert res[0][3][k].shape == rm[k].shape, k
+        assert rel(res[0][3][k], rm[k]) < 1e-9, k
+        assert np.array_equal(res[0][3][k], res[1][3][k]), k          # every rank holds the same maps
+    assert np.array_equal(res[0][3]['hits'], rm['hits'])
+    nhit = res[0][4]
+    assert 0 < nhit < 0.5 * npix and nhit == res[1][4]

@@ -97,7 +97,7 @@ def _gloo_rank(rank, world, port, p, t, w, q):
     from comapreduce_amd.mapmaking.destriper import DeviceDestriper
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
-    os.environ['COMAP_DS_RANKS'] = 'shard'    # the sharded CG (small problems are gathered by default)
+    os.environ["COMAP_DS_RANKS"] = "shard"    # the sharded CG (the default; "auto" may gather small problems)
     torch.cuda.set_device(0)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     no = t.size // L
@@ -143,7 +143,7 @@ def _compact_rank(rank, world, port, p, t, w, npix, q):
     from comapreduce_amd.mapmaking.destriper import DeviceDestriper
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
-    os.environ['COMAP_DS_RANKS'] = 'shard'    # the sharded CG (small problems are gathered by default)
+    os.environ["COMAP_DS_RANKS"] = "shard"    # the sharded CG (the default; "auto" may gather small problems)
     torch.cuda.set_device(0)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     no = t.shape[-1] // L
@@ -195,7 +195,7 @@ def _uneven_rank(rank, world, port, p, t, w, frac, q):
     from comapreduce_amd.mapmaking.destriper import DeviceDestriper
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
-    os.environ['COMAP_DS_RANKS'] = 'shard'    # the sharded CG (small problems are gathered by default)
+    os.environ["COMAP_DS_RANKS"] = "shard"    # the sharded CG (the default; "auto" may gather small problems)
     torch.cuda.set_device(0)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     no = t.shape[-1] // L
