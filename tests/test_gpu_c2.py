@@ -353,7 +353,7 @@ def test_c5_two_ranks_sharded_field_scale():
     """The sharded multi-rank solve at field scale (C5 per-GPU size: 8 obs x 19 feeds x
     180k samples, 4 bands, 547k offsets, 480x480 CAR), split 4 + 4 observations over 2
     gloo ranks sharing cuda:0 (Destriper.py:61-82, 183-204: partial maps and CG sums
-    over ranks).  Offsets and maps <= 1e-9 of the single-rank solve, hits bit-exact,
+    over ranks).  Offsets and maps <= 1e-7 of the single-rank solve, hits bit-exact,
     equal iteration counts; the compacted union covers only the hit pixels."""
     import os
     import torch
@@ -379,10 +379,15 @@ def test_c5_two_ranks_sharded_field_scale():
     assert list(res[0][2]) == list(res[1][2]) == [C5_ITERS] * 4
     x = np.concatenate([res[0][1], res[1][1]], axis=-1)
     assert x.shape == rx.shape == (4, 8 * 19 * 180_000 // L)
-    assert rel(x, rx) < 1e-9
+    # two partial sums per all-reduce instead of one sequential sum: rounding-level
+    # differences, which 30 CG iterations carry into the offsets' unconstrained constant
+    # mode (A's null space) -- measured 4.9e-9 on band 1 (r04a); north_star allows 1e-5
+    for b in range(4):
+        assert rel(x[b], rx[b]) < 1e-7, b
     for k in ('map', 'naive', 'weight', 'hits'):
         assert res[0][3][k].shape == rm[k].shape, k
-        assert rel(res[0][3][k], rm[k]) < 1e-9, k
+        for b in range(4):
+            assert rel(res[0][3][k][b], rm[k][b]) < 1e-7, (k, b)
         assert np.array_equal(res[0][3][k], res[1][3][k]), k          # every rank holds the same maps
     assert np.array_equal(res[0][3]['hits'], rm['hits'])
     nhit = res[0][4]
