@@ -4,9 +4,10 @@
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 run_destriper.py parameters.ini
 
 One process per GPU (torch.distributed over RCCL, RANK/WORLD_SIZE from the
-environment) replaces mpi4py.  Per band: read_comap_data (host prep + one
-batched device median per rank) -> run_destriper (device CG, per-iteration
-SUM all-reduce of the map numerator) -> rank 0 writes the FITS maps.
+environment) replaces mpi4py.  The 4 sidebands together: read_comap_data_bands
+(the whole data prep on the device: weights, cuts, pixel ids, the 400-sample
+high-pass) -> one batched device destriper solve (per-iteration SUM all-reduce of
+the map numerator across ranks) -> rank 0 writes each band's FITS maps.
 
 Reference behaviours kept: files lacking averaged_tod/tod are dropped; the
 source of the FIRST file decides calibrator mode (offset_length 250,

@@ -4,7 +4,9 @@ make_golden.py --only-comapdata running the reference COMAPData module).
 
 The astrometric leaves (WCS, healpy Rotator, get_sun) are this repo's
 restatements on both sides, so these tests pin everything downstream of
-them; the leaves themselves are parity-unpinned."""
+them; the WCS and Sun leaves are pinned to astropy 4.3.1 separately
+(tests/test_astro_golden.py), healpy's Rotator / ang2pix stay unpinned
+(healpy is absent from the image)."""
 import os
 import sys
 
