@@ -78,6 +78,16 @@ struct comap_destriper {
     // problems, whose 4 kernels per iteration run shorter than their host enqueue; larger
     // ones enqueue eagerly (no capture: 0.4 ms at C4 that no replay won back)
     int cg_graph = -1;          // -1: by size (COMAP_DS_CGGRAPH=0 / 1 overrides)
+    // sliced-ELLPACK copy of the offset-major rows for the projection (COMAP_DS_SELL): chunk c
+    // = 64 consecutive offsets (one wave, lane = offset), padded to its longest row and stored
+    // column-major -- entry j of lane l at sbase[c] + 64 j + l -- so a lane streams its row
+    // with coalesced loads, no row-pointer load and no cross-lane reduction
+    bool sell = false;
+    int sell_u = 8;            // entry loads in flight per lane
+    int64_t nsell = 0;         // padded entries
+    int64_t *sbase = nullptr;  // [NC + 1]
+    int32_t *spix = nullptr;   // [nsell] pixel, -1 off-map, kSellPad padding
+    void *sco = nullptr;       // [nsell][nb] counts (uint8) or weights (f64)
     uint8_t *ocnt = nullptr;   // [nnz][nb]
     uint8_t *pcnt = nullptr;   // [nnzp][nb]
     double *wbar = nullptr;    // [NO][nb]
@@ -989,6 +999,146 @@ __global__ void __launch_bounds__(256) k_ds_project(const int64_t *__restrict__ 
     }
 }
 
+// ---------------------------------------------------------------- sliced-ELLPACK projection
+constexpr int32_t kSellPad = (int32_t)0x80808080;   // memset pattern 0x80: a padding slot
+
+// chunk widths: sw[c] = 64 x the longest row of offsets [64c, 64c + 64); sw[NC] = 0
+__global__ void k_sell_width(const int64_t *__restrict__ orow, int64_t NO, int64_t NC, int64_t *__restrict__ sw)
+{
+    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c > NC) return;
+    const int64_t o = c * 64 + (threadIdx.x & 63);
+    int64_t len = (c < NC && o < NO) ? orow[o + 1] - orow[o] : 0;
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) len = max(len, (int64_t)__shfl_xor(len, s, 64));
+    if ((threadIdx.x & 63) == 0) sw[c] = 64 * len;
+}
+
+// one thread per offset: its row's entries into the chunk's columns (coalesced writes)
+template <int NB, bool CF>
+__global__ void k_sell_fill(const int64_t *__restrict__ orow, const int32_t *__restrict__ opix,
+                            const void *__restrict__ oco, const int64_t *__restrict__ sbase, int64_t NO,
+                            int32_t *__restrict__ spix, void *__restrict__ sco)
+{
+    const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= NO) return;
+    const int64_t e0 = orow[o], n = orow[o + 1] - e0;
+    const int64_t b = sbase[o >> 6] + (o & 63);
+    for (int64_t j = 0; j < n; ++j) {
+        spix[b + 64 * j] = opix[e0 + j];
+        if constexpr (CF) {
+            const uint8_t *src = reinterpret_cast<const uint8_t *>(oco) + (e0 + j) * NB;
+            uint8_t *dst = reinterpret_cast<uint8_t *>(sco) + (b + 64 * j) * NB;
+#pragma unroll
+            for (int k = 0; k < NB; ++k) dst[k] = src[k];
+        } else {
+            const double *src = reinterpret_cast<const double *>(oco) + (e0 + j) * NB;
+            double *dst = reinterpret_cast<double *>(sco) + (b + 64 * j) * NB;
+#pragma unroll
+            for (int k = 0; k < NB; ++k) dst[k] = src[k];
+        }
+    }
+}
+
+// k_ds_project on the sliced-ELLPACK rows: one wave per chunk of 64 offsets (chunks dealt
+// to the grid's waves round-robin), lane = offset.  Each lane walks its row in groups of U
+// entries: the group's pixel ids and coefficients are coalesced loads issued one group
+// ahead of its map gathers, and the row sum is a plain in-order fma chain per lane (no
+// shuffles).  Same outputs as k_ds_project (y, block partials of y.x per band).
+template <int NB, bool CF, int U>
+__global__ void __launch_bounds__(256) k_ds_project_sell(const int64_t *__restrict__ sbase,
+                                                         const int32_t *__restrict__ spix, const void *__restrict__ sco,
+                                                         const double *__restrict__ wbar, const double *__restrict__ ws,
+                                                         const double *__restrict__ tw, const double *__restrict__ x,
+                                                         const double *__restrict__ num, const double *__restrict__ h,
+                                                         int64_t NO, int64_t npix, double *__restrict__ y,
+                                                         double *__restrict__ dot_part, const int32_t *__restrict__ flags,
+                                                         int64_t pstride = kPartMax)
+{
+    __shared__ double red[4 * NB];
+    if (cg_done(flags)) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t NC = (NO + 63) >> 6;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    double acc[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[b] = 0.0;
+    const int32_t last = (int32_t)(npix - 1);
+    for (int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < NC; c += nw) {
+        const int64_t b0 = sbase[c], W = (sbase[c + 1] - b0) >> 6;
+        const int64_t o = c * 64 + lane;
+        const int32_t *pp = spix + b0 + lane;
+        double g[NB];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) g[b] = 0.0;
+        int32_t q[U];
+        Coef<NB, CF> a[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool in = u < W;
+            q[u] = in ? pp[64 * u] : kSellPad;
+            if (in) a[u].load(sco, b0 + 64 * u + lane);
+        }
+        for (int64_t j = 0; j < W; j += U) {
+            double mv[U][NB];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (q[u] != kSellPad) {
+                    const int64_t qq = q[u] >= 0 ? q[u] : last;     // m[-1] for off-map samples
+                    if (h) {
+#pragma unroll
+                        for (int b = 0; b < NB; ++b) mv[u][b] = map_value(num, h, qq * NB + b);
+                    } else {
+                        ldb<NB>(num + qq * NB, mv[u]);
+                    }
+                }
+            }
+            const int64_t jn = j + U;
+            int32_t qn[U];
+            Coef<NB, CF> an[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const bool in = jn + u < W;
+                qn[u] = in ? pp[64 * (jn + u)] : kSellPad;
+                if (in) an[u].load(sco, b0 + 64 * (jn + u) + lane);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (q[u] != kSellPad) {
+#pragma unroll
+                    for (int b = 0; b < NB; ++b) g[b] = fma(a[u].get(b), mv[u][b], g[b]);
+                }
+#pragma unroll
+            for (int u = 0; u < U; ++u) { q[u] = qn[u]; a[u] = an[u]; }
+        }
+        if (o < NO) {
+            double xo[NB], v[NB];
+            if (x) {
+                ldb<NB>(x + o * NB, xo);
+            } else {
+#pragma unroll
+                for (int b = 0; b < NB; ++b) xo[b] = 0.0;
+            }
+            if constexpr (CF) {
+                double wb[NB];
+                ldb<NB>(wbar + o * NB, wb);
+#pragma unroll
+                for (int b = 0; b < NB; ++b) g[b] *= wb[b];
+            }
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                v[b] = (x ? ws[o * NB + b] * xo[b] : tw[o * NB + b]) - g[b];
+                if (dot_part) acc[b] = fma(v[b], xo[b], acc[b]);
+            }
+            stb<NB>(y + o * NB, v);
+        }
+    }
+    if (dot_part) {
+        block_partials<NB>(acc, red, dot_part + blockIdx.x, pstride);
+        if (pstride < kPartMax && blockIdx.x == 0) zero_tail<NB>(dot_part, pstride, gridDim.x);
+    }
+}
+
 // per-band block partials of sum_o a[o][b] c[o][b]
 template <int NB>
 __global__ void __launch_bounds__(256) k_dot_part(const double *__restrict__ a, const double *__restrict__ c, int64_t n,
@@ -1283,7 +1433,7 @@ inline int project_lanes(const comap_destriper *d)
 }
 inline unsigned project_grid(const comap_destriper *d, int64_t cap)
 {
-    const int64_t per = 256 / project_lanes(d);
+    const int64_t per = d->sell ? 256 : 256 / project_lanes(d);   // offsets per block sweep
     return (unsigned)std::max<int64_t>(1, std::min<int64_t>((d->NO + per - 1) / per, std::min<int64_t>(cap, d->proj_blocks)));
 }
 
@@ -1293,6 +1443,15 @@ unsigned launch_project_u(const comap_destriper *d, hipStream_t st, const double
                           const double *h, double *y, double *part, const int32_t *flags, int64_t pstride)
 {
     const unsigned pg = project_grid(d, pstride);
+    if (d->sell) {
+        if (d->sell_u == 4)
+            k_ds_project_sell<NB, CF, 4><<<pg, 256, 0, st>>>(d->sbase, d->spix, d->sco, d->wbar, d->ws, d->tw, x, num,
+                                                             h, d->NO, d->npix, y, part, flags, pstride);
+        else
+            k_ds_project_sell<NB, CF, 8><<<pg, 256, 0, st>>>(d->sbase, d->spix, d->sco, d->wbar, d->ws, d->tw, x, num,
+                                                             h, d->NO, d->npix, y, part, flags, pstride);
+        return pg;
+    }
     const void *co = CF ? (const void *)d->ocnt : (const void *)d->ow;
 #define COMAP_PROJ(G) k_ds_project<G, NB, CF, U><<<pg, 256, 0, st>>>(d->orow, d->opix, co, d->wbar, d->ws, d->tw, x, \
                                                                      num, h, d->NO, d->npix, y, part, flags, pstride)
@@ -1435,7 +1594,7 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     ar.cap = Arena::bytes<char>(cub_tb) + Arena::bytes<int64_t>(NO + 1) + 8 * Arena::bytes<int32_t>(N) +
              Arena::bytes<double>((size_t)N * 2 * NB) + Arena::bytes<int64_t>(npix + 1) +
              2 * Arena::bytes<int32_t>(npix) + Arena::bytes<int64_t>(2) + Arena::bytes<int32_t>(N) +
-             Arena::bytes<int32_t>(1) + 2 * Arena::bytes<uint64_t>(N);
+             Arena::bytes<int32_t>(1) + 2 * Arena::bytes<uint64_t>(N) + Arena::bytes<int64_t>(NO / 64 + 2);
     COMAP_CHECK(ctx, comap_tmp_alloc((void **)&ar.base, ar.cap, st));
     struct ArenaFree {
         Arena *a;
@@ -1459,6 +1618,8 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     int64_t *counts = ar.take<int64_t>(2);
     int32_t *nonuni = ar.take<int32_t>(1);
     uint64_t *epay = ar.take<uint64_t>(N), *epay2 = ar.take<uint64_t>(N);   // count form: offset << 32 | counts
+    const int64_t NC = (NO + 63) / 64;                                          // sliced-ELLPACK chunks
+    int64_t *swid = ar.take<int64_t>(NC + 1);
     // ---- 1. spatial processing order of the offsets
     if (spatial) {
         k_offset_keys<<<grid_for(NO), 256, 0, st>>>(pix, NO, L, npix, ekey, eval);
@@ -1476,6 +1637,17 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     COMAP_LAUNCH_CHECK(ctx);
     COMAP_CHECK(ctx, hipMemsetAsync(cnt + NO, 0, 8, st));
     COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(cub_tmp, scan_tb, cnt, d->orow, (int)(NO + 1), st));
+    {
+        const char *se = getenv("COMAP_DS_SELL");            // 1: sliced-ELLPACK projection
+        d->sell = se && se[0] == '1';
+    }
+    if (d->sell) {
+        if (dalloc(ctx, &d->sbase, NC + 1)) return -2;
+        k_sell_width<<<(unsigned)((NC + 1 + 3) / 4), 256, 0, st>>>(d->orow, NO, NC, swid);
+        COMAP_LAUNCH_CHECK(ctx);
+        COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(cub_tmp, scan_tb, swid, d->sbase, (int)(NC + 1), st));
+        COMAP_CHECK(ctx, hipMemcpyAsync(&d->nsell, d->sbase + NC, 8, hipMemcpyDeviceToHost, st));
+    }
     int32_t nonuni_h = 0;
     COMAP_CHECK(ctx, hipMemcpyAsync(&d->nnz, d->orow + NO, 8, hipMemcpyDeviceToHost, st));
     COMAP_CHECK(ctx, hipMemcpyAsync(&nonuni_h, nonuni, 4, hipMemcpyDeviceToHost, st));
@@ -1498,6 +1670,7 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         d->proj_u = env_int("COMAP_DS_PU", 4, {4, 8});
         d->proj_blocks = env_int("COMAP_DS_PB", kProjBlocks, {256, 512, 1024, 2048, 4096, 8192});
         d->cg_graph = env_int("COMAP_DS_CGGRAPH", -1, {0, 1});
+        d->sell_u = env_int("COMAP_DS_SU", 8, {4, 8});
     }
     rc |= dalloc(ctx, &d->opix, d->nnz);
     rc |= dalloc(ctx, &d->poff, d->nnz);          // nnzp <= nnz (off-map entries are not binned)
@@ -1519,6 +1692,20 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
                                                           d->opix, d->ow, nullptr, ekey, eval, eoff)));
     }
     COMAP_LAUNCH_CHECK(ctx);
+    if (d->sell) {
+        if (dalloc(ctx, &d->spix, d->nsell)) return -2;
+        if (d->cf ? dalloc(ctx, (uint8_t **)&d->sco, d->nsell * NB) : dalloc(ctx, (double **)&d->sco, d->nsell * NB))
+            return -2;
+        COMAP_CHECK(ctx, hipMemsetAsync(d->spix, 0x80, 4 * (size_t)d->nsell, st));
+        if (d->cf) {
+            COMAP_NB_SWITCH(nb, (k_sell_fill<NB, true><<<grid_for(NO, 1ll << 30), 256, 0, st>>>(
+                                    d->orow, d->opix, d->ocnt, d->sbase, NO, d->spix, d->sco)));
+        } else {
+            COMAP_NB_SWITCH(nb, (k_sell_fill<NB, false><<<grid_for(NO, 1ll << 30), 256, 0, st>>>(
+                                    d->orow, d->opix, d->ow, d->sbase, NO, d->spix, d->sco)));
+        }
+        COMAP_LAUNCH_CHECK(ctx);
+    }
     // ---- 4. pixel-major transpose (stable: offset order within a pixel)
     if (d->cf) {
         COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(cub_tmp, sort64_tb, ekey, ekey2, epay, epay2, (int)d->nnz,
@@ -1576,7 +1763,8 @@ extern "C" int comap_destripe_destroy(comap_destriper *d)
     // after a device sync; the blocks then go back to the caches
     (void)hipDeviceSynchronize();
     void *b[] = {d->orow, d->opix, d->ow, d->ws, d->tw, d->prow, d->poff, d->pw, d->h, d->hits, d->nnum, d->part, d->scal,
-                 d->cg, d->flags, d->hrow, d->hprow, d->perm, d->ocnt, d->pcnt, d->wbar, d->pt};
+                 d->cg, d->flags, d->hrow, d->hprow, d->perm, d->ocnt, d->pcnt, d->wbar, d->pt, d->sbase, d->spix,
+                 d->sco};
     comap_tmp_free_on(b, (int)(sizeof(b) / sizeof(b[0])), nullptr, true);
     comap_pinned_free(d->flags_host);
     comap_pinned_free(d->thr_host);

@@ -13,6 +13,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 SETTINGS = [
     {},
+    {'COMAP_DS_SELL': '1'},
+    {'COMAP_DS_SELL': '1', 'COMAP_DS_SU': '4'},
+    {'COMAP_DS_SELL': '1', 'COMAP_DS_PB': '2048'},
+    {'COMAP_DS_SELL': '1', 'COMAP_DS_SU': '4', 'COMAP_DS_PB': '2048'},
+    {'COMAP_DS_SELL': '1', 'COMAP_DS_PB': '512'},
     {'COMAP_DS_PG': '8'},
     {'COMAP_DS_PG': '8', 'COMAP_DS_PU': '8'},
     {'COMAP_DS_PG': '4', 'COMAP_DS_PU': '8'},
@@ -26,7 +31,7 @@ SETTINGS = [
     {'COMAP_DS_BL': '8'},
     {'COMAP_DS_BL': '16'},
 ]
-KEYS = ('COMAP_DS_PG', 'COMAP_DS_PU', 'COMAP_DS_PB', 'COMAP_DS_BU', 'COMAP_DS_BL')
+KEYS = ('COMAP_DS_PG', 'COMAP_DS_PU', 'COMAP_DS_PB', 'COMAP_DS_BU', 'COMAP_DS_BL', 'COMAP_DS_SELL', 'COMAP_DS_SU')
 
 
 def main():
