@@ -421,6 +421,7 @@ def destriper_c5_leg(n_obs, niter, device, world, rank, n_bands=1):
             'survey_bytes_per_band_iter_per_gpu': algo,
             'work_saving_vs_survey_bytes': algo * n_bands / max(op_bytes, 1),
             'operator_bytes_per_iter': op_bytes, 'entry_bytes': prob.entry_bytes(),
+            'sell_entries': prob.sell_entries(),
             'operator_roofline_frac': op_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 

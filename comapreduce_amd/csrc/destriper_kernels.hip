@@ -1778,6 +1778,8 @@ extern "C" int comap_destripe_destroy(comap_destriper *d)
 extern "C" int64_t comap_destripe_n_offsets(const comap_destriper *d) { return d ? d->NO : -1; }
 extern "C" int32_t comap_destripe_n_bands(const comap_destriper *d) { return d ? d->nb : -1; }
 
+extern "C" int64_t comap_destripe_sell_entries(const comap_destriper *d) { return d && d->sell ? d->nsell : -1; }
+
 extern "C" int32_t comap_destripe_entry_bytes(const comap_destriper *d)
 {
     return d ? (d->cf ? 4 + d->nb : 4 + 8 * d->nb) : -1;

@@ -317,6 +317,10 @@ class DeviceOps:
         """Bytes per operator entry: 4 + NB (count form) or 4 + 8 NB."""
         return int(N.lib().comap_destripe_entry_bytes(self.h))
 
+    def sell_entries(self):
+        """Padded entries of the projection's sliced-ELLPACK rows (-1: none)."""
+        return int(N.lib().comap_destripe_sell_entries(self.h))
+
     # ---- vector helpers
     def zeros(self, n):
         return self.torch.zeros(n, dtype=self.torch.float64, device=self.dev)
@@ -641,6 +645,9 @@ class DeviceDestriper:
 
     def entry_bytes(self):
         return self.ops.entry_bytes()
+
+    def sell_entries(self):
+        return self.ops.sell_entries()
 
     def solve(self, threshold=1e-6, niter=100, to_host=False):
         """to_host: maps as host NumPy arrays (rank 0; None on the others) -- one

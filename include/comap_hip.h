@@ -239,6 +239,9 @@ int comap_destripe_nnz(const comap_destriper *d, int64_t *nnz_offset_major, int6
  * non-zero weights per band are one value, so an entry keeps uint8 sample counts;
  * COMAP_DS_CF=0 disables it) or 4 + 8 n_bands (f64 weight sums). */
 int32_t comap_destripe_entry_bytes(const comap_destriper *d);
+/* Padded entries of the projection's sliced-ELLPACK row copy (COMAP_DS_SELL=1; chunks of
+ * 64 offsets padded to their longest row), or -1 when the problem has none. */
+int64_t comap_destripe_sell_entries(const comap_destriper *d);
 /* Local (this rank) sample-level maps, summed in binValues order:
  * h = sum w, hits = sum 1, naive_num = sum w tod (any may be NULL). */
 int comap_destripe_local_maps(comap_destriper *d, double *h_dev, double *hits_dev, double *naive_num_dev);
