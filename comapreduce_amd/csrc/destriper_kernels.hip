@@ -84,6 +84,8 @@ struct comap_destriper {
     // with coalesced loads, no row-pointer load and no cross-lane reduction
     bool sell = false;
     int sell_u = 8;            // entry loads in flight per lane
+    bool bin_xcd = false;      // XCD-contiguous block order of the bin (COMAP_DS_BXCD)
+    bool proj_xcd = false;     // ... of the sliced-ELLPACK projection (COMAP_DS_PXCD)
     int64_t nsell = 0;         // padded entries
     int64_t *sbase = nullptr;  // [NC + 1]
     int32_t *spix = nullptr;   // [nsell] pixel, -1 off-map, kSellPad padding
@@ -220,12 +222,9 @@ struct Coef<NB, false> {
 // and 233 -> 290 us for four -- the round-robin order streams the entry arrays with
 // every XCD on neighbouring lines, and the map / offset vectors are re-read from the
 // 256 MB Infinity Cache either way.
-#ifndef COMAP_DS_XCD
-#define COMAP_DS_XCD 0
-#endif
-__device__ __forceinline__ int64_t xcd_block(int64_t bid, int64_t nwg)
+__device__ __forceinline__ int64_t xcd_block(int64_t bid, int64_t nwg, bool on)
 {
-    if (!COMAP_DS_XCD) return bid;
+    if (!on) return bid;
     const int64_t q = nwg / 8, r = nwg % 8, x = bid % 8;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
 }
@@ -802,12 +801,13 @@ __global__ void __launch_bounds__(256) k_ds_bin(const int64_t *__restrict__ prow
                                                 const void *__restrict__ pw, const double *__restrict__ x,
                                                 int64_t npix, const double *__restrict__ base,
                                                 const double *__restrict__ hdiv, double *__restrict__ num,
-                                                const int32_t *__restrict__ flags, const int32_t *__restrict__ rows = nullptr)
+                                                const int32_t *__restrict__ flags, const int32_t *__restrict__ rows,
+                                                bool xcd)
 {
     if (cg_done(flags)) return;
     const int sub = threadIdx.x & (kBinLanes - 1);
     const int64_t step = (int64_t)gridDim.x * blockDim.x / kBinLanes;
-    const int64_t lb = xcd_block(blockIdx.x, gridDim.x);
+    const int64_t lb = xcd_block(blockIdx.x, gridDim.x, xcd);
     // rows != NULL: only the listed (non-empty) rows, npix = their count, and prow holds
     // their entry ranges (hprow: row i spans [prow[i], prow[i + 1]), no dependent row load)
     for (int64_t i = (lb * blockDim.x + threadIdx.x) / kBinLanes; i < npix; i += step) {
@@ -1053,18 +1053,21 @@ __global__ void __launch_bounds__(256) k_ds_project_sell(const int64_t *__restri
                                                          const double *__restrict__ num, const double *__restrict__ h,
                                                          int64_t NO, int64_t npix, double *__restrict__ y,
                                                          double *__restrict__ dot_part, const int32_t *__restrict__ flags,
-                                                         int64_t pstride = kPartMax)
+                                                         int64_t pstride, bool xcd)
 {
     __shared__ double red[4 * NB];
     if (cg_done(flags)) return;
     const int lane = threadIdx.x & 63;
     const int64_t NC = (NO + 63) >> 6;
     const int64_t nw = (int64_t)gridDim.x * 4;
+    // xcd: the blocks an XCD runs take a contiguous run of chunks (spatially sorted offsets:
+    // that XCD's L2 then holds one region of the map instead of all of it)
+    const int64_t lb = xcd_block(blockIdx.x, gridDim.x, xcd);
     double acc[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) acc[b] = 0.0;
     const int32_t last = (int32_t)(npix - 1);
-    for (int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < NC; c += nw) {
+    for (int64_t c = lb * 4 + (threadIdx.x >> 6); c < NC; c += nw) {
         const int64_t b0 = sbase[c], W = (sbase[c + 1] - b0) >> 6;
         const int64_t o = c * 64 + lane;
         const int32_t *pp = spix + b0 + lane;
@@ -1386,7 +1389,8 @@ void launch_bin_u(const comap_destriper *d, hipStream_t st, const double *x, con
     const int lanes = d->bin_lanes ? d->bin_lanes : (mean >= 24 ? 16 : (mean >= 10 ? 8 : 4));
     const unsigned g = grid_for(np * lanes, 65536);
     const void *co = CF ? (const void *)d->pcnt : (const void *)d->pw;
-#define COMAP_BIN(LN) k_ds_bin<LN, NB, CF, U><<<g, 256, 0, st>>>(rp, d->poff, co, x, np, base, hdiv, num, flags, rows)
+#define COMAP_BIN(LN) k_ds_bin<LN, NB, CF, U><<<g, 256, 0, st>>>(rp, d->poff, co, x, np, base, hdiv, num, flags, rows, \
+                                                                 d->bin_xcd)
     switch (lanes) {
     case 64: COMAP_BIN(64); break;
     case 32: COMAP_BIN(32); break;
@@ -1446,10 +1450,10 @@ unsigned launch_project_u(const comap_destriper *d, hipStream_t st, const double
     if (d->sell) {
         if (d->sell_u == 4)
             k_ds_project_sell<NB, CF, 4><<<pg, 256, 0, st>>>(d->sbase, d->spix, d->sco, d->wbar, d->ws, d->tw, x, num,
-                                                             h, d->NO, d->npix, y, part, flags, pstride);
+                                                             h, d->NO, d->npix, y, part, flags, pstride, d->proj_xcd);
         else
             k_ds_project_sell<NB, CF, 8><<<pg, 256, 0, st>>>(d->sbase, d->spix, d->sco, d->wbar, d->ws, d->tw, x, num,
-                                                             h, d->NO, d->npix, y, part, flags, pstride);
+                                                             h, d->NO, d->npix, y, part, flags, pstride, d->proj_xcd);
         return pg;
     }
     const void *co = CF ? (const void *)d->ocnt : (const void *)d->ow;
@@ -1671,6 +1675,8 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         d->proj_blocks = env_int("COMAP_DS_PB", kProjBlocks, {256, 512, 1024, 2048, 4096, 8192});
         d->cg_graph = env_int("COMAP_DS_CGGRAPH", -1, {0, 1});
         d->sell_u = env_int("COMAP_DS_SU", 8, {4, 8});
+        d->bin_xcd = env_int("COMAP_DS_BXCD", 0, {0, 1}) == 1;
+        d->proj_xcd = env_int("COMAP_DS_PXCD", 0, {0, 1}) == 1;
     }
     rc |= dalloc(ctx, &d->opix, d->nnz);
     rc |= dalloc(ctx, &d->poff, d->nnz);          // nnzp <= nnz (off-map entries are not binned)
