@@ -86,6 +86,8 @@ struct comap_destriper {
     int sell_u = 8;            // entry loads in flight per lane
     bool bin_xcd = false;      // XCD-contiguous block order of the bin (COMAP_DS_BXCD)
     bool proj_xcd = false;     // ... of the sliced-ELLPACK projection (COMAP_DS_PXCD)
+    bool ds_nt = false;        // non-temporal entry loads in the bin and the SELL projection (COMAP_DS_NT)
+    bool sell_pre = false;     // SELL projection: the lane's x / wbar / ws loaded before its row (COMAP_DS_SPRE)
     int64_t nsell = 0;         // padded entries
     int64_t *sbase = nullptr;  // [NC + 1]
     int32_t *spix = nullptr;   // [nsell] pixel, -1 off-map, kSellPad padding
@@ -147,6 +149,31 @@ __device__ __forceinline__ void ldb(const double *__restrict__ p, double (&v)[NB
     }
 }
 
+// streamed-once operands (the operator's entries): NT = non-temporal loads, which do not
+// allocate in L2 and so leave it to the gathered map / direction vectors
+template <bool NT, typename T>
+__device__ __forceinline__ T ld_nt(const T *p)
+{
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+template <int NB, bool NT>
+__device__ __forceinline__ void ldb_nt(const double *__restrict__ p, double (&v)[NB])
+{
+    if constexpr (NB % 2 == 0) {
+#pragma unroll
+        for (int b = 0; b < NB; b += 2) {
+            const d2v t = ld_nt<NT>(reinterpret_cast<const d2v *>(p + b));
+            v[b] = t.x;
+            v[b + 1] = t.y;
+        }
+    } else {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) v[b] = ld_nt<NT>(p + b);
+    }
+}
+
 template <int NB>
 __device__ __forceinline__ void stb(double *__restrict__ p, const double (&v)[NB])
 {
@@ -195,21 +222,23 @@ struct Coef;
 template <int NB>
 struct Coef<NB, true> {
     uint32_t v = 0;
+    template <bool NT = false>
     __device__ __forceinline__ void load(const void *__restrict__ base, int64_t k)
     {
         const uint8_t *c = reinterpret_cast<const uint8_t *>(base) + k * NB;
-        if constexpr (NB == 4) v = *reinterpret_cast<const uint32_t *>(c);
-        else if constexpr (NB == 2) v = *reinterpret_cast<const uint16_t *>(c);
-        else v = c[0];
+        if constexpr (NB == 4) v = ld_nt<NT>(reinterpret_cast<const uint32_t *>(c));
+        else if constexpr (NB == 2) v = ld_nt<NT>(reinterpret_cast<const uint16_t *>(c));
+        else v = ld_nt<NT>(c);
     }
     __device__ __forceinline__ double get(int b) const { return (double)((v >> (8 * b)) & 0xffu); }
 };
 template <int NB>
 struct Coef<NB, false> {
     double v[NB] = {};
+    template <bool NT = false>
     __device__ __forceinline__ void load(const void *__restrict__ base, int64_t k)
     {
-        ldb<NB>(reinterpret_cast<const double *>(base) + k * NB, v);
+        ldb_nt<NB, NT>(reinterpret_cast<const double *>(base) + k * NB, v);
     }
     __device__ __forceinline__ double get(int b) const { return v[b]; }
 };
@@ -796,7 +825,7 @@ __device__ __forceinline__ double map_value(const double *num, const double *h, 
 // entries), lane-strided; each lane issues kBinU entry loads, then kBinU gathers of the
 // NB-band x vectors, before its fmas (in entry order, so the sum is the plain
 // lane-strided one), then a kBinLanes-lane reduction.
-template <int kBinLanes, int NB, bool CF, int kBinU>
+template <int kBinLanes, int NB, bool CF, int kBinU, bool NT = false>
 __global__ void __launch_bounds__(256) k_ds_bin(const int64_t *__restrict__ prow, const int32_t *__restrict__ poff,
                                                 const void *__restrict__ pw, const double *__restrict__ x,
                                                 int64_t npix, const double *__restrict__ base,
@@ -830,8 +859,8 @@ __global__ void __launch_bounds__(256) k_ds_bin(const int64_t *__restrict__ prow
 #pragma unroll
         for (int u = 0; u < kBinU; ++u) {
             const bool in = k + u * kBinLanes < e1;
-            o[u] = in ? poff[k + u * kBinLanes] : 0;
-            if (in) a[u].load(pw, k + u * kBinLanes);
+            o[u] = in ? ld_nt<NT>(poff + k + u * kBinLanes) : 0;
+            if (in) a[u].template load<NT>(pw, k + u * kBinLanes);
         }
         while (k < e1) {
             double xv[kBinU][NB];
@@ -843,8 +872,8 @@ __global__ void __launch_bounds__(256) k_ds_bin(const int64_t *__restrict__ prow
 #pragma unroll
             for (int u = 0; u < kBinU; ++u) {
                 const bool in = kn + u * kBinLanes < e1;
-                on[u] = in ? poff[kn + u * kBinLanes] : 0;
-                if (in) an[u].load(pw, kn + u * kBinLanes);
+                on[u] = in ? ld_nt<NT>(poff + kn + u * kBinLanes) : 0;
+                if (in) an[u].template load<NT>(pw, kn + u * kBinLanes);
             }
 #pragma unroll
             for (int u = 0; u < kBinU; ++u)
@@ -1045,7 +1074,7 @@ __global__ void k_sell_fill(const int64_t *__restrict__ orow, const int32_t *__r
 // entries: the group's pixel ids and coefficients are coalesced loads issued one group
 // ahead of its map gathers, and the row sum is a plain in-order fma chain per lane (no
 // shuffles).  Same outputs as k_ds_project (y, block partials of y.x per band).
-template <int NB, bool CF, int U>
+template <int NB, bool CF, int U, bool NT = false, bool PRE = false>
 __global__ void __launch_bounds__(256) k_ds_project_sell(const int64_t *__restrict__ sbase,
                                                          const int32_t *__restrict__ spix, const void *__restrict__ sco,
                                                          const double *__restrict__ wbar, const double *__restrict__ ws,
@@ -1071,6 +1100,15 @@ __global__ void __launch_bounds__(256) k_ds_project_sell(const int64_t *__restri
         const int64_t b0 = sbase[c], W = (sbase[c + 1] - b0) >> 6;
         const int64_t o = c * 64 + lane;
         const int32_t *pp = spix + b0 + lane;
+        // PRE: the lane's own x / wbar / ws, loaded before the row walk (their latency then
+        // overlaps the gathers instead of following them)
+        double xo[NB], wb[NB], wsv[NB];
+        if constexpr (PRE) {
+            const int64_t oc = o < NO ? o : NO - 1;
+            if (x) ldb_nt<NB, NT>(x + oc * NB, xo);
+            if constexpr (CF) ldb_nt<NB, NT>(wbar + oc * NB, wb);
+            ldb_nt<NB, NT>((x ? ws : tw) + oc * NB, wsv);
+        }
         double g[NB];
 #pragma unroll
         for (int b = 0; b < NB; ++b) g[b] = 0.0;
@@ -1079,8 +1117,8 @@ __global__ void __launch_bounds__(256) k_ds_project_sell(const int64_t *__restri
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const bool in = u < W;
-            q[u] = in ? pp[64 * u] : kSellPad;
-            if (in) a[u].load(sco, b0 + 64 * u + lane);
+            q[u] = in ? ld_nt<NT>(pp + 64 * u) : kSellPad;
+            if (in) a[u].template load<NT>(sco, b0 + 64 * u + lane);
         }
         for (int64_t j = 0; j < W; j += U) {
             double mv[U][NB];
@@ -1102,8 +1140,8 @@ __global__ void __launch_bounds__(256) k_ds_project_sell(const int64_t *__restri
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const bool in = jn + u < W;
-                qn[u] = in ? pp[64 * (jn + u)] : kSellPad;
-                if (in) an[u].load(sco, b0 + 64 * (jn + u) + lane);
+                qn[u] = in ? ld_nt<NT>(pp + 64 * (jn + u)) : kSellPad;
+                if (in) an[u].template load<NT>(sco, b0 + 64 * (jn + u) + lane);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u)
@@ -1115,22 +1153,23 @@ __global__ void __launch_bounds__(256) k_ds_project_sell(const int64_t *__restri
             for (int u = 0; u < U; ++u) { q[u] = qn[u]; a[u] = an[u]; }
         }
         if (o < NO) {
-            double xo[NB], v[NB];
-            if (x) {
-                ldb<NB>(x + o * NB, xo);
-            } else {
+            double v[NB];
+            if constexpr (!PRE) {
+                if (x) ldb_nt<NB, NT>(x + o * NB, xo);
+                if constexpr (CF) ldb_nt<NB, NT>(wbar + o * NB, wb);
+                ldb_nt<NB, NT>((x ? ws : tw) + o * NB, wsv);
+            }
+            if (!x) {
 #pragma unroll
                 for (int b = 0; b < NB; ++b) xo[b] = 0.0;
             }
             if constexpr (CF) {
-                double wb[NB];
-                ldb<NB>(wbar + o * NB, wb);
 #pragma unroll
                 for (int b = 0; b < NB; ++b) g[b] *= wb[b];
             }
 #pragma unroll
             for (int b = 0; b < NB; ++b) {
-                v[b] = (x ? ws[o * NB + b] * xo[b] : tw[o * NB + b]) - g[b];
+                v[b] = (x ? wsv[b] * xo[b] : wsv[b]) - g[b];
                 if (dot_part) acc[b] = fma(v[b], xo[b], acc[b]);
             }
             stb<NB>(y + o * NB, v);
@@ -1391,6 +1430,21 @@ void launch_bin_u(const comap_destriper *d, hipStream_t st, const double *x, con
     const void *co = CF ? (const void *)d->pcnt : (const void *)d->pw;
 #define COMAP_BIN(LN) k_ds_bin<LN, NB, CF, U><<<g, 256, 0, st>>>(rp, d->poff, co, x, np, base, hdiv, num, flags, rows, \
                                                                  d->bin_xcd)
+    if constexpr (U == 4) {
+        if (d->ds_nt) {
+#define COMAP_BIN_NT(LN) k_ds_bin<LN, NB, CF, 4, true><<<g, 256, 0, st>>>(rp, d->poff, co, x, np, base, hdiv, num, \
+                                                                          flags, rows, d->bin_xcd)
+            switch (lanes) {
+            case 64: COMAP_BIN_NT(64); break;
+            case 32: COMAP_BIN_NT(32); break;
+            case 16: COMAP_BIN_NT(16); break;
+            case 8: COMAP_BIN_NT(8); break;
+            default: COMAP_BIN_NT(4);
+            }
+#undef COMAP_BIN_NT
+            return;
+        }
+    }
     switch (lanes) {
     case 64: COMAP_BIN(64); break;
     case 32: COMAP_BIN(32); break;
@@ -1448,12 +1502,14 @@ unsigned launch_project_u(const comap_destriper *d, hipStream_t st, const double
 {
     const unsigned pg = project_grid(d, pstride);
     if (d->sell) {
-        if (d->sell_u == 4)
-            k_ds_project_sell<NB, CF, 4><<<pg, 256, 0, st>>>(d->sbase, d->spix, d->sco, d->wbar, d->ws, d->tw, x, num,
-                                                             h, d->NO, d->npix, y, part, flags, pstride, d->proj_xcd);
-        else
-            k_ds_project_sell<NB, CF, 8><<<pg, 256, 0, st>>>(d->sbase, d->spix, d->sco, d->wbar, d->ws, d->tw, x, num,
-                                                             h, d->NO, d->npix, y, part, flags, pstride, d->proj_xcd);
+#define COMAP_SELL(UU, NT, PRE) k_ds_project_sell<NB, CF, UU, NT, PRE><<<pg, 256, 0, st>>>(                        \
+        d->sbase, d->spix, d->sco, d->wbar, d->ws, d->tw, x, num, h, d->NO, d->npix, y, part, flags, pstride, d->proj_xcd)
+        if (d->sell_u == 4) COMAP_SELL(4, false, false);
+        else if (d->ds_nt && d->sell_pre) COMAP_SELL(8, true, true);
+        else if (d->ds_nt) COMAP_SELL(8, true, false);
+        else if (d->sell_pre) COMAP_SELL(8, false, true);
+        else COMAP_SELL(8, false, false);
+#undef COMAP_SELL
         return pg;
     }
     const void *co = CF ? (const void *)d->ocnt : (const void *)d->ow;
@@ -1677,6 +1733,8 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         d->sell_u = env_int("COMAP_DS_SU", 8, {4, 8});
         d->bin_xcd = env_int("COMAP_DS_BXCD", 0, {0, 1}) == 1;
         d->proj_xcd = env_int("COMAP_DS_PXCD", 0, {0, 1}) == 1;
+        d->ds_nt = env_int("COMAP_DS_NT", 0, {0, 1}) == 1;
+        d->sell_pre = env_int("COMAP_DS_SPRE", 0, {0, 1}) == 1;
     }
     rc |= dalloc(ctx, &d->opix, d->nnz);
     rc |= dalloc(ctx, &d->poff, d->nnz);          // nnzp <= nnz (off-map entries are not binned)
