@@ -88,6 +88,8 @@ struct comap_destriper {
     bool proj_xcd = false;     // ... of the sliced-ELLPACK projection (COMAP_DS_PXCD)
     bool ds_nt = false;        // non-temporal entry loads in the bin and the SELL projection (COMAP_DS_NT)
     bool sell_pre = false;     // SELL projection: the lane's x / wbar / ws loaded before its row (COMAP_DS_SPRE)
+    int sell_cw = 64;          // offsets per SELL chunk: 64, or 32 for the 4-band lane-pair kernel
+    bool bin_pairs = false;    // 4 bands: lane-pair bin (COMAP_DS_BPAIR)
     int64_t nsell = 0;         // padded entries
     int64_t *sbase = nullptr;  // [NC + 1]
     int32_t *spix = nullptr;   // [nsell] pixel, -1 off-map, kSellPad padding
@@ -1031,38 +1033,40 @@ __global__ void __launch_bounds__(256) k_ds_project(const int64_t *__restrict__ 
 // ---------------------------------------------------------------- sliced-ELLPACK projection
 constexpr int32_t kSellPad = (int32_t)0x80808080;   // memset pattern 0x80: a padding slot
 
-// chunk widths: sw[c] = 64 x the longest row of offsets [64c, 64c + 64); sw[NC] = 0
+// chunk widths: sw[c] = CW x the longest row of offsets [CW c, CW c + CW); sw[NC] = 0.
+// CW (chunk width, offsets per chunk) = 64, or 32 for the 4-band lane-pair projection.
+template <int CW>
 __global__ void k_sell_width(const int64_t *__restrict__ orow, int64_t NO, int64_t NC, int64_t *__restrict__ sw)
 {
-    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / CW;
     if (c > NC) return;
-    const int64_t o = c * 64 + (threadIdx.x & 63);
+    const int64_t o = c * CW + (threadIdx.x & (CW - 1));
     int64_t len = (c < NC && o < NO) ? orow[o + 1] - orow[o] : 0;
 #pragma unroll
-    for (int s = 32; s > 0; s >>= 1) len = max(len, (int64_t)__shfl_xor(len, s, 64));
-    if ((threadIdx.x & 63) == 0) sw[c] = 64 * len;
+    for (int s = CW / 2; s > 0; s >>= 1) len = max(len, (int64_t)__shfl_xor(len, s, CW));
+    if ((threadIdx.x & (CW - 1)) == 0) sw[c] = CW * len;
 }
 
 // one thread per offset: its row's entries into the chunk's columns (coalesced writes)
 template <int NB, bool CF>
 __global__ void k_sell_fill(const int64_t *__restrict__ orow, const int32_t *__restrict__ opix,
-                            const void *__restrict__ oco, const int64_t *__restrict__ sbase, int64_t NO,
+                            const void *__restrict__ oco, const int64_t *__restrict__ sbase, int64_t NO, int cw,
                             int32_t *__restrict__ spix, void *__restrict__ sco)
 {
     const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (o >= NO) return;
     const int64_t e0 = orow[o], n = orow[o + 1] - e0;
-    const int64_t b = sbase[o >> 6] + (o & 63);
+    const int64_t b = sbase[o / cw] + (o % cw);
     for (int64_t j = 0; j < n; ++j) {
-        spix[b + 64 * j] = opix[e0 + j];
+        spix[b + cw * j] = opix[e0 + j];
         if constexpr (CF) {
             const uint8_t *src = reinterpret_cast<const uint8_t *>(oco) + (e0 + j) * NB;
-            uint8_t *dst = reinterpret_cast<uint8_t *>(sco) + (b + 64 * j) * NB;
+            uint8_t *dst = reinterpret_cast<uint8_t *>(sco) + (b + cw * j) * NB;
 #pragma unroll
             for (int k = 0; k < NB; ++k) dst[k] = src[k];
         } else {
             const double *src = reinterpret_cast<const double *>(oco) + (e0 + j) * NB;
-            double *dst = reinterpret_cast<double *>(sco) + (b + 64 * j) * NB;
+            double *dst = reinterpret_cast<double *>(sco) + (b + cw * j) * NB;
 #pragma unroll
             for (int k = 0; k < NB; ++k) dst[k] = src[k];
         }
@@ -1178,6 +1182,198 @@ __global__ void __launch_bounds__(256) k_ds_project_sell(const int64_t *__restri
     if (dot_part) {
         block_partials<NB>(acc, red, dot_part + blockIdx.x, pstride);
         if (pstride < kPartMax && blockIdx.x == 0) zero_tail<NB>(dot_part, pstride, gridDim.x);
+    }
+}
+
+// 4 bands, lane pairs: a 32-B gather of one entry's 4 bands by one lane is two 16-B load
+// instructions, each touching its own cache line per lane.  Here the lanes 2s and 2s + 1 take
+// the same entry, bands 0-1 and 2-3, so one load instruction gathers 32 entries' full
+// vectors with each pair on one 32-B segment: half the vector-memory line lookups per entry.
+// Chunks are 32 offsets (sliced-ELLPACK with CW = 32); both lanes of a pair read the entry's
+// pixel and counts (the same address).  Per offset and band the sum is the same in-order
+// chain as k_ds_project_sell's.
+template <bool CF, int U>
+__global__ void __launch_bounds__(256) k_ds_project_sell_pairs(const int64_t *__restrict__ sbase,
+                                                               const int32_t *__restrict__ spix,
+                                                               const void *__restrict__ sco,
+                                                               const double *__restrict__ wbar,
+                                                               const double *__restrict__ ws,
+                                                               const double *__restrict__ tw, const double *__restrict__ x,
+                                                               const double *__restrict__ num, const double *__restrict__ h,
+                                                               int64_t NO, int64_t npix, double *__restrict__ y,
+                                                               double *__restrict__ dot_part,
+                                                               const int32_t *__restrict__ flags, int64_t pstride)
+{
+    constexpr int NB = 4;
+    __shared__ double red[4 * NB];
+    if (cg_done(flags)) return;
+    const int lane = threadIdx.x & 63;
+    const int half = lane & 1, slot = lane >> 1;
+    const int64_t NC = (NO + 31) >> 5;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    double acc[2] = {0.0, 0.0};
+    const int32_t last = (int32_t)(npix - 1);
+    for (int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < NC; c += nw) {
+        const int64_t b0 = sbase[c], W = (sbase[c + 1] - b0) >> 5;
+        const int64_t o = c * 32 + slot;
+        const int32_t *pp = spix + b0 + slot;
+        double g[2] = {0.0, 0.0};
+        int32_t q[U];
+        Coef<NB, CF> a[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool in = u < W;
+            q[u] = in ? pp[32 * u] : kSellPad;
+            if (in) a[u].load(sco, b0 + 32 * u + slot);
+        }
+        for (int64_t j = 0; j < W; j += U) {
+            double mv[U][2];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (q[u] != kSellPad) {
+                    const int64_t qq = q[u] >= 0 ? q[u] : last;     // m[-1] for off-map samples
+                    if (h) {
+                        mv[u][0] = map_value(num, h, qq * NB + 2 * half);
+                        mv[u][1] = map_value(num, h, qq * NB + 2 * half + 1);
+                    } else {
+                        const d2v t = *reinterpret_cast<const d2v *>(num + qq * NB + 2 * half);
+                        mv[u][0] = t.x;
+                        mv[u][1] = t.y;
+                    }
+                }
+            }
+            const int64_t jn = j + U;
+            int32_t qn[U];
+            Coef<NB, CF> an[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const bool in = jn + u < W;
+                qn[u] = in ? pp[32 * (jn + u)] : kSellPad;
+                if (in) an[u].load(sco, b0 + 32 * (jn + u) + slot);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (q[u] != kSellPad) {
+                    g[0] = fma(a[u].get(2 * half), mv[u][0], g[0]);
+                    g[1] = fma(a[u].get(2 * half + 1), mv[u][1], g[1]);
+                }
+#pragma unroll
+            for (int u = 0; u < U; ++u) { q[u] = qn[u]; a[u] = an[u]; }
+        }
+        if (o < NO) {
+            const int64_t k = o * NB + 2 * half;
+            double xo[2] = {0.0, 0.0}, wsv[2], v[2];
+            if (x) {
+                const d2v t = *reinterpret_cast<const d2v *>(x + k);
+                xo[0] = t.x;
+                xo[1] = t.y;
+            }
+            {
+                const d2v t = *reinterpret_cast<const d2v *>((x ? ws : tw) + k);
+                wsv[0] = t.x;
+                wsv[1] = t.y;
+            }
+            if constexpr (CF) {
+                const d2v t = *reinterpret_cast<const d2v *>(wbar + k);
+                g[0] *= t.x;
+                g[1] *= t.y;
+            }
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                v[b] = (x ? wsv[b] * xo[b] : wsv[b]) - g[b];
+                if (dot_part) acc[b] = fma(v[b], xo[b], acc[b]);
+            }
+            d2v t;
+            t.x = v[0];
+            t.y = v[1];
+            *reinterpret_cast<d2v *>(y + k) = t;
+        }
+    }
+    if (dot_part) {
+        double a4[NB];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) a4[b] = ((b >> 1) == half) ? acc[b & 1] : 0.0;
+        block_partials<NB>(a4, red, dot_part + blockIdx.x, pstride);
+        if (pstride < kPartMax && blockIdx.x == 0) zero_tail<NB>(dot_part, pstride, gridDim.x);
+    }
+}
+
+// k_ds_bin for 4 bands with lane pairs (see k_ds_project_sell_pairs): kBinLanes lanes per
+// pixel row = kBinLanes / 2 entry slots, lanes 2s / 2s + 1 gather bands 0-1 / 2-3 of the
+// slot's entry as one 32-B segment; the pair-halves are reduced separately.
+template <int kBinLanes, bool CF, int kBinU>
+__global__ void __launch_bounds__(256) k_ds_bin_pairs(const int64_t *__restrict__ prow,
+                                                      const int32_t *__restrict__ poff, const void *__restrict__ pw,
+                                                      const double *__restrict__ x, int64_t npix,
+                                                      const double *__restrict__ base, const double *__restrict__ hdiv,
+                                                      double *__restrict__ num, const int32_t *__restrict__ flags,
+                                                      const int32_t *__restrict__ rows)
+{
+    constexpr int NB = 4;
+    constexpr int kSlots = kBinLanes / 2;
+    if (cg_done(flags)) return;
+    const int sub = threadIdx.x & (kBinLanes - 1);
+    const int half = sub & 1, slot = sub >> 1;
+    const int64_t step = (int64_t)gridDim.x * blockDim.x / kBinLanes;
+    for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kBinLanes; i < npix; i += step) {
+        const int64_t p = rows ? (int64_t)rows[i] : i;
+        double s0 = 0.0, s1 = 0.0;
+        double tail[2] = {0.0, 0.0};
+        if (slot == 0 && (base || hdiv)) {
+            const d2v t = *reinterpret_cast<const d2v *>((base ? base : hdiv) + p * NB + 2 * half);
+            tail[0] = t.x;
+            tail[1] = t.y;
+        }
+        const int64_t e1 = prow[i + 1];
+        int64_t k = prow[i] + slot;
+        int32_t o[kBinU];
+        Coef<NB, CF> a[kBinU];
+#pragma unroll
+        for (int u = 0; u < kBinU; ++u) {
+            const bool in = k + u * kSlots < e1;
+            o[u] = in ? poff[k + u * kSlots] : 0;
+            if (in) a[u].load(pw, k + u * kSlots);
+        }
+        while (k < e1) {
+            d2v xv[kBinU];
+#pragma unroll
+            for (int u = 0; u < kBinU; ++u) xv[u] = *reinterpret_cast<const d2v *>(x + (int64_t)o[u] * NB + 2 * half);
+            const int64_t kn = k + kSlots * kBinU;
+            int32_t on[kBinU];
+            Coef<NB, CF> an[kBinU];
+#pragma unroll
+            for (int u = 0; u < kBinU; ++u) {
+                const bool in = kn + u * kSlots < e1;
+                on[u] = in ? poff[kn + u * kSlots] : 0;
+                if (in) an[u].load(pw, kn + u * kSlots);
+            }
+#pragma unroll
+            for (int u = 0; u < kBinU; ++u)
+                if (k + u * kSlots < e1) {
+                    s0 = fma(a[u].get(2 * half), xv[u].x, s0);
+                    s1 = fma(a[u].get(2 * half + 1), xv[u].y, s1);
+                }
+#pragma unroll
+            for (int u = 0; u < kBinU; ++u) { o[u] = on[u]; a[u] = an[u]; }
+            k = kn;
+        }
+#pragma unroll
+        for (int w = kBinLanes / 2; w > 1; w >>= 1) {
+            s0 += __shfl_xor(s0, w, kBinLanes);
+            s1 += __shfl_xor(s1, w, kBinLanes);
+        }
+        if (slot == 0) {
+            double r[2] = {s0, s1};
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                if (base) r[b] = tail[b] - r[b];
+                else if (hdiv) { const double hv = tail[b]; r[b] = hv != 0.0 ? r[b] / hv : r[b]; }
+            }
+            d2v t;
+            t.x = r[0];
+            t.y = r[1];
+            *reinterpret_cast<d2v *>(num + p * NB + 2 * half) = t;
+        }
     }
 }
 
@@ -1430,6 +1626,20 @@ void launch_bin_u(const comap_destriper *d, hipStream_t st, const double *x, con
     const void *co = CF ? (const void *)d->pcnt : (const void *)d->pw;
 #define COMAP_BIN(LN) k_ds_bin<LN, NB, CF, U><<<g, 256, 0, st>>>(rp, d->poff, co, x, np, base, hdiv, num, flags, rows, \
                                                                  d->bin_xcd)
+    if constexpr (NB == 4) {
+        if (d->bin_pairs) {
+#define COMAP_BIN_P(LN) k_ds_bin_pairs<LN, CF, U><<<g, 256, 0, st>>>(rp, d->poff, co, x, np, base, hdiv, num, flags, rows)
+            switch (lanes) {
+            case 64: COMAP_BIN_P(64); break;
+            case 32: COMAP_BIN_P(32); break;
+            case 16: COMAP_BIN_P(16); break;
+            case 8: COMAP_BIN_P(8); break;
+            default: COMAP_BIN_P(4);
+            }
+#undef COMAP_BIN_P
+            return;
+        }
+    }
     if constexpr (U == 4) {
         if (d->ds_nt) {
 #define COMAP_BIN_NT(LN) k_ds_bin<LN, NB, CF, 4, true><<<g, 256, 0, st>>>(rp, d->poff, co, x, np, base, hdiv, num, \
@@ -1501,6 +1711,20 @@ unsigned launch_project_u(const comap_destriper *d, hipStream_t st, const double
                           const double *h, double *y, double *part, const int32_t *flags, int64_t pstride)
 {
     const unsigned pg = project_grid(d, pstride);
+    if (d->sell && d->sell_cw == 32) {
+        if constexpr (NB == 4) {
+            const int64_t per = 4 * 32;          // offsets per block sweep
+            const unsigned pg2 = (unsigned)std::max<int64_t>(
+                1, std::min<int64_t>((d->NO + per - 1) / per, std::min<int64_t>(pstride, d->proj_blocks)));
+            if (d->sell_u == 4)
+                k_ds_project_sell_pairs<CF, 4><<<pg2, 256, 0, st>>>(d->sbase, d->spix, d->sco, d->wbar, d->ws, d->tw,
+                                                                   x, num, h, d->NO, d->npix, y, part, flags, pstride);
+            else
+                k_ds_project_sell_pairs<CF, 8><<<pg2, 256, 0, st>>>(d->sbase, d->spix, d->sco, d->wbar, d->ws, d->tw,
+                                                                   x, num, h, d->NO, d->npix, y, part, flags, pstride);
+            return pg2;
+        }
+    }
     if (d->sell) {
 #define COMAP_SELL(UU, NT, PRE) k_ds_project_sell<NB, CF, UU, NT, PRE><<<pg, 256, 0, st>>>(                        \
         d->sbase, d->spix, d->sco, d->wbar, d->ws, d->tw, x, num, h, d->NO, d->npix, y, part, flags, pstride, d->proj_xcd)
@@ -1654,7 +1878,7 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     ar.cap = Arena::bytes<char>(cub_tb) + Arena::bytes<int64_t>(NO + 1) + 8 * Arena::bytes<int32_t>(N) +
              Arena::bytes<double>((size_t)N * 2 * NB) + Arena::bytes<int64_t>(npix + 1) +
              2 * Arena::bytes<int32_t>(npix) + Arena::bytes<int64_t>(2) + Arena::bytes<int32_t>(N) +
-             Arena::bytes<int32_t>(1) + 2 * Arena::bytes<uint64_t>(N) + Arena::bytes<int64_t>(NO / 64 + 2);
+             Arena::bytes<int32_t>(1) + 2 * Arena::bytes<uint64_t>(N) + Arena::bytes<int64_t>(NO / 32 + 2);
     COMAP_CHECK(ctx, comap_tmp_alloc((void **)&ar.base, ar.cap, st));
     struct ArenaFree {
         Arena *a;
@@ -1678,7 +1902,7 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     int64_t *counts = ar.take<int64_t>(2);
     int32_t *nonuni = ar.take<int32_t>(1);
     uint64_t *epay = ar.take<uint64_t>(N), *epay2 = ar.take<uint64_t>(N);   // count form: offset << 32 | counts
-    const int64_t NC = (NO + 63) / 64;                                          // sliced-ELLPACK chunks
+    const int64_t NC = (NO + 31) / 32;                      // sliced-ELLPACK chunks (at most, CW >= 32)
     int64_t *swid = ar.take<int64_t>(NC + 1);
     // ---- 1. spatial processing order of the offsets
     if (spatial) {
@@ -1701,12 +1925,18 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         const char *se = getenv("COMAP_DS_SELL");            // 1: sliced-ELLPACK projection
         d->sell = se && se[0] == '1';
     }
+    int64_t NCs = NC;
     if (d->sell) {
-        if (dalloc(ctx, &d->sbase, NC + 1)) return -2;
-        k_sell_width<<<(unsigned)((NC + 1 + 3) / 4), 256, 0, st>>>(d->orow, NO, NC, swid);
+        const char *pe = getenv("COMAP_DS_PPAIR");            // 4 bands: lane-pair SELL projection
+        d->sell_cw = (nb == 4 && pe && pe[0] == '1') ? 32 : 64;
+        NCs = (NO + d->sell_cw - 1) / d->sell_cw;
+        if (dalloc(ctx, &d->sbase, NCs + 1)) return -2;
+        const unsigned wg = (unsigned)(((NCs + 1) * d->sell_cw + 255) / 256);
+        if (d->sell_cw == 32) k_sell_width<32><<<wg, 256, 0, st>>>(d->orow, NO, NCs, swid);
+        else k_sell_width<64><<<wg, 256, 0, st>>>(d->orow, NO, NCs, swid);
         COMAP_LAUNCH_CHECK(ctx);
-        COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(cub_tmp, scan_tb, swid, d->sbase, (int)(NC + 1), st));
-        COMAP_CHECK(ctx, hipMemcpyAsync(&d->nsell, d->sbase + NC, 8, hipMemcpyDeviceToHost, st));
+        COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(cub_tmp, scan_tb, swid, d->sbase, (int)(NCs + 1), st));
+        COMAP_CHECK(ctx, hipMemcpyAsync(&d->nsell, d->sbase + NCs, 8, hipMemcpyDeviceToHost, st));
     }
     int32_t nonuni_h = 0;
     COMAP_CHECK(ctx, hipMemcpyAsync(&d->nnz, d->orow + NO, 8, hipMemcpyDeviceToHost, st));
@@ -1735,6 +1965,7 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         d->proj_xcd = env_int("COMAP_DS_PXCD", 0, {0, 1}) == 1;
         d->ds_nt = env_int("COMAP_DS_NT", 0, {0, 1}) == 1;
         d->sell_pre = env_int("COMAP_DS_SPRE", 0, {0, 1}) == 1;
+        d->bin_pairs = env_int("COMAP_DS_BPAIR", 0, {0, 1}) == 1;
     }
     rc |= dalloc(ctx, &d->opix, d->nnz);
     rc |= dalloc(ctx, &d->poff, d->nnz);          // nnzp <= nnz (off-map entries are not binned)
@@ -1763,10 +1994,10 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         COMAP_CHECK(ctx, hipMemsetAsync(d->spix, 0x80, 4 * (size_t)d->nsell, st));
         if (d->cf) {
             COMAP_NB_SWITCH(nb, (k_sell_fill<NB, true><<<grid_for(NO, 1ll << 30), 256, 0, st>>>(
-                                    d->orow, d->opix, d->ocnt, d->sbase, NO, d->spix, d->sco)));
+                                    d->orow, d->opix, d->ocnt, d->sbase, NO, d->sell_cw, d->spix, d->sco)));
         } else {
             COMAP_NB_SWITCH(nb, (k_sell_fill<NB, false><<<grid_for(NO, 1ll << 30), 256, 0, st>>>(
-                                    d->orow, d->opix, d->ow, d->sbase, NO, d->spix, d->sco)));
+                                    d->orow, d->opix, d->ow, d->sbase, NO, d->sell_cw, d->spix, d->sco)));
         }
         COMAP_LAUNCH_CHECK(ctx);
     }

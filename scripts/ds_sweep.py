@@ -13,16 +13,18 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 SETTINGS = [
     {},
-    {'COMAP_DS_NT': '1'},
     {'COMAP_DS_SELL': '1', 'COMAP_DS_PB': '2048'},
-    {'COMAP_DS_SELL': '1', 'COMAP_DS_PB': '2048', 'COMAP_DS_NT': '1'},
-    {'COMAP_DS_SELL': '1', 'COMAP_DS_PB': '2048', 'COMAP_DS_SPRE': '1'},
-    {'COMAP_DS_SELL': '1', 'COMAP_DS_PB': '2048', 'COMAP_DS_NT': '1', 'COMAP_DS_SPRE': '1'},
-    {'COMAP_DS_SELL': '1', 'COMAP_DS_PB': '1024', 'COMAP_DS_NT': '1', 'COMAP_DS_SPRE': '1'},
-    {'COMAP_DS_SELL': '1', 'COMAP_DS_PB': '4096', 'COMAP_DS_NT': '1', 'COMAP_DS_SPRE': '1'},
+    {'COMAP_DS_BPAIR': '1'},
+    {'COMAP_DS_SELL': '1', 'COMAP_DS_PB': '2048', 'COMAP_DS_PPAIR': '1'},
+    {'COMAP_DS_SELL': '1', 'COMAP_DS_PB': '2048', 'COMAP_DS_PPAIR': '1', 'COMAP_DS_BPAIR': '1'},
+    {'COMAP_DS_SELL': '1', 'COMAP_DS_PB': '1024', 'COMAP_DS_PPAIR': '1', 'COMAP_DS_BPAIR': '1'},
+    {'COMAP_DS_SELL': '1', 'COMAP_DS_PB': '4096', 'COMAP_DS_PPAIR': '1', 'COMAP_DS_BPAIR': '1'},
+    {'COMAP_DS_SELL': '1', 'COMAP_DS_PB': '2048', 'COMAP_DS_PPAIR': '1', 'COMAP_DS_BPAIR': '1', 'COMAP_DS_BL': '32'},
+    {'COMAP_DS_SELL': '1', 'COMAP_DS_PB': '2048', 'COMAP_DS_PPAIR': '1', 'COMAP_DS_BPAIR': '1', 'COMAP_DS_BU': '8'},
+    {'COMAP_DS_SELL': '1', 'COMAP_DS_PB': '2048', 'COMAP_DS_PPAIR': '1', 'COMAP_DS_BPAIR': '1', 'COMAP_DS_SU': '4'},
 ]
 KEYS = ('COMAP_DS_PG', 'COMAP_DS_PU', 'COMAP_DS_PB', 'COMAP_DS_BU', 'COMAP_DS_BL', 'COMAP_DS_SELL', 'COMAP_DS_SU',
-        'COMAP_DS_PXCD', 'COMAP_DS_BXCD', 'COMAP_DS_NT', 'COMAP_DS_SPRE')
+        'COMAP_DS_PXCD', 'COMAP_DS_BXCD', 'COMAP_DS_NT', 'COMAP_DS_SPRE', 'COMAP_DS_PPAIR', 'COMAP_DS_BPAIR')
 
 
 def main():

@@ -389,7 +389,8 @@ def test_graph_driver_captures_rccl_allreduce():
 
 @pytest.mark.parametrize('form,nb', [('count', 1), ('count', 4), ('count', 2), ('full', 1), ('full', 4),
                                      ('nonuniform', 1), ('nonuniform', 4), ('sell-count', 1), ('sell-count', 4),
-                                     ('sell-count', 2), ('sell-full', 1), ('sell-full', 4)])
+                                     ('sell-count', 2), ('sell-full', 1), ('sell-full', 4), ('pair-count', 4),
+                                     ('pair-full', 4)])
 def test_entry_forms_vs_oracle(form, nb, monkeypatch):
     """The operator's two entry forms against the oracle: the count form (uint8
     non-zero-sample counts per band, s_e = wbar_o c_e; chosen when every offset's
@@ -397,11 +398,16 @@ def test_entry_forms_vs_oracle(form, nb, monkeypatch):
     zeroed cuts are), the f64 weight sums (COMAP_DS_CF=0), and weights that vary inside
     an offset (the set-up falls back to the f64 form by itself).  Same solve to 1e-9,
     weight / hits bit-exact, the same iteration counts.  sell-*: the projection on the
-    sliced-ELLPACK copy of the offset rows (COMAP_DS_SELL=1), both entry forms."""
+    sliced-ELLPACK copy of the offset rows (COMAP_DS_SELL=1), both entry forms; pair-*:
+    4 bands with the lane-pair projection and bin."""
     import oracle.destriper as od
     from comapreduce_amd.mapmaking.destriper import DeviceDestriper
     if form.startswith('sell-'):
         monkeypatch.setenv('COMAP_DS_SELL', '1')
+        form = form[5:]
+    if form.startswith('pair-'):         # 4 bands: lane-pair SELL projection and bin
+        for k in ('COMAP_DS_SELL', 'COMAP_DS_PPAIR', 'COMAP_DS_BPAIR'):
+            monkeypatch.setenv(k, '1')
         form = form[5:]
     if form == 'full':
         monkeypatch.setenv('COMAP_DS_CF', '0')
