@@ -41,6 +41,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cmath>
+#include <type_traits>
 #include <cstdlib>
 #include <cstring>
 
@@ -125,6 +126,7 @@ constexpr int kProjBlocks = 1024; // k_ds_project grid cap: its p.q partials are
 constexpr int kDirBlocks = 1024;  // CG direction grid cap
 constexpr int kPartMax = 8192;     // >= every reduction grid below
 constexpr int kCgBatch = 16;       // CG iterations per replayed graph (one host check per batch)
+constexpr int64_t kSellMinOffsets = 131072;   // sliced-ELLPACK projection by default from this many offsets
 
 typedef double d2v __attribute__((ext_vector_type(2)));
 
@@ -1047,29 +1049,65 @@ __global__ void k_sell_width(const int64_t *__restrict__ orow, int64_t NO, int64
     if ((threadIdx.x & (CW - 1)) == 0) sw[c] = CW * len;
 }
 
-// one thread per offset: its row's entries into the chunk's columns (coalesced writes)
+// The sliced-ELLPACK fill, one workgroup per chunk: the chunk's CSR range (contiguous: its offsets are
+// consecutive rows) is staged in LDS with coalesced loads, then the padded column-major
+// slots are written in order (coalesced, padding included: no memset).  Chunks holding more
+// than kSellStage entries read their rows straight from global memory.
+constexpr int kSellStage = 4096;
 template <int NB, bool CF>
-__global__ void k_sell_fill(const int64_t *__restrict__ orow, const int32_t *__restrict__ opix,
-                            const void *__restrict__ oco, const int64_t *__restrict__ sbase, int64_t NO, int cw,
-                            int32_t *__restrict__ spix, void *__restrict__ sco)
+__global__ void __launch_bounds__(256) k_sell_fill_lds(const int64_t *__restrict__ orow,
+                                                       const int32_t *__restrict__ opix,
+                                                       const void *__restrict__ oco,
+                                                       const int64_t *__restrict__ sbase, int64_t NO, int cw,
+                                                       int32_t *__restrict__ spix, void *__restrict__ sco)
 {
-    const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (o >= NO) return;
-    const int64_t e0 = orow[o], n = orow[o + 1] - e0;
-    const int64_t b = sbase[o / cw] + (o % cw);
-    for (int64_t j = 0; j < n; ++j) {
-        spix[b + cw * j] = opix[e0 + j];
-        if constexpr (CF) {
-            const uint8_t *src = reinterpret_cast<const uint8_t *>(oco) + (e0 + j) * NB;
-            uint8_t *dst = reinterpret_cast<uint8_t *>(sco) + (b + cw * j) * NB;
+    using CoefT = typename std::conditional<CF, uint8_t, double>::type;
+    __shared__ int32_t lp[kSellStage];
+    __shared__ CoefT lc[CF ? kSellStage * NB : 1];
+    __shared__ int32_t rs[64], rn[64];
+    const int64_t c = blockIdx.x;
+    const int64_t o0 = c * cw;
+    const int nrow = (int)std::min<int64_t>(cw, NO - o0);
+    const int64_t e0 = orow[o0];
+    const int64_t ne = orow[o0 + nrow] - e0;
+    if (threadIdx.x < cw) {
+        const int r = threadIdx.x;
+        rs[r] = r < nrow ? (int)(orow[o0 + r] - e0) : 0;
+        rn[r] = r < nrow ? (int)(orow[o0 + r + 1] - orow[o0 + r]) : 0;
+    }
+    const bool staged = ne <= kSellStage && CF;
+    if (staged) {
+        for (int64_t i = threadIdx.x; i < ne; i += blockDim.x) {
+            lp[i] = opix[e0 + i];
 #pragma unroll
-            for (int k = 0; k < NB; ++k) dst[k] = src[k];
-        } else {
-            const double *src = reinterpret_cast<const double *>(oco) + (e0 + j) * NB;
-            double *dst = reinterpret_cast<double *>(sco) + (b + cw * j) * NB;
-#pragma unroll
-            for (int k = 0; k < NB; ++k) dst[k] = src[k];
+            for (int k = 0; k < NB; ++k) lc[i * NB + k] = reinterpret_cast<const CoefT *>(oco)[(e0 + i) * NB + k];
         }
+    }
+    __syncthreads();
+    const int64_t b0 = sbase[c], nslot = sbase[c + 1] - b0;
+    for (int64_t sl = threadIdx.x; sl < nslot; sl += blockDim.x) {
+        const int r = (int)(sl % cw);
+        const int64_t j = sl / cw;
+        const bool in = j < rn[r];
+        const int64_t ei = (int64_t)rs[r] + j;
+        int32_t q = kSellPad;
+        CoefT a[NB];
+#pragma unroll
+        for (int k = 0; k < NB; ++k) a[k] = 0;
+        if (in) {
+            if (staged) {
+                q = lp[ei];
+#pragma unroll
+                for (int k = 0; k < NB; ++k) a[k] = lc[ei * NB + k];
+            } else {
+                q = opix[e0 + ei];
+#pragma unroll
+                for (int k = 0; k < NB; ++k) a[k] = reinterpret_cast<const CoefT *>(oco)[(e0 + ei) * NB + k];
+            }
+        }
+        spix[b0 + sl] = q;
+#pragma unroll
+        for (int k = 0; k < NB; ++k) reinterpret_cast<CoefT *>(sco)[(b0 + sl) * NB + k] = a[k];
     }
 }
 
@@ -1922,8 +1960,11 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     COMAP_CHECK(ctx, hipMemsetAsync(cnt + NO, 0, 8, st));
     COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(cub_tmp, scan_tb, cnt, d->orow, (int)(NO + 1), st));
     {
-        const char *se = getenv("COMAP_DS_SELL");            // 1: sliced-ELLPACK projection
-        d->sell = se && se[0] == '1';
+        // sliced-ELLPACK projection: default for large problems (C5, 547k offsets: 1 band
+        // 0.112 -> 0.098 ms per CG iteration, 4 bands 0.261 -> 0.236, r04j); a C4-size problem
+        // (35k offsets) gains nothing its extra set-up pass would not cost.  COMAP_DS_SELL=0/1
+        const char *se = getenv("COMAP_DS_SELL");
+        d->sell = se ? se[0] == '1' : NO >= kSellMinOffsets;
     }
     int64_t NCs = NC;
     if (d->sell) {
@@ -1958,7 +1999,10 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         d->bin_u = env_int("COMAP_DS_BU", 4, {4, 8});
         d->proj_lanes = env_int("COMAP_DS_PG", 0, {4, 8, 16, 32, 64});
         d->proj_u = env_int("COMAP_DS_PU", 4, {4, 8});
-        d->proj_blocks = env_int("COMAP_DS_PB", kProjBlocks, {256, 512, 1024, 2048, 4096, 8192});
+        // the SELL projection runs one chunk per wave at 2048 blocks (1024: 0.254 vs 0.244 ms per
+        // 4-band C5 iteration, r04h); its p.q partials fit kPartMax and the dist slots below
+        d->proj_blocks = env_int("COMAP_DS_PB", d->sell ? 2 * kProjBlocks : kProjBlocks,
+                                 {256, 512, 1024, 2048, 4096, 8192});
         d->cg_graph = env_int("COMAP_DS_CGGRAPH", -1, {0, 1});
         d->sell_u = env_int("COMAP_DS_SU", 8, {4, 8});
         d->bin_xcd = env_int("COMAP_DS_BXCD", 0, {0, 1}) == 1;
@@ -1991,12 +2035,12 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         if (dalloc(ctx, &d->spix, d->nsell)) return -2;
         if (d->cf ? dalloc(ctx, (uint8_t **)&d->sco, d->nsell * NB) : dalloc(ctx, (double **)&d->sco, d->nsell * NB))
             return -2;
-        COMAP_CHECK(ctx, hipMemsetAsync(d->spix, 0x80, 4 * (size_t)d->nsell, st));
+        const unsigned nch = (unsigned)((NO + d->sell_cw - 1) / d->sell_cw);
         if (d->cf) {
-            COMAP_NB_SWITCH(nb, (k_sell_fill<NB, true><<<grid_for(NO, 1ll << 30), 256, 0, st>>>(
+            COMAP_NB_SWITCH(nb, (k_sell_fill_lds<NB, true><<<nch, 256, 0, st>>>(
                                     d->orow, d->opix, d->ocnt, d->sbase, NO, d->sell_cw, d->spix, d->sco)));
         } else {
-            COMAP_NB_SWITCH(nb, (k_sell_fill<NB, false><<<grid_for(NO, 1ll << 30), 256, 0, st>>>(
+            COMAP_NB_SWITCH(nb, (k_sell_fill_lds<NB, false><<<nch, 256, 0, st>>>(
                                     d->orow, d->opix, d->ow, d->sbase, NO, d->sell_cw, d->spix, d->sco)));
         }
         COMAP_LAUNCH_CHECK(ctx);
