@@ -226,7 +226,15 @@ def read_comap_data_bands(filelist, map_info, bands=(0, 1, 2, 3), use_gain_filte
                           device=pointing.device)
         hit[pointing + 1] = 1
         local = torch.nonzero(hit).reshape(-1) - 1
-    remapping_array = find_unique_values(local.cpu().numpy()).astype(int)
+    import torch.distributed as dist
+    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    if healpix or multi or not device_outputs:
+        # the union over ranks is a collective: every rank forms it here, in call order
+        remapping_array = find_unique_values(local.cpu().numpy()).astype(int)
+    else:
+        # one rank, device outputs (the in-memory chain): the union is the local set; it is
+        # copied to the host only when read, so the prep queues on without a host round trip
+        remapping_array = None
     mark('unique')
     if healpix:      # COMAPData.py:572-573: pixel ids -> positions in the union over ranks
         # index_replace (COMAPData.py:43-58) as written: the inverse sort permutation
@@ -240,6 +248,35 @@ def read_comap_data_bands(filelist, map_info, bands=(0, 1, 2, 3), use_gain_filte
            'ra': cut.ra, 'dec': cut.dec, 'feedid': cut.feedid, 'obsids': cut.obsid}
     if not device_outputs:
         out = {k: v.cpu().numpy() for k, v in out.items()}
-    out['remapping_array'] = remapping_array
+    if remapping_array is None:
+        out = _LazyOutputs(out)
+        out.lazy('remapping_array', lambda: np.unique(local.cpu().numpy()).astype(int))
+    else:
+        out['remapping_array'] = remapping_array
     mark('outputs')
     return out
+
+
+class _LazyOutputs(dict):
+    """read_comap_data_bands' result dict with entries computed on first access (a host
+    copy the caller may never need)."""
+
+    def lazy(self, key, fn):
+        self._lazy = getattr(self, '_lazy', {})
+        self._lazy[key] = fn
+        dict.__setitem__(self, key, None)
+
+    def __getitem__(self, key):
+        fns = getattr(self, '_lazy', {})
+        if key in fns:
+            dict.__setitem__(self, key, fns.pop(key)())
+        return dict.__getitem__(self, key)
+
+    def get(self, key, default=None):
+        return self[key] if key in self else default
+
+    def items(self):
+        return [(k, self[k]) for k in list(self.keys())]
+
+    def values(self):
+        return [self[k] for k in list(self.keys())]
