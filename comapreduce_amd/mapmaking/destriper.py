@@ -463,9 +463,7 @@ class DeviceOps:
         host = torch.from_numpy(host_np)
         ready = torch.cuda.Event()
         ready.record(cur)
-        cs = getattr(self, '_copy_stream', None)
-        if cs is None:
-            cs = self._copy_stream = torch.cuda.Stream(self.dev)
+        cs = copy_stream(self.dev)
         cs.wait_event(ready)
         with torch.cuda.stream(cs):
             host[1:].copy_(static, non_blocking=True)
@@ -479,6 +477,21 @@ class DeviceOps:
         cs.synchronize()
         maps = {k: host_np[i] for i, k in enumerate(('map', 'naive', 'weight', 'hits'))}
         return x, [int(v) for v in it][:nbo], maps
+
+
+_COPY_STREAMS = {}
+
+
+def copy_stream(dev):
+    """One side stream per device for the maps' device -> host copies, kept for the
+    process: a torch.cuda.Stream created per problem cost the chain ~1 ms of idle GPU before
+    its first CG kernel (the creation waits for the device, r04l trace)."""
+    import torch
+    key = torch.device(dev).index if not isinstance(dev, int) else dev
+    cs = _COPY_STREAMS.get(key)
+    if cs is None:
+        cs = _COPY_STREAMS[key] = torch.cuda.Stream(dev)
+    return cs
 
 
 class DeviceDestriper:
