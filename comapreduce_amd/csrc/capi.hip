@@ -322,10 +322,80 @@ void comap_pinned_trim()
         for (void *p : kv.second) (void)hipHostFree(p);
 }
 
+namespace {
+struct StageBlock {
+    void *p = nullptr;
+    size_t bytes = 0;
+    hipEvent_t ev = nullptr;    // recorded after the block's last copy
+};
+struct StagePool {
+    std::mutex mu;
+    std::vector<StageBlock> idle;
+};
+StagePool &stage_pool()
+{
+    static StagePool *s = new StagePool();
+    return *s;
+}
+}  // namespace
+
+hipError_t comap_upload(void *dst_dev, const void *src_host, size_t bytes, hipStream_t st)
+{
+    if (!bytes) return hipSuccess;
+    StagePool &sp = stage_pool();
+    StageBlock b;
+    {
+        std::lock_guard<std::mutex> lock(sp.mu);
+        for (size_t i = 0; i < sp.idle.size(); ++i) {
+            StageBlock &c = sp.idle[i];
+            if (c.bytes >= bytes && (!c.ev || hipEventQuery(c.ev) == hipSuccess)) {
+                b = c;
+                sp.idle.erase(sp.idle.begin() + (std::ptrdiff_t)i);
+                break;
+            }
+        }
+    }
+    if (!b.p) {
+        b.bytes = tmp_class(std::max<size_t>(bytes, 65536));
+        hipError_t e = hipHostMalloc(&b.p, b.bytes, hipHostMallocDefault);
+        if (e != hipSuccess) return e;
+        e = hipEventCreateWithFlags(&b.ev, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            (void)hipHostFree(b.p);
+            return e;
+        }
+    }
+    std::memcpy(b.p, src_host, bytes);
+    hipError_t e = hipMemcpyAsync(dst_dev, b.p, bytes, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipEventRecord(b.ev, st);
+    if (e != hipSuccess) (void)hipStreamSynchronize(st);    // the block is idle again either way
+    std::lock_guard<std::mutex> lock(sp.mu);
+    sp.idle.push_back(b);
+    return e;
+}
+
+static void stage_trim()
+{
+    StagePool &sp = stage_pool();
+    std::vector<StageBlock> v;
+    {
+        std::lock_guard<std::mutex> lock(sp.mu);
+        v.swap(sp.idle);
+    }
+    for (StageBlock &b : v) {
+        if (b.ev) {
+            (void)hipEventSynchronize(b.ev);
+            (void)hipEventDestroy(b.ev);
+        }
+        (void)hipHostFree(b.p);
+    }
+}
+
 extern "C" int comap_cache_trim(void)
 {
     comap_tmp_trim();
     comap_pinned_trim();
+    stage_trim();
     return 0;
 }
 

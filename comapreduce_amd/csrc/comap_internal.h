@@ -81,10 +81,16 @@ void comap_pinned_trim();
 hipError_t comap_stream_acquire(hipStream_t *s);
 void comap_stream_release(hipStream_t s);
 
+// Host -> device copy through a page-locked staging block: the host array may be reused
+// or freed as soon as this returns (the staging block is handed out again only once the
+// copy has run), so no stream synchronisation is needed for the host buffer's lifetime.
+hipError_t comap_upload(void *dst_dev, const void *src_host, size_t bytes, hipStream_t st);
+
 struct DevTemps {
     std::vector<void *> p;
     hipStream_t st = nullptr;
-    explicit DevTemps(hipStream_t s = nullptr) : st(s) {}
+    bool sync = true;     // false: no host wait on exit, the blocks are freed behind the stream's work
+    explicit DevTemps(hipStream_t s = nullptr, bool sync_on_exit = true) : st(s), sync(sync_on_exit) {}
     DevTemps(const DevTemps &) = delete;
     DevTemps &operator=(const DevTemps &) = delete;
     // stream-ordered pool allocations (the context keeps the device pool's memory cached,
@@ -101,8 +107,8 @@ struct DevTemps {
     ~DevTemps()
     {
         if (p.empty()) return;
-        (void)hipStreamSynchronize(st);
-        comap_tmp_free_on(p.data(), (int)p.size(), st, true);
+        if (sync) (void)hipStreamSynchronize(st);
+        comap_tmp_free_on(p.data(), (int)p.size(), st, sync);
     }
 };
 

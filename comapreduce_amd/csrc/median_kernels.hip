@@ -1129,18 +1129,17 @@ static int plan_slide(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
     mp->nsegs = (int32_t)segs.size();
     mp->njobs = (int32_t)jobs.size();
     hipStream_t st = ctx->stream;
-    COMAP_CHECK(ctx, hipMalloc((void **)&mp->jobs, sizeof(MedJob) * std::max<size_t>(1, jobs.size())));
-    COMAP_CHECK(ctx, hipMalloc((void **)&mp->segs, sizeof(SlideSeg) * std::max<size_t>(1, segs.size())));
-    if (!jobs.empty())
-        COMAP_CHECK(ctx, hipMemcpyAsync(mp->jobs, jobs.data(), sizeof(MedJob) * jobs.size(), hipMemcpyHostToDevice, st));
-    if (!segs.empty())
-        COMAP_CHECK(ctx, hipMemcpyAsync(mp->segs, segs.data(), sizeof(SlideSeg) * segs.size(), hipMemcpyHostToDevice, st));
+    mp->alloc_stream = st;
+    // (comap_median_plan_free returns these to the temporaries cache)
+    COMAP_CHECK(ctx, comap_tmp_alloc((void **)&mp->jobs, sizeof(MedJob) * std::max<size_t>(1, jobs.size()), st));
+    COMAP_CHECK(ctx, comap_tmp_alloc((void **)&mp->segs, sizeof(SlideSeg) * std::max<size_t>(1, segs.size()), st));
+    if (!jobs.empty()) COMAP_CHECK(ctx, comap_upload(mp->jobs, jobs.data(), sizeof(MedJob) * jobs.size(), st));
+    if (!segs.empty()) COMAP_CHECK(ctx, comap_upload(mp->segs, segs.data(), sizeof(SlideSeg) * segs.size(), st));
     const int sm = (int)slide_smem(w);
     COMAP_CHECK(ctx, hipFuncSetAttribute((const void *)k_med_slide<4>, hipFuncAttributeMaxDynamicSharedMemorySize, sm));
     COMAP_CHECK(ctx, hipFuncSetAttribute((const void *)k_med_slide<8>, hipFuncAttributeMaxDynamicSharedMemorySize, sm));
     COMAP_CHECK(ctx, hipFuncSetAttribute((const void *)k_med_slide<16>, hipFuncAttributeMaxDynamicSharedMemorySize, sm));
     COMAP_CHECK(ctx, hipFuncSetAttribute((const void *)k_med_slide<32>, hipFuncAttributeMaxDynamicSharedMemorySize, sm));
-    COMAP_CHECK(ctx, hipStreamSynchronize(st));   // host vectors go out of scope
     return 0;
 }
 
@@ -1289,14 +1288,12 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
     COMAP_CHECK(ctx, alloc((void **)&mp->redo, 4 * 3 * jobs.size()));   // flags | begin | end
     if (mp->wm) {
         COMAP_CHECK(ctx, alloc((void **)&mp->slo, 4 * jobs.size()));
-        COMAP_CHECK(ctx, hipMemcpyAsync(mp->slo, slo.data(), 4 * slo.size(), hipMemcpyHostToDevice, st));
+        COMAP_CHECK(ctx, comap_upload(mp->slo, slo.data(), 4 * slo.size(), st));
     }
     COMAP_CHECK(ctx, alloc((void **)&mp->krange, 16 * jobs.size()));    // per-series key min, max
-    COMAP_CHECK(ctx, hipMemcpyAsync(mp->jobs, jobs.data(), sizeof(MedJob) * jobs.size(), hipMemcpyHostToDevice, st));
-    COMAP_CHECK(ctx, hipMemcpyAsync(mp->seg, seg.data(), 4 * seg.size(), hipMemcpyHostToDevice, st));
-    if (!wsegs.empty())
-        COMAP_CHECK(ctx, hipMemcpyAsync(mp->segs, wsegs.data(), sizeof(SlideSeg) * wsegs.size(), hipMemcpyHostToDevice,
-                                        st));
+    COMAP_CHECK(ctx, comap_upload(mp->jobs, jobs.data(), sizeof(MedJob) * jobs.size(), st));
+    COMAP_CHECK(ctx, comap_upload(mp->seg, seg.data(), 4 * seg.size(), st));
+    if (!wsegs.empty()) COMAP_CHECK(ctx, comap_upload(mp->segs, wsegs.data(), sizeof(SlideSeg) * wsegs.size(), st));
     {
         // measured: C3 shard (106 series) 0.49 -> 0.40 ms of median, C2 (836) 2.06 -> 2.03
         const char *wenv = getenv("COMAP_SORT_WIDE");
@@ -1314,15 +1311,13 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
         COMAP_CHECK(ctx, hipFuncSetAttribute(mp->wmq ? (const void *)k_med_wm4 : (const void *)k_med_wm,
                                              hipFuncAttributeMaxDynamicSharedMemorySize,
                                              (int)std::max<size_t>(mp->wm_smem, 16)));
-        COMAP_CHECK(ctx, hipStreamSynchronize(st));   // host vectors go out of scope
-        return 0;
+        return 0;   // (the uploads went through staging: no host wait for the host vectors)
     }
     const size_t sm = walk_smem(mp->nwmax, mp->lc);
     if (sm > 160 * 1024) return comap_fail(ctx, -1, "median plan: LDS budget exceeded");
     const void *wk = mp->lc == 64 ? (const void *)k_med_walk<64> : mp->lc == 128 ? (const void *)k_med_walk<128>
                    : mp->lc == 512 ? (const void *)k_med_walk<512> : (const void *)k_med_walk<256>;
     COMAP_CHECK(ctx, hipFuncSetAttribute(wk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
-    COMAP_CHECK(ctx, hipStreamSynchronize(st));   // host vectors go out of scope
     return 0;
 }
 

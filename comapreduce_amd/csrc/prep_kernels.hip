@@ -657,7 +657,7 @@ extern "C" int comap_prep_percentiles(comap_ctx *ctx, const double *az, const do
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, (uint16_t *)nullptr, (uint16_t *)nullptr,
                                              (unsigned long long *)nullptr, (unsigned long long *)nullptr, (int)tot, 0,
                                              sbits, st);
-    DevTemps tmp(st);
+    DevTemps tmp(st, false);   // freed behind the queued work (stream-safe cache): no host wait
     unsigned long long *k0 = nullptr, *k1 = nullptr, *cnt = nullptr;
     uint16_t *s0 = nullptr, *s1 = nullptr;
     char *tb = nullptr;
@@ -706,7 +706,7 @@ extern "C" int comap_prep_highpass(comap_ctx *ctx, double *x, const int64_t *seg
     COMAP_DEVICE_GUARD(ctx);
     if (nseg == 0) return 0;
     hipStream_t st = ctx->stream;
-    DevTemps tmp(st);
+    DevTemps tmp(st, false);   // freed behind the queued work (stream-safe cache): no host wait
     int64_t *cnt = nullptr, *off = nullptr;
     COMAP_CHECK(ctx, tmp.alloc(&cnt, (size_t)nseg));
     COMAP_CHECK(ctx, tmp.alloc(&off, (size_t)nseg));
@@ -723,7 +723,7 @@ extern "C" int comap_prep_highpass(comap_ctx *ctx, double *x, const int64_t *seg
     COMAP_CHECK(ctx, tmp.alloc(&vals, (size_t)total));
     COMAP_CHECK(ctx, tmp.alloc(&filt, (size_t)total));
     COMAP_CHECK(ctx, tmp.alloc(&pos, (size_t)total));
-    COMAP_CHECK(ctx, hipMemcpyAsync(off, o.data(), 8 * (size_t)nseg, hipMemcpyHostToDevice, st));
+    COMAP_CHECK(ctx, comap_upload(off, o.data(), 8 * (size_t)nseg, st));
     k_seg_compact<<<nseg, 256, 0, st>>>(x, seg_dev, off, vals, pos);
     COMAP_LAUNCH_CHECK(ctx);
     std::vector<MedJob> jobs;
@@ -764,7 +764,8 @@ extern "C" int comap_prep_highpass(comap_ctx *ctx, double *x, const int64_t *seg
         const auto t1 = now();
         if (!rc) rc = comap_median_run(ctx, &mp);
         const auto t2 = now();
-        // the plan's buffers come from the stream-ordered pool: freed behind the walk, no sync
+        // the plan's buffers go back to the temporaries cache behind an event after the walk
+        // (reuse on another stream waits for it): no host wait
         comap_median_plan_free(&mp);
         const auto t3 = now();
         if (prof) {
@@ -788,8 +789,7 @@ extern "C" int comap_prep_highpass(comap_ctx *ctx, double *x, const int64_t *seg
         const size_t n = v.size();
         const double med = n % 2 ? v[n / 2] : (v[n / 2 - 1] + v[n / 2]) / 2.0;
         std::vector<double> f(n, med);
-        COMAP_CHECK(ctx, hipMemcpyAsync(filt + o[k], f.data(), 8 * n, hipMemcpyHostToDevice, st));
-        COMAP_CHECK(ctx, hipStreamSynchronize(st));
+        COMAP_CHECK(ctx, comap_upload(filt + o[k], f.data(), 8 * n, st));
     }
     k_seg_subtract<<<nseg, 256, 0, st>>>(x, seg_dev, off, cnt, filt, pos);
     COMAP_LAUNCH_CHECK(ctx);
@@ -811,7 +811,7 @@ extern "C" int comap_prep_cut(comap_ctx *ctx, const comap_prep_out *in, int32_t 
     *n_kept_out = 0;
     if (NO == 0) return 0;
     hipStream_t st = ctx->stream;
-    DevTemps tmp(st);
+    DevTemps tmp(st, false);   // freed behind the queued work (stream-safe cache): no host wait
     uint8_t *keep = nullptr;
     int32_t *kept = nullptr, *newo = nullptr;
     COMAP_CHECK(ctx, tmp.alloc(&keep, (size_t)nb * NO));

@@ -313,8 +313,10 @@ def prep_flat(files, filelist, map_info, bands, use_gain_filter, offset_length, 
         mark('highpass_upload')
         N.check(lib.comap_prep_highpass(c, N.dptr(out.tod), N.dptr(sd), n_segs, MEDFILT_STEP), c,
                 'comap_prep_highpass')
-    torch.cuda.current_stream(dev).synchronize()
     mark('highpass')
+    # every tensor kept alive above is either device memory on this stream (torch reuses it
+    # only in stream order), the side stream's percentiles (record_stream'd) or torch's
+    # pinned staging (freed behind its copy): released without a host wait
     del keep_alive
     mark('release')
     return out
