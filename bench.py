@@ -387,8 +387,8 @@ def destriper_c5_leg(n_obs, niter, device, world, rank, n_bands=1):
     L, npix = 50, 480 * 480
     pix, tod, w = synthetic.destriper_inputs_device(n_obs, offset_length=L, device=device, seed=1000 + rank,
                                                     n_bands=n_bands)
-    _timed_setup(pix, tod, w, L, npix, device=device)        # warm (first use of these sizes)
-    prob, setup = _timed_setup(pix, tod, w, L, npix, device=device)
+    _timed_setup(pix, tod, w, L, npix, device=device, map_shape=(480, 480))        # warm (first use of these sizes)
+    prob, setup = _timed_setup(pix, tod, w, L, npix, device=device, map_shape=(480, 480))
     prob.solve(threshold=0.0, niter=3)   # warm (graph capture, RCCL communicators)
     torch.cuda.synchronize()
     if world > 1:
@@ -422,7 +422,7 @@ def destriper_c5_leg(n_obs, niter, device, world, rank, n_bands=1):
             'survey_bytes_per_band_iter_per_gpu': algo,
             'work_saving_vs_survey_bytes': algo * n_bands / max(op_bytes, 1),
             'operator_bytes_per_iter': op_bytes, 'entry_bytes': prob.entry_bytes(),
-            'sell_entries': prob.sell_entries(),
+            'sell_entries': prob.sell_entries(), 'tile_segments': prob.tile_segments(),
             'operator_roofline_frac': op_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 

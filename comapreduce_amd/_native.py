@@ -81,6 +81,8 @@ _SIGS = {
     'comap_destripe_nnz': (c_int, [c_void_p, P_int64, P_int64]),
     'comap_destripe_entry_bytes': (ctypes.c_int32, [c_void_p]),
     'comap_destripe_sell_entries': (c_int64, [c_void_p]),
+    'comap_destripe_tiles': (c_int, [c_void_p, c_int64]),
+    'comap_destripe_tile_segments': (c_int64, [c_void_p]),
     'comap_destripe_local_maps': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     'comap_destripe_bin': (c_int, [c_void_p, c_void_p, c_int32, c_void_p]),
     'comap_destripe_project': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

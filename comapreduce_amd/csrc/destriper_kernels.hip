@@ -91,6 +91,21 @@ struct comap_destriper {
     bool sell_pre = false;     // SELL projection: the lane's x / wbar / ws loaded before its row (COMAP_DS_SPRE)
     int sell_cw = 64;          // offsets per SELL chunk: 64, or 32 for the 4-band lane-pair kernel
     bool bin_pairs = false;    // 4 bands: lane-pair bin (COMAP_DS_BPAIR)
+    // map-tile projection (comap_destripe_tiles): the offset rows split by map tile; a
+    // workgroup stages one tile of m in LDS and sums every (offset, tile) segment from
+    // there, a combine pass adds each offset's segments in tile order
+    bool tiles = false;
+    int64_t nx = 0, ntx = 0, nty = 0;
+    int tile_w = 0, tile_h = 0;        // tile width / height in pixels
+    int64_t nseg = 0, nchunk_t = 0, nwg_t = 0;
+    uint64_t *tent = nullptr;          // [chunk slots] hi32: local pixel (0xffffffff: padding), lo32: packed counts
+    double *tentw = nullptr;           // [chunk slots][nb] f64 weights (full form)
+    int64_t *tcbase = nullptr;         // [nchunk_t + 1] chunk slot starts
+    int32_t *tslot = nullptr;          // [nchunk_t * 64] partial slot of each chunk lane (-1: none)
+    int32_t *twg = nullptr;            // [nwg_t][2] (tile, first chunk), chunks of one tile per workgroup
+    int32_t *tcend = nullptr;          // [ntiles] one past the tile's last chunk
+    int64_t *pstart = nullptr;         // [NO + 1] an offset's partial slots
+    double *tpart = nullptr;           // [nseg][nb] per-(offset, tile) partial sums
     int64_t nsell = 0;         // padded entries
     int64_t *sbase = nullptr;  // [NC + 1]
     int32_t *spix = nullptr;   // [nsell] pixel, -1 off-map, kSellPad padding
@@ -1415,6 +1430,268 @@ __global__ void __launch_bounds__(256) k_ds_bin_pairs(const int64_t *__restrict_
     }
 }
 
+// ---------------------------------------------------------------- map-tile projection
+// Tiles of TW x TH map pixels hold 4096 / NB pixels (32 KB of m per tile in LDS).  An
+// entry's tile and local index come from its pixel (off-map entries gather m[npix - 1]).
+struct TileGeom {
+    int64_t nx, npix, ntx;
+    int tw, th;
+    __device__ __forceinline__ void of(int32_t q, int32_t &tile, int32_t &local) const
+    {
+        const int64_t p = (q >= 0 && q < npix) ? q : npix - 1;
+        const int64_t py = p / nx, px = p - py * nx;
+        tile = (int32_t)((py / th) * ntx + px / tw);
+        local = (int32_t)((py % th) * tw + px % tw);
+    }
+};
+
+// entry -> (tile key, entry id); the CSR rows are in internal offset order, so a stable
+// sort by tile leaves every tile's entries ordered by (offset, position in row)
+__global__ void k_tile_keys(const int32_t *__restrict__ opix, int64_t nnz, TileGeom g, int32_t *__restrict__ key,
+                            int32_t *__restrict__ val)
+{
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nnz; e += (int64_t)gridDim.x * blockDim.x) {
+        int32_t t, l;
+        g.of(opix[e], t, l);
+        key[e] = t;
+        val[e] = (int32_t)e;
+    }
+}
+
+// offset of every entry (the CSR row it sits in)
+__global__ void k_entry_offset(const int64_t *__restrict__ orow, int64_t NO, int32_t *__restrict__ eo)
+{
+    for (int64_t o = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; o < NO; o += (int64_t)gridDim.x * blockDim.x)
+        for (int64_t e = orow[o]; e < orow[o + 1]; ++e) eo[e] = (int32_t)o;
+}
+
+// segment starts in the tile-sorted order: flag[s] = 1 where (tile, offset) changes
+__global__ void k_seg_flags(const int32_t *__restrict__ tkey, const int32_t *__restrict__ sval,
+                            const int32_t *__restrict__ eo, int64_t n, int32_t *__restrict__ flag)
+{
+    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < n; s += (int64_t)gridDim.x * blockDim.x)
+        flag[s] = (s == 0 || tkey[s] != tkey[s - 1] || eo[sval[s]] != eo[sval[s - 1]]) ? 1 : 0;
+}
+
+// per segment: its tile, offset, first sorted position (segment id = inclusive scan - 1)
+__global__ void k_seg_table(const int32_t *__restrict__ tkey, const int32_t *__restrict__ sval,
+                            const int32_t *__restrict__ eo, const int32_t *__restrict__ flag,
+                            const int32_t *__restrict__ sid, int64_t n, int32_t *__restrict__ seg_tile,
+                            int32_t *__restrict__ seg_off, int32_t *__restrict__ seg_first)
+{
+    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < n; s += (int64_t)gridDim.x * blockDim.x)
+        if (flag[s]) {
+            const int32_t k = sid[s];
+            seg_tile[k] = tkey[s];
+            seg_off[k] = eo[sval[s]];
+            seg_first[k] = (int32_t)s;
+        }
+}
+
+// per tile: its first segment (segments are tile-major); chunk counts
+__global__ void k_tile_first_seg(const int32_t *__restrict__ seg_tile, int64_t nseg, int64_t ntiles,
+                                 int32_t *__restrict__ tfirst)
+{
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k <= nseg; k += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t t1 = k < nseg ? seg_tile[k] : (int32_t)ntiles;
+        const int32_t t0 = k > 0 ? seg_tile[k - 1] : -1;
+        for (int32_t t = t0 + 1; t <= t1 && t < ntiles + 1; ++t) tfirst[t] = (int32_t)k;
+    }
+}
+
+// chunk c (64 consecutive segments of one tile): its width (64 x longest segment)
+__global__ void k_tile_chunk_width(const int32_t *__restrict__ chunk_tile, const int32_t *__restrict__ chunk_seg0,
+                                   const int32_t *__restrict__ tfirst, const int32_t *__restrict__ seg_first,
+                                   int64_t nseg, int64_t nent, int64_t nchunk, int64_t *__restrict__ cw)
+{
+    const int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (c > nchunk) return;
+    int64_t len = 0;
+    if (c < nchunk) {
+        const int64_t k = (int64_t)chunk_seg0[c] + lane;
+        if (k < tfirst[chunk_tile[c] + 1]) len = (k + 1 < nseg ? seg_first[k + 1] : nent) - seg_first[k];
+    }
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) len = max(len, (int64_t)__shfl_xor(len, s, 64));
+    if (lane == 0) cw[c] = 64 * len;
+}
+
+// chunk slots: lane = segment, entry j of the segment at tcbase[c] + 64 j + lane; the
+// lane's partial slot
+template <int NB, bool CF>
+__global__ void k_tile_fill(const int32_t *__restrict__ chunk_tile, const int32_t *__restrict__ chunk_seg0,
+                            const int32_t *__restrict__ tfirst, const int32_t *__restrict__ seg_first,
+                            const int32_t *__restrict__ seg_slot, const int32_t *__restrict__ sval,
+                            const int32_t *__restrict__ opix, const void *__restrict__ oco, TileGeom g, int64_t nseg,
+                            int64_t nent, int64_t nchunk, const int64_t *__restrict__ tcbase, uint64_t *__restrict__ tent,
+                            double *__restrict__ tentw, int32_t *__restrict__ tslot)
+{
+    const int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (c >= nchunk) return;
+    const int64_t k = (int64_t)chunk_seg0[c] + lane;
+    const bool real = k < tfirst[chunk_tile[c] + 1];
+    const int64_t s0 = real ? seg_first[k] : 0;
+    const int64_t len = real ? (k + 1 < nseg ? seg_first[k + 1] : nent) - s0 : 0;
+    tslot[c * 64 + lane] = real ? seg_slot[k] : -1;
+    const int64_t b0 = tcbase[c], W = (tcbase[c + 1] - b0) >> 6;
+    for (int64_t j = 0; j < W; ++j) {
+        const int64_t slot = b0 + 64 * j + lane;
+        uint64_t v = ~0ull;
+        if (j < len) {
+            const int32_t e = sval[s0 + j];
+            int32_t t, l;
+            g.of(opix[e], t, l);
+            uint32_t pk = 0;
+            if constexpr (CF) {
+                const uint8_t *cc = reinterpret_cast<const uint8_t *>(oco) + (int64_t)e * NB;
+#pragma unroll
+                for (int b = 0; b < NB; ++b) pk |= (uint32_t)cc[b] << (8 * b);
+            } else {
+#pragma unroll
+                for (int b = 0; b < NB; ++b) tentw[slot * NB + b] = reinterpret_cast<const double *>(oco)[(int64_t)e * NB + b];
+            }
+            v = ((uint64_t)(uint32_t)l << 32) | pk;
+        }
+        tent[slot] = v;
+    }
+}
+
+__global__ void k_iota(int32_t *__restrict__ v, int64_t n)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        v[i] = (int32_t)i;
+}
+
+// segments sorted by offset (stable: tile order within an offset): slot of each segment =
+// its position; pstart[o] = first position of offset o (offsets without segments: the next)
+__global__ void k_seg_slots(const int32_t *__restrict__ offk, const int32_t *__restrict__ ids, int64_t nseg,
+                            int64_t NO, int32_t *__restrict__ seg_slot, int64_t *__restrict__ pstart)
+{
+    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s <= nseg; s += (int64_t)gridDim.x * blockDim.x) {
+        if (s < nseg) seg_slot[ids[s]] = (int32_t)s;
+        const int64_t o1 = s < nseg ? offk[s] : NO;
+        const int64_t o0 = s > 0 ? offk[s - 1] : -1;
+        for (int64_t o = o0 + 1; o <= o1 && o <= NO; ++o) pstart[o] = s;
+    }
+}
+
+// The tile pass: one workgroup = one tile's m staged in LDS + up to 4 of its chunks (one
+// per wave, lane = (offset, tile) segment); each lane's in-order fma chain over its
+// segment's entries from LDS; partial sums to tpart[slot].
+template <int NB, bool CF, int U>
+__global__ void __launch_bounds__(256) k_ds_project_tile(const int32_t *__restrict__ twg,
+                                                         const int32_t *__restrict__ tcend,
+                                                         const int64_t *__restrict__ tcbase,
+                                                         const uint64_t *__restrict__ tent,
+                                                         const double *__restrict__ tentw,
+                                                         const int32_t *__restrict__ tslot, TileGeom g,
+                                                         const double *__restrict__ num, const double *__restrict__ h,
+                                                         double *__restrict__ tpart, const int32_t *__restrict__ flags)
+{
+    constexpr int kTilePix = 4096 / NB;
+    __shared__ double m[kTilePix * NB];
+    if (cg_done(flags)) return;
+    const int32_t t = twg[2 * blockIdx.x], c0 = twg[2 * blockIdx.x + 1];
+    const int64_t ty = t / g.ntx, tx = t - ty * g.ntx;
+    // stage the tile: row r of the tile = tw pixels, NB doubles each, contiguous in the map
+    for (int i = threadIdx.x; i < g.tw * g.th * NB; i += blockDim.x) {
+        const int local = i / NB, b = i - local * NB;
+        const int64_t py = ty * g.th + local / g.tw, px = tx * g.tw + local % g.tw;
+        const int64_t p = py * g.nx + px;
+        double v = 0.0;
+        if (px < g.nx && p < g.npix) v = h ? map_value(num, h, p * NB + b) : num[p * NB + b];
+        m[i] = v;
+    }
+    __syncthreads();
+    const int64_t c = (int64_t)c0 + (threadIdx.x >> 6);
+    if (c >= tcend[t]) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t b0 = tcbase[c], W = (tcbase[c + 1] - b0) >> 6;
+    double acc[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[b] = 0.0;
+    for (int64_t j = 0; j < W; j += U) {
+        uint64_t v[U];
+        double wv[U][NB];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool in = j + u < W;
+            v[u] = in ? tent[b0 + 64 * (j + u) + lane] : ~0ull;
+            if constexpr (!CF) {
+                if (in) ldb<NB>(tentw + (b0 + 64 * (j + u) + lane) * NB, wv[u]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if ((uint32_t)(v[u] >> 32) != 0xffffffffu) {
+                const int l = (int)(v[u] >> 32);
+                const double *mm = m + l * NB;
+#pragma unroll
+                for (int b = 0; b < NB; ++b) {
+                    const double a = CF ? (double)((uint32_t)(v[u] >> (8 * b)) & 0xffu) : wv[u][b];
+                    acc[b] = fma(a, mm[b], acc[b]);
+                }
+            }
+        }
+    }
+    const int32_t sl = tslot[c * 64 + lane];
+    if (sl >= 0) stb<NB>(tpart + (int64_t)sl * NB, acc);
+}
+
+// y_o = ws_o x_o - wbar_o sum_t tpart[o, t] (tile order), block partials of y.x; x == NULL:
+// y_o = tw_o - ... (the b vector).  Same outputs as k_ds_project.
+template <int NB, bool CF>
+__global__ void __launch_bounds__(256) k_ds_tile_combine(const int64_t *__restrict__ pstart,
+                                                         const double *__restrict__ tpart,
+                                                         const double *__restrict__ wbar, const double *__restrict__ ws,
+                                                         const double *__restrict__ tw, const double *__restrict__ x,
+                                                         int64_t NO, double *__restrict__ y,
+                                                         double *__restrict__ dot_part, const int32_t *__restrict__ flags,
+                                                         int64_t pstride)
+{
+    __shared__ double red[4 * NB];
+    if (cg_done(flags)) return;
+    double acc[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[b] = 0.0;
+    for (int64_t o = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; o < NO; o += (int64_t)gridDim.x * blockDim.x) {
+        double gsum[NB], xo[NB], wsv[NB], v[NB];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) gsum[b] = 0.0;
+        const int64_t s1 = pstart[o + 1];
+        for (int64_t sidx = pstart[o]; sidx < s1; ++sidx) {
+            double pv[NB];
+            ldb<NB>(tpart + sidx * NB, pv);
+#pragma unroll
+            for (int b = 0; b < NB; ++b) gsum[b] += pv[b];
+        }
+        if (x) ldb<NB>(x + o * NB, xo);
+        else {
+#pragma unroll
+            for (int b = 0; b < NB; ++b) xo[b] = 0.0;
+        }
+        ldb<NB>((x ? ws : tw) + o * NB, wsv);
+        if constexpr (CF) {
+            double wb[NB];
+            ldb<NB>(wbar + o * NB, wb);
+#pragma unroll
+            for (int b = 0; b < NB; ++b) gsum[b] *= wb[b];
+        }
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            v[b] = (x ? wsv[b] * xo[b] : wsv[b]) - gsum[b];
+            if (dot_part) acc[b] = fma(v[b], xo[b], acc[b]);
+        }
+        stb<NB>(y + o * NB, v);
+    }
+    if (dot_part) {
+        block_partials<NB>(acc, red, dot_part + blockIdx.x, pstride);
+        if (pstride < kPartMax && blockIdx.x == 0) zero_tail<NB>(dot_part, pstride, gridDim.x);
+    }
+}
+
 // per-band block partials of sum_o a[o][b] c[o][b]
 template <int NB>
 __global__ void __launch_bounds__(256) k_dot_part(const double *__restrict__ a, const double *__restrict__ c, int64_t n,
@@ -1748,6 +2025,16 @@ template <int NB, bool CF, int U>
 unsigned launch_project_u(const comap_destriper *d, hipStream_t st, const double *x, const double *num,
                           const double *h, double *y, double *part, const int32_t *flags, int64_t pstride)
 {
+    if (d->tiles) {
+        const TileGeom g{d->nx, d->npix, d->ntx, d->tile_w, d->tile_h};
+        k_ds_project_tile<NB, CF, 8><<<(unsigned)d->nwg_t, 256, 0, st>>>(d->twg, d->tcend, d->tcbase, d->tent, d->tentw,
+                                                                     d->tslot, g, num, h, d->tpart, flags);
+        const unsigned cg = (unsigned)std::max<int64_t>(
+            1, std::min<int64_t>((d->NO + 255) / 256, std::min<int64_t>(pstride, d->proj_blocks)));
+        k_ds_tile_combine<NB, CF><<<cg, 256, 0, st>>>(d->pstart, d->tpart, d->wbar, d->ws, d->tw, x, d->NO, y, part,
+                                                      flags, pstride);
+        return cg;
+    }
     const unsigned pg = project_grid(d, pstride);
     if (d->sell && d->sell_cw == 32) {
         if constexpr (NB == 4) {
@@ -2103,7 +2390,7 @@ extern "C" int comap_destripe_destroy(comap_destriper *d)
     (void)hipDeviceSynchronize();
     void *b[] = {d->orow, d->opix, d->ow, d->ws, d->tw, d->prow, d->poff, d->pw, d->h, d->hits, d->nnum, d->part, d->scal,
                  d->cg, d->flags, d->hrow, d->hprow, d->perm, d->ocnt, d->pcnt, d->wbar, d->pt, d->sbase, d->spix,
-                 d->sco};
+                 d->sco, d->tent, d->tentw, d->tcbase, d->tslot, d->twg, d->tcend, d->pstart, d->tpart};
     comap_tmp_free_on(b, (int)(sizeof(b) / sizeof(b[0])), nullptr, true);
     comap_pinned_free(d->flags_host);
     comap_pinned_free(d->thr_host);
@@ -2123,6 +2410,166 @@ extern "C" int32_t comap_destripe_entry_bytes(const comap_destriper *d)
 {
     return d ? (d->cf ? 4 + d->nb : 4 + 8 * d->nb) : -1;
 }
+
+// Map-tile projection for a map laid out in rows of nx pixels (CAR / WCS maps: p = y nx +
+// x).  Builds, from the offset-major rows: the entries sorted by (tile, offset, position),
+// their (offset, tile) segments, each offset's partial slots in tile order, and per tile
+// sliced-ELLPACK chunks of 64 segments.  Synchronises the host twice (sizes).
+extern "C" int comap_destripe_tiles(comap_destriper *d, int64_t nx)
+{
+    if (!d) return -1;
+    COMAP_DEVICE_GUARD(d->ctx);
+    comap_ctx *ctx = d->ctx;
+    if (nx <= 0) return comap_fail(ctx, -1, "comap_destripe_tiles: nx must be positive");
+    if (d->tiles) return 0;
+    if (!d->cf && !d->ow) return comap_fail(ctx, -1, "comap_destripe_tiles: no offset-major weights");
+    hipStream_t st = ctx->stream;
+    const int nb = d->nb;
+    const int64_t nnz = d->nnz, NO = d->NO;
+    TileGeom g{};
+    g.nx = nx;
+    g.npix = d->npix;
+    g.tw = nb == 4 ? 32 : 64;
+    g.th = nb == 1 ? 64 : 32;
+    const int64_t ny = (d->npix + nx - 1) / nx;
+    g.ntx = (nx + g.tw - 1) / g.tw;
+    const int64_t nty = (ny + g.th - 1) / g.th;
+    const int64_t ntiles = g.ntx * nty;
+    if (ntiles >= (1ll << 30) || nnz >= (1ll << 31)) return comap_fail(ctx, -1, "comap_destripe_tiles: too large");
+    int tbits = 1;
+    while ((1ll << tbits) <= ntiles) ++tbits;
+    int obits = 1;
+    while ((1ll << obits) <= NO) ++obits;
+    DevTemps tmp(st, false);
+    int32_t *key = nullptr, *key2 = nullptr, *val = nullptr, *sval = nullptr, *eo = nullptr, *flag = nullptr,
+            *sid = nullptr;
+    COMAP_CHECK(ctx, tmp.alloc(&key, (size_t)nnz));
+    COMAP_CHECK(ctx, tmp.alloc(&key2, (size_t)nnz));
+    COMAP_CHECK(ctx, tmp.alloc(&val, (size_t)nnz));
+    COMAP_CHECK(ctx, tmp.alloc(&sval, (size_t)nnz));
+    COMAP_CHECK(ctx, tmp.alloc(&eo, (size_t)nnz));
+    COMAP_CHECK(ctx, tmp.alloc(&flag, (size_t)nnz));
+    COMAP_CHECK(ctx, tmp.alloc(&sid, (size_t)nnz));
+    size_t tb = 0, tb2 = 0, tb3 = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key, key2, val, sval, (int)nnz, 0, tbits, st);
+    (void)hipcub::DeviceScan::InclusiveSum(nullptr, tb2, flag, sid, (int)nnz, st);
+    char *cub = nullptr;
+    k_tile_keys<<<grid_for(nnz, 8192), 256, 0, st>>>(d->opix, nnz, g, key, val);
+    k_entry_offset<<<grid_for(NO, 8192), 256, 0, st>>>(d->orow, NO, eo);
+    COMAP_LAUNCH_CHECK(ctx);
+    COMAP_CHECK(ctx, tmp.alloc(&cub, std::max(tb, tb2) + 256));
+    COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(cub, tb, key, key2, val, sval, (int)nnz, 0, tbits, st));
+    k_seg_flags<<<grid_for(nnz, 8192), 256, 0, st>>>(key2, sval, eo, nnz, flag);
+    COMAP_LAUNCH_CHECK(ctx);
+    COMAP_CHECK(ctx, hipcub::DeviceScan::InclusiveSum(cub, tb2, flag, sid, (int)nnz, st));
+    int32_t nseg_h = 0;
+    COMAP_CHECK(ctx, hipMemcpyAsync(&nseg_h, sid + nnz - 1, 4, hipMemcpyDeviceToHost, st));
+    COMAP_CHECK(ctx, hipStreamSynchronize(st));
+    const int64_t nseg = nseg_h;
+    // sid is the inclusive scan: segment id = sid - 1
+    int32_t *seg_tile = nullptr, *seg_off = nullptr, *seg_first = nullptr, *seg_ids = nullptr, *seg_ids2 = nullptr,
+            *seg_offk = nullptr, *tfirst = nullptr, *seg_slot = nullptr;
+    COMAP_CHECK(ctx, tmp.alloc(&seg_tile, (size_t)nseg));
+    COMAP_CHECK(ctx, tmp.alloc(&seg_off, (size_t)nseg));
+    COMAP_CHECK(ctx, tmp.alloc(&seg_first, (size_t)nseg));
+    COMAP_CHECK(ctx, tmp.alloc(&seg_ids, (size_t)nseg));
+    COMAP_CHECK(ctx, tmp.alloc(&seg_ids2, (size_t)nseg));
+    COMAP_CHECK(ctx, tmp.alloc(&seg_offk, (size_t)nseg));
+    COMAP_CHECK(ctx, tmp.alloc(&seg_slot, (size_t)nseg));
+    COMAP_CHECK(ctx, tmp.alloc(&tfirst, (size_t)ntiles + 2));
+    {
+        // segment table (ids from the inclusive scan, shifted by one)
+        k_seg_table<<<grid_for(nnz, 8192), 256, 0, st>>>(key2, sval, eo, flag, sid, nnz, seg_tile - 1, seg_off - 1,
+                                                       seg_first - 1);
+        COMAP_LAUNCH_CHECK(ctx);
+    }
+    // each offset's slots in tile order: segments stably sorted by offset
+    k_iota<<<grid_for(nseg, 8192), 256, 0, st>>>(seg_ids, nseg);
+    COMAP_LAUNCH_CHECK(ctx);
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb3, seg_off, seg_offk, seg_ids, seg_ids2, (int)nseg, 0, obits,
+                                             st);
+    char *cub3 = nullptr;
+    COMAP_CHECK(ctx, tmp.alloc(&cub3, tb3 + 256));
+    COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(cub3, tb3, seg_off, seg_offk, seg_ids, seg_ids2, (int)nseg, 0,
+                                                        obits, st));
+    if (dalloc(ctx, &d->pstart, NO + 1) || dalloc(ctx, &d->tpart, (size_t)nseg * nb)) return -2;
+    k_seg_slots<<<grid_for(nseg, 8192), 256, 0, st>>>(seg_offk, seg_ids2, nseg, NO, seg_slot, d->pstart);
+    k_tile_first_seg<<<grid_for(nseg + 1, 8192), 256, 0, st>>>(seg_tile, nseg, ntiles, tfirst);
+    COMAP_LAUNCH_CHECK(ctx);
+    std::vector<int32_t> tf((size_t)ntiles + 1);
+    COMAP_CHECK(ctx, hipMemcpyAsync(tf.data(), tfirst, 4 * tf.size(), hipMemcpyDeviceToHost, st));
+    COMAP_CHECK(ctx, hipStreamSynchronize(st));
+    // chunks (64 segments of one tile) and workgroups (4 chunks of one tile) on the host
+    std::vector<int32_t> ch_tile, ch_seg0, wg, tcend((size_t)ntiles);
+    for (int64_t t = 0; t < ntiles; ++t) {
+        const int32_t k0 = tf[t], k1 = tf[t + 1];
+        const int32_t cfirst = (int32_t)ch_tile.size();
+        for (int32_t k = k0; k < k1; k += 64) {
+            ch_tile.push_back((int32_t)t);
+            ch_seg0.push_back(k);
+        }
+        tcend[t] = (int32_t)ch_tile.size();
+        for (int32_t c = cfirst; c < tcend[t]; c += 4) {
+            wg.push_back((int32_t)t);
+            wg.push_back(c);
+        }
+    }
+    const int64_t nchunk = (int64_t)ch_tile.size();
+    int32_t *dch_tile = nullptr, *dch_seg0 = nullptr;
+    int64_t *cw = nullptr;
+    COMAP_CHECK(ctx, tmp.alloc(&dch_tile, (size_t)nchunk + 1));
+    COMAP_CHECK(ctx, tmp.alloc(&dch_seg0, (size_t)nchunk + 1));
+    COMAP_CHECK(ctx, tmp.alloc(&cw, (size_t)nchunk + 1));
+    if (dalloc(ctx, &d->tcbase, nchunk + 1) || dalloc(ctx, &d->tslot, nchunk * 64) ||
+        dalloc(ctx, &d->twg, std::max<size_t>(wg.size(), 2)) || dalloc(ctx, &d->tcend, ntiles))
+        return -2;
+    if (nchunk) {
+        COMAP_CHECK(ctx, comap_upload(dch_tile, ch_tile.data(), 4 * ch_tile.size(), st));
+        COMAP_CHECK(ctx, comap_upload(dch_seg0, ch_seg0.data(), 4 * ch_seg0.size(), st));
+    }
+    if (!wg.empty()) COMAP_CHECK(ctx, comap_upload(d->twg, wg.data(), 4 * wg.size(), st));
+    COMAP_CHECK(ctx, comap_upload(d->tcend, tcend.data(), 4 * tcend.size(), st));
+    k_tile_chunk_width<<<(unsigned)(((nchunk + 1) * 64 + 255) / 256), 256, 0, st>>>(dch_tile, dch_seg0, tfirst, seg_first,
+                                                                              nseg, nnz, nchunk, cw);
+    COMAP_LAUNCH_CHECK(ctx);
+    size_t tb4 = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb4, cw, d->tcbase, (int)(nchunk + 1), st);
+    char *cub4 = nullptr;
+    COMAP_CHECK(ctx, tmp.alloc(&cub4, tb4 + 256));
+    COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(cub4, tb4, cw, d->tcbase, (int)(nchunk + 1), st));
+    int64_t nslots = 0;
+    COMAP_CHECK(ctx, hipMemcpyAsync(&nslots, d->tcbase + nchunk, 8, hipMemcpyDeviceToHost, st));
+    COMAP_CHECK(ctx, hipStreamSynchronize(st));
+    if (dalloc(ctx, &d->tent, std::max<int64_t>(nslots, 1))) return -2;
+    if (!d->cf && dalloc(ctx, &d->tentw, std::max<int64_t>(nslots, 1) * nb)) return -2;
+    if (nchunk) {
+        const unsigned gch = (unsigned)((nchunk * 64 + 255) / 256);
+        if (d->cf) {
+            COMAP_NB_SWITCH(nb, (k_tile_fill<NB, true><<<gch, 256, 0, st>>>(dch_tile, dch_seg0, tfirst, seg_first,
+                                                                           seg_slot, sval, d->opix, d->ocnt, g, nseg,
+                                                                           nnz, nchunk, d->tcbase, d->tent, d->tentw,
+                                                                           d->tslot)));
+        } else {
+            COMAP_NB_SWITCH(nb, (k_tile_fill<NB, false><<<gch, 256, 0, st>>>(dch_tile, dch_seg0, tfirst, seg_first,
+                                                                            seg_slot, sval, d->opix, d->ow, g, nseg,
+                                                                            nnz, nchunk, d->tcbase, d->tent,
+                                                                            d->tentw, d->tslot)));
+        }
+        COMAP_LAUNCH_CHECK(ctx);
+    }
+    d->nx = nx;
+    d->ntx = g.ntx;
+    d->nty = nty;
+    d->tile_w = g.tw;
+    d->tile_h = g.th;
+    d->nseg = nseg;
+    d->nchunk_t = nchunk;
+    d->nwg_t = (int64_t)wg.size() / 2;
+    d->tiles = d->nwg_t > 0;
+    return 0;
+}
+
+extern "C" int64_t comap_destripe_tile_segments(const comap_destriper *d) { return d && d->tiles ? d->nseg : -1; }
 
 extern "C" int comap_destripe_nnz(const comap_destriper *d, int64_t *nnz_offset_major, int64_t *nnz_pixel_major)
 {

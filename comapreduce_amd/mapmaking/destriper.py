@@ -231,7 +231,7 @@ class DeviceOps:
     N/L]) marks the offsets each band's data prep kept.  Per-band vectors are
     interleaved band-fastest ([N/L][nb], [npix][nb])."""
 
-    def __init__(self, pixels, tod, weights, offset_length, npix, device=None, keep=None):
+    def __init__(self, pixels, tod, weights, offset_length, npix, device=None, keep=None, map_shape=None):
         import torch
         self.torch = torch
         device = N.current_device() if device is None else int(device)
@@ -274,6 +274,14 @@ class DeviceOps:
                 'comap_destripe_create_bands')
         self.h = h
         self.n_offsets = int(N.lib().comap_destripe_n_offsets(h))
+        # map-tile projection (comap_destripe_tiles) for a row-major map of known width:
+        # COMAP_DS_TILES=1 / 0 forces it on / off, by default from TILE_MIN_OFFSETS offsets
+        te = os.environ.get('COMAP_DS_TILES')
+        if map_shape is not None and (te == '1' or (te is None and self.n_offsets >= TILE_MIN_OFFSETS)):
+            ny, nx = (int(v) for v in map_shape)
+            if ny * nx != self.npix:
+                raise ValueError(f'map_shape {map_shape} does not hold {self.npix} pixels')
+            N.check(N.lib().comap_destripe_tiles(h, nx), self.ctx, 'comap_destripe_tiles')
 
     def _t(self, a, dt):
         torch = self.torch
@@ -320,6 +328,10 @@ class DeviceOps:
     def sell_entries(self):
         """Padded entries of the projection's sliced-ELLPACK rows (-1: none)."""
         return int(N.lib().comap_destripe_sell_entries(self.h))
+
+    def tile_segments(self):
+        """(offset, map tile) segments of the tile projection (-1: not in use)."""
+        return int(N.lib().comap_destripe_tile_segments(self.h))
 
     # ---- vector helpers
     def zeros(self, n):
@@ -479,6 +491,7 @@ class DeviceOps:
         return x, [int(v) for v in it][:nbo], maps
 
 
+TILE_MIN_OFFSETS = 1 << 62     # map-tile projection: opt-in until measured (COMAP_DS_TILES=1)
 _COPY_STREAMS = {}
 
 
@@ -510,8 +523,9 @@ class DeviceDestriper:
     sharded).  The default is COMAP_DS_RANKS=shard until a multi-GPU run replaces the
     model's assumed all-reduce latency and bandwidth; gather forces the other."""
 
-    def __init__(self, pixels, tod, weights, offset_length, npix, device=None, keep=None):
+    def __init__(self, pixels, tod, weights, offset_length, npix, device=None, keep=None, map_shape=None):
         self.npix_full, self.hit_index = int(npix), None
+        self.map_shape = map_shape
         self.multi = np.ndim(tod) == 2 if not hasattr(tod, 'dim') else tod.dim() == 2
         self.gathered, self.plan = None, None
         d = _dist()
@@ -521,7 +535,8 @@ class DeviceDestriper:
                 return
             if os.environ.get('COMAP_DS_COMPACT', '1') != '0':
                 pixels, npix = self._compact(pixels, int(npix), device)
-        self.ops = N.retry_oom(DeviceOps, pixels, tod, weights, offset_length, npix, device, keep)
+                map_shape = None                 # the relabelled pixels have no map layout
+        self.ops = N.retry_oom(DeviceOps, pixels, tod, weights, offset_length, npix, device, keep, map_shape)
 
     # ---- rank policy
     def _choose_gather(self, d, pixels, tod, offset_length):
@@ -587,7 +602,7 @@ class DeviceDestriper:
         k_all = cat(kp, L) if kp is not None else None
         if not self.multi:
             t_all, w_all = t_all.reshape(-1), w_all.reshape(-1)
-        self.ops = DeviceOps(p_all, t_all, w_all, L, npix, device, k_all)
+        self.ops = DeviceOps(p_all, t_all, w_all, L, npix, device, k_all, self.map_shape)
         self._ref = (device, nbands)
 
     def _solve_gathered(self, d, threshold, niter):
@@ -661,6 +676,9 @@ class DeviceDestriper:
 
     def sell_entries(self):
         return self.ops.sell_entries()
+
+    def tile_segments(self):
+        return self.ops.tile_segments()
 
     def solve(self, threshold=1e-6, niter=100, to_host=False):
         """to_host: maps as host NumPy arrays (rank 0; None on the others) -- one

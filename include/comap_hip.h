@@ -242,6 +242,14 @@ int32_t comap_destripe_entry_bytes(const comap_destriper *d);
 /* Padded entries of the projection's sliced-ELLPACK row copy (COMAP_DS_SELL=1; chunks of
  * 64 offsets padded to their longest row), or -1 when the problem has none. */
 int64_t comap_destripe_sell_entries(const comap_destriper *d);
+/* Map-tile projection (optional, after create): the map is laid out in rows of nx pixels
+ * (CAR / WCS maps, p = y nx + x).  The projection then stages one tile of the map (32 KB:
+ * 32 x 32 pixels for 4 bands, 64 x 32 for 2, 64 x 64 for 1) in LDS per workgroup and sums
+ * each (offset, tile) segment of the offset rows from there; a combine pass adds an
+ * offset's segments in tile order.  Synchronises the host.  _tile_segments: the number of
+ * (offset, tile) segments, or -1 without tiles. */
+int comap_destripe_tiles(comap_destriper *d, int64_t nx);
+int64_t comap_destripe_tile_segments(const comap_destriper *d);
 /* Local (this rank) sample-level maps, summed in binValues order:
  * h = sum w, hits = sum 1, naive_num = sum w tod (any may be NULL). */
 int comap_destripe_local_maps(comap_destriper *d, double *h_dev, double *hits_dev, double *naive_num_dev);

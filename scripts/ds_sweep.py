@@ -13,18 +13,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 SETTINGS = [
     {},
-    {'COMAP_DS_SELL': '1', 'COMAP_DS_PB': '2048'},
-    {'COMAP_DS_BPAIR': '1'},
-    {'COMAP_DS_SELL': '1', 'COMAP_DS_PB': '2048', 'COMAP_DS_PPAIR': '1'},
-    {'COMAP_DS_SELL': '1', 'COMAP_DS_PB': '2048', 'COMAP_DS_PPAIR': '1', 'COMAP_DS_BPAIR': '1'},
-    {'COMAP_DS_SELL': '1', 'COMAP_DS_PB': '1024', 'COMAP_DS_PPAIR': '1', 'COMAP_DS_BPAIR': '1'},
-    {'COMAP_DS_SELL': '1', 'COMAP_DS_PB': '4096', 'COMAP_DS_PPAIR': '1', 'COMAP_DS_BPAIR': '1'},
-    {'COMAP_DS_SELL': '1', 'COMAP_DS_PB': '2048', 'COMAP_DS_PPAIR': '1', 'COMAP_DS_BPAIR': '1', 'COMAP_DS_BL': '32'},
-    {'COMAP_DS_SELL': '1', 'COMAP_DS_PB': '2048', 'COMAP_DS_PPAIR': '1', 'COMAP_DS_BPAIR': '1', 'COMAP_DS_BU': '8'},
-    {'COMAP_DS_SELL': '1', 'COMAP_DS_PB': '2048', 'COMAP_DS_PPAIR': '1', 'COMAP_DS_BPAIR': '1', 'COMAP_DS_SU': '4'},
+    {'COMAP_DS_TILES': '1'},
+    {'COMAP_DS_TILES': '1', 'COMAP_DS_PB': '1024'},
+    {'COMAP_DS_SELL': '0'},
 ]
 KEYS = ('COMAP_DS_PG', 'COMAP_DS_PU', 'COMAP_DS_PB', 'COMAP_DS_BU', 'COMAP_DS_BL', 'COMAP_DS_SELL', 'COMAP_DS_SU',
-        'COMAP_DS_PXCD', 'COMAP_DS_BXCD', 'COMAP_DS_NT', 'COMAP_DS_SPRE', 'COMAP_DS_PPAIR', 'COMAP_DS_BPAIR')
+        'COMAP_DS_PXCD', 'COMAP_DS_BXCD', 'COMAP_DS_NT', 'COMAP_DS_SPRE', 'COMAP_DS_PPAIR', 'COMAP_DS_BPAIR', 'COMAP_DS_TILES')
 
 
 def main():
@@ -41,7 +35,7 @@ def main():
             for k in KEYS:
                 os.environ.pop(k, None)
             os.environ.update(st)
-            prob = D.DeviceDestriper(pix, tod, w, 50, 480 * 480, device=0)
+            prob = D.DeviceDestriper(pix, tod, w, 50, 480 * 480, device=0, map_shape=(480, 480))
             prob.solve(threshold=0.0, niter=3)
             best = None
             for _ in range(2):

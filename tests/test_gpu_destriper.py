@@ -390,7 +390,8 @@ def test_graph_driver_captures_rccl_allreduce():
 @pytest.mark.parametrize('form,nb', [('count', 1), ('count', 4), ('count', 2), ('full', 1), ('full', 4),
                                      ('nonuniform', 1), ('nonuniform', 4), ('sell-count', 1), ('sell-count', 4),
                                      ('sell-count', 2), ('sell-full', 1), ('sell-full', 4), ('pair-count', 4),
-                                     ('pair-full', 4)])
+                                     ('pair-full', 4), ('tile-count', 1), ('tile-count', 2), ('tile-count', 4),
+                                     ('tile-full', 1), ('tile-full', 4)])
 def test_entry_forms_vs_oracle(form, nb, monkeypatch):
     """The operator's two entry forms against the oracle: the count form (uint8
     non-zero-sample counts per band, s_e = wbar_o c_e; chosen when every offset's
@@ -399,11 +400,14 @@ def test_entry_forms_vs_oracle(form, nb, monkeypatch):
     an offset (the set-up falls back to the f64 form by itself).  Same solve to 1e-9,
     weight / hits bit-exact, the same iteration counts.  sell-*: the projection on the
     sliced-ELLPACK copy of the offset rows (COMAP_DS_SELL=1), both entry forms; pair-*:
-    4 bands with the lane-pair projection and bin."""
+    4 bands with the lane-pair projection and bin; tile-*: the map-tile projection."""
     import oracle.destriper as od
     from comapreduce_amd.mapmaking.destriper import DeviceDestriper
     if form.startswith('sell-'):
         monkeypatch.setenv('COMAP_DS_SELL', '1')
+        form = form[5:]
+    if form.startswith('tile-'):         # map-tile projection (the golden map is 60 x 60)
+        monkeypatch.setenv('COMAP_DS_TILES', '1')
         form = form[5:]
     if form.startswith('pair-'):         # 4 bands: lane-pair SELL projection and bin
         for k in ('COMAP_DS_SELL', 'COMAP_DS_PPAIR', 'COMAP_DS_BPAIR'):
@@ -416,9 +420,11 @@ def test_entry_forms_vs_oracle(form, nb, monkeypatch):
     if form == 'nonuniform':
         ws = ws * np.random.default_rng(5).uniform(0.5, 2.0, ws.shape)
     want_bytes = 4 + nb if form == 'count' else 4 + 8 * nb
+    tiles = os.environ.get('COMAP_DS_TILES') == '1'
     if nb == 1:
-        dd = DeviceDestriper(p, tods[0], ws[0], L, NPIX)
+        dd = DeviceDestriper(p, tods[0], ws[0], L, NPIX, map_shape=(60, 60))
         assert dd.entry_bytes() == want_bytes
+        assert (dd.tile_segments() > 0) == tiles
         res = dd.solve(1e-6, 100)
         ref, xr, itr = od.destriper_iteration(p, tods[0], ws[0], L, NPIX, threshold=1e-6, niter=100)
         assert res['iters'] == itr
@@ -427,8 +433,9 @@ def test_entry_forms_vs_oracle(form, nb, monkeypatch):
         assert np.array_equal(m['weight'], ref['weight']) and np.array_equal(m['hits'], ref['hits'])
         assert rel(m['map'], ref['map']) < 1e-9
         return
-    dd = DeviceDestriper(p, tods, ws, L, NPIX, keep=keep)
+    dd = DeviceDestriper(p, tods, ws, L, NPIX, keep=keep, map_shape=(60, 60))
     assert dd.entry_bytes() == want_bytes
+    assert (dd.tile_segments() > 0) == tiles
     res = dd.solve(1e-6, 100)
     for b in range(nb):
         sel = np.repeat(keep[b], L)
