@@ -2421,7 +2421,7 @@ extern "C" int comap_destripe_tiles(comap_destriper *d, int64_t nx)
     COMAP_DEVICE_GUARD(d->ctx);
     comap_ctx *ctx = d->ctx;
     if (nx <= 0) return comap_fail(ctx, -1, "comap_destripe_tiles: nx must be positive");
-    if (d->tiles) return 0;
+    if (d->tiles || d->nnz == 0) return 0;
     if (!d->cf && !d->ow) return comap_fail(ctx, -1, "comap_destripe_tiles: no offset-major weights");
     hipStream_t st = ctx->stream;
     const int nb = d->nb;
