@@ -1577,62 +1577,108 @@ __global__ void k_seg_slots(const int32_t *__restrict__ offk, const int32_t *__r
     }
 }
 
-// The tile pass: one workgroup = one tile's m staged in LDS + up to 4 of its chunks (one
-// per wave, lane = (offset, tile) segment); each lane's in-order fma chain over its
-// segment's entries from LDS; partial sums to tpart[slot].
+// The tile pass: one workgroup = one tile's m staged in LDS + up to kTileChunks of its
+// chunks (one per wave, lane = (offset, tile) segment); each lane's in-order fma chain over
+// its segment's entries from LDS (entry loads issued one group ahead); partial sums to
+// tpart[slot].
+constexpr int kTileChunks = 16;      // waves (chunks) per workgroup: 1024 threads share one staged tile
 template <int NB, bool CF, int U>
-__global__ void __launch_bounds__(256) k_ds_project_tile(const int32_t *__restrict__ twg,
-                                                         const int32_t *__restrict__ tcend,
-                                                         const int64_t *__restrict__ tcbase,
-                                                         const uint64_t *__restrict__ tent,
-                                                         const double *__restrict__ tentw,
-                                                         const int32_t *__restrict__ tslot, TileGeom g,
-                                                         const double *__restrict__ num, const double *__restrict__ h,
-                                                         double *__restrict__ tpart, const int32_t *__restrict__ flags)
+__global__ void __launch_bounds__(1024) k_ds_project_tile(const int32_t *__restrict__ twg,
+                                                          const int32_t *__restrict__ tcend,
+                                                          const int64_t *__restrict__ tcbase,
+                                                          const uint64_t *__restrict__ tent,
+                                                          const double *__restrict__ tentw,
+                                                          const int32_t *__restrict__ tslot, TileGeom g,
+                                                          const double *__restrict__ num, const double *__restrict__ h,
+                                                          double *__restrict__ tpart, const int32_t *__restrict__ flags)
 {
     constexpr int kTilePix = 4096 / NB;
     __shared__ double m[kTilePix * NB];
     if (cg_done(flags)) return;
     const int32_t t = twg[2 * blockIdx.x], c0 = twg[2 * blockIdx.x + 1];
     const int64_t ty = t / g.ntx, tx = t - ty * g.ntx;
-    // stage the tile: row r of the tile = tw pixels, NB doubles each, contiguous in the map
-    for (int i = threadIdx.x; i < g.tw * g.th * NB; i += blockDim.x) {
-        const int local = i / NB, b = i - local * NB;
-        const int64_t py = ty * g.th + local / g.tw, px = tx * g.tw + local % g.tw;
-        const int64_t p = py * g.nx + px;
-        double v = 0.0;
-        if (px < g.nx && p < g.npix) v = h ? map_value(num, h, p * NB + b) : num[p * NB + b];
-        m[i] = v;
+    const int lane = threadIdx.x & 63;
+    const int64_t c = (int64_t)c0 + (threadIdx.x >> 6);
+    const bool active = c < tcend[t];
+    // this wave's first group of entries, in flight while the tile is staged
+    const int64_t b0 = active ? tcbase[c] : 0, W = active ? (tcbase[c + 1] - b0) >> 6 : 0;
+    uint64_t v[U];
+    double wv[U][NB];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const bool in = u < W;
+        v[u] = in ? tent[b0 + 64 * u + lane] : ~0ull;
+        if constexpr (!CF) {
+            if (in) ldb<NB>(tentw + (b0 + 64 * u + lane) * NB, wv[u]);
+        }
+    }
+    // stage the tile: 4096 doubles, 2 per thread-load (16 B), all loads before the stores
+    {
+        constexpr int kPer = 4096 / 2 / 1024;          // d2v loads per thread
+        d2v st[kPer];
+#pragma unroll
+        for (int r = 0; r < kPer; ++r) {
+            const int i = 2 * (threadIdx.x + 1024 * r);   // even: a band pair of one pixel (NB even) or 2 pixels (NB 1)
+            const int local = i / NB, b = i - local * NB;
+            const int64_t py = ty * g.th + local / g.tw, px = tx * g.tw + local % g.tw;
+            const int64_t p = py * g.nx + px;
+            d2v val;
+            val.x = 0.0;
+            val.y = 0.0;
+            if constexpr (NB == 1) {
+                const int64_t px2 = px + 1, p2 = p + 1;           // the next pixel of the same tile row
+                if (px < g.nx && p < g.npix) val.x = h ? map_value(num, h, p) : num[p];
+                if (px2 < g.nx && p2 < g.npix && (local + 1) % g.tw != 0) val.y = h ? map_value(num, h, p2) : num[p2];
+            } else {
+                if (px < g.nx && p < g.npix) {
+                    if (h) {
+                        val.x = map_value(num, h, p * NB + b);
+                        val.y = map_value(num, h, p * NB + b + 1);
+                    } else {
+                        val = *reinterpret_cast<const d2v *>(num + p * NB + b);
+                    }
+                }
+            }
+            st[r] = val;
+        }
+#pragma unroll
+        for (int r = 0; r < kPer; ++r) *reinterpret_cast<d2v *>(m + 2 * (threadIdx.x + 1024 * r)) = st[r];
     }
     __syncthreads();
-    const int64_t c = (int64_t)c0 + (threadIdx.x >> 6);
-    if (c >= tcend[t]) return;
-    const int lane = threadIdx.x & 63;
-    const int64_t b0 = tcbase[c], W = (tcbase[c + 1] - b0) >> 6;
+    if (!active) return;
     double acc[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) acc[b] = 0.0;
     for (int64_t j = 0; j < W; j += U) {
-        uint64_t v[U];
-        double wv[U][NB];
+        uint64_t vn[U];
+        double wn[U][NB];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const bool in = j + u < W;
-            v[u] = in ? tent[b0 + 64 * (j + u) + lane] : ~0ull;
+            const bool in = j + U + u < W;
+            vn[u] = in ? tent[b0 + 64 * (j + U + u) + lane] : ~0ull;
             if constexpr (!CF) {
-                if (in) ldb<NB>(tentw + (b0 + 64 * (j + u) + lane) * NB, wv[u]);
+                if (in) ldb<NB>(tentw + (b0 + 64 * (j + U + u) + lane) * NB, wn[u]);
             }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if ((uint32_t)(v[u] >> 32) != 0xffffffffu) {
                 const int l = (int)(v[u] >> 32);
-                const double *mm = m + l * NB;
+                double mm[NB];
+                ldb<NB>(m + l * NB, mm);
 #pragma unroll
                 for (int b = 0; b < NB; ++b) {
                     const double a = CF ? (double)((uint32_t)(v[u] >> (8 * b)) & 0xffu) : wv[u][b];
                     acc[b] = fma(a, mm[b], acc[b]);
                 }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            v[u] = vn[u];
+            if constexpr (!CF) {
+#pragma unroll
+                for (int b = 0; b < NB; ++b) wv[u][b] = wn[u][b];
             }
         }
     }
@@ -2027,8 +2073,8 @@ unsigned launch_project_u(const comap_destriper *d, hipStream_t st, const double
 {
     if (d->tiles) {
         const TileGeom g{d->nx, d->npix, d->ntx, d->tile_w, d->tile_h};
-        k_ds_project_tile<NB, CF, 8><<<(unsigned)d->nwg_t, 256, 0, st>>>(d->twg, d->tcend, d->tcbase, d->tent, d->tentw,
-                                                                     d->tslot, g, num, h, d->tpart, flags);
+        k_ds_project_tile<NB, CF, 8><<<(unsigned)d->nwg_t, 1024, 0, st>>>(d->twg, d->tcend, d->tcbase, d->tent,
+                                                                      d->tentw, d->tslot, g, num, h, d->tpart, flags);
         const unsigned cg = (unsigned)std::max<int64_t>(
             1, std::min<int64_t>((d->NO + 255) / 256, std::min<int64_t>(pstride, d->proj_blocks)));
         k_ds_tile_combine<NB, CF><<<cg, 256, 0, st>>>(d->pstart, d->tpart, d->wbar, d->ws, d->tw, x, d->NO, y, part,
@@ -2509,7 +2555,7 @@ extern "C" int comap_destripe_tiles(comap_destriper *d, int64_t nx)
             ch_seg0.push_back(k);
         }
         tcend[t] = (int32_t)ch_tile.size();
-        for (int32_t c = cfirst; c < tcend[t]; c += 4) {
+        for (int32_t c = cfirst; c < tcend[t]; c += kTileChunks) {
             wg.push_back((int32_t)t);
             wg.push_back(c);
         }
