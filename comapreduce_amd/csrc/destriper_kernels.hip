@@ -1517,45 +1517,47 @@ __global__ void k_tile_chunk_width(const int32_t *__restrict__ chunk_tile, const
     if (lane == 0) cw[c] = 64 * len;
 }
 
-// chunk slots: lane = segment, entry j of the segment at tcbase[c] + 64 j + lane; the
-// lane's partial slot
+// chunk slots: lane = segment, entry j of the segment at tcbase[c] + 64 j + lane.  One
+// thread per tile-sorted entry (coalesced reads); the padding slots keep the memset's
+// all-ones pattern.
 template <int NB, bool CF>
-__global__ void k_tile_fill(const int32_t *__restrict__ chunk_tile, const int32_t *__restrict__ chunk_seg0,
-                            const int32_t *__restrict__ tfirst, const int32_t *__restrict__ seg_first,
-                            const int32_t *__restrict__ seg_slot, const int32_t *__restrict__ sval,
-                            const int32_t *__restrict__ opix, const void *__restrict__ oco, TileGeom g, int64_t nseg,
-                            int64_t nent, int64_t nchunk, const int64_t *__restrict__ tcbase, uint64_t *__restrict__ tent,
-                            double *__restrict__ tentw, int32_t *__restrict__ tslot)
+__global__ void k_tile_fill(const int32_t *__restrict__ sid, const int32_t *__restrict__ seg_tile,
+                            const int32_t *__restrict__ seg_first, const int32_t *__restrict__ tfirst,
+                            const int32_t *__restrict__ tcfirst, const int32_t *__restrict__ sval,
+                            const int32_t *__restrict__ opix, const void *__restrict__ oco, TileGeom g, int64_t nent,
+                            const int64_t *__restrict__ tcbase, uint64_t *__restrict__ tent, double *__restrict__ tentw)
+{
+    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < nent; s += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t k = sid[s] - 1;                         // segment
+        const int32_t t = seg_tile[k];
+        const int32_t kr = k - tfirst[t];
+        const int64_t c = (int64_t)tcfirst[t] + kr / 64;
+        const int64_t slot = tcbase[c] + 64 * (int64_t)(s - seg_first[k]) + (kr & 63);
+        const int32_t e = sval[s];
+        int32_t tt, l;
+        g.of(opix[e], tt, l);
+        uint32_t pk = 0;
+        if constexpr (CF) {
+            const uint8_t *cc = reinterpret_cast<const uint8_t *>(oco) + (int64_t)e * NB;
+#pragma unroll
+            for (int b = 0; b < NB; ++b) pk |= (uint32_t)cc[b] << (8 * b);
+        } else {
+#pragma unroll
+            for (int b = 0; b < NB; ++b) tentw[slot * NB + b] = reinterpret_cast<const double *>(oco)[(int64_t)e * NB + b];
+        }
+        tent[slot] = ((uint64_t)(uint32_t)l << 32) | pk;
+    }
+}
+
+// the partial slot of every chunk lane (-1: a lane past its tile's segments)
+__global__ void k_tile_slots(const int32_t *__restrict__ chunk_tile, const int32_t *__restrict__ chunk_seg0,
+                             const int32_t *__restrict__ tfirst, const int32_t *__restrict__ seg_slot, int64_t nchunk,
+                             int32_t *__restrict__ tslot)
 {
     const int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int lane = threadIdx.x & 63;
     if (c >= nchunk) return;
-    const int64_t k = (int64_t)chunk_seg0[c] + lane;
-    const bool real = k < tfirst[chunk_tile[c] + 1];
-    const int64_t s0 = real ? seg_first[k] : 0;
-    const int64_t len = real ? (k + 1 < nseg ? seg_first[k + 1] : nent) - s0 : 0;
-    tslot[c * 64 + lane] = real ? seg_slot[k] : -1;
-    const int64_t b0 = tcbase[c], W = (tcbase[c + 1] - b0) >> 6;
-    for (int64_t j = 0; j < W; ++j) {
-        const int64_t slot = b0 + 64 * j + lane;
-        uint64_t v = ~0ull;
-        if (j < len) {
-            const int32_t e = sval[s0 + j];
-            int32_t t, l;
-            g.of(opix[e], t, l);
-            uint32_t pk = 0;
-            if constexpr (CF) {
-                const uint8_t *cc = reinterpret_cast<const uint8_t *>(oco) + (int64_t)e * NB;
-#pragma unroll
-                for (int b = 0; b < NB; ++b) pk |= (uint32_t)cc[b] << (8 * b);
-            } else {
-#pragma unroll
-                for (int b = 0; b < NB; ++b) tentw[slot * NB + b] = reinterpret_cast<const double *>(oco)[(int64_t)e * NB + b];
-            }
-            v = ((uint64_t)(uint32_t)l << 32) | pk;
-        }
-        tent[slot] = v;
-    }
+    const int64_t k = (int64_t)chunk_seg0[c] + (threadIdx.x & 63);
+    tslot[c * 64 + (threadIdx.x & 63)] = k < tfirst[chunk_tile[c] + 1] ? seg_slot[k] : -1;
 }
 
 __global__ void k_iota(int32_t *__restrict__ v, int64_t n)
@@ -2546,10 +2548,11 @@ extern "C" int comap_destripe_tiles(comap_destriper *d, int64_t nx)
     COMAP_CHECK(ctx, hipMemcpyAsync(tf.data(), tfirst, 4 * tf.size(), hipMemcpyDeviceToHost, st));
     COMAP_CHECK(ctx, hipStreamSynchronize(st));
     // chunks (64 segments of one tile) and workgroups (4 chunks of one tile) on the host
-    std::vector<int32_t> ch_tile, ch_seg0, wg, tcend((size_t)ntiles);
+    std::vector<int32_t> ch_tile, ch_seg0, wg, tcend((size_t)ntiles), tcf((size_t)ntiles);
     for (int64_t t = 0; t < ntiles; ++t) {
         const int32_t k0 = tf[t], k1 = tf[t + 1];
         const int32_t cfirst = (int32_t)ch_tile.size();
+        tcf[t] = cfirst;
         for (int32_t k = k0; k < k1; k += 64) {
             ch_tile.push_back((int32_t)t);
             ch_seg0.push_back(k);
@@ -2561,8 +2564,10 @@ extern "C" int comap_destripe_tiles(comap_destriper *d, int64_t nx)
         }
     }
     const int64_t nchunk = (int64_t)ch_tile.size();
-    int32_t *dch_tile = nullptr, *dch_seg0 = nullptr;
+    int32_t *dch_tile = nullptr, *dch_seg0 = nullptr, *dtcf = nullptr;
     int64_t *cw = nullptr;
+    COMAP_CHECK(ctx, tmp.alloc(&dtcf, (size_t)ntiles));
+    COMAP_CHECK(ctx, comap_upload(dtcf, tcf.data(), 4 * tcf.size(), st));
     COMAP_CHECK(ctx, tmp.alloc(&dch_tile, (size_t)nchunk + 1));
     COMAP_CHECK(ctx, tmp.alloc(&dch_seg0, (size_t)nchunk + 1));
     COMAP_CHECK(ctx, tmp.alloc(&cw, (size_t)nchunk + 1));
@@ -2590,16 +2595,16 @@ extern "C" int comap_destripe_tiles(comap_destriper *d, int64_t nx)
     if (!d->cf && dalloc(ctx, &d->tentw, std::max<int64_t>(nslots, 1) * nb)) return -2;
     if (nchunk) {
         const unsigned gch = (unsigned)((nchunk * 64 + 255) / 256);
+        k_tile_slots<<<gch, 256, 0, st>>>(dch_tile, dch_seg0, tfirst, seg_slot, nchunk, d->tslot);
+        COMAP_CHECK(ctx, hipMemsetAsync(d->tent, 0xff, 8 * (size_t)nslots, st));     // padding
         if (d->cf) {
-            COMAP_NB_SWITCH(nb, (k_tile_fill<NB, true><<<gch, 256, 0, st>>>(dch_tile, dch_seg0, tfirst, seg_first,
-                                                                           seg_slot, sval, d->opix, d->ocnt, g, nseg,
-                                                                           nnz, nchunk, d->tcbase, d->tent, d->tentw,
-                                                                           d->tslot)));
+            COMAP_NB_SWITCH(nb, (k_tile_fill<NB, true><<<grid_for(nnz, 16384), 256, 0, st>>>(
+                                    sid, seg_tile, seg_first, tfirst, dtcf, sval, d->opix, d->ocnt, g, nnz, d->tcbase,
+                                    d->tent, d->tentw)));
         } else {
-            COMAP_NB_SWITCH(nb, (k_tile_fill<NB, false><<<gch, 256, 0, st>>>(dch_tile, dch_seg0, tfirst, seg_first,
-                                                                            seg_slot, sval, d->opix, d->ow, g, nseg,
-                                                                            nnz, nchunk, d->tcbase, d->tent,
-                                                                            d->tentw, d->tslot)));
+            COMAP_NB_SWITCH(nb, (k_tile_fill<NB, false><<<grid_for(nnz, 16384), 256, 0, st>>>(
+                                    sid, seg_tile, seg_first, tfirst, dtcf, sval, d->opix, d->ow, g, nnz, d->tcbase,
+                                    d->tent, d->tentw)));
         }
         COMAP_LAUNCH_CHECK(ctx);
     }
