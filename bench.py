@@ -547,10 +547,10 @@ def chain_fn(data, device):
 def chain_pipeline_fn(data, device):
     """The north_star chain for a stream of observations, software-pipelined on one GPU:
     observation k's map-making (read_comap_data_bands -> batched destriper solve to 1e-6
-    -> maps to the host) runs on its own stream while observation k + 1's Level-1 pass A
-    (56 GB of streaming) runs on the default stream -- the map-making's short,
-    latency-bound kernels and host round trips then hide under the streaming pass instead
-    of following the reduction.  Each observation's work and results are those of
+    -> maps to the host) runs on its own high-priority stream while observation k + 1's
+    Level-1 passes B and C (110 GB of streaming) run on the default stream -- the
+    map-making's short, latency-bound kernels and host round trips then hide under the
+    streaming passes instead of following the reduction.  Each observation's work and results are those of
     chain_fn (the same calls, the same kernels); the observations are the same resident
     cube, reduced again each time (as bench.py's steps are).
 
@@ -565,8 +565,11 @@ def chain_pipeline_fn(data, device):
     dev = torch.device('cuda', device)
     obsid = int(data.obsid) if data.obsid > 0 else 1
     pointing = pointing_device(data, dev)
-    smap = torch.cuda.Stream(dev)        # map-making of the previous observation
-    side = torch.cuda.Stream(dev)        # its az / el percentiles
+    # map-making of the previous observation (high priority: its short kernels get CUs
+    # ahead of the streaming passes' next workgroups), and its az / el percentiles
+    prio = int(os.environ.get('COMAP_PIPE_PRIO', '-1'))
+    smap = torch.cuda.Stream(dev, priority=prio)
+    side = torch.cuda.Stream(dev, priority=prio)
 
     def l1_stage(cls, level2):
         st = cls(level2=level2, device=device, device_outputs=True)
@@ -595,21 +598,20 @@ def chain_pipeline_fn(data, device):
         for k in range(n + 1):
             cur = None
             if k < n:
+                # observation k's Level-1 reduction: pass A, the host-side fits, then passes
+                # B / C queued (comap_l1_average returns without waiting for them)
                 cur = COMAPLevel2(filename='/nonexistent/level2.hd5')
-                l1_stage(A.MeasureSystemTemperature, cur)       # queues observation k's pass A
+                for cls in (A.MeasureSystemTemperature, A.AtmosphereRemoval, A.Level1AveragingGainCorrection):
+                    l1_stage(cls, cur)
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(dev))
             if prev is not None:
+                # the previous observation's maps while this one's passes B / C stream
                 m, it = maps_of(*prev)
                 maps.append(m)
                 iters.append(it)
                 t_done.append(time.perf_counter())
-            if cur is not None:
-                l1_stage(A.AtmosphereRemoval, cur)
-                l1_stage(A.Level1AveragingGainCorrection, cur)
-                ev = torch.cuda.Event()
-                ev.record(torch.cuda.current_stream(dev))
-                prev = (cur, ev)
-            else:
-                prev = None
+            prev = (cur, ev) if cur is not None else None
         return maps, iters, t_done
     return run
 
