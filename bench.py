@@ -66,7 +66,6 @@ def parse():
     ap.add_argument('--check', action='store_true', help='compare one unit against the CPU oracle')
     ap.add_argument('--no-e2e', action='store_true', help='skip the host-cube -> host-Level-2 leg')
     ap.add_argument('--no-chain', action='store_true', help='skip the L1 -> L2 -> maps chain leg')
-    ap.add_argument('--no-pipeline', action='store_true', help='skip the pipelined multi-observation chain')
     ap.add_argument('--shard-of', type=int, default=0,
                     help='measurement aid: reduce only rank 0\'s C3 shard of an N-way split, in this one process')
     return ap.parse_args()
@@ -544,103 +543,6 @@ def chain_fn(data, device):
     return chain
 
 
-def chain_pipeline_fn(data, device):
-    """The north_star chain for a stream of observations, software-pipelined on one GPU:
-    observation k's map-making (read_comap_data_bands -> batched destriper solve to 1e-6
-    -> maps to the host) runs on its own high-priority stream while observation k + 1's
-    Level-1 passes B and C (110 GB of streaming) run on the default stream -- the
-    map-making's short, latency-bound kernels and host round trips then hide under the
-    streaming passes instead of following the reduction.  Each observation's work and results are those of
-    chain_fn (the same calls, the same kernels); the observations are the same resident
-    cube, reduced again each time (as bench.py's steps are).
-
-    Returns ``run(n) -> (maps list, iters list, t_done list)``: t_done[k] = host clock when
-    observation k's maps were on the host."""
-    import torch
-    from comapreduce_amd import Analysis as A
-    from comapreduce_amd.mapmaking import comapdata as CD
-    from comapreduce_amd.mapmaking import destriper as D
-    from comapreduce_amd.mapmaking import prep as P
-    from comapreduce_amd.pipeline.datahandling import COMAPLevel2
-    dev = torch.device('cuda', device)
-    obsid = int(data.obsid) if data.obsid > 0 else 1
-    pointing = pointing_device(data, dev)
-    # map-making of the previous observation (high priority: its short kernels get CUs
-    # ahead of the streaming passes' next workgroups), and its az / el percentiles
-    prio = int(os.environ.get('COMAP_PIPE_PRIO', '-1'))
-    smap = torch.cuda.Stream(dev, priority=prio)
-    side = torch.cuda.Stream(dev, priority=prio)
-
-    def l1_stage(cls, level2):
-        st = cls(level2=level2, device=device, device_outputs=True)
-        if not st(data, level2):
-            raise RuntimeError(f'{cls.__name__} stopped the file')
-        level2.update(st)
-
-    def maps_of(level2, l1_done):
-        smap.wait_event(l1_done)         # this observation's Level-2 only, not the next pass A
-        with torch.cuda.stream(smap):
-            store = level2_store_device(level2, data, obsid, dev, pointing)
-            side.wait_event(l1_done)
-            with torch.cuda.stream(side):
-                pp = P.precompute_pointing([CD.Level2File(*store[k], k) for k in store], list(store),
-                                           [i + 1 for i in range(19)], device)
-            r = CD.read_comap_data_bands(list(store), c4_map_info(), bands=(0, 1, 2, 3), offset_length=50,
-                                         store=store, device=device, device_outputs=True, pointing=pp)
-            prob = D.DeviceDestriper(r['pointing'].to(torch.int32), r['tod'], r['weights'], 50, 480 * 480,
-                                     device=device, keep=r['keep'])
-            res = prob.solve(threshold=1e-6, niter=100, to_host=True)     # synchronises smap
-        return res['maps'], res['iters']
-
-    def run(n):
-        maps, iters, t_done = [], [], []
-        prev = None
-        for k in range(n + 1):
-            cur = None
-            if k < n:
-                # observation k's Level-1 reduction: pass A, the host-side fits, then passes
-                # B / C queued (comap_l1_average returns without waiting for them)
-                cur = COMAPLevel2(filename='/nonexistent/level2.hd5')
-                for cls in (A.MeasureSystemTemperature, A.AtmosphereRemoval, A.Level1AveragingGainCorrection):
-                    l1_stage(cls, cur)
-                ev = torch.cuda.Event()
-                ev.record(torch.cuda.current_stream(dev))
-            if prev is not None:
-                # the previous observation's maps while this one's passes B / C stream
-                m, it = maps_of(*prev)
-                maps.append(m)
-                iters.append(it)
-                t_done.append(time.perf_counter())
-            prev = (cur, ev) if cur is not None else None
-        return maps, iters, t_done
-    return run
-
-
-def chain_pipeline_leg(data, device, l1_bytes, op_bytes, n_obs=6):
-    """Steady-state period of chain_pipeline_fn: the median interval between consecutive
-    observations' maps arriving on the host (after the first), with the roofline of the
-    chain's algorithmic bytes per observation over that period."""
-    import torch
-    run = chain_pipeline_fn(data, device)
-    run(2)                                          # warm
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    maps, iters, t_done = run(n_obs)
-    torch.cuda.synchronize()
-    wall = (time.perf_counter() - t0) * 1e3
-    for m in maps:
-        assert np.isfinite(m['map']).all(), 'pipelined chain maps not finite'
-    d = np.diff(np.asarray(t_done)) * 1e3
-    period = float(np.median(d))
-    algo = l1_bytes + op_bytes * max(iters[-1])
-    return {'config': f'north_star chain pipelined over {n_obs} observations (the same resident C2 cube reduced '
-                      'again each time): observation k\'s read_comap_data_bands + batched destriper (threshold 1e-6) '
-                      '+ maps to host on a second stream while observation k+1\'s Level-1 reduction streams',
-            'n_obs': n_obs, 'wall_ms': wall, 'period_ms': period, 'periods_ms': d.tolist(),
-            'iters': iters[-1], 'algo_bytes_per_obs': algo, 'achieved_GBs': algo / (period * 1e-3) / 1e9,
-            'roofline_frac': algo / (period * 1e-3) / 1e9 / HBM_PEAK_GBS}
-
-
 def e2e_leg(F, T, device):
     """C2 from host memory, the Runner path (Running.py:120-153): the Level-1 cube is
     a pageable host NumPy array (as read from a file), the stages upload it
@@ -757,9 +659,6 @@ def main():
         scan_sc0 = sh.samples_x_channels()
         l1_bytes = sum(ALGO_BYTES_PER_SAMPCH_PASS * scan_sc0 * frac[k] for k in type_streaming())
         chain = chain_leg(data, device, l1_bytes)
-        if not args.no_pipeline:
-            chain['pipelined'] = chain_pipeline_leg(data, device, l1_bytes,
-                                                    (chain['algo_bytes'] - l1_bytes) / max(max(chain['iters']), 1))
 
     c5 = None
     if not args.no_destriper and args.c5_obs > 0:

@@ -263,22 +263,6 @@ def test_chain_as_timed_vs_oracle(c2):
         assert rel(got['map'][b], ref['map']) < 1e-5, b
 
 
-def test_chain_pipelined_equals_serial(c2):
-    """The pipelined multi-observation chain (bench.chain_pipeline_fn: observation k's
-    map-making on a second stream while observation k + 1's Level-1 reduction streams)
-    delivers, for every observation, the serial chain's maps bit for bit and the same
-    iteration counts (the serial chain is pinned to the oracle above)."""
-    import bench
-    data, _, _ = c2
-    ref = bench.chain_fn(data, 0)(False)
-    maps, iters, t_done = bench.chain_pipeline_fn(data, 0)(3)
-    assert len(maps) == 3 and len(t_done) == 3
-    for m, it in zip(maps, iters):
-        assert it == ref['iters']
-        for k in ('map', 'naive', 'weight', 'hits'):
-            assert np.array_equal(m[k], ref['maps'][k]), k
-
-
 def test_c5_two_observations_two_bands_vs_oracle():
     """Reduced C5: 2 observations x 19 feeds x 180,000 samples (6.8 M samples, 137k
     offsets, 480x480 CAR), 2 sidebands batched, 12 CG iterations, against the oracle
