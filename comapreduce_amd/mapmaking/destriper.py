@@ -334,6 +334,10 @@ class DeviceOps:
         return int(N.lib().comap_destripe_tile_segments(self.h))
 
     # ---- vector helpers
+    def empty(self, n):
+        """[n] float64 on the device, uninitialised (for outputs a call writes in full)."""
+        return self.torch.empty(n, dtype=self.torch.float64, device=self.dev)
+
     def zeros(self, n):
         return self.torch.zeros(n, dtype=self.torch.float64, device=self.dev)
 
@@ -446,8 +450,8 @@ class DeviceOps:
     def solve_native(self, threshold, niter):
         """x [N/L * nb], iterations per band (list), maps {k: [npix * nb]} (interleaved)."""
         nb = self.nb
-        x = self.zeros(self.n_offsets * nb)
-        maps = {k: self.zeros(self.npix * nb) for k in ('map', 'naive', 'weight', 'hits')}
+        x = self.empty(self.n_offsets * nb)                  # the solve writes x and every map in full
+        maps = {k: self.empty(self.npix * nb) for k in ('map', 'naive', 'weight', 'hits')}
         it = (ctypes.c_int32 * nb)()
         self._c('comap_destripe_solve', self.h, float(threshold), int(niter), N.dptr(x), N.dptr(maps['map']),
                 N.dptr(maps['naive']), N.dptr(maps['weight']), N.dptr(maps['hits']),
@@ -464,7 +468,7 @@ class DeviceOps:
         nb, npix, nbo = self.nb, self.npix, self.n_bands
         cur = torch.cuda.current_stream(self.dev)
         m = torch.empty((4, npix * nb), dtype=torch.float64, device=self.dev)    # map, naive, weight, hits
-        nn = self.zeros(npix * nb)
+        nn = self.empty(npix * nb)                                              # local_maps copies it in full
         self._c('comap_destripe_local_maps', self.h, N.dptr(m[2]), N.dptr(m[3]), N.dptr(nn))
         self._c('comap_destripe_div_map', self.h, N.dptr(nn), None, N.dptr(m[1]))
         bands = m.view(4, npix, nb).permute(0, 2, 1)[:, :nbo]                    # [4, n_bands, npix] view
@@ -480,7 +484,7 @@ class DeviceOps:
         with torch.cuda.stream(cs):
             host[1:].copy_(static, non_blocking=True)
         static.record_stream(cs)
-        x = self.zeros(self.n_offsets * nb)
+        x = self.empty(self.n_offsets * nb)                                     # written in full by the solve
         it = (ctypes.c_int32 * nb)()
         self._c('comap_destripe_solve', self.h, float(threshold), int(niter), N.dptr(x), N.dptr(m[0]), None, None,
                 None, ctypes.cast(it, ctypes.POINTER(ctypes.c_int32)))

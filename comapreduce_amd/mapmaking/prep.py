@@ -79,14 +79,22 @@ class FlatArrays:
     """read_comap_data's flat vectors on the device: tod / weights [nb, n], the rest [n]."""
 
     def __init__(self, torch, dev, nb, n):
+        # uninitialised: the gather kernel writes every sample of every file's rows (zeros for
+        # skipped feeds) and the cut writes every kept sample; zero_range covers the rest
         f64 = dict(dtype=torch.float64, device=dev)
-        self.tod = torch.zeros((nb, n), **f64)
-        self.w = torch.zeros((nb, n), **f64)
-        self.az, self.el, self.ra, self.dec = (torch.zeros(n, **f64) for _ in range(4))
-        self.feedid = torch.zeros(n, dtype=torch.int64, device=dev)
-        self.obsid = torch.zeros(n, dtype=torch.int64, device=dev)
-        self.pix = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.tod = torch.empty((nb, n), **f64)
+        self.w = torch.empty((nb, n), **f64)
+        self.az, self.el, self.ra, self.dec = (torch.empty(n, **f64) for _ in range(4))
+        self.feedid = torch.empty(n, dtype=torch.int64, device=dev)
+        self.obsid = torch.empty(n, dtype=torch.int64, device=dev)
+        self.pix = torch.empty(n, dtype=torch.int32, device=dev)
         self.n = n
+
+    def zero_range(self, a, b):
+        for t in (self.tod, self.w):
+            t[:, a:b] = 0
+        for t in (self.az, self.el, self.ra, self.dec, self.feedid, self.obsid, self.pix):
+            t[a:b] = 0
 
     def struct(self, offset=0):
         d = N.dptr
@@ -190,6 +198,7 @@ def prep_flat(files, filelist, map_info, bands, use_gain_filter, offset_length, 
         if len(edges) == 0 or nrow == 0 or ds == 0:
             # get_tod returns zeros; read_pixels leaves its zero rows (COMAPData.py:294-296)
             if nrow * ds:
+                out.zero_range(last, last + nrow * ds)
                 out.obsid[last:last + nrow * ds] = obsid
             last += nrow * ds
             continue
