@@ -94,6 +94,7 @@ struct comap_destriper {
     // map-tile projection (comap_destripe_tiles): the offset rows split by map tile; a
     // workgroup stages one tile of m in LDS and sums every (offset, tile) segment from
     // there, a combine pass adds each offset's segments in tile order
+    bool walk = false;                 // sample-level maps by the member-mask walk (set-up)
     bool tiles = false;
     int64_t nx = 0, ntx = 0, nty = 0;
     int tile_w = 0, tile_h = 0;        // tile width / height in pixels
@@ -284,6 +285,61 @@ __device__ __forceinline__ double wave_sum(double v)
     return v;
 }
 
+// Wave sums of V values per lane (V a power of two <= 64) by a reduce-scatter butterfly:
+// the first log2 V steps exchange half of the remaining values (each lane keeps the half
+// its lane bit selects), the rest reduce the single value left, so V sums cost V - 1 + 6 -
+// log2 V exchanges instead of 6 V.  Afterwards x[0] holds value lane / (64 / V)'s total (a
+// fixed order; a + b == b + a, so both lanes of a pair hold the same bits).
+template <int V>
+__device__ __forceinline__ void wave_sum_scatter(double (&x)[V], int lane)
+{
+    // (values held in named registers and selected as values: a select between two array
+    // elements was turned into a lane-dependent index, i.e. v_cndmask chains over all V)
+    static_assert(V == 2 || V == 4 || V == 8, "V");
+    double y[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) y[j] = x[j];
+    int h = V / 2, sft = 32;
+    if constexpr (V >= 8) {
+        const bool up = (lane & sft) != 0;
+        const double s0 = up ? y[0] : y[4], s1 = up ? y[1] : y[5], s2 = up ? y[2] : y[6], s3 = up ? y[3] : y[7];
+        const double k0 = up ? y[4] : y[0], k1 = up ? y[5] : y[1], k2 = up ? y[6] : y[2], k3 = up ? y[7] : y[3];
+        y[0] = k0 + __shfl_xor(s0, sft, 64);
+        y[1] = k1 + __shfl_xor(s1, sft, 64);
+        y[2] = k2 + __shfl_xor(s2, sft, 64);
+        y[3] = k3 + __shfl_xor(s3, sft, 64);
+        h >>= 1;
+        sft >>= 1;
+    }
+    if constexpr (V >= 4) {
+        const bool up = (lane & sft) != 0;
+        const double s0 = up ? y[0] : y[2], s1 = up ? y[1] : y[3];
+        const double k0 = up ? y[2] : y[0], k1 = up ? y[3] : y[1];
+        y[0] = k0 + __shfl_xor(s0, sft, 64);
+        y[1] = k1 + __shfl_xor(s1, sft, 64);
+        h >>= 1;
+        sft >>= 1;
+    }
+    {
+        const bool up = (lane & sft) != 0;
+        const double s0 = up ? y[0] : y[1], k0 = up ? y[1] : y[0];
+        y[0] = k0 + __shfl_xor(s0, sft, 64);
+        sft >>= 1;
+    }
+    (void)h;
+#pragma unroll
+    for (int o = 32 / V; o > 0; o >>= 1) y[0] += __shfl_xor(y[0], o, 64);
+    x[0] = y[0];
+}
+
+// v of lane `src` (wave-uniform) by two v_readlane
+__device__ __forceinline__ double read_lane(double v, int src)
+{
+    const uint64_t u = __double_as_longlong(v);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, src), hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), src);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
 // Fixed-order sum of n block partials by one 256-thread block (k_dot_final's order).
 // Each thread adds part[tid], part[tid + 256], ... in that order; the loads are issued
 // 8 at a time before the adds (a serial load -> add chain costs one L2 round trip per
@@ -400,6 +456,21 @@ __global__ void k_offset_keys(const int32_t *__restrict__ pix, int64_t NO, int L
     }
 }
 
+// Member-mask walk: one record per kept entry -- internal / caller's offset, packed
+// per-band counts, member mask (sample j of the offset = bit j), the offset's weight per
+// band (count form: every non-zero weight) -- written by the count pass in slot order
+// (offset k's entries at k L ...) and gathered by the sample walk (16-B aligned: vector
+// loads and stores)
+template <int K, int NB>
+struct alignas(16) WalkEnt {
+    uint32_t k, o, cnt, pad;
+    uint64_t mask[K];
+    double wb[NB];
+};
+static_assert(sizeof(WalkEnt<1, 4>) == 64 && sizeof(WalkEnt<1, 2>) == 48 && sizeof(WalkEnt<1, 1>) == 32 &&
+                  sizeof(WalkEnt<4, 4>) == 80,
+              "WalkEnt size = 16-B rounded words (create_bands' rec_words)");
+
 // Offset rows of the sparse operator, one wave per row k (offset o = perm[k]): lane l
 // holds samples l, l + 64, ... (K per lane, L <= 64 K).  The distinct pixels of the
 // offset are found in first-occurrence order by a leader loop (the first pending
@@ -430,39 +501,53 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
                                                  const int64_t *__restrict__ orow, int32_t *__restrict__ opix,
                                                  double *__restrict__ ow, uint8_t *__restrict__ ocnt,
                                                  int32_t *__restrict__ ekey, int32_t *__restrict__ eval,
-                                                 int32_t *__restrict__ eoff, uint64_t *__restrict__ epay)
+                                                 int32_t *__restrict__ eoff, uint64_t *__restrict__ epay,
+                                                 WalkEnt<K, NB> *__restrict__ rec, uint32_t *__restrict__ hextra,
+                                                 const uint8_t *__restrict__ keep, int32_t *__restrict__ nonfin)
 {
 #pragma clang fp contract(off)
     const int lane = threadIdx.x & 63;
-    const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (k >= NO) return;
-    const int64_t o = perm ? (int64_t)perm[k] : k;
-    const int64_t base = o * L;
     constexpr int32_t kNone = INT32_MIN;    // lanes past the offset's end (real pixels are >= -1)
-    int32_t q[K];
-    unsigned long long rem[K];
-    // the offset's weights, staged in LDS by coalesced loads: the group sums below read
-    // their members from here instead of one dependent global load per member (the count
-    // pass took 3.2 ms at C5 with 4 bands, 80 % of its wave cycles waiting)
+    // the offset's weights, staged in LDS: the group sums below read their members from
+    // here instead of one dependent global load per member (the count pass took 3.2 ms at
+    // C5 with 4 bands, 80 % of its wave cycles waiting)
     __shared__ double wsh[4][K * 64 * NB];
     double *wl = wsh[threadIdx.x >> 6];
-#pragma unroll
-    for (int m = 0; m < K; ++m) {
-        const int j = lane + 64 * m;
-        q[m] = j < L ? pix[base + j] : kNone;
-        rem[m] = __ballot(j < L);
-#pragma unroll
-        for (int b = 0; b < NB; ++b) wl[(64 * m + lane) * NB + b] = j < L ? w[(int64_t)b * N + base + j] : 0.0;
-    }
-    // count pass: the offset's tod loads go out with the pixels and weights, so their
-    // latency hides under the leader loop instead of following it
-    double ti[K][NB];
-    if constexpr (!FILL) {
+    // waves walk offsets k, k + nw, ... (grid-stride; the launch covers every offset
+    // once by default -- a persistent grid that loaded the next offset during the current
+    // one's leader loop took 100+ VGPRs, half the occupancy, and was no faster, r04z)
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    int32_t qn[K];
+    double wn[K][NB], tn[K][NB];
+    auto fetch = [&](int64_t kk) {
+        const int64_t bs = (perm ? (int64_t)perm[kk] : kk) * L;
 #pragma unroll
         for (int m = 0; m < K; ++m) {
             const int j = lane + 64 * m;
+            qn[m] = j < L ? pix[bs + j] : kNone;
 #pragma unroll
-            for (int b = 0; b < NB; ++b) ti[m][b] = j < L ? tod[(int64_t)b * N + base + j] : 0.0;
+            for (int b = 0; b < NB; ++b) {
+                wn[m][b] = j < L ? w[(int64_t)b * N + bs + j] : 0.0;
+                if constexpr (!FILL) tn[m][b] = j < L ? tod[(int64_t)b * N + bs + j] : 0.0;
+            }
+        }
+    };
+    for (; k < NO; k += nw) {
+    fetch(k);
+    const int64_t o = perm ? (int64_t)perm[k] : k;
+    const int64_t base = o * L;
+    int32_t q[K];
+    unsigned long long rem[K];
+    double ti[K][NB];
+#pragma unroll
+    for (int m = 0; m < K; ++m) {
+        q[m] = qn[m];
+        rem[m] = __ballot(lane + 64 * m < L);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            wl[(64 * m + lane) * NB + b] = wn[m][b];
+            if constexpr (!FILL) ti[m][b] = tn[m][b];
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // the staged weights, before other lanes read them
@@ -495,8 +580,41 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
             }
         }
     }
+    // count pass: the count-form test first -- per band, every non-zero weight finite and
+    // equal to the first one (ballot + readlane) -- with the non-zero masks
+    double wi[K][NB], refb[NB];
+    unsigned long long nzm[NB][K];
+    bool uni = true;
+    if constexpr (!FILL) {
+#pragma unroll
+        for (int m = 0; m < K; ++m)
+#pragma unroll
+            for (int b = 0; b < NB; ++b) wi[m][b] = wl[(64 * m + lane) * NB + b];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            double ref = 0.0;
+            bool found = false, bad = false;
+#pragma unroll
+            for (int m = 0; m < K; ++m) {
+                nzm[b][m] = __ballot(wi[m][b] != 0.0);
+                if (!found && nzm[b][m]) {
+                    found = true;
+                    ref = read_lane(wi[m][b], __ffsll((long long)nzm[b][m]) - 1);
+                }
+            }
+#pragma unroll
+            for (int m = 0; m < K; ++m) {
+                const double v = wi[m][b];
+                bad |= v != 0.0 && (!isfinite(v) || v != ref);
+            }
+            refb[b] = ref;
+            uni &= __ballot(bad) == 0ull;
+        }
+    }
     // per head: the group's in-order weight sums per band (and, for the count form, its
-    // number of non-zero-weight samples)
+    // number of non-zero-weight samples).  A uniform offset in the count pass needs only
+    // the counts (its group sums are count x weight: non-zero iff the count is), which are
+    // popcounts of member mask & non-zero mask -- no per-member loop
     double gs[K][NB];
     int gc[K][NB];
     bool keepe[K];
@@ -506,6 +624,19 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
         for (int b = 0; b < NB; ++b) {
             gs[m][b] = 0.0;
             gc[m][b] = 0;
+        }
+        if (!FILL && uni) {
+            bool any = false;
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                int n = 0;
+#pragma unroll
+                for (int c = 0; c < K; ++c) n += __popcll(mem[m][c] & nzm[b][c]);
+                gc[m][b] = n;
+                any |= n != 0;
+            }
+            keepe[m] = head[m] && any;
+            continue;
         }
         if (head[m]) {
             // members in sample order, all bands per member (one NB-wide LDS read each);
@@ -533,53 +664,69 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
         int64_t c0 = 0;
 #pragma unroll
         for (int m = 0; m < K; ++m) c0 += __popcll(__ballot(keepe[m]));
-        double wi[K][NB];
+        bool nf = false;
 #pragma unroll
         for (int m = 0; m < K; ++m) {
             const int j = lane + 64 * m;
-#pragma unroll
-            for (int b = 0; b < NB; ++b) wi[m][b] = wl[(64 * m + lane) * NB + b];
             if (j < L) {
                 const int64_t i = base + j;
-                double pl[2 * NB];
+                if (payload && rec) {
+                    // member-mask walk: (tod w) per band, sample-major (NB doubles a sample)
+                    double pt[NB];
 #pragma unroll
-                for (int b = 0; b < NB; ++b) { pl[b] = wi[m][b]; pl[NB + b] = ti[m][b] * wi[m][b]; }
-                stb<2 * NB>(payload + i * 2 * NB, pl);
-                skey[i] = (q[m] >= 0 && q[m] < npix) ? q[m] : (int32_t)npix;
-                sval[i] = (int32_t)i;
+                    for (int b = 0; b < NB; ++b) pt[b] = ti[m][b] * wi[m][b];
+                    stb<NB>(payload + i * NB, pt);
+                } else if (payload) {
+                    double pl[2 * NB];
+#pragma unroll
+                    for (int b = 0; b < NB; ++b) { pl[b] = wi[m][b]; pl[NB + b] = ti[m][b] * wi[m][b]; }
+                    stb<2 * NB>(payload + i * 2 * NB, pl);
+                    skey[i] = (q[m] >= 0 && q[m] < npix) ? q[m] : (int32_t)npix;
+                    sval[i] = (int32_t)i;
+                }
+#pragma unroll
+                for (int b = 0; b < NB; ++b) nf |= !isfinite(ti[m][b]);
             }
         }
+        // member-mask walk (no payload): hits of the groups that hold no entry (every weight
+        // zero) by integer adds -- order-free, exact -- and a flag for non-finite tod, which
+        // such groups would carry into the naive numerator (the set-up then takes the
+        // payload walk, which reproduces that)
+        if (rec) {
+            if (nonfin && __ballot(nf) && lane == 0) nonfin[0] = 1;
+#pragma unroll
+            for (int m = 0; m < K; ++m)
+                if (head[m] && !keepe[m] && q[m] >= 0 && q[m] < npix) {
+                    uint32_t cnt_m = 0;
+#pragma unroll
+                    for (int c = 0; c < K; ++c) cnt_m += (uint32_t)__popcll(mem[m][c]);
+#pragma unroll
+                    for (int b = 0; b < NB; ++b)
+                        if (!keep || keep[(int64_t)b * NO + o]) atomicAdd(hextra + (int64_t)q[m] * NB + b, cnt_m);
+                }
+        }
+        // per band: the offset's sums (lane order, then wave_sum_scatter's fixed butterfly) and
+        // the count-form test's result (ballot + readlane above instead of two more 6-step
+        // reductions per band: most of the count pass's LDS-pipe time was 4 x 4 bpermute
+        // butterflies, r04w)
+        if (!uni && lane == 0) nonuni[0] = 1;
+        double red[2 * NB];
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
             double sw = 0.0, st = 0.0;
-            // count-form test: the offset's non-zero weights in band b are one finite value
-            double mn = INFINITY, mx = -INFINITY;
-            bool bad = false;
 #pragma unroll
             for (int m = 0; m < K; ++m) {
                 sw += wi[m][b];
                 if (lane + 64 * m < L) st = fma(wi[m][b], ti[m][b], st);   // fused, as before the rewrite
-                const double v = wi[m][b];
-                if (v != 0.0) {
-                    bad |= !isfinite(v);
-                    mn = fmin(mn, v);
-                    mx = fmax(mx, v);
-                }
             }
-            sw = wave_sum(sw);
-            st = wave_sum(st);
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                mn = fmin(mn, __shfl_xor(mn, o, 64));
-                mx = fmax(mx, __shfl_xor(mx, o, 64));
-            }
-            bad = __ballot(bad) != 0ull;
-            if (lane == 0) {
-                ws[k * NB + b] = sw;
-                tw[k * NB + b] = st;
-                wbar[k * NB + b] = mx == -INFINITY ? 0.0 : mx;
-                if (bad || (mx != -INFINITY && mn != mx)) nonuni[0] = 1;
-            }
+            red[2 * b] = sw;
+            red[2 * b + 1] = st;
+            if (lane == 0) wbar[k * NB + b] = refb[b];
+        }
+        wave_sum_scatter<2 * NB>(red, lane);
+        if ((lane & (64 / (2 * NB) - 1)) == 0) {
+            const int idx = lane / (64 / (2 * NB));           // value held: band idx / 2, sum idx % 2
+            (idx & 1 ? tw : ws)[k * NB + (idx >> 1)] = red[0];
         }
         if (lane == 0) cnt[k] = c0;
         if (eval) {
@@ -594,6 +741,18 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
                     for (int b = 0; b < NB; ++b) pk |= (uint32_t)(gc[m][b] & 255) << (8 * b);
                     eval[si] = q[m];
                     eoff[si] = (int32_t)pk;
+                    if (rec) {
+                        WalkEnt<K, NB> en;
+                        en.k = (uint32_t)k;
+                        en.o = (uint32_t)o;
+                        en.cnt = pk;
+                        en.pad = 0;
+#pragma unroll
+                        for (int c = 0; c < K; ++c) en.mask[c] = mem[m][c];
+#pragma unroll
+                        for (int b = 0; b < NB; ++b) en.wb[b] = refb[b];
+                        rec[si] = en;
+                    }
                 }
                 r0 += __popcll(bm);
             }
@@ -616,6 +775,7 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
             e += __popcll(bm);
         }
     }
+    }   // offsets of this wave
 }
 
 // Count-form fill: row k's kept entries, left by the count pass in slots
@@ -655,12 +815,21 @@ template <int NB, bool FILL, bool CF>
 void launch_rows(int L, hipStream_t st, const int32_t *pix, const double *w, const double *tod, int64_t N,
                  int64_t NO, int64_t npix, const int32_t *perm, int64_t *cnt, double *ws, double *tw, double *payload,
                  int32_t *skey, int32_t *sval, double *wbar, int32_t *nonuni, const int64_t *orow, int32_t *opix,
-                 double *ow, uint8_t *ocnt, int32_t *ekey, int32_t *eval, int32_t *eoff, uint64_t *epay = nullptr)
+                 double *ow, uint8_t *ocnt, int32_t *ekey, int32_t *eval, int32_t *eoff, uint64_t *epay = nullptr,
+                 void *rec = nullptr, uint32_t *hextra = nullptr, const uint8_t *keep = nullptr,
+                 int32_t *nonfin = nullptr)
 {
-    const unsigned blocks = (unsigned)((NO + 3) / 4);
+    // k_ds_rows' grid: COMAP_DS_RB blocks at most (default: one offset per wave)
+    static const int64_t cap = [] {
+        const char *v = getenv("COMAP_DS_RB");
+        const int64_t x = v ? atoll(v) : 0;
+        return x >= 256 && x <= (1 << 20) ? x : (int64_t)(1 << 20);
+    }();
+    const unsigned blocks = (unsigned)std::min<int64_t>((NO + 3) / 4, cap);
 #define COMAP_ROWS(K) k_ds_rows<K, NB, FILL, CF><<<blocks, 256, 0, st>>>(pix, w, tod, N, NO, L, npix, perm, cnt, ws, \
                                                                           tw, payload, skey, sval, wbar, nonuni, orow, \
-                                                                          opix, ow, ocnt, ekey, eval, eoff, epay)
+                                                                          opix, ow, ocnt, ekey, eval, eoff, epay, \
+                                                                          (WalkEnt<K, NB> *)rec, hextra, keep, nonfin)
     if (L <= 64) COMAP_ROWS(1);
     else if (L <= 128) COMAP_ROWS(2);
     else COMAP_ROWS(4);
@@ -694,6 +863,51 @@ __global__ void k_rowptr(const int32_t *__restrict__ skey, int64_t n, int64_t np
 {
     for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p <= npix; p += (int64_t)gridDim.x * blockDim.x)
         row[p] = lb32(skey, n, p);
+}
+
+// cnt_nat[perm[k]] = cnt[k]: the offsets' kept-entry counts in the caller's offset order
+__global__ void k_cnt_natural(const int64_t *__restrict__ cnt, const int32_t *__restrict__ perm, int64_t NO,
+                              int64_t *__restrict__ cnt_nat)
+{
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k <= NO; k += (int64_t)gridDim.x * blockDim.x)
+        cnt_nat[k < NO ? (perm ? (int64_t)perm[k] : k) : NO] = k < NO ? cnt[k] : 0;
+}
+
+// Count-form fill for the member-mask walk: row k's kept entries from the count pass's slots
+// into the CSR rows (pixel, packed counts), and the transpose's sort pairs (pixel key, slot
+// k L + r: the entry's walk record) in the caller's offset order (orow_nat), so the stable
+// sort by pixel leaves each pixel's entries in sample order -- the order binValues adds
+// them in.  16 lanes per row (rows hold ~30 entries; a wave per row waited on its loads:
+// 0.6 ms at C5).
+template <int NB>
+__global__ void __launch_bounds__(256) k_ds_compact_walk(const int64_t *__restrict__ orow,
+                                                         const int64_t *__restrict__ orow_nat,
+                                                         const int32_t *__restrict__ perm, int64_t NO, int L,
+                                                         int64_t npix, const int32_t *__restrict__ spx,
+                                                         const int32_t *__restrict__ spk,
+                                                         int32_t *__restrict__ opix, uint8_t *__restrict__ ocnt,
+                                                         int32_t *__restrict__ ekey, int32_t *__restrict__ eval)
+{
+    const int sub = threadIdx.x & 15;
+    const int64_t k = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+    if (k >= NO) return;
+    const int64_t o = perm ? (int64_t)perm[k] : k;
+    const int64_t e0 = orow[k], c = orow[k + 1] - e0, n0 = orow_nat[o];
+    for (int64_t r = sub; r < c; r += 16) {
+        const int32_t q = spx[k * L + r];
+        const uint32_t pk = (uint32_t)spk[k * L + r];
+        const int64_t ei = e0 + r;
+        opix[ei] = q;
+        if constexpr (NB == 4) {
+            *reinterpret_cast<uint32_t *>(ocnt + ei * 4) = pk;
+        } else if constexpr (NB == 2) {
+            *reinterpret_cast<uint16_t *>(ocnt + ei * 2) = (uint16_t)pk;
+        } else {
+            ocnt[ei] = (uint8_t)pk;
+        }
+        ekey[n0 + r] = (q >= 0 && q < npix) ? q : (int32_t)npix;
+        eval[n0 + r] = (int32_t)(k * L + r);
+    }
 }
 
 // pixel-major entries: sorted position k < nnzp (= prow[npix], read on the device) takes
@@ -829,6 +1043,165 @@ __global__ void __launch_bounds__(256) k_sample_walk(const int64_t *__restrict__
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // read before the next chunk overwrites
         }
         if (lane < 3 * NB) (kind == 0 ? h : kind == 1 ? nnum : hits)[p * NB + b] = acc;
+    }
+}
+
+// position of the r-th (0-based) set bit of x (r < popcount(x)): six halving steps
+__device__ __forceinline__ int select_bit(uint64_t x, int r)
+{
+    int pos = 0;
+#pragma unroll
+    for (int sh = 32; sh > 0; sh >>= 1) {
+        const int c = __popcll(x & ((1ull << sh) - 1ull));
+        if (r >= c) { r -= c; x >>= sh; pos += sh; }
+    }
+    return pos;
+}
+
+// Sample-level maps from the pixel-major entries (member-mask walk): one wave per pixel.
+// Per chunk the wave takes the row's next entries (caller's offset order) whose members
+// fit 64 M slots, one entry per lane (one packed-record gather each, which also writes the
+// entry's pixel-major offset / counts for the CG bin); then every lane fills member slots
+// t = lane + 64 u: the owning entry from the chunk's start-position mask, the member's
+// sample from the entry's mask (sample order: an entry's members ascending, entries by
+// offset), and its (w, tod w) per band into LDS.  tod w comes from the count pass's
+// sample-major copy (ptw, one 8 NB-byte read); w is the offset's weight wb when all the
+// group's members have a non-zero weight in the band (count form: they all equal wb), 0
+// when none has, and only a mixed group reads w itself.  Then 3 NB lanes run the ordered
+// sums exactly as k_sample_walk does over the sorted samples.  Samples of groups without
+// an entry carry zero weights (they add nothing to h or to the naive numerator); their
+// hits come from the count pass's integer adds.
+template <int NB, int K, int M>
+__global__ void __launch_bounds__(256) k_sample_walk2(const int64_t *__restrict__ prow,
+                                                      const int32_t *__restrict__ sval,
+                                                      const WalkEnt<K, NB> *__restrict__ ent,
+                                                      const double *__restrict__ w, const double *__restrict__ ptw,
+                                                      int64_t N, int64_t npix, int L, int64_t NO,
+                                                      const uint8_t *__restrict__ keep,
+                                                      const uint32_t *__restrict__ hextra, double *__restrict__ h,
+                                                      double *__restrict__ hits, double *__restrict__ nnum,
+                                                      int32_t *__restrict__ poff, uint8_t *__restrict__ pcnt,
+                                                      bool xcd)
+{
+#pragma clang fp contract(off)
+    constexpr int CAP = 64 * M;
+    __shared__ double spl[4][CAP * 2 * NB];
+    __shared__ uint32_t smk[4][CAP];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    double *pl = spl[wv];
+    uint32_t *mk = smk[wv];
+    const int kind = lane / NB, b = lane % NB;     // this lane's ordered sum (lanes < 3 NB)
+    const int col = kind == 2 ? 0 : kind * NB + b;
+    // xcd: each XCD walks one contiguous eighth of the pixels
+    const int64_t lb = xcd_block(blockIdx.x, gridDim.x, xcd);
+    for (int64_t p = lb * 4 + wv; p < npix; p += (int64_t)gridDim.x * 4) {
+        const int64_t lo = prow[p], hi = prow[p + 1];
+        double acc = 0.0;
+        for (int64_t c = lo; c < hi;) {
+            const int64_t e = c + lane;
+            WalkEnt<K, NB> en;
+            uint32_t cnt = 0;
+            if (e < hi) {
+                en = ent[sval[e]];
+#pragma unroll
+                for (int q = 0; q < K; ++q) cnt += (uint32_t)__popcll(en.mask[q]);
+            } else {
+                en.k = en.o = en.cnt = 0;
+#pragma unroll
+                for (int q = 0; q < K; ++q) en.mask[q] = 0ull;
+#pragma unroll
+                for (int q = 0; q < NB; ++q) en.wb[q] = 0.0;
+            }
+            // inclusive prefix of the member counts over the wave
+            uint32_t inc = cnt;
+#pragma unroll
+            for (int sft = 1; sft < 64; sft <<= 1) {
+                const uint32_t v = __shfl_up(inc, sft, 64);
+                if (lane >= sft) inc += v;
+            }
+            const bool take = e < hi && inc <= (uint32_t)CAP;
+            const int ntake = __popcll(__ballot(take));     // >= 1: one entry holds <= L <= CAP members
+            const int total = (int)__shfl(inc, ntake - 1, 64);
+            const uint32_t excl = inc - cnt;
+            uint32_t kb = 0;
+            if (take) {
+                poff[e] = (int32_t)en.k;
+                if constexpr (NB == 4) *reinterpret_cast<uint32_t *>(pcnt + e * 4) = en.cnt;
+                else if constexpr (NB == 2) *reinterpret_cast<uint16_t *>(pcnt + e * 2) = (uint16_t)en.cnt;
+                else pcnt[e] = (uint8_t)en.cnt;
+#pragma unroll
+                for (int bb = 0; bb < NB; ++bb) kb |= (uint32_t)(!keep || keep[(int64_t)bb * NO + en.o]) << bb;
+            }
+            // the chunk's entry start positions (taken entries hold >= 1 member each)
+            uint64_t sm[M];
+#pragma unroll
+            for (int u = 0; u < M; ++u) {
+                uint64_t bit = (take && (int)(excl >> 6) == u) ? (1ull << (excl & 63)) : 0ull;
+#pragma unroll
+                for (int sft = 32; sft > 0; sft >>= 1) bit |= (uint64_t)__shfl_xor((long long)bit, sft, 64);
+                sm[u] = bit;
+            }
+#pragma unroll
+            for (int u = 0; u < M; ++u) {
+                const int t = lane + 64 * u;
+                // owning entry: start positions at or before t, minus one
+                int j = 0;
+#pragma unroll
+                for (int v = 0; v < M; ++v) {
+                    const uint64_t lm = v < u ? ~0ull : (v == u ? (lane == 63 ? ~0ull : ((2ull << lane) - 1ull)) : 0ull);
+                    j += __popcll(sm[v] & lm);
+                }
+                j = t < total ? j - 1 : 0;
+                const uint32_t exj = (uint32_t)__shfl((int)excl, j, 64);
+                const uint32_t nmj = (uint32_t)__shfl((int)cnt, j, 64);
+                const uint32_t oj = (uint32_t)__shfl((int)en.o, j, 64);
+                const uint32_t kbj = (uint32_t)__shfl((int)kb, j, 64);
+                const uint32_t gcj = (uint32_t)__shfl((int)en.cnt, j, 64);
+                uint64_t mj[K];
+#pragma unroll
+                for (int q = 0; q < K; ++q) mj[q] = (uint64_t)__shfl((long long)en.mask[q], j, 64);
+                double wbj[NB];
+#pragma unroll
+                for (int q = 0; q < NB; ++q) wbj[q] = __shfl(en.wb[q], j, 64);
+                if (t < total) {
+                    int r = t - (int)exj, bitpos = 0;
+#pragma unroll
+                    for (int q = 0; q < K; ++q) {
+                        const int cq = __popcll(mj[q]);
+                        if (r >= 0 && r < cq) bitpos = 64 * q + select_bit(mj[q], r);
+                        r -= cq;
+                    }
+                    const int64_t i = (int64_t)oj * L + bitpos;
+                    double pv[NB];
+                    ldb<NB>(ptw + i * NB, pv);
+#pragma unroll
+                    for (int bb = 0; bb < NB; ++bb) {
+                        const uint32_t gc = (gcj >> (8 * bb)) & 255u;
+                        pl[t * 2 * NB + bb] = gc == nmj ? wbj[bb] : (gc == 0 ? 0.0 : w[(int64_t)bb * N + i]);
+                        pl[t * 2 * NB + NB + bb] = pv[bb];
+                    }
+                    mk[t] = kbj;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // the chunk, before other lanes read it
+            if (lane < 3 * NB) {
+                if (kind == 2) {
+                    for (int t = 0; t < total; ++t) acc = ((mk[t] >> b) & 1u) ? acc + 1.0 : acc;
+                } else {
+#pragma unroll 8
+                    for (int t = 0; t < total; ++t) {
+                        const double v = pl[t * 2 * NB + col];
+                        acc = ((mk[t] >> b) & 1u) ? acc + v : acc;
+                    }
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // read before the next chunk overwrites
+            c += ntake;
+        }
+        if (lane < 3 * NB) {
+            if (kind == 2) acc += (double)hextra[p * NB + b];
+            (kind == 0 ? h : kind == 1 ? nnum : hits)[p * NB + b] = acc;
+        }
     }
 }
 
@@ -2247,11 +2620,16 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tb, (int64_t *)nullptr, (int64_t *)nullptr, (int)(NO + 1), st);
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan32_tb, (int32_t *)nullptr, (int32_t *)nullptr, (int)npix, st);
     const size_t cub_tb = std::max({sort_tb, sort64_tb, scan_tb, scan32_tb});
+    const int KW = L <= 64 ? 1 : (L <= 128 ? 2 : 4);     // member-mask words per entry (k_ds_rows' K)
+    const int64_t rec_words = (2 + KW + NB + 1) / 2 * 2;   // sizeof(WalkEnt<KW, NB>) / 8 (16-B aligned)
     Arena ar;
     ar.cap = Arena::bytes<char>(cub_tb) + Arena::bytes<int64_t>(NO + 1) + 8 * Arena::bytes<int32_t>(N) +
              Arena::bytes<double>((size_t)N * 2 * NB) + Arena::bytes<int64_t>(npix + 1) +
              2 * Arena::bytes<int32_t>(npix) + Arena::bytes<int64_t>(2) + Arena::bytes<int32_t>(N) +
-             Arena::bytes<int32_t>(1) + 2 * Arena::bytes<uint64_t>(N) + Arena::bytes<int64_t>(NO / 32 + 2);
+             Arena::bytes<int32_t>(1) + 2 * Arena::bytes<uint64_t>(N) + Arena::bytes<int64_t>(NO / 32 + 2) +
+             Arena::bytes<uint64_t>((size_t)N * rec_words) +
+             Arena::bytes<uint32_t>((size_t)npix * NB) +
+             2 * Arena::bytes<int64_t>(NO + 1) + Arena::bytes<int32_t>(1);
     COMAP_CHECK(ctx, comap_tmp_alloc((void **)&ar.base, ar.cap, st));
     struct ArenaFree {
         Arena *a;
@@ -2277,6 +2655,17 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     uint64_t *epay = ar.take<uint64_t>(N), *epay2 = ar.take<uint64_t>(N);   // count form: offset << 32 | counts
     const int64_t NC = (NO + 31) / 32;                      // sliced-ELLPACK chunks (at most, CW >= 32)
     int64_t *swid = ar.take<int64_t>(NC + 1);
+    // member-mask walk (count form): slot / entry member masks, integer hits of the groups
+    // without an entry, the transpose's rows in the caller's offset order
+    void *went = ar.take<uint64_t>((size_t)N * rec_words);      // WalkEnt<KW, NB> per slot
+    uint32_t *hextra = ar.take<uint32_t>((size_t)npix * NB);
+    int64_t *cnt_nat = ar.take<int64_t>(NO + 1), *orow_nat = ar.take<int64_t>(NO + 1);
+    int32_t *nonfin = ar.take<int32_t>(1);
+    bool walk = true;
+    {
+        const char *we = getenv("COMAP_DS_WALK");        // 0: the sorted-sample payload walk
+        walk = !(we && we[0] == '0');
+    }
     // ---- 1. spatial processing order of the offsets
     if (spatial) {
         k_offset_keys<<<grid_for(NO), 256, 0, st>>>(pix, NO, L, npix, ekey, eval);
@@ -2287,13 +2676,28 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     // ---- 2. count pass (+ the count-form test: non-zero weights uniform per offset and band)
     COMAP_CHECK(ctx, hipMemsetAsync(nonuni, 0, 4, st));
     // (eval / eoff: the count-form fill's entry slots, unused by the f64 path until its
-    // own fill pass overwrites them)
-    COMAP_NB_SWITCH(nb, (launch_rows<NB, false, false>(L, st, pix, w, tod, N, NO, npix, d->perm, cnt, d->ws, d->tw,
-                                                       payload, skey, sval, d->wbar, nonuni, nullptr, nullptr, nullptr,
-                                                       nullptr, nullptr, eval, eoff)));
+    // own fill pass overwrites them).  Member-mask walk: no per-sample payload or sample
+    // sort keys, but the slots' member masks, the empty groups' hits and the tod check
+    auto count_pass = [&](bool with_payload) {
+        COMAP_NB_SWITCH(nb, (launch_rows<NB, false, false>(
+                                L, st, pix, w, tod, N, NO, npix, d->perm, cnt, d->ws, d->tw,
+                                payload, skey, sval, d->wbar, nonuni, nullptr, nullptr,
+                                nullptr, nullptr, nullptr, eval, eoff, nullptr, with_payload ? nullptr : went,
+                                with_payload ? nullptr : hextra, keep, with_payload ? nullptr : nonfin)));
+    };
+    if (walk) {
+        COMAP_CHECK(ctx, hipMemsetAsync(hextra, 0, 4 * (size_t)npix * NB, st));
+        COMAP_CHECK(ctx, hipMemsetAsync(nonfin, 0, 4, st));
+    }
+    count_pass(!walk);
     COMAP_LAUNCH_CHECK(ctx);
     COMAP_CHECK(ctx, hipMemsetAsync(cnt + NO, 0, 8, st));
     COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(cub_tmp, scan_tb, cnt, d->orow, (int)(NO + 1), st));
+    if (walk) {
+        k_cnt_natural<<<grid_for(NO + 1, 8192), 256, 0, st>>>(cnt, d->perm, NO, cnt_nat);
+        COMAP_LAUNCH_CHECK(ctx);
+        COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(cub_tmp, scan_tb, cnt_nat, orow_nat, (int)(NO + 1), st));
+    }
     {
         // sliced-ELLPACK projection: default for large problems (C5, 547k offsets: 1 band
         // 0.112 -> 0.098 ms per CG iteration, 4 bands 0.261 -> 0.236, r04j); a C4-size problem
@@ -2314,9 +2718,10 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(cub_tmp, scan_tb, swid, d->sbase, (int)(NCs + 1), st));
         COMAP_CHECK(ctx, hipMemcpyAsync(&d->nsell, d->sbase + NCs, 8, hipMemcpyDeviceToHost, st));
     }
-    int32_t nonuni_h = 0;
+    int32_t nonuni_h = 0, nonfin_h = 0;
     COMAP_CHECK(ctx, hipMemcpyAsync(&d->nnz, d->orow + NO, 8, hipMemcpyDeviceToHost, st));
     COMAP_CHECK(ctx, hipMemcpyAsync(&nonuni_h, nonuni, 4, hipMemcpyDeviceToHost, st));
+    if (walk) COMAP_CHECK(ctx, hipMemcpyAsync(&nonfin_h, nonfin, 4, hipMemcpyDeviceToHost, st));
     COMAP_CHECK(ctx, hipStreamSynchronize(st));
     {
         const char *cfe = getenv("COMAP_DS_CF");             // 0: always the f64 entry weights
@@ -2346,6 +2751,13 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         d->sell_pre = env_int("COMAP_DS_SPRE", 0, {0, 1}) == 1;
         d->bin_pairs = env_int("COMAP_DS_BPAIR", 0, {0, 1}) == 1;
     }
+    // the member-mask walk needs the count form and finite tod everywhere; otherwise the
+    // count pass runs again with the per-sample payload for the sorted-sample walk
+    if (walk && (!d->cf || nonfin_h)) {
+        walk = false;
+        count_pass(true);
+        COMAP_LAUNCH_CHECK(ctx);
+    }
     rc |= dalloc(ctx, &d->opix, d->nnz);
     rc |= dalloc(ctx, &d->poff, d->nnz);          // nnzp <= nnz (off-map entries are not binned)
     if (d->cf) {
@@ -2357,7 +2769,11 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     }
     if (rc) return -2;
     // ---- 3. fill pass
-    if (d->cf) {
+    int32_t *evn = skey2, *evn2 = sval2;   // walk: the sample-sort arrays are free
+    if (walk) {
+        COMAP_NB_SWITCH(nb, (k_ds_compact_walk<NB><<<(unsigned)((NO + 15) / 16), 256, 0, st>>>(
+                                d->orow, orow_nat, d->perm, NO, L, npix, eval, eoff, d->opix, d->ocnt, ekey, evn)));
+    } else if (d->cf) {
         COMAP_NB_SWITCH(nb, (k_ds_compact_cf<NB><<<(unsigned)((NO + 3) / 4), 256, 0, st>>>(
                                 d->orow, NO, L, npix, eval, eoff, d->opix, d->ocnt, ekey, epay)));
     } else {
@@ -2381,7 +2797,10 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         COMAP_LAUNCH_CHECK(ctx);
     }
     // ---- 4. pixel-major transpose (stable: offset order within a pixel)
-    if (d->cf) {
+    if (walk) {
+        COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(cub_tmp, sort_tb, ekey, ekey2, evn, evn2, (int)d->nnz, 0,
+                                                            end_bit, st));
+    } else if (d->cf) {
         COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(cub_tmp, sort64_tb, ekey, ekey2, epay, epay2, (int)d->nnz,
                                                             0, end_bit, st));
     } else {
@@ -2390,7 +2809,9 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     }
     k_rowptr<<<grid_for(npix + 1), 256, 0, st>>>(ekey2, d->nnz, npix, d->prow);
     COMAP_LAUNCH_CHECK(ctx);
-    if (d->cf) {
+    if (walk) {
+        // (the sample walk below writes the pixel-major offsets / counts)
+    } else if (d->cf) {
         COMAP_NB_SWITCH(nb, k_pixel_entries_cf<NB><<<grid_for(d->nnz, 8192), 256, 0, st>>>(epay2, d->prow + npix,
                                                                                             d->poff, d->pcnt));
     } else {
@@ -2405,14 +2826,31 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     k_hit_rows<<<grid_for(npix), 256, 0, st>>>(d->prow, hflag, hpos, npix, d->hrow, d->hprow, counts);
     COMAP_LAUNCH_CHECK(ctx);
     // ---- 5. sample-level maps (binValues order)
-    COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(cub_tmp, sort_tb, skey, skey2, sval, sval2, (int)N, 0, end_bit,
-                                                        st));
-    k_rowptr<<<grid_for(npix + 1), 256, 0, st>>>(skey2, N, npix, srow);
+    const unsigned wgrid = (unsigned)std::min<int64_t>((npix + 3) / 4, 65536);
+    if (walk) {
+        // member slots per lane and chunk (>= KW: one entry's members fit a chunk)
+        const char *wm = getenv("COMAP_DS_WALKM");
+        const int M = std::max(KW, wm && wm[0] == '2' ? 2 : 1);
+        const char *wxe = getenv("COMAP_DS_WXCD");
+        const bool wx = wxe && wxe[0] == '1';
+#define COMAP_W2(KK, MM) k_sample_walk2<NB, KK, MM><<<wgrid, 256, 0, st>>>(                                   \
+        d->prow, evn2, (const WalkEnt<KK, NB> *)went, w, payload, N, npix, L, NO, keep, hextra, d->h, d->hits, d->nnum, \
+        d->poff, d->pcnt, wx)
+        if (KW == 1 && M == 1) { COMAP_NB_SWITCH(nb, COMAP_W2(1, 1)); }
+        else if (KW == 1) { COMAP_NB_SWITCH(nb, COMAP_W2(1, 2)); }
+        else if (KW == 2) { COMAP_NB_SWITCH(nb, COMAP_W2(2, 2)); }
+        else { COMAP_NB_SWITCH(nb, COMAP_W2(4, 4)); }
+#undef COMAP_W2
+    } else {
+        COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(cub_tmp, sort_tb, skey, skey2, sval, sval2, (int)N, 0,
+                                                            end_bit, st));
+        k_rowptr<<<grid_for(npix + 1), 256, 0, st>>>(skey2, N, npix, srow);
+        COMAP_LAUNCH_CHECK(ctx);
+        COMAP_NB_SWITCH(nb, k_sample_walk<NB><<<wgrid, 256, 0, st>>>(srow, sval2, payload, npix, L, NO, keep, d->h,
+                                                                     d->hits, d->nnum));
+    }
     COMAP_LAUNCH_CHECK(ctx);
-    COMAP_NB_SWITCH(nb, k_sample_walk<NB><<<(unsigned)std::min<int64_t>((npix + 3) / 4, 65536), 256, 0, st>>>(
-                            srow, sval2, payload, npix, L, NO, keep,
-                                                                          d->h, d->hits, d->nnum));
-    COMAP_LAUNCH_CHECK(ctx);
+    d->walk = walk;
     int64_t hc[2] = {0, 0};
     COMAP_CHECK(ctx, hipMemcpyAsync(hc, counts, 16, hipMemcpyDeviceToHost, st));
     COMAP_CHECK(ctx, hipStreamSynchronize(st));
