@@ -456,21 +456,6 @@ __global__ void k_offset_keys(const int32_t *__restrict__ pix, int64_t NO, int L
     }
 }
 
-// Member-mask walk: one record per kept entry -- internal / caller's offset, packed
-// per-band counts, member mask (sample j of the offset = bit j), the offset's weight per
-// band (count form: every non-zero weight) -- written by the count pass in slot order
-// (offset k's entries at k L ...) and gathered by the sample walk (16-B aligned: vector
-// loads and stores)
-template <int K, int NB>
-struct alignas(16) WalkEnt {
-    uint32_t k, o, cnt, pad;
-    uint64_t mask[K];
-    double wb[NB];
-};
-static_assert(sizeof(WalkEnt<1, 4>) == 64 && sizeof(WalkEnt<1, 2>) == 48 && sizeof(WalkEnt<1, 1>) == 32 &&
-                  sizeof(WalkEnt<4, 4>) == 80,
-              "WalkEnt size = 16-B rounded words (create_bands' rec_words)");
-
 // Offset rows of the sparse operator, one wave per row k (offset o = perm[k]): lane l
 // holds samples l, l + 64, ... (K per lane, L <= 64 K).  The distinct pixels of the
 // offset are found in first-occurrence order by a leader loop (the first pending
@@ -502,7 +487,7 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
                                                  double *__restrict__ ow, uint8_t *__restrict__ ocnt,
                                                  int32_t *__restrict__ ekey, int32_t *__restrict__ eval,
                                                  int32_t *__restrict__ eoff, uint64_t *__restrict__ epay,
-                                                 WalkEnt<K, NB> *__restrict__ rec, uint32_t *__restrict__ hextra,
+                                                 uint64_t *__restrict__ smask, uint32_t *__restrict__ hextra,
                                                  const uint8_t *__restrict__ keep, int32_t *__restrict__ nonfin)
 {
 #pragma clang fp contract(off)
@@ -670,7 +655,7 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
             const int j = lane + 64 * m;
             if (j < L) {
                 const int64_t i = base + j;
-                if (payload && rec) {
+                if (payload && smask) {
                     // member-mask walk: (tod w) per band, sample-major (NB doubles a sample)
                     double pt[NB];
 #pragma unroll
@@ -688,11 +673,18 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
                 for (int b = 0; b < NB; ++b) nf |= !isfinite(ti[m][b]);
             }
         }
+        // flags[1]: a pixel index >= npix (the caller's error; -1 marks an unbinned sample)
+        if (nonfin) {
+            bool ob = false;
+#pragma unroll
+            for (int m = 0; m < K; ++m) ob |= q[m] != kNone && q[m] >= npix;
+            if (__ballot(ob) && lane == 0) nonfin[1] = 1;
+        }
         // member-mask walk (no payload): hits of the groups that hold no entry (every weight
         // zero) by integer adds -- order-free, exact -- and a flag for non-finite tod, which
         // such groups would carry into the naive numerator (the set-up then takes the
         // payload walk, which reproduces that)
-        if (rec) {
+        if (smask) {
             if (nonfin && __ballot(nf) && lane == 0) nonfin[0] = 1;
 #pragma unroll
             for (int m = 0; m < K; ++m)
@@ -741,17 +733,9 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
                     for (int b = 0; b < NB; ++b) pk |= (uint32_t)(gc[m][b] & 255) << (8 * b);
                     eval[si] = q[m];
                     eoff[si] = (int32_t)pk;
-                    if (rec) {
-                        WalkEnt<K, NB> en;
-                        en.k = (uint32_t)k;
-                        en.o = (uint32_t)o;
-                        en.cnt = pk;
-                        en.pad = 0;
+                    if (smask) {
 #pragma unroll
-                        for (int c = 0; c < K; ++c) en.mask[c] = mem[m][c];
-#pragma unroll
-                        for (int b = 0; b < NB; ++b) en.wb[b] = refb[b];
-                        rec[si] = en;
+                        for (int c = 0; c < K; ++c) smask[si * K + c] = mem[m][c];
                     }
                 }
                 r0 += __popcll(bm);
@@ -816,7 +800,7 @@ void launch_rows(int L, hipStream_t st, const int32_t *pix, const double *w, con
                  int64_t NO, int64_t npix, const int32_t *perm, int64_t *cnt, double *ws, double *tw, double *payload,
                  int32_t *skey, int32_t *sval, double *wbar, int32_t *nonuni, const int64_t *orow, int32_t *opix,
                  double *ow, uint8_t *ocnt, int32_t *ekey, int32_t *eval, int32_t *eoff, uint64_t *epay = nullptr,
-                 void *rec = nullptr, uint32_t *hextra = nullptr, const uint8_t *keep = nullptr,
+                 uint64_t *smask = nullptr, uint32_t *hextra = nullptr, const uint8_t *keep = nullptr,
                  int32_t *nonfin = nullptr)
 {
     // k_ds_rows' grid: COMAP_DS_RB blocks at most (default: one offset per wave)
@@ -829,7 +813,7 @@ void launch_rows(int L, hipStream_t st, const int32_t *pix, const double *w, con
 #define COMAP_ROWS(K) k_ds_rows<K, NB, FILL, CF><<<blocks, 256, 0, st>>>(pix, w, tod, N, NO, L, npix, perm, cnt, ws, \
                                                                           tw, payload, skey, sval, wbar, nonuni, orow, \
                                                                           opix, ow, ocnt, ekey, eval, eoff, epay, \
-                                                                          (WalkEnt<K, NB> *)rec, hextra, keep, nonfin)
+                                                                          smask, hextra, keep, nonfin)
     if (L <= 64) COMAP_ROWS(1);
     else if (L <= 128) COMAP_ROWS(2);
     else COMAP_ROWS(4);
@@ -1046,6 +1030,14 @@ __global__ void __launch_bounds__(256) k_sample_walk(const int64_t *__restrict__
     }
 }
 
+// one entry as the sample walk sees it
+template <int K, int NB>
+struct Ent {
+    uint32_t k, o, cnt;
+    uint64_t mask[K];
+    double wb[NB];
+};
+
 // position of the r-th (0-based) set bit of x (r < popcount(x)): six halving steps
 __device__ __forceinline__ int select_bit(uint64_t x, int r)
 {
@@ -1074,7 +1066,10 @@ __device__ __forceinline__ int select_bit(uint64_t x, int r)
 template <int NB, int K, int M>
 __global__ void __launch_bounds__(256) k_sample_walk2(const int64_t *__restrict__ prow,
                                                       const int32_t *__restrict__ sval,
-                                                      const WalkEnt<K, NB> *__restrict__ ent,
+                                                      const uint64_t *__restrict__ smask,
+                                                      const int32_t *__restrict__ spk,
+                                                      const int32_t *__restrict__ perm,
+                                                      const double *__restrict__ wbar,
                                                       const double *__restrict__ w, const double *__restrict__ ptw,
                                                       int64_t N, int64_t npix, int L, int64_t NO,
                                                       const uint8_t *__restrict__ keep,
@@ -1099,10 +1094,19 @@ __global__ void __launch_bounds__(256) k_sample_walk2(const int64_t *__restrict_
         double acc = 0.0;
         for (int64_t c = lo; c < hi;) {
             const int64_t e = c + lane;
-            WalkEnt<K, NB> en;
+            // the entry's slot si = k L + r: its member mask and counts from the count pass,
+            // its offsets and weights from k -- four independent gathers
+            Ent<K, NB> en;
             uint32_t cnt = 0;
             if (e < hi) {
-                en = ent[sval[e]];
+                const int64_t si = sval[e];
+                const int64_t kk = si / L;
+                en.k = (uint32_t)kk;
+                en.o = perm ? (uint32_t)perm[kk] : (uint32_t)kk;
+                en.cnt = (uint32_t)spk[si];
+#pragma unroll
+                for (int q = 0; q < K; ++q) en.mask[q] = smask[si * K + q];
+                ldb<NB>(wbar + kk * NB, en.wb);
 #pragma unroll
                 for (int q = 0; q < K; ++q) cnt += (uint32_t)__popcll(en.mask[q]);
             } else {
@@ -2621,15 +2625,14 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan32_tb, (int32_t *)nullptr, (int32_t *)nullptr, (int)npix, st);
     const size_t cub_tb = std::max({sort_tb, sort64_tb, scan_tb, scan32_tb});
     const int KW = L <= 64 ? 1 : (L <= 128 ? 2 : 4);     // member-mask words per entry (k_ds_rows' K)
-    const int64_t rec_words = (2 + KW + NB + 1) / 2 * 2;   // sizeof(WalkEnt<KW, NB>) / 8 (16-B aligned)
     Arena ar;
     ar.cap = Arena::bytes<char>(cub_tb) + Arena::bytes<int64_t>(NO + 1) + 8 * Arena::bytes<int32_t>(N) +
              Arena::bytes<double>((size_t)N * 2 * NB) + Arena::bytes<int64_t>(npix + 1) +
              2 * Arena::bytes<int32_t>(npix) + Arena::bytes<int64_t>(2) + Arena::bytes<int32_t>(N) +
              Arena::bytes<int32_t>(1) + 2 * Arena::bytes<uint64_t>(N) + Arena::bytes<int64_t>(NO / 32 + 2) +
-             Arena::bytes<uint64_t>((size_t)N * rec_words) +
+             Arena::bytes<uint64_t>((size_t)N * KW) +
              Arena::bytes<uint32_t>((size_t)npix * NB) +
-             2 * Arena::bytes<int64_t>(NO + 1) + Arena::bytes<int32_t>(1);
+             2 * Arena::bytes<int64_t>(NO + 1) + Arena::bytes<int32_t>(2);
     COMAP_CHECK(ctx, comap_tmp_alloc((void **)&ar.base, ar.cap, st));
     struct ArenaFree {
         Arena *a;
@@ -2657,10 +2660,10 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     int64_t *swid = ar.take<int64_t>(NC + 1);
     // member-mask walk (count form): slot / entry member masks, integer hits of the groups
     // without an entry, the transpose's rows in the caller's offset order
-    void *went = ar.take<uint64_t>((size_t)N * rec_words);      // WalkEnt<KW, NB> per slot
+    uint64_t *smask = ar.take<uint64_t>((size_t)N * KW);         // member masks per slot
     uint32_t *hextra = ar.take<uint32_t>((size_t)npix * NB);
     int64_t *cnt_nat = ar.take<int64_t>(NO + 1), *orow_nat = ar.take<int64_t>(NO + 1);
-    int32_t *nonfin = ar.take<int32_t>(1);
+    int32_t *nonfin = ar.take<int32_t>(2);       // [non-finite tod, pixel index >= npix]
     bool walk = true;
     {
         const char *we = getenv("COMAP_DS_WALK");        // 0: the sorted-sample payload walk
@@ -2682,12 +2685,12 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         COMAP_NB_SWITCH(nb, (launch_rows<NB, false, false>(
                                 L, st, pix, w, tod, N, NO, npix, d->perm, cnt, d->ws, d->tw,
                                 payload, skey, sval, d->wbar, nonuni, nullptr, nullptr,
-                                nullptr, nullptr, nullptr, eval, eoff, nullptr, with_payload ? nullptr : went,
-                                with_payload ? nullptr : hextra, keep, with_payload ? nullptr : nonfin)));
+                                nullptr, nullptr, nullptr, eval, eoff, nullptr, with_payload ? nullptr : smask,
+                                with_payload ? nullptr : hextra, keep, nonfin)));
     };
+    COMAP_CHECK(ctx, hipMemsetAsync(nonfin, 0, 8, st));
     if (walk) {
         COMAP_CHECK(ctx, hipMemsetAsync(hextra, 0, 4 * (size_t)npix * NB, st));
-        COMAP_CHECK(ctx, hipMemsetAsync(nonfin, 0, 4, st));
     }
     count_pass(!walk);
     COMAP_LAUNCH_CHECK(ctx);
@@ -2718,11 +2721,13 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(cub_tmp, scan_tb, swid, d->sbase, (int)(NCs + 1), st));
         COMAP_CHECK(ctx, hipMemcpyAsync(&d->nsell, d->sbase + NCs, 8, hipMemcpyDeviceToHost, st));
     }
-    int32_t nonuni_h = 0, nonfin_h = 0;
+    int32_t nonuni_h = 0, flags_h[2] = {0, 0};
     COMAP_CHECK(ctx, hipMemcpyAsync(&d->nnz, d->orow + NO, 8, hipMemcpyDeviceToHost, st));
     COMAP_CHECK(ctx, hipMemcpyAsync(&nonuni_h, nonuni, 4, hipMemcpyDeviceToHost, st));
-    if (walk) COMAP_CHECK(ctx, hipMemcpyAsync(&nonfin_h, nonfin, 4, hipMemcpyDeviceToHost, st));
+    COMAP_CHECK(ctx, hipMemcpyAsync(flags_h, nonfin, 8, hipMemcpyDeviceToHost, st));
     COMAP_CHECK(ctx, hipStreamSynchronize(st));
+    const int32_t nonfin_h = flags_h[0];
+    if (flags_h[1]) return comap_fail(ctx, -3, "pixel index out of range for the map (>= npix)");
     {
         const char *cfe = getenv("COMAP_DS_CF");             // 0: always the f64 entry weights
         d->cf = !nonuni_h && L <= 255 && !(cfe && cfe[0] == '0');
@@ -2834,7 +2839,7 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         const char *wxe = getenv("COMAP_DS_WXCD");
         const bool wx = wxe && wxe[0] == '1';
 #define COMAP_W2(KK, MM) k_sample_walk2<NB, KK, MM><<<wgrid, 256, 0, st>>>(                                   \
-        d->prow, evn2, (const WalkEnt<KK, NB> *)went, w, payload, N, npix, L, NO, keep, hextra, d->h, d->hits, d->nnum, \
+        d->prow, evn2, smask, eoff, d->perm, d->wbar, w, payload, N, npix, L, NO, keep, hextra, d->h, d->hits, d->nnum, \
         d->poff, d->pcnt, wx)
         if (KW == 1 && M == 1) { COMAP_NB_SWITCH(nb, COMAP_W2(1, 1)); }
         else if (KW == 1) { COMAP_NB_SWITCH(nb, COMAP_W2(1, 2)); }

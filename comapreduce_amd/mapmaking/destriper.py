@@ -251,9 +251,7 @@ class DeviceOps:
             raise ValueError('pointing, tod and weights must have the same length')
         if n % offset_length:
             raise ValueError('number of samples must be a multiple of offset_length')
-        pmax = int(self.pix.max().item()) if n else -1
-        if pmax >= npix:
-            raise IndexError(f'pixel index {pmax} out of range for a map of {npix} pixels')
+        # (pixel indices >= npix are caught by the set-up's count pass on the device: rc -3)
         self.L, self.npix = int(offset_length), int(npix)
         kp = None
         if keep is not None:
@@ -268,10 +266,12 @@ class DeviceOps:
         self.tod, self.w, self.keep = tod2.contiguous(), w2.contiguous(), kp
         h = ctypes.c_void_p()
         N.bind_stream(self.ctx, self.dev)
-        N.check(N.lib().comap_destripe_create_bands(self.ctx, N.dptr(self.pix), N.dptr(self.tod), N.dptr(self.w),
-                                                    None if kp is None else N.dptr(kp), n, self.L, self.npix,
-                                                    self.nb, ctypes.byref(h)), self.ctx,
-                'comap_destripe_create_bands')
+        rc = N.lib().comap_destripe_create_bands(self.ctx, N.dptr(self.pix), N.dptr(self.tod), N.dptr(self.w),
+                                                 None if kp is None else N.dptr(kp), n, self.L, self.npix,
+                                                 self.nb, ctypes.byref(h))
+        if rc == -3:
+            raise IndexError(f'pixel index out of range for a map of {npix} pixels')
+        N.check(rc, self.ctx, 'comap_destripe_create_bands')
         self.h = h
         self.n_offsets = int(N.lib().comap_destripe_n_offsets(h))
         # map-tile projection (comap_destripe_tiles) for a row-major map of known width:

@@ -225,7 +225,9 @@ int comap_destripe_create(comap_ctx *ctx, const int32_t *pixels_dev, const doubl
  * Offset order: the problem processes its offsets in an internal (spatially
  * sorted) order; every offset vector the functions below take or return is in
  * that order, except the x of comap_destripe_solve, which is in the caller's
- * order.  comap_destripe_offsets_natural converts an internal vector. */
+ * order.  comap_destripe_offsets_natural converts an internal vector.
+ * Returns -3 when a pixel index is >= npix (checked on the device by the set-up's
+ * count pass; the reference would raise IndexError binning it). */
 int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pixels_dev, const double *tod_dev,
                                 const double *weights_dev, const uint8_t *keep_dev, int64_t n_samples,
                                 int32_t offset_length, int64_t npix, int32_t n_bands, comap_destriper **out);

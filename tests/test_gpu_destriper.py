@@ -468,3 +468,59 @@ def test_solve_to_host_equals_device_maps(nb):
     for k, v in want.items():
         assert got['maps'][k].shape == v.shape, k
         assert np.array_equal(got['maps'][k], v), k
+
+
+@pytest.mark.parametrize('case,Lc,nb', [('walk', 50, 4), ('payload', 50, 4), ('walk', 100, 1), ('walk', 250, 2),
+                                        ('zeros', 50, 4), ('nonfinite', 50, 1), ('nonfinite', 50, 4)])
+def test_sample_maps_set_up_paths(case, Lc, nb, monkeypatch):
+    """The set-up's sample-level maps (weight, hits, naive: binValues' sample order, so
+    bit-exact) on each of its paths against the oracle: the member-mask walk (default;
+    member masks of 1, 2 and 4 words for L = 50, 100, 250), the sorted-sample payload walk
+    (COMAP_DS_WALK=0), kept offsets holding all-zero-weight pixel groups (their hits come
+    from the count pass's integer adds), and non-finite tod on zero-weight samples (the
+    set-up falls back to the payload walk, whose NaN reaches the naive map as
+    binValues' does; the solve itself is not compared there)."""
+    import oracle.destriper as od
+    from comapreduce_amd.mapmaking.destriper import DeviceDestriper
+    if case == 'payload':
+        monkeypatch.setenv('COMAP_DS_WALK', '0')
+    p, tods, ws, keep = _bands_problem(max(nb, 2))
+    tods, ws, keep = tods[:nb].copy(), ws[:nb].copy(), keep[:nb]
+    if Lc != L:                       # whole offsets of the new length, no band drops
+        n = p.size // Lc * Lc
+        p, tods, ws = p[:n], tods[:, :n], ws[:, :n]
+        keep = np.ones((nb, n // Lc), dtype=bool)
+        ws[ws == 0] = 1.0
+    rng = np.random.default_rng(3)
+    if case in ('zeros', 'nonfinite'):
+        zero = rng.choice(p.size, p.size // 20, replace=False)
+        ws[:, zero] = 0.0
+    if case == 'nonfinite':
+        tods[:, zero[:7]] = np.nan
+        tods[:, zero[7:9]] = np.inf
+    dd = DeviceDestriper(p, tods if nb > 1 else tods[0], ws if nb > 1 else ws[0], Lc, NPIX,
+                         keep=keep if nb > 1 else None)
+    finite = case != 'nonfinite'
+    res = dd.solve(1e-6 if finite else 0.0, 100 if finite else 2)
+    for b in range(nb):
+        sel = np.repeat(keep[b], Lc)
+        ref, xr, itr = od.destriper_iteration(p[sel], tods[b][sel], ws[b][sel], Lc, NPIX,
+                                              threshold=1e-6 if finite else 0.0, niter=100 if finite else 2)
+        m = {k: (v[b] if nb > 1 else v).cpu().numpy() for k, v in res['maps'].items()}
+        assert np.array_equal(m['weight'], ref['weight']), (case, b)
+        assert np.array_equal(m['hits'], ref['hits']), (case, b)
+        assert np.array_equal(m['naive'], ref['naive'], equal_nan=True), (case, b)
+        if finite:
+            assert (res['iters'][b] if nb > 1 else res['iters']) == itr
+            assert rel(m['map'], ref['map']) < 1e-9, (case, b)
+
+
+def test_pixel_out_of_range_raises():
+    """A pixel index >= npix is an error (the reference's binning would index past the
+    map); the set-up's count pass finds it on the device."""
+    from comapreduce_amd.mapmaking.destriper import DeviceDestriper
+    p, t, w = synthetic.destriper_inputs()
+    p = p.copy()
+    p[1234] = NPIX
+    with pytest.raises(IndexError):
+        DeviceDestriper(p, t, w, L, NPIX)
