@@ -127,6 +127,8 @@ def test_gpu_prep_pieces_vs_numpy():
             assert (np.isnan(want) and np.isnan(got)) or want == got, (T, r, want, got)
         az = np.round(rng.standard_normal((3, T)) * 20 + 180, 2)
         az[1, rng.random(T) < 0.1] = np.nan
+        az[0] = np.round(rng.standard_normal(T) * 2, 1)          # both signs, zeros, -0.0, ties
+        az[0, rng.random(T) < 0.05] = -0.0
         el = np.round(rng.standard_normal((3, T)) * 5 + 45, 3)
         el[2, 0] = np.nan if T > 3 else el[2, 0]
         pct = torch.empty((3, 4), dtype=torch.float64, device='cuda')
