@@ -951,10 +951,22 @@ __global__ void k_scale(const double *__restrict__ wbar, const double *__restric
 
 // Non-empty pixel rows for the CG bin: flag, exclusive scan, then the compact list with
 // each row's entry range (hprow[i] = prow[hrow[i]], hprow[nh] = nnzp) and nh itself.
-__global__ void k_hit_flags(const int64_t *__restrict__ prow, int64_t npix, int32_t *__restrict__ flag)
+// h != NULL (member-mask walk, which visits the non-empty rows only): an empty row's
+// sample-level maps here -- h = naive numerator = 0, hits = its zero-weight samples' count
+__global__ void k_hit_flags(const int64_t *__restrict__ prow, int64_t npix, int32_t *__restrict__ flag, int nb,
+                            const uint32_t *__restrict__ hextra, double *__restrict__ h, double *__restrict__ hits,
+                            double *__restrict__ nnum)
 {
-    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x)
-        flag[p] = prow[p + 1] > prow[p] ? 1 : 0;
+    for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x) {
+        const bool hit = prow[p + 1] > prow[p];
+        flag[p] = hit ? 1 : 0;
+        if (h && !hit)
+            for (int b = 0; b < nb; ++b) {
+                h[p * nb + b] = 0.0;
+                nnum[p * nb + b] = 0.0;
+                hits[p * nb + b] = (double)hextra[p * nb + b];
+            }
+    }
 }
 
 __global__ void k_hit_rows(const int64_t *__restrict__ prow, const int32_t *__restrict__ flag,
@@ -1064,7 +1076,9 @@ __device__ __forceinline__ int select_bit(uint64_t x, int r)
 // an entry carry zero weights (they add nothing to h or to the naive numerator); their
 // hits come from the count pass's integer adds.
 template <int NB, int K, int M>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) k_sample_walk2(const int64_t *__restrict__ prow,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) k_sample_walk2(const int32_t *__restrict__ hrow,
+                                                      const int64_t *__restrict__ hprow,
+                                                      const int64_t *__restrict__ counts,
                                                       const int32_t *__restrict__ sval,
                                                       const uint64_t *__restrict__ smask,
                                                       const int32_t *__restrict__ spk,
@@ -1088,9 +1102,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) k
     const int kind = lane / NB, b = lane % NB;     // this lane's ordered sum (lanes < 3 NB)
     const int col = kind == 2 ? 0 : kind * NB + b;
     // xcd: each XCD walks one contiguous eighth of the pixels
+    // the non-empty rows only (k_hit_flags wrote the empty ones): row i of nh = counts[1]
     const int64_t lb = xcd_block(blockIdx.x, gridDim.x, xcd);
-    for (int64_t p = lb * 4 + wv; p < npix; p += (int64_t)gridDim.x * 4) {
-        const int64_t lo = prow[p], hi = prow[p + 1];
+    const int64_t nh = counts[1];
+    for (int64_t i = lb * 4 + wv; i < nh; i += (int64_t)gridDim.x * 4) {
+        const int64_t p = hrow[i];
+        const int64_t lo = hprow[i], hi = hprow[i + 1];
         double acc = 0.0;
         for (int64_t c = lo; c < hi;) {
             const int64_t e = c + lane;
@@ -2825,7 +2842,8 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
                                                                                          d->pcnt));
     }
     COMAP_LAUNCH_CHECK(ctx);
-    k_hit_flags<<<grid_for(npix), 256, 0, st>>>(d->prow, npix, hflag);
+    k_hit_flags<<<grid_for(npix), 256, 0, st>>>(d->prow, npix, hflag, nb, hextra, walk ? d->h : nullptr, d->hits,
+                                                d->nnum);
     COMAP_LAUNCH_CHECK(ctx);
     COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(cub_tmp, scan32_tb, hflag, hpos, (int)npix, st));
     k_hit_rows<<<grid_for(npix), 256, 0, st>>>(d->prow, hflag, hpos, npix, d->hrow, d->hprow, counts);
@@ -2838,8 +2856,9 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         const int M = std::max(KW, wm && wm[0] == '2' ? 2 : 1);
         const char *wxe = getenv("COMAP_DS_WXCD");
         const bool wx = wxe && wxe[0] == '1';
-#define COMAP_W2(KK, MM) k_sample_walk2<NB, KK, MM><<<wgrid, 256, 0, st>>>(                                   \
-        d->prow, evn2, smask, eoff, d->perm, d->wbar, w, payload, N, npix, L, NO, keep, hextra, d->h, d->hits, d->nnum, \
+        const unsigned wgrid2 = wgrid;     // one wave per row (a fixed 2048-block grid: C5 0.80 -> 1.04 ms)
+#define COMAP_W2(KK, MM) k_sample_walk2<NB, KK, MM><<<wgrid2, 256, 0, st>>>(                                  \
+        d->hrow, d->hprow, counts, evn2, smask, eoff, d->perm, d->wbar, w, payload, N, npix, L, NO, keep, hextra, d->h, d->hits, d->nnum, \
         d->poff, d->pcnt, wx)
         if (KW == 1 && M == 1) { COMAP_NB_SWITCH(nb, COMAP_W2(1, 1)); }
         else if (KW == 1) { COMAP_NB_SWITCH(nb, COMAP_W2(1, 2)); }
