@@ -456,6 +456,17 @@ __global__ void k_offset_keys(const int32_t *__restrict__ pix, int64_t NO, int L
     }
 }
 
+// Member-mask walk: a kept entry's slot record, written by the count pass at slot
+// k L + r (offset k's r-th entry) -- pixel, packed per-band non-zero counts, member mask
+// (sample j of the offset = bit j) -- one 16-B-aligned gather for the sample walk
+template <int K>
+struct alignas(16) SlotRec {
+    int32_t pix;
+    uint32_t cnt;
+    uint64_t mask[K];
+};
+static_assert(sizeof(SlotRec<1>) == 16 && sizeof(SlotRec<2>) == 32 && sizeof(SlotRec<4>) == 48, "SlotRec");
+
 // Offset rows of the sparse operator, one wave per row k (offset o = perm[k]): lane l
 // holds samples l, l + 64, ... (K per lane, L <= 64 K).  The distinct pixels of the
 // offset are found in first-occurrence order by a leader loop (the first pending
@@ -487,7 +498,7 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
                                                  double *__restrict__ ow, uint8_t *__restrict__ ocnt,
                                                  int32_t *__restrict__ ekey, int32_t *__restrict__ eval,
                                                  int32_t *__restrict__ eoff, uint64_t *__restrict__ epay,
-                                                 uint64_t *__restrict__ smask, uint32_t *__restrict__ hextra,
+                                                 SlotRec<K> *__restrict__ srec, uint32_t *__restrict__ hextra,
                                                  const uint8_t *__restrict__ keep, int32_t *__restrict__ nonfin)
 {
 #pragma clang fp contract(off)
@@ -655,12 +666,13 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
             const int j = lane + 64 * m;
             if (j < L) {
                 const int64_t i = base + j;
-                if (payload && smask) {
+                if (payload && srec) {
                     // member-mask walk: (tod w) per band, sample-major (NB doubles a sample)
+                    // in the internal offset order (slot k L + j), so the walk needs no perm
                     double pt[NB];
 #pragma unroll
                     for (int b = 0; b < NB; ++b) pt[b] = ti[m][b] * wi[m][b];
-                    stb<NB>(payload + i * NB, pt);
+                    stb<NB>(payload + (k * L + j) * NB, pt);
                 } else if (payload) {
                     double pl[2 * NB];
 #pragma unroll
@@ -684,7 +696,7 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
         // zero) by integer adds -- order-free, exact -- and a flag for non-finite tod, which
         // such groups would carry into the naive numerator (the set-up then takes the
         // payload walk, which reproduces that)
-        if (smask) {
+        if (srec) {
             if (nonfin && __ballot(nf) && lane == 0) nonfin[0] = 1;
 #pragma unroll
             for (int m = 0; m < K; ++m)
@@ -721,7 +733,7 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
             (idx & 1 ? tw : ws)[k * NB + (idx >> 1)] = red[0];
         }
         if (lane == 0) cnt[k] = c0;
-        if (eval) {
+        if (eval || srec) {
             int64_t r0 = k * L;
 #pragma unroll
             for (int m = 0; m < K; ++m) {
@@ -731,11 +743,16 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
                     uint32_t pk = 0;
 #pragma unroll
                     for (int b = 0; b < NB; ++b) pk |= (uint32_t)(gc[m][b] & 255) << (8 * b);
-                    eval[si] = q[m];
-                    eoff[si] = (int32_t)pk;
-                    if (smask) {
+                    if (srec) {
+                        SlotRec<K> rc;
+                        rc.pix = q[m];
+                        rc.cnt = pk;
 #pragma unroll
-                        for (int c = 0; c < K; ++c) smask[si * K + c] = mem[m][c];
+                        for (int c = 0; c < K; ++c) rc.mask[c] = mem[m][c];
+                        srec[si] = rc;
+                    } else {
+                        eval[si] = q[m];
+                        eoff[si] = (int32_t)pk;
                     }
                 }
                 r0 += __popcll(bm);
@@ -800,7 +817,7 @@ void launch_rows(int L, hipStream_t st, const int32_t *pix, const double *w, con
                  int64_t NO, int64_t npix, const int32_t *perm, int64_t *cnt, double *ws, double *tw, double *payload,
                  int32_t *skey, int32_t *sval, double *wbar, int32_t *nonuni, const int64_t *orow, int32_t *opix,
                  double *ow, uint8_t *ocnt, int32_t *ekey, int32_t *eval, int32_t *eoff, uint64_t *epay = nullptr,
-                 uint64_t *smask = nullptr, uint32_t *hextra = nullptr, const uint8_t *keep = nullptr,
+                 void *srec = nullptr, uint32_t *hextra = nullptr, const uint8_t *keep = nullptr,
                  int32_t *nonfin = nullptr)
 {
     // k_ds_rows' grid: COMAP_DS_RB blocks at most (default: one offset per wave)
@@ -813,7 +830,7 @@ void launch_rows(int L, hipStream_t st, const int32_t *pix, const double *w, con
 #define COMAP_ROWS(K) k_ds_rows<K, NB, FILL, CF><<<blocks, 256, 0, st>>>(pix, w, tod, N, NO, L, npix, perm, cnt, ws, \
                                                                           tw, payload, skey, sval, wbar, nonuni, orow, \
                                                                           opix, ow, ocnt, ekey, eval, eoff, epay, \
-                                                                          smask, hextra, keep, nonfin)
+                                                                          (SlotRec<K> *)srec, hextra, keep, nonfin)
     if (L <= 64) COMAP_ROWS(1);
     else if (L <= 128) COMAP_ROWS(2);
     else COMAP_ROWS(4);
@@ -863,12 +880,11 @@ __global__ void k_cnt_natural(const int64_t *__restrict__ cnt, const int32_t *__
 // sort by pixel leaves each pixel's entries in sample order -- the order binValues adds
 // them in.  16 lanes per row (rows hold ~30 entries; a wave per row waited on its loads:
 // 0.6 ms at C5).
-template <int NB>
+template <int NB, int K>
 __global__ void __launch_bounds__(256) k_ds_compact_walk(const int64_t *__restrict__ orow,
                                                          const int64_t *__restrict__ orow_nat,
                                                          const int32_t *__restrict__ perm, int64_t NO, int L,
-                                                         int64_t npix, const int32_t *__restrict__ spx,
-                                                         const int32_t *__restrict__ spk,
+                                                         int64_t npix, const SlotRec<K> *__restrict__ srec,
                                                          int32_t *__restrict__ opix, uint8_t *__restrict__ ocnt,
                                                          int32_t *__restrict__ ekey, int32_t *__restrict__ eval)
 {
@@ -878,8 +894,8 @@ __global__ void __launch_bounds__(256) k_ds_compact_walk(const int64_t *__restri
     const int64_t o = perm ? (int64_t)perm[k] : k;
     const int64_t e0 = orow[k], c = orow[k + 1] - e0, n0 = orow_nat[o];
     for (int64_t r = sub; r < c; r += 16) {
-        const int32_t q = spx[k * L + r];
-        const uint32_t pk = (uint32_t)spk[k * L + r];
+        const int32_t q = srec[k * L + r].pix;
+        const uint32_t pk = srec[k * L + r].cnt;
         const int64_t ei = e0 + r;
         opix[ei] = q;
         if constexpr (NB == 4) {
@@ -1080,8 +1096,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) k
                                                       const int64_t *__restrict__ hprow,
                                                       const int64_t *__restrict__ counts,
                                                       const int32_t *__restrict__ sval,
-                                                      const uint64_t *__restrict__ smask,
-                                                      const int32_t *__restrict__ spk,
+                                                      const SlotRec<K> *__restrict__ srec,
                                                       const int32_t *__restrict__ perm,
                                                       const double *__restrict__ wbar,
                                                       const double *__restrict__ w, const double *__restrict__ ptw,
@@ -1111,18 +1126,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) k
         double acc = 0.0;
         for (int64_t c = lo; c < hi;) {
             const int64_t e = c + lane;
-            // the entry's slot si = k L + r: its member mask and counts from the count pass,
-            // its offsets and weights from k -- four independent gathers
+            // the entry's slot si = k L + r: its record (member mask, counts) from the count
+            // pass and the offset's weights from k -- two independent gathers (the caller's
+            // offset o only for a keep mask)
             Ent<K, NB> en;
             uint32_t cnt = 0;
             if (e < hi) {
                 const int64_t si = sval[e];
                 const int64_t kk = si / L;
+                const SlotRec<K> rc = srec[si];
                 en.k = (uint32_t)kk;
-                en.o = perm ? (uint32_t)perm[kk] : (uint32_t)kk;
-                en.cnt = (uint32_t)spk[si];
+                en.o = (keep && perm) ? (uint32_t)perm[kk] : (uint32_t)kk;
+                en.cnt = rc.cnt;
 #pragma unroll
-                for (int q = 0; q < K; ++q) en.mask[q] = smask[si * K + q];
+                for (int q = 0; q < K; ++q) en.mask[q] = rc.mask[q];
                 ldb<NB>(wbar + kk * NB, en.wb);
 #pragma unroll
                 for (int q = 0; q < K; ++q) cnt += (uint32_t)__popcll(en.mask[q]);
@@ -1175,7 +1192,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) k
                 j = t < total ? j - 1 : 0;
                 const uint32_t exj = (uint32_t)__shfl((int)excl, j, 64);
                 const uint32_t nmj = (uint32_t)__shfl((int)cnt, j, 64);
-                const uint32_t oj = (uint32_t)__shfl((int)en.o, j, 64);
+                const uint32_t kj = (uint32_t)__shfl((int)en.k, j, 64);
                 const uint32_t kbj = (uint32_t)__shfl((int)kb, j, 64);
                 const uint32_t gcj = (uint32_t)__shfl((int)en.cnt, j, 64);
                 uint64_t mj[K];
@@ -1192,13 +1209,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) k
                         if (r >= 0 && r < cq) bitpos = 64 * q + select_bit(mj[q], r);
                         r -= cq;
                     }
-                    const int64_t i = (int64_t)oj * L + bitpos;
                     double pv[NB];
-                    ldb<NB>(ptw + i * NB, pv);
+                    ldb<NB>(ptw + ((int64_t)kj * L + bitpos) * NB, pv);
 #pragma unroll
                     for (int bb = 0; bb < NB; ++bb) {
                         const uint32_t gc = (gcj >> (8 * bb)) & 255u;
-                        pl[t * 2 * NB + bb] = gc == nmj ? wbj[bb] : (gc == 0 ? 0.0 : w[(int64_t)bb * N + i]);
+                        double wv = gc == nmj ? wbj[bb] : 0.0;
+                        if (gc != 0 && gc != nmj) {    // a mixed group: the sample's own weight
+                            const int64_t on = perm ? (int64_t)perm[kj] : (int64_t)kj;
+                            wv = w[(int64_t)bb * N + on * L + bitpos];
+                        }
+                        pl[t * 2 * NB + bb] = wv;
                         pl[t * 2 * NB + NB + bb] = pv[bb];
                     }
                     mk[t] = kbj;
@@ -2642,12 +2663,13 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan32_tb, (int32_t *)nullptr, (int32_t *)nullptr, (int)npix, st);
     const size_t cub_tb = std::max({sort_tb, sort64_tb, scan_tb, scan32_tb});
     const int KW = L <= 64 ? 1 : (L <= 128 ? 2 : 4);     // member-mask words per entry (k_ds_rows' K)
+    const int64_t rec_words = KW == 1 ? 2 : (KW == 2 ? 4 : 6);   // sizeof(SlotRec<KW>) / 8
     Arena ar;
     ar.cap = Arena::bytes<char>(cub_tb) + Arena::bytes<int64_t>(NO + 1) + 8 * Arena::bytes<int32_t>(N) +
              Arena::bytes<double>((size_t)N * 2 * NB) + Arena::bytes<int64_t>(npix + 1) +
              2 * Arena::bytes<int32_t>(npix) + Arena::bytes<int64_t>(2) + Arena::bytes<int32_t>(N) +
              Arena::bytes<int32_t>(1) + 2 * Arena::bytes<uint64_t>(N) + Arena::bytes<int64_t>(NO / 32 + 2) +
-             Arena::bytes<uint64_t>((size_t)N * KW) +
+             Arena::bytes<uint64_t>((size_t)N * rec_words) +
              Arena::bytes<uint32_t>((size_t)npix * NB) +
              2 * Arena::bytes<int64_t>(NO + 1) + Arena::bytes<int32_t>(2);
     COMAP_CHECK(ctx, comap_tmp_alloc((void **)&ar.base, ar.cap, st));
@@ -2677,7 +2699,7 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     int64_t *swid = ar.take<int64_t>(NC + 1);
     // member-mask walk (count form): slot / entry member masks, integer hits of the groups
     // without an entry, the transpose's rows in the caller's offset order
-    uint64_t *smask = ar.take<uint64_t>((size_t)N * KW);         // member masks per slot
+    void *srec = ar.take<uint64_t>((size_t)N * rec_words);       // SlotRec<KW> per slot
     uint32_t *hextra = ar.take<uint32_t>((size_t)npix * NB);
     int64_t *cnt_nat = ar.take<int64_t>(NO + 1), *orow_nat = ar.take<int64_t>(NO + 1);
     int32_t *nonfin = ar.take<int32_t>(2);       // [non-finite tod, pixel index >= npix]
@@ -2702,7 +2724,7 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         COMAP_NB_SWITCH(nb, (launch_rows<NB, false, false>(
                                 L, st, pix, w, tod, N, NO, npix, d->perm, cnt, d->ws, d->tw,
                                 payload, skey, sval, d->wbar, nonuni, nullptr, nullptr,
-                                nullptr, nullptr, nullptr, eval, eoff, nullptr, with_payload ? nullptr : smask,
+                                nullptr, nullptr, nullptr, eval, eoff, nullptr, with_payload ? nullptr : srec,
                                 with_payload ? nullptr : hextra, keep, nonfin)));
     };
     COMAP_CHECK(ctx, hipMemsetAsync(nonfin, 0, 8, st));
@@ -2793,8 +2815,12 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     // ---- 3. fill pass
     int32_t *evn = skey2, *evn2 = sval2;   // walk: the sample-sort arrays are free
     if (walk) {
-        COMAP_NB_SWITCH(nb, (k_ds_compact_walk<NB><<<(unsigned)((NO + 15) / 16), 256, 0, st>>>(
-                                d->orow, orow_nat, d->perm, NO, L, npix, eval, eoff, d->opix, d->ocnt, ekey, evn)));
+#define COMAP_CW(KK) k_ds_compact_walk<NB, KK><<<(unsigned)((NO + 15) / 16), 256, 0, st>>>(                     \
+        d->orow, orow_nat, d->perm, NO, L, npix, (const SlotRec<KK> *)srec, d->opix, d->ocnt, ekey, evn)
+        if (KW == 1) { COMAP_NB_SWITCH(nb, COMAP_CW(1)); }
+        else if (KW == 2) { COMAP_NB_SWITCH(nb, COMAP_CW(2)); }
+        else { COMAP_NB_SWITCH(nb, COMAP_CW(4)); }
+#undef COMAP_CW
     } else if (d->cf) {
         COMAP_NB_SWITCH(nb, (k_ds_compact_cf<NB><<<(unsigned)((NO + 3) / 4), 256, 0, st>>>(
                                 d->orow, NO, L, npix, eval, eoff, d->opix, d->ocnt, ekey, epay)));
@@ -2858,7 +2884,7 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         const bool wx = wxe && wxe[0] == '1';
         const unsigned wgrid2 = wgrid;     // one wave per row (a fixed 2048-block grid: C5 0.80 -> 1.04 ms)
 #define COMAP_W2(KK, MM) k_sample_walk2<NB, KK, MM><<<wgrid2, 256, 0, st>>>(                                  \
-        d->hrow, d->hprow, counts, evn2, smask, eoff, d->perm, d->wbar, w, payload, N, npix, L, NO, keep, hextra, d->h, d->hits, d->nnum, \
+        d->hrow, d->hprow, counts, evn2, (const SlotRec<KK> *)srec, d->perm, d->wbar, w, payload, N, npix, L, NO, keep, hextra, d->h, d->hits, d->nnum, \
         d->poff, d->pcnt, wx)
         if (KW == 1 && M == 1) { COMAP_NB_SWITCH(nb, COMAP_W2(1, 1)); }
         else if (KW == 1) { COMAP_NB_SWITCH(nb, COMAP_W2(1, 2)); }
