@@ -39,6 +39,7 @@
 #include "comap_internal.h"
 
 #include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include <cmath>
 #include <type_traits>
@@ -442,17 +443,27 @@ __device__ __forceinline__ void block_partials(double (&acc)[NB], double *red, d
 // of map rows, and puts offsets that cross the same pixels next to each other in the
 // CG vectors (the bin's x gathers).  Key: that pixel (npix when the offset is all
 // off-map); a stable sort keeps time order among equal keys.
-__global__ void k_offset_keys(const int32_t *__restrict__ pix, int64_t NO, int L, int64_t npix,
-                              int32_t *__restrict__ key, int32_t *__restrict__ val)
+// (one wave per offset: its pixels by coalesced loads, the first on-map one by a ballot;
+// a thread per offset walked an off-map offset's L pixels one dependent load at a time)
+__global__ void __launch_bounds__(256) k_offset_keys(const int32_t *__restrict__ pix, int64_t NO, int L, int64_t npix,
+                                                     int32_t *__restrict__ key, int32_t *__restrict__ val)
 {
-    for (int64_t o = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; o < NO; o += (int64_t)gridDim.x * blockDim.x) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); o < NO; o += (int64_t)gridDim.x * 4) {
         int32_t k = (int32_t)npix;
-        for (int j = 0; j < L; ++j) {
-            const int32_t p = pix[o * L + j];
-            if (p >= 0) { k = p; break; }
+        for (int j0 = 0; j0 < L; j0 += 64) {
+            const int j = j0 + lane;
+            const int32_t p = j < L ? pix[o * L + j] : -1;
+            const unsigned long long v = __ballot(p >= 0);
+            if (v) {
+                k = __shfl(p, __ffsll((long long)v) - 1, 64);
+                break;
+            }
         }
-        key[o] = k;
-        val[o] = (int32_t)o;
+        if (lane == 0) {
+            key[o] = k;
+            val[o] = (int32_t)o;
+        }
     }
 }
 
@@ -857,6 +868,27 @@ __device__ __forceinline__ int64_t lb32(const int32_t *a, int64_t n, int64_t v)
         if (a[m] < v) lo = m + 1; else hi = m;
     }
     return lo;
+}
+
+// Stable sort of int32 (key, value) pairs on key bits [0, end_bit): nine = rocprim's onesweep
+// with 9-bit digits (match-based ranking: 512 buckets do not fit the basic rank's LDS) and
+// no merge-sort path -- for the spatial offset sort, 18-bit pixel keys of 547 k offsets in
+// 2 passes (63 us) instead of hipcub's ~20 block-merge kernels (131 us) at C5.  The
+// transpose (15.4 M pairs) stays on hipcub's 8-bit onesweep: 410 us in 3 passes against
+// 537 us in 2 with the match ranking (r04zr).  Keys are non-negative.
+using Sort9Config = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 12>, rocprim::kernel_config<256, 12>, 9,
+                                        rocprim::block_radix_rank_algorithm::match>,
+    0>;
+
+hipError_t sort_pairs_i32(bool nine, void *tmp, size_t &bytes, const int32_t *kin, int32_t *kout, const int32_t *vin,
+                          int32_t *vout, int64_t n, int end_bit, hipStream_t st)
+{
+    if (nine)
+        return rocprim::radix_sort_pairs<Sort9Config>(tmp, bytes, kin, kout, vin, vout, (unsigned)n, 0u,
+                                                      (unsigned)end_bit, st);
+    return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, kin, kout, vin, vout, (int)n, 0, end_bit, st);
 }
 
 // row[p] = first sorted position with key >= p, p in [0, npix]
@@ -2654,8 +2686,16 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     while ((1ll << end_bit) <= npix) ++end_bit;
     // ---- scratch: sizes first (hipcub temp storage for the largest sort / scan), one allocation
     size_t sort_tb = 0, scan_tb = 0, scan32_tb = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tb, (int32_t *)nullptr, (int32_t *)nullptr,
-                                             (int32_t *)nullptr, (int32_t *)nullptr, (int)N, 0, end_bit, st);
+    const bool nine = [] {
+        const char *v = getenv("COMAP_DS_SORT9");        // 0: hipcub's radix sort for the offset sort too
+        return !(v && v[0] == '0');
+    }();
+    (void)sort_pairs_i32(false, nullptr, sort_tb, nullptr, nullptr, nullptr, nullptr, N, end_bit, st);
+    {
+        size_t tb9 = 0;       // the spatial offset sort (NO pairs)
+        (void)sort_pairs_i32(nine, nullptr, tb9, nullptr, nullptr, nullptr, nullptr, NO, end_bit, st);
+        sort_tb = std::max(sort_tb, tb9);
+    }
     size_t sort64_tb = 0;   // the count form's transpose: (pixel, u64 offset|counts) pairs
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort64_tb, (int32_t *)nullptr, (int32_t *)nullptr,
                                              (uint64_t *)nullptr, (uint64_t *)nullptr, (int)N, 0, end_bit, st);
@@ -2710,10 +2750,10 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     }
     // ---- 1. spatial processing order of the offsets
     if (spatial) {
-        k_offset_keys<<<grid_for(NO), 256, 0, st>>>(pix, NO, L, npix, ekey, eval);
+        k_offset_keys<<<(unsigned)std::min<int64_t>((NO + 3) / 4, 65536), 256, 0, st>>>(pix, NO, L, npix, ekey, eval);
         COMAP_LAUNCH_CHECK(ctx);
-        COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(cub_tmp, sort_tb, ekey, ekey2, eval, d->perm, (int)NO, 0,
-                                                            end_bit, st));
+        size_t tb = cub_tb;
+        COMAP_CHECK(ctx, sort_pairs_i32(nine, cub_tmp, tb, ekey, ekey2, eval, d->perm, NO, end_bit, st));
     }
     // ---- 2. count pass (+ the count-form test: non-zero weights uniform per offset and band)
     COMAP_CHECK(ctx, hipMemsetAsync(nonuni, 0, 4, st));
@@ -2846,8 +2886,8 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     }
     // ---- 4. pixel-major transpose (stable: offset order within a pixel)
     if (walk) {
-        COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(cub_tmp, sort_tb, ekey, ekey2, evn, evn2, (int)d->nnz, 0,
-                                                            end_bit, st));
+        size_t tb = cub_tb;
+        COMAP_CHECK(ctx, sort_pairs_i32(false, cub_tmp, tb, ekey, ekey2, evn, evn2, d->nnz, end_bit, st));
     } else if (d->cf) {
         COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(cub_tmp, sort64_tb, ekey, ekey2, epay, epay2, (int)d->nnz,
                                                             0, end_bit, st));
