@@ -898,6 +898,21 @@ __global__ void k_rowptr(const int32_t *__restrict__ skey, int64_t n, int64_t np
         row[p] = lb32(skey, n, p);
 }
 
+// The set-up's first host read-back in one piece: nnz, the SELL slot count, the count-form
+// and tod / pixel-range flags (four pageable copies cost ~20 us of idle GPU each)
+__global__ void k_setup_sizes(const int64_t *__restrict__ orow, int64_t NO, const int64_t *__restrict__ sbase,
+                              int64_t NCs, const int32_t *__restrict__ nonuni, const int32_t *__restrict__ flags,
+                              int64_t *__restrict__ out)
+{
+    if (threadIdx.x == 0) {
+        out[0] = orow[NO];
+        out[1] = sbase ? sbase[NCs] : 0;
+        out[2] = nonuni[0];
+        out[3] = flags[0];
+        out[4] = flags[1];
+    }
+}
+
 // cnt_nat[perm[k]] = cnt[k]: the offsets' kept-entry counts in the caller's offset order
 __global__ void k_cnt_natural(const int64_t *__restrict__ cnt, const int32_t *__restrict__ perm, int64_t NO,
                               int64_t *__restrict__ cnt_nat)
@@ -2707,7 +2722,7 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     Arena ar;
     ar.cap = Arena::bytes<char>(cub_tb) + Arena::bytes<int64_t>(NO + 1) + 8 * Arena::bytes<int32_t>(N) +
              Arena::bytes<double>((size_t)N * 2 * NB) + Arena::bytes<int64_t>(npix + 1) +
-             2 * Arena::bytes<int32_t>(npix) + Arena::bytes<int64_t>(2) + Arena::bytes<int32_t>(N) +
+             2 * Arena::bytes<int32_t>(npix) + Arena::bytes<int64_t>(8) + Arena::bytes<int32_t>(N) +
              Arena::bytes<int32_t>(1) + 2 * Arena::bytes<uint64_t>(N) + Arena::bytes<int64_t>(NO / 32 + 2) +
              Arena::bytes<uint64_t>((size_t)N * rec_words) +
              Arena::bytes<uint32_t>((size_t)npix * NB) +
@@ -2732,7 +2747,7 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     double *payload = ar.take<double>((size_t)N * 2 * NB);
     int64_t *srow = ar.take<int64_t>(npix + 1);
     int32_t *hflag = ar.take<int32_t>(npix), *hpos = ar.take<int32_t>(npix);
-    int64_t *counts = ar.take<int64_t>(2);
+    int64_t *counts = ar.take<int64_t>(8);      // [nnzp, nh] (k_hit_rows); first the set-up sizes (k_setup_sizes)
     int32_t *nonuni = ar.take<int32_t>(1);
     uint64_t *epay = ar.take<uint64_t>(N), *epay2 = ar.take<uint64_t>(N);   // count form: offset << 32 | counts
     const int64_t NC = (NO + 31) / 32;                      // sliced-ELLPACK chunks (at most, CW >= 32)
@@ -2798,15 +2813,21 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         else k_sell_width<64><<<wg, 256, 0, st>>>(d->orow, NO, NCs, swid);
         COMAP_LAUNCH_CHECK(ctx);
         COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(cub_tmp, scan_tb, swid, d->sbase, (int)(NCs + 1), st));
-        COMAP_CHECK(ctx, hipMemcpyAsync(&d->nsell, d->sbase + NCs, 8, hipMemcpyDeviceToHost, st));
     }
-    int32_t nonuni_h = 0, flags_h[2] = {0, 0};
-    COMAP_CHECK(ctx, hipMemcpyAsync(&d->nnz, d->orow + NO, 8, hipMemcpyDeviceToHost, st));
-    COMAP_CHECK(ctx, hipMemcpyAsync(&nonuni_h, nonuni, 4, hipMemcpyDeviceToHost, st));
-    COMAP_CHECK(ctx, hipMemcpyAsync(flags_h, nonfin, 8, hipMemcpyDeviceToHost, st));
+    // one read-back into a page-locked block (sizes + flags), one sync
+    struct PinnedWords {
+        int64_t *p = nullptr;
+        ~PinnedWords() { if (p) comap_pinned_free(p); }
+    } hw;
+    COMAP_CHECK(ctx, comap_pinned_alloc((void **)&hw.p, 8 * 8));
+    k_setup_sizes<<<1, 64, 0, st>>>(d->orow, NO, d->sell ? d->sbase : nullptr, NCs, nonuni, nonfin, counts);
+    COMAP_LAUNCH_CHECK(ctx);
+    COMAP_CHECK(ctx, hipMemcpyAsync(hw.p, counts, 5 * 8, hipMemcpyDeviceToHost, st));
     COMAP_CHECK(ctx, hipStreamSynchronize(st));
-    const int32_t nonfin_h = flags_h[0];
-    if (flags_h[1]) return comap_fail(ctx, -3, "pixel index out of range for the map (>= npix)");
+    d->nnz = hw.p[0];
+    if (d->sell) d->nsell = hw.p[1];
+    const int32_t nonuni_h = (int32_t)hw.p[2], nonfin_h = (int32_t)hw.p[3];
+    if (hw.p[4]) return comap_fail(ctx, -3, "pixel index out of range for the map (>= npix)");
     {
         const char *cfe = getenv("COMAP_DS_CF");             // 0: always the f64 entry weights
         d->cf = !nonuni_h && L <= 255 && !(cfe && cfe[0] == '0');
@@ -2941,11 +2962,10 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     }
     COMAP_LAUNCH_CHECK(ctx);
     d->walk = walk;
-    int64_t hc[2] = {0, 0};
-    COMAP_CHECK(ctx, hipMemcpyAsync(hc, counts, 16, hipMemcpyDeviceToHost, st));
+    COMAP_CHECK(ctx, hipMemcpyAsync(hw.p, counts, 16, hipMemcpyDeviceToHost, st));
     COMAP_CHECK(ctx, hipStreamSynchronize(st));
-    d->nnzp = hc[0];
-    d->nh = hc[1];
+    d->nnzp = hw.p[0];
+    d->nh = hw.p[1];
     own.d = nullptr;
     *out = d;
     return 0;
