@@ -328,6 +328,11 @@ def prep_flat(files, filelist, map_info, bands, use_gain_filter, offset_length, 
     # pinned staging (freed behind its copy): released without a host wait
     del keep_alive
     mark('release')
+    # countDataSize sizes every file for ALL selected feeds (COMAPData.py:163-187), but a
+    # file fills only the rows of the selected feeds it holds: the tail stays zero, as the
+    # reference's np.zeros arrays do (FlatArrays is uninitialised)
+    if last < out.n:
+        out.zero_range(last, out.n)
     return out
 
 

@@ -312,6 +312,27 @@ def test_gpu_prep_many_scans_vs_oracle(case_store, name):
             assert np.array_equal(a, b), k
 
 
+@pytest.mark.gpu
+def test_gpu_prep_selected_feeds_missing_from_file(case_store):
+    """A feed selection wider than a file's feeds (countDataSize sizes the arrays for every
+    selected feed, the file fills only the rows it holds): the unfilled tail is zeros and
+    cut like the reference's, so the outputs equal the oracle's (an uninitialised tail
+    once reached the map binning as garbage pixel ids)."""
+    from oracle import comapdata as oc
+    store, names = case_store
+    case = cc.CASES[list(cc.CASES)[0]]
+    feeds = list(cc.FEEDS) + [f for f in range(1, 20) if f not in cc.FEEDS][:3]
+    ref = oc.read_comap_data(names, store, map_info(case['map']), feeds=feeds, **case['kw'])
+    got = cd.read_comap_data(names, map_info(case['map']), feeds=feeds, store=store, **case['kw'])
+    for k, a, b in zip(cc.OUTPUTS, got, ref):
+        a, b = np.asarray(a), np.asarray(b)
+        assert a.shape == b.shape, k
+        if k in TRIG:
+            assert np.max(np.abs(a - b)) <= 1e-12 * max(np.max(np.abs(b)), 1.0), k
+        else:
+            assert np.array_equal(a, b), k
+
+
 def test_oracle_many_scans_runs(case_store):
     """The many-scan fixture is a real case for the oracle: several scans of each kind."""
     from oracle import comapdata as oc
