@@ -247,6 +247,13 @@ struct comap_l1_plan {
     int64_t *nanpos = nullptr;         // [nanpos_cap] cube element offsets the fill overwrote
     int64_t nanpos_cap = 0;
     int64_t *nanpos_n = nullptr;       // [1] entries used
+    // select_time over every (unit, band) pair, gated on the device by pass A's row flags
+    // (comap_l1_atmosphere enqueues it without waiting for pass A's NaN count)
+    int32_t *sel_pairs = nullptr;      // [U*4][2] (unit, band)
+    int64_t *sel_voff = nullptr;       // [U*4 + 1] offsets of each pair's valid mask
+    int32_t *sel_flag = nullptr;       // [U*4] pair has a non-finite sample in a fitted channel
+    uint8_t *sel_valid = nullptr;      // [sel_voff[U*4] + 1]
+    int sel_maxn = 0;
     // comap_l1_vane's hot/cold index lists: host arrays are copied into pinned staging
     // and uploaded asynchronously (no host wait); the event guards the staging reuse
     char *vane_pinned = nullptr, *vane_dev = nullptr;

@@ -291,20 +291,26 @@ __global__ void __launch_bounds__(256) k_moments(const float *__restrict__ tod, 
 // 994 fitted channels of the band are finite.  One workgroup per
 // (unit, band, 1024-sample tile) marks valid[t]; a second kernel recomputes
 // the fit sums of that (unit, band) over the valid samples.
+// The pairs: list[0 .. *count) of pair ids (grid-strided over blockIdx.y).
 __global__ void __launch_bounds__(256) k_select_time(const float *__restrict__ tod, const int32_t *__restrict__ units,
                                                      const int32_t *__restrict__ pairs, int64_t T,
-                                                     const int64_t *__restrict__ voff, uint8_t *__restrict__ valid)
+                                                     const int64_t *__restrict__ voff, uint8_t *__restrict__ valid,
+                                                     const int32_t *__restrict__ list,
+                                                     const int32_t *__restrict__ count)
 {
-    const int pr = blockIdx.y;
-    const int u = pairs[2 * pr], b = pairs[2 * pr + 1];
-    const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n) return;
-    const float *p = tod + (int64_t)(f * kBands + b) * kChannels * T + t0 + t;
-    bool ok = true;
-    for (int c = 10; c < 1014; ++c)
-        if (atmos_channel(c) && !isfinite(p[(int64_t)c * T])) ok = false;
-    valid[voff[pr] + t] = ok;
+    const int np = *count;
+    for (int li = blockIdx.y; li < np; li += gridDim.y) {
+        const int pr = list[li];
+        const int u = pairs[2 * pr], b = pairs[2 * pr + 1];
+        const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
+        const int t = blockIdx.x * blockDim.x + threadIdx.x;
+        if (t >= n) continue;
+        const float *p = tod + (int64_t)(f * kBands + b) * kChannels * T + t0 + t;
+        bool ok = true;
+        for (int c = 10; c < 1014; ++c)
+            if (atmos_channel(c) && !isfinite(p[(int64_t)c * T])) ok = false;
+        valid[voff[pr] + t] = ok;
+    }
 }
 
 // per (pair, channel): Sd, SAd over valid t -> fs[0/1][u*4096+b*1024+c];
@@ -314,9 +320,13 @@ __global__ void __launch_bounds__(256) k_masked_fit_sums(const float *__restrict
                                                          const int32_t *__restrict__ pairs, int64_t T,
                                                          const int64_t *__restrict__ voff,
                                                          const uint8_t *__restrict__ valid, int64_t UC,
-                                                         double *__restrict__ fs, double *__restrict__ ub)
+                                                         double *__restrict__ fs, double *__restrict__ ub,
+                                                         const int32_t *__restrict__ list,
+                                                         const int32_t *__restrict__ count)
 {
-    const int pr = blockIdx.y;
+    const int np = *count;
+    for (int li = blockIdx.y; li < np; li += gridDim.y) {
+    const int pr = list[li];
     const int u = pairs[2 * pr], b = pairs[2 * pr + 1];
     const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -345,6 +355,39 @@ __global__ void __launch_bounds__(256) k_masked_fit_sums(const float *__restrict
             o[0] = cn; o[1] = sa; o[2] = saa;
         }
     }
+    }   // listed pairs
+}
+
+// flag[u*4+b]: pass A found a non-finite sample in one of the band's fitted channels (the
+// (unit, band) pairs whose fit select_time restricts); one wave per pair
+__global__ void __launch_bounds__(256) k_pair_flags(const int32_t *__restrict__ rowbad, int npairs,
+                                                    int32_t *__restrict__ flag)
+{
+    const int lane = threadIdx.x & 63;
+    const int pr = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (pr >= npairs) return;
+    const int u = pr / kBands, b = pr % kBands;
+    const int32_t *rb = rowbad + (int64_t)u * kBC + b * kChannels;
+    bool any = false;
+    for (int c = lane; c < kChannels; c += 64) any |= atmos_channel(c) && rb[c] > 0;
+    any = __ballot(any) != 0ull;
+    if (lane == 0) flag[pr] = any ? 1 : 0;
+}
+
+// the flagged pairs in order (one wave): list[0 .. count)
+__global__ void k_pair_list(const int32_t *__restrict__ flag, int npairs, int32_t *__restrict__ list,
+                            int32_t *__restrict__ count)
+{
+    const int lane = threadIdx.x & 63;
+    int base = 0;
+    for (int i0 = 0; i0 < npairs; i0 += 64) {
+        const int i = i0 + lane;
+        const bool f = i < npairs && flag[i];
+        const unsigned long long m = __ballot(f);
+        if (f) list[base + __popcll(m & ((1ull << lane) - 1ull))] = i;
+        base += __popcll(m);
+    }
+    if (lane == 0) *count = base;
 }
 
 // ub[(u*4+b)] = unit airmass sums (NaN-free case: every sample is fitted)
@@ -409,9 +452,11 @@ __global__ void k_fit_from_median(const int32_t *__restrict__ units, const int32
 // AtmosphereRemoval.fit_atmosphere (Level1Averaging.py:197-227): the
 // block-diagonal spsolve is an independent 2x2 normal-equation solve per
 // channel: [[n, SA],[SA, SAA]] [o, a]^T = [Sd, SAd]^T.
+// fs_sel / sel (select_time): the (unit, band) pairs flagged in sel read their sums from fs_sel
 __global__ void k_atmos_fit(const int32_t *__restrict__ units, const double *__restrict__ ubs,
                             const double *__restrict__ fs, int64_t UC, int F, int U,
-                            double *__restrict__ fit)
+                            double *__restrict__ fit, const double *__restrict__ fs_sel = nullptr,
+                            const int32_t *__restrict__ sel = nullptr)
 {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= (int64_t)U * kBC) return;
@@ -423,7 +468,8 @@ __global__ void k_atmos_fit(const int32_t *__restrict__ units, const double *__r
     const double n = q[0], sa = q[1], saa = q[2];
     double o = NAN, a = NAN;
     if (atmos_channel(c) && n >= 100.0) {    // MINIMUM_CHUNK_SIZE (Level1Averaging.py:207-208)
-        const double sd = fs[i], sad = fs[UC + i];
+        const double *src = (sel && sel[(int64_t)u * kBands + b]) ? fs_sel : fs;
+        const double sd = src[i], sad = src[UC + i];
         const double det = n * saa - sa * sa;
         o = (saa * sd - sa * sad) / det;
         a = (n * sad - sa * sd) / det;
@@ -1486,7 +1532,8 @@ extern "C" int comap_l1_plan_destroy(comap_l1_plan *p)
     void *bufs[] = {p->units, p->tiles, p->tiles_b, p->gaps, p->airmass, p->unit_sums, p->mom,
                     p->nan_count, p->alpha, p->nf, p->bsum, p->mb, p->mf, p->ssum, p->sdm, p->gw,
                     p->gmode, p->kap, p->dsum, p->xreg, p->dG, p->rowbad, p->ubs, p->fitsum, p->oa,
-                    p->flag, p->dlist, p->dcnt, p->dw, p->nanpos, p->nanpos_n, p->vane_dev};
+                    p->flag, p->dlist, p->dcnt, p->dw, p->nanpos, p->nanpos_n, p->vane_dev,
+                    p->sel_pairs, p->sel_voff, p->sel_flag, p->sel_valid};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (int g = 0; g < comap_l1_plan::kMaxGroups; ++g) {
@@ -1583,53 +1630,58 @@ extern "C" int comap_l1_atmosphere(comap_l1_plan *p, const int32_t *const_el_uni
     p->pre_a_valid = false;            // a later vane call orders itself after this stage
     comap_ctx *ctx = p->ctx;
     hipStream_t st = ctx->stream;
-    int rc = p->prefetched ? wait_moments(p) : run_moments(p);   // pass A, unless comap_l1_prefetch ran it
+    // pass A, unless comap_l1_prefetch queued it; its NaN count is not waited for here: the
+    // NaN path below is gated on the device by pass A's row flags, so this stage queues
+    // behind pass A with no host round trip (comap_l1_average reads the count)
+    int rc = p->prefetched ? 0 : launch_moments(p);
     p->prefetched = false;
     if (rc) return rc;
     const int64_t UC = (int64_t)p->U * kBC;
     const int UB = p->U * kBands;
     k_ub_from_units<<<(UB + 255) / 256, 256, 0, st>>>(p->unit_sums, p->U, p->ubs);
     COMAP_LAUNCH_CHECK(ctx);
-    const double *fs = p->mom;
-    if (p->nan_total > 0) {
-        // select_time: (unit, band) pairs with a non-finite sample in a fitted channel
-        std::vector<int32_t> rb;
-        if ((rc = fetch_rowbad(p, rb))) return rc;
-        std::vector<int32_t> pairs;
-        std::vector<int64_t> voff(1, 0);
+    // select_time: the (unit, band) pairs with a non-finite sample in a fitted channel get
+    // their fit sums over the samples where every fitted channel is finite (into fitsum);
+    // every other pair keeps pass A's sums
+    if (!p->sel_pairs) {
+        std::vector<int32_t> pairs(2 * (size_t)UB);
+        std::vector<int64_t> voff(UB + 1, 0);
+        int maxn = 0;
         for (int u = 0; u < p->U; ++u)
             for (int b = 0; b < kBands; ++b) {
-                bool any = false;
-                for (int c = 0; c < kChannels && !any; ++c)
-                    any = atmos_channel_host(c) && rb[(size_t)u * kBC + b * kChannels + c] > 0;
-                if (!any) continue;
-                pairs.push_back(u);
-                pairs.push_back(b);
-                voff.push_back(voff.back() + p->units_h[4 * u + 3]);
+                const int pr = u * kBands + b;
+                pairs[2 * pr] = u;
+                pairs[2 * pr + 1] = b;
+                voff[pr + 1] = voff[pr] + p->units_h[4 * u + 3];
+                maxn = std::max(maxn, p->units_h[4 * u + 3]);
             }
-        if (!pairs.empty()) {
-            const int np = (int)pairs.size() / 2;
-            int32_t *dpairs = nullptr;
-            int64_t *dvoff = nullptr;
-            uint8_t *valid = nullptr;
-            DevTemps tmp(st);
-            COMAP_CHECK(ctx, tmp.alloc(&dpairs, pairs.size()));
-            COMAP_CHECK(ctx, tmp.alloc(&dvoff, voff.size()));
-            COMAP_CHECK(ctx, tmp.alloc(&valid, voff.back() + 1));
-            COMAP_CHECK(ctx, hipMemcpyAsync(dpairs, pairs.data(), 4 * pairs.size(), hipMemcpyHostToDevice, st));
-            COMAP_CHECK(ctx, hipMemcpyAsync(dvoff, voff.data(), 8 * voff.size(), hipMemcpyHostToDevice, st));
-            COMAP_CHECK(ctx, hipMemcpyAsync(p->fitsum, p->mom, 16 * UC, hipMemcpyDeviceToDevice, st));
-            int maxn = 0;
-            for (int k = 0; k < np; ++k) maxn = std::max(maxn, p->units_h[4 * pairs[2 * k] + 3]);
-            k_select_time<<<dim3((maxn + 255) / 256, np), 256, 0, st>>>(p->tod, p->units, dpairs, p->T, dvoff, valid);
-            COMAP_LAUNCH_CHECK(ctx);
-            k_masked_fit_sums<<<dim3(kChannels / 4, np), 256, 0, st>>>(p->tod, p->airmass, p->units, dpairs, p->T,
-                                                                       dvoff, valid, UC, p->fitsum, p->ubs);
-            COMAP_LAUNCH_CHECK(ctx);
-            fs = p->fitsum;
-        }
+        COMAP_CHECK(ctx, hipMalloc((void **)&p->sel_pairs, 4 * pairs.size()));
+        COMAP_CHECK(ctx, hipMalloc((void **)&p->sel_voff, 8 * voff.size()));
+        COMAP_CHECK(ctx, hipMalloc((void **)&p->sel_flag, 4 * (2 * (size_t)UB + 1)));   // flags, list, count
+        COMAP_CHECK(ctx, hipMalloc((void **)&p->sel_valid, (size_t)voff.back() + 1));
+        COMAP_CHECK(ctx, comap_upload(p->sel_pairs, pairs.data(), 4 * pairs.size(), st));
+        COMAP_CHECK(ctx, comap_upload(p->sel_voff, voff.data(), 8 * voff.size(), st));
+        p->sel_maxn = maxn;
     }
-    PROF(p, KV_ATMOS_FIT, k_atmos_fit<<<(UC + 255) / 256, 256, 0, st>>>(p->units, p->ubs, fs, UC, p->F, p->U, fit));
+    int32_t *plist = p->sel_flag + UB, *pcount = p->sel_flag + 2 * UB;
+    k_pair_flags<<<(UB + 3) / 4, 256, 0, st>>>(p->rowbad, UB, p->sel_flag);
+    COMAP_LAUNCH_CHECK(ctx);
+    k_pair_list<<<1, 64, 0, st>>>(p->sel_flag, UB, plist, pcount);
+    COMAP_LAUNCH_CHECK(ctx);
+    if (p->sel_maxn > 0) {
+        // (a NaN-free cube lists no pair: both kernels return at once)
+        const unsigned gy = (unsigned)std::min(UB, 16);    // a few blocks: the listed pairs are strided
+        k_select_time<<<dim3((p->sel_maxn + 255) / 256, gy), 256, 0, st>>>(p->tod, p->units, p->sel_pairs, p->T,
+                                                                           p->sel_voff, p->sel_valid, plist, pcount);
+        COMAP_LAUNCH_CHECK(ctx);
+        k_masked_fit_sums<<<dim3(kChannels / 4, gy), 256, 0, st>>>(p->tod, p->airmass, p->units, p->sel_pairs, p->T,
+                                                                   p->sel_voff, p->sel_valid, UC, p->fitsum, p->ubs,
+                                                                   plist, pcount);
+        COMAP_LAUNCH_CHECK(ctx);
+    }
+    const double *fs = p->mom;
+    PROF(p, KV_ATMOS_FIT, k_atmos_fit<<<(UC + 255) / 256, 256, 0, st>>>(p->units, p->ubs, fs, UC, p->F, p->U, fit,
+                                                                        p->fitsum, p->sel_flag));
     COMAP_LAUNCH_CHECK(ctx);
     if (n_const_el > 0) {
         // constant-elevation scans: (nanmedian over the scan, 0) for every channel
