@@ -1156,13 +1156,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) k
 {
 #pragma clang fp contract(off)
     constexpr int CAP = 64 * M;
-    __shared__ double spl[4][CAP * 2 * NB];
-    __shared__ uint32_t smk[4][CAP];
+    // per member slot, 3 NB doubles: w, tod w and 1 per band, each 0 where the band does not
+    // keep the member's offset -- adding +0 leaves a sum that never holds -0 unchanged, so
+    // lane l < 3 NB runs its ordered sum as one unconditional chain over column l
+    __shared__ double spl[4][CAP * 3 * NB];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     double *pl = spl[wv];
-    uint32_t *mk = smk[wv];
     const int kind = lane / NB, b = lane % NB;     // this lane's ordered sum (lanes < 3 NB)
-    const int col = kind == 2 ? 0 : kind * NB + b;
     // xcd: each XCD walks one contiguous eighth of the pixels
     // the non-empty rows only (k_hit_flags wrote the empty ones): row i of nh = counts[1]
     const int64_t lb = xcd_block(blockIdx.x, gridDim.x, xcd);
@@ -1266,23 +1266,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) k
                             const int64_t on = perm ? (int64_t)perm[kj] : (int64_t)kj;
                             wv = w[(int64_t)bb * N + on * L + bitpos];
                         }
-                        pl[t * 2 * NB + bb] = wv;
-                        pl[t * 2 * NB + NB + bb] = pv[bb];
+                        const bool kept = (kbj >> bb) & 1u;
+                        pl[t * 3 * NB + bb] = kept ? wv : 0.0;
+                        pl[t * 3 * NB + NB + bb] = kept ? pv[bb] : 0.0;
+                        pl[t * 3 * NB + 2 * NB + bb] = kept ? 1.0 : 0.0;
                     }
-                    mk[t] = kbj;
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // the chunk, before other lanes read it
             if (lane < 3 * NB) {
-                if (kind == 2) {
-                    for (int t = 0; t < total; ++t) acc = ((mk[t] >> b) & 1u) ? acc + 1.0 : acc;
-                } else {
 #pragma unroll 8
-                    for (int t = 0; t < total; ++t) {
-                        const double v = pl[t * 2 * NB + col];
-                        acc = ((mk[t] >> b) & 1u) ? acc + v : acc;
-                    }
-                }
+                for (int t = 0; t < total; ++t) acc += pl[t * 3 * NB + lane];
             }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // read before the next chunk overwrites
             c += ntake;
