@@ -567,6 +567,40 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
 #pragma unroll
         for (int c = 0; c < K; ++c) mem[m][c] = 0ull;
     }
+    if constexpr (K == 1) {
+        // one sample per lane: the groups by an LDS hash table instead of the leader loop's
+        // ~30 dependent readlane / ballot rounds per offset -- every lane inserts its pixel
+        // (linear probing, compare-and-swap), the slot keeps the smallest lane (the first
+        // occurrence: the group's head, as the leader loop picks it) and the OR of the
+        // members' lane bits.  Same heads, same masks.
+        constexpr int kSlots = 128;
+        constexpr int32_t kEmpty = INT32_MIN + 1;
+        __shared__ int32_t hkey[4][kSlots], hmin[4][kSlots];
+        __shared__ unsigned long long hmsk[4][kSlots];
+        int32_t *hk = hkey[threadIdx.x >> 6], *hm = hmin[threadIdx.x >> 6];
+        unsigned long long *hb = hmsk[threadIdx.x >> 6];
+#pragma unroll
+        for (int z = lane; z < kSlots; z += 64) {
+            hk[z] = kEmpty;
+            hm[z] = 64;
+            hb[z] = 0ull;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        const bool valid = lane < L;
+        int slot = (int)(((uint32_t)q[0] * 2654435761u) >> 25);
+        if (valid) {
+            for (;;) {
+                const int32_t old = atomicCAS(&hk[slot], kEmpty, q[0]);
+                if (old == kEmpty || old == q[0]) break;
+                slot = (slot + 1) & (kSlots - 1);
+            }
+            atomicMin(&hm[slot], lane);
+            atomicOr(&hb[slot], 1ull << lane);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        head[0] = valid && hm[slot] == lane;
+        mem[0][0] = head[0] ? hb[slot] : 0ull;
+    } else {
 #pragma unroll
     for (int m = 0; m < K; ++m) {
         while (rem[m]) {
@@ -587,6 +621,7 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
             }
         }
     }
+    }   // K > 1: the leader loop
     // count pass: the count-form test first -- per band, every non-zero weight finite and
     // equal to the first one (ballot + readlane) -- with the non-zero masks
     double wi[K][NB], refb[NB];
