@@ -917,24 +917,15 @@ using Sort9Config = rocprim::radix_sort_config<
                                         rocprim::block_radix_rank_algorithm::match>,
     0>;
 
-template <unsigned BS, unsigned IPT>
-using Sort8Config = rocprim::radix_sort_config<
-    rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<BS, IPT>, rocprim::kernel_config<BS, IPT>, 8>, 0>;
-
-// variant (measurement knob COMAP_DS_TSORT for the transpose): 0 hipcub's default, 1 / 2 / 3
-// rocprim onesweep with 8-bit digits and 256 x 16 / 256 x 8 / 256 x 20 (threads x items)
-hipError_t sort_pairs_i32(int variant, void *tmp, size_t &bytes, const int32_t *kin, int32_t *kout,
+// (rocprim onesweep with 8-bit digits at 256 x 16 / 256 x 8 / 256 x 20 threads x items ran
+// the transpose in 1.52 / 2.92 / 1.29 ms against hipcub's 0.43, r04ts: removed)
+hipError_t sort_pairs_i32(bool nine, void *tmp, size_t &bytes, const int32_t *kin, int32_t *kout,
                           const int32_t *vin, int32_t *vout, int64_t n, int end_bit, hipStream_t st)
 {
-    const unsigned un = (unsigned)n, eb = (unsigned)end_bit;
-    switch (variant) {
-    case 9: return rocprim::radix_sort_pairs<Sort9Config>(tmp, bytes, kin, kout, vin, vout, un, 0u, eb, st);
-    case 1: return rocprim::radix_sort_pairs<Sort8Config<256, 16>>(tmp, bytes, kin, kout, vin, vout, un, 0u, eb, st);
-    case 2: return rocprim::radix_sort_pairs<Sort8Config<256, 8>>(tmp, bytes, kin, kout, vin, vout, un, 0u, eb, st);
-    case 3: return rocprim::radix_sort_pairs<Sort8Config<256, 20>>(tmp, bytes, kin, kout, vin, vout, un, 0u, eb, st);
-    default: return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, kin, kout, vin, vout, (int)n, 0, end_bit, st);
-    }
+    if (nine)
+        return rocprim::radix_sort_pairs<Sort9Config>(tmp, bytes, kin, kout, vin, vout, (unsigned)n, 0u,
+                                                      (unsigned)end_bit, st);
+    return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, kin, kout, vin, vout, (int)n, 0, end_bit, st);
 }
 
 // row[p] = first sorted position with key >= p, p in [0, npix]
@@ -2745,15 +2736,10 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         const char *v = getenv("COMAP_DS_SORT9");        // 0: hipcub's radix sort for the offset sort too
         return !(v && v[0] == '0');
     }();
-    static const int tsort = [] {
-        const char *v = getenv("COMAP_DS_TSORT");
-        const int x = v ? atoi(v) : 0;
-        return (x >= 0 && x <= 3) ? x : 0;
-    }();
-    (void)sort_pairs_i32(tsort, nullptr, sort_tb, nullptr, nullptr, nullptr, nullptr, N, end_bit, st);
+    (void)sort_pairs_i32(false, nullptr, sort_tb, nullptr, nullptr, nullptr, nullptr, N, end_bit, st);
     {
         size_t tb9 = 0;       // the spatial offset sort (NO pairs)
-        (void)sort_pairs_i32(nine ? 9 : 0, nullptr, tb9, nullptr, nullptr, nullptr, nullptr, NO, end_bit, st);
+        (void)sort_pairs_i32(nine, nullptr, tb9, nullptr, nullptr, nullptr, nullptr, NO, end_bit, st);
         sort_tb = std::max(sort_tb, tb9);
     }
     size_t sort64_tb = 0;   // the count form's transpose: (pixel, u64 offset|counts) pairs
@@ -2813,7 +2799,7 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         k_offset_keys<<<(unsigned)std::min<int64_t>((NO + 3) / 4, 65536), 256, 0, st>>>(pix, NO, L, npix, ekey, eval);
         COMAP_LAUNCH_CHECK(ctx);
         size_t tb = cub_tb;
-        COMAP_CHECK(ctx, sort_pairs_i32(nine ? 9 : 0, cub_tmp, tb, ekey, ekey2, eval, d->perm, NO, end_bit, st));
+        COMAP_CHECK(ctx, sort_pairs_i32(nine, cub_tmp, tb, ekey, ekey2, eval, d->perm, NO, end_bit, st));
     }
     // ---- 2. count pass (+ the count-form test: non-zero weights uniform per offset and band)
     COMAP_CHECK(ctx, hipMemsetAsync(nonuni, 0, 4, st));
@@ -2953,7 +2939,7 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     // ---- 4. pixel-major transpose (stable: offset order within a pixel)
     if (walk) {
         size_t tb = cub_tb;
-        COMAP_CHECK(ctx, sort_pairs_i32(tsort, cub_tmp, tb, ekey, ekey2, evn, evn2, d->nnz, end_bit, st));
+        COMAP_CHECK(ctx, sort_pairs_i32(false, cub_tmp, tb, ekey, ekey2, evn, evn2, d->nnz, end_bit, st));
     } else if (d->cf) {
         COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(cub_tmp, sort64_tb, ekey, ekey2, epay, epay2, (int)d->nnz,
                                                             0, end_bit, st));
