@@ -63,6 +63,8 @@ def parse():
     ap.add_argument('--no-destriper', action='store_true')
     ap.add_argument('--destriper-iters', type=int, default=100)
     ap.add_argument('--c5-obs', type=int, default=8, help='observations per GPU in the C5 destriper leg (0: skip)')
+    ap.add_argument('--c5-field-obs', type=int, default=64,
+                    help='observations of the C5 field solved as ONE system over all ranks (configs[4]; 0: skip)')
     ap.add_argument('--check', action='store_true', help='compare one unit against the CPU oracle')
     ap.add_argument('--no-e2e', action='store_true', help='skip the host-cube -> host-Level-2 leg')
     ap.add_argument('--no-chain', action='store_true', help='skip the L1 -> L2 -> maps chain leg')
@@ -386,8 +388,8 @@ def destriper_c5_leg(n_obs, niter, device, world, rank, n_bands=1):
     L, npix = 50, 480 * 480
     pix, tod, w = synthetic.destriper_inputs_device(n_obs, offset_length=L, device=device, seed=1000 + rank,
                                                     n_bands=n_bands)
-    _timed_setup(pix, tod, w, L, npix, device=device, map_shape=(480, 480))        # warm (first use of these sizes)
-    prob, setup = _timed_setup(pix, tod, w, L, npix, device=device, map_shape=(480, 480))
+    _timed_setup(pix, tod, w, L, npix, device=device)        # warm (first use of these sizes)
+    prob, setup = _timed_setup(pix, tod, w, L, npix, device=device)
     prob.solve(threshold=0.0, niter=3)   # warm (graph capture, RCCL communicators)
     torch.cuda.synchronize()
     if world > 1:
@@ -407,7 +409,12 @@ def destriper_c5_leg(n_obs, niter, device, world, rank, n_bands=1):
     ms = dt / it * 1e3
     ms_band = ms / n_bands
     op_bytes = operator_bytes(prob, NO, n_bands)
-    return {'config': f'C5: {n_obs} obs x 19 feeds x 180000 samples per GPU, {n_bands} band(s) per solve, L={L}, '
+    comm = None
+    if world > 1:       # the measured per-iteration all-reduce time and bytes (rankplan's alpha / beta)
+        ta = D.TimedAllreduce()
+        prob.solve(threshold=0.0, niter=20, allreduce=ta)
+        comm = ta.summary(20)
+    return {'comm_rank0': comm, 'config': f'C5: {n_obs} obs x 19 feeds x 180000 samples per GPU, {n_bands} band(s) per solve, L={L}, '
                       f'480x480 CAR, {niter} CG iterations (no early exit), {world} rank(s)',
             'cg_iters_per_s': it / dt, 'band_iters_per_s': n_bands * it / dt, 'ms_per_iter': ms,
             'ms_per_band_iter': ms_band, 'iters': res['iters'],
@@ -421,8 +428,107 @@ def destriper_c5_leg(n_obs, niter, device, world, rank, n_bands=1):
             'survey_bytes_per_band_iter_per_gpu': algo,
             'work_saving_vs_survey_bytes': algo * n_bands / max(op_bytes, 1),
             'operator_bytes_per_iter': op_bytes, 'entry_bytes': prob.entry_bytes(),
-            'sell_entries': prob.sell_entries(), 'tile_segments': prob.tile_segments(),
+            'sell_entries': prob.sell_entries(),
             'operator_roofline_frac': op_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+
+
+def allreduce_probe(dev, sizes, reps=30):
+    """Measured RCCL all-reduce cost on this node at the CG's message sizes (bytes): per
+    size the mean of ``reps`` back-to-back collectives between device syncs, then the
+    least-squares alpha (us) + bytes / beta (GB/s) line that mapmaking/rankplan.py's
+    cost model takes (scripts/rankplan_calibrate.py turns these fields of the SCALE runs
+    into its table).  Collective: every rank calls it."""
+    import torch
+    import torch.distributed as dist
+    pts = []
+    for b in sizes:
+        t = torch.zeros(max(1, int(b) // 8), dtype=torch.float64, device=dev)
+        for _ in range(3):
+            dist.all_reduce(t)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            dist.all_reduce(t)
+        torch.cuda.synchronize()
+        us = (time.perf_counter() - t0) / reps * 1e6
+        e = torch.tensor([us], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        pts.append({'bytes': int(t.numel() * 8), 'us': float(e.item())})
+    x = np.array([p['bytes'] for p in pts], float)
+    y = np.array([p['us'] for p in pts], float)
+    A = np.stack([np.ones_like(x), x], axis=1)
+    (alpha, slope), *_ = np.linalg.lstsq(A, y, rcond=None)
+    return {'n_ranks': dist.get_world_size(), 'backend': dist.get_backend(), 'reps': reps, 'points': pts,
+            'alpha_us': float(alpha), 'beta_GBs': float(1e-3 / slope) if slope > 0 else None}
+
+
+def destriper_c5_field_leg(n_obs, niter, device, world, rank, n_bands=4):
+    """configs[4] as stated: n_obs (64) synthetic observations x 19 feeds x 180,000 samples
+    co-added into ONE 480 x 480 1' CAR field map and solved as one system (run_destriper.py:
+    131-189 puts every rank's files into one map).  On N ranks the observations are split
+    N ways (rank r: observations [r n / N, (r + 1) n / N)), so total work is fixed
+    ("scaling": strong): the map numerator (compacted to the hit pixels) and the CG block
+    partials are all-reduced over RCCL every iteration.  Reports the set-up, ms per CG
+    iteration (fixed niter, no early exit; the max over ranks) and the converged solve
+    (threshold 1e-6); with N > 1 also the measured per-iteration all-reduce time and bytes
+    (TimedAllreduce) and the RCCL alpha / beta probe at the CG's message sizes."""
+    import torch
+    import torch.distributed as dist
+    from comapreduce_amd import synthetic
+    from comapreduce_amd.mapmaking import destriper as D
+    L, npix = 50, 480 * 480
+    lo, hi = n_obs * rank // world, n_obs * (rank + 1) // world
+    pix, tod, w = synthetic.destriper_inputs_device(hi - lo, offset_length=L, device=device, seed=5000,
+                                                    n_bands=n_bands, obs0=lo)
+    _timed_setup(pix, tod, w, L, npix, device=device)          # warm (first use of these sizes)
+    prob, setup = _timed_setup(pix, tod, w, L, npix, device=device)
+    N_local = int(pix.numel())
+    del pix, tod, w
+    prob.solve(threshold=0.0, niter=3)   # warm
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    conv, conv_s = _timed_solve(prob, 1e-6, 100)
+    if world > 1:
+        dist.barrier()
+    res, dt = _timed_solve(prob, 0.0, niter)
+    it = max(max(res['iters']) if n_bands > 1 else res['iters'], 1)
+    times = [dt, setup, conv_s]
+    if world > 1:
+        e = torch.tensor(times, device='cuda', dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        times = [float(v) for v in e.tolist()]
+    dt, setup, conv_s = times
+    N = N_local
+    if world > 1:
+        nt = torch.tensor([N_local], device='cuda', dtype=torch.int64)
+        dist.all_reduce(nt)
+        N = int(nt.item())
+    out = {'config': f'configs[4]: {n_obs} obs x 19 feeds x 180000 samples co-added into ONE 480x480 CAR field map, '
+                     f'{n_bands} bands batched, L={L}, split over {world} rank(s) by observation (strong scaling), '
+                     f'{niter} CG iterations (no early exit)',
+           'n_samples_per_band': N, 'n_offsets': N // L, 'n_samples_rank0': N_local,
+           'setup_ms': setup * 1e3, 'ms_per_iter': dt / it * 1e3, 'cg_iters_per_s': it / dt,
+           'band_iters_per_s': n_bands * it / dt, 'iters': res['iters'],
+           'converged': {'threshold': 1e-6, 'iters': conv['iters'], 'solve_ms': conv_s * 1e3,
+                         'setup_plus_solve_ms': (setup + conv_s) * 1e3},
+           'scaling': 'strong', 'nnz_rank0': prob.nnz(), 'entry_bytes': prob.entry_bytes()}
+    if world == 1:
+        op_bytes = operator_bytes(prob, N // L, n_bands)
+        out['operator_bytes_per_iter'] = op_bytes
+        out['operator_roofline_frac'] = op_bytes / (dt / it) / 1e9 / HBM_PEAK_GBS
+    else:
+        ta = D.TimedAllreduce()
+        prob.solve(threshold=0.0, niter=20, allreduce=ta)
+        out['comm_rank0'] = ta.summary(20)
+        nb = 4 if n_bands == 3 else n_bands
+        nmap = int(prob.hit_index.numel()) if prob.hit_index is not None else npix
+        out['allreduce_probe'] = allreduce_probe(torch.device('cuda', device),
+                                                 [8 * nb, 8 * nb * 1024, 8 * nb * nmap, 1 << 20])
+    del prob, res, conv
+    torch.cuda.empty_cache()
+    return out
 
 
 def pointing_device(data, dev):
@@ -637,10 +743,13 @@ def main():
         level2 = reduce_step(data, device)
     kprof = obs.profile_collect()
     obs.profile(False)
+    rank_ms = None
     if world > 1:
         e = torch.tensor([elapsed], device='cuda', dtype=torch.float64)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
+        parts = [torch.zeros_like(e) for _ in range(world)]
+        dist.all_gather(parts, e)               # every rank's own step time (the shard balance)
+        rank_ms = [float(p.item()) / args.steps * 1e3 for p in parts]
+        elapsed = max(float(p.item()) for p in parts)
 
     frac = obs.pass_fractions()
     vane_search_ms = getattr(obs, 'last_vane_search_ms', None)
@@ -667,6 +776,12 @@ def main():
         c5 = destriper_c5_leg(args.c5_obs, args.destriper_iters, device, world, rank)
         torch.cuda.empty_cache()
         c5['bands4'] = destriper_c5_leg(args.c5_obs, args.destriper_iters, device, world, rank, n_bands=4)
+    c5f = None
+    if not args.no_destriper and args.c5_field_obs > 0:
+        if c5 is None:
+            del data, level2, obs
+        torch.cuda.empty_cache()
+        c5f = destriper_c5_field_leg(args.c5_field_obs, args.destriper_iters, device, world, rank)
 
     e2e = None
     if not args.no_e2e and world == 1:
@@ -742,6 +857,10 @@ def main():
             line['destriper'] = dstr
         if c5 is not None:
             line['destriper_c5'] = c5
+        if c5f is not None:
+            line['destriper_c5_field'] = c5f
+        if rank_ms is not None:
+            line['rank_ms_per_step'] = rank_ms
         if chain is not None:
             line['chain_l1_to_maps'] = chain
         if e2e is not None:

@@ -81,8 +81,6 @@ _SIGS = {
     'comap_destripe_nnz': (c_int, [c_void_p, P_int64, P_int64]),
     'comap_destripe_entry_bytes': (ctypes.c_int32, [c_void_p]),
     'comap_destripe_sell_entries': (c_int64, [c_void_p]),
-    'comap_destripe_tiles': (c_int, [c_void_p, c_int64]),
-    'comap_destripe_tile_segments': (c_int64, [c_void_p]),
     'comap_destripe_local_maps': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     'comap_destripe_bin': (c_int, [c_void_p, c_void_p, c_int32, c_void_p]),
     'comap_destripe_project': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -231,6 +229,29 @@ def retry_oom(fn, *args, **kw):
             raise
         trim_caches()
         return fn(*args, **kw)
+
+
+POISON = os.environ.get('COMAP_POISON') == '1'
+
+
+def device_empty(shape, dtype, device):
+    """Uninitialised device tensor for an output a kernel writes in full: torch.empty,
+    retried once after trimming the library's cached temporaries on an out-of-memory
+    (the cache may hold memory torch's allocator cannot see).  COMAP_POISON=1 (debug)
+    fills it with 0xff bytes -- NaN for floats, -1 for integers -- as the library does
+    its own temporaries, so an element no kernel wrote shows up in the results."""
+    import torch
+    t = retry_oom(torch.empty, shape, dtype=dtype, device=device)
+    if POISON:
+        if t.is_floating_point():
+            t.fill_(float('nan'))
+        elif t.dtype == torch.bool:
+            t.fill_(True)
+        elif t.dtype == torch.uint8:
+            t.fill_(255)
+        else:
+            t.fill_(-1)
+    return t
 
 
 def host_empty(shape, dtype='float64'):

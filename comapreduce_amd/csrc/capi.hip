@@ -129,8 +129,22 @@ std::shared_ptr<hipEvent_t> record_use(hipStream_t st)
 bool make_safe(const LastUse &u, hipStream_t st)
 {
     if (!u.ev || u.st == st) return true;            // idle, or same stream: stream order
-    if (capturing(st)) return hipEventQuery(*u.ev) == hipSuccess;   // no cross-stream edge into a graph
-    return hipStreamWaitEvent(st, *u.ev, 0) == hipSuccess;
+    if (!*u.ev) return false;                        // freed under capture: its own stream only
+    // no cross-stream edge into a graph: under capture only completed blocks are reused
+    const hipError_t e = capturing(st) ? hipEventQuery(*u.ev) : hipStreamWaitEvent(st, *u.ev, 0);
+    if (e == hipSuccess) return true;
+    (void)hipGetLastError();      // NotReady / a failed wait must not surface in a later launch check
+    return false;
+}
+// COMAP_POISON=1 (debug): every temporary block handed out is filled with 0xff bytes (NaN
+// for f64 / f32, -1 for integers), so a kernel that reads what no kernel wrote shows it
+bool poison_on()
+{
+    static const bool on = [] {
+        const char *e = getenv("COMAP_POISON");
+        return e && e[0] == '1';
+    }();
+    return on;
 }
 }  // namespace
 
@@ -151,7 +165,7 @@ hipError_t comap_tmp_alloc(void **p, size_t bytes, hipStream_t st)
                 v.erase(v.begin() + (std::ptrdiff_t)i);
                 c.cached[dev] -= cls;
                 c.live[*p] = {dev, cls, st};
-                return hipSuccess;
+                return poison_on() ? hipMemsetAsync(*p, 0xff, cls, st) : hipSuccess;
             }
         }
     }
@@ -165,6 +179,7 @@ hipError_t comap_tmp_alloc(void **p, size_t bytes, hipStream_t st)
         std::lock_guard<std::mutex> lock(c.mu);
         c.live[*p] = {dev, cls, st};
     }
+    if (e == hipSuccess && poison_on()) e = hipMemsetAsync(*p, 0xff, cls, st);
     return e;
 }
 
@@ -348,11 +363,14 @@ hipError_t comap_upload(void *dst_dev, const void *src_host, size_t bytes, hipSt
         std::lock_guard<std::mutex> lock(sp.mu);
         for (size_t i = 0; i < sp.idle.size(); ++i) {
             StageBlock &c = sp.idle[i];
-            if (c.bytes >= bytes && (!c.ev || hipEventQuery(c.ev) == hipSuccess)) {
-                b = c;
-                sp.idle.erase(sp.idle.begin() + (std::ptrdiff_t)i);
-                break;
+            if (c.bytes < bytes) continue;
+            if (c.ev && hipEventQuery(c.ev) != hipSuccess) {
+                (void)hipGetLastError();          // NotReady is not an error of the next launch
+                continue;
             }
+            b = c;
+            sp.idle.erase(sp.idle.begin() + (std::ptrdiff_t)i);
+            break;
         }
     }
     if (!b.p) {

@@ -11,8 +11,9 @@
 //     num = W x               num_p = sum_{e in pixel row p} s_e x_{o(e)}
 //     m   = num / h           (m_p = num_p where h_p == 0, as share_map)
 //     y_o = ws_o x_o - sum_{e in offset row o} s_e m_{p(e)}      (op_Z + F^T W)
-// Off-map samples (pixel -1) are never binned but gather m[npix-1], the
-// reference's m[-1] wrap (Destriper.py:211).  One CG iteration streams
+// Off-map samples (negative pixel ids p >= -npix) are never binned but gather m[npix + p],
+// numpy's index wrap in the reference's m[pointing] (Destriper.py:211; -1 reads the last
+// pixel); ids < -npix are rejected as numpy raises there.  One CG iteration streams
 // 2 nnz entries instead of 6 N samples; all reductions are fixed-order
 // (deterministic).  The sample-level maps (weight map h, hits, naive
 // numerator sum w tod) are summed per pixel in sample order after a stable
@@ -85,29 +86,7 @@ struct comap_destriper {
     // column-major -- entry j of lane l at sbase[c] + 64 j + l -- so a lane streams its row
     // with coalesced loads, no row-pointer load and no cross-lane reduction
     bool sell = false;
-    int sell_u = 8;            // entry loads in flight per lane
-    bool bin_xcd = false;      // XCD-contiguous block order of the bin (COMAP_DS_BXCD)
-    bool proj_xcd = false;     // ... of the sliced-ELLPACK projection (COMAP_DS_PXCD)
-    bool ds_nt = false;        // non-temporal entry loads in the bin and the SELL projection (COMAP_DS_NT)
-    bool sell_pre = false;     // SELL projection: the lane's x / wbar / ws loaded before its row (COMAP_DS_SPRE)
-    int sell_cw = 64;          // offsets per SELL chunk: 64, or 32 for the 4-band lane-pair kernel
-    bool bin_pairs = false;    // 4 bands: lane-pair bin (COMAP_DS_BPAIR)
-    // map-tile projection (comap_destripe_tiles): the offset rows split by map tile; a
-    // workgroup stages one tile of m in LDS and sums every (offset, tile) segment from
-    // there, a combine pass adds each offset's segments in tile order
-    bool walk = false;                 // sample-level maps by the member-mask walk (set-up)
-    bool tiles = false;
-    int64_t nx = 0, ntx = 0, nty = 0;
-    int tile_w = 0, tile_h = 0;        // tile width / height in pixels
-    int64_t nseg = 0, nchunk_t = 0, nwg_t = 0;
-    uint64_t *tent = nullptr;          // [chunk slots] hi32: local pixel (0xffffffff: padding), lo32: packed counts
-    double *tentw = nullptr;           // [chunk slots][nb] f64 weights (full form)
-    int64_t *tcbase = nullptr;         // [nchunk_t + 1] chunk slot starts
-    int32_t *tslot = nullptr;          // [nchunk_t * 64] partial slot of each chunk lane (-1: none)
-    int32_t *twg = nullptr;            // [nwg_t][2] (tile, first chunk), chunks of one tile per workgroup
-    int32_t *tcend = nullptr;          // [ntiles] one past the tile's last chunk
-    int64_t *pstart = nullptr;         // [NO + 1] an offset's partial slots
-    double *tpart = nullptr;           // [nseg][nb] per-(offset, tile) partial sums
+    bool walk = false;         // sample-level maps by the member-mask walk (set-up)
     int64_t nsell = 0;         // padded entries
     int64_t *sbase = nullptr;  // [NC + 1]
     int32_t *spix = nullptr;   // [nsell] pixel, -1 off-map, kSellPad padding
@@ -170,31 +149,6 @@ __device__ __forceinline__ void ldb(const double *__restrict__ p, double (&v)[NB
     }
 }
 
-// streamed-once operands (the operator's entries): NT = non-temporal loads, which do not
-// allocate in L2 and so leave it to the gathered map / direction vectors
-template <bool NT, typename T>
-__device__ __forceinline__ T ld_nt(const T *p)
-{
-    if constexpr (NT) return __builtin_nontemporal_load(p);
-    else return *p;
-}
-
-template <int NB, bool NT>
-__device__ __forceinline__ void ldb_nt(const double *__restrict__ p, double (&v)[NB])
-{
-    if constexpr (NB % 2 == 0) {
-#pragma unroll
-        for (int b = 0; b < NB; b += 2) {
-            const d2v t = ld_nt<NT>(reinterpret_cast<const d2v *>(p + b));
-            v[b] = t.x;
-            v[b + 1] = t.y;
-        }
-    } else {
-#pragma unroll
-        for (int b = 0; b < NB; ++b) v[b] = ld_nt<NT>(p + b);
-    }
-}
-
 template <int NB>
 __device__ __forceinline__ void stb(double *__restrict__ p, const double (&v)[NB])
 {
@@ -243,41 +197,24 @@ struct Coef;
 template <int NB>
 struct Coef<NB, true> {
     uint32_t v = 0;
-    template <bool NT = false>
     __device__ __forceinline__ void load(const void *__restrict__ base, int64_t k)
     {
         const uint8_t *c = reinterpret_cast<const uint8_t *>(base) + k * NB;
-        if constexpr (NB == 4) v = ld_nt<NT>(reinterpret_cast<const uint32_t *>(c));
-        else if constexpr (NB == 2) v = ld_nt<NT>(reinterpret_cast<const uint16_t *>(c));
-        else v = ld_nt<NT>(c);
+        if constexpr (NB == 4) v = *reinterpret_cast<const uint32_t *>(c);
+        else if constexpr (NB == 2) v = *reinterpret_cast<const uint16_t *>(c);
+        else v = *c;
     }
     __device__ __forceinline__ double get(int b) const { return (double)((v >> (8 * b)) & 0xffu); }
 };
 template <int NB>
 struct Coef<NB, false> {
     double v[NB] = {};
-    template <bool NT = false>
     __device__ __forceinline__ void load(const void *__restrict__ base, int64_t k)
     {
-        ldb_nt<NB, NT>(reinterpret_cast<const double *>(base) + k * NB, v);
+        ldb<NB>(reinterpret_cast<const double *>(base) + k * NB, v);
     }
     __device__ __forceinline__ double get(int b) const { return v[b]; }
 };
-
-// XCD-aware block order (bijective for any grid): blocks b and b + 8 share an XCD
-// (MI355X_MICROARCH.md, workgroup dispatch), so logical block ids are dealt to the 8
-// groups in contiguous runs (each XCD's L2 then serves a contiguous range of map rows
-// or offsets).  Measured at C5 and NOT used (COMAP_DS_XCD=0): k_ds_bin 111 -> 131 us,
-// k_ds_project (contiguous offset runs per block) 114 -> 151 us for one band, 200 -> 234
-// and 233 -> 290 us for four -- the round-robin order streams the entry arrays with
-// every XCD on neighbouring lines, and the map / offset vectors are re-read from the
-// 256 MB Infinity Cache either way.
-__device__ __forceinline__ int64_t xcd_block(int64_t bid, int64_t nwg, bool on)
-{
-    if (!on) return bid;
-    const int64_t q = nwg / 8, r = nwg % 8, x = bid % 8;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
-}
 
 __device__ __forceinline__ double wave_sum(double v)
 {
@@ -731,11 +668,12 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
                 for (int b = 0; b < NB; ++b) nf |= !isfinite(ti[m][b]);
             }
         }
-        // flags[1]: a pixel index >= npix (the caller's error; -1 marks an unbinned sample)
+        // flags[1]: a pixel index >= npix or < -npix (the caller's error: numpy's m[pointing]
+        // raises IndexError there; a negative id marks an unbinned sample that reads m[npix + p])
         if (nonfin) {
             bool ob = false;
 #pragma unroll
-            for (int m = 0; m < K; ++m) ob |= q[m] != kNone && q[m] >= npix;
+            for (int m = 0; m < K; ++m) ob |= q[m] != kNone && (q[m] >= npix || q[m] < -npix);
             if (__ballot(ob) && lane == 0) nonfin[1] = 1;
         }
         // member-mask walk (no payload): hits of the groups that hold no entry (every weight
@@ -1188,8 +1126,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) k
                                                       const uint8_t *__restrict__ keep,
                                                       const uint32_t *__restrict__ hextra, double *__restrict__ h,
                                                       double *__restrict__ hits, double *__restrict__ nnum,
-                                                      int32_t *__restrict__ poff, uint8_t *__restrict__ pcnt,
-                                                      bool xcd)
+                                                      int32_t *__restrict__ poff, uint8_t *__restrict__ pcnt)
 {
 #pragma clang fp contract(off)
     constexpr int CAP = 64 * M;
@@ -1200,11 +1137,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) k
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     double *pl = spl[wv];
     const int kind = lane / NB, b = lane % NB;     // this lane's ordered sum (lanes < 3 NB)
-    // xcd: each XCD walks one contiguous eighth of the pixels
     // the non-empty rows only (k_hit_flags wrote the empty ones): row i of nh = counts[1]
-    const int64_t lb = xcd_block(blockIdx.x, gridDim.x, xcd);
     const int64_t nh = counts[1];
-    for (int64_t i = lb * 4 + wv; i < nh; i += (int64_t)gridDim.x * 4) {
+    for (int64_t i = (int64_t)blockIdx.x * 4 + wv; i < nh; i += (int64_t)gridDim.x * 4) {
         const int64_t p = hrow[i];
         const int64_t lo = hprow[i], hi = hprow[i + 1];
         double acc = 0.0;
@@ -1325,6 +1260,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) k
     }
 }
 
+// The map pixel a projection entry gathers: op_Z reads m[pointing] (Destriper.py:206-213),
+// so an unbinned sample's negative id p in [-npix, -1] reads m[npix + p] -- numpy's index
+// wrap (-1: the last pixel).  The set-up rejects p < -npix (numpy's IndexError).
+__device__ __forceinline__ int64_t wrap_pixel(int32_t p, int64_t npix) { return p >= 0 ? (int64_t)p : npix + p; }
+
 __device__ __forceinline__ double map_value(const double *num, const double *h, int64_t q)
 {
     const double hv = h[q];
@@ -1337,21 +1277,19 @@ __device__ __forceinline__ double map_value(const double *num, const double *h, 
 // entries), lane-strided; each lane issues kBinU entry loads, then kBinU gathers of the
 // NB-band x vectors, before its fmas (in entry order, so the sum is the plain
 // lane-strided one), then a kBinLanes-lane reduction.
-template <int kBinLanes, int NB, bool CF, int kBinU, bool NT = false>
+template <int kBinLanes, int NB, bool CF, int kBinU>
 __global__ void __launch_bounds__(256) k_ds_bin(const int64_t *__restrict__ prow, const int32_t *__restrict__ poff,
                                                 const void *__restrict__ pw, const double *__restrict__ x,
                                                 int64_t npix, const double *__restrict__ base,
                                                 const double *__restrict__ hdiv, double *__restrict__ num,
-                                                const int32_t *__restrict__ flags, const int32_t *__restrict__ rows,
-                                                bool xcd)
+                                                const int32_t *__restrict__ flags, const int32_t *__restrict__ rows)
 {
     if (cg_done(flags)) return;
     const int sub = threadIdx.x & (kBinLanes - 1);
     const int64_t step = (int64_t)gridDim.x * blockDim.x / kBinLanes;
-    const int64_t lb = xcd_block(blockIdx.x, gridDim.x, xcd);
     // rows != NULL: only the listed (non-empty) rows, npix = their count, and prow holds
     // their entry ranges (hprow: row i spans [prow[i], prow[i + 1]), no dependent row load)
-    for (int64_t i = (lb * blockDim.x + threadIdx.x) / kBinLanes; i < npix; i += step) {
+    for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kBinLanes; i < npix; i += step) {
         const int64_t p = rows ? (int64_t)rows[i] : i;
         double s[NB];
 #pragma unroll
@@ -1371,8 +1309,8 @@ __global__ void __launch_bounds__(256) k_ds_bin(const int64_t *__restrict__ prow
 #pragma unroll
         for (int u = 0; u < kBinU; ++u) {
             const bool in = k + u * kBinLanes < e1;
-            o[u] = in ? ld_nt<NT>(poff + k + u * kBinLanes) : 0;
-            if (in) a[u].template load<NT>(pw, k + u * kBinLanes);
+            o[u] = in ? poff[k + u * kBinLanes] : 0;
+            if (in) a[u].load(pw, k + u * kBinLanes);
         }
         while (k < e1) {
             double xv[kBinU][NB];
@@ -1384,8 +1322,8 @@ __global__ void __launch_bounds__(256) k_ds_bin(const int64_t *__restrict__ prow
 #pragma unroll
             for (int u = 0; u < kBinU; ++u) {
                 const bool in = kn + u * kBinLanes < e1;
-                on[u] = in ? ld_nt<NT>(poff + kn + u * kBinLanes) : 0;
-                if (in) an[u].template load<NT>(pw, kn + u * kBinLanes);
+                on[u] = in ? poff[kn + u * kBinLanes] : 0;
+                if (in) an[u].load(pw, kn + u * kBinLanes);
             }
 #pragma unroll
             for (int u = 0; u < kBinU; ++u)
@@ -1451,8 +1389,7 @@ __global__ void __launch_bounds__(256) k_ds_project(const int64_t *__restrict__ 
 #pragma unroll
         for (int u = 0; u < kProjU; ++u) {
             const bool in = e + u * G < e1;
-            const int32_t pp = in ? opix[e + u * G] : (int32_t)(npix - 1);
-            q[u] = pp >= 0 ? pp : (int32_t)(npix - 1);   // m[-1] for off-map samples
+            q[u] = in ? (int32_t)wrap_pixel(opix[e + u * G], npix) : 0;   // numpy's m[p] wrap for p < 0
             if (in) a[u].load(ow, e + u * G);
             else a[u] = Coef<NB, CF>();
         }
@@ -1543,18 +1480,16 @@ __global__ void __launch_bounds__(256) k_ds_project(const int64_t *__restrict__ 
 // ---------------------------------------------------------------- sliced-ELLPACK projection
 constexpr int32_t kSellPad = (int32_t)0x80808080;   // memset pattern 0x80: a padding slot
 
-// chunk widths: sw[c] = CW x the longest row of offsets [CW c, CW c + CW); sw[NC] = 0.
-// CW (chunk width, offsets per chunk) = 64, or 32 for the 4-band lane-pair projection.
-template <int CW>
+// chunk widths: sw[c] = 64 x the longest row of offsets [64 c, 64 c + 64); sw[NC] = 0.
 __global__ void k_sell_width(const int64_t *__restrict__ orow, int64_t NO, int64_t NC, int64_t *__restrict__ sw)
 {
-    const int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / CW;
+    const int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (c > NC) return;
-    const int64_t o = c * CW + (threadIdx.x & (CW - 1));
+    const int64_t o = c * 64 + (threadIdx.x & 63);
     int64_t len = (c < NC && o < NO) ? orow[o + 1] - orow[o] : 0;
 #pragma unroll
-    for (int s = CW / 2; s > 0; s >>= 1) len = max(len, (int64_t)__shfl_xor(len, s, CW));
-    if ((threadIdx.x & (CW - 1)) == 0) sw[c] = CW * len;
+    for (int s = 32; s > 0; s >>= 1) len = max(len, (int64_t)__shfl_xor(len, s, 64));
+    if ((threadIdx.x & 63) == 0) sw[c] = 64 * len;
 }
 
 // The sliced-ELLPACK fill, one workgroup per chunk: the chunk's CSR range (contiguous: its offsets are
@@ -1566,13 +1501,14 @@ template <int NB, bool CF>
 __global__ void __launch_bounds__(256) k_sell_fill_lds(const int64_t *__restrict__ orow,
                                                        const int32_t *__restrict__ opix,
                                                        const void *__restrict__ oco,
-                                                       const int64_t *__restrict__ sbase, int64_t NO, int cw,
+                                                       const int64_t *__restrict__ sbase, int64_t NO,
                                                        int32_t *__restrict__ spix, void *__restrict__ sco)
 {
     using CoefT = typename std::conditional<CF, uint8_t, double>::type;
     __shared__ int32_t lp[kSellStage];
     __shared__ CoefT lc[CF ? kSellStage * NB : 1];
     __shared__ int32_t rs[64], rn[64];
+    constexpr int cw = 64;
     const int64_t c = blockIdx.x;
     const int64_t o0 = c * cw;
     const int nrow = (int)std::min<int64_t>(cw, NO - o0);
@@ -1624,7 +1560,7 @@ __global__ void __launch_bounds__(256) k_sell_fill_lds(const int64_t *__restrict
 // entries: the group's pixel ids and coefficients are coalesced loads issued one group
 // ahead of its map gathers, and the row sum is a plain in-order fma chain per lane (no
 // shuffles).  Same outputs as k_ds_project (y, block partials of y.x per band).
-template <int NB, bool CF, int U, bool NT = false, bool PRE = false>
+template <int NB, bool CF, int U>
 __global__ void __launch_bounds__(256) k_ds_project_sell(const int64_t *__restrict__ sbase,
                                                          const int32_t *__restrict__ spix, const void *__restrict__ sco,
                                                          const double *__restrict__ wbar, const double *__restrict__ ws,
@@ -1632,33 +1568,20 @@ __global__ void __launch_bounds__(256) k_ds_project_sell(const int64_t *__restri
                                                          const double *__restrict__ num, const double *__restrict__ h,
                                                          int64_t NO, int64_t npix, double *__restrict__ y,
                                                          double *__restrict__ dot_part, const int32_t *__restrict__ flags,
-                                                         int64_t pstride, bool xcd)
+                                                         int64_t pstride)
 {
     __shared__ double red[4 * NB];
     if (cg_done(flags)) return;
     const int lane = threadIdx.x & 63;
     const int64_t NC = (NO + 63) >> 6;
     const int64_t nw = (int64_t)gridDim.x * 4;
-    // xcd: the blocks an XCD runs take a contiguous run of chunks (spatially sorted offsets:
-    // that XCD's L2 then holds one region of the map instead of all of it)
-    const int64_t lb = xcd_block(blockIdx.x, gridDim.x, xcd);
     double acc[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) acc[b] = 0.0;
-    const int32_t last = (int32_t)(npix - 1);
-    for (int64_t c = lb * 4 + (threadIdx.x >> 6); c < NC; c += nw) {
+    for (int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < NC; c += nw) {
         const int64_t b0 = sbase[c], W = (sbase[c + 1] - b0) >> 6;
         const int64_t o = c * 64 + lane;
         const int32_t *pp = spix + b0 + lane;
-        // PRE: the lane's own x / wbar / ws, loaded before the row walk (their latency then
-        // overlaps the gathers instead of following them)
-        double xo[NB], wb[NB], wsv[NB];
-        if constexpr (PRE) {
-            const int64_t oc = o < NO ? o : NO - 1;
-            if (x) ldb_nt<NB, NT>(x + oc * NB, xo);
-            if constexpr (CF) ldb_nt<NB, NT>(wbar + oc * NB, wb);
-            ldb_nt<NB, NT>((x ? ws : tw) + oc * NB, wsv);
-        }
         double g[NB];
 #pragma unroll
         for (int b = 0; b < NB; ++b) g[b] = 0.0;
@@ -1667,15 +1590,15 @@ __global__ void __launch_bounds__(256) k_ds_project_sell(const int64_t *__restri
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const bool in = u < W;
-            q[u] = in ? ld_nt<NT>(pp + 64 * u) : kSellPad;
-            if (in) a[u].template load<NT>(sco, b0 + 64 * u + lane);
+            q[u] = in ? pp[64 * u] : kSellPad;
+            if (in) a[u].load(sco, b0 + 64 * u + lane);
         }
         for (int64_t j = 0; j < W; j += U) {
             double mv[U][NB];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 if (q[u] != kSellPad) {
-                    const int64_t qq = q[u] >= 0 ? q[u] : last;     // m[-1] for off-map samples
+                    const int64_t qq = wrap_pixel(q[u], npix);     // m[p] with numpy's wrap for p < 0
                     if (h) {
 #pragma unroll
                         for (int b = 0; b < NB; ++b) mv[u][b] = map_value(num, h, qq * NB + b);
@@ -1690,8 +1613,8 @@ __global__ void __launch_bounds__(256) k_ds_project_sell(const int64_t *__restri
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const bool in = jn + u < W;
-                qn[u] = in ? ld_nt<NT>(pp + 64 * (jn + u)) : kSellPad;
-                if (in) an[u].template load<NT>(sco, b0 + 64 * (jn + u) + lane);
+                qn[u] = in ? pp[64 * (jn + u)] : kSellPad;
+                if (in) an[u].load(sco, b0 + 64 * (jn + u) + lane);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u)
@@ -1703,12 +1626,10 @@ __global__ void __launch_bounds__(256) k_ds_project_sell(const int64_t *__restri
             for (int u = 0; u < U; ++u) { q[u] = qn[u]; a[u] = an[u]; }
         }
         if (o < NO) {
-            double v[NB];
-            if constexpr (!PRE) {
-                if (x) ldb_nt<NB, NT>(x + o * NB, xo);
-                if constexpr (CF) ldb_nt<NB, NT>(wbar + o * NB, wb);
-                ldb_nt<NB, NT>((x ? ws : tw) + o * NB, wsv);
-            }
+            double v[NB], xo[NB], wb[NB], wsv[NB];
+            if (x) ldb<NB>(x + o * NB, xo);
+            if constexpr (CF) ldb<NB>(wbar + o * NB, wb);
+            ldb<NB>((x ? ws : tw) + o * NB, wsv);
             if (!x) {
 #pragma unroll
                 for (int b = 0; b < NB; ++b) xo[b] = 0.0;
@@ -1724,508 +1645,6 @@ __global__ void __launch_bounds__(256) k_ds_project_sell(const int64_t *__restri
             }
             stb<NB>(y + o * NB, v);
         }
-    }
-    if (dot_part) {
-        block_partials<NB>(acc, red, dot_part + blockIdx.x, pstride);
-        if (pstride < kPartMax && blockIdx.x == 0) zero_tail<NB>(dot_part, pstride, gridDim.x);
-    }
-}
-
-// 4 bands, lane pairs: a 32-B gather of one entry's 4 bands by one lane is two 16-B load
-// instructions, each touching its own cache line per lane.  Here the lanes 2s and 2s + 1 take
-// the same entry, bands 0-1 and 2-3, so one load instruction gathers 32 entries' full
-// vectors with each pair on one 32-B segment: half the vector-memory line lookups per entry.
-// Chunks are 32 offsets (sliced-ELLPACK with CW = 32); both lanes of a pair read the entry's
-// pixel and counts (the same address).  Per offset and band the sum is the same in-order
-// chain as k_ds_project_sell's.
-template <bool CF, int U>
-__global__ void __launch_bounds__(256) k_ds_project_sell_pairs(const int64_t *__restrict__ sbase,
-                                                               const int32_t *__restrict__ spix,
-                                                               const void *__restrict__ sco,
-                                                               const double *__restrict__ wbar,
-                                                               const double *__restrict__ ws,
-                                                               const double *__restrict__ tw, const double *__restrict__ x,
-                                                               const double *__restrict__ num, const double *__restrict__ h,
-                                                               int64_t NO, int64_t npix, double *__restrict__ y,
-                                                               double *__restrict__ dot_part,
-                                                               const int32_t *__restrict__ flags, int64_t pstride)
-{
-    constexpr int NB = 4;
-    __shared__ double red[4 * NB];
-    if (cg_done(flags)) return;
-    const int lane = threadIdx.x & 63;
-    const int half = lane & 1, slot = lane >> 1;
-    const int64_t NC = (NO + 31) >> 5;
-    const int64_t nw = (int64_t)gridDim.x * 4;
-    double acc[2] = {0.0, 0.0};
-    const int32_t last = (int32_t)(npix - 1);
-    for (int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < NC; c += nw) {
-        const int64_t b0 = sbase[c], W = (sbase[c + 1] - b0) >> 5;
-        const int64_t o = c * 32 + slot;
-        const int32_t *pp = spix + b0 + slot;
-        double g[2] = {0.0, 0.0};
-        int32_t q[U];
-        Coef<NB, CF> a[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const bool in = u < W;
-            q[u] = in ? pp[32 * u] : kSellPad;
-            if (in) a[u].load(sco, b0 + 32 * u + slot);
-        }
-        for (int64_t j = 0; j < W; j += U) {
-            double mv[U][2];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (q[u] != kSellPad) {
-                    const int64_t qq = q[u] >= 0 ? q[u] : last;     // m[-1] for off-map samples
-                    if (h) {
-                        mv[u][0] = map_value(num, h, qq * NB + 2 * half);
-                        mv[u][1] = map_value(num, h, qq * NB + 2 * half + 1);
-                    } else {
-                        const d2v t = *reinterpret_cast<const d2v *>(num + qq * NB + 2 * half);
-                        mv[u][0] = t.x;
-                        mv[u][1] = t.y;
-                    }
-                }
-            }
-            const int64_t jn = j + U;
-            int32_t qn[U];
-            Coef<NB, CF> an[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const bool in = jn + u < W;
-                qn[u] = in ? pp[32 * (jn + u)] : kSellPad;
-                if (in) an[u].load(sco, b0 + 32 * (jn + u) + slot);
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (q[u] != kSellPad) {
-                    g[0] = fma(a[u].get(2 * half), mv[u][0], g[0]);
-                    g[1] = fma(a[u].get(2 * half + 1), mv[u][1], g[1]);
-                }
-#pragma unroll
-            for (int u = 0; u < U; ++u) { q[u] = qn[u]; a[u] = an[u]; }
-        }
-        if (o < NO) {
-            const int64_t k = o * NB + 2 * half;
-            double xo[2] = {0.0, 0.0}, wsv[2], v[2];
-            if (x) {
-                const d2v t = *reinterpret_cast<const d2v *>(x + k);
-                xo[0] = t.x;
-                xo[1] = t.y;
-            }
-            {
-                const d2v t = *reinterpret_cast<const d2v *>((x ? ws : tw) + k);
-                wsv[0] = t.x;
-                wsv[1] = t.y;
-            }
-            if constexpr (CF) {
-                const d2v t = *reinterpret_cast<const d2v *>(wbar + k);
-                g[0] *= t.x;
-                g[1] *= t.y;
-            }
-#pragma unroll
-            for (int b = 0; b < 2; ++b) {
-                v[b] = (x ? wsv[b] * xo[b] : wsv[b]) - g[b];
-                if (dot_part) acc[b] = fma(v[b], xo[b], acc[b]);
-            }
-            d2v t;
-            t.x = v[0];
-            t.y = v[1];
-            *reinterpret_cast<d2v *>(y + k) = t;
-        }
-    }
-    if (dot_part) {
-        double a4[NB];
-#pragma unroll
-        for (int b = 0; b < NB; ++b) a4[b] = ((b >> 1) == half) ? acc[b & 1] : 0.0;
-        block_partials<NB>(a4, red, dot_part + blockIdx.x, pstride);
-        if (pstride < kPartMax && blockIdx.x == 0) zero_tail<NB>(dot_part, pstride, gridDim.x);
-    }
-}
-
-// k_ds_bin for 4 bands with lane pairs (see k_ds_project_sell_pairs): kBinLanes lanes per
-// pixel row = kBinLanes / 2 entry slots, lanes 2s / 2s + 1 gather bands 0-1 / 2-3 of the
-// slot's entry as one 32-B segment; the pair-halves are reduced separately.
-template <int kBinLanes, bool CF, int kBinU>
-__global__ void __launch_bounds__(256) k_ds_bin_pairs(const int64_t *__restrict__ prow,
-                                                      const int32_t *__restrict__ poff, const void *__restrict__ pw,
-                                                      const double *__restrict__ x, int64_t npix,
-                                                      const double *__restrict__ base, const double *__restrict__ hdiv,
-                                                      double *__restrict__ num, const int32_t *__restrict__ flags,
-                                                      const int32_t *__restrict__ rows)
-{
-    constexpr int NB = 4;
-    constexpr int kSlots = kBinLanes / 2;
-    if (cg_done(flags)) return;
-    const int sub = threadIdx.x & (kBinLanes - 1);
-    const int half = sub & 1, slot = sub >> 1;
-    const int64_t step = (int64_t)gridDim.x * blockDim.x / kBinLanes;
-    for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kBinLanes; i < npix; i += step) {
-        const int64_t p = rows ? (int64_t)rows[i] : i;
-        double s0 = 0.0, s1 = 0.0;
-        double tail[2] = {0.0, 0.0};
-        if (slot == 0 && (base || hdiv)) {
-            const d2v t = *reinterpret_cast<const d2v *>((base ? base : hdiv) + p * NB + 2 * half);
-            tail[0] = t.x;
-            tail[1] = t.y;
-        }
-        const int64_t e1 = prow[i + 1];
-        int64_t k = prow[i] + slot;
-        int32_t o[kBinU];
-        Coef<NB, CF> a[kBinU];
-#pragma unroll
-        for (int u = 0; u < kBinU; ++u) {
-            const bool in = k + u * kSlots < e1;
-            o[u] = in ? poff[k + u * kSlots] : 0;
-            if (in) a[u].load(pw, k + u * kSlots);
-        }
-        while (k < e1) {
-            d2v xv[kBinU];
-#pragma unroll
-            for (int u = 0; u < kBinU; ++u) xv[u] = *reinterpret_cast<const d2v *>(x + (int64_t)o[u] * NB + 2 * half);
-            const int64_t kn = k + kSlots * kBinU;
-            int32_t on[kBinU];
-            Coef<NB, CF> an[kBinU];
-#pragma unroll
-            for (int u = 0; u < kBinU; ++u) {
-                const bool in = kn + u * kSlots < e1;
-                on[u] = in ? poff[kn + u * kSlots] : 0;
-                if (in) an[u].load(pw, kn + u * kSlots);
-            }
-#pragma unroll
-            for (int u = 0; u < kBinU; ++u)
-                if (k + u * kSlots < e1) {
-                    s0 = fma(a[u].get(2 * half), xv[u].x, s0);
-                    s1 = fma(a[u].get(2 * half + 1), xv[u].y, s1);
-                }
-#pragma unroll
-            for (int u = 0; u < kBinU; ++u) { o[u] = on[u]; a[u] = an[u]; }
-            k = kn;
-        }
-#pragma unroll
-        for (int w = kBinLanes / 2; w > 1; w >>= 1) {
-            s0 += __shfl_xor(s0, w, kBinLanes);
-            s1 += __shfl_xor(s1, w, kBinLanes);
-        }
-        if (slot == 0) {
-            double r[2] = {s0, s1};
-#pragma unroll
-            for (int b = 0; b < 2; ++b) {
-                if (base) r[b] = tail[b] - r[b];
-                else if (hdiv) { const double hv = tail[b]; r[b] = hv != 0.0 ? r[b] / hv : r[b]; }
-            }
-            d2v t;
-            t.x = r[0];
-            t.y = r[1];
-            *reinterpret_cast<d2v *>(num + p * NB + 2 * half) = t;
-        }
-    }
-}
-
-// ---------------------------------------------------------------- map-tile projection
-// Tiles of TW x TH map pixels hold 4096 / NB pixels (32 KB of m per tile in LDS).  An
-// entry's tile and local index come from its pixel (off-map entries gather m[npix - 1]).
-struct TileGeom {
-    int64_t nx, npix, ntx;
-    int tw, th;
-    __device__ __forceinline__ void of(int32_t q, int32_t &tile, int32_t &local) const
-    {
-        const int64_t p = (q >= 0 && q < npix) ? q : npix - 1;
-        const int64_t py = p / nx, px = p - py * nx;
-        tile = (int32_t)((py / th) * ntx + px / tw);
-        local = (int32_t)((py % th) * tw + px % tw);
-    }
-};
-
-// entry -> (tile key, entry id); the CSR rows are in internal offset order, so a stable
-// sort by tile leaves every tile's entries ordered by (offset, position in row)
-__global__ void k_tile_keys(const int32_t *__restrict__ opix, int64_t nnz, TileGeom g, int32_t *__restrict__ key,
-                            int32_t *__restrict__ val)
-{
-    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nnz; e += (int64_t)gridDim.x * blockDim.x) {
-        int32_t t, l;
-        g.of(opix[e], t, l);
-        key[e] = t;
-        val[e] = (int32_t)e;
-    }
-}
-
-// offset of every entry (the CSR row it sits in)
-__global__ void k_entry_offset(const int64_t *__restrict__ orow, int64_t NO, int32_t *__restrict__ eo)
-{
-    for (int64_t o = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; o < NO; o += (int64_t)gridDim.x * blockDim.x)
-        for (int64_t e = orow[o]; e < orow[o + 1]; ++e) eo[e] = (int32_t)o;
-}
-
-// segment starts in the tile-sorted order: flag[s] = 1 where (tile, offset) changes
-__global__ void k_seg_flags(const int32_t *__restrict__ tkey, const int32_t *__restrict__ sval,
-                            const int32_t *__restrict__ eo, int64_t n, int32_t *__restrict__ flag)
-{
-    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < n; s += (int64_t)gridDim.x * blockDim.x)
-        flag[s] = (s == 0 || tkey[s] != tkey[s - 1] || eo[sval[s]] != eo[sval[s - 1]]) ? 1 : 0;
-}
-
-// per segment: its tile, offset, first sorted position (segment id = inclusive scan - 1)
-__global__ void k_seg_table(const int32_t *__restrict__ tkey, const int32_t *__restrict__ sval,
-                            const int32_t *__restrict__ eo, const int32_t *__restrict__ flag,
-                            const int32_t *__restrict__ sid, int64_t n, int32_t *__restrict__ seg_tile,
-                            int32_t *__restrict__ seg_off, int32_t *__restrict__ seg_first)
-{
-    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < n; s += (int64_t)gridDim.x * blockDim.x)
-        if (flag[s]) {
-            const int32_t k = sid[s];
-            seg_tile[k] = tkey[s];
-            seg_off[k] = eo[sval[s]];
-            seg_first[k] = (int32_t)s;
-        }
-}
-
-// per tile: its first segment (segments are tile-major); chunk counts
-__global__ void k_tile_first_seg(const int32_t *__restrict__ seg_tile, int64_t nseg, int64_t ntiles,
-                                 int32_t *__restrict__ tfirst)
-{
-    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k <= nseg; k += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t t1 = k < nseg ? seg_tile[k] : (int32_t)ntiles;
-        const int32_t t0 = k > 0 ? seg_tile[k - 1] : -1;
-        for (int32_t t = t0 + 1; t <= t1 && t < ntiles + 1; ++t) tfirst[t] = (int32_t)k;
-    }
-}
-
-// chunk c (64 consecutive segments of one tile): its width (64 x longest segment)
-__global__ void k_tile_chunk_width(const int32_t *__restrict__ chunk_tile, const int32_t *__restrict__ chunk_seg0,
-                                   const int32_t *__restrict__ tfirst, const int32_t *__restrict__ seg_first,
-                                   int64_t nseg, int64_t nent, int64_t nchunk, int64_t *__restrict__ cw)
-{
-    const int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int lane = threadIdx.x & 63;
-    if (c > nchunk) return;
-    int64_t len = 0;
-    if (c < nchunk) {
-        const int64_t k = (int64_t)chunk_seg0[c] + lane;
-        if (k < tfirst[chunk_tile[c] + 1]) len = (k + 1 < nseg ? seg_first[k + 1] : nent) - seg_first[k];
-    }
-#pragma unroll
-    for (int s = 32; s > 0; s >>= 1) len = max(len, (int64_t)__shfl_xor(len, s, 64));
-    if (lane == 0) cw[c] = 64 * len;
-}
-
-// chunk slots: lane = segment, entry j of the segment at tcbase[c] + 64 j + lane.  One
-// thread per tile-sorted entry (coalesced reads); the padding slots keep the memset's
-// all-ones pattern.
-template <int NB, bool CF>
-__global__ void k_tile_fill(const int32_t *__restrict__ sid, const int32_t *__restrict__ seg_tile,
-                            const int32_t *__restrict__ seg_first, const int32_t *__restrict__ tfirst,
-                            const int32_t *__restrict__ tcfirst, const int32_t *__restrict__ sval,
-                            const int32_t *__restrict__ opix, const void *__restrict__ oco, TileGeom g, int64_t nent,
-                            const int64_t *__restrict__ tcbase, uint64_t *__restrict__ tent, double *__restrict__ tentw)
-{
-    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < nent; s += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t k = sid[s] - 1;                         // segment
-        const int32_t t = seg_tile[k];
-        const int32_t kr = k - tfirst[t];
-        const int64_t c = (int64_t)tcfirst[t] + kr / 64;
-        const int64_t slot = tcbase[c] + 64 * (int64_t)(s - seg_first[k]) + (kr & 63);
-        const int32_t e = sval[s];
-        int32_t tt, l;
-        g.of(opix[e], tt, l);
-        uint32_t pk = 0;
-        if constexpr (CF) {
-            const uint8_t *cc = reinterpret_cast<const uint8_t *>(oco) + (int64_t)e * NB;
-#pragma unroll
-            for (int b = 0; b < NB; ++b) pk |= (uint32_t)cc[b] << (8 * b);
-        } else {
-#pragma unroll
-            for (int b = 0; b < NB; ++b) tentw[slot * NB + b] = reinterpret_cast<const double *>(oco)[(int64_t)e * NB + b];
-        }
-        tent[slot] = ((uint64_t)(uint32_t)l << 32) | pk;
-    }
-}
-
-// the partial slot of every chunk lane (-1: a lane past its tile's segments)
-__global__ void k_tile_slots(const int32_t *__restrict__ chunk_tile, const int32_t *__restrict__ chunk_seg0,
-                             const int32_t *__restrict__ tfirst, const int32_t *__restrict__ seg_slot, int64_t nchunk,
-                             int32_t *__restrict__ tslot)
-{
-    const int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (c >= nchunk) return;
-    const int64_t k = (int64_t)chunk_seg0[c] + (threadIdx.x & 63);
-    tslot[c * 64 + (threadIdx.x & 63)] = k < tfirst[chunk_tile[c] + 1] ? seg_slot[k] : -1;
-}
-
-__global__ void k_iota(int32_t *__restrict__ v, int64_t n)
-{
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        v[i] = (int32_t)i;
-}
-
-// segments sorted by offset (stable: tile order within an offset): slot of each segment =
-// its position; pstart[o] = first position of offset o (offsets without segments: the next)
-__global__ void k_seg_slots(const int32_t *__restrict__ offk, const int32_t *__restrict__ ids, int64_t nseg,
-                            int64_t NO, int32_t *__restrict__ seg_slot, int64_t *__restrict__ pstart)
-{
-    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s <= nseg; s += (int64_t)gridDim.x * blockDim.x) {
-        if (s < nseg) seg_slot[ids[s]] = (int32_t)s;
-        const int64_t o1 = s < nseg ? offk[s] : NO;
-        const int64_t o0 = s > 0 ? offk[s - 1] : -1;
-        for (int64_t o = o0 + 1; o <= o1 && o <= NO; ++o) pstart[o] = s;
-    }
-}
-
-// The tile pass: one workgroup = one tile's m staged in LDS + up to kTileChunks of its
-// chunks (one per wave, lane = (offset, tile) segment); each lane's in-order fma chain over
-// its segment's entries from LDS (entry loads issued one group ahead); partial sums to
-// tpart[slot].
-constexpr int kTileChunks = 16;      // waves (chunks) per workgroup: 1024 threads share one staged tile
-template <int NB, bool CF, int U>
-__global__ void __launch_bounds__(1024) k_ds_project_tile(const int32_t *__restrict__ twg,
-                                                          const int32_t *__restrict__ tcend,
-                                                          const int64_t *__restrict__ tcbase,
-                                                          const uint64_t *__restrict__ tent,
-                                                          const double *__restrict__ tentw,
-                                                          const int32_t *__restrict__ tslot, TileGeom g,
-                                                          const double *__restrict__ num, const double *__restrict__ h,
-                                                          double *__restrict__ tpart, const int32_t *__restrict__ flags)
-{
-    constexpr int kTilePix = 4096 / NB;
-    __shared__ double m[kTilePix * NB];
-    if (cg_done(flags)) return;
-    const int32_t t = twg[2 * blockIdx.x], c0 = twg[2 * blockIdx.x + 1];
-    const int64_t ty = t / g.ntx, tx = t - ty * g.ntx;
-    const int lane = threadIdx.x & 63;
-    const int64_t c = (int64_t)c0 + (threadIdx.x >> 6);
-    const bool active = c < tcend[t];
-    // this wave's first group of entries, in flight while the tile is staged
-    const int64_t b0 = active ? tcbase[c] : 0, W = active ? (tcbase[c + 1] - b0) >> 6 : 0;
-    uint64_t v[U];
-    double wv[U][NB];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const bool in = u < W;
-        v[u] = in ? tent[b0 + 64 * u + lane] : ~0ull;
-        if constexpr (!CF) {
-            if (in) ldb<NB>(tentw + (b0 + 64 * u + lane) * NB, wv[u]);
-        }
-    }
-    // stage the tile: 4096 doubles, 2 per thread-load (16 B), all loads before the stores
-    {
-        constexpr int kPer = 4096 / 2 / 1024;          // d2v loads per thread
-        d2v st[kPer];
-#pragma unroll
-        for (int r = 0; r < kPer; ++r) {
-            const int i = 2 * (threadIdx.x + 1024 * r);   // even: a band pair of one pixel (NB even) or 2 pixels (NB 1)
-            const int local = i / NB, b = i - local * NB;
-            const int64_t py = ty * g.th + local / g.tw, px = tx * g.tw + local % g.tw;
-            const int64_t p = py * g.nx + px;
-            d2v val;
-            val.x = 0.0;
-            val.y = 0.0;
-            if constexpr (NB == 1) {
-                const int64_t px2 = px + 1, p2 = p + 1;           // the next pixel of the same tile row
-                if (px < g.nx && p < g.npix) val.x = h ? map_value(num, h, p) : num[p];
-                if (px2 < g.nx && p2 < g.npix && (local + 1) % g.tw != 0) val.y = h ? map_value(num, h, p2) : num[p2];
-            } else {
-                if (px < g.nx && p < g.npix) {
-                    if (h) {
-                        val.x = map_value(num, h, p * NB + b);
-                        val.y = map_value(num, h, p * NB + b + 1);
-                    } else {
-                        val = *reinterpret_cast<const d2v *>(num + p * NB + b);
-                    }
-                }
-            }
-            st[r] = val;
-        }
-#pragma unroll
-        for (int r = 0; r < kPer; ++r) *reinterpret_cast<d2v *>(m + 2 * (threadIdx.x + 1024 * r)) = st[r];
-    }
-    __syncthreads();
-    if (!active) return;
-    double acc[NB];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) acc[b] = 0.0;
-    for (int64_t j = 0; j < W; j += U) {
-        uint64_t vn[U];
-        double wn[U][NB];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const bool in = j + U + u < W;
-            vn[u] = in ? tent[b0 + 64 * (j + U + u) + lane] : ~0ull;
-            if constexpr (!CF) {
-                if (in) ldb<NB>(tentw + (b0 + 64 * (j + U + u) + lane) * NB, wn[u]);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if ((uint32_t)(v[u] >> 32) != 0xffffffffu) {
-                const int l = (int)(v[u] >> 32);
-                double mm[NB];
-                ldb<NB>(m + l * NB, mm);
-#pragma unroll
-                for (int b = 0; b < NB; ++b) {
-                    const double a = CF ? (double)((uint32_t)(v[u] >> (8 * b)) & 0xffu) : wv[u][b];
-                    acc[b] = fma(a, mm[b], acc[b]);
-                }
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            v[u] = vn[u];
-            if constexpr (!CF) {
-#pragma unroll
-                for (int b = 0; b < NB; ++b) wv[u][b] = wn[u][b];
-            }
-        }
-    }
-    const int32_t sl = tslot[c * 64 + lane];
-    if (sl >= 0) stb<NB>(tpart + (int64_t)sl * NB, acc);
-}
-
-// y_o = ws_o x_o - wbar_o sum_t tpart[o, t] (tile order), block partials of y.x; x == NULL:
-// y_o = tw_o - ... (the b vector).  Same outputs as k_ds_project.
-template <int NB, bool CF>
-__global__ void __launch_bounds__(256) k_ds_tile_combine(const int64_t *__restrict__ pstart,
-                                                         const double *__restrict__ tpart,
-                                                         const double *__restrict__ wbar, const double *__restrict__ ws,
-                                                         const double *__restrict__ tw, const double *__restrict__ x,
-                                                         int64_t NO, double *__restrict__ y,
-                                                         double *__restrict__ dot_part, const int32_t *__restrict__ flags,
-                                                         int64_t pstride)
-{
-    __shared__ double red[4 * NB];
-    if (cg_done(flags)) return;
-    double acc[NB];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) acc[b] = 0.0;
-    for (int64_t o = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; o < NO; o += (int64_t)gridDim.x * blockDim.x) {
-        double gsum[NB], xo[NB], wsv[NB], v[NB];
-#pragma unroll
-        for (int b = 0; b < NB; ++b) gsum[b] = 0.0;
-        const int64_t s1 = pstart[o + 1];
-        for (int64_t sidx = pstart[o]; sidx < s1; ++sidx) {
-            double pv[NB];
-            ldb<NB>(tpart + sidx * NB, pv);
-#pragma unroll
-            for (int b = 0; b < NB; ++b) gsum[b] += pv[b];
-        }
-        if (x) ldb<NB>(x + o * NB, xo);
-        else {
-#pragma unroll
-            for (int b = 0; b < NB; ++b) xo[b] = 0.0;
-        }
-        ldb<NB>((x ? ws : tw) + o * NB, wsv);
-        if constexpr (CF) {
-            double wb[NB];
-            ldb<NB>(wbar + o * NB, wb);
-#pragma unroll
-            for (int b = 0; b < NB; ++b) gsum[b] *= wb[b];
-        }
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            v[b] = (x ? wsv[b] * xo[b] : wsv[b]) - gsum[b];
-            if (dot_part) acc[b] = fma(v[b], xo[b], acc[b]);
-        }
-        stb<NB>(y + o * NB, v);
     }
     if (dot_part) {
         block_partials<NB>(acc, red, dot_part + blockIdx.x, pstride);
@@ -2480,37 +1899,7 @@ void launch_bin_u(const comap_destriper *d, hipStream_t st, const double *x, con
     const int lanes = d->bin_lanes ? d->bin_lanes : (mean >= 24 ? 16 : (mean >= 10 ? 8 : 4));
     const unsigned g = grid_for(np * lanes, 65536);
     const void *co = CF ? (const void *)d->pcnt : (const void *)d->pw;
-#define COMAP_BIN(LN) k_ds_bin<LN, NB, CF, U><<<g, 256, 0, st>>>(rp, d->poff, co, x, np, base, hdiv, num, flags, rows, \
-                                                                 d->bin_xcd)
-    if constexpr (NB == 4) {
-        if (d->bin_pairs) {
-#define COMAP_BIN_P(LN) k_ds_bin_pairs<LN, CF, U><<<g, 256, 0, st>>>(rp, d->poff, co, x, np, base, hdiv, num, flags, rows)
-            switch (lanes) {
-            case 64: COMAP_BIN_P(64); break;
-            case 32: COMAP_BIN_P(32); break;
-            case 16: COMAP_BIN_P(16); break;
-            case 8: COMAP_BIN_P(8); break;
-            default: COMAP_BIN_P(4);
-            }
-#undef COMAP_BIN_P
-            return;
-        }
-    }
-    if constexpr (U == 4) {
-        if (d->ds_nt) {
-#define COMAP_BIN_NT(LN) k_ds_bin<LN, NB, CF, 4, true><<<g, 256, 0, st>>>(rp, d->poff, co, x, np, base, hdiv, num, \
-                                                                          flags, rows, d->bin_xcd)
-            switch (lanes) {
-            case 64: COMAP_BIN_NT(64); break;
-            case 32: COMAP_BIN_NT(32); break;
-            case 16: COMAP_BIN_NT(16); break;
-            case 8: COMAP_BIN_NT(8); break;
-            default: COMAP_BIN_NT(4);
-            }
-#undef COMAP_BIN_NT
-            return;
-        }
-    }
+#define COMAP_BIN(LN) k_ds_bin<LN, NB, CF, U><<<g, 256, 0, st>>>(rp, d->poff, co, x, np, base, hdiv, num, flags, rows)
     switch (lanes) {
     case 64: COMAP_BIN(64); break;
     case 32: COMAP_BIN(32); break;
@@ -2566,40 +1955,10 @@ template <int NB, bool CF, int U>
 unsigned launch_project_u(const comap_destriper *d, hipStream_t st, const double *x, const double *num,
                           const double *h, double *y, double *part, const int32_t *flags, int64_t pstride)
 {
-    if (d->tiles) {
-        const TileGeom g{d->nx, d->npix, d->ntx, d->tile_w, d->tile_h};
-        k_ds_project_tile<NB, CF, 8><<<(unsigned)d->nwg_t, 1024, 0, st>>>(d->twg, d->tcend, d->tcbase, d->tent,
-                                                                      d->tentw, d->tslot, g, num, h, d->tpart, flags);
-        const unsigned cg = (unsigned)std::max<int64_t>(
-            1, std::min<int64_t>((d->NO + 255) / 256, std::min<int64_t>(pstride, d->proj_blocks)));
-        k_ds_tile_combine<NB, CF><<<cg, 256, 0, st>>>(d->pstart, d->tpart, d->wbar, d->ws, d->tw, x, d->NO, y, part,
-                                                      flags, pstride);
-        return cg;
-    }
     const unsigned pg = project_grid(d, pstride);
-    if (d->sell && d->sell_cw == 32) {
-        if constexpr (NB == 4) {
-            const int64_t per = 4 * 32;          // offsets per block sweep
-            const unsigned pg2 = (unsigned)std::max<int64_t>(
-                1, std::min<int64_t>((d->NO + per - 1) / per, std::min<int64_t>(pstride, d->proj_blocks)));
-            if (d->sell_u == 4)
-                k_ds_project_sell_pairs<CF, 4><<<pg2, 256, 0, st>>>(d->sbase, d->spix, d->sco, d->wbar, d->ws, d->tw,
-                                                                   x, num, h, d->NO, d->npix, y, part, flags, pstride);
-            else
-                k_ds_project_sell_pairs<CF, 8><<<pg2, 256, 0, st>>>(d->sbase, d->spix, d->sco, d->wbar, d->ws, d->tw,
-                                                                   x, num, h, d->NO, d->npix, y, part, flags, pstride);
-            return pg2;
-        }
-    }
     if (d->sell) {
-#define COMAP_SELL(UU, NT, PRE) k_ds_project_sell<NB, CF, UU, NT, PRE><<<pg, 256, 0, st>>>(                        \
-        d->sbase, d->spix, d->sco, d->wbar, d->ws, d->tw, x, num, h, d->NO, d->npix, y, part, flags, pstride, d->proj_xcd)
-        if (d->sell_u == 4) COMAP_SELL(4, false, false);
-        else if (d->ds_nt && d->sell_pre) COMAP_SELL(8, true, true);
-        else if (d->ds_nt) COMAP_SELL(8, true, false);
-        else if (d->sell_pre) COMAP_SELL(8, false, true);
-        else COMAP_SELL(8, false, false);
-#undef COMAP_SELL
+        k_ds_project_sell<NB, CF, 8><<<pg, 256, 0, st>>>(d->sbase, d->spix, d->sco, d->wbar, d->ws, d->tw, x, num, h,
+                                                        d->NO, d->npix, y, part, flags, pstride);
         return pg;
     }
     const void *co = CF ? (const void *)d->ocnt : (const void *)d->ow;
@@ -2703,7 +2062,8 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     if (nb != 1 && nb != 2 && nb != 4) return comap_fail(ctx, -1, "bands per problem must be 1, 2 or 4");
     if (L < 1 || L > 256) return comap_fail(ctx, -1, "offset_length must be in [1, 256]");
     if (N <= 0 || N % L) return comap_fail(ctx, -1, "n_samples must be a positive multiple of offset_length");
-    if (npix <= 0 || npix >= (1ll << 31) - 1 || N >= (1ll << 31)) return comap_fail(ctx, -1, "size limits exceeded");
+    // (npix below the SELL padding id's magnitude, so no pixel id in [-npix, npix) is the pad)
+    if (npix <= 0 || npix >= 0x7f7f7f7fll || N >= (1ll << 31)) return comap_fail(ctx, -1, "size limits exceeded");
     hipStream_t st = ctx->stream;
     auto *d = new comap_destriper();
     d->ctx = ctx; d->N = N; d->L = L; d->NO = N / L; d->npix = npix; d->nb = nb;
@@ -2732,14 +2092,10 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     while ((1ll << end_bit) <= npix) ++end_bit;
     // ---- scratch: sizes first (hipcub temp storage for the largest sort / scan), one allocation
     size_t sort_tb = 0, scan_tb = 0, scan32_tb = 0;
-    const bool nine = [] {
-        const char *v = getenv("COMAP_DS_SORT9");        // 0: hipcub's radix sort for the offset sort too
-        return !(v && v[0] == '0');
-    }();
     (void)sort_pairs_i32(false, nullptr, sort_tb, nullptr, nullptr, nullptr, nullptr, N, end_bit, st);
     {
         size_t tb9 = 0;       // the spatial offset sort (NO pairs)
-        (void)sort_pairs_i32(nine, nullptr, tb9, nullptr, nullptr, nullptr, nullptr, NO, end_bit, st);
+        (void)sort_pairs_i32(true, nullptr, tb9, nullptr, nullptr, nullptr, nullptr, NO, end_bit, st);
         sort_tb = std::max(sort_tb, tb9);
     }
     size_t sort64_tb = 0;   // the count form's transpose: (pixel, u64 offset|counts) pairs
@@ -2799,7 +2155,7 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         k_offset_keys<<<(unsigned)std::min<int64_t>((NO + 3) / 4, 65536), 256, 0, st>>>(pix, NO, L, npix, ekey, eval);
         COMAP_LAUNCH_CHECK(ctx);
         size_t tb = cub_tb;
-        COMAP_CHECK(ctx, sort_pairs_i32(nine, cub_tmp, tb, ekey, ekey2, eval, d->perm, NO, end_bit, st));
+        COMAP_CHECK(ctx, sort_pairs_i32(true, cub_tmp, tb, ekey, ekey2, eval, d->perm, NO, end_bit, st));
     }
     // ---- 2. count pass (+ the count-form test: non-zero weights uniform per offset and band)
     COMAP_CHECK(ctx, hipMemsetAsync(nonuni, 0, 4, st));
@@ -2835,13 +2191,10 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     }
     int64_t NCs = NC;
     if (d->sell) {
-        const char *pe = getenv("COMAP_DS_PPAIR");            // 4 bands: lane-pair SELL projection
-        d->sell_cw = (nb == 4 && pe && pe[0] == '1') ? 32 : 64;
-        NCs = (NO + d->sell_cw - 1) / d->sell_cw;
+        NCs = (NO + 63) / 64;
         if (dalloc(ctx, &d->sbase, NCs + 1)) return -2;
-        const unsigned wg = (unsigned)(((NCs + 1) * d->sell_cw + 255) / 256);
-        if (d->sell_cw == 32) k_sell_width<32><<<wg, 256, 0, st>>>(d->orow, NO, NCs, swid);
-        else k_sell_width<64><<<wg, 256, 0, st>>>(d->orow, NO, NCs, swid);
+        const unsigned wg = (unsigned)(((NCs + 1) * 64 + 255) / 256);
+        k_sell_width<<<wg, 256, 0, st>>>(d->orow, NO, NCs, swid);
         COMAP_LAUNCH_CHECK(ctx);
         COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(cub_tmp, scan_tb, swid, d->sbase, (int)(NCs + 1), st));
     }
@@ -2858,7 +2211,7 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     d->nnz = hw.p[0];
     if (d->sell) d->nsell = hw.p[1];
     const int32_t nonuni_h = (int32_t)hw.p[2], nonfin_h = (int32_t)hw.p[3];
-    if (hw.p[4]) return comap_fail(ctx, -3, "pixel index out of range for the map (>= npix)");
+    if (hw.p[4]) return comap_fail(ctx, -3, "pixel index out of range for the map (>= npix or < -npix)");
     {
         const char *cfe = getenv("COMAP_DS_CF");             // 0: always the f64 entry weights
         d->cf = !nonuni_h && L <= 255 && !(cfe && cfe[0] == '0');
@@ -2880,12 +2233,6 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         d->proj_blocks = env_int("COMAP_DS_PB", d->sell ? 2 * kProjBlocks : kProjBlocks,
                                  {256, 512, 1024, 2048, 4096, 8192});
         d->cg_graph = env_int("COMAP_DS_CGGRAPH", -1, {0, 1});
-        d->sell_u = env_int("COMAP_DS_SU", 8, {4, 8});
-        d->bin_xcd = env_int("COMAP_DS_BXCD", 0, {0, 1}) == 1;
-        d->proj_xcd = env_int("COMAP_DS_PXCD", 0, {0, 1}) == 1;
-        d->ds_nt = env_int("COMAP_DS_NT", 0, {0, 1}) == 1;
-        d->sell_pre = env_int("COMAP_DS_SPRE", 0, {0, 1}) == 1;
-        d->bin_pairs = env_int("COMAP_DS_BPAIR", 0, {0, 1}) == 1;
     }
     // the member-mask walk needs the count form and finite tod everywhere; otherwise the
     // count pass runs again with the per-sample payload for the sorted-sample walk
@@ -2926,13 +2273,13 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         if (dalloc(ctx, &d->spix, d->nsell)) return -2;
         if (d->cf ? dalloc(ctx, (uint8_t **)&d->sco, d->nsell * NB) : dalloc(ctx, (double **)&d->sco, d->nsell * NB))
             return -2;
-        const unsigned nch = (unsigned)((NO + d->sell_cw - 1) / d->sell_cw);
+        const unsigned nch = (unsigned)((NO + 63) / 64);
         if (d->cf) {
             COMAP_NB_SWITCH(nb, (k_sell_fill_lds<NB, true><<<nch, 256, 0, st>>>(
-                                    d->orow, d->opix, d->ocnt, d->sbase, NO, d->sell_cw, d->spix, d->sco)));
+                                    d->orow, d->opix, d->ocnt, d->sbase, NO, d->spix, d->sco)));
         } else {
             COMAP_NB_SWITCH(nb, (k_sell_fill_lds<NB, false><<<nch, 256, 0, st>>>(
-                                    d->orow, d->opix, d->ow, d->sbase, NO, d->sell_cw, d->spix, d->sco)));
+                                    d->orow, d->opix, d->ow, d->sbase, NO, d->spix, d->sco)));
         }
         COMAP_LAUNCH_CHECK(ctx);
     }
@@ -2969,17 +2316,12 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     // ---- 5. sample-level maps (binValues order)
     const unsigned wgrid = (unsigned)std::min<int64_t>((npix + 3) / 4, 65536);
     if (walk) {
-        // member slots per lane and chunk (>= KW: one entry's members fit a chunk)
-        const char *wm = getenv("COMAP_DS_WALKM");
-        const int M = std::max(KW, wm && wm[0] == '2' ? 2 : 1);
-        const char *wxe = getenv("COMAP_DS_WXCD");
-        const bool wx = wxe && wxe[0] == '1';
-        const unsigned wgrid2 = wgrid;     // one wave per row (a fixed 2048-block grid: C5 0.80 -> 1.04 ms)
-#define COMAP_W2(KK, MM) k_sample_walk2<NB, KK, MM><<<wgrid2, 256, 0, st>>>(                                  \
-        d->hrow, d->hprow, counts, evn2, (const SlotRec<KK> *)srec, d->perm, d->wbar, w, payload, N, npix, L, NO, keep, hextra, d->h, d->hits, d->nnum, \
-        d->poff, d->pcnt, wx)
-        if (KW == 1 && M == 1) { COMAP_NB_SWITCH(nb, COMAP_W2(1, 1)); }
-        else if (KW == 1) { COMAP_NB_SWITCH(nb, COMAP_W2(1, 2)); }
+        // member slots per lane and chunk: 64 KW (one entry's members fit a chunk); one wave per
+        // row (a fixed 2048-block grid: C5 0.80 -> 1.04 ms)
+#define COMAP_W2(KK, MM) k_sample_walk2<NB, KK, MM><<<wgrid, 256, 0, st>>>(                                   \
+        d->hrow, d->hprow, counts, evn2, (const SlotRec<KK> *)srec, d->perm, d->wbar, w, payload, N, npix, L, NO, keep, \
+        hextra, d->h, d->hits, d->nnum, d->poff, d->pcnt)
+        if (KW == 1) { COMAP_NB_SWITCH(nb, COMAP_W2(1, 1)); }
         else if (KW == 2) { COMAP_NB_SWITCH(nb, COMAP_W2(2, 2)); }
         else { COMAP_NB_SWITCH(nb, COMAP_W2(4, 4)); }
 #undef COMAP_W2
@@ -3017,7 +2359,7 @@ extern "C" int comap_destripe_destroy(comap_destriper *d)
     (void)hipDeviceSynchronize();
     void *b[] = {d->orow, d->opix, d->ow, d->ws, d->tw, d->prow, d->poff, d->pw, d->h, d->hits, d->nnum, d->part, d->scal,
                  d->cg, d->flags, d->hrow, d->hprow, d->perm, d->ocnt, d->pcnt, d->wbar, d->pt, d->sbase, d->spix,
-                 d->sco, d->tent, d->tentw, d->tcbase, d->tslot, d->twg, d->tcend, d->pstart, d->tpart};
+                 d->sco};
     comap_tmp_free_on(b, (int)(sizeof(b) / sizeof(b[0])), nullptr, true);
     comap_pinned_free(d->flags_host);
     comap_pinned_free(d->thr_host);
@@ -3037,169 +2379,6 @@ extern "C" int32_t comap_destripe_entry_bytes(const comap_destriper *d)
 {
     return d ? (d->cf ? 4 + d->nb : 4 + 8 * d->nb) : -1;
 }
-
-// Map-tile projection for a map laid out in rows of nx pixels (CAR / WCS maps: p = y nx +
-// x).  Builds, from the offset-major rows: the entries sorted by (tile, offset, position),
-// their (offset, tile) segments, each offset's partial slots in tile order, and per tile
-// sliced-ELLPACK chunks of 64 segments.  Synchronises the host twice (sizes).
-extern "C" int comap_destripe_tiles(comap_destriper *d, int64_t nx)
-{
-    if (!d) return -1;
-    COMAP_DEVICE_GUARD(d->ctx);
-    comap_ctx *ctx = d->ctx;
-    if (nx <= 0) return comap_fail(ctx, -1, "comap_destripe_tiles: nx must be positive");
-    if (d->tiles || d->nnz == 0) return 0;
-    if (!d->cf && !d->ow) return comap_fail(ctx, -1, "comap_destripe_tiles: no offset-major weights");
-    hipStream_t st = ctx->stream;
-    const int nb = d->nb;
-    const int64_t nnz = d->nnz, NO = d->NO;
-    TileGeom g{};
-    g.nx = nx;
-    g.npix = d->npix;
-    g.tw = nb == 4 ? 32 : 64;
-    g.th = nb == 1 ? 64 : 32;
-    const int64_t ny = (d->npix + nx - 1) / nx;
-    g.ntx = (nx + g.tw - 1) / g.tw;
-    const int64_t nty = (ny + g.th - 1) / g.th;
-    const int64_t ntiles = g.ntx * nty;
-    if (ntiles >= (1ll << 30) || nnz >= (1ll << 31)) return comap_fail(ctx, -1, "comap_destripe_tiles: too large");
-    int tbits = 1;
-    while ((1ll << tbits) <= ntiles) ++tbits;
-    int obits = 1;
-    while ((1ll << obits) <= NO) ++obits;
-    DevTemps tmp(st, false);
-    int32_t *key = nullptr, *key2 = nullptr, *val = nullptr, *sval = nullptr, *eo = nullptr, *flag = nullptr,
-            *sid = nullptr;
-    COMAP_CHECK(ctx, tmp.alloc(&key, (size_t)nnz));
-    COMAP_CHECK(ctx, tmp.alloc(&key2, (size_t)nnz));
-    COMAP_CHECK(ctx, tmp.alloc(&val, (size_t)nnz));
-    COMAP_CHECK(ctx, tmp.alloc(&sval, (size_t)nnz));
-    COMAP_CHECK(ctx, tmp.alloc(&eo, (size_t)nnz));
-    COMAP_CHECK(ctx, tmp.alloc(&flag, (size_t)nnz));
-    COMAP_CHECK(ctx, tmp.alloc(&sid, (size_t)nnz));
-    size_t tb = 0, tb2 = 0, tb3 = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key, key2, val, sval, (int)nnz, 0, tbits, st);
-    (void)hipcub::DeviceScan::InclusiveSum(nullptr, tb2, flag, sid, (int)nnz, st);
-    char *cub = nullptr;
-    k_tile_keys<<<grid_for(nnz, 8192), 256, 0, st>>>(d->opix, nnz, g, key, val);
-    k_entry_offset<<<grid_for(NO, 8192), 256, 0, st>>>(d->orow, NO, eo);
-    COMAP_LAUNCH_CHECK(ctx);
-    COMAP_CHECK(ctx, tmp.alloc(&cub, std::max(tb, tb2) + 256));
-    COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(cub, tb, key, key2, val, sval, (int)nnz, 0, tbits, st));
-    k_seg_flags<<<grid_for(nnz, 8192), 256, 0, st>>>(key2, sval, eo, nnz, flag);
-    COMAP_LAUNCH_CHECK(ctx);
-    COMAP_CHECK(ctx, hipcub::DeviceScan::InclusiveSum(cub, tb2, flag, sid, (int)nnz, st));
-    int32_t nseg_h = 0;
-    COMAP_CHECK(ctx, hipMemcpyAsync(&nseg_h, sid + nnz - 1, 4, hipMemcpyDeviceToHost, st));
-    COMAP_CHECK(ctx, hipStreamSynchronize(st));
-    const int64_t nseg = nseg_h;
-    // sid is the inclusive scan: segment id = sid - 1
-    int32_t *seg_tile = nullptr, *seg_off = nullptr, *seg_first = nullptr, *seg_ids = nullptr, *seg_ids2 = nullptr,
-            *seg_offk = nullptr, *tfirst = nullptr, *seg_slot = nullptr;
-    COMAP_CHECK(ctx, tmp.alloc(&seg_tile, (size_t)nseg));
-    COMAP_CHECK(ctx, tmp.alloc(&seg_off, (size_t)nseg));
-    COMAP_CHECK(ctx, tmp.alloc(&seg_first, (size_t)nseg));
-    COMAP_CHECK(ctx, tmp.alloc(&seg_ids, (size_t)nseg));
-    COMAP_CHECK(ctx, tmp.alloc(&seg_ids2, (size_t)nseg));
-    COMAP_CHECK(ctx, tmp.alloc(&seg_offk, (size_t)nseg));
-    COMAP_CHECK(ctx, tmp.alloc(&seg_slot, (size_t)nseg));
-    COMAP_CHECK(ctx, tmp.alloc(&tfirst, (size_t)ntiles + 2));
-    {
-        // segment table (ids from the inclusive scan, shifted by one)
-        k_seg_table<<<grid_for(nnz, 8192), 256, 0, st>>>(key2, sval, eo, flag, sid, nnz, seg_tile - 1, seg_off - 1,
-                                                       seg_first - 1);
-        COMAP_LAUNCH_CHECK(ctx);
-    }
-    // each offset's slots in tile order: segments stably sorted by offset
-    k_iota<<<grid_for(nseg, 8192), 256, 0, st>>>(seg_ids, nseg);
-    COMAP_LAUNCH_CHECK(ctx);
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb3, seg_off, seg_offk, seg_ids, seg_ids2, (int)nseg, 0, obits,
-                                             st);
-    char *cub3 = nullptr;
-    COMAP_CHECK(ctx, tmp.alloc(&cub3, tb3 + 256));
-    COMAP_CHECK(ctx, hipcub::DeviceRadixSort::SortPairs(cub3, tb3, seg_off, seg_offk, seg_ids, seg_ids2, (int)nseg, 0,
-                                                        obits, st));
-    if (dalloc(ctx, &d->pstart, NO + 1) || dalloc(ctx, &d->tpart, (size_t)nseg * nb)) return -2;
-    k_seg_slots<<<grid_for(nseg, 8192), 256, 0, st>>>(seg_offk, seg_ids2, nseg, NO, seg_slot, d->pstart);
-    k_tile_first_seg<<<grid_for(nseg + 1, 8192), 256, 0, st>>>(seg_tile, nseg, ntiles, tfirst);
-    COMAP_LAUNCH_CHECK(ctx);
-    std::vector<int32_t> tf((size_t)ntiles + 1);
-    COMAP_CHECK(ctx, hipMemcpyAsync(tf.data(), tfirst, 4 * tf.size(), hipMemcpyDeviceToHost, st));
-    COMAP_CHECK(ctx, hipStreamSynchronize(st));
-    // chunks (64 segments of one tile) and workgroups (4 chunks of one tile) on the host
-    std::vector<int32_t> ch_tile, ch_seg0, wg, tcend((size_t)ntiles), tcf((size_t)ntiles);
-    for (int64_t t = 0; t < ntiles; ++t) {
-        const int32_t k0 = tf[t], k1 = tf[t + 1];
-        const int32_t cfirst = (int32_t)ch_tile.size();
-        tcf[t] = cfirst;
-        for (int32_t k = k0; k < k1; k += 64) {
-            ch_tile.push_back((int32_t)t);
-            ch_seg0.push_back(k);
-        }
-        tcend[t] = (int32_t)ch_tile.size();
-        for (int32_t c = cfirst; c < tcend[t]; c += kTileChunks) {
-            wg.push_back((int32_t)t);
-            wg.push_back(c);
-        }
-    }
-    const int64_t nchunk = (int64_t)ch_tile.size();
-    int32_t *dch_tile = nullptr, *dch_seg0 = nullptr, *dtcf = nullptr;
-    int64_t *cw = nullptr;
-    COMAP_CHECK(ctx, tmp.alloc(&dtcf, (size_t)ntiles));
-    COMAP_CHECK(ctx, comap_upload(dtcf, tcf.data(), 4 * tcf.size(), st));
-    COMAP_CHECK(ctx, tmp.alloc(&dch_tile, (size_t)nchunk + 1));
-    COMAP_CHECK(ctx, tmp.alloc(&dch_seg0, (size_t)nchunk + 1));
-    COMAP_CHECK(ctx, tmp.alloc(&cw, (size_t)nchunk + 1));
-    if (dalloc(ctx, &d->tcbase, nchunk + 1) || dalloc(ctx, &d->tslot, nchunk * 64) ||
-        dalloc(ctx, &d->twg, std::max<size_t>(wg.size(), 2)) || dalloc(ctx, &d->tcend, ntiles))
-        return -2;
-    if (nchunk) {
-        COMAP_CHECK(ctx, comap_upload(dch_tile, ch_tile.data(), 4 * ch_tile.size(), st));
-        COMAP_CHECK(ctx, comap_upload(dch_seg0, ch_seg0.data(), 4 * ch_seg0.size(), st));
-    }
-    if (!wg.empty()) COMAP_CHECK(ctx, comap_upload(d->twg, wg.data(), 4 * wg.size(), st));
-    COMAP_CHECK(ctx, comap_upload(d->tcend, tcend.data(), 4 * tcend.size(), st));
-    k_tile_chunk_width<<<(unsigned)(((nchunk + 1) * 64 + 255) / 256), 256, 0, st>>>(dch_tile, dch_seg0, tfirst, seg_first,
-                                                                              nseg, nnz, nchunk, cw);
-    COMAP_LAUNCH_CHECK(ctx);
-    size_t tb4 = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb4, cw, d->tcbase, (int)(nchunk + 1), st);
-    char *cub4 = nullptr;
-    COMAP_CHECK(ctx, tmp.alloc(&cub4, tb4 + 256));
-    COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(cub4, tb4, cw, d->tcbase, (int)(nchunk + 1), st));
-    int64_t nslots = 0;
-    COMAP_CHECK(ctx, hipMemcpyAsync(&nslots, d->tcbase + nchunk, 8, hipMemcpyDeviceToHost, st));
-    COMAP_CHECK(ctx, hipStreamSynchronize(st));
-    if (dalloc(ctx, &d->tent, std::max<int64_t>(nslots, 1))) return -2;
-    if (!d->cf && dalloc(ctx, &d->tentw, std::max<int64_t>(nslots, 1) * nb)) return -2;
-    if (nchunk) {
-        const unsigned gch = (unsigned)((nchunk * 64 + 255) / 256);
-        k_tile_slots<<<gch, 256, 0, st>>>(dch_tile, dch_seg0, tfirst, seg_slot, nchunk, d->tslot);
-        COMAP_CHECK(ctx, hipMemsetAsync(d->tent, 0xff, 8 * (size_t)nslots, st));     // padding
-        if (d->cf) {
-            COMAP_NB_SWITCH(nb, (k_tile_fill<NB, true><<<grid_for(nnz, 16384), 256, 0, st>>>(
-                                    sid, seg_tile, seg_first, tfirst, dtcf, sval, d->opix, d->ocnt, g, nnz, d->tcbase,
-                                    d->tent, d->tentw)));
-        } else {
-            COMAP_NB_SWITCH(nb, (k_tile_fill<NB, false><<<grid_for(nnz, 16384), 256, 0, st>>>(
-                                    sid, seg_tile, seg_first, tfirst, dtcf, sval, d->opix, d->ow, g, nnz, d->tcbase,
-                                    d->tent, d->tentw)));
-        }
-        COMAP_LAUNCH_CHECK(ctx);
-    }
-    d->nx = nx;
-    d->ntx = g.ntx;
-    d->nty = nty;
-    d->tile_w = g.tw;
-    d->tile_h = g.th;
-    d->nseg = nseg;
-    d->nchunk_t = nchunk;
-    d->nwg_t = (int64_t)wg.size() / 2;
-    d->tiles = d->nwg_t > 0;
-    return 0;
-}
-
-extern "C" int64_t comap_destripe_tile_segments(const comap_destriper *d) { return d && d->tiles ? d->nseg : -1; }
 
 extern "C" int comap_destripe_nnz(const comap_destriper *d, int64_t *nnz_offset_major, int64_t *nnz_pixel_major)
 {

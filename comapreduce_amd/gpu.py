@@ -238,8 +238,8 @@ class GPUObservation:
         if nV == 0:
             return None, None
         # comap_l1_vane zeroes both before its kernel writes them (no-vane rows stay 0)
-        tsys = torch.empty((nV, self.F, N_BANDS, N_CHANNELS), dtype=torch.float64, device=self.tdev)
-        gain = torch.empty_like(tsys)
+        tsys = N.device_empty((nV, self.F, N_BANDS, N_CHANNELS), torch.float64, self.tdev)
+        gain = N.device_empty(tuple(tsys.shape), torch.float64, self.tdev)
         self._bind()
         # The band-average windows are copied first (pinned, asynchronous), then pass A
         # (which does not depend on the vane) is queued behind them, so the host search
@@ -289,7 +289,7 @@ class GPUObservation:
         gn = to_device(gain0, torch.float64, self.tdev)
         # every sample is written by comap_l1_average (the units' by the reduction, the
         # rest -- scan gaps, a shard's foreign units -- zeroed there)
-        out = torch.empty((3, self.F, N_BANDS, self.T), dtype=torch.float64, device=self.tdev)
+        out = N.device_empty((3, self.F, N_BANDS, self.T), torch.float64, self.tdev)
         self._bind()
         N.check(N.lib().comap_l1_average(self.plan, N.dptr(fit), N.dptr(ts), N.dptr(gn), int(bool(calibrator)),
                                          N.dptr(out[0]), N.dptr(out[1]), N.dptr(out[2])), self.ctx,
@@ -316,7 +316,7 @@ class GPUObservation:
         wd = to_device(np.ascontiguousarray(w), torch.float64, self.tdev)
         sd = to_device(np.ascontiguousarray(wsum), torch.float64, self.tdev)
         gn = to_device(gain0, torch.float64, self.tdev)
-        out = torch.empty((2, self.F, N_BANDS, nb, self.T), dtype=torch.float64, device=self.tdev)
+        out = N.device_empty((2, self.F, N_BANDS, nb, self.T), torch.float64, self.tdev)
         self._bind()
         N.check(N.lib().comap_l1_channel_bin(self.plan, int(bin_size), N.dptr(wd), N.dptr(gn), N.dptr(sd),
                                              N.dptr(out[0]), N.dptr(out[1])), self.ctx, 'comap_l1_channel_bin')

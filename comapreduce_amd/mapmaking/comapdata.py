@@ -259,18 +259,36 @@ def read_comap_data_bands(filelist, map_info, bands=(0, 1, 2, 3), use_gain_filte
 
 class _LazyOutputs(dict):
     """read_comap_data_bands' result dict with entries computed on first access (a host
-    copy the caller may never need)."""
+    copy the caller may never need).  Every way of reading the dict goes through
+    __getitem__: iteration (so dict(r) / {**r} take the keys() + [] path instead of
+    copying the raw slots), copy, pop, popitem, setdefault and pickling resolve the
+    pending entries first; a pending slot holds a sentinel, never a plausible value."""
+
+    class _Pending:
+        def __repr__(self):
+            return '<pending lazy value>'
 
     def lazy(self, key, fn):
         self._lazy = getattr(self, '_lazy', {})
         self._lazy[key] = fn
-        dict.__setitem__(self, key, None)
+        dict.__setitem__(self, key, _LazyOutputs._Pending())
 
-    def __getitem__(self, key):
+    def _resolve(self, key):
         fns = getattr(self, '_lazy', {})
         if key in fns:
             dict.__setitem__(self, key, fns.pop(key)())
+
+    def resolve_all(self):
+        for k in list(getattr(self, '_lazy', {})):
+            self._resolve(k)
+        return self
+
+    def __getitem__(self, key):
+        self._resolve(key)
         return dict.__getitem__(self, key)
+
+    def __iter__(self):
+        return iter(list(dict.keys(self)))
 
     def get(self, key, default=None):
         return self[key] if key in self else default
@@ -280,3 +298,21 @@ class _LazyOutputs(dict):
 
     def values(self):
         return [self[k] for k in list(self.keys())]
+
+    def copy(self):
+        return dict(self.resolve_all().items())
+
+    def pop(self, key, *default):
+        self._resolve(key)
+        return dict.pop(self, key, *default)
+
+    def popitem(self):
+        self.resolve_all()
+        return dict.popitem(self)
+
+    def setdefault(self, key, default=None):
+        self._resolve(key)
+        return dict.setdefault(self, key, default)
+
+    def __reduce__(self):
+        return (dict, (dict(self.resolve_all().items()),))

@@ -44,19 +44,55 @@ def torch_allreduce(t):
     return t
 
 
+class TimedAllreduce:
+    """torch_allreduce with every call bracketed by HIP events on the current stream (the
+    stream the CG kernels run on, which waits for the collective): the measured
+    all-reduce time and bytes per CG iteration that mapmaking/rankplan.py's alpha / beta
+    are calibrated from (bench.py, N > 1).  The first ``skip`` calls (the set-up sums of
+    h, the naive numerator and rr0 in cg_solve_batched) are recorded apart."""
+
+    def __init__(self, skip=3):
+        self.calls, self.skip = [], skip
+
+    def __call__(self, t):
+        import torch
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        torch_allreduce(t)
+        e1.record()
+        self.calls.append((t.numel() * t.element_size(), e0, e1))
+        return t
+
+    def summary(self, iterations):
+        import torch
+        torch.cuda.synchronize()
+        body = self.calls[self.skip:]
+        ms = [a.elapsed_time(b) for _, a, b in body]
+        it = max(int(iterations), 1)
+        per = len(body) // it if body else 0
+        sizes = [n for n, _, _ in body[:per]]
+        by_call = [sum(ms[k::per]) / it for k in range(per)] if per else []
+        return {'iterations': it, 'calls_per_iter': per, 'bytes_per_call': sizes,
+                'ms_per_call': by_call, 'allreduce_ms_per_iter': sum(ms) / it,
+                'bytes_per_iter': sum(sizes)}
+
+
 def compact_pixels(pix, npix, allreduce):
-    """(pixel ids relabelled onto the union over ranks of the hit pixels, int32 with
-    -1 kept; the union's pixel ids, increasing).  Pixel npix - 1 is always in the
-    union (the off-map m[-1] reads of Destriper.py:206-213 then land on the union's
-    last slot).  pix: int64 torch tensor on any device; allreduce sums in place."""
+    """(pixel ids relabelled onto the union over ranks of the pixels the operator touches,
+    int32; the union's pixel ids, increasing).  The union holds every binned pixel and
+    every pixel an unbinned sample reads: op_Z reads m[pointing] (Destriper.py:206-213),
+    so a negative id p reads pixel npix + p.  Such a sample keeps a negative id in the
+    compacted map of nc pixels, cid[npix + p] - nc, which reads the same pixel there.
+    pix: int64 torch tensor on any device (ids in [-npix, npix)); allreduce sums in place."""
     import torch
+    read = torch.remainder(pix, npix)            # the pixel each sample bins or reads
     hit = torch.zeros(npix, dtype=torch.int32, device=pix.device)
-    hit[pix[pix >= 0]] = 1
-    hit[npix - 1] = 1
+    hit[read] = 1
     allreduce(hit)
     keep = hit > 0
     cid = torch.cumsum(keep.to(torch.int64), 0) - 1
-    comp = torch.where(pix >= 0, cid[pix.clamp(min=0)], torch.full_like(pix, -1))
+    nc = int(keep.sum().item())
+    comp = torch.where(pix >= 0, cid[read], cid[read] - nc)
     return comp.to(torch.int32), torch.nonzero(keep).reshape(-1)
 
 
@@ -231,7 +267,7 @@ class DeviceOps:
     N/L]) marks the offsets each band's data prep kept.  Per-band vectors are
     interleaved band-fastest ([N/L][nb], [npix][nb])."""
 
-    def __init__(self, pixels, tod, weights, offset_length, npix, device=None, keep=None, map_shape=None):
+    def __init__(self, pixels, tod, weights, offset_length, npix, device=None, keep=None):
         import torch
         self.torch = torch
         device = N.current_device() if device is None else int(device)
@@ -270,18 +306,10 @@ class DeviceOps:
                                                  None if kp is None else N.dptr(kp), n, self.L, self.npix,
                                                  self.nb, ctypes.byref(h))
         if rc == -3:
-            raise IndexError(f'pixel index out of range for a map of {npix} pixels')
+            raise IndexError(f'pixel index out of range for a map of {npix} pixels (valid: -{npix} .. {npix - 1})')
         N.check(rc, self.ctx, 'comap_destripe_create_bands')
         self.h = h
         self.n_offsets = int(N.lib().comap_destripe_n_offsets(h))
-        # map-tile projection (comap_destripe_tiles) for a row-major map of known width:
-        # COMAP_DS_TILES=1 / 0 forces it on / off, by default from TILE_MIN_OFFSETS offsets
-        te = os.environ.get('COMAP_DS_TILES')
-        if map_shape is not None and (te == '1' or (te is None and self.n_offsets >= TILE_MIN_OFFSETS)):
-            ny, nx = (int(v) for v in map_shape)
-            if ny * nx != self.npix:
-                raise ValueError(f'map_shape {map_shape} does not hold {self.npix} pixels')
-            N.check(N.lib().comap_destripe_tiles(h, nx), self.ctx, 'comap_destripe_tiles')
 
     def _t(self, a, dt):
         torch = self.torch
@@ -329,14 +357,10 @@ class DeviceOps:
         """Padded entries of the projection's sliced-ELLPACK rows (-1: none)."""
         return int(N.lib().comap_destripe_sell_entries(self.h))
 
-    def tile_segments(self):
-        """(offset, map tile) segments of the tile projection (-1: not in use)."""
-        return int(N.lib().comap_destripe_tile_segments(self.h))
-
     # ---- vector helpers
     def empty(self, n):
         """[n] float64 on the device, uninitialised (for outputs a call writes in full)."""
-        return self.torch.empty(n, dtype=self.torch.float64, device=self.dev)
+        return N.device_empty(n, self.torch.float64, self.dev)
 
     def zeros(self, n):
         return self.torch.zeros(n, dtype=self.torch.float64, device=self.dev)
@@ -467,7 +491,7 @@ class DeviceOps:
         torch = self.torch
         nb, npix, nbo = self.nb, self.npix, self.n_bands
         cur = torch.cuda.current_stream(self.dev)
-        m = torch.empty((4, npix * nb), dtype=torch.float64, device=self.dev)    # map, naive, weight, hits
+        m = N.device_empty((4, npix * nb), torch.float64, self.dev)              # map, naive, weight, hits
         nn = self.empty(npix * nb)                                              # local_maps copies it in full
         self._c('comap_destripe_local_maps', self.h, N.dptr(m[2]), N.dptr(m[3]), N.dptr(nn))
         self._c('comap_destripe_div_map', self.h, N.dptr(nn), None, N.dptr(m[1]))
@@ -495,7 +519,6 @@ class DeviceOps:
         return x, [int(v) for v in it][:nbo], maps
 
 
-TILE_MIN_OFFSETS = 1 << 62     # map-tile projection: opt-in until measured (COMAP_DS_TILES=1)
 _COPY_STREAMS = {}
 
 
@@ -527,9 +550,8 @@ class DeviceDestriper:
     sharded).  The default is COMAP_DS_RANKS=shard until a multi-GPU run replaces the
     model's assumed all-reduce latency and bandwidth; gather forces the other."""
 
-    def __init__(self, pixels, tod, weights, offset_length, npix, device=None, keep=None, map_shape=None):
+    def __init__(self, pixels, tod, weights, offset_length, npix, device=None, keep=None):
         self.npix_full, self.hit_index = int(npix), None
-        self.map_shape = map_shape
         self.multi = np.ndim(tod) == 2 if not hasattr(tod, 'dim') else tod.dim() == 2
         self.gathered, self.plan = None, None
         d = _dist()
@@ -539,8 +561,7 @@ class DeviceDestriper:
                 return
             if os.environ.get('COMAP_DS_COMPACT', '1') != '0':
                 pixels, npix = self._compact(pixels, int(npix), device)
-                map_shape = None                 # the relabelled pixels have no map layout
-        self.ops = N.retry_oom(DeviceOps, pixels, tod, weights, offset_length, npix, device, keep, map_shape)
+        self.ops = N.retry_oom(DeviceOps, pixels, tod, weights, offset_length, npix, device, keep)
 
     # ---- rank policy
     def _choose_gather(self, d, pixels, tod, offset_length):
@@ -606,7 +627,7 @@ class DeviceDestriper:
         k_all = cat(kp, L) if kp is not None else None
         if not self.multi:
             t_all, w_all = t_all.reshape(-1), w_all.reshape(-1)
-        self.ops = DeviceOps(p_all, t_all, w_all, L, npix, device, k_all, self.map_shape)
+        self.ops = DeviceOps(p_all, t_all, w_all, L, npix, device, k_all)
         self._ref = (device, nbands)
 
     def _solve_gathered(self, d, threshold, niter):
@@ -650,16 +671,16 @@ class DeviceDestriper:
         (Destriper.py:183-204); only pixels some rank's samples hit can be non-zero.
         Relabel the pixels onto that union, in increasing pixel order, so every
         all-reduce carries the hit pixels only ("compact to hit pixels").
-        The relabelling is monotone, and pixel npix - 1 is always kept (off-map
-        samples read m[-1], Destriper.py:206-213): the per-pixel sums, the offsets'
-        spatial order and hence every iterate are unchanged, bit for bit.  Maps are
+        The relabelling is monotone, and the pixels that unbinned samples read are kept
+        (a negative id p reads m[npix + p], Destriper.py:206-213): the per-pixel sums, the
+        offsets' spatial order and hence every iterate are unchanged, bit for bit.  Maps are
         expanded back to npix in solve()."""
         import torch
         dev = torch.device('cuda', N.current_device() if device is None else int(device))
         pix = pixels.to(device=dev, dtype=torch.int64).reshape(-1) if isinstance(pixels, torch.Tensor) else \
             torch.from_numpy(np.ascontiguousarray(pixels, dtype=np.int64)).to(dev).reshape(-1)
-        if pix.numel() and int(pix.max().item()) >= npix:
-            raise IndexError(f'pixel index {int(pix.max().item())} out of range for a map of {npix} pixels')
+        if pix.numel() and (int(pix.max().item()) >= npix or int(pix.min().item()) < -npix):
+            raise IndexError(f'pixel index out of range for a map of {npix} pixels (valid: -{npix} .. {npix - 1})')
         comp, self.hit_index = compact_pixels(pix, npix, torch_allreduce)
         return comp, int(self.hit_index.numel())
 
@@ -681,12 +702,11 @@ class DeviceDestriper:
     def sell_entries(self):
         return self.ops.sell_entries()
 
-    def tile_segments(self):
-        return self.ops.tile_segments()
-
-    def solve(self, threshold=1e-6, niter=100, to_host=False):
+    def solve(self, threshold=1e-6, niter=100, to_host=False, allreduce=None):
         """to_host: maps as host NumPy arrays (rank 0; None on the others) -- one
-        rank solving alone overlaps their copy with the CG (solve_native_host)."""
+        rank solving alone overlaps their copy with the CG (solve_native_host).
+        allreduce: the sharded CG's sum across ranks (default torch_allreduce; bench.py
+        passes a TimedAllreduce to measure the per-iteration collective cost)."""
         d = _dist()
         ops = self.ops
         if to_host and self.gathered is None and (d is None or d.get_world_size() == 1):
@@ -719,7 +739,7 @@ class DeviceDestriper:
                     import warnings
                     warnings.warn(f'COMAP_DS_GRAPH=1 needs the nccl (RCCL) backend, not {d.get_backend()}: '
                                   'using the eager CG driver')
-            x, it, h, nnum = solver(ops, torch_allreduce, threshold, niter)
+            x, it, h, nnum = solver(ops, allreduce or torch_allreduce, threshold, niter)
             _, hits, _ = ops.local_maps()
             torch_allreduce(hits)
             num = ops.zeros(ops.npix * ops.nb)

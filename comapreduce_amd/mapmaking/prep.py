@@ -81,13 +81,14 @@ class FlatArrays:
     def __init__(self, torch, dev, nb, n):
         # uninitialised: the gather kernel writes every sample of every file's rows (zeros for
         # skipped feeds) and the cut writes every kept sample; zero_range covers the rest
-        f64 = dict(dtype=torch.float64, device=dev)
-        self.tod = torch.empty((nb, n), **f64)
-        self.w = torch.empty((nb, n), **f64)
-        self.az, self.el, self.ra, self.dec = (torch.empty(n, **f64) for _ in range(4))
-        self.feedid = torch.empty(n, dtype=torch.int64, device=dev)
-        self.obsid = torch.empty(n, dtype=torch.int64, device=dev)
-        self.pix = torch.empty(n, dtype=torch.int32, device=dev)
+        # (N.device_empty: COMAP_POISON=1 fills them with NaN / -1 to prove that claim)
+        E, f8 = N.device_empty, torch.float64
+        self.tod = E((nb, n), f8, dev)
+        self.w = E((nb, n), f8, dev)
+        self.az, self.el, self.ra, self.dec = (E(n, f8, dev) for _ in range(4))
+        self.feedid = E(n, torch.int64, dev)
+        self.obsid = E(n, torch.int64, dev)
+        self.pix = E(n, torch.int32, dev)
         self.n = n
 
     def zero_range(self, a, b):
@@ -258,7 +259,7 @@ def prep_flat(files, filelist, map_info, bands, use_gain_filter, offset_length, 
         rr, rs, pr, dsc, drs, dps, drf, drc, dlive = _dev_pack(
             torch, dev, (rms_rows, rms_scale, row_src[live].astype(np.int32), scans, row_src, pix_src, row_feed,
                          row_cal, live.astype(np.int64)))
-        rms = torch.empty(max(1, rms_rows.size), dtype=torch.float64, device=dev)
+        rms = N.device_empty(max(1, rms_rows.size), torch.float64, dev)
         mark('file_meta')
         N.check(lib.comap_prep_auto_rms(c, N.dptr(tod), T, N.dptr(rr), N.dptr(rs), int(rms_rows.size), T,
                                         N.dptr(rms)), c, 'comap_prep_auto_rms')

@@ -27,7 +27,7 @@ def spike_mask(tod, scan_edges, medfilt_window=100, step=100, threshold=10.0, de
     t = to_device(tod, torch.float64, dev)
     F, B, T = t.shape
     edges = np.ascontiguousarray(np.asarray(to_host(scan_edges), dtype=np.int64).reshape(-1, 2))
-    mask = torch.empty((F, B, T), dtype=torch.uint8, device=dev)
+    mask = N.device_empty((F, B, T), torch.uint8, dev)
     c = N.ctx(device)
     N.bind_stream(c, dev)
     N.check(N.lib().comap_spikes(c, N.dptr(t), F * B, T, N.hptr(edges, ctypes.c_int64), edges.shape[0],

@@ -323,50 +323,65 @@ def level2_mapmaking(obs_id: int, n_feeds: int = 19, n_samples: int = 45_000, sk
     return data, attrs, filename
 
 
+C5_AMP_DEG = 3.8      # C5 Lissajous half-width: inside the 480 x 1' map's +-4.0 deg (every sample on-map)
+
+
 def destriper_inputs_device(n_obs: int, n_feeds: int = 19, n_samples: int = 180_000, offset_length: int = 50,
                             nx: int = 480, ny: int = 480, cdelt: float = 1.0 / 60.0, device: int = 0, seed: int = 0,
-                            n_bands: int = 1):
+                            n_bands: int = 1, amp: float = C5_AMP_DEG, obs0: int = 0):
     """Destriper inputs at the SURVEY.md §8(d) C5 scale, generated on the device
-    (bench only): n_obs observations x n_feeds feeds x n_samples samples,
-    each (obs, feed) series cut to a multiple of offset_length; Lissajous
-    pointing over an nx x ny CAR field (pixel = floor(x + 0.5), off-map -> -1),
-    smooth sky + random-walk (1/f) offsets + white noise, inverse-variance
-    weights.  Returns (pixels int32 [N], tod f64, weights f64) CUDA tensors;
-    tod / weights are [N] for n_bands = 1, else [n_bands, N] (the same sky and
-    pointing, independent offsets and noise per band)."""
-    if n_bands > 1:
-        pix, t0, w0 = destriper_inputs_device(n_obs, n_feeds, n_samples, offset_length, nx, ny, cdelt, device, seed)
-        import torch
-        tods, ws = [t0], [w0]
-        for b in range(1, n_bands):
-            _, tb, wb = destriper_inputs_device(n_obs, n_feeds, n_samples, offset_length, nx, ny, cdelt, device,
-                                                seed + 7919 * b)
-            tods.append(tb)
-            ws.append(wb)
-        return pix, torch.stack(tods), torch.stack(ws)
-    import math
+    (bench only): observations obs0 .. obs0 + n_obs - 1 of a field, each n_feeds feeds x
+    n_samples samples, every (obs, feed) series cut to a multiple of offset_length;
+    Lissajous pointing of half-width ``amp`` degrees over an nx x ny CAR field (pixel =
+    floor(x + 0.5), off-map -> -1), smooth sky + random-walk (1/f) offsets + white
+    noise, inverse-variance weights.  Returns (pixels int32 [N], tod f64, weights f64)
+    CUDA tensors; tod / weights are [N] for n_bands = 1, else [n_bands, N] (the same sky
+    and pointing, independent offsets and noise per band).  Every observation is drawn
+    from its own generator, so a rank generating observations [obs0, obs0 + n) of a
+    field gets exactly those observations' samples of the whole field.
+
+    The default half-width (3.8 deg on the +-4.0 deg map) keeps every sample on the
+    map.  Rounds 2-4 drew 4.2 deg: ~37 % of the samples then fell off the map and, as
+    the reference's op_Z does (Destriper.py:206-213), gathered m[-1] in the projection
+    without being binned -- a non-symmetric operator on which the (p == pb) BiCG does
+    not converge (the round-5 probe)."""
     import torch
+    if n_bands > 1:
+        pix, t0, w0 = destriper_inputs_device(n_obs, n_feeds, n_samples, offset_length, nx, ny, cdelt, device, seed,
+                                              amp=amp, obs0=obs0)
+        tods = torch.empty((n_bands,) + tuple(t0.shape), dtype=torch.float64, device=t0.device)
+        ws = torch.empty_like(tods)
+        tods[0], ws[0] = t0, w0
+        del t0, w0
+        for b in range(1, n_bands):
+            _, tods[b], ws[b] = destriper_inputs_device(n_obs, n_feeds, n_samples, offset_length, nx, ny, cdelt,
+                                                        device, seed + 7919 * b, amp=amp, obs0=obs0)
+        return pix, tods, ws
+    import math
     dev = torch.device('cuda', device)
-    g = torch.Generator(device=dev)
-    g.manual_seed(int(seed))
     n = n_samples // offset_length * offset_length
-    S = n_obs * n_feeds
-    t = torch.arange(n, device=dev, dtype=torch.float64)[None, :]
-    k = torch.arange(S, device=dev, dtype=torch.float64)[:, None]
-    ra = 4.2 * torch.sin(2 * math.pi * t / (1250.0 + 7.0 * k) + 0.37 * k)       # degrees from the field centre
-    dec = 4.2 * torch.sin(2 * math.pi * t / (1700.0 + 5.0 * k) + 1.1 * k)
-    px = torch.floor(-ra / cdelt + (nx / 2 - 1) + 0.5)
-    py = torch.floor(dec / cdelt + (ny / 2 - 1) + 0.5)
-    ok = (px >= 0) & (px <= nx - 1) & (py >= 0) & (py <= ny - 1)
-    pix = torch.where(ok, py * nx + px, torch.full_like(px, -1)).to(torch.int32)
-    del px, py, ok
-    sky = 0.05 * torch.sin(2.1 * ra) * torch.cos(1.7 * dec)
-    del ra, dec
     no = n // offset_length
-    steps = torch.randn((S, no), generator=g, device=dev, dtype=torch.float64) * 2e-3
-    sky += torch.cumsum(steps, dim=1).repeat_interleave(offset_length, dim=1)
-    del steps
-    sigma = 4e-3 + 2e-3 * torch.rand((S, 1), generator=g, device=dev, dtype=torch.float64)
-    sky += sigma * torch.randn((S, n), generator=g, device=dev, dtype=torch.float64)
-    w = (1.0 / sigma ** 2).expand(S, n).contiguous()
-    return pix.reshape(-1), sky.reshape(-1), w.reshape(-1)
+    S = n_obs * n_feeds
+    pix = torch.empty((S, n), dtype=torch.int32, device=dev)
+    tod = torch.empty((S, n), dtype=torch.float64, device=dev)
+    w = torch.empty((S, n), dtype=torch.float64, device=dev)
+    t = torch.arange(n, device=dev, dtype=torch.float64)[None, :]
+    g = torch.Generator(device=dev)
+    for j, o in enumerate(range(obs0, obs0 + n_obs)):
+        g.manual_seed(int(seed) * 1_000_003 + o)
+        rows = slice(j * n_feeds, (j + 1) * n_feeds)
+        k = torch.arange(o * n_feeds, (o + 1) * n_feeds, device=dev, dtype=torch.float64)[:, None]
+        ra = amp * torch.sin(2 * math.pi * t / (1250.0 + 7.0 * k) + 0.37 * k)       # degrees from the field centre
+        dec = amp * torch.sin(2 * math.pi * t / (1700.0 + 5.0 * k) + 1.1 * k)
+        px = torch.floor(-ra / cdelt + (nx / 2 - 1) + 0.5)
+        py = torch.floor(dec / cdelt + (ny / 2 - 1) + 0.5)
+        ok = (px >= 0) & (px <= nx - 1) & (py >= 0) & (py <= ny - 1)
+        pix[rows] = torch.where(ok, py * nx + px, torch.full_like(px, -1)).to(torch.int32)
+        sky = 0.05 * torch.sin(2.1 * ra) * torch.cos(1.7 * dec)
+        steps = torch.randn((n_feeds, no), generator=g, device=dev, dtype=torch.float64) * 2e-3
+        sky += torch.cumsum(steps, dim=1).repeat_interleave(offset_length, dim=1)
+        sigma = 4e-3 + 2e-3 * torch.rand((n_feeds, 1), generator=g, device=dev, dtype=torch.float64)
+        sky += sigma * torch.randn((n_feeds, n), generator=g, device=dev, dtype=torch.float64)
+        tod[rows] = sky
+        w[rows] = 1.0 / sigma ** 2
+    return pix.reshape(-1), tod.reshape(-1), w.reshape(-1)

@@ -207,9 +207,11 @@ int comap_synth_tod(comap_ctx *ctx, int32_t n_feeds, int32_t feed0, int64_t n_sa
 
 /* ------------------------------------------------------------ destriper */
 /* Destriper problem on one rank (MapMaking/Destriper.py:155-263): samples
- * [N] with int32 pixel (-1 = off-map), f64 tod and weights, N a multiple of
- * offset_length (<= 256; calibrators use 250), map of npix pixels.  Builds the constant
- * offset<->pixel sparse operator and the sample-level maps once. */
+ * [N] with int32 pixel, f64 tod and weights, N a multiple of offset_length (<= 256;
+ * calibrators use 250), map of npix pixels.  A negative pixel p (-1 = off-map) is never
+ * binned, and its sample's projection reads m[npix + p] -- numpy's wrap in the
+ * reference's m[pointing] (Destriper.py:206-213).  Builds the constant offset<->pixel
+ * sparse operator and the sample-level maps once. */
 int comap_destripe_create(comap_ctx *ctx, const int32_t *pixels_dev, const double *tod_dev,
                           const double *weights_dev, int64_t n_samples, int32_t offset_length,
                           int64_t npix, comap_destriper **out);
@@ -226,8 +228,8 @@ int comap_destripe_create(comap_ctx *ctx, const int32_t *pixels_dev, const doubl
  * sorted) order; every offset vector the functions below take or return is in
  * that order, except the x of comap_destripe_solve, which is in the caller's
  * order.  comap_destripe_offsets_natural converts an internal vector.
- * Returns -3 when a pixel index is >= npix (checked on the device by the set-up's
- * count pass; the reference would raise IndexError binning it). */
+ * Returns -3 when a pixel index is >= npix or < -npix (checked on the device by the
+ * set-up's count pass; the reference raises IndexError there, binning or reading m). */
 int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pixels_dev, const double *tod_dev,
                                 const double *weights_dev, const uint8_t *keep_dev, int64_t n_samples,
                                 int32_t offset_length, int64_t npix, int32_t n_bands, comap_destriper **out);
@@ -244,14 +246,6 @@ int32_t comap_destripe_entry_bytes(const comap_destriper *d);
 /* Padded entries of the projection's sliced-ELLPACK row copy (COMAP_DS_SELL=1; chunks of
  * 64 offsets padded to their longest row), or -1 when the problem has none. */
 int64_t comap_destripe_sell_entries(const comap_destriper *d);
-/* Map-tile projection (optional, after create): the map is laid out in rows of nx pixels
- * (CAR / WCS maps, p = y nx + x).  The projection then stages one tile of the map (32 KB:
- * 32 x 32 pixels for 4 bands, 64 x 32 for 2, 64 x 64 for 1) in LDS per workgroup and sums
- * each (offset, tile) segment of the offset rows from there; a combine pass adds an
- * offset's segments in tile order.  Synchronises the host.  _tile_segments: the number of
- * (offset, tile) segments, or -1 without tiles. */
-int comap_destripe_tiles(comap_destriper *d, int64_t nx);
-int64_t comap_destripe_tile_segments(const comap_destriper *d);
 /* Local (this rank) sample-level maps, summed in binValues order:
  * h = sum w, hits = sum 1, naive_num = sum w tod (any may be NULL). */
 int comap_destripe_local_maps(comap_destriper *d, double *h_dev, double *hits_dev, double *naive_num_dev);

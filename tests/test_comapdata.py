@@ -340,3 +340,23 @@ def test_oracle_many_scans_runs(case_store):
     case = cc.CASES['car']
     res = oc.read_comap_data(names, store, map_info(case['map']), feeds=cc.FEEDS, **case['kw'])
     assert S > 64 and res[0].size > 0 and res[0].size % 50 == 0
+
+
+def test_lazy_outputs_resolve_on_every_read_path():
+    """read_comap_data_bands' one-rank device-output dict forms remapping_array on first
+    read; dict(r), {**r}, copy, pop, iteration and pickling must all see the value,
+    never a placeholder."""
+    import pickle
+    from comapreduce_amd.mapmaking.comapdata import _LazyOutputs
+
+    def make(v):
+        r = _LazyOutputs({'tod': 1})
+        r.lazy('remapping_array', lambda: v)
+        return r
+    assert dict(make(1))['remapping_array'] == 1
+    assert {**make(2)}['remapping_array'] == 2
+    assert make(3).copy()['remapping_array'] == 3
+    assert make(4).pop('remapping_array') == 4
+    assert pickle.loads(pickle.dumps(make(5)))['remapping_array'] == 5
+    assert [make(6)[k] for k in make(6)] == [1, 6]
+    assert dict(make(7).items())['remapping_array'] == 7
