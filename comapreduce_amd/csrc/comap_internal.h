@@ -178,6 +178,9 @@ struct MedPlan {
     void *krange = nullptr;      // dev [njobs][2] u64: per-series key min, max (proxy scaling)
     void *temp = nullptr;
     size_t temp_bytes = 0;
+    int64_t numax = 0;           // longest sort segment (the block sort takes those <= kBlockSortMax)
+    bool blocksort = true;       // segments sorted whole in LDS by one workgroup (k_med_blocksort)
+    hipEvent_t plan_ev = nullptr;         // recorded on alloc_stream after the plan's uploads
     hipStream_t alloc_stream = nullptr;   // its buffers come from the device pool on this stream
     hipStream_t run_stream = nullptr;     // the stream of its last comap_median_run (their last use)
 };

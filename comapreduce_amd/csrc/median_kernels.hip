@@ -34,6 +34,7 @@
 #include "comap_internal.h"
 
 #include <hipcub/hipcub.hpp>
+#include <rocprim/block/block_radix_sort.hpp>
 #include <rocprim/device/device_segmented_radix_sort.hpp>
 
 #include <algorithm>
@@ -1091,6 +1092,68 @@ hipError_t seg_sort(void *tmp, size_t &tb, const K *k0, K *k1, const int32_t *v0
                                                               beg, end, 0u, end_bit, st);
 }
 
+// Segments of up to kBlockSortMax elements are sorted whole in LDS by one 1024-thread
+// workgroup: proxies computed from the values (k_med_keys' map), a block radix sort of
+// (proxy, position) pairs on the pbits significant bits (rocprim block_radix_sort, 8-bit
+// match ranking: pbits / 8 passes through LDS instead of through HBM), written as the
+// sorted keys / positions the fix-up reads.  Stable (blocked input = position order), so
+// the result equals the segmented device sort's.  Longer segments get their keys written
+// and a [begin, end) range for that sort (empty ranges for the others).
+constexpr int kBsThreads = 1024, kBsItems = 16;
+constexpr int64_t kBlockSortMax = (int64_t)kBsThreads * kBsItems;
+__global__ void __launch_bounds__(kBsThreads) k_med_blocksort(const MedJob *__restrict__ jobs,
+                                                              const int32_t *__restrict__ seg, int32_t njobs, int32_t w,
+                                                              const unsigned long long *__restrict__ kr,
+                                                              const int32_t *__restrict__ slo, int pbits,
+                                                              uint32_t *__restrict__ k0, int32_t *__restrict__ v0,
+                                                              uint32_t *__restrict__ k1, int32_t *__restrict__ v1,
+                                                              int32_t *__restrict__ beg, int32_t *__restrict__ end)
+{
+    using BS = rocprim::block_radix_sort<uint32_t, kBsThreads, kBsItems, int32_t>;
+    __shared__ typename BS::storage_type bst;
+    const int jb = blockIdx.x;
+    if (jb >= njobs) return;
+    const MedJob job = jobs[jb];
+    const int32_t s0 = seg[jb], ns = seg[jb + 1] - s0;
+    const int h = w / 2;
+    const int64_t base = job.out_lo - h;
+    const uint64_t kmin = kr[2 * jb];
+    const uint64_t range = kr[2 * jb + 1] - kmin;
+    const int bits = range ? 64 - __clzll((long long)range) : 0;
+    const int shift = bits > pbits ? bits - pbits : 0;
+    const bool large = ns > kBlockSortMax;
+    if (threadIdx.x == 0) {
+        beg[jb] = s0;
+        end[jb] = large ? s0 + ns : s0;
+    }
+    if (large) {        // the segmented device sort's input
+        for (int i = threadIdx.x; i < ns; i += kBsThreads) {
+            k0[s0 + i] = key32_of(key_of(seg_elem(job, slo, jb, base, h, i)), kmin, shift);
+            v0[s0 + i] = i;
+        }
+        return;
+    }
+    if (ns == 0) return;
+    uint32_t k[kBsItems];
+    int32_t v[kBsItems];
+#pragma unroll
+    for (int u = 0; u < kBsItems; ++u) {
+        const int i = threadIdx.x * kBsItems + u;         // blocked: position order = input order
+        v[u] = i;
+        // padding sorts last: all-ones in the sorted bits, after every real key (stable)
+        k[u] = i < ns ? key32_of(key_of(seg_elem(job, slo, jb, base, h, i)), kmin, shift) : 0xffffffffu;
+    }
+    BS().sort_to_striped(k, v, bst, 0, (unsigned)pbits);
+#pragma unroll
+    for (int u = 0; u < kBsItems; ++u) {
+        const int i = threadIdx.x + kBsThreads * u;       // striped: coalesced stores
+        if (i < ns) {
+            k1[s0 + i] = k[u];
+            v1[s0 + i] = v[u];
+        }
+    }
+}
+
 size_t walk_smem(int nwmax, int lt) { return 4 * (2 * (size_t)lt + 16) + 16 * (size_t)nwmax + 8 * (size_t)lt + 64; }
 
 }  // namespace
@@ -1135,6 +1198,8 @@ static int plan_slide(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
     COMAP_CHECK(ctx, comap_tmp_alloc((void **)&mp->segs, sizeof(SlideSeg) * std::max<size_t>(1, segs.size()), st));
     if (!jobs.empty()) COMAP_CHECK(ctx, comap_upload(mp->jobs, jobs.data(), sizeof(MedJob) * jobs.size(), st));
     if (!segs.empty()) COMAP_CHECK(ctx, comap_upload(mp->segs, segs.data(), sizeof(SlideSeg) * segs.size(), st));
+    COMAP_CHECK(ctx, hipEventCreateWithFlags(&mp->plan_ev, hipEventDisableTiming));
+    COMAP_CHECK(ctx, hipEventRecord(mp->plan_ev, st));
     const int sm = (int)slide_smem(w);
     COMAP_CHECK(ctx, hipFuncSetAttribute((const void *)k_med_slide<4>, hipFuncAttributeMaxDynamicSharedMemorySize, sm));
     COMAP_CHECK(ctx, hipFuncSetAttribute((const void *)k_med_slide<8>, hipFuncAttributeMaxDynamicSharedMemorySize, sm));
@@ -1270,6 +1335,11 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
         }
     }
     mp->nwmax = (int32_t)((nsmax + 31) / 32);
+    mp->numax = numax;
+    {
+        const char *be = getenv("COMAP_MEDIAN_BLOCKSORT");     // 0: every segment on the device-wide sort
+        mp->blocksort = !(be && be[0] == '0');
+    }
     mp->njobs = (int32_t)jobs.size();
     mp->nitems = seg.back();
     mp->nchunks = nchunks;
@@ -1307,6 +1377,10 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
     tb = std::max(tb, tb32);
     mp->temp_bytes = tb;
     COMAP_CHECK(ctx, alloc(&mp->temp, tb));
+    // the plan's uploads are ordered on alloc_stream only: a run on another stream waits
+    // for this event first (comap_median_run)
+    COMAP_CHECK(ctx, hipEventCreateWithFlags(&mp->plan_ev, hipEventDisableTiming));
+    COMAP_CHECK(ctx, hipEventRecord(mp->plan_ev, st));
     if (mp->wm) {
         COMAP_CHECK(ctx, hipFuncSetAttribute(mp->wmq ? (const void *)k_med_wm4 : (const void *)k_med_wm,
                                              hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1328,6 +1402,7 @@ void comap_median_plan_free(MedPlan *mp)
     // the last use is the last walk (whose stream waited for the plan's uploads on the
     // allocation stream): one event there guards every buffer's reuse
     comap_tmp_free_on(b, (int)(sizeof(b) / sizeof(b[0])), mp->run_stream ? mp->run_stream : mp->alloc_stream, false);
+    if (mp->plan_ev) (void)hipEventDestroy(mp->plan_ev);
     *mp = MedPlan();
 }
 
@@ -1336,6 +1411,7 @@ int comap_median_run(comap_ctx *ctx, MedPlan *mp, hipStream_t st)
     mp->run_stream = st;
     if (mp->slide) {
         if (mp->nsegs == 0) return 0;
+        if (mp->plan_ev && st != mp->alloc_stream) COMAP_CHECK(ctx, hipStreamWaitEvent(st, mp->plan_ev, 0));
         const size_t sm = slide_smem(mp->w);
         switch (mp->kper) {
         case 4: k_med_slide<4><<<mp->nsegs, kSlideThreads, sm, st>>>(mp->jobs, mp->segs, mp->w); break;
@@ -1347,6 +1423,7 @@ int comap_median_run(comap_ctx *ctx, MedPlan *mp, hipStream_t st)
         return 0;
     }
     if (mp->nchunks == 0) return 0;
+    if (mp->plan_ev && st != mp->alloc_stream) COMAP_CHECK(ctx, hipStreamWaitEvent(st, mp->plan_ev, 0));
     dim3 g1(64, (unsigned)mp->njobs);
     size_t tb = mp->temp_bytes;
     if (mp->key32) {
@@ -1355,11 +1432,21 @@ int comap_median_run(comap_ctx *ctx, MedPlan *mp, hipStream_t st)
         unsigned long long *kr = (unsigned long long *)mp->krange;
         k_med_range<<<mp->njobs, kRangeThreads, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, kr, mp->slo, flag);
         COMAP_LAUNCH_CHECK(ctx);
-        k_med_keys<uint32_t><<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, k0, mp->v0, kr, mp->slo,
-                                                 mp->pbits);
-        COMAP_LAUNCH_CHECK(ctx);
-        COMAP_CHECK(ctx, seg_sort(mp->temp, tb, (const uint32_t *)k0, k1, mp->v0, mp->v1, (int)mp->nitems, mp->njobs,
-                                  mp->seg, mp->seg + 1, st, mp->wide, (unsigned)mp->pbits));
+        if (mp->blocksort) {
+            // segments <= kBlockSortMax sorted in LDS; the longer ones (if any) by the device sort
+            k_med_blocksort<<<mp->njobs, kBsThreads, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, kr, mp->slo,
+                                                             mp->pbits, k0, mp->v0, k1, mp->v1, beg, end);
+            COMAP_LAUNCH_CHECK(ctx);
+            if (mp->numax > kBlockSortMax)
+                COMAP_CHECK(ctx, seg_sort(mp->temp, tb, (const uint32_t *)k0, k1, mp->v0, mp->v1, (int)mp->nitems,
+                                          mp->njobs, beg, end, st, mp->wide, (unsigned)mp->pbits));
+        } else {
+            k_med_keys<uint32_t><<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, k0, mp->v0, kr, mp->slo,
+                                                     mp->pbits);
+            COMAP_LAUNCH_CHECK(ctx);
+            COMAP_CHECK(ctx, seg_sort(mp->temp, tb, (const uint32_t *)k0, k1, mp->v0, mp->v1, (int)mp->nitems,
+                                      mp->njobs, mp->seg, mp->seg + 1, st, mp->wide, (unsigned)mp->pbits));
+        }
         k_med_fix<<<g1, 256, 0, st>>>(mp->jobs, mp->seg, mp->njobs, mp->w, k1, mp->v1, flag, mp->slo);
         COMAP_LAUNCH_CHECK(ctx);
         // the flagged segments (if any) again on exact 64-bit keys; the rest are empty ranges

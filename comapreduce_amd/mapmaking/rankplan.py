@@ -15,15 +15,35 @@ plan() compares the two for the expected iteration count and returns the faster.
 The a / b / s constants are fitted to this build's single-GPU measurements (bench.py
 C4 and C5 legs, count-form operator, r03d: 1 band 22 / 152 us per iteration at
 1.76 M / 27.4 M samples, 4 bands 34 / 339 us; set-up 1.0 / 5.05 ms and 2.27 / 9.1 ms).
-alpha and beta are NOT measured here (the one-GPU box cannot run two RCCL ranks; a
-one-rank all-reduce costs 10 us of host enqueue, profiles/r03/r03n_rccl_one_rank.log):
-alpha(n) = 10 us + 2 (n - 1) x 1.5 us per ring hop and beta = 100 GB/s are modelling
-assumptions for 8 MI355X on xGMI (7 links x ~153 GB/s per GPU), to be replaced by the
-driver's multi-GPU measurement.
+alpha and beta cannot be measured on the one-GPU box (it cannot run two RCCL ranks; a
+one-rank all-reduce costs 10 us of host enqueue, profiles/r03/r03n_rccl_one_rank.log).
+Until a multi-GPU run has measured them, alpha(n) = 10 us + 2 (n - 1) x 1.5 us per ring
+hop and beta = 100 GB/s are assumptions for 8 MI355X on xGMI (7 links x ~153 GB/s per
+GPU).  bench.py measures both on every N > 1 run (``allreduce_probe``: the all-reduce
+time at the CG's message sizes, fitted to alpha + bytes / beta, and ``comm_rank0``: the
+all-reduce time per CG iteration inside the solve); scripts/rankplan_calibrate.py writes
+them from the driver's SCALE records into rankplan_measured.json beside this file, and
+CostModel() then uses the measured alpha(n) / beta(n) for the rank counts it covers.
 """
 from __future__ import annotations
 
+import json
+import os
 from dataclasses import dataclass, field
+
+MEASURED = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'rankplan_measured.json')
+
+
+def _load_measured(path=MEASURED):
+    """{'alpha_us': {n: us}, 'beta_GBs': {n: GB/s}} from a calibration file, or empty."""
+    try:
+        with open(path) as f:
+            m = json.load(f)
+    except (OSError, ValueError):
+        return {}, {}
+    a = {int(k): float(v) for k, v in m.get('alpha_us', {}).items()}
+    b = {int(k): float(v) for k, v in m.get('beta_GBs', {}).items() if v}
+    return a, b
 
 
 @dataclass
@@ -36,15 +56,38 @@ class CostModel:
     alpha_hop_us: float = 1.5                            # per ring step (2 (n - 1) steps)
     beta_gbs: float = 100.0                              # all-reduce bus bandwidth
     gather_gbs: float = 150.0                            # inputs gathered to one rank (7 links in parallel)
+    # measured per rank count (rankplan_measured.json, scripts/rankplan_calibrate.py); None:
+    # load the file beside this module when it exists
+    alpha_measured: dict = None
+    beta_measured: dict = None
+
+    def __post_init__(self):
+        if self.alpha_measured is None or self.beta_measured is None:
+            a, b = _load_measured()
+            self.alpha_measured = a if self.alpha_measured is None else self.alpha_measured
+            self.beta_measured = b if self.beta_measured is None else self.beta_measured
 
     def alpha_us(self, n):
-        return 0.0 if n <= 1 else self.alpha0_us + 2 * (n - 1) * self.alpha_hop_us
+        if n <= 1:
+            return 0.0
+        if n in self.alpha_measured:
+            return self.alpha_measured[n]
+        return self.alpha0_us + 2 * (n - 1) * self.alpha_hop_us
+
+    def beta(self, n):
+        return self.beta_measured.get(n, self.beta_gbs)
+
+    def measured(self, n):
+        return n in self.alpha_measured
 
     def iter_us(self, n_samples, nb, n, map_bytes):
         nb = 4 if nb == 3 else nb
         t = self.a_us + self.b_us_per_msample[nb] * n_samples / 1e6 / n
         if n > 1:
-            t += 3 * self.alpha_us(n) + map_bytes * 2 * (n - 1) / n / (self.beta_gbs * 1e3)
+            # alpha + bytes / beta per all-reduce (the probe's fit already holds the ring's
+            # 2 (n - 1) / n factor in beta when measured)
+            ring = 1.0 if self.measured(n) else 2 * (n - 1) / n
+            t += 3 * self.alpha_us(n) + map_bytes * ring / (self.beta(n) * 1e3)
         return t
 
     def setup_ms(self, n_samples, nb, n):

@@ -27,3 +27,32 @@ def test_sharded_iteration_time_shape():
     c4 = rankplan.plan(1.76e6, 4, 8)['iter_us_by_ranks']
     assert c4[8] > c4[1]                                           # one observation does not
     assert m.alpha_us(1) == 0.0 and m.alpha_us(8) > m.alpha_us(2)
+
+
+def test_measured_alpha_beta_replace_the_assumptions(tmp_path):
+    """scripts/rankplan_calibrate.py turns bench.py's N > 1 allreduce_probe fields into
+    rankplan_measured.json; CostModel then uses the measured alpha / beta for those rank
+    counts and keeps the assumptions for the others."""
+    import json
+    import subprocess
+    import sys
+    rec = {'parsed': {'destriper_c5_field': {'allreduce_probe': {
+        'n_ranks': 4, 'points': [{'bytes': 32, 'us': 31.0}, {'bytes': 1 << 20, 'us': 52.0}],
+        'alpha_us': 31.0, 'beta_GBs': 50.0}, 'comm_rank0': {'allreduce_ms_per_iter': 0.12}}}}
+    src = tmp_path / 'SCALE_test.json'
+    src.write_text(json.dumps([rec]))
+    out = rankplan.MEASURED
+    saved = open(out).read() if __import__('os').path.exists(out) else None
+    try:
+        subprocess.run([sys.executable, 'scripts/rankplan_calibrate.py', str(src)], check=True, capture_output=True,
+                       cwd=__import__('os').path.dirname(__import__('os').path.dirname(__file__)))
+        m = rankplan.CostModel()
+        assert m.alpha_us(4) == 31.0 and m.beta(4) == 50.0 and m.measured(4)
+        assert not m.measured(8) and m.alpha_us(8) == m.alpha0_us + 14 * m.alpha_hop_us
+        t = m.iter_us(1e6, 1, 4, 1e6)
+        assert t == pytest.approx(m.a_us + m.b_us_per_msample[1] / 4 + 3 * 31.0 + 1e6 / 50e3)
+    finally:
+        if saved is None:
+            __import__('os').remove(out)
+        else:
+            open(out, 'w').write(saved)
