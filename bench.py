@@ -212,8 +212,8 @@ def cpu_baseline(level2=None, data=None):
     if dref:
         out['destriper_reference'] = {
             'value': dref['iters_per_s'], 'unit': 'CG iterations/s', 'cores': 1, 'kind': 'reference',
-            'sample': f"reference Destriper.cgm on a C4-size problem ({dref['n_samples']} samples, "
-                      f"{dref['n_offsets']} offsets, 480x480 map, L=50): {dref['iters']} iterations in "
+            'sample': f"reference Destriper.cgm on {dref.get('inputs', 'a C4-size problem')} ({dref['n_samples']} "
+                      f"samples, {dref['n_offsets']} offsets, 480x480 map, L=50): {dref['iters']} iterations in "
                       f"{dref['seconds']:.1f} s (3 matvecs/iteration as shipped), build container; "
                       'tests/golden/golden_meta.json reference_destriper_c4'}
     return out

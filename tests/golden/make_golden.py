@@ -427,14 +427,25 @@ def run_destriper(out, meta):
                                     seed=7, sha256=[synthetic.sha256(a) for a in (pointing, tod, weights)])
 
 
-def run_destriper_timing(meta):
+def run_destriper_timing(meta, c4_npz=None):
     """The reference's CG at C4 size (19 feeds x 180,000 samples, L = 50,
     480 x 480 map) timed here for the bench line's CPU baseline: destriper_iteration with
     niter = 4 and niter = 1 (threshold 0), the difference / 3 = seconds per CG iteration
-    (3 op_Ax calls each, as shipped)."""
+    (3 op_Ax calls each, as shipped).  c4_npz: the bench's own C4 problem (dumped on the GPU
+    box by scripts/dump_c4_problem.py: read_comap_data band 0 of the reduced C2 observation),
+    so the reference is timed on exactly what the GPU leg solves; without it a synthetic
+    problem of 3.42 M samples (rounds 1-4)."""
     import Destriper
     L = 50
-    pointing, tod, weights = synthetic.destriper_inputs(n_feeds=19, n_samples=180_000, npix_side=480)
+    if c4_npz:
+        z = np.load(c4_npz)
+        pointing, tod, weights = (np.asarray(z['pointing'], np.int64), np.asarray(z['tod'], np.float64),
+                                  np.asarray(z['weights'], np.float64))
+        src = f'the bench C4 problem (scripts/dump_c4_problem.py -> {os.path.basename(c4_npz)}, ' \
+              f'sha256 {synthetic.sha256(tod)[:16]})'
+    else:
+        pointing, tod, weights = synthetic.destriper_inputs(n_feeds=19, n_samples=180_000, npix_side=480)
+        src = 'synthetic.destriper_inputs(n_feeds=19, n_samples=180000, npix_side=480)'
     pixel_edges = np.arange(480 * 480)
     z = np.zeros(tod.size)
     feedid = np.repeat(np.arange(1, 20), tod.size // 19)
@@ -448,8 +459,7 @@ def run_destriper_timing(meta):
     per = (secs[4] - secs[1]) / 3
     meta['reference_destriper_c4'] = {'n_samples': int(tod.size), 'n_offsets': int(tod.size // L),
                                       'iters': 3, 'seconds': secs[4] - secs[1], 'iters_per_s': 1.0 / per,
-                                      'inputs': 'synthetic.destriper_inputs(n_feeds=19, n_samples=180000, '
-                                                'npix_side=480)', 'host': '8-core Xeon build container, 1 process'}
+                                      'inputs': src, 'host': '8-core Xeon build container, 1 process'}
 
 
 def main():
@@ -461,6 +471,7 @@ def main():
     ap.add_argument('--only-noise', action='store_true')
     ap.add_argument('--only-variants-new', action='store_true', help='tinyscan + f3 variants only')
     ap.add_argument('--only-timing', action='store_true', help='reference destriper C4 timing only')
+    ap.add_argument('--c4-npz', default=None, help='time the reference on this dumped C4 problem')
     args = ap.parse_args()
     if args.only_variants_new or args.only_timing:
         os.environ.setdefault('MPLBACKEND', 'agg')
@@ -474,7 +485,7 @@ def main():
             for name in ('tinyscan', 'f3'):
                 meta[f'l1_{name}_sha256'] = run_l1_variant(name, figdir)
         if args.only_timing:
-            run_destriper_timing(meta)
+            run_destriper_timing(meta, args.c4_npz)
         json.dump(meta, open(mp, 'w'), indent=1, default=str)
         return
     if args.only_noise:
