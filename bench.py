@@ -340,8 +340,8 @@ def destriper_leg(level2, data, niter, device, want_cpu=False):
                                      device=device)[:3]
     prep = time.perf_counter() - t0
     td, wd, pd = (torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (tod, w, pix.astype(np.int32)))
-    _timed_setup(pd, td, wd, 50, 480 * 480, device=device)        # warm (module load, first allocations)
-    prob, setup = _timed_setup(pd, td, wd, 50, 480 * 480, device=device)
+    _timed_setup(pd, td, wd, 50, 480 * 480, device=device, map_shape=(480, 480))   # warm (module load, allocations)
+    prob, setup = _timed_setup(pd, td, wd, 50, 480 * 480, device=device, map_shape=(480, 480))
     prob.solve(threshold=0.0, niter=3)   # warm
     conv, conv_s = _timed_solve(prob, 1e-6, 100)
     res, dt = _timed_solve(prob, 0.0, niter)
@@ -358,8 +358,8 @@ def destriper_leg(level2, data, niter, device, want_cpu=False):
     prep4 = time.perf_counter() - t0
     t4, w4, p4, k4 = (torch.from_numpy(np.ascontiguousarray(a)).to(dev)
                       for a in (r['tod'], r['weights'], r['pointing'].astype(np.int32), r['keep']))
-    _timed_setup(p4, t4, w4, 50, 480 * 480, device=device, keep=k4)   # warm (first use of these sizes)
-    prob4, setup4 = _timed_setup(p4, t4, w4, 50, 480 * 480, device=device, keep=k4)
+    _timed_setup(p4, t4, w4, 50, 480 * 480, device=device, keep=k4, map_shape=(480, 480))   # warm (first use)
+    prob4, setup4 = _timed_setup(p4, t4, w4, 50, 480 * 480, device=device, keep=k4, map_shape=(480, 480))
     prob4.solve(threshold=0.0, niter=3)
     conv4, conv4_s = _timed_solve(prob4, 1e-6, 100)
     res4, dt4 = _timed_solve(prob4, 0.0, niter)
@@ -388,8 +388,8 @@ def destriper_c5_leg(n_obs, niter, device, world, rank, n_bands=1):
     L, npix = 50, 480 * 480
     pix, tod, w = synthetic.destriper_inputs_device(n_obs, offset_length=L, device=device, seed=1000 + rank,
                                                     n_bands=n_bands)
-    _timed_setup(pix, tod, w, L, npix, device=device)        # warm (first use of these sizes)
-    prob, setup = _timed_setup(pix, tod, w, L, npix, device=device)
+    _timed_setup(pix, tod, w, L, npix, device=device, map_shape=(480, 480))        # warm (first use of these sizes)
+    prob, setup = _timed_setup(pix, tod, w, L, npix, device=device, map_shape=(480, 480))
     prob.solve(threshold=0.0, niter=3)   # warm (graph capture, RCCL communicators)
     torch.cuda.synchronize()
     if world > 1:
@@ -481,8 +481,8 @@ def destriper_c5_field_leg(n_obs, niter, device, world, rank, n_bands=4):
     lo, hi = n_obs * rank // world, n_obs * (rank + 1) // world
     pix, tod, w = synthetic.destriper_inputs_device(hi - lo, offset_length=L, device=device, seed=5000,
                                                     n_bands=n_bands, obs0=lo)
-    _timed_setup(pix, tod, w, L, npix, device=device)          # warm (first use of these sizes)
-    prob, setup = _timed_setup(pix, tod, w, L, npix, device=device)
+    _timed_setup(pix, tod, w, L, npix, device=device, map_shape=(480, 480))          # warm (first use of these sizes)
+    prob, setup = _timed_setup(pix, tod, w, L, npix, device=device, map_shape=(480, 480))
     N_local = int(pix.numel())
     del pix, tod, w
     prob.solve(threshold=0.0, niter=3)   # warm
@@ -637,7 +637,7 @@ def chain_fn(data, device):
                                      device=device, device_outputs=True, pointing=pp)
         mark('prep_ms')
         prob = D.DeviceDestriper(r['pointing'].to(torch.int32), r['tod'], r['weights'], 50, 480 * 480,
-                                 device=device, keep=r['keep'])
+                                 device=device, keep=r['keep'], map_shape=(480, 480))
         mark('setup_ms')
         res = prob.solve(threshold=1e-6, niter=100, to_host=True)    # maps copied to the host
         mark('solve_and_maps_ms')

@@ -124,7 +124,8 @@ def main(filelistname, offset_length=50, feed_weights=None, prefix='fg9', output
                                             calibrator=calibrator, healpix=healpix, store=store, device=device)
         pixel_edges = _healpix_edges(r['pointing']) if healpix else np.arange(nxpix * nypix)
         res = run_destriper_bands(r['pointing'], r['tod'], r['weights'], offset_length, pixel_edges, keep=r['keep'],
-                                  threshold=threshold, niter=niter, device=device)
+                                  threshold=threshold, niter=niter, device=device,
+                                  map_shape=None if healpix else (nypix, nxpix))
         for iband, maps in zip(bands, res):
             maps = {'All': maps['All']}
             if rank == 0:
@@ -142,7 +143,7 @@ def main(filelistname, offset_length=50, feed_weights=None, prefix='fg9', output
         pixel_edges = _healpix_edges(pointing) if healpix else np.arange(nxpix * nypix)
         maps = run_destriper(pointing, tod, weights, offset_length, pixel_edges, az, el, ra, dec, feedid, obsids,
                              obsid_cuts, threshold=threshold, niter=niter, chi2_cutoff=20,
-                             device=device)
+                             device=device, map_shape=None if healpix else (nypix, nxpix))
         if rank == 0:
             if healpix:
                 write_map_healpix(prefix, maps, remap, map_info, output_dir, iband)

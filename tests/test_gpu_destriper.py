@@ -135,7 +135,7 @@ def test_destriper_two_ranks_distributed_path(golden):
     assert rel(m['naive'], golden['destriper_naive']) < 1e-5
 
 
-def _compact_rank(rank, world, port, p, t, w, npix, q):
+def _compact_rank(rank, world, port, p, t, w, npix, q, shape=None):
     """Solve this rank's half with the map all-reduces compacted to the hit pixels
     (DeviceDestriper's default across ranks) and without (COMAP_DS_COMPACT=0)."""
     import torch
@@ -151,7 +151,7 @@ def _compact_rank(rank, world, port, p, t, w, npix, q):
     out = []
     for compact in ('1', '0'):
         os.environ['COMAP_DS_COMPACT'] = compact
-        prob = DeviceDestriper(p[lo:hi], t[..., lo:hi], w[..., lo:hi], L, npix, device=0)
+        prob = DeviceDestriper(p[lo:hi], t[..., lo:hi], w[..., lo:hi], L, npix, device=0, map_shape=shape)
         res = prob.solve(1e-6, 60)
         out.append((prob.hit_index is not None, res['x'].cpu().numpy(), res['iters'],
                     {k: v.cpu().numpy() for k, v in res['maps'].items()}))
@@ -160,13 +160,14 @@ def _compact_rank(rank, world, port, p, t, w, npix, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('nb,wrap', [(1, False), (4, False), (4, True)])
-def test_two_ranks_compacted_map_allreduce_bit_identical(nb, wrap):
+@pytest.mark.parametrize('nb,wrap,tile', [(1, False, False), (4, False, False), (4, True, False), (4, True, True)])
+def test_two_ranks_compacted_map_allreduce_bit_identical(nb, wrap, tile):
     """Across ranks the map numerator is all-reduced over the union of the pixels the
     operator touches only (a monotone relabelling; the pixels unbinned samples read,
     m[npix + p], are kept): on a 200x200 map the golden pointing covers ~9%, and
     offsets, iteration counts and every map equal the uncompacted solve bit for bit,
-    on 2 gloo ranks.  wrap: off-map ids spread over [-npix, -1]."""
+    on 2 gloo ranks.  wrap: off-map ids spread over [-npix, -1]; tile: both solves on the
+    2-D tiled pixel layout (map_shape), maps returned in the caller's order."""
     import torch.multiprocessing as mp
     p0, tods, ws, _ = _bands_problem(4)
     big = 200
@@ -177,8 +178,9 @@ def test_two_ranks_compacted_map_allreduce_bit_identical(nb, wrap):
     t, w = (tods, ws) if nb == 4 else (tods[0], ws[0])
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    port = 29500 + os.getpid() % 190 + (3 if wrap else 0) + nb
-    procs = [ctx.Process(target=_compact_rank, args=(r, 2, port, p, t, w, big * big, q)) for r in range(2)]
+    port = 29500 + os.getpid() % 190 + (3 if wrap else 0) + nb + (7 if tile else 0)
+    shape = (big, big) if tile else None
+    procs = [ctx.Process(target=_compact_rank, args=(r, 2, port, p, t, w, big * big, q, shape)) for r in range(2)]
     for pr in procs:
         pr.start()
     res = sorted([q.get(timeout=240) for _ in range(2)], key=lambda r: r[0])
@@ -481,6 +483,46 @@ def test_negative_pixel_ids_wrap_vs_oracle(nb, sell, monkeypatch):
     bad[7] = -NPIX - 1
     with pytest.raises(IndexError):
         DeviceDestriper(bad, tods[0], ws[0], L, NPIX)
+
+
+@pytest.mark.parametrize('nb,wrap', [(1, False), (4, False), (3, True)])
+def test_tiled_layout_equals_row_major(nb, wrap, monkeypatch):
+    """map_shape: the operator on the 2-D tiled internal pixel order (T x T tiles, Morton
+    inside) -- a relabelling, so the sample-level maps (weight / hits / naive) are equal
+    bit for bit, offsets and map <= 1e-9 (other summation orders), the same iteration
+    counts, and the maps come back in the caller's row-major order (device and to_host
+    paths).  wrap: negative ids below -1 read the same pixel through the relabel."""
+    from comapreduce_amd.mapmaking.destriper import DeviceDestriper
+    p, tods, ws, keep = _bands_problem(4)
+    p = p.copy()
+    if wrap:
+        off = p < 0
+        p[off] = -np.random.default_rng(12).integers(1, NPIX + 1, int(off.sum()))
+    if nb == 1:
+        args, kw = (p, tods[0], ws[0], L, NPIX), {}
+    else:
+        args, kw = (p, tods[:nb], ws[:nb], L, NPIX), {'keep': keep[:nb]}
+    monkeypatch.setenv('COMAP_DS_TILE', '0')
+    ref = DeviceDestriper(*args, map_shape=(60, 60), **kw)
+    assert ref.layout is None
+    r0 = ref.solve(1e-6, 100)
+    for T in ('8', '16'):
+        monkeypatch.setenv('COMAP_DS_TILE', T)
+        dd = DeviceDestriper(*args, map_shape=(60, 60), **kw)
+        assert dd.layout is not None and dd.npix_full >= NPIX
+        res = dd.solve(1e-6, 100)
+        assert res['iters'] == r0['iters']
+        m = {k: v.cpu().numpy() for k, v in res['maps'].items()}
+        m0 = {k: v.cpu().numpy() for k, v in r0['maps'].items()}
+        for k in ('weight', 'hits', 'naive'):
+            assert m[k].shape == m0[k].shape and np.array_equal(m[k], m0[k]), (T, k)
+        assert rel(m['map'], m0['map']) < 1e-9
+        assert rel(res['x'].cpu().numpy(), r0['x'].cpu().numpy()) < 1e-9
+        hres = dd.solve(1e-6, 100, to_host=True)
+        for k in ('weight', 'hits', 'naive', 'map'):
+            assert np.array_equal(np.asarray(hres['maps'][k]), m[k]), (T, k)
+    with pytest.raises(ValueError):
+        DeviceDestriper(*args, map_shape=(60, 61), **kw)
 
 
 @pytest.mark.parametrize('nb', [1, 3, 4])
