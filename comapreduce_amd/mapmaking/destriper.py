@@ -538,6 +538,9 @@ def copy_stream(dev):
 TILE = 8     # map layout tile (pixels per side) for a known map shape; COMAP_DS_TILE=0: row-major
 
 
+_LAYOUTS = {}
+
+
 def tiled_layout(ny, nx, T, device):
     """Internal id of every row-major pixel of an ny x nx map on a 2-D tiled layout: T x T
     tiles in row-major tile order, the pixels of a tile in Morton (Z) order; and the padded
@@ -546,6 +549,9 @@ def tiled_layout(ny, nx, T, device):
     obs: 1 band 0.139 -> 0.124, 4 bands 0.295 -> 0.275 ms per CG iteration with T = 8,
     scripts/ds_tiling_probe.py, profiles/r05/r05c_py2.log)."""
     import torch
+    key = (int(ny), int(nx), int(T), str(device))
+    if key in _LAYOUTS:
+        return _LAYOUTS[key]
     p = torch.arange(ny * nx, device=device, dtype=torch.int64)
     y, x = p // nx, p % nx
     ntx, nty = (nx + T - 1) // T, (ny + T - 1) // T
@@ -554,7 +560,9 @@ def tiled_layout(ny, nx, T, device):
     for b in range(max(1, (T - 1).bit_length())):
         z |= ((ix >> b) & 1) << (2 * b)
         z |= ((iy >> b) & 1) << (2 * b + 1)
-    return ((y // T) * ntx + x // T) * T * T + z, ntx * nty * T * T
+    ids = (((y // T) * ntx + x // T) * T * T + z).to(torch.int32)
+    _LAYOUTS[key] = (ids, ntx * nty * T * T)
+    return _LAYOUTS[key]
 
 
 class DeviceDestriper:
@@ -704,20 +712,22 @@ class DeviceDestriper:
         reads m[npix + p]) becomes the negative id that reads the same pixel there."""
         import torch
         dev = torch.device('cuda', N.current_device() if device is None else int(device))
-        pix = pixels.to(device=dev, dtype=torch.int64).reshape(-1) if isinstance(pixels, torch.Tensor) else \
-            torch.from_numpy(np.ascontiguousarray(pixels, dtype=np.int64)).to(dev).reshape(-1)
-        if pix.numel() and (int(pix.max().item()) >= npix or int(pix.min().item()) < -npix):
-            raise IndexError(f'pixel index out of range for a map of {npix} pixels (valid: -{npix} .. {npix - 1})')
+        pix = pixels.to(device=dev, dtype=torch.int32).reshape(-1) if isinstance(pixels, torch.Tensor) else \
+            torch.from_numpy(np.ascontiguousarray(pixels, dtype=np.int32)).to(dev).reshape(-1)
         ids, nt = tiled_layout(ny, nx, T, dev)
-        t = ids[torch.remainder(pix, npix)]
+        # int32 throughout and no host sync: an id outside [-npix, npix) becomes nt, which the
+        # set-up's device range check rejects (IndexError), as it would the original id
+        bad = (pix >= npix) | (pix < -npix)
+        neg = pix < 0
+        t = ids.index_select(0, torch.where(bad, torch.zeros_like(pix), torch.where(neg, pix + npix, pix)))
         self.layout = ids
-        return torch.where(pix >= 0, t, t - nt).to(torch.int32), nt
+        return torch.where(bad, torch.full_like(pix, nt), torch.where(neg, t - nt, t)), nt
 
     def _untile(self, v, nb):
         """[npix_internal * nb] interleaved map -> the caller's row-major [npix * nb]."""
         if self.layout is None:
             return v
-        return v.reshape(-1, nb).index_select(0, self.layout).reshape(-1)
+        return v.reshape(-1, nb).index_select(0, self.layout).reshape(-1)   # (int32 ids)
 
     def _compact(self, pixels, npix, device):
         """Across ranks the map numerator is all-reduced every CG iteration

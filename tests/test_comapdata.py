@@ -272,34 +272,39 @@ def test_nan_samples_do_not_abort_prep(case_store):
     assert np.unique(np.asarray(res[8])[moved]).size == 1                # only that feed's samples moved
 
 
-def _many_scans_store(case_store):
+def _many_scans_store(case_store, dense=False):
     """File 13 of the golden scenario re-cut into 82 scans (> the 64 a scan table once
     held): lengths cycle through 30 (shorter than L: no samples), 120 / 260 / 75 / 240
-    (short segments, np.nanmedian) and 900 (> 2 x 400: the running median)."""
+    (short segments, np.nanmedian) and 900 (> 2 x 400: the running median).  dense: more
+    than 128 scans (the gather kernel's in-LDS scan table holds 128; beyond it the table is
+    binary-searched in HBM) -- shorter cycles, 5-sample gaps."""
     store, names = case_store
     ds, attrs = store[names[1]]
     ds = dict(ds)
     T = ds['averaged_tod/tod'].shape[-1]
     edges, t = [], 100
-    cyc = (30, 120, 260, 900, 75, 240)
+    cyc = (30, 60, 100, 75, 90, 45, 55, 65, 820) if dense else (30, 120, 260, 900, 75, 240)
+    gap = 5 if dense else 20
     while True:
         n = cyc[len(edges) % len(cyc)]
         if t + n > T:
             break
         edges.append((t, t + n))
-        t += n + 20
+        t += n + gap
     ds['averaged_tod/scan_edges'] = np.asarray(edges, dtype=np.int64)
     return {names[1]: (ds, attrs)}, [names[1]], len(edges)
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('dense', [False, True])
 @pytest.mark.parametrize('name', list(cc.CASES))
-def test_gpu_prep_many_scans_vs_oracle(case_store, name):
-    """read_comap_data on a file of 82 scans (COMAPData.py:350-360 loops over any number)
-    == the oracle, bit for bit except the Sun-centric trigonometric leaves."""
+def test_gpu_prep_many_scans_vs_oracle(case_store, name, dense):
+    """read_comap_data on a file of 82 (dense: > 128, the HBM-searched scan table) scans
+    (COMAPData.py:350-360 loops over any number) == the oracle, bit for bit except the
+    Sun-centric trigonometric leaves."""
     from oracle import comapdata as oc
-    store, names, S = _many_scans_store(case_store)
-    assert S > 64
+    store, names, S = _many_scans_store(case_store, dense)
+    assert S > (128 if dense else 64), S
     case = cc.CASES[name]
     ref = oc.read_comap_data(names, store, map_info(case['map']), feeds=cc.FEEDS, **case['kw'])
     got = cd.read_comap_data(names, map_info(case['map']), feeds=cc.FEEDS, store=store, **case['kw'])
