@@ -86,7 +86,6 @@ struct comap_destriper {
     // column-major -- entry j of lane l at sbase[c] + 64 j + l -- so a lane streams its row
     // with coalesced loads, no row-pointer load and no cross-lane reduction
     bool sell = false;
-    bool quad = false;         // 4 bands: band-lane bin and projection (COMAP_DS_QUAD)
     bool walk = false;         // sample-level maps by the member-mask walk (set-up)
     int64_t nsell = 0;         // padded entries
     int64_t *sbase = nullptr;  // [NC + 1]
@@ -1653,156 +1652,6 @@ __global__ void __launch_bounds__(256) k_ds_project_sell(const int64_t *__restri
     }
 }
 
-// 4 bands, band lanes: the sliced-ELLPACK projection with lane = (offset, band) -- a wave
-// takes a quarter chunk (16 offsets x 4 bands), lane 4 s + b walks offset s's row for band
-// b: the quad of lanes of one entry reads its pixel id and counts once (same address) and
-// gathers the entry's 32-B map vector as four 8-B loads of consecutive addresses, where the
-// one-lane-per-offset kernel issues two scattered 16-B loads per lane.  Each lane's sum is
-// its band's plain in-order fma chain (the same order as k_ds_project_sell's band b).
-template <bool CF, int U>
-__global__ void __launch_bounds__(256) k_ds_project_sell4q(const int64_t *__restrict__ sbase,
-                                                           const int32_t *__restrict__ spix,
-                                                           const void *__restrict__ sco,
-                                                           const double *__restrict__ wbar,
-                                                           const double *__restrict__ ws,
-                                                           const double *__restrict__ tw, const double *__restrict__ x,
-                                                           const double *__restrict__ num, const double *__restrict__ h,
-                                                           int64_t NO, int64_t npix, double *__restrict__ y,
-                                                           double *__restrict__ dot_part,
-                                                           const int32_t *__restrict__ flags, int64_t pstride)
-{
-    constexpr int NB = 4;
-    __shared__ double red[4 * NB];
-    if (cg_done(flags)) return;
-    const int lane = threadIdx.x & 63, b = lane & 3, sl = lane >> 2;
-    const int64_t nq = ((NO + 63) >> 6) * 4;        // quarter chunks
-    const int64_t nw = (int64_t)gridDim.x * 4;
-    auto coef = [&](int64_t slot) -> double {
-        if constexpr (CF) return (double)reinterpret_cast<const uint8_t *>(sco)[slot * NB + b];
-        else return reinterpret_cast<const double *>(sco)[slot * NB + b];
-    };
-    double acc = 0.0;
-    for (int64_t cq = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); cq < nq; cq += nw) {
-        const int64_t c = cq >> 2;
-        const int col = (int)(cq & 3) * 16 + sl;
-        const int64_t b0 = sbase[c], W = (sbase[c + 1] - b0) >> 6;
-        const int64_t o = c * 64 + col;
-        const int32_t *pp = spix + b0 + col;
-        double g = 0.0;
-        int32_t q[U];
-        double a[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const bool in = u < W;
-            q[u] = in ? pp[64 * u] : kSellPad;
-            a[u] = in ? coef(b0 + 64 * u + col) : 0.0;
-        }
-        for (int64_t j = 0; j < W; j += U) {
-            double mv[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (q[u] != kSellPad) {
-                    const int64_t qq = wrap_pixel(q[u], npix) * NB + b;
-                    mv[u] = h ? map_value(num, h, qq) : num[qq];
-                }
-            }
-            const int64_t jn = j + U;
-            int32_t qn[U];
-            double an[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const bool in = jn + u < W;
-                qn[u] = in ? pp[64 * (jn + u)] : kSellPad;
-                an[u] = in ? coef(b0 + 64 * (jn + u) + col) : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (q[u] != kSellPad) g = fma(a[u], mv[u], g);
-#pragma unroll
-            for (int u = 0; u < U; ++u) { q[u] = qn[u]; a[u] = an[u]; }
-        }
-        if (o < NO) {
-            const int64_t k = o * NB + b;
-            const double xo = x ? x[k] : 0.0;
-            if constexpr (CF) g *= wbar[k];
-            const double v = (x ? ws[k] * xo : tw[k]) - g;
-            y[k] = v;
-            if (dot_part) acc = fma(v, xo, acc);
-        }
-    }
-    if (dot_part) {
-        double a4[NB];
-#pragma unroll
-        for (int bb = 0; bb < NB; ++bb) a4[bb] = bb == b ? acc : 0.0;
-        block_partials<NB>(a4, red, dot_part + blockIdx.x, pstride);
-        if (pstride < kPartMax && blockIdx.x == 0) zero_tail<NB>(dot_part, pstride, gridDim.x);
-    }
-}
-
-// k_ds_bin for 4 bands with band lanes: 4 kSlots lanes per pixel row, lane 4 t + b takes
-// the row's entries t, t + kSlots, ... for band b (the quad reads the entry's offset id and
-// counts once and the offset's 32-B x vector as four consecutive 8-B loads), then the
-// kSlots partial sums of each band are reduced across the row's lanes.
-template <int kSlots, bool CF, int kBinU>
-__global__ void __launch_bounds__(256) k_ds_bin4q(const int64_t *__restrict__ prow, const int32_t *__restrict__ poff,
-                                                  const void *__restrict__ pw, const double *__restrict__ x,
-                                                  int64_t npix, const double *__restrict__ base,
-                                                  const double *__restrict__ hdiv, double *__restrict__ num,
-                                                  const int32_t *__restrict__ flags, const int32_t *__restrict__ rows)
-{
-    constexpr int NB = 4, LN = 4 * kSlots;
-    if (cg_done(flags)) return;
-    const int sub = threadIdx.x & (LN - 1), b = sub & 3, t = sub >> 2;
-    const int64_t step = (int64_t)gridDim.x * blockDim.x / LN;
-    auto coef = [&](int64_t k) -> double {
-        if constexpr (CF) return (double)reinterpret_cast<const uint8_t *>(pw)[k * NB + b];
-        else return reinterpret_cast<const double *>(pw)[k * NB + b];
-    };
-    for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LN; i < npix; i += step) {
-        const int64_t p = rows ? (int64_t)rows[i] : i;
-        double tail = 0.0;
-        if (t == 0 && (base || hdiv)) tail = (base ? base : hdiv)[p * NB + b];
-        const int64_t e1 = prow[i + 1];
-        int64_t k = prow[i] + t;
-        double s = 0.0;
-        int32_t o[kBinU];
-        double a[kBinU];
-#pragma unroll
-        for (int u = 0; u < kBinU; ++u) {
-            const bool in = k + u * kSlots < e1;
-            o[u] = in ? poff[k + u * kSlots] : 0;
-            a[u] = in ? coef(k + u * kSlots) : 0.0;
-        }
-        while (k < e1) {
-            double xv[kBinU];
-#pragma unroll
-            for (int u = 0; u < kBinU; ++u) xv[u] = x[(int64_t)o[u] * NB + b];
-            const int64_t kn = k + kSlots * kBinU;
-            int32_t on[kBinU];
-            double an[kBinU];
-#pragma unroll
-            for (int u = 0; u < kBinU; ++u) {
-                const bool in = kn + u * kSlots < e1;
-                on[u] = in ? poff[kn + u * kSlots] : 0;
-                an[u] = in ? coef(kn + u * kSlots) : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < kBinU; ++u)
-                if (k + u * kSlots < e1) s = fma(a[u], xv[u], s);
-#pragma unroll
-            for (int u = 0; u < kBinU; ++u) { o[u] = on[u]; a[u] = an[u]; }
-            k = kn;
-        }
-#pragma unroll
-        for (int w = LN / 2; w >= 4; w >>= 1) s += __shfl_xor(s, w, LN);
-        if (t == 0) {
-            if (base) s = tail - s;
-            else if (hdiv) s = tail != 0.0 ? s / tail : s;
-            num[p * NB + b] = s;
-        }
-    }
-}
-
 // per-band block partials of sum_o a[o][b] c[o][b]
 template <int NB>
 __global__ void __launch_bounds__(256) k_dot_part(const double *__restrict__ a, const double *__restrict__ c, int64_t n,
@@ -2048,22 +1897,6 @@ void launch_bin_u(const comap_destriper *d, hipStream_t st, const double *x, con
     const int64_t *rp = hit_rows ? d->hprow : d->prow;
     const int64_t mean = np ? d->nnzp / np : 0;
     const void *co = CF ? (const void *)d->pcnt : (const void *)d->pw;
-    if constexpr (NB == 4) {
-        if (d->quad) {
-            // band lanes: 4 per entry slot, entry slots per row by the mean row length
-            const int slots = mean >= 48 ? 16 : (mean >= 24 ? 8 : (mean >= 10 ? 4 : 2));
-            const unsigned gq = grid_for(np * 4 * slots, 65536);
-#define COMAP_BINQ(SL) k_ds_bin4q<SL, CF, U><<<gq, 256, 0, st>>>(rp, d->poff, co, x, np, base, hdiv, num, flags, rows)
-            switch (slots) {
-            case 16: COMAP_BINQ(16); break;
-            case 8: COMAP_BINQ(8); break;
-            case 4: COMAP_BINQ(4); break;
-            default: COMAP_BINQ(2);
-            }
-#undef COMAP_BINQ
-            return;
-        }
-    }
     const int lanes = d->bin_lanes ? d->bin_lanes : (mean >= 24 ? 16 : (mean >= 10 ? 8 : 4));
     const unsigned g = grid_for(np * lanes, 65536);
 #define COMAP_BIN(LN) k_ds_bin<LN, NB, CF, U><<<g, 256, 0, st>>>(rp, d->poff, co, x, np, base, hdiv, num, flags, rows)
@@ -2124,13 +1957,6 @@ unsigned launch_project_u(const comap_destriper *d, hipStream_t st, const double
 {
     const unsigned pg = project_grid(d, pstride);
     if (d->sell) {
-        if constexpr (NB == 4) {
-            if (d->quad) {
-                k_ds_project_sell4q<CF, 8><<<pg, 256, 0, st>>>(d->sbase, d->spix, d->sco, d->wbar, d->ws, d->tw, x,
-                                                              num, h, d->NO, d->npix, y, part, flags, pstride);
-                return pg;
-            }
-        }
         k_ds_project_sell<NB, CF, 8><<<pg, 256, 0, st>>>(d->sbase, d->spix, d->sco, d->wbar, d->ws, d->tw, x, num, h,
                                                         d->NO, d->npix, y, part, flags, pstride);
         return pg;
@@ -2407,7 +2233,6 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
         d->proj_blocks = env_int("COMAP_DS_PB", d->sell ? 2 * kProjBlocks : kProjBlocks,
                                  {256, 512, 1024, 2048, 4096, 8192});
         d->cg_graph = env_int("COMAP_DS_CGGRAPH", -1, {0, 1});
-        d->quad = nb == 4 && env_int("COMAP_DS_QUAD", 0, {0, 1}) == 1;
     }
     // the member-mask walk needs the count form and finite tod everywhere; otherwise the
     // count pass runs again with the per-sample payload for the sorted-sample walk
