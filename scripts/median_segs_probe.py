@@ -4,7 +4,7 @@ so 912 series make 3.6 rounds on 256 CUs; splitting series into more, shorter se
 packs 2-3 workgroups per CU (each re-reads its job's sorted sources).  Runs bench.py's L1
 step + chain per value in a child process and prints the L1 median kernel time and the
 chain's synced prep phase.
-    python scripts/median_segs_probe.py [targets...]"""
+    python scripts/median_segs_probe.py [targets or KEY=VAL,KEY=VAL specs...]"""
 import json
 import os
 import subprocess
@@ -12,9 +12,10 @@ import sys
 
 
 def main():
-    targets = [int(v) for v in sys.argv[1:]] or [128, 1024, 2048, 4096]
-    for t in targets:
-        env = dict(os.environ, COMAP_MEDIAN_WMSEGS=str(t))
+    specs = sys.argv[1:] or ['128', '1024', '2048', '4096']
+    for t in specs:
+        extra = dict(kv.split('=') for kv in t.split(',')) if '=' in t else {'COMAP_MEDIAN_WMSEGS': t}
+        env = dict(os.environ, **extra)
         out = subprocess.run([sys.executable, 'bench.py', '--steps', '3', '--warmup', '1', '--no-e2e',
                               '--no-cpu-baseline', '--c5-obs', '0', '--c5-field-obs', '0'],
                              env=env, capture_output=True, text=True, timeout=280)

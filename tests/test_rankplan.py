@@ -6,9 +6,10 @@ import pytest
 from comapreduce_amd.mapmaking import rankplan
 
 
-@pytest.mark.parametrize('n,nb,us', [(1.76e6, 1, 22.0), (27.36e6, 1, 152.0), (1.76e6, 4, 34.0), (27.36e6, 4, 339.0)])
+@pytest.mark.parametrize('n,nb,us', [(1.76e6, 1, 21.8), (27.36e6, 1, 124.0), (1.76e6, 4, 29.9), (27.36e6, 4, 275.0)])
 def test_single_rank_iteration_matches_measurement(n, nb, us):
-    # bench.py r03d: C4 45.4k / 29.5k it/s (1 / 4 bands), C5 0.152 / 0.339 ms per iteration
+    # bench.py r05c / ds_tiling_probe: C4 45.8k it/s (1 band) and 134k band-it/s (4 bands),
+    # C5 (8 obs, tiled layout) 0.124 / 0.275 ms per iteration
     assert rankplan.CostModel().iter_us(n, nb, 1, 0) == pytest.approx(us, rel=0.06)
 
 
