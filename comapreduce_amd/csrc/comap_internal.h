@@ -143,20 +143,17 @@ struct MedJob {
     const double *gate; // optional: skip the job when *gate <= 0 (band count N_b)
 };
 
-// A k_med_slide work item: outputs [o0, o1) of one job.
+// A walk work item (k_med_wm / k_med_walk segment): outputs [o0, o1) of one job.
 struct SlideSeg {
     int32_t job, pad_;
     int64_t o0, o1;
 };
 
-// Sliding-median plan.  slide: k_med_slide over `segs` (windows up to ~12k);
-// otherwise the global-sort path (jobs, per-job sorted-key segments, k_med_walk
-// segments in `segs`, buffers).
+// Sliding-median plan: jobs, per-job sorted-key segments, walk segments in `segs`,
+// buffers.
 struct MedPlan {
-    bool slide = false;
-    SlideSeg *segs = nullptr;    // dev [nsegs] k_med_slide or k_med_walk segments
+    SlideSeg *segs = nullptr;    // dev [nsegs] k_med_wm or k_med_walk segments
     int32_t nsegs = 0;
-    int32_t kper = 0;
     int32_t w = 0, lc = 0, nwmax = 0, njobs = 0;
     int32_t nitems = 0;
     int64_t nchunks = 0;
@@ -169,7 +166,6 @@ struct MedPlan {
     int32_t pbits = 32;          // significant proxy bits (radix-sort digit passes = pbits / 8)
     bool wide = false;           // segmented sort with 1024-thread workgroups (few series)
     bool wm = false;             // walk = wavelet-matrix range order statistics (k_med_wm)
-    bool wmq = false;            // ... on 2-bit digits (k_med_wm4: half the levels)
     int32_t wmL = 0;             // wavelet-matrix levels (bits of the largest rank)
     size_t wm_smem = 0;          // its dynamic LDS bytes
     int32_t *slo = nullptr;      // dev [njobs] first source index of each job (wavelet-matrix walk: the

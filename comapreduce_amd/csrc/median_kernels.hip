@@ -43,18 +43,10 @@
 
 namespace {
 
-constexpr int kWalkThreads = 256;   // = outputs per chunk (lc)
-
 __device__ __forceinline__ uint64_t key_of(double v)
 {
     const uint64_t b = __double_as_longlong(v);
     return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
-}
-
-__device__ __forceinline__ double val_of(uint64_t k)
-{
-    const uint64_t b = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
-    return __longlong_as_double(b);
 }
 
 // index into j.src of the virtual series' element at pos (see xprime)
@@ -666,404 +658,13 @@ __global__ void __launch_bounds__(kWmThreads) k_med_wm(const MedJob *__restrict_
     }
 }
 
-// The same walk on a 4-ary wavelet matrix: each level partitions the sequence by a
-// 2-bit digit (4 buckets, stable), so a query takes L/2 levels.  A level word covers
-// 32 positions: the digit's low and high bit planes and the counts of digits <= 0,
-// <= 1, <= 2 before the word (one 16-B LDS read gives all three ranks of a position).
-__device__ __forceinline__ void wm4_rle(const uint4 *__restrict__ lv, int i, int (&r)[4])
-{
-    const uint4 e = lv[i >> 5];
-    const uint32_t m = (1u << (i & 31)) - 1u, lo = e.x, hi = e.y;
-    r[0] = (int)(e.z & 0xffffu) + __popc(~hi & ~lo & m);
-    r[1] = (int)(e.z >> 16) + __popc(~hi & m);
-    r[2] = (int)e.w + __popc(~(hi & lo) & m);
-    r[3] = i;
-}
-
-__device__ __forceinline__ int wm4_bucket(int r, const int (&n)[4])
-{
-    return r < n[0] ? 0 : r < n[1] ? 1 : r < n[2] ? 2 : 3;
-}
-
-__global__ void __launch_bounds__(kWmThreads) k_med_wm4(const MedJob *__restrict__ jobs,
-                                                        const SlideSeg *__restrict__ wsegs,
-                                                        const int32_t *__restrict__ seg,
-                                                        const int32_t *__restrict__ sidx,
-                                                        const int32_t *__restrict__ slo, int32_t w, int32_t D)
-{
-    extern __shared__ __align__(16) unsigned char smem[];
-    __shared__ unsigned long long wtot[kWmThreads / 64];
-    __shared__ int cst[16][4];                      // per level: bucket starts
-    const SlideSeg sg = wsegs[blockIdx.x];
-    const MedJob job = jobs[sg.job];
-    if (job.gate && *job.gate <= 0.0) return;
-    const int32_t s0 = seg[sg.job], nu = seg[sg.job + 1] - s0, sl = slo[sg.job];
-    const int c0 = (int)(sg.o0 - job.out_lo);
-    const int nout = (int)(sg.o1 - sg.o0);
-    const int ns = nout + w - 1;
-    const int nw = (ns + 31) >> 5;                 // <= kWmThreads (plan)
-    const int ld = nw + 1;
-    const int h = w / 2;
-    const int64_t base = job.out_lo - h;
-    uint4 *lev = reinterpret_cast<uint4 *>(smem);                       // [D][ld]
-    const size_t lbytes = max((size_t)D * ld * 16, (size_t)nw * 64 + 16);
-    uint16_t *S = reinterpret_cast<uint16_t *>(smem + lbytes);          // [nw * 32]
-    uint16_t *uinv = reinterpret_cast<uint16_t *>(smem);
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const uint16_t pad = (uint16_t)((1u << (2 * D)) - 1u);
-    int64_t a_, b_;
-    src_interval(job, base + c0, base + c0 + ns, h, a_, b_);
-    for (int i = tid; i < nu; i += kWmThreads) {
-        const int64_t s = sl + sidx[s0 + i];
-        if (s >= a_ && s < b_) uinv[s - a_] = (uint16_t)i;
-    }
-    __syncthreads();
-    for (int i = tid; i < nw * 32; i += kWmThreads)
-        S[i] = i < ns ? uinv[src_index(job, base + c0 + i, h) - a_] : pad;
-    __syncthreads();
-    const bool own = tid < nw;
-    for (int d = D - 1; d >= 0; --d) {
-        const int sh = 2 * d;
-        uint16_t v[32];
-        uint32_t lo = 0, hi = 0;
-        if (own) {
-            const uint4 *p = reinterpret_cast<const uint4 *>(S + 32 * tid);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint4 x = p[q];
-                const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    v[8 * q + 2 * t] = (uint16_t)(xw[t] & 0xffffu);
-                    v[8 * q + 2 * t + 1] = (uint16_t)(xw[t] >> 16);
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < 32; ++j) {
-                lo |= (uint32_t)((v[j] >> sh) & 1u) << j;
-                hi |= (uint32_t)((v[j] >> (sh + 1)) & 1u) << j;
-            }
-        }
-        const uint32_t e0 = ~hi & ~lo, e1 = ~hi & lo, e2 = hi & ~lo, e3 = hi & lo;
-        // counts of digits 0, 1, 2 in 16-bit fields (<= 32768 each: no carries between fields)
-        const unsigned long long cnt = own ? ((unsigned long long)__popc(e0) | ((unsigned long long)__popc(e1) << 16) |
-                                              ((unsigned long long)__popc(e2) << 32))
-                                           : 0ull;
-        unsigned long long incl = cnt;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const unsigned long long y = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += y;
-        }
-        if (lane == 63) wtot[wv] = incl;
-        __syncthreads();
-        unsigned long long before = 0, tot = 0;
-#pragma unroll
-        for (int u = 0; u < kWmThreads / 64; ++u) {
-            const unsigned long long t = wtot[u];
-            before += u < wv ? t : 0ull;
-            tot += t;
-        }
-        const unsigned long long pre = before + incl - cnt;
-        const int P0 = (int)(pre & 0xffff), P1 = (int)((pre >> 16) & 0xffff), P2 = (int)((pre >> 32) & 0xffff);
-        const int T0 = (int)(tot & 0xffff), T1 = (int)((tot >> 16) & 0xffff), T2 = (int)((tot >> 32) & 0xffff);
-        uint4 *lv = lev + (size_t)d * ld;
-        if (own) lv[tid] = make_uint4(lo, hi, (uint32_t)P0 | ((uint32_t)(P0 + P1) << 16), (uint32_t)(P0 + P1 + P2));
-        if (tid == 0) {
-            lv[nw] = make_uint4(0u, 0u, (uint32_t)T0 | ((uint32_t)(T0 + T1) << 16), (uint32_t)(T0 + T1 + T2));
-            cst[d][0] = 0; cst[d][1] = T0; cst[d][2] = T0 + T1; cst[d][3] = T0 + T1 + T2;
-        }
-        __syncthreads();                           // every read of S (and wtot) is done
-        if (own && d > 0) {
-            const int pc[4] = {P0, T0 + P1, T0 + T1 + P2, T0 + T1 + T2 + (32 * tid - P0 - P1 - P2)};
-            const uint32_t ec[4] = {e0, e1, e2, e3};
-#pragma unroll
-            for (int j = 0; j < 32; ++j) {
-                const uint32_t below = (1u << j) - 1u;
-                const int c = (int)(((hi >> j) & 1u) * 2u + ((lo >> j) & 1u));
-                S[pc[c] + __popc(ec[c] & below)] = v[j];
-            }
-        }
-        __syncthreads();
-    }
-    const bool two = (w % 2) == 0;
-    const int r_lo = two ? (w / 2 - 1) : (w / 2);
-    const int32_t *sp = sidx + s0;
-    auto value = [&](uint32_t u) { return job.src[sl + sp[u]]; };   // value of sorted index u
-    for (int k = tid; k < nout; k += kWmThreads) {
-        int a = k, b = k + w, r = r_lo;
-        int a2 = 0, b2 = 0, r2 = 0;
-        uint32_t v1 = 0, v2 = 0;
-        bool split = false;
-        for (int d = D - 1; d >= 0; --d) {
-            const uint4 *lv = lev + (size_t)d * ld;
-            const int *C = cst[d];
-            if (split) {                           // the upper statistic on its own path
-                int ra[4], rb[4], n[4];
-                wm4_rle(lv, a2, ra);
-                wm4_rle(lv, b2, rb);
-#pragma unroll
-                for (int t = 0; t < 4; ++t) n[t] = rb[t] - ra[t];
-                const int c = wm4_bucket(r2, n);
-                const int pa = c ? ra[c - 1] : 0, pb = c ? rb[c - 1] : 0;
-                r2 -= c ? n[c - 1] : 0;
-                a2 = C[c] + ra[c] - pa;
-                b2 = C[c] + rb[c] - pb;
-                v2 |= (uint32_t)c << (2 * d);
-            }
-            int ra[4], rb[4], n[4];
-            wm4_rle(lv, a, ra);
-            wm4_rle(lv, b, rb);
-#pragma unroll
-            for (int t = 0; t < 4; ++t) n[t] = rb[t] - ra[t];
-            const int c = wm4_bucket(r, n);
-            if (two && !split) {
-                const int cu = wm4_bucket(r + 1, n);
-                if (cu != c) {                     // the two part here: upper = first of bucket cu
-                    split = true;
-                    const int pa = ra[cu - 1], pb = rb[cu - 1];
-                    r2 = r + 1 - n[cu - 1];
-                    a2 = C[cu] + ra[cu] - pa;
-                    b2 = C[cu] + rb[cu] - pb;
-                    v2 = v1 | ((uint32_t)cu << (2 * d));
-                }
-            }
-            const int pa = c ? ra[c - 1] : 0, pb = c ? rb[c - 1] : 0;
-            r -= c ? n[c - 1] : 0;
-            a = C[c] + ra[c] - pa;
-            b = C[c] + rb[c] - pb;
-            v1 |= (uint32_t)c << (2 * d);
-        }
-        const double lo = value(v1);
-        double out = lo;
-        if (two) out = (value(split ? v2 : v1) + lo) / 2.0;
-        job.dst[sg.o0 + k - job.out_lo] = out;
-    }
-}
-
 // LDS of a wavelet-matrix segment: the level words (whose space first holds the 16-bit
 // source -> sorted-index table, at most one entry per position) + the 16-bit sequence;
-// binary: L levels of 8-B words, 4-ary: L/2 levels of 16-B words
-size_t wm_smem(int L, int nw, bool quad = false)
+// L levels of 8-B words
+size_t wm_smem(int L, int nw)
 {
-    const size_t lv = quad ? (size_t)((L + 1) / 2) * (nw + 1) * 16 : (size_t)L * (nw + 1) * 8;
+    const size_t lv = (size_t)L * (nw + 1) * 8;
     return std::max<size_t>(lv, (size_t)nw * 64 + 16) + (size_t)nw * 64;
-}
-
-// ------------------------------------------------------------------ sliding sorted window
-// k_med_slide: one workgroup walks a segment of a series chunk by chunk
-// (kSlideL outputs per chunk), keeping the chunk's union window U sorted in
-// LDS as (key, position) pairs.  Moving to the next chunk removes the kSlideL
-// positions that leave and merges the kSlideL that enter: both small sets are
-// sorted by counting ranks (one broadcast LDS sweep per element), after which
-// every element's new index is known in closed form -- its old index minus
-// the leaving elements below it plus the entering elements below it -- so
-// the merge is one parallel scatter (survivors: contiguous per-thread runs
-// whose two counts advance linearly after one binary search).  The per-output
-// walk over the zone list E is the one k_med_walk uses, with U explicit (no
-// rank bitmaps).  No global sort: every value is keyed once as it enters and
-// once as it leaves.  Positions are kept mod 2^16 and compared relative to the
-// chunk's first union position (the live span is < 2^16).
-constexpr int kSlideL = 256;           // outputs per chunk
-constexpr int kSlideThreads = 512;     // threads 0..255: entering set; 256..511: leaving set
-
-struct KP {
-    uint64_t k;
-    int r;        // position relative to the current union start
-};
-
-__device__ __forceinline__ bool kp_less(const KP &a, const KP &b) { return a.k < b.k || (a.k == b.k && a.r < b.r); }
-
-template <int kPer>   // U entries per thread: w + kSlideL - 1 <= kPer * kSlideThreads
-__global__ void __launch_bounds__(kSlideThreads) k_med_slide(const MedJob *__restrict__ jobs,
-                                                             const SlideSeg *__restrict__ segs, int32_t w)
-{
-    extern __shared__ __align__(16) unsigned char smem[];
-    const int Mcap = w + kSlideL - 1;
-    uint64_t *sk = reinterpret_cast<uint64_t *>(smem);     // U keys [Mcap]
-    uint64_t *xk = sk + Mcap;                              // staging keys: entering | leaving [2L]
-    uint64_t *ok = xk + 2 * kSlideL;                       // sorted keys:  entering | leaving [2L]
-    uint16_t *sp = reinterpret_cast<uint16_t *>(ok + 2 * kSlideL);   // U positions mod 2^16
-    uint16_t *xp = sp + Mcap;
-    uint16_t *op = xp + 2 * kSlideL;
-    uint32_t *E = reinterpret_cast<uint32_t *>(((uintptr_t)(op + 2 * kSlideL) + 15) & ~(uintptr_t)15);   // [2L+16]
-    __shared__ int s_scan[kSlideThreads / 64];
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, wid = tid >> 6;
-    const SlideSeg sg = segs[blockIdx.x];
-    const MedJob job = jobs[sg.job];
-    if (job.gate && *job.gate <= 0.0) return;
-    const int h = w / 2;
-
-    int64_t i0 = sg.o0;
-    int L = (int)min((int64_t)kSlideL, sg.o1 - i0);
-    int64_t P = i0 - h;                     // first union position of the current chunk
-    auto rel = [&](uint16_t p16) -> int { return (int)(uint16_t)(p16 - (uint16_t)P); };
-
-    // One merge round: positions [a, b) enter, [P, P + nr) leave (na, nr <= kSlideL).
-    auto round = [&](int M, int64_t a, int na, int nr) -> int {
-        const int half = tid >> 8, tl = tid & (kSlideL - 1);
-        const int n = half ? nr : na;
-        uint64_t *hx = xk + half * kSlideL, *ho = ok + half * kSlideL;
-        uint16_t *hxp = xp + half * kSlideL, *hop = op + half * kSlideL;
-        KP me = {0, 0};
-        if (tl < n) {
-            const int64_t pos = half ? P + tl : a + tl;
-            me.k = key_of(xprime(job, pos, h));
-            me.r = (int)(pos - P);
-            hx[tl] = me.k;
-            hxp[tl] = (uint16_t)pos;
-        }
-        __syncthreads();
-        if (tl < n) {               // counting rank within the set (distinct positions: a permutation)
-            int rk = 0;
-            for (int j = 0; j < n; ++j) {
-                const KP o = {hx[j], rel(hxp[j])};
-                rk += kp_less(o, me);
-            }
-            ho[rk] = me.k;
-            hop[rk] = hxp[tl];
-        }
-        __syncthreads();
-        const uint64_t *nk = ok, *rk = ok + kSlideL;
-        const uint16_t *np = op, *rp = op + kSlideL;
-        auto lb = [&](const uint64_t *k, const uint16_t *p, int cnt, const KP &x) -> int {
-            int lo = 0, hi = cnt;
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                const KP o = {k[mid], rel(p[mid])};
-                if (kp_less(o, x)) lo = mid + 1; else hi = mid;
-            }
-            return lo;
-        };
-        // survivors: a contiguous run of U per thread
-        const int per = (M + kSlideThreads - 1) / kSlideThreads;
-        const int ib = min(M, tid * per);
-        uint64_t mk[kPer];
-        uint32_t mpf[kPer];          // pos16 | fin << 16 (fin = 0xffff: leaving)
-        int iR = 0, iN = 0;
-        if (ib < M) {
-            const KP x0 = {sk[ib], rel(sp[ib])};
-            iR = lb(rk, rp, nr, x0);
-            iN = lb(nk, np, na, x0);
-        }
-#pragma unroll
-        for (int m = 0; m < kPer; ++m) {
-            const int i = ib + m;
-            mpf[m] = 0xffff0000u;
-            if (m < per && i < M) {
-                const uint16_t p16 = sp[i];
-                const KP x = {sk[i], rel(p16)};
-                while (iR < nr && kp_less(KP{rk[iR], rel(rp[iR])}, x)) ++iR;
-                while (iN < na && kp_less(KP{nk[iN], rel(np[iN])}, x)) ++iN;
-                mk[m] = x.k;
-                if (x.r >= nr) mpf[m] = (uint32_t)p16 | ((uint32_t)(i - iR + iN) << 16);
-            }
-        }
-        // entering element tid: its rank in the set + the survivors below it
-        int efin = -1;
-        uint64_t ek = 0;
-        uint16_t ep = 0;
-        if (tid < na) {
-            ek = nk[tid];
-            ep = np[tid];
-            const KP x = {ek, rel(ep)};
-            efin = tid + lb(sk, sp, M, x) - lb(rk, rp, nr, x);
-        }
-        __syncthreads();
-#pragma unroll
-        for (int m = 0; m < kPer; ++m) {
-            const uint32_t f = mpf[m] >> 16;
-            if (f != 0xffffu) { sk[f] = mk[m]; sp[f] = (uint16_t)(mpf[m] & 0xffffu); }
-        }
-        if (efin >= 0) { sk[efin] = ek; sp[efin] = ep; }
-        __syncthreads();
-        return M - nr + na;
-    };
-
-    // initial union of the first chunk: positions [P, P + w + L - 1)
-    int M = 0;
-    for (int64_t a = P; a < P + w + L - 1; a += kSlideL)
-        M = round(M, a, (int)min((int64_t)kSlideL, P + w + L - 1 - a), 0);
-    const int r_lo = (w % 2 == 0) ? (w / 2 - 1) : (w / 2);
-    for (;;) {
-        // ---- zone list E in U order: offsets < L-1 or >= w (excluded by some output's window)
-        const int per = (M + kSlideThreads - 1) / kSlideThreads;
-        const int ib = min(M, tid * per), ie = min(M, ib + per);
-        int cz = 0;
-        for (int i = ib; i < ie; ++i) {
-            const int pz = rel(sp[i]);
-            cz += (pz < L - 1) | (pz >= w);
-        }
-        int incl = cz;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += y;
-        }
-        if (lane == 63) s_scan[wid] = incl;
-        __syncthreads();
-        int off = 0, ne = 0;
-#pragma unroll
-        for (int v = 0; v < kSlideThreads / 64; ++v) {
-            const int x = s_scan[v];
-            off += (v < wid) ? x : 0;
-            ne += x;
-        }
-        int z = off + incl - cz;
-        for (int i = ib; i < ie; ++i) {
-            const int pz = rel(sp[i]);
-            if ((pz < L - 1) | (pz >= w)) E[z++] = ((uint32_t)i << 16) | (uint32_t)pz;
-        }
-        if (tid < 16) E[ne + tid] = 0xffffffffu;   // sentinels: U index 0xffff > any q
-        __syncthreads();
-        // ---- walk: output k's r-th smallest = U[q], q pushed up by every excluded zone entry below it
-        if (tid < L) {
-            const int k = tid;
-            int q = r_lo, j = 0, jstop = 0;
-            for (;;) {
-                const uint4 v = *reinterpret_cast<const uint4 *>(E + j);
-                const uint32_t es[4] = {v.x, v.y, v.z, v.w};
-                bool stop = false;
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    if (!stop) {
-                        const uint32_t e = es[t];
-                        if ((int)(e >> 16) > q) { stop = true; jstop = j + t; }
-                        else { const int pp = (int)(e & 0xffff); q += (pp < k) | (pp >= k + w); }
-                    }
-                }
-                if (stop) break;
-                j += 4;
-            }
-            const double v1 = val_of(sk[q]);
-            double out = v1;
-            if (w % 2 == 0) {
-                q = q + 1;
-                for (j = jstop;; ++j) {
-                    const uint32_t e = E[j];
-                    if ((int)(e >> 16) > q) break;
-                    const int pp = (int)(e & 0xffff);
-                    q += (pp < k) | (pp >= k + w);
-                }
-                out = (val_of(sk[q]) + v1) / 2.0;
-            }
-            job.dst[i0 + k - job.out_lo] = out;
-        }
-        // ---- next chunk: positions [P, P+L) leave, [P+w+L-1, P+L+w+L'-1) enter
-        const int64_t i1 = i0 + L;
-        if (i1 >= sg.o1) break;
-        const int L1 = (int)min((int64_t)kSlideL, sg.o1 - i1);
-        __syncthreads();          // E and U reads of the walk are done
-        M = round(M, P + w + L - 1, L1, L);
-        i0 = i1; L = L1; P = i0 - h;
-    }
-}
-
-size_t slide_smem(int w)
-{
-    return (size_t)(w + kSlideL - 1 + 4 * kSlideL) * 10 + 16 + 4 * (2 * kSlideL + 16);
 }
 
 // Segmented radix sort of the series keys (u64 keys, i32 positions).
@@ -1164,50 +765,6 @@ size_t walk_smem(int nwmax, int lt) { return 4 * (2 * (size_t)lt + 16) + 16 * (s
 constexpr int64_t kMaxOut = 65536;
 constexpr int32_t kMaxWindow = 32768;   // keeps U indices and offsets within 16 bits
 
-// Sliding-window plan: every job cut into segments of whole chunks, enough of
-// them to fill the chip (each segment pays one initial sort of its first window).
-static int plan_slide(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jobs, int32_t w)
-{
-    mp->slide = true;
-    const int mcap = w + kSlideL - 1;
-    mp->kper = mcap <= 4 * kSlideThreads ? 4 : mcap <= 8 * kSlideThreads ? 8 : mcap <= 16 * kSlideThreads ? 16 : 32;
-    int64_t total = 0;
-    for (const MedJob &j : jobs) total += std::max<int64_t>(0, j.out_hi - j.out_lo);
-    // aim for >= 1024 segments, but never shorter than max(8 chunks, 2 windows) of outputs
-    const int64_t want = (total + 1023) / 1024;
-    int64_t seg_len = std::max<int64_t>(want, std::max<int64_t>(8 * kSlideL, 2 * (int64_t)w));
-    seg_len = (seg_len + kSlideL - 1) / kSlideL * kSlideL;
-    std::vector<SlideSeg> segs;
-    for (size_t j = 0; j < jobs.size(); ++j) {
-        const int64_t lo = jobs[j].out_lo, hi = jobs[j].out_hi;
-        if (hi <= lo) continue;
-        const int64_t nseg = (hi - lo + seg_len - 1) / seg_len;
-        const int64_t len = ((hi - lo + nseg - 1) / nseg + kSlideL - 1) / kSlideL * kSlideL;   // balanced
-        for (int64_t o = lo; o < hi; o += len) {
-            SlideSeg sg;
-            sg.job = (int32_t)j; sg.pad_ = 0; sg.o0 = o; sg.o1 = std::min(hi, o + len);
-            segs.push_back(sg);
-        }
-    }
-    mp->nsegs = (int32_t)segs.size();
-    mp->njobs = (int32_t)jobs.size();
-    hipStream_t st = ctx->stream;
-    mp->alloc_stream = st;
-    // (comap_median_plan_free returns these to the temporaries cache)
-    COMAP_CHECK(ctx, comap_tmp_alloc((void **)&mp->jobs, sizeof(MedJob) * std::max<size_t>(1, jobs.size()), st));
-    COMAP_CHECK(ctx, comap_tmp_alloc((void **)&mp->segs, sizeof(SlideSeg) * std::max<size_t>(1, segs.size()), st));
-    if (!jobs.empty()) COMAP_CHECK(ctx, comap_upload(mp->jobs, jobs.data(), sizeof(MedJob) * jobs.size(), st));
-    if (!segs.empty()) COMAP_CHECK(ctx, comap_upload(mp->segs, segs.data(), sizeof(SlideSeg) * segs.size(), st));
-    COMAP_CHECK(ctx, hipEventCreateWithFlags(&mp->plan_ev, hipEventDisableTiming));
-    COMAP_CHECK(ctx, hipEventRecord(mp->plan_ev, st));
-    const int sm = (int)slide_smem(w);
-    COMAP_CHECK(ctx, hipFuncSetAttribute((const void *)k_med_slide<4>, hipFuncAttributeMaxDynamicSharedMemorySize, sm));
-    COMAP_CHECK(ctx, hipFuncSetAttribute((const void *)k_med_slide<8>, hipFuncAttributeMaxDynamicSharedMemorySize, sm));
-    COMAP_CHECK(ctx, hipFuncSetAttribute((const void *)k_med_slide<16>, hipFuncAttributeMaxDynamicSharedMemorySize, sm));
-    COMAP_CHECK(ctx, hipFuncSetAttribute((const void *)k_med_slide<32>, hipFuncAttributeMaxDynamicSharedMemorySize, sm));
-    return 0;
-}
-
 int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jobs_in, int32_t w)
 {
     mp->w = w;
@@ -1218,38 +775,21 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
     if (mp->lc != 64 && mp->lc != 256 && mp->lc != 512) mp->lc = 128;
     const char *k32 = getenv("COMAP_MEDIAN_KEY32");           // 0: sort the full u64 keys directly
     mp->key32 = !(k32 && !strcmp(k32, "0"));
-    // proxy bits: the series' key range is scaled onto this many bits and the radix sort
-    // runs bits / 8 digit passes; fewer bits = one pass less but more proxy collisions
-    // for k_med_fix (measured at C2: 24 bits 1.18 ms of median, 32 bits 1.00 ms)
-    const char *pb = getenv("COMAP_MEDIAN_PBITS");
-    mp->pbits = pb ? std::min(32, std::max(8, atoi(pb) / 8 * 8)) : 32;
+    // proxy bits: the series' key range is scaled onto 32 bits, 4 radix digit passes
+    // (24 bits: one pass less but more proxy collisions for k_med_fix, measured slower:
+    // C2 median 1.18 vs 1.00 ms with the device sort, 1.06 vs 0.88 with the block sort)
+    mp->pbits = 32;
     if (w < 1 || w > kMaxWindow) return comap_fail(ctx, -1, "median window must be 1 <= w <= 32768");
-    const char *force = getenv("COMAP_MEDIAN_PATH");         // "sort" / "slide": test both paths
-    const int mcap = w + kSlideL - 1;
-    const bool fits = slide_smem(w) <= 160 * 1024 && mcap <= 32 * kSlideThreads && mcap + kSlideL < 65536;
-    // the global-sort path is the default (measured faster at w = 6000); the sliding
-    // sorted window is selected with COMAP_MEDIAN_PATH=slide
-    if (fits && force && !strcmp(force, "slide")) return plan_slide(ctx, mp, jobs_in, w);
-    // Sub-job length: at most kMaxOut outputs (LDS bitmaps), and short enough that
-    // there are >= kMinSegs sorted segments -- the segmented sort runs one block per
-    // segment, so a plan of few long series (a C3 shard: ~100 of 16k outputs) would
-    // leave most CUs idle; each extra segment re-sorts w - 1 values.
-    const char *ms = getenv("COMAP_MEDIAN_MINSEGS");
-    const int64_t kMinSegs = ms ? atoll(ms) : 0;   // measured: splitting costs more than it fills (off)
+    // Sub-job length: at most kMaxOut outputs (LDS bitmaps).  (Splitting series further to
+    // put more sort segments on the chip at C3 shard size measured slower: each extra
+    // segment re-sorts w - 1 values.)
     int64_t total_out = 0;
     for (const MedJob &j : jobs_in) total_out += std::max<int64_t>(0, j.out_hi - j.out_lo);
     // the walk: wavelet matrix (default) or the bitmap walk (COMAP_MEDIAN_WALK=bitmap);
     // the wavelet matrix keeps ranks in 16 bits, so sub-jobs stay within 65536 positions
     const char *walk_env = getenv("COMAP_MEDIAN_WALK");
     mp->wm = !(walk_env && !strcmp(walk_env, "bitmap")) && w <= 16384;
-    // 4-ary levels only on request (measured at C2: 1.08 ms of median vs 0.99 binary)
-    mp->wmq = mp->wm && walk_env && !strcmp(walk_env, "wm4");
-    int64_t max_out = mp->wm ? std::min<int64_t>(kMaxOut, 65536 - (int64_t)w + 1) : kMaxOut;
-    if (kMinSegs > 0 && total_out > 0) {
-        const int64_t want = (total_out + kMinSegs - 1) / kMinSegs;
-        max_out = std::min<int64_t>(max_out, std::max<int64_t>(4 * (int64_t)kWalkThreads,
-                                                               (want + mp->lc - 1) / mp->lc * mp->lc));
-    }
+    const int64_t max_out = mp->wm ? std::min<int64_t>(kMaxOut, 65536 - (int64_t)w + 1) : kMaxOut;
     std::vector<MedJob> jobs;
     for (const MedJob &j : jobs_in) {
         if (j.out_hi - j.out_lo <= max_out) { jobs.push_back(j); continue; }
@@ -1304,7 +844,6 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
         // 16-bit sequence fit the LDS budget, and enough of them to fill the chip
         int L = 1;
         while ((int64_t)1 << L < numax) ++L;
-        if (mp->wmq) L = (L + 1) / 2 * 2;       // whole 2-bit digits
         const int64_t budget = 150 * 1024;
         const int64_t nwcap = std::min<int64_t>(kWmThreads, (budget - 8 * L) / (std::max(8 * L, 64) + 64));
         const int64_t seg_cap = nwcap * 32 - (w - 1);
@@ -1327,7 +866,7 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
                     SlideSeg sg;
                     sg.job = (int32_t)j; sg.pad_ = 0; sg.o0 = o; sg.o1 = std::min(jobs[j].out_hi, o + len);
                     wsegs.push_back(sg);
-                    smax = std::max(smax, wm_smem(L, (int)((sg.o1 - sg.o0 + w - 1 + 31) / 32), mp->wmq));
+                    smax = std::max(smax, wm_smem(L, (int)((sg.o1 - sg.o0 + w - 1 + 31) / 32)));
                 }
             }
             mp->wmL = L;
@@ -1382,7 +921,7 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
     COMAP_CHECK(ctx, hipEventCreateWithFlags(&mp->plan_ev, hipEventDisableTiming));
     COMAP_CHECK(ctx, hipEventRecord(mp->plan_ev, st));
     if (mp->wm) {
-        COMAP_CHECK(ctx, hipFuncSetAttribute(mp->wmq ? (const void *)k_med_wm4 : (const void *)k_med_wm,
+        COMAP_CHECK(ctx, hipFuncSetAttribute((const void *)k_med_wm,
                                              hipFuncAttributeMaxDynamicSharedMemorySize,
                                              (int)std::max<size_t>(mp->wm_smem, 16)));
         return 0;   // (the uploads went through staging: no host wait for the host vectors)
@@ -1409,19 +948,6 @@ void comap_median_plan_free(MedPlan *mp)
 int comap_median_run(comap_ctx *ctx, MedPlan *mp, hipStream_t st)
 {
     mp->run_stream = st;
-    if (mp->slide) {
-        if (mp->nsegs == 0) return 0;
-        if (mp->plan_ev && st != mp->alloc_stream) COMAP_CHECK(ctx, hipStreamWaitEvent(st, mp->plan_ev, 0));
-        const size_t sm = slide_smem(mp->w);
-        switch (mp->kper) {
-        case 4: k_med_slide<4><<<mp->nsegs, kSlideThreads, sm, st>>>(mp->jobs, mp->segs, mp->w); break;
-        case 8: k_med_slide<8><<<mp->nsegs, kSlideThreads, sm, st>>>(mp->jobs, mp->segs, mp->w); break;
-        case 16: k_med_slide<16><<<mp->nsegs, kSlideThreads, sm, st>>>(mp->jobs, mp->segs, mp->w); break;
-        default: k_med_slide<32><<<mp->nsegs, kSlideThreads, sm, st>>>(mp->jobs, mp->segs, mp->w); break;
-        }
-        COMAP_LAUNCH_CHECK(ctx);
-        return 0;
-    }
     if (mp->nchunks == 0) return 0;
     if (mp->plan_ev && st != mp->alloc_stream) COMAP_CHECK(ctx, hipStreamWaitEvent(st, mp->plan_ev, 0));
     dim3 g1(64, (unsigned)mp->njobs);
@@ -1463,10 +989,7 @@ int comap_median_run(comap_ctx *ctx, MedPlan *mp, hipStream_t st)
                                   mp->njobs, mp->seg, mp->seg + 1, st, mp->wide));
     }
     if (mp->wm) {   // the wavelet-matrix walk reads the sorted positions directly
-        if (mp->nsegs > 0 && mp->wmq)
-            k_med_wm4<<<mp->nsegs, kWmThreads, mp->wm_smem, st>>>(mp->jobs, mp->segs, mp->seg, mp->v1, mp->slo, mp->w,
-                                                                  mp->wmL / 2);
-        else if (mp->nsegs > 0)
+        if (mp->nsegs > 0)
             k_med_wm<<<mp->nsegs, kWmThreads, mp->wm_smem, st>>>(mp->jobs, mp->segs, mp->seg, mp->v1, mp->slo, mp->w,
                                                                  mp->wmL);
         COMAP_LAUNCH_CHECK(ctx);

@@ -1,5 +1,6 @@
 """C5 destriper alone (bench.destriper_c5_leg), for rocprofv3 kernel traces and PMC passes:
-    python scripts/ds_c5.py [n_obs] [n_bands] [niter]"""
+    python scripts/ds_c5.py [n_obs] [n_bands] [niter] [field]
+("field": bench.destriper_c5_field_leg, the configs[4] field solved as one system)"""
 import json
 import os
 import sys
@@ -14,7 +15,8 @@ def main():
     nb = int(sys.argv[2]) if len(sys.argv) > 2 else 4
     niter = int(sys.argv[3]) if len(sys.argv) > 3 else 50
     torch.cuda.set_device(0)
-    print(json.dumps(bench.destriper_c5_leg(n_obs, niter, 0, 1, 0, n_bands=nb)), flush=True)
+    leg = bench.destriper_c5_field_leg if 'field' in sys.argv[4:] else bench.destriper_c5_leg
+    print(json.dumps(leg(n_obs, niter, 0, 1, 0, n_bands=nb)), flush=True)
 
 
 if __name__ == '__main__':

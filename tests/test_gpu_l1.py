@@ -51,16 +51,16 @@ def test_medfilt_dropin_bit_exact(meta, golden_dir):
 
 
 def _median_path(path, monkeypatch):
-    """'slide': the sliding sorted window; 'sort': global sort + binary wavelet-matrix
-    walk (the default); 'wm4': 4-ary wavelet matrix; 'bitmap': the chunked bitmap walk."""
-    monkeypatch.setenv('COMAP_MEDIAN_PATH', 'slide' if path == 'slide' else 'sort')
-    monkeypatch.setenv('COMAP_MEDIAN_WALK', {'bitmap': 'bitmap', 'wm4': 'wm4'}.get(path, 'wm'))
+    """'sort': segments sorted in LDS (longer ones on the device-wide sort) + the
+    wavelet-matrix walk (the default); 'devsort': every segment on the device-wide
+    segmented sort; 'bitmap': the chunked bitmap walk (windows > 16384)."""
+    monkeypatch.setenv('COMAP_MEDIAN_BLOCKSORT', '0' if path == 'devsort' else '1')
+    monkeypatch.setenv('COMAP_MEDIAN_WALK', 'bitmap' if path == 'bitmap' else 'wm')
 
 
-@pytest.mark.parametrize('path', ['slide', 'sort', 'wm4', 'bitmap'])
+@pytest.mark.parametrize('path', ['sort', 'devsort', 'bitmap'])
 def test_medfilt_dropin_ties_and_edges(path, monkeypatch):
-    """Every device median path: the sliding sorted window (windows up to ~12k)
-    and the global-sort path (every window) with either walk."""
+    """Every device median path: either sort of the segments, either walk."""
     _median_path(path, monkeypatch)
     from comapreduce_amd.tools.medfilt import medfilt
     rng = np.random.default_rng(9)
@@ -70,7 +70,7 @@ def test_medfilt_dropin_ties_and_edges(path, monkeypatch):
         assert np.array_equal(medfilt(x.copy(), w), oracle.medfilt(x.copy(), w)), (n, w)
 
 
-@pytest.mark.parametrize('path', ['slide', 'sort', 'wm4', 'bitmap'])
+@pytest.mark.parametrize('path', ['sort', 'devsort', 'bitmap'])
 def test_medfilt_long_series_split(path, monkeypatch):
     """Series longer than one median sub-job / segment are split internally."""
     _median_path(path, monkeypatch)
@@ -84,8 +84,7 @@ def test_medfilt_long_series_split(path, monkeypatch):
     assert np.array_equal(got, oracle.medfilt(z, 400)[y.size:2 * y.size])
 
 
-@pytest.mark.parametrize('key32,lc,S', [('1', 'wm', ''), ('0', 'wm', ''), ('1', 'wm', '7'), ('1', 'wm4', ''),
-                                        ('1', 'wm4', '7'), ('1', '128', ''),
+@pytest.mark.parametrize('key32,lc,S', [('1', 'wm', ''), ('0', 'wm', ''), ('1', 'wm', '7'), ('1', '128', ''),
                                         ('0', '128', ''), ('1', '64', ''), ('1', '256', ''),
                                         ('1', '512', ''), ('1', '128', '1'), ('1', '128', '3'), ('1', '64', '16')])
 def test_medfilt_sort_proxy_runs(key32, lc, S, monkeypatch):
@@ -94,9 +93,8 @@ def test_medfilt_sort_proxy_runs(key32, lc, S, monkeypatch):
     re-sorted on u64 keys), signed zeros and negative values; u64-key path; the
     wavelet-matrix walk (one or several segments per series), and the bitmap walk with
     64/256/512-output chunks and 1..16 chunks per walk workgroup for comparison."""
-    monkeypatch.setenv('COMAP_MEDIAN_PATH', 'sort')
     monkeypatch.setenv('COMAP_MEDIAN_KEY32', key32)
-    if lc in ('wm', 'wm4'):
+    if lc == 'wm':
         monkeypatch.setenv('COMAP_MEDIAN_WALK', lc)
         if S:
             monkeypatch.setenv('COMAP_MEDIAN_WMSEGS', S)   # segments to fill the chip (splits every series)
