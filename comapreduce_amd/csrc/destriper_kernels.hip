@@ -415,6 +415,18 @@ struct alignas(16) SlotRec {
 };
 static_assert(sizeof(SlotRec<1>) == 16 && sizeof(SlotRec<2>) == 32 && sizeof(SlotRec<4>) == 48, "SlotRec");
 
+// Orders a wave's LDS writes before its later LDS reads by other lanes (and reads before
+// later overwrites) where each wave owns its LDS region: one wave's LDS operations execute
+// in issue order, so only the compiler must keep them in place.  A workgroup-scope fence
+// would also wait for every global load and store the wave has in flight (s_waitcnt
+// vmcnt(0)): the next chunk's prefetched loads and the previous chunk's stores.
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Offset rows of the sparse operator, one wave per row k (offset o = perm[k]): lane l
 // holds samples l, l + 64, ... (K per lane, L <= 64 K).  The distinct pixels of the
 // offset are found in first-occurrence order by a leader loop (the first pending
@@ -494,7 +506,7 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
             if constexpr (!FILL) ti[m][b] = tn[m][b];
         }
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // the staged weights, before other lanes read them
+    wave_lds_sync();   // the staged weights, before other lanes read them
     // leader loop: head lanes and their members (per chunk of the leader)
     bool head[K];
     unsigned long long mem[K][K];
@@ -522,7 +534,7 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
             hm[z] = 64;
             hb[z] = 0ull;
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        wave_lds_sync();
         const bool valid = lane < L;
         int slot = (int)(((uint32_t)q[0] * 2654435761u) >> 25);
         if (valid) {
@@ -534,7 +546,7 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
             atomicMin(&hm[slot], lane);
             atomicOr(&hb[slot], 1ull << lane);
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        wave_lds_sync();
         head[0] = valid && hm[slot] == lane;
         mem[0][0] = head[0] ? hb[slot] : 0ull;
     } else {
@@ -896,6 +908,19 @@ __global__ void k_cnt_natural(const int64_t *__restrict__ cnt, const int32_t *__
         cnt_nat[k < NO ? (perm ? (int64_t)perm[k] : k) : NO] = k < NO ? cnt[k] : 0;
 }
 
+// kint[k] = bit b set when band b keeps offset perm[k] (keep [nb][NO] in the caller's
+// offset order): the sample walk reads one byte per entry by its internal offset k
+__global__ void k_keep_bits(const uint8_t *__restrict__ keep, const int32_t *__restrict__ perm, int64_t NO, int nb,
+                            uint8_t *__restrict__ kint)
+{
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < NO; k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t o = perm ? (int64_t)perm[k] : k;
+        uint32_t m = 0;
+        for (int b = 0; b < nb; ++b) m |= (uint32_t)(keep[(int64_t)b * NO + o] != 0) << b;
+        kint[k] = (uint8_t)m;
+    }
+}
+
 // Count-form fill for the member-mask walk: row k's kept entries from the count pass's slots
 // into the CSR rows (pixel, packed counts), and the transpose's sort pairs (pixel key, slot
 // k L + r: the entry's walk record) in the caller's offset order (orow_nat), so the stable
@@ -1062,7 +1087,7 @@ __global__ void __launch_bounds__(256) k_sample_walk(const int64_t *__restrict__
                 for (int bb = 0; bb < NB; ++bb) m |= (uint32_t)(!keep || keep[(int64_t)bb * NO + o]) << bb;
                 mk[lane] = m;
             }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // the chunk, before other lanes read it
+            wave_lds_sync();   // the chunk, before other lanes read it
             if (lane < 3 * NB) {
                 if (kind == 2) {
                     for (int t = 0; t < n; ++t) acc = ((mk[t] >> b) & 1u) ? acc + 1.0 : acc;
@@ -1074,19 +1099,25 @@ __global__ void __launch_bounds__(256) k_sample_walk(const int64_t *__restrict__
                     }
                 }
             }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // read before the next chunk overwrites
+            wave_lds_sync();   // read before the next chunk overwrites
         }
         if (lane < 3 * NB) (kind == 0 ? h : kind == 1 ? nnum : hits)[p * NB + b] = acc;
     }
 }
 
-// one entry as the sample walk sees it
-template <int K, int NB>
-struct Ent {
-    uint32_t k, o, cnt;
-    uint64_t mask[K];
-    double wb[NB];
-};
+// every band's non-zero-weight count of a group is 0 or all n of its members (packed
+// 8-bit counts): the group's weights are the offset's wb or zero
+template <int NB>
+__device__ __forceinline__ bool uniform_counts(uint32_t gc, uint32_t n)
+{
+    bool u = true;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const uint32_t c = (gc >> (8 * b)) & 255u;
+        u = u && (c == 0u || c == n);
+    }
+    return u;
+}
 
 // position of the r-th (0-based) set bit of x (r < popcount(x)): six halving steps
 __device__ __forceinline__ int select_bit(uint64_t x, int r)
@@ -1123,7 +1154,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) k
                                                       const double *__restrict__ wbar,
                                                       const double *__restrict__ w, const double *__restrict__ ptw,
                                                       int64_t N, int64_t npix, int L, int64_t NO,
-                                                      const uint8_t *__restrict__ keep,
+                                                      const uint8_t *__restrict__ kint,
                                                       const uint32_t *__restrict__ hextra, double *__restrict__ h,
                                                       double *__restrict__ hits, double *__restrict__ nnum,
                                                       int32_t *__restrict__ poff, uint8_t *__restrict__ pcnt)
@@ -1143,32 +1174,35 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) k
         const int64_t p = hrow[i];
         const int64_t lo = hprow[i], hi = hprow[i + 1];
         double acc = 0.0;
+        // slot ids of a chunk's entries: each chunk loads the next chunk's as soon as its own
+        // extent is known, so they are in flight during its member gathers (lanes past the
+        // row's end re-read its last entry: an unconditional load, no select waiting on it)
+        int64_t si_n = sval[lo + lane < hi ? lo + lane : hi - 1];
         for (int64_t c = lo; c < hi;) {
             const int64_t e = c + lane;
+            const bool live = e < hi;
             // the entry's slot si = k L + r: its record (member mask, counts) from the count
-            // pass and the offset's weights from k -- two independent gathers (the caller's
-            // offset o only for a keep mask)
-            Ent<K, NB> en;
-            uint32_t cnt = 0;
-            if (e < hi) {
-                const int64_t si = sval[e];
-                const int64_t kk = si / L;
-                const SlotRec<K> rc = srec[si];
-                en.k = (uint32_t)kk;
-                en.o = (keep && perm) ? (uint32_t)perm[kk] : (uint32_t)kk;
-                en.cnt = rc.cnt;
-#pragma unroll
-                for (int q = 0; q < K; ++q) en.mask[q] = rc.mask[q];
-                ldb<NB>(wbar + kk * NB, en.wb);
-#pragma unroll
-                for (int q = 0; q < K; ++q) cnt += (uint32_t)__popcll(en.mask[q]);
+            // pass, the offset's weights and keep bits from k -- independent gathers
+            const int64_t si = si_n;
+            const int64_t kk = si / L;
+            SlotRec<K> rc;
+            double wb[NB];
+            uint32_t kb = (1u << NB) - 1u;
+            if (live) {
+                rc = srec[si];
+                ldb<NB>(wbar + kk * NB, wb);
+                if (kint) kb = kint[kk];
             } else {
-                en.k = en.o = en.cnt = 0;
+                rc.pix = 0;
+                rc.cnt = 0;
 #pragma unroll
-                for (int q = 0; q < K; ++q) en.mask[q] = 0ull;
+                for (int q = 0; q < K; ++q) rc.mask[q] = 0ull;
 #pragma unroll
-                for (int q = 0; q < NB; ++q) en.wb[q] = 0.0;
+                for (int q = 0; q < NB; ++q) wb[q] = 0.0;
             }
+            uint32_t cnt = 0;
+#pragma unroll
+            for (int q = 0; q < K; ++q) cnt += (uint32_t)__popcll(rc.mask[q]);
             // inclusive prefix of the member counts over the wave
             uint32_t inc = cnt;
 #pragma unroll
@@ -1176,19 +1210,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) k
                 const uint32_t v = __shfl_up(inc, sft, 64);
                 if (lane >= sft) inc += v;
             }
-            const bool take = e < hi && inc <= (uint32_t)CAP;
+            const bool take = live && inc <= (uint32_t)CAP;
             const int ntake = __popcll(__ballot(take));     // >= 1: one entry holds <= L <= CAP members
             const int total = (int)__shfl(inc, ntake - 1, 64);
             const uint32_t excl = inc - cnt;
-            uint32_t kb = 0;
-            if (take) {
-                poff[e] = (int32_t)en.k;
-                if constexpr (NB == 4) *reinterpret_cast<uint32_t *>(pcnt + e * 4) = en.cnt;
-                else if constexpr (NB == 2) *reinterpret_cast<uint16_t *>(pcnt + e * 2) = (uint16_t)en.cnt;
-                else pcnt[e] = (uint8_t)en.cnt;
-#pragma unroll
-                for (int bb = 0; bb < NB; ++bb) kb |= (uint32_t)(!keep || keep[(int64_t)bb * NO + en.o]) << bb;
-            }
             // the chunk's entry start positions (taken entries hold >= 1 member each)
             uint64_t sm[M];
 #pragma unroll
@@ -1211,15 +1236,28 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) k
                 j = t < total ? j - 1 : 0;
                 const uint32_t exj = (uint32_t)__shfl((int)excl, j, 64);
                 const uint32_t nmj = (uint32_t)__shfl((int)cnt, j, 64);
-                const uint32_t kj = (uint32_t)__shfl((int)en.k, j, 64);
+                const uint32_t kj = (uint32_t)__shfl((int)kk, j, 64);
                 const uint32_t kbj = (uint32_t)__shfl((int)kb, j, 64);
-                const uint32_t gcj = (uint32_t)__shfl((int)en.cnt, j, 64);
+                const uint32_t gcj = (uint32_t)__shfl((int)rc.cnt, j, 64);
                 uint64_t mj[K];
 #pragma unroll
-                for (int q = 0; q < K; ++q) mj[q] = (uint64_t)__shfl((long long)en.mask[q], j, 64);
+                for (int q = 0; q < K; ++q) mj[q] = (uint64_t)__shfl((long long)rc.mask[q], j, 64);
                 double wbj[NB];
 #pragma unroll
-                for (int q = 0; q < NB; ++q) wbj[q] = __shfl(en.wb[q], j, 64);
+                for (int q = 0; q < NB; ++q) wbj[q] = __shfl(wb[q], j, 64);
+                if (u == 0) {
+                    // the taken entries' pixel-major offset / counts for the CG bin, then the
+                    // next chunk's slot ids: issued after the wait for this chunk's records
+                    // and before its member gathers, they retire during those (in-order vmcnt)
+                    if (take) {
+                        poff[e] = (int32_t)kk;
+                        if constexpr (NB == 4) *reinterpret_cast<uint32_t *>(pcnt + e * 4) = rc.cnt;
+                        else if constexpr (NB == 2) *reinterpret_cast<uint16_t *>(pcnt + e * 2) = (uint16_t)rc.cnt;
+                        else pcnt[e] = (uint8_t)rc.cnt;
+                    }
+                    const int64_t en = c + ntake + lane;
+                    si_n = sval[en < hi ? en : hi - 1];
+                }
                 if (t < total) {
                     int r = t - (int)exj, bitpos = 0;
 #pragma unroll
@@ -1230,27 +1268,36 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) k
                     }
                     double pv[NB];
                     ldb<NB>(ptw + ((int64_t)kj * L + bitpos) * NB, pv);
+                    double wvs[NB];
 #pragma unroll
                     for (int bb = 0; bb < NB; ++bb) {
                         const uint32_t gc = (gcj >> (8 * bb)) & 255u;
-                        double wv = gc == nmj ? wbj[bb] : 0.0;
-                        if (gc != 0 && gc != nmj) {    // a mixed group: the sample's own weight
-                            const int64_t on = perm ? (int64_t)perm[kj] : (int64_t)kj;
-                            wv = w[(int64_t)bb * N + on * L + bitpos];
+                        wvs[bb] = gc == nmj ? wbj[bb] : 0.0;
+                    }
+                    if (!uniform_counts<NB>(gcj, nmj)) {
+                        // a mixed group (some members zero-weight in a band): the sample's own weight
+                        const int64_t on = perm ? (int64_t)perm[kj] : (int64_t)kj;
+#pragma unroll
+                        for (int bb = 0; bb < NB; ++bb) {
+                            const uint32_t gc = (gcj >> (8 * bb)) & 255u;
+                            if (gc != 0 && gc != nmj) wvs[bb] = w[(int64_t)bb * N + on * L + bitpos];
                         }
+                    }
+#pragma unroll
+                    for (int bb = 0; bb < NB; ++bb) {
                         const bool kept = (kbj >> bb) & 1u;
-                        pl[t * 3 * NB + bb] = kept ? wv : 0.0;
+                        pl[t * 3 * NB + bb] = kept ? wvs[bb] : 0.0;
                         pl[t * 3 * NB + NB + bb] = kept ? pv[bb] : 0.0;
                         pl[t * 3 * NB + 2 * NB + bb] = kept ? 1.0 : 0.0;
                     }
                 }
             }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // the chunk, before other lanes read it
+            wave_lds_sync();   // the chunk, before other lanes read it
             if (lane < 3 * NB) {
 #pragma unroll 8
                 for (int t = 0; t < total; ++t) acc += pl[t * 3 * NB + lane];
             }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // read before the next chunk overwrites
+            wave_lds_sync();   // read before the next chunk overwrites
             c += ntake;
         }
         if (lane < 3 * NB) {
@@ -2113,7 +2160,7 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
              Arena::bytes<int32_t>(1) + 2 * Arena::bytes<uint64_t>(N) + Arena::bytes<int64_t>(NO / 32 + 2) +
              Arena::bytes<uint64_t>((size_t)N * rec_words) +
              Arena::bytes<uint32_t>((size_t)npix * NB) +
-             2 * Arena::bytes<int64_t>(NO + 1) + Arena::bytes<int32_t>(2);
+             2 * Arena::bytes<int64_t>(NO + 1) + Arena::bytes<int32_t>(2) + Arena::bytes<uint8_t>(NO);
     COMAP_CHECK(ctx, comap_tmp_alloc((void **)&ar.base, ar.cap, st));
     struct ArenaFree {
         Arena *a;
@@ -2145,6 +2192,7 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     uint32_t *hextra = ar.take<uint32_t>((size_t)npix * NB);
     int64_t *cnt_nat = ar.take<int64_t>(NO + 1), *orow_nat = ar.take<int64_t>(NO + 1);
     int32_t *nonfin = ar.take<int32_t>(2);       // [non-finite tod, pixel index >= npix]
+    uint8_t *kint = keep ? ar.take<uint8_t>(NO) : nullptr;   // keep bits by internal offset (sample walk)
     bool walk = true;
     {
         const char *we = getenv("COMAP_DS_WALK");        // 0: the sorted-sample payload walk
@@ -2316,10 +2364,14 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     // ---- 5. sample-level maps (binValues order)
     const unsigned wgrid = (unsigned)std::min<int64_t>((npix + 3) / 4, 65536);
     if (walk) {
+        if (kint) {
+            k_keep_bits<<<grid_for(NO, 8192), 256, 0, st>>>(keep, d->perm, NO, nb, kint);
+            COMAP_LAUNCH_CHECK(ctx);
+        }
         // member slots per lane and chunk: 64 KW (one entry's members fit a chunk); one wave per
         // row (a fixed 2048-block grid: C5 0.80 -> 1.04 ms)
 #define COMAP_W2(KK, MM) k_sample_walk2<NB, KK, MM><<<wgrid, 256, 0, st>>>(                                   \
-        d->hrow, d->hprow, counts, evn2, (const SlotRec<KK> *)srec, d->perm, d->wbar, w, payload, N, npix, L, NO, keep, \
+        d->hrow, d->hprow, counts, evn2, (const SlotRec<KK> *)srec, d->perm, d->wbar, w, payload, N, npix, L, NO, kint, \
         hextra, d->h, d->hits, d->nnum, d->poff, d->pcnt)
         if (KW == 1) { COMAP_NB_SWITCH(nb, COMAP_W2(1, 1)); }
         else if (KW == 2) { COMAP_NB_SWITCH(nb, COMAP_W2(2, 2)); }

@@ -29,8 +29,8 @@ for step in "$@"; do
            d=gpurun_out/${TAG}_pmc_$(echo $cnt | tr ' ' '_' | cut -c1-40)
            timeout -s KILL 300 rocprofv3 --pmc $cnt --output-format csv -d $d -o run -- python3 bench.py $bargs \
              > $d.log 2>&1 ;;
-    dsprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_dstrace -o run \
-             -- python3 scripts/ds_c5.py ${arg:-8 4 50} > gpurun_out/${TAG}_dsprof.log 2>&1 ;;
+    dsprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_dstrace${NSTEP} -o run \
+             -- python3 scripts/ds_c5.py ${arg:-8 4 50} > gpurun_out/${TAG}_dsprof${NSTEP}.log 2>&1 ;;
     dspmc) cnt=${arg%%@*}; dargs=${arg#*@}; [ "$dargs" = "$arg" ] && dargs="8 4 20"
            d=gpurun_out/${TAG}_dspmc_$(echo $cnt | tr ' ' '_' | cut -c1-40)
            timeout -s KILL 240 rocprofv3 --pmc $cnt --output-format csv -d $d -o run -- python3 scripts/ds_c5.py $dargs \
