@@ -1145,7 +1145,7 @@ __device__ __forceinline__ int select_bit(uint64_t x, int r)
 // an entry carry zero weights (they add nothing to h or to the naive numerator); their
 // hits come from the count pass's integer adds.
 template <int NB, int K, int M>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) k_sample_walk2(const int32_t *__restrict__ hrow,
+__global__ void __launch_bounds__(256) k_sample_walk2(const int32_t *__restrict__ hrow,
                                                       const int64_t *__restrict__ hprow,
                                                       const int64_t *__restrict__ counts,
                                                       const int32_t *__restrict__ sval,
