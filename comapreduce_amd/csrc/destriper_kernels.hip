@@ -2396,6 +2396,48 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     return 0;
 }
 
+namespace {
+__device__ __forceinline__ int32_t relabel_one(int32_t p32, const int32_t *__restrict__ lut, int64_t npix, int64_t nt)
+{
+    const int64_t p = p32;
+    if (p >= npix || p < -npix) return (int32_t)nt;
+    return p >= 0 ? lut[p] : (int32_t)((int64_t)lut[npix + p] - nt);
+}
+
+// four ids per thread (16-B loads and stores; torch's blocks are 256-B aligned), the tail
+// one by one
+__global__ void k_relabel_pixels(const int32_t *__restrict__ pix, int64_t n, const int32_t *__restrict__ lut,
+                                 int64_t npix, int64_t nt, int32_t *__restrict__ out)
+{
+    const int64_t n4 = ((uintptr_t)pix % 16 == 0 && (uintptr_t)out % 16 == 0) ? n / 4 : 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    for (int64_t i = t0; i < n4; i += stride) {
+        const int4 v = reinterpret_cast<const int4 *>(pix)[i];
+        int4 r;
+        r.x = relabel_one(v.x, lut, npix, nt);
+        r.y = relabel_one(v.y, lut, npix, nt);
+        r.z = relabel_one(v.z, lut, npix, nt);
+        r.w = relabel_one(v.w, lut, npix, nt);
+        reinterpret_cast<int4 *>(out)[i] = r;
+    }
+    for (int64_t i = 4 * n4 + t0; i < n; i += stride) out[i] = relabel_one(pix[i], lut, npix, nt);
+}
+}  // namespace
+
+extern "C" int comap_relabel_pixels(comap_ctx *ctx, const int32_t *pix, int64_t n, const int32_t *lut, int64_t npix,
+                                    int64_t n_internal, int32_t *out)
+{
+    if (!ctx || (n > 0 && (!pix || !lut || !out)) || n < 0 || npix <= 0 || n_internal < npix ||
+        n_internal >= (1ll << 31))
+        return -1;
+    COMAP_DEVICE_GUARD(ctx);
+    if (n == 0) return 0;
+    k_relabel_pixels<<<grid_for((n + 3) / 4, 16384), 256, 0, ctx->stream>>>(pix, n, lut, npix, n_internal, out);
+    COMAP_LAUNCH_CHECK(ctx);
+    return 0;
+}
+
 extern "C" int comap_destripe_create(comap_ctx *ctx, const int32_t *pix, const double *tod, const double *w,
                                      int64_t N, int32_t L, int64_t npix, comap_destriper **out)
 {

@@ -715,13 +715,16 @@ class DeviceDestriper:
         pix = pixels.to(device=dev, dtype=torch.int32).reshape(-1) if isinstance(pixels, torch.Tensor) else \
             torch.from_numpy(np.ascontiguousarray(pixels, dtype=np.int32)).to(dev).reshape(-1)
         ids, nt = tiled_layout(ny, nx, T, dev)
-        # int32 throughout and no host sync: an id outside [-npix, npix) becomes nt, which the
-        # set-up's device range check rejects (IndexError), as it would the original id
-        bad = (pix >= npix) | (pix < -npix)
-        neg = pix < 0
-        t = ids.index_select(0, torch.where(bad, torch.zeros_like(pix), torch.where(neg, pix + npix, pix)))
+        # one device pass (comap_relabel_pixels), no host sync: an id outside [-npix, npix)
+        # becomes nt, which the set-up's device range check rejects (IndexError), as it
+        # would the original id
+        out = torch.empty_like(pix)
+        c = N.ctx(dev.index)
+        N.bind_stream(c, dev)
+        N.check(N.lib().comap_relabel_pixels(c, N.dptr(pix), pix.numel(), N.dptr(ids), int(npix), int(nt),
+                                             N.dptr(out)), c, 'comap_relabel_pixels')
         self.layout = ids
-        return torch.where(bad, torch.full_like(pix, nt), torch.where(neg, t - nt, t)), nt
+        return out, nt
 
     def _untile(self, v, nb):
         """[npix_internal * nb] interleaved map -> the caller's row-major [npix * nb]."""

@@ -318,6 +318,14 @@ int comap_destripe_div_map(comap_destriper *d, const double *num_dev, const doub
 int comap_destripe_solve(comap_destriper *d, double threshold, int32_t niter, double *x_dev,
                          double *map_dev, double *naive_dev, double *weight_dev,
                          double *hits_dev, int32_t *iters_out);
+/* Pixel ids onto an internal map layout (the 2-D tiled layout of DeviceDestriper's
+ * map_shape): out[i] = lut[p] for 0 <= p < npix, lut[npix + p] - n_internal for
+ * -npix <= p < 0 (an unbinned sample's id p reads m[npix + p]: the negative id that
+ * reads the same pixel of the internal map), n_internal for any other id (the set-up's
+ * range check then rejects it, as it would the original).  Device pointers; one pass,
+ * no host sync (replaces Destriper.py's row-major m[pointing] indexing order only). */
+int comap_relabel_pixels(comap_ctx *ctx, const int32_t *pix_dev, int64_t n, const int32_t *lut_dev, int64_t npix,
+                         int64_t n_internal, int32_t *out_dev);
 
 /* ------------------------------------------------------------ destriper data prep (COMAPData.py) */
 /* One Level-2 file's inputs to comap_prep_gather (device pointers).  Output row r

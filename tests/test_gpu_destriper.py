@@ -361,6 +361,33 @@ def test_graph_driver_matches_batched(niter):
     assert np.array_equal(xg.cpu().numpy(), xb.cpu().numpy())
 
 
+def test_library_calls_after_capture_on_another_stream():
+    """After the graph driver's capture (library temporaries may be freed while the stream
+    is capturing: their reuse event is null), calls bound to a different stream take fresh
+    or safely reusable blocks and leave no stale HIP error behind for the next launch check
+    (capi.hip make_safe / comap_upload clear the error of a failed query)."""
+    import torch
+    from comapreduce_amd import _native as N
+    from comapreduce_amd.mapmaking.destriper import DeviceDestriper, DeviceOps, cg_solve_graph
+    from comapreduce_amd.tools.medfilt import medfilt_batch
+    import oracle
+    p, tods, ws, keep = _bands_problem(4)
+    ops = DeviceOps(p, tods, ws, L, NPIX, keep=keep)
+    cg_solve_graph(ops, lambda a: a, threshold=1e-6, niter=20)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        N.bind_stream(N.ctx(0), torch.device('cuda', 0))
+        x = np.random.default_rng(2).standard_normal(5000)
+        got = medfilt_batch([x], 401, reflect=True)[0]
+        z = np.concatenate((x[::-1], x, x[::-1]))
+        assert np.array_equal(got, oracle.medfilt(z, 401)[x.size:2 * x.size])
+        r = DeviceDestriper(p, tods[0], ws[0], L, NPIX).solve(1e-6, 100)
+        assert r['iters'] > 0
+    torch.cuda.synchronize()
+    N.bind_stream(N.ctx(0), torch.device('cuda', 0))
+
+
 def _nccl_graph_rank(port, q):
     """One-rank RCCL process group: the graph driver captures real ncclAllReduce calls."""
     import torch
@@ -523,6 +550,31 @@ def test_tiled_layout_equals_row_major(nb, wrap, monkeypatch):
             assert np.array_equal(np.asarray(hres['maps'][k]), m[k]), (T, k)
     with pytest.raises(ValueError):
         DeviceDestriper(*args, map_shape=(60, 61), **kw)
+
+
+def test_relabel_pixels_kernel():
+    """comap_relabel_pixels (the tiled layout's one-pass relabel) against its numpy
+    statement: ids in [0, npix) through the table, ids in [-npix, 0) to the negative id
+    that reads the same internal pixel, anything else to n_internal."""
+    import torch
+    from comapreduce_amd import _native as N
+    from comapreduce_amd.mapmaking.destriper import tiled_layout
+    ny, nx, T = 37, 53, 8
+    npix = ny * nx
+    ids, nt = tiled_layout(ny, nx, T, torch.device('cuda', 0))
+    rng = np.random.default_rng(3)
+    p = rng.integers(-npix - 40, npix + 40, 200_003).astype(np.int32)
+    p[:4] = [0, npix - 1, -1, -npix]
+    pd = torch.from_numpy(p).cuda()
+    out = torch.empty_like(pd)
+    c = N.ctx(0)
+    N.bind_stream(c, torch.device('cuda', 0))
+    N.check(N.lib().comap_relabel_pixels(c, N.dptr(pd), pd.numel(), N.dptr(ids), npix, nt, N.dptr(out)), c, 'relabel')
+    lut = ids.cpu().numpy().astype(np.int64)
+    q = p.astype(np.int64)
+    want = np.where((q >= npix) | (q < -npix), nt,
+                    np.where(q >= 0, lut[np.clip(q, 0, npix - 1)], lut[np.clip(q + npix, 0, npix - 1)] - nt))
+    assert np.array_equal(out.cpu().numpy().astype(np.int64), want)
 
 
 @pytest.mark.parametrize('nb', [1, 3, 4])
