@@ -14,10 +14,10 @@ plan() compares the two for the expected iteration count and returns the faster.
 
 The a / b / s constants are fitted to this build's single-GPU measurements (bench.py
 C4 and C5 legs, count-form operator, tiled pixel layout, round 5: 1 band 21.8 / 124 us per
-iteration at 1.76 M / 27.36 M samples, 4 bands 29.9 / 275 us; set-up 1 band 2.70 ms and 4
-bands 3.43 / 24.1 ms at 27.36 M / 218.9 M samples -- the 64-observation field, whose
-iteration, 1.61 ms, the per-sample model overestimates: its pointing holds fewer entries
-per sample).
+iteration at 1.76 M / 27.36 M samples, 4 bands 29.9 / 275 us; set-up 1 band 2.58 ms and 4
+bands 3.21 / 22.0 ms at 27.36 M / 218.9 M samples (profiles/r05/r05x_bench.log) -- the
+64-observation field, whose iteration, 1.47 ms, the per-sample model overestimates: its
+pointing holds fewer entries per sample).
 alpha and beta cannot be measured on the one-GPU box (it cannot run two RCCL ranks; a
 one-rank all-reduce costs 10 us of host enqueue, profiles/r03/r03n_rccl_one_rank.log).
 Until a multi-GPU run has measured them, alpha(n) = 10 us + 2 (n - 1) x 1.5 us per ring
@@ -53,8 +53,8 @@ def _load_measured(path=MEASURED):
 class CostModel:
     a_us: float = 14.0                                   # per-iteration latency floor
     b_us_per_msample: dict = field(default_factory=lambda: {1: 3.99, 2: 6.5, 4: 9.57})
-    setup0_ms: dict = field(default_factory=lambda: {1: 0.24, 2: 0.36, 4: 0.48})
-    setup1_ms_per_msample: dict = field(default_factory=lambda: {1: 0.090, 2: 0.10, 4: 0.108})
+    setup0_ms: dict = field(default_factory=lambda: {1: 0.24, 2: 0.38, 4: 0.53})
+    setup1_ms_per_msample: dict = field(default_factory=lambda: {1: 0.086, 2: 0.092, 4: 0.098})
     alpha0_us: float = 10.0                              # one all-reduce: enqueue / protocol floor
     alpha_hop_us: float = 1.5                            # per ring step (2 (n - 1) steps)
     beta_gbs: float = 100.0                              # all-reduce bus bandwidth
