@@ -216,6 +216,20 @@ struct Coef<NB, false> {
     __device__ __forceinline__ double get(int b) const { return v[b]; }
 };
 
+// Inclusive prefix sum over the 64 lanes by DPP: row_shr 1 / 2 / 4 / 8 inside each 16-lane
+// row (zeros shifted in), then row_bcast 15 / 31 carry the row totals into the later rows.
+// Every lane must be active.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
+{
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);   // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);   // row_bcast:15 -> rows 1, 3
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);   // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
 __device__ __forceinline__ double wave_sum(double v)
 {
 #pragma unroll
@@ -1165,8 +1179,10 @@ __global__ void __launch_bounds__(256) k_sample_walk2(const int32_t *__restrict_
     // keep the member's offset -- adding +0 leaves a sum that never holds -0 unchanged, so
     // lane l < 3 NB runs its ordered sum as one unconditional chain over column l
     __shared__ double spl[4][CAP * 3 * NB];
+    __shared__ uint8_t sfl[4][CAP];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     double *pl = spl[wv];
+    uint8_t *fl = sfl[wv];
     const int kind = lane / NB, b = lane % NB;     // this lane's ordered sum (lanes < 3 NB)
     // the non-empty rows only (k_hit_flags wrote the empty ones): row i of nh = counts[1]
     const int64_t nh = counts[1];
@@ -1203,26 +1219,22 @@ __global__ void __launch_bounds__(256) k_sample_walk2(const int32_t *__restrict_
             uint32_t cnt = 0;
 #pragma unroll
             for (int q = 0; q < K; ++q) cnt += (uint32_t)__popcll(rc.mask[q]);
-            // inclusive prefix of the member counts over the wave
-            uint32_t inc = cnt;
-#pragma unroll
-            for (int sft = 1; sft < 64; sft <<= 1) {
-                const uint32_t v = __shfl_up(inc, sft, 64);
-                if (lane >= sft) inc += v;
-            }
+            // inclusive prefix of the member counts over the wave (DPP, no LDS permutes)
+            const uint32_t inc = wave_incl_scan(cnt);
             const bool take = live && inc <= (uint32_t)CAP;
             const int ntake = __popcll(__ballot(take));     // >= 1: one entry holds <= L <= CAP members
             const int total = (int)__shfl(inc, ntake - 1, 64);
             const uint32_t excl = inc - cnt;
-            // the chunk's entry start positions (taken entries hold >= 1 member each)
+            // the chunk's entry start positions (taken entries hold >= 1 member each): each
+            // taken entry flags its first slot in LDS, a ballot per 64 slots reads them back
             uint64_t sm[M];
 #pragma unroll
-            for (int u = 0; u < M; ++u) {
-                uint64_t bit = (take && (int)(excl >> 6) == u) ? (1ull << (excl & 63)) : 0ull;
+            for (int u = 0; u < M; ++u) fl[lane + 64 * u] = 0;
+            wave_lds_sync();
+            if (take) fl[excl] = 1;
+            wave_lds_sync();
 #pragma unroll
-                for (int sft = 32; sft > 0; sft >>= 1) bit |= (uint64_t)__shfl_xor((long long)bit, sft, 64);
-                sm[u] = bit;
-            }
+            for (int u = 0; u < M; ++u) sm[u] = __ballot(fl[lane + 64 * u] != 0);
 #pragma unroll
             for (int u = 0; u < M; ++u) {
                 const int t = lane + 64 * u;
