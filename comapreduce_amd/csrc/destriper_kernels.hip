@@ -516,11 +516,13 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
         rem[m] = __ballot(lane + 64 * m < L);
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
-            wl[(64 * m + lane) * NB + b] = wn[m][b];
-            if constexpr (!FILL) ti[m][b] = tn[m][b];
+            if constexpr (FILL) wl[(64 * m + lane) * NB + b] = wn[m][b];
+            else ti[m][b] = tn[m][b];
         }
     }
-    wave_lds_sync();   // the staged weights, before other lanes read them
+    // (the fill pass reads group members' weights from LDS; the count pass stages them only
+    // for an offset whose weights fail the count-form test, below)
+    if constexpr (FILL) wave_lds_sync();
     // leader loop: head lanes and their members (per chunk of the leader)
     bool head[K];
     unsigned long long mem[K][K];
@@ -594,7 +596,7 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
 #pragma unroll
         for (int m = 0; m < K; ++m)
 #pragma unroll
-            for (int b = 0; b < NB; ++b) wi[m][b] = wl[(64 * m + lane) * NB + b];
+            for (int b = 0; b < NB; ++b) wi[m][b] = wn[m][b];
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
             double ref = 0.0;
@@ -614,6 +616,13 @@ __global__ void __launch_bounds__(256) k_ds_rows(const int32_t *__restrict__ pix
             }
             refb[b] = ref;
             uni &= __ballot(bad) == 0ull;
+        }
+        if (!uni) {      // wave-uniform: the group sums below read members' weights
+#pragma unroll
+            for (int m = 0; m < K; ++m)
+#pragma unroll
+                for (int b = 0; b < NB; ++b) wl[(64 * m + lane) * NB + b] = wi[m][b];
+            wave_lds_sync();
         }
     }
     // per head: the group's in-order weight sums per band (and, for the count form, its
