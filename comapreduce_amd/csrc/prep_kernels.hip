@@ -618,8 +618,14 @@ __global__ void __launch_bounds__(256) k_prep_gather(comap_prep_file f, comap_pr
 }
 
 // ---------------------------------------------------------------- running-median high-pass
-// segment k = x[seg[2k] .. seg[2k] + seg[2k+1]); its median input = the non-zero finite samples
-__device__ __forceinline__ bool hp_keep(double v) { return v != 0.0 && isfinite(v); }
+// segment k = x[seg[2k] .. seg[2k] + seg[2k+1]); its median input = the non-zero samples
+// (bad = tod == 0, COMAPData.py:357-360) that are not NaN.  +-inf stays in, as in the
+// reference (the two-heap orders +-inf like any value, so the window median is still an
+// order statistic).  NaN is left out: np.nanmedian (the <= 2w branch, :79) ignores it, so
+// short segments match the reference with NaN too; in the running median (> 2w) the
+// reference's result for a window holding NaN depends on its two-heap's history, which
+// the order-statistics kernels do not reproduce.
+__device__ __forceinline__ bool hp_keep(double v) { return v != 0.0 && !isnan(v); }
 
 __global__ void __launch_bounds__(256) k_seg_count(const double *__restrict__ x, const int64_t *__restrict__ seg,
                                                    int64_t *__restrict__ cnt)
@@ -667,9 +673,9 @@ __global__ void __launch_bounds__(256) k_seg_compact(const double *__restrict__ 
 
 // Segments with 1 .. 2w median-input values: np.nanmedian of the values (COMAPData.py:79),
 // broadcast.  One workgroup per segment (the others exit at once): every value's rank =
-// the values below it plus the equal ones before it (the values are finite and non-zero),
-// so the sorted order needs no sort; even counts average the two middle values as
-// np.median does ((a + b) / 2).
+// the values below it plus the equal ones before it (the values are non-zero and not NaN;
+// +-inf compare like any value), so the sorted order needs no sort; even counts average
+// the two middle values as np.median does ((a + b) / 2).
 constexpr int kSmallSeg = 2048;
 __global__ void __launch_bounds__(256) k_seg_small_median(const double *__restrict__ vals,
                                                           const int64_t *__restrict__ off,
@@ -923,7 +929,7 @@ extern "C" int comap_prep_highpass(comap_ctx *ctx, double *x, const int64_t *seg
         }
         if (rc) return rc;
     }
-    // short segments: np.nanmedian of their (finite) values -- a mean of the two middle
+    // short segments: np.nanmedian of their (non-NaN) values -- a mean of the two middle
     // values for an even count -- broadcast (np.ones(n) * m)
     if (any_small_dev) {
         k_seg_small_median<<<nseg, 256, 0, st>>>(vals, off, cnt, nsmall_dev, filt);

@@ -179,6 +179,63 @@ def test_gpu_highpass_vs_reference_medfilt(w):
 
 
 @pytest.mark.gpu
+def test_gpu_highpass_nonfinite_vs_reference():
+    """COMAPData.median_filter on non-zero samples that include +-inf and NaN
+    (COMAPData.py:72-81, 357-360): +-inf stays in the running median's input (single
+    samples, runs that make window medians +-inf, windows whose middle pair is -inf / +inf
+    -> NaN); short segments (<= 2w non-zero values, NaN included) get np.nanmedian of
+    the non-NaN values; NaN samples stay NaN.  Checked against oracle.medfilt, which
+    test_oracle_golden pins to the reference's compiled filter on +-inf input.  (Long
+    segments holding NaN are unpinned, DESIGN.md §9, and are not in this fixture.)"""
+    import torch
+    import oracle
+    from comapreduce_amd import _native as N
+    c = N.ctx(0)
+    N.bind_stream(c, torch.device('cuda', 0))
+    w = 400
+    rng = np.random.default_rng(77)
+    lens = [3000, 2 * w + 3, 5000, 500, 700, 120, 4000]
+    parts = []
+    for k, n in enumerate(lens):
+        v = np.round(rng.standard_normal(n) * 4, 1)
+        v[rng.random(n) < 0.1] = 0.0
+        if n > 2 * w:                                   # running median: +-inf only
+            v[rng.random(n) < 0.02] = np.inf
+            v[rng.random(n) < 0.02] = -np.inf
+            if k == 2:
+                v[1000:1250] = np.inf                   # window medians +inf
+                v[1250:1500] = -np.inf                  # middle pair -inf / +inf -> NaN
+        else:                                           # np.nanmedian: NaN and +-inf
+            v[rng.random(n) < 0.15] = np.nan
+            v[3] = np.inf
+            if k == 5:
+                v[:] = np.nan                           # all NaN: nanmedian NaN
+        parts.append(v)
+    x = np.concatenate(parts)
+    starts = np.concatenate(([0], np.cumsum(lens)[:-1]))
+    segs = np.stack([starts, np.asarray(lens)], axis=1).astype(np.int64)
+    sd = torch.as_tensor(segs, device='cuda')
+    xd = torch.as_tensor(x, device='cuda')
+    N.check(N.lib().comap_prep_highpass(c, N.dptr(xd), N.dptr(sd), len(lens), w), c, 'highpass')
+    got = xd.cpu().numpy()
+    with np.errstate(invalid='ignore'):
+        for s0, n in segs:
+            seg = x[s0:s0 + n]
+            nz = seg != 0
+            v = seg[nz]
+            if v.size > 2 * w:
+                z = np.concatenate((v[::-1], v, v[::-1]))
+                f = oracle.medfilt(z, w)[v.size:2 * v.size]
+            else:
+                f = np.ones(v.size) * (np.nanmedian(v) if (~np.isnan(v)).any() else np.nan)
+            want = seg.copy()
+            want[nz] = v - f
+            assert np.array_equal(got[s0:s0 + n], want, equal_nan=True), (s0, n)
+            if v.size > 2 * w:
+                assert np.isinf(f).any() or n != 5000
+
+
+@pytest.mark.gpu
 def test_gpu_medfilt_batch_reflect_bit_exact():
     import oracle
     from comapreduce_amd.tools.medfilt import medfilt_batch
@@ -248,11 +305,12 @@ def test_read_comap_data_bands_equals_per_band(case_store):
 
 @pytest.mark.gpu
 def test_nan_samples_do_not_abort_prep(case_store):
-    """A non-finite Level-2 sample (e.g. a zero vane gain upstream) is left out of
-    the 400-sample median input instead of aborting the run; it ends with tod 0 and
-    weight 0 as in the reference (COMAPData.py:550-552).  The other samples of its
-    series are filtered against the median of the finite ones (parity unpinned for
-    such a series)."""
+    """A NaN Level-2 sample (e.g. a zero vane gain upstream) in a scan longer than 2 x 400
+    is left out of the running-median input instead of aborting the run; it ends with
+    tod 0 and weight 0 as in the reference (COMAPData.py:550-552).  The other samples of
+    its series are filtered against the running median of the non-NaN ones (parity
+    unpinned for such a series: the reference's two-heap result then depends on its
+    insertion history)."""
     store, names = case_store
     ds, attrs = store[names[1]]
     ds = dict(ds)
@@ -329,6 +387,65 @@ def test_gpu_prep_selected_feeds_missing_from_file(case_store):
     feeds = list(cc.FEEDS) + [f for f in range(1, 20) if f not in cc.FEEDS][:3]
     ref = oc.read_comap_data(names, store, map_info(case['map']), feeds=feeds, **case['kw'])
     got = cd.read_comap_data(names, map_info(case['map']), feeds=feeds, store=store, **case['kw'])
+    for k, a, b in zip(cc.OUTPUTS, got, ref):
+        a, b = np.asarray(a), np.asarray(b)
+        assert a.shape == b.shape, k
+        if k in TRIG:
+            assert np.max(np.abs(a - b)) <= 1e-12 * max(np.max(np.abs(b)), 1.0), k
+        else:
+            assert np.array_equal(a, b), k
+
+
+def _nonfinite_store(case_store):
+    """The 82-scan file with +-inf samples inside 900-sample scans (the running median
+    over > 2 x 400 values: the reference keeps +-inf in its input, bad = tod == 0,
+    COMAPData.py:357-360) of file feed 0, and NaN inside 120- and 260-sample scans
+    (np.nanmedian, :79: NaN ignored) of file feed 2.  +-inf makes feed 0's auto_rms weight
+    non-finite, so the cut drops its offsets (:550-557); NaN leaves feed 2's weight finite
+    and its short scans visible.  medfilt_batch pins +-inf inside the running median
+    itself (test_gpu_l1.py::test_medfilt_dropin_infinities)."""
+    store, names, S = _many_scans_store(case_store)
+    ds, attrs = store[names[0]]
+    ds = dict(ds)
+    tod = ds['averaged_tod/tod'].copy()
+    edges = ds['averaged_tod/scan_edges']
+    lengths = edges[:, 1] - edges[:, 0]
+    longs = edges[lengths == 900]
+    shorts = edges[(lengths == 120) | (lengths == 260)]
+    assert len(longs) >= 3 and len(shorts) >= 4
+    for k, (s, e) in enumerate(longs[:3]):
+        tod[0, :, s + 300 + 7 * k] = np.inf
+        tod[0, :, s + 420:s + 426] = np.inf                 # a run: shifts the order by 6
+        tod[0, :, s + 610 + k] = -np.inf
+    for k, (s, e) in enumerate(shorts[:4]):
+        tod[2, :, s + 10 + k] = np.nan
+        tod[2, :, s + 40:s + 44] = np.nan
+    ds['averaged_tod/tod'] = tod
+    return {names[0]: (ds, attrs)}, names
+
+
+def test_oracle_nonfinite_prep_runs(case_store):
+    """The oracle runs the +-inf / NaN fixture, and its running median (oracle.medfilt)
+    equals the reference's compiled filter on series holding +-inf (test_oracle_golden
+    pins that directly)."""
+    from oracle import comapdata as oc
+    store, names = _nonfinite_store(case_store)
+    case = cc.CASES['car']
+    res = oc.read_comap_data(names, store, map_info(case['map']), feeds=cc.FEEDS, **case['kw'])
+    assert np.isfinite(res[0]).all() and np.isfinite(res[1]).all() and res[0].size > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', list(cc.CASES))
+def test_gpu_prep_nonfinite_vs_oracle(case_store, name):
+    """+-inf samples stay in the 400-sample running-median input and NaN drops out of
+    the short scans' np.nanmedian, as in the reference (COMAPData.py:72-81, 357-360):
+    read_comap_data == the oracle bit for bit (Sun-centric trigonometric leaves aside)."""
+    from oracle import comapdata as oc
+    store, names = _nonfinite_store(case_store)
+    case = cc.CASES[name]
+    ref = oc.read_comap_data(names, store, map_info(case['map']), feeds=cc.FEEDS, **case['kw'])
+    got = cd.read_comap_data(names, map_info(case['map']), feeds=cc.FEEDS, store=store, **case['kw'])
     for k, a, b in zip(cc.OUTPUTS, got, ref):
         a, b = np.asarray(a), np.asarray(b)
         assert a.shape == b.shape, k

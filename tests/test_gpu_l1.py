@@ -70,6 +70,37 @@ def test_medfilt_dropin_ties_and_edges(path, monkeypatch):
         assert np.array_equal(medfilt(x.copy(), w), oracle.medfilt(x.copy(), w)), (n, w)
 
 
+def _inf_series(rng, n):
+    """Rounded normals (ties) with scattered +-inf, a run of +inf that makes window
+    medians +inf and a following run of -inf whose windows' middle pair is -inf / +inf
+    (the even-w mean is NaN, as Mediator::getMedian's (a + b) / 2 gives)."""
+    x = np.round(rng.standard_normal(n), 1)
+    x[rng.random(n) < 0.03] = np.inf
+    x[rng.random(n) < 0.03] = -np.inf
+    a = n // 3
+    x[a:a + 300] = np.inf
+    x[a + 300:a + 600] = -np.inf
+    return x
+
+
+@pytest.mark.parametrize('path', ['sort', 'devsort', 'bitmap'])
+def test_medfilt_dropin_infinities(path, monkeypatch):
+    """+-inf input (the reference's two-heap orders +-inf like any value, so every
+    window median is an order statistic): drop-in medfilt and the reflect-padded batch ==
+    oracle.medfilt, which test_oracle_golden pins to the reference's compiled filter on
+    this input."""
+    _median_path(path, monkeypatch)
+    from comapreduce_amd.tools.medfilt import medfilt, medfilt_batch
+    rng = np.random.default_rng(31)
+    for n, w in [(5000, 400), (4000, 401), (3000, 6), (9000, 6000)]:
+        x = _inf_series(rng, n)
+        assert np.array_equal(medfilt(x.copy(), w), oracle.medfilt(x.copy(), w), equal_nan=True), (n, w)
+    series = [_inf_series(rng, n) for n in (1201, 5000, 900)]
+    for s, g in zip(series, medfilt_batch(series, 400, reflect=True)):
+        z = np.concatenate((s[::-1], s, s[::-1]))
+        assert np.array_equal(g, oracle.medfilt(z, 400)[s.size:2 * s.size], equal_nan=True), s.size
+
+
 @pytest.mark.parametrize('path', ['sort', 'devsort', 'bitmap'])
 def test_medfilt_long_series_split(path, monkeypatch):
     """Series longer than one median sub-job / segment are split internally."""

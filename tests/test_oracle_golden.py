@@ -47,6 +47,27 @@ def test_medfilt_oracle_vs_reference_random():
         assert np.array_equal(oracle.medfilt(x.copy(), w), oracle.medfilt_reference(x.copy(), w))
 
 
+def test_medfilt_oracle_vs_reference_infinities():
+    """+-inf samples (scattered, a run making window medians +inf, a run whose windows'
+    middle pair is -inf / +inf): the order-statistics oracle == the reference's compiled
+    two-heap filter, NaN results included."""
+    if oracle.ref_lib() is None:
+        pytest.skip('oracle/_ref not built')
+    rng = np.random.default_rng(31)
+    for n, w in [(5000, 400), (4000, 401), (3000, 6), (9000, 6000), (2000, 1)]:
+        x = np.round(rng.standard_normal(n), 1)
+        x[rng.random(n) < 0.03] = np.inf
+        x[rng.random(n) < 0.03] = -np.inf
+        a = n // 3
+        x[a:a + 300] = np.inf
+        x[a + 300:a + 600] = -np.inf
+        want = oracle.medfilt_reference(x.copy(), w)
+        got = oracle.medfilt(x.copy(), w)
+        assert np.array_equal(got, want, equal_nan=True), (n, w)
+        if w <= 401:                               # the 300-runs dominate these windows
+            assert np.isinf(want).any() and (w % 2 or np.isnan(want).any()), (n, w)
+
+
 def test_binvalues_oracle_bit_exact(golden_dir):
     b = np.load(os.path.join(golden_dir, 'golden_binvalues.npz'))
     rng = np.random.default_rng(21)
