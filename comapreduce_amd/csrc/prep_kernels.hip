@@ -627,47 +627,69 @@ __global__ void __launch_bounds__(256) k_prep_gather(comap_prep_file f, comap_pr
 // the order-statistics kernels do not reproduce.
 __device__ __forceinline__ bool hp_keep(double v) { return v != 0.0 && !isnan(v); }
 
-__global__ void __launch_bounds__(256) k_seg_count(const double *__restrict__ x, const int64_t *__restrict__ seg,
-                                                   int64_t *__restrict__ cnt)
+// One 1024-thread workgroup per segment (a chain segment holds ~8 k samples: 16 waves
+// keep enough loads in flight; 256 threads left the pass latency-bound at ~1.2 TB/s).
+constexpr int kSegThreads = 1024;
+constexpr int kSegItems = 4;     // consecutive samples per thread per compaction round
+
+__global__ void __launch_bounds__(kSegThreads) k_seg_count(const double *__restrict__ x,
+                                                           const int64_t *__restrict__ seg,
+                                                           int64_t *__restrict__ cnt)
 {
-    __shared__ unsigned long long c_s;
+    __shared__ unsigned c_s[kSegThreads / 64];
     const double *p = x + seg[2 * blockIdx.x];
     const int64_t n = seg[2 * blockIdx.x + 1];
-    if (threadIdx.x == 0) c_s = 0;
+    unsigned c = 0;
+    int64_t i = threadIdx.x;
+    for (; i + kSegThreads < n; i += 2 * kSegThreads) {     // two independent loads per trip
+        const double a = p[i], b = p[i + kSegThreads];
+        c += hp_keep(a) + hp_keep(b);
+    }
+    if (i < n) c += hp_keep(p[i]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0) c_s[threadIdx.x >> 6] = c;
     __syncthreads();
-    unsigned long long c = 0;
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) c += hp_keep(p[i]);
-    atomicAdd(&c_s, c);
-    __syncthreads();
-    if (threadIdx.x == 0) cnt[blockIdx.x] = (int64_t)c_s;
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int v = 0; v < kSegThreads / 64; ++v) t += c_s[v];
+        cnt[blockIdx.x] = (int64_t)t;
+    }
 }
 
-// compacted values (in order) and their positions, one block per segment
-__global__ void __launch_bounds__(256) k_seg_compact(const double *__restrict__ x, const int64_t *__restrict__ seg,
-                                                     const int64_t *__restrict__ off, double *__restrict__ vals,
-                                                     int32_t *__restrict__ pos)
+// compacted values (in order) and their positions, one workgroup per segment: each round
+// takes kSegThreads x kSegItems consecutive samples (kSegItems per thread), one block scan
+__global__ void __launch_bounds__(kSegThreads) k_seg_compact(const double *__restrict__ x,
+                                                             const int64_t *__restrict__ seg,
+                                                             const int64_t *__restrict__ off,
+                                                             double *__restrict__ vals, int32_t *__restrict__ pos)
 {
-    typedef hipcub::BlockScan<int, 256> Scan;
+    typedef hipcub::BlockScan<int, kSegThreads> Scan;
     __shared__ typename Scan::TempStorage ts;
-    __shared__ int64_t run;
     const double *p = x + seg[2 * blockIdx.x];
     const int64_t n = seg[2 * blockIdx.x + 1];
-    const int64_t o0 = off[blockIdx.x];
-    if (threadIdx.x == 0) run = 0;
-    __syncthreads();
-    for (int64_t b = 0; b < n; b += 256) {
-        const int64_t i = b + threadIdx.x;
-        const double v = i < n ? p[i] : 0.0;
-        const int k = i < n && hp_keep(v);
-        int ex = 0, tot = 0;
-        Scan(ts).ExclusiveSum(k, ex, tot);
-        if (k) {
-            vals[o0 + run + ex] = v;
-            pos[o0 + run + ex] = (int32_t)i;
+    double *vo = vals + off[blockIdx.x];
+    int32_t *po = pos + off[blockIdx.x];
+    int64_t run = 0;
+    for (int64_t b = 0; b < n; b += (int64_t)kSegThreads * kSegItems) {
+        const int64_t i0 = b + (int64_t)threadIdx.x * kSegItems;
+        double v[kSegItems];
+        int k[kSegItems], ex[kSegItems];
+#pragma unroll
+        for (int j = 0; j < kSegItems; ++j) {
+            v[j] = i0 + j < n ? p[i0 + j] : 0.0;
+            k[j] = i0 + j < n && hp_keep(v[j]);
         }
-        __syncthreads();
-        if (threadIdx.x == 0) run += tot;
-        __syncthreads();
+        int tot = 0;
+        Scan(ts).ExclusiveSum(k, ex, tot);
+#pragma unroll
+        for (int j = 0; j < kSegItems; ++j)
+            if (k[j]) {
+                vo[run + ex[j]] = v[j];
+                po[run + ex[j]] = (int32_t)(i0 + j);
+            }
+        run += tot;
+        __syncthreads();     // the scan's temporary storage is reused next round
     }
 }
 
@@ -699,13 +721,18 @@ __global__ void __launch_bounds__(256) k_seg_small_median(const double *__restri
     for (int i = threadIdx.x; i < n; i += blockDim.x) filt[o0 + i] = med;
 }
 
-__global__ void k_seg_subtract(double *__restrict__ x, const int64_t *__restrict__ seg, const int64_t *__restrict__ off,
-                               const int64_t *__restrict__ cnt, const double *__restrict__ filt,
-                               const int32_t *__restrict__ pos)
+// grid (segment, 256-value chunk): every compacted value back to its sample
+__global__ void __launch_bounds__(256) k_seg_subtract(double *__restrict__ x, const int64_t *__restrict__ seg,
+                                                      const int64_t *__restrict__ off,
+                                                      const int64_t *__restrict__ cnt,
+                                                      const double *__restrict__ filt,
+                                                      const int32_t *__restrict__ pos)
 {
+    const int64_t n = cnt[blockIdx.x];
     double *p = x + seg[2 * blockIdx.x];
-    const int64_t o0 = off[blockIdx.x], n = cnt[blockIdx.x];
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) p[pos[o0 + i]] -= filt[o0 + i];
+    const int64_t o0 = off[blockIdx.x];
+    for (int64_t i = (int64_t)blockIdx.y * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.y * 256)
+        p[pos[o0 + i]] -= filt[o0 + i];
 }
 
 // ---------------------------------------------------------------- NaN and empty-offset cuts
@@ -864,13 +891,17 @@ extern "C" int comap_prep_highpass(comap_ctx *ctx, double *x, const int64_t *seg
     int64_t *cnt = nullptr, *off = nullptr;
     COMAP_CHECK(ctx, tmp.alloc(&cnt, (size_t)nseg));
     COMAP_CHECK(ctx, tmp.alloc(&off, (size_t)nseg));
-    k_seg_count<<<nseg, 256, 0, st>>>(x, seg_dev, cnt);
+    k_seg_count<<<nseg, kSegThreads, 0, st>>>(x, seg_dev, cnt);
     COMAP_LAUNCH_CHECK(ctx);
     std::vector<int64_t> c(nseg), o(nseg);
     COMAP_CHECK(ctx, hipMemcpyAsync(c.data(), cnt, 8 * (size_t)nseg, hipMemcpyDeviceToHost, st));
     COMAP_CHECK(ctx, hipStreamSynchronize(st));
-    int64_t total = 0;
-    for (int k = 0; k < nseg; ++k) { o[k] = total; total += c[k]; }
+    int64_t total = 0, cmax = 0;
+    for (int k = 0; k < nseg; ++k) {
+        o[k] = total;
+        total += c[k];
+        cmax = std::max(cmax, c[k]);
+    }
     if (total == 0) return 0;
     double *vals = nullptr, *filt = nullptr;
     int32_t *pos = nullptr;
@@ -878,7 +909,7 @@ extern "C" int comap_prep_highpass(comap_ctx *ctx, double *x, const int64_t *seg
     COMAP_CHECK(ctx, tmp.alloc(&filt, (size_t)total));
     COMAP_CHECK(ctx, tmp.alloc(&pos, (size_t)total));
     COMAP_CHECK(ctx, comap_upload(off, o.data(), 8 * (size_t)nseg, st));
-    k_seg_compact<<<nseg, 256, 0, st>>>(x, seg_dev, off, vals, pos);
+    k_seg_compact<<<nseg, kSegThreads, 0, st>>>(x, seg_dev, off, vals, pos);
     COMAP_LAUNCH_CHECK(ctx);
     std::vector<MedJob> jobs;
     std::vector<int> small;      // short segments the device kernel cannot hold (2w > kSmallSeg)
@@ -945,7 +976,8 @@ extern "C" int comap_prep_highpass(comap_ctx *ctx, double *x, const int64_t *seg
         std::vector<double> f(n, med);
         COMAP_CHECK(ctx, comap_upload(filt + o[k], f.data(), 8 * n, st));
     }
-    k_seg_subtract<<<nseg, 256, 0, st>>>(x, seg_dev, off, cnt, filt, pos);
+    const unsigned chunks = (unsigned)std::min<int64_t>((cmax + 255) / 256, 4096);
+    k_seg_subtract<<<dim3((unsigned)nseg, chunks), 256, 0, st>>>(x, seg_dev, off, cnt, filt, pos);
     COMAP_LAUNCH_CHECK(ctx);
     return 0;
 }
