@@ -572,14 +572,20 @@ def chain_leg(data, device, l1_bytes, reps=3):
     Timed as one host wall clock per chain, no synchronisation between the phases: the
     pointing-only part of the prep (az / el percentiles, prep.precompute_pointing) is
     enqueued on a side stream as soon as the reduction's last stage has been queued, so
-    it runs beside the reduction's tail.  The median of ``reps`` chains; one extra chain
-    with a device sync at every phase boundary gives the phase breakdown.  Roofline: the
+    it runs beside the reduction's tail.  The median of ``reps`` chains; 5 extra chains
+    with a device sync at every phase boundary give the phase breakdown (per-phase median).  Roofline: the
     L1 passes' design bytes + the operator bytes of every CG iteration, over the wall."""
     import torch
     chain = chain_fn(data, device)
     chain(False)                                   # warm the prep / set-up paths
-    phases = chain(True)
-    phases.pop('maps')
+    # per-phase median of 5 synced chains: one synced chain's prep phase moved 2.4 - 5.7 ms
+    # with the host's scheduling (r05ab3)
+    synced = []
+    for _ in range(5):
+        ph = chain(True)
+        ph.pop('maps')
+        synced.append(ph)
+    phases = {k: (float(np.median([p[k] for p in synced])) if k.endswith('_ms') else v) for k, v in synced[-1].items()}
     walls = []
     for _ in range(reps):
         torch.cuda.synchronize()
@@ -598,7 +604,7 @@ def chain_leg(data, device, l1_bytes, reps=3):
                       '(max 100 it), L=50, 480x480 CAR -> 4 bands of maps on the host',
             'reps': reps, 'wall_ms': wall, 'wall_ms_all': walls, 'iters': info['iters'],
             'phases_synced_ms': {k: v for k, v in phases.items() if k.endswith('_ms')},
-            'phases_note': 'one extra chain with a device sync at every phase boundary (no overlap)',
+            'phases_note': 'per-phase median of 5 extra chains with a device sync at every phase boundary (no overlap)',
             'algo_bytes': algo, 'achieved_GBs': algo / (wall * 1e-3) / 1e9,
             'roofline_frac': algo / (wall * 1e-3) / 1e9 / HBM_PEAK_GBS,
             'roofline_note': 'algorithmic bytes = the 3 L1 streaming passes (design bytes) + the batched operator '
