@@ -385,8 +385,10 @@ int comap_prep_percentiles(comap_ctx *ctx, const double *az_dev, const double *e
  * before the high-pass; `wcs` may be NULL when f->pixels is given. */
 int comap_prep_gather(comap_ctx *ctx, const comap_prep_file *f, const comap_prep_wcs *wcs,
                       const comap_prep_out *out);
-/* x[seg] -= median_filter(x[seg][keep], w) on keep = non-zero finite samples of each
- * segment seg_dev[k] = {element offset, length} (COMAPData.py:72-81, 353-360).
+/* x[seg] -= median_filter(x[seg][keep], w) on keep = non-zero, non-NaN samples of each
+ * segment seg_dev[k] = {element offset, length} (COMAPData.py:72-81, 353-360): +-inf
+ * stays in the median input as in the reference; NaN samples are left out and stay NaN
+ * (exact for segments of <= 2w values, where the reference takes np.nanmedian).
  * Synchronises (segment lengths size the median plan). */
 int comap_prep_highpass(comap_ctx *ctx, double *x_dev, const int64_t *seg_dev, int32_t nseg, int32_t w);
 /* NaN -> 0, keep[b][o] = any weight of offset o in band b non-zero, the union of kept
