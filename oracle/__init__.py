@@ -69,6 +69,8 @@ def medfilt(x, w):
     """In-place semantics of medfilt.medfilt (medfilt.pyx:26-33); returns the array."""
     x = np.ascontiguousarray(x, dtype=np.float64)
     rc = lib().oracle_medfilt(_dptr(x), x.size, int(w))
+    if rc == -3:
+        raise ValueError('oracle_medfilt: NaN input (the two-heap order for NaN is not restated)')
     if rc != 0:
         raise ValueError(f'oracle_medfilt failed rc={rc} (n={x.size}, w={w})')
     return x

@@ -45,6 +45,10 @@ static double xprime(const double *x, int64_t n, int64_t h, int64_t j)
 int oracle_medfilt(double *x, int64_t n, int32_t w)
 {
     if (w < 1 || n < 1 || n < w) return -1;
+    /* the sorted window needs a total order: NaN is outside this restatement (the
+       reference's two-heap result for it depends on its history) -- refuse it */
+    for (int64_t i = 0; i < n; ++i)
+        if (x[i] != x[i]) return -3;
     const int64_t h = w / 2;
     double *orig = (double *)malloc(sizeof(double) * (size_t)n);
     double *s = (double *)malloc(sizeof(double) * (size_t)w);

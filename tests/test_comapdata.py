@@ -310,7 +310,8 @@ def test_nan_samples_do_not_abort_prep(case_store):
     tod 0 and weight 0 as in the reference (COMAPData.py:550-552).  The other samples of
     its series are filtered against the running median of the non-NaN ones (parity
     unpinned for such a series: the reference's two-heap result then depends on its
-    insertion history)."""
+    insertion history) -- checked bit for bit against the oracle's prep
+    with NaN taken out of the median input, the documented semantics."""
     store, names = case_store
     ds, attrs = store[names[1]]
     ds = dict(ds)
@@ -328,6 +329,28 @@ def test_nan_samples_do_not_abort_prep(case_store):
     moved = t != clean[0]
     assert t.size == clean[0].size and moved.any()
     assert np.unique(np.asarray(res[8])[moved]).size == 1                # only that feed's samples moved
+    # the documented semantics, bit for bit: the oracle's prep with NaN taken out of the
+    # median input (NaN samples stay NaN until the cut zeroes them)
+    from oracle import comapdata as oc
+
+    def median_filter_without_nan(tod, w, _orig=oc.median_filter):
+        keep = ~np.isnan(tod)
+        out = np.full(tod.size, np.nan)
+        if keep.any():
+            out[keep] = _orig(tod[keep], w)
+        return out
+    mp = pytest.MonkeyPatch()
+    mp.setattr(oc, 'median_filter', median_filter_without_nan)
+    try:
+        ref = oc.read_comap_data([names[1]], st, map_info(case['map']), feeds=cc.FEEDS, **case['kw'])
+    finally:
+        mp.undo()
+    for k, a, b in zip(cc.OUTPUTS, res, ref):
+        a, b = np.asarray(a), np.asarray(b)
+        if k in TRIG:
+            assert np.max(np.abs(a - b)) <= 1e-12 * max(np.max(np.abs(b)), 1.0), k
+        else:
+            assert np.array_equal(a, b), k
 
 
 def _many_scans_store(case_store, dense=False):

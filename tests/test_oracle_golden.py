@@ -68,6 +68,15 @@ def test_medfilt_oracle_vs_reference_infinities():
             assert np.isinf(want).any() and (w % 2 or np.isnan(want).any()), (n, w)
 
 
+def test_medfilt_oracle_refuses_nan():
+    """The order-statistics restatement has no NaN semantics (the reference's two-heap
+    result then depends on its history): it raises instead of reading past its window."""
+    x = np.arange(50.0)
+    x[20] = np.nan
+    with pytest.raises(ValueError, match='NaN'):
+        oracle.medfilt(x, 5)
+
+
 def test_binvalues_oracle_bit_exact(golden_dir):
     b = np.load(os.path.join(golden_dir, 'golden_binvalues.npz'))
     rng = np.random.default_rng(21)
