@@ -551,10 +551,11 @@ extern "C" int comap_medfilt_f64(comap_ctx *ctx, double *x, int64_t n, int32_t w
 {
     if (!ctx || !x) return -1;
     COMAP_DEVICE_GUARD(ctx);
-    if (w < 1 || n < w) return comap_fail(ctx, -1, "medfilt requires 1 <= w <= n");
-    for (int64_t i = 0; i < n; ++i)
-        if (std::isnan(x[i])) return comap_fail(ctx, -3, "medfilt input contains NaN");
+    // medianFilter.cpp:4-30 stays inside the array for n >= ceil(w/2)
+    if (w < 1 || n < (int64_t)(w / 2 + w % 2)) return comap_fail(ctx, -1, "medfilt requires 1 <= w and ceil(w/2) <= n");
     if (n + w >= (1ll << 31)) return comap_fail(ctx, -1, "medfilt series too long");
+    bool nan = false;
+    for (int64_t i = 0; i < n && !nan; ++i) nan = std::isnan(x[i]);
     char *s = nullptr;
     int rc = comap_scratch(ctx, 16 * (size_t)n + 64, (void **)&s);
     if (rc) return rc;
@@ -566,8 +567,14 @@ extern "C" int comap_medfilt_f64(comap_ctx *ctx, double *x, int64_t n, int32_t w
     hipStream_t st = ctx->stream;
     COMAP_CHECK(ctx, hipMemcpyAsync(dsrc, x, 8 * n, hipMemcpyHostToDevice, st));
     MedPlan mp;
-    rc = comap_median_plan(ctx, &mp, std::vector<MedJob>{job}, w);
-    if (!rc) rc = comap_median_run(ctx, &mp);
+    // NaN (history-dependent two-heap order) or a series shorter than the window: the exact
+    // two-heap replay; otherwise the order-statistics plan
+    const bool replay = nan || n < w || w > 32768;
+    if (replay) rc = comap_median_replay(ctx, std::vector<MedJob>{job}, w, st);
+    else {
+        rc = comap_median_plan(ctx, &mp, std::vector<MedJob>{job}, w);
+        if (!rc) rc = comap_median_run(ctx, &mp);
+    }
     if (!rc) {
         hipError_t e = hipMemcpyAsync(x, ddst, 8 * n, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
@@ -580,32 +587,32 @@ extern "C" int comap_medfilt_f64(comap_ctx *ctx, double *x, int64_t n, int32_t w
 // ------------------------------------------------------------------ batched median
 // Series s = x[offsets[s] .. offsets[s+1]).  mode 0: medfilt semantics, all
 // outputs; mode 1: the middle third of medfilt on [x[::-1], x, x[::-1]]
-// (Level1Averaging.py:696-700, COMAPData.py:72-81), computed without the pad.
+// (Level1Averaging.py:696-700, COMAPData.py:72-81), computed without the pad.  Series
+// holding NaN, or shorter than the window, take the exact two-heap replay.
 extern "C" int comap_medfilt_batch_f64(comap_ctx *ctx, const double *x, const int64_t *offsets, int32_t nseries,
                                        int32_t w, int32_t mode, double *out)
 {
     if (!ctx || !x || !offsets || !out || nseries < 0 || (mode != 0 && mode != 1)) return -1;
     COMAP_DEVICE_GUARD(ctx);
     if (nseries == 0) return 0;
+    if (w < 1) return comap_fail(ctx, -1, "medfilt requires w >= 1");
     const int64_t total = offsets[nseries];
+    const int64_t need = w / 2 + w % 2;     // medianFilter.cpp stays inside the array from ceil(w/2) values
     for (int s = 0; s < nseries; ++s) {
         const int64_t n = offsets[s + 1] - offsets[s];
         if (n < 0) return comap_fail(ctx, -1, "offsets must be non-decreasing");
-        // mode 1 equals medfilt on the padded array only when no output window
-        // reaches the pad's head/tail replacement: n >= w
-        if (n > 0 && n < w) return comap_fail(ctx, -1, "series shorter than the window");
+        if (n > 0 && (mode == 0 ? n : 3 * n) < need) return comap_fail(ctx, -1, "series shorter than ceil(w/2)");
     }
-    for (int64_t i = 0; i < total; ++i)
-        if (std::isnan(x[i])) return comap_fail(ctx, -3, "medfilt input contains NaN");
     char *s = nullptr;
     int rc = comap_scratch(ctx, 16 * (size_t)total + 64, (void **)&s);
     if (rc) return rc;
     double *dsrc = (double *)s;
     double *ddst = dsrc + total;
-    std::vector<MedJob> jobs(nseries);
+    std::vector<MedJob> jobs, replay;
     for (int k = 0; k < nseries; ++k) {
         const int64_t n = offsets[k + 1] - offsets[k];
-        MedJob &j = jobs[k];
+        if (n == 0) continue;
+        MedJob j;
         j.src = dsrc + offsets[k];
         j.dst = ddst + offsets[k];
         j.n = n;
@@ -614,12 +621,20 @@ extern "C" int comap_medfilt_batch_f64(comap_ctx *ctx, const double *x, const in
         j.gate = nullptr;
         j.out_lo = mode == 0 ? 0 : n;
         j.out_hi = mode == 0 ? n : 2 * n;
+        bool nan = false;
+        for (int64_t i = offsets[k]; i < offsets[k + 1] && !nan; ++i) nan = std::isnan(x[i]);
+        // mode 1 equals medfilt on the padded array on the order-statistics path only when
+        // no output window reaches the pad's head / tail replacement: n >= w
+        (nan || n < w || w > 32768 ? replay : jobs).push_back(j);
     }
     hipStream_t st = ctx->stream;
     COMAP_CHECK(ctx, hipMemcpyAsync(dsrc, x, 8 * total, hipMemcpyHostToDevice, st));
     MedPlan mp;
-    rc = comap_median_plan(ctx, &mp, jobs, w);
-    if (!rc) rc = comap_median_run(ctx, &mp);
+    if (!jobs.empty()) {
+        rc = comap_median_plan(ctx, &mp, jobs, w);
+        if (!rc) rc = comap_median_run(ctx, &mp);
+    }
+    if (!rc) rc = comap_median_replay(ctx, replay, w, st);
     if (!rc) {
         hipError_t e = hipMemcpyAsync(out, ddst, 8 * total, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);

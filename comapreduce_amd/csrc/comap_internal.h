@@ -185,6 +185,12 @@ int comap_median_plan(comap_ctx *ctx, MedPlan *mp, const std::vector<MedJob> &jo
 void comap_median_plan_free(MedPlan *mp);
 int comap_median_run(comap_ctx *ctx, MedPlan *mp, hipStream_t stream);
 inline int comap_median_run(comap_ctx *ctx, MedPlan *mp) { return comap_median_run(ctx, mp, ctx->stream); }
+// Exact replay of the reference's two-heap filter (Mediator.h / medianFilter.cpp) for the
+// series the order-statistics plan does not serve: NaN-bearing series (the two-heap's NaN
+// result follows its insertion history) and ceil(w/2) <= length < w.  One workgroup per
+// job; job.mode 0 = medfilt on src[0..n), 1 = medfilt on [src[::-1], src, src[::-1]]
+// (3n values); outputs [out_lo, out_hi) of the filtered array go to dst.  Enqueued on st.
+int comap_median_replay(comap_ctx *ctx, const std::vector<MedJob> &jobs, int32_t w, hipStream_t st);
 
 // ------------------------------------------------------------------ L1 plan
 struct comap_l1_plan {
@@ -267,6 +273,11 @@ struct comap_l1_plan {
     double *fitsum = nullptr;          // [2][U*4096] masked Sd, SAd (select_time path)
     double *oa = nullptr;              // [U*4096][2] offset/slope L1AGC subtracts
     int32_t *flag = nullptr;           // [1] phase-1 kappa mismatch -> legacy passes C, D run
+    // non-finite filtered rows (k_unit_flags, k_special_rows): ynf[u] = the gain fit's input
+    // holds a non-finite value (dG = 0); ugate[u] = a band-0 row's filtered values hold
+    // +-inf (fit_power_spectrum raises: dG None, no in-place zeroing)
+    int32_t *ynf = nullptr;            // [U]
+    int32_t *ugate = nullptr;          // [U]
     // channel list per (unit, band) for passes B and C: the median channels with alpha != 0,
     // ascending (k_coef_d phase 0)
     int32_t *dlist = nullptr;          // [U*4][1024]

@@ -864,6 +864,97 @@ __global__ void __launch_bounds__(1024) k_gain_weights(const double *__restrict_
     if (threadIdx.x == 0) gmode[f] = mode;
 }
 
+// ------------------------------------------------------------------ non-finite filtered rows
+// After fill_bad_data only +-inf samples and rows whose normalisation failed (alpha = 0:
+// rms NaN / 0, or a NaN atmosphere fit) make the filtered TOD y non-finite.  The reference
+// then behaves as follows (Level1Averaging.py:681-708, 552-589, 834-867;
+// GainSubtraction.py:127-128, 154-158):
+//  * alpha = 0: the row is NaN throughout;
+//  * a row with +-inf samples and a finite rms ("special"): A^T y of the median-filter
+//    regression is non-finite, np.linalg.solve (LU with partial pivoting) returns non-finite
+//    x, and y_t = m_t - (x0 + mf_t x1) is +-inf or NaN at EVERY sample;
+//  * any non-finite y on the gain fit's channels makes b = P^T Z d non-finite: cg's first
+//    matvec raises and solve_gain_solution returns dG = 0;
+//  * +-inf anywhere in a band-0 row (the channel nanmean of fit_power_spectrum holds it)
+//    makes the PSD bins NaN: IndexError, dG = None and the gain function's in-place
+//    zeroing of y never happens;
+//  * weighted_average_over_band zeroes a channel's weight when its residual at the scan's
+//    first sample is NaN and turns NaN entries into 0 -- +-inf entries stay (and 0 * inf is
+//    NaN for a zero weight).
+// Special rows are therefore excluded from the fused channel sums and added per sample by
+// k_special_rows, which evaluates them exactly as the reference does.
+
+// ynf[u]: a gain-fit input row (band the median filter ran on, median channel, not zeroed
+// by gain_subtraction_fit's mask or a NaN Tsys) is non-finite.  One block per unit.
+__global__ void __launch_bounds__(256) k_unit_flags(const int32_t *__restrict__ units,
+                                                    const double *__restrict__ alpha,
+                                                    const int32_t *__restrict__ rowbad,
+                                                    const double *__restrict__ bsum,
+                                                    const double *__restrict__ tsys0, int32_t *__restrict__ ynf)
+{
+    __shared__ double red[4];
+    const int u = blockIdx.x;
+    const int f = units[4 * u];
+    double any = 0.0;
+    for (int k = threadIdx.x; k < kBC; k += blockDim.x) {
+        const int b = k / kChannels, c = k % kChannels;
+        if (bsum[4 * ((int64_t)u * kBands + b) + 3] <= 0 || !median_channel(c) || gain_masked(c)) continue;
+        if (isnan(tsys0[(int64_t)f * kBC + k])) continue;
+        const int64_t i = (int64_t)u * kBC + k;
+        if (alpha[i] == 0.0 || rowbad[i] > 0) any = 1.0;
+    }
+    any = block_sum256(any, red);
+    if (threadIdx.x == 0) ynf[u] = any > 0.0;
+}
+
+// The regression solve of Level1Averaging.py:704 for a non-finite right-hand side
+// (sy = sum y, sym = sum mf y): np.linalg.solve's LU with partial pivoting on
+// [[n, Smf], [Smf, Smm]], whose +-inf / NaN outcome differs from Cramer's rule when the
+// pivot row swaps (|Smf| > n).
+__device__ __forceinline__ void solve2_lu(double n, double Smf, double Smm, double sy, double sym, double &x0,
+                                          double &x1)
+{
+    if (fabs(Smf) > fabs(n)) {            // idamax picks row 1
+        const double l = n / Smf, u11 = Smf - l * Smm;
+        const double y1 = sy - l * sym;
+        x1 = y1 / u11;
+        x0 = (sym - Smm * x1) / Smf;
+    } else {
+        const double l = Smf / n, u11 = Smm - l * Smf;
+        const double y1 = sym - l * sy;
+        x1 = y1 / u11;
+        x0 = (sy - Smf * x1) / n;
+    }
+}
+
+// A special row: band the median ran on, median channel, finite alpha, +-inf samples
+__device__ __forceinline__ bool special_row(bool band_on, int c, double al, int32_t rb)
+{
+    return band_on && median_channel(c) && al != 0.0 && rb > 0;
+}
+
+// y_t of a special row (the reference's order: m_t - (x0 + mf_t x1))
+__device__ __forceinline__ double special_y(double al, double o, double a, double x0, double x1, float d, double At,
+                                            double mft)
+{
+    const double m = ((double)d - (o + a * At)) * al;
+    return m - (x0 + mft * x1);
+}
+
+// weighted_average_over_band's weights for a special row: W (residual; zero when the
+// residual at the scan's first sample is NaN) and Wo (tod_original; also zero when
+// (y * Tsys) there is NaN)
+__device__ __forceinline__ void special_weights(int c, double tsv, double nf, double g, double y0, double &W,
+                                                double &Wo)
+{
+    W = 1.0 / (tsv * tsv);
+    if (tsv == 0.0) W = 0.0;
+    if (c < 50 || c >= 974 || c == 512 || (c >= 510 && c < 515)) W = 0.0;
+    if (isnan(y0 * nf / g)) W = 0.0;
+    Wo = W;
+    if (isnan(tsv) || isnan(y0 * tsv)) Wo = 0.0;
+}
+
 // ------------------------------------------------------------------ L1AGC coefficients II
 // Regression solve + the filtered-TOD coefficients f_ct = fa d + fb + fg A_t + fd mf_t
 // and the three channel weightings pass D sums:
@@ -883,7 +974,11 @@ __global__ void __launch_bounds__(256) k_coef_d(const int32_t *__restrict__ unit
                                                 double *__restrict__ kap, double *__restrict__ dsum,
                                                 double *__restrict__ xreg, int phase,
                                                 int32_t *__restrict__ flag, int32_t *__restrict__ dlist,
-                                                int32_t *__restrict__ dcnt, double *__restrict__ dw)
+                                                int32_t *__restrict__ dcnt, double *__restrict__ dw,
+                                                const int32_t *__restrict__ rowbad, const float *__restrict__ tod,
+                                                int64_t T, const double *__restrict__ A,
+                                                const double *__restrict__ mf, const int32_t *__restrict__ ynf,
+                                                const int32_t *__restrict__ ugate)
 {
     __shared__ double red[4];
     __shared__ double s_kap[4][kChannels];     // alpha, kg, kr, ko (phase 0 channel list)
@@ -904,12 +999,13 @@ __global__ void __launch_bounds__(256) k_coef_d(const int32_t *__restrict__ unit
     // channel mean: np.fft of n <= 4 samples leaves no finite PSD bin (ValueError /
     // IndexError), so dG = None and the gain function (and its in-place zeroing) never
     // runs.  For n >= 5 and finite samples the gate passes (every band-0 channel outside
-    // the median set is 0, so the channel nanmean is finite); +-inf samples are outside
-    // parity.
-    const bool gate = n >= 5.0;
+    // the median set is 0, so the channel nanmean is finite).  A band-0 row holding +-inf
+    // after the filter fails the gate too (ugate, k_special_rows); a non-finite gain-fit
+    // input leaves dG = 0 (ynf, k_unit_flags) -- see "non-finite filtered rows" above.
+    const bool gate = n >= 5.0 && !(ugate && ugate[u]);
     const bool gain_called = !calibrator && gate;
     const bool zero = gain_called;
-    const bool use_dg = gain_called && gm == 0;
+    const bool use_dg = gain_called && gm == 0 && !ynf[u];
     const double det = n * Smm - Smf * Smf;
     double acc[12];
 #pragma unroll
@@ -919,6 +1015,9 @@ __global__ void __launch_bounds__(256) k_coef_d(const int32_t *__restrict__ unit
         const double o = oa[2 * i], a = oa[2 * i + 1];
         const double al = alpha[i];
         const double tsv = tsys0[(int64_t)f * kBC + b * kChannels + c];
+        const bool zeroed = zero && (gain_masked(c) || isnan(tsv));     // y row set to 0 in place
+        // a special row (+-inf samples, finite rms) not zeroed: k_special_rows adds it
+        const bool special = special_row(band_on, c, al, rowbad[i]) && !zeroed;
         // ---- filtered TOD coefficients
         double fa = 0, fb = 0, fg = 0, fd = 0, x0 = 0, x1 = 0;
         if (band_on && median_channel(c)) {
@@ -927,8 +1026,12 @@ __global__ void __launch_bounds__(256) k_coef_d(const int32_t *__restrict__ unit
                 const double sy = al * (mom[i] - n * o - a * SA);
                 const double sym = al * (sdmi - o * Smf - a * SAm);
                 if (phase != 0) {    // phase 0: x unknown yet; kappa never depends on x unless x is NaN
-                    x0 = (Smm * sy - Smf * sym) / det;
-                    x1 = (n * sym - Smf * sy) / det;
+                    if (isfinite(sy) && isfinite(sym)) {
+                        x0 = (Smm * sy - Smf * sym) / det;
+                        x1 = (n * sym - Smf * sy) / det;
+                    } else {
+                        solve2_lu(n, Smf, Smm, sy, sym, x0, x1);
+                    }
                 }
                 fa = al; fb = -(al * o + x0); fg = -al * a; fd = -x1;
             } else {                      // NaN channel inside the regression set
@@ -937,25 +1040,36 @@ __global__ void __launch_bounds__(256) k_coef_d(const int32_t *__restrict__ unit
         }
         xreg[2 * i] = x0;
         xreg[2 * i + 1] = x1;
-        if (zero && (gain_masked(c) || isnan(tsv))) { fa = fb = fg = fd = 0.0; }
+        if (zeroed) { fa = fb = fg = fd = 0.0; }
         const bool fnan = isnan(fa) || isnan(fb) || isnan(fg) || isnan(fd);
         // ---- gain template weight
-        const double kg = use_dg ? gw[(int64_t)f * kBC + b * kChannels + c] : 0.0;
+        const double kg = (use_dg && !special) ? gw[(int64_t)f * kBC + b * kChannels + c] : 0.0;
         // ---- band-average weights (Level1Averaging.py:841-845, 593-596)
         double W = 1.0 / (tsv * tsv);
         if (tsv == 0.0) W = 0.0;
         if (c < 50 || c >= 974 || c == 512 || (c >= 510 && c < 515)) W = 0.0;
         const double nfg = nf[i] / gain0[(int64_t)f * kBC + b * kChannels + c];
         if (isnan(nfg) || fnan) W = 0.0;                       // residual[...,0] NaN
-        const double kr = (W == 0.0) ? 0.0 : W * nfg;          // never 0 * NaN
+        double kr = (W == 0.0) ? 0.0 : W * nfg;                // never 0 * NaN
         double Wo = W;
         if (isnan(tsv) || fnan) Wo = 0.0;                      // (clean*Tsys)[...,0] NaN
-        const double ko = (Wo == 0.0) ? 0.0 : Wo * tsv;
+        double ko = (Wo == 0.0) ? 0.0 : Wo * tsv;
+        if (special) {          // out of the fused sums; its weights from y at the scan's first sample
+            kr = ko = 0.0;
+            W = Wo = 0.0;
+            if (phase != 0) {
+                const int t0 = units[4 * u + 2];
+                const float d0 = tod[((int64_t)f * kBC + b * kChannels + c) * T + t0];
+                const double y0 = special_y(al, o, a, x0, x1, d0, A[(int64_t)f * T + t0],
+                                            mf[((int64_t)f * kBands + b) * T + t0]);
+                special_weights(c, tsv, nf[i], gain0[(int64_t)f * kBC + b * kChannels + c], y0, W, Wo);
+            }
+        }
         // ---- kappa (zero weights contribute exactly nothing, as NaN->0 does)
         const double kgfa = (kg == 0.0) ? 0.0 : kg * fa;
         const double krfa = (kr == 0.0) ? 0.0 : kr * fa;
         const double kofa = (ko == 0.0) ? 0.0 : ko * fa;
-        if (phase == 1) {        // kappa with the regression known must equal the phase-0 kappa
+        if (phase >= 1) {        // kappa with the regression (and the gate) known must equal the earlier kappa
             if (__double_as_longlong(kap[i]) != __double_as_longlong(kgfa) ||
                 __double_as_longlong(kap[UC + i]) != __double_as_longlong(krfa) ||
                 __double_as_longlong(kap[2 * UC + i]) != __double_as_longlong(kofa))
@@ -998,6 +1112,94 @@ __global__ void __launch_bounds__(256) k_coef_d(const int32_t *__restrict__ unit
             },
             dlist + (int64_t)ub * kChannels);
         if (threadIdx.x == 0) dcnt[ub] = nc;
+    }
+}
+
+// ------------------------------------------------------------------ special rows
+// One block per (unit, band).  mode 0 (after k_coef_d phase 1, before phase 2): ugate[u] =
+// a band-0 special row's y holds +-inf somewhere (fit_power_spectrum's channel nanmean is
+// then non-finite; evaluated before the gain function's zeroing).  mode 1 (after the
+// outputs are formed): every special row that was not zeroed adds its residual and
+// tod_original terms per sample exactly as weighted_average_over_band forms them
+// (Level1Averaging.py:592-599): NaN entries -> 0, +-inf entries kept, times the row's
+// weight (0 * inf = NaN), divided by the band's weight sum.  Launched only when pass A
+// found non-finite samples after the NaN fill.
+__global__ void __launch_bounds__(256) k_special_rows(int mode, const int32_t *__restrict__ units,
+                                                      const float *__restrict__ tod, int64_t T,
+                                                      const double *__restrict__ A, const double *__restrict__ mf,
+                                                      const double *__restrict__ oa, const double *__restrict__ alpha,
+                                                      const double *__restrict__ nf, const int32_t *__restrict__ rowbad,
+                                                      const double *__restrict__ bsum, const double *__restrict__ xreg,
+                                                      const double *__restrict__ tsys0, const double *__restrict__ gain0,
+                                                      const double *__restrict__ dsum, int calibrator,
+                                                      int32_t *__restrict__ ugate, double *__restrict__ tod_out,
+                                                      double *__restrict__ orig_out)
+{
+    __shared__ int nrow;
+    __shared__ int16_t rows[kChannels];
+    __shared__ double rw[kChannels], rwo[kChannels];
+    const int ub = blockIdx.x;
+    const int u = ub / kBands, b = ub % kBands;
+    if (mode == 0 && b != 0) return;
+    const int f = units[4 * u], t0 = units[4 * u + 2], n = units[4 * u + 3];
+    const bool band_on = bsum[4 * (int64_t)ub + 3] > 0;
+    if (!band_on) return;
+    const bool zero = mode == 1 && !calibrator && n >= 5 && !ugate[u];
+    if (threadIdx.x == 0) nrow = 0;
+    __syncthreads();
+    const int64_t kb = (int64_t)u * kBC + b * kChannels, fb = (int64_t)f * kBC + b * kChannels;
+    for (int c = threadIdx.x; c < kChannels; c += blockDim.x) {
+        const int64_t i = kb + c;
+        if (!special_row(band_on, c, alpha[i], rowbad[i])) continue;
+        const double tsv = tsys0[fb + c];
+        if (zero && (gain_masked(c) || isnan(tsv))) continue;       // y zeroed in place
+        const float d0 = tod[(fb + c) * T + t0];
+        const double y0 = special_y(alpha[i], oa[2 * i], oa[2 * i + 1], xreg[2 * i], xreg[2 * i + 1], d0,
+                                    A[(int64_t)f * T + t0], mf[((int64_t)f * kBands + b) * T + t0]);
+        double W, Wo;
+        special_weights(c, tsv, nf[i], gain0[fb + c], y0, W, Wo);
+        const int k = atomicAdd(&nrow, 1);
+        rows[k] = (int16_t)c;
+        rw[k] = W;
+        rwo[k] = Wo;
+    }
+    __syncthreads();
+    const int nr = nrow;
+    if (nr == 0) return;
+    const double *a = A + (int64_t)f * T + t0;
+    const double *m = mf + ((int64_t)f * kBands + b) * T + t0;
+    if (mode == 0) {
+        bool inf = false;
+        for (int t = threadIdx.x; t < n; t += blockDim.x)
+            for (int k = 0; k < nr; ++k) {
+                const int64_t i = kb + rows[k];
+                const double y = special_y(alpha[i], oa[2 * i], oa[2 * i + 1], xreg[2 * i], xreg[2 * i + 1],
+                                           tod[(fb + rows[k]) * T + t0 + t], a[t], m[t]);
+                inf |= isinf(y);
+            }
+        if (inf) ugate[u] = 1;
+        return;
+    }
+    const double *ds = dsum + 16 * (int64_t)ub;
+    const double SW = ds[10], SWo = ds[11];
+    double *to = tod_out + ((int64_t)f * kBands + b) * T + t0;
+    double *oo = orig_out + ((int64_t)f * kBands + b) * T + t0;
+    for (int t = threadIdx.x; t < n; t += blockDim.x) {
+        double sr = 0.0, so = 0.0;
+        for (int k = 0; k < nr; ++k) {
+            const int c = rows[k];
+            const int64_t i = kb + c;
+            const double y = special_y(alpha[i], oa[2 * i], oa[2 * i + 1], xreg[2 * i], xreg[2 * i + 1],
+                                       tod[(fb + c) * T + t0 + t], a[t], m[t]);
+            double r = y * nf[i] / gain0[fb + c];
+            if (isnan(r)) r = 0.0;
+            sr += rw[k] * r;
+            double q = y * tsys0[fb + c];
+            if (isnan(q)) q = 0.0;
+            so += rwo[k] * q;
+        }
+        to[t] += sr / SW;
+        oo[t] += so / SWo;
     }
 }
 
@@ -1464,6 +1666,8 @@ extern "C" int comap_l1_plan_create(comap_ctx *ctx, const comap_obs_desc *d, com
     rc |= dalloc(ctx, &p->ubs, 4 * (size_t)p->U * kBands);
     rc |= dalloc(ctx, &p->fitsum, 2 * (size_t)UC);
     rc |= dalloc(ctx, &p->oa, 2 * (size_t)UC);
+    rc |= dalloc(ctx, &p->ynf, (size_t)p->U);
+    rc |= dalloc(ctx, &p->ugate, (size_t)p->U);
     if (rc) { delete p; return -2; }
     // pass B / median / pass C pipeline groups (comap_l1_average): contiguous unit ranges
     // COMAP_GROUPS (env) overrides the compiled default -- measurement knob
@@ -1533,7 +1737,7 @@ extern "C" int comap_l1_plan_destroy(comap_l1_plan *p)
                     p->nan_count, p->alpha, p->nf, p->bsum, p->mb, p->mf, p->ssum, p->sdm, p->gw,
                     p->gmode, p->kap, p->dsum, p->xreg, p->dG, p->rowbad, p->ubs, p->fitsum, p->oa,
                     p->flag, p->dlist, p->dcnt, p->dw, p->nanpos, p->nanpos_n, p->vane_dev,
-                    p->sel_pairs, p->sel_voff, p->sel_flag, p->sel_valid};
+                    p->sel_pairs, p->sel_voff, p->sel_flag, p->sel_valid, p->ynf, p->ugate};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (int g = 0; g < comap_l1_plan::kMaxGroups; ++g) {
@@ -1803,13 +2007,23 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
     COMAP_LAUNCH_CHECK(ctx);
     PROF(p, KV_GAIN_WEIGHTS, k_gain_weights<<<p->F, 1024, 0, st>>>(tsys0, p->gw, p->gmode));
     COMAP_LAUNCH_CHECK(ctx);
-    auto coef_d = [&](int phase) {
+    k_unit_flags<<<p->U, 256, 0, st>>>(p->units, p->alpha, p->rowbad, p->bsum, tsys0, p->ynf);
+    COMAP_LAUNCH_CHECK(ctx);
+    // +-inf samples left after the NaN fill (pass A counted them): special rows (k_special_rows)
+    const bool special = p->nan_total > 0;
+    auto coef_d = [&](int phase, const int32_t *ugate) {
         k_coef_d<<<UB, 256, 0, st>>>(p->units, p->unit_sums, p->mom, UC, p->oa, p->alpha, p->nf, p->bsum, p->ssum,
                                      p->sdm, tsys0, gain0, p->gw, p->gmode, calibrator, p->kap, p->dsum, p->xreg,
-                                     phase, p->flag, p->dlist, p->dcnt, p->dw);
+                                     phase, p->flag, p->dlist, p->dcnt, p->dw, p->rowbad, p->tod, p->T, p->airmass,
+                                     p->mf, p->ynf, ugate);
+    };
+    auto special_rows = [&](int mode) {
+        k_special_rows<<<UB, 256, 0, st>>>(mode, p->units, p->tod, p->T, p->airmass, p->mf, p->oa, p->alpha, p->nf,
+                                           p->rowbad, p->bsum, p->xreg, tsys0, gain0, p->dsum, calibrator, p->ugate,
+                                           tod_out, orig_out);
     };
     // phase 0: the kappa weights and the channel list (no regression needed)
-    PROF(p, KV_COEF_D, coef_d(0));
+    PROF(p, KV_COEF_D, coef_d(0, nullptr));
     COMAP_LAUNCH_CHECK(ctx);
     // Pass B (band means + every per-sample output sum), the sliding median and pass C
     // (regression sums) are software-pipelined over the unit groups on two streams:
@@ -1844,8 +2058,20 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
         COMAP_LAUNCH_CHECK(ctx);
     }
     // phase 1: regression solve, per-band constants, kappa re-check
-    PROF(p, KV_COEF_D, coef_d(1));
+    PROF(p, KV_COEF_D, coef_d(1, nullptr));
     COMAP_LAUNCH_CHECK(ctx);
+    if (special) {
+        // the fit_power_spectrum gate of units whose band-0 special rows hold +-inf, then the
+        // coefficients again with it (a kappa that changes sets the flag: legacy pass D)
+        COMAP_CHECK(ctx, hipMemsetAsync(p->ugate, 0, 4 * (size_t)p->U, st));
+        special_rows(0);
+        COMAP_LAUNCH_CHECK(ctx);
+        coef_d(2, p->ugate);
+        COMAP_LAUNCH_CHECK(ctx);
+        // pass B's fused sums took kappa 0 * inf = NaN at a special row's +-inf samples; the
+        // legacy pass D re-forms every output and skips kappa-0 channels
+        COMAP_CHECK(ctx, hipMemsetAsync(p->flag, 0xff, 4, st));
+    }
     // legacy pass D: exits at once unless phase 1 found a kappa that depends on the
     // regression (a NaN regression coefficient), in which case it recomputes the outputs
     // exactly from phase 1's constants (a former separate phase-2 k_coef_d launch
@@ -1857,6 +2083,10 @@ extern "C" int comap_l1_average(comap_l1_plan *p, const double *fit, const doubl
     PROF(p, KV_FINISH, k_finish<<<p->n_tiles, 256, 0, st>>>(p->units, p->tiles, p->T, p->airmass, p->mf, p->dsum,
                                                             tod_out, orig_out, p->dG, p->flag));
     COMAP_LAUNCH_CHECK(ctx);
+    if (special) {
+        special_rows(1);
+        COMAP_LAUNCH_CHECK(ctx);
+    }
     PROF(p, KV_SCAN_WEIGHTS, k_scan_weights<<<UB, 256, 0, st>>>(p->units, p->T, tod_out, w_out));
     COMAP_LAUNCH_CHECK(ctx);
     return 0;

@@ -1012,3 +1012,162 @@ int comap_median_run(comap_ctx *ctx, MedPlan *mp, hipStream_t st)
     COMAP_LAUNCH_CHECK(ctx);
     return 0;
 }
+
+// ------------------------------------------------------------------ two-heap replay
+// The order statistics above are the reference's result only when every comparison is a
+// total order.  For a series holding NaN, Mediator's comparisons with NaN are all false,
+// so which value sits at the median slot follows the heap's whole insertion history
+// (Mediator.h:36-99); the drop-in (medfilt.pyx:26-33) and the data prep's running median
+// (COMAPData.py:72-81, 357-360) feed such series to it.  They are replayed here exactly:
+// one workgroup per series, the series materialised in a work array, one lane running
+// medianFilter.cpp:4-30's four phases on it in place over a two-heap kept in LDS (or in a
+// global scratch block for windows above kReplayLdsWindow), then the requested outputs
+// copied out.  The series are rare (NaN-bearing) and independent, so a serial lane per
+// series is the exact and sufficient shape.
+namespace {
+
+constexpr int kReplayThreads = 256;
+constexpr int kReplayLdsWindow = 10240;          // 16 B per window slot: <= 160 KiB of LDS
+
+struct ReplayHeap {
+    int n;              // window
+    double *val;        // ring slot -> value
+    int *at;            // ring slot -> heap position
+    int *hp;            // heap position + n/2 -> ring slot
+    int nlo, nhi, cur;
+
+    __device__ int &slot(int pos) { return hp[pos + n / 2]; }
+    __device__ bool below(int i, int j) { return val[slot(i)] < val[slot(j)]; }
+    __device__ bool order(int i, int j)      // swap positions i, j when value(i) < value(j)
+    {
+        const int a = slot(i), b = slot(j);
+        if (!(val[a] < val[b])) return false;
+        slot(i) = b; slot(j) = a;
+        at[b] = i; at[a] = j;
+        return true;
+    }
+    __device__ bool hi_up(int i) { while (i > 0 && order(i, i / 2)) i /= 2; return i == 0; }
+    __device__ bool lo_up(int i) { while (i < 0 && order(i / 2, i)) i /= 2; return i == 0; }
+    __device__ void hi_down(int i)
+    {
+        for (i *= 2; i <= nhi; i *= 2) {
+            if (i < nhi && below(i + 1, i)) ++i;
+            if (!order(i, i / 2)) break;
+        }
+    }
+    __device__ void lo_down(int i)
+    {
+        for (i *= 2; i >= -nlo; i *= 2) {
+            if (i > -nlo && below(i, i - 1)) --i;
+            if (!order(i / 2, i)) break;
+        }
+    }
+    __device__ void init()
+    {
+        nlo = nhi = cur = 0;
+        for (int s = n - 1; s >= 0; --s) {      // slot s starts at 0, -1, +1, -2, +2, ...
+            const int pos = ((s + 1) / 2) * ((s & 1) ? -1 : 1);
+            at[s] = pos;
+            slot(pos) = s;
+            val[s] = 0.0;
+        }
+    }
+    __device__ void push(double v)
+    {
+        const int p = at[cur];
+        const double old = val[cur];
+        val[cur] = v;
+        cur = cur + 1 == n ? 0 : cur + 1;
+        if (p > 0) {
+            if (nhi < (n - 1) / 2) ++nhi;
+            else if (v > old) { hi_down(p); return; }
+            if (hi_up(p) && order(0, -1)) lo_down(-1);
+        } else if (p < 0) {
+            if (nlo < n / 2) ++nlo;
+            else if (v < old) { lo_down(p); return; }
+            if (lo_up(p) && nhi && order(1, 0)) hi_down(1);
+        } else {
+            if (nlo && lo_up(-1)) lo_down(-1);
+            if (nhi && hi_up(1)) hi_down(1);
+        }
+    }
+    __device__ double median()
+    {
+        double v = val[slot(0)];
+        if (nhi < nlo) v = (v + val[slot(-1)]) / 2;
+        return v;
+    }
+};
+
+// job j: work[woff[j] .. + m) = the (virtual) series, m = n (mode 0) or 3n (mode 1); the
+// filter runs on it in place; outputs [out_lo, out_hi) -> dst.  heap_g (global heap
+// arrays, 16 w bytes per job) is used when w > kReplayLdsWindow.
+__global__ void __launch_bounds__(kReplayThreads) k_med_replay(const MedJob *__restrict__ jobs,
+                                                               const int64_t *__restrict__ woff,
+                                                               double *__restrict__ work, int w,
+                                                               char *__restrict__ heap_g)
+{
+    extern __shared__ double replay_lds[];
+    const MedJob j = jobs[blockIdx.x];
+    const int64_t n = j.n, m = j.mode == 0 ? n : 3 * n;
+    double *z = work + woff[blockIdx.x];
+    for (int64_t i = threadIdx.x; i < m; i += kReplayThreads) {
+        int64_t s = i;
+        if (j.mode != 0) s = i < n ? n - 1 - i : (i < 2 * n ? i - n : 3 * n - 1 - i);
+        z[i] = j.src[s];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        ReplayHeap h;
+        h.n = w;
+        char *base = w <= kReplayLdsWindow ? (char *)replay_lds : heap_g + 16 * (int64_t)w * blockIdx.x;
+        h.val = (double *)base;
+        h.at = (int *)(base + 8 * (int64_t)w);
+        h.hp = h.at + w;
+        h.init();
+        const int64_t hw = w / 2, off = w / 2 + w % 2;
+        for (int64_t i = 0; i < hw; ++i) { h.push(z[0]); z[i] = h.median(); }
+        for (int64_t i = 0; i < off; ++i) h.push(z[i]);
+        for (int64_t i = 0; i < m - off; ++i) { z[i] = h.median(); h.push(z[i + off]); }
+        for (int64_t i = m - off; i < m; ++i) { z[i] = h.median(); h.push(z[m - 1]); }
+    }
+    __syncthreads();
+    for (int64_t i = j.out_lo + threadIdx.x; i < j.out_hi; i += kReplayThreads) j.dst[i - j.out_lo] = z[i];
+}
+
+}  // namespace
+
+int comap_median_replay(comap_ctx *ctx, const std::vector<MedJob> &jobs, int32_t w, hipStream_t st)
+{
+    if (jobs.empty()) return 0;
+    if (w < 1) return comap_fail(ctx, -1, "median window must be >= 1");
+    std::vector<int64_t> woff(jobs.size() + 1, 0);
+    for (size_t k = 0; k < jobs.size(); ++k) {
+        const MedJob &j = jobs[k];
+        const int64_t m = j.mode == 0 ? j.n : 3 * j.n;
+        // medianFilter.cpp reads and writes outside the array below ceil(w/2) values
+        if (m < (int64_t)(w / 2 + w % 2) || j.n < 1)
+            return comap_fail(ctx, -1, "median replay: series shorter than ceil(w/2)");
+        if (j.out_lo < 0 || j.out_hi > m || j.out_lo > j.out_hi) return comap_fail(ctx, -1, "median replay: bad range");
+        woff[k + 1] = woff[k] + m;
+    }
+    const int nj = (int)jobs.size();
+    DevTemps tmp(st, false);     // freed behind the queued work
+    MedJob *djobs = nullptr;
+    int64_t *dwoff = nullptr;
+    double *work = nullptr;
+    char *heap_g = nullptr;
+    COMAP_CHECK(ctx, tmp.alloc(&djobs, jobs.size()));
+    COMAP_CHECK(ctx, tmp.alloc(&dwoff, woff.size()));
+    COMAP_CHECK(ctx, tmp.alloc(&work, (size_t)woff.back()));
+    const bool lds = w <= kReplayLdsWindow;
+    if (!lds) COMAP_CHECK(ctx, tmp.alloc(&heap_g, 16 * (size_t)w * jobs.size()));
+    COMAP_CHECK(ctx, comap_upload(djobs, jobs.data(), sizeof(MedJob) * jobs.size(), st));
+    COMAP_CHECK(ctx, comap_upload(dwoff, woff.data(), 8 * woff.size(), st));
+    const size_t sm = lds ? 16 * (size_t)w : 0;
+    COMAP_CHECK(ctx, hipFuncSetAttribute((const void *)k_med_replay, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)std::max<size_t>(sm, 16)));
+    k_med_replay<<<nj, kReplayThreads, sm, st>>>(djobs, dwoff, work, w, heap_g);
+    COMAP_LAUNCH_CHECK(ctx);
+    return 0;
+}

@@ -619,13 +619,12 @@ __global__ void __launch_bounds__(256) k_prep_gather(comap_prep_file f, comap_pr
 
 // ---------------------------------------------------------------- running-median high-pass
 // segment k = x[seg[2k] .. seg[2k] + seg[2k+1]); its median input = the non-zero samples
-// (bad = tod == 0, COMAPData.py:357-360) that are not NaN.  +-inf stays in, as in the
-// reference (the two-heap orders +-inf like any value, so the window median is still an
-// order statistic).  NaN is left out: np.nanmedian (the <= 2w branch, :79) ignores it, so
-// short segments match the reference with NaN too; in the running median (> 2w) the
-// reference's result for a window holding NaN depends on its two-heap's history, which
-// the order-statistics kernels do not reproduce.
-__device__ __forceinline__ bool hp_keep(double v) { return v != 0.0 && !isnan(v); }
+// (bad = tod == 0, COMAPData.py:357-360), NaN and +-inf included as in the reference.  A
+// segment of <= 2w values takes np.nanmedian (:79, NaN ignored); a longer one the running
+// median, where the order-statistics plan serves NaN-free segments and a segment holding
+// NaN is replayed through the reference's two-heap (comap_median_replay), whose result for
+// NaN follows its insertion history.
+__device__ __forceinline__ bool hp_keep(double v) { return v != 0.0; }
 
 // One 1024-thread workgroup per segment (a chain segment holds ~8 k samples: 16 waves
 // keep enough loads in flight; 256 threads left the pass latency-bound at ~1.2 TB/s).
@@ -636,24 +635,39 @@ __global__ void __launch_bounds__(kSegThreads) k_seg_count(const double *__restr
                                                            const int64_t *__restrict__ seg,
                                                            int64_t *__restrict__ cnt)
 {
-    __shared__ unsigned c_s[kSegThreads / 64];
+    // cnt[k] = median-input values of segment k, cnt[nseg + k] = NaN among them
+    __shared__ unsigned c_s[kSegThreads / 64], q_s[kSegThreads / 64];
     const double *p = x + seg[2 * blockIdx.x];
     const int64_t n = seg[2 * blockIdx.x + 1];
-    unsigned c = 0;
+    unsigned c = 0, q = 0;
     int64_t i = threadIdx.x;
     for (; i + kSegThreads < n; i += 2 * kSegThreads) {     // two independent loads per trip
         const double a = p[i], b = p[i + kSegThreads];
         c += hp_keep(a) + hp_keep(b);
+        q += isnan(a) + isnan(b);
     }
-    if (i < n) c += hp_keep(p[i]);
+    if (i < n) {
+        c += hp_keep(p[i]);
+        q += isnan(p[i]);
+    }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-    if ((threadIdx.x & 63) == 0) c_s[threadIdx.x >> 6] = c;
+    for (int o = 32; o > 0; o >>= 1) {
+        c += __shfl_xor(c, o, 64);
+        q += __shfl_xor(q, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        c_s[threadIdx.x >> 6] = c;
+        q_s[threadIdx.x >> 6] = q;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-        unsigned long long t = 0;
-        for (int v = 0; v < kSegThreads / 64; ++v) t += c_s[v];
+        unsigned long long t = 0, u = 0;
+        for (int v = 0; v < kSegThreads / 64; ++v) {
+            t += c_s[v];
+            u += q_s[v];
+        }
         cnt[blockIdx.x] = (int64_t)t;
+        cnt[gridDim.x + blockIdx.x] = (int64_t)u;
     }
 }
 
@@ -694,10 +708,10 @@ __global__ void __launch_bounds__(kSegThreads) k_seg_compact(const double *__res
 }
 
 // Segments with 1 .. 2w median-input values: np.nanmedian of the values (COMAPData.py:79),
-// broadcast.  One workgroup per segment (the others exit at once): every value's rank =
-// the values below it plus the equal ones before it (the values are non-zero and not NaN;
-// +-inf compare like any value), so the sorted order needs no sort; even counts average
-// the two middle values as np.median does ((a + b) / 2).
+// broadcast.  One workgroup per segment (the others exit at once): every non-NaN value's
+// rank = the non-NaN values below it plus the equal ones before it (+-inf compare like any
+// value), so the sorted order needs no sort; NaN is ignored (all NaN: the median is NaN);
+// even counts average the two middle values as np.median does ((a + b) / 2).
 constexpr int kSmallSeg = 2048;
 __global__ void __launch_bounds__(256) k_seg_small_median(const double *__restrict__ vals,
                                                           const int64_t *__restrict__ off,
@@ -707,17 +721,27 @@ __global__ void __launch_bounds__(256) k_seg_small_median(const double *__restri
     const int64_t n = cnt[blockIdx.x];
     if (n == 0 || n > nmax) return;
     __shared__ double v[kSmallSeg], srt[kSmallSeg];
+    __shared__ int nn_s;
     const int64_t o0 = off[blockIdx.x];
-    for (int i = threadIdx.x; i < n; i += blockDim.x) v[i] = vals[o0 + i];
+    if (threadIdx.x == 0) nn_s = 0;
     __syncthreads();
+    int nn = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        v[i] = vals[o0 + i];
+        nn += !isnan(v[i]);
+    }
+    atomicAdd(&nn_s, nn);
+    __syncthreads();
+    const int m = nn_s;
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         const double x = v[i];
+        if (isnan(x)) continue;
         int r = 0;
         for (int j = 0; j < n; ++j) r += (v[j] < x) || (v[j] == x && j < i);
         srt[r] = x;
     }
     __syncthreads();
-    const double med = (n & 1) ? srt[n / 2] : (srt[n / 2 - 1] + srt[n / 2]) / 2.0;
+    const double med = m == 0 ? (double)NAN : (m & 1) ? srt[m / 2] : (srt[m / 2 - 1] + srt[m / 2]) / 2.0;
     for (int i = threadIdx.x; i < n; i += blockDim.x) filt[o0 + i] = med;
 }
 
@@ -889,12 +913,12 @@ extern "C" int comap_prep_highpass(comap_ctx *ctx, double *x, const int64_t *seg
     hipStream_t st = ctx->stream;
     DevTemps tmp(st, false);   // freed behind the queued work (stream-safe cache): no host wait
     int64_t *cnt = nullptr, *off = nullptr;
-    COMAP_CHECK(ctx, tmp.alloc(&cnt, (size_t)nseg));
+    COMAP_CHECK(ctx, tmp.alloc(&cnt, 2 * (size_t)nseg));
     COMAP_CHECK(ctx, tmp.alloc(&off, (size_t)nseg));
     k_seg_count<<<nseg, kSegThreads, 0, st>>>(x, seg_dev, cnt);
     COMAP_LAUNCH_CHECK(ctx);
-    std::vector<int64_t> c(nseg), o(nseg);
-    COMAP_CHECK(ctx, hipMemcpyAsync(c.data(), cnt, 8 * (size_t)nseg, hipMemcpyDeviceToHost, st));
+    std::vector<int64_t> c(2 * (size_t)nseg), o(nseg);     // counts, then NaN counts
+    COMAP_CHECK(ctx, hipMemcpyAsync(c.data(), cnt, 16 * (size_t)nseg, hipMemcpyDeviceToHost, st));
     COMAP_CHECK(ctx, hipStreamSynchronize(st));
     int64_t total = 0, cmax = 0;
     for (int k = 0; k < nseg; ++k) {
@@ -911,7 +935,7 @@ extern "C" int comap_prep_highpass(comap_ctx *ctx, double *x, const int64_t *seg
     COMAP_CHECK(ctx, comap_upload(off, o.data(), 8 * (size_t)nseg, st));
     k_seg_compact<<<nseg, kSegThreads, 0, st>>>(x, seg_dev, off, vals, pos);
     COMAP_LAUNCH_CHECK(ctx);
-    std::vector<MedJob> jobs;
+    std::vector<MedJob> jobs, replay;
     std::vector<int> small;      // short segments the device kernel cannot hold (2w > kSmallSeg)
     const int64_t nsmall_dev = 2 * (int64_t)w <= kSmallSeg ? 2 * (int64_t)w : 0;
     bool any_small_dev = false;
@@ -931,12 +955,13 @@ extern "C" int comap_prep_highpass(comap_ctx *ctx, double *x, const int64_t *seg
             j.mode = 1;
             j.pad_ = 0;
             j.gate = nullptr;
-            jobs.push_back(j);
+            (c[nseg + k] > 0 ? replay : jobs).push_back(j);     // NaN: the two-heap's own order
         } else {
             small.push_back(k);
         }
     }
-    int rc = 0;
+    int rc = comap_median_replay(ctx, replay, w, st);
+    if (rc) return rc;
     // (a chunked small-window median -- one workgroup per 256 outputs bitonic-sorting its
     // union window in registers / LDS -- matched this bit for bit but ran 1.9 ms against
     // the plan's ~0.9 ms at the chain's 912 segments, r03t7: removed)
@@ -970,9 +995,11 @@ extern "C" int comap_prep_highpass(comap_ctx *ctx, double *x, const int64_t *seg
         std::vector<double> v(c[k]);
         COMAP_CHECK(ctx, hipMemcpyAsync(v.data(), vals + o[k], 8 * v.size(), hipMemcpyDeviceToHost, st));
         COMAP_CHECK(ctx, hipStreamSynchronize(st));
-        std::sort(v.begin(), v.end());
         const size_t n = v.size();
-        const double med = n % 2 ? v[n / 2] : (v[n / 2 - 1] + v[n / 2]) / 2.0;
+        v.erase(std::remove_if(v.begin(), v.end(), [](double a) { return std::isnan(a); }), v.end());
+        std::sort(v.begin(), v.end());
+        const size_t m = v.size();     // np.nanmedian: NaN ignored, all NaN -> NaN
+        const double med = m == 0 ? NAN : m % 2 ? v[m / 2] : (v[m / 2 - 1] + v[m / 2]) / 2.0;
         std::vector<double> f(n, med);
         COMAP_CHECK(ctx, comap_upload(filt + o[k], f.data(), 8 * n, st));
     }

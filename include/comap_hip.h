@@ -67,17 +67,23 @@ int comap_cache_trim(void);
 int comap_cache_bytes(int64_t *device_cached, int64_t *device_live, int64_t *host_cached);
 
 /* ------------------------------------------------------------ drop-ins (host arrays) */
-/* In place, identical to medfilt.medfilt(x, w): out[i] = median of
+/* In place, identical to medfilt.medfilt(x, w) for any double input: NaN-free
+ * x with n >= w takes the order-statistics kernels (out[i] = median of
  * x'[i-w/2 .. i-w/2+w-1] with x'[j<w/2] = x[0], x'[j>=n] = x[n-1]; even w
- * averages the two middle values.  Requires w <= n, w <= 32768 and a
- * NaN-free x (returns -3 on NaN: the two-heap's NaN order is undefined). */
+ * averages the two middle values); x holding NaN (every comparison of the
+ * reference's two-heap with NaN is false, so its result follows the insertion
+ * history), or ceil(w/2) <= n < w, is replayed exactly through the two-heap on
+ * the device (Mediator.h:36-99, one workgroup per series).  Requires
+ * n >= ceil(w/2): below it medianFilter.cpp reads and writes outside the array. */
 int comap_medfilt_f64(comap_ctx *ctx, double *x_host, int64_t n, int32_t w);
 /* Batched sliding median of nseries host series x[offsets[s]..offsets[s+1]).
  * mode 0: medfilt semantics (as comap_medfilt_f64) for every output;
  * mode 1: out = medfilt([x[::-1], x, x[::-1]], w)[n:2n], the reflect-padded
  * high-pass filter of Level1Averaging.median_filter / COMAPData.median_filter
  * (Level1Averaging.py:696-700, COMAPData.py:72-81), without materialising
- * the pad (requires n >= w in both modes).  out_host has offsets[nseries] values. */
+ * the pad.  Series holding NaN or shorter than w take the two-heap replay (as
+ * comap_medfilt_f64); every series needs ceil(w/2) values (mode 0) or
+ * 3n >= ceil(w/2) (mode 1).  out_host has offsets[nseries] values. */
 int comap_medfilt_batch_f64(comap_ctx *ctx, const double *x_host, const int64_t *offsets_host,
                             int32_t nseries, int32_t w, int32_t mode, double *out_host);
 /* image[p] += weights[i] (or += 1 when weights == NULL) for 0 <= p < npix
@@ -385,10 +391,11 @@ int comap_prep_percentiles(comap_ctx *ctx, const double *az_dev, const double *e
  * before the high-pass; `wcs` may be NULL when f->pixels is given. */
 int comap_prep_gather(comap_ctx *ctx, const comap_prep_file *f, const comap_prep_wcs *wcs,
                       const comap_prep_out *out);
-/* x[seg] -= median_filter(x[seg][keep], w) on keep = non-zero, non-NaN samples of each
- * segment seg_dev[k] = {element offset, length} (COMAPData.py:72-81, 353-360): +-inf
- * stays in the median input as in the reference; NaN samples are left out and stay NaN
- * (exact for segments of <= 2w values, where the reference takes np.nanmedian).
+/* x[seg] -= median_filter(x[seg][keep], w) on keep = the non-zero samples of each
+ * segment seg_dev[k] = {element offset, length} (COMAPData.py:72-81, 353-360; bad =
+ * tod == 0, so NaN and +-inf stay in the median input as in the reference): segments of
+ * <= 2w values take np.nanmedian, longer ones the running median -- the two-heap replay
+ * for a segment holding NaN, whose result follows the reference's insertion history.
  * Synchronises (segment lengths size the median plan). */
 int comap_prep_highpass(comap_ctx *ctx, double *x_dev, const int64_t *seg_dev, int32_t nseg, int32_t w);
 /* NaN -> 0, keep[b][o] = any weight of offset o in band b non-zero, the union of kept

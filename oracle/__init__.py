@@ -40,6 +40,8 @@ def lib():
         lp = ctypes.POINTER(ctypes.c_int64)
         L.oracle_medfilt.argtypes = [dp, ctypes.c_int64, ctypes.c_int32]
         L.oracle_medfilt.restype = ctypes.c_int
+        L.oracle_medfilt_twoheap.argtypes = [dp, ctypes.c_int64, ctypes.c_int32]
+        L.oracle_medfilt_twoheap.restype = ctypes.c_int
         L.oracle_bin_values.argtypes = [dp, ctypes.c_int64, lp, dp, lp, ctypes.c_int64]
         L.oracle_bin_values.restype = ctypes.c_int
         _LIB = L
@@ -66,13 +68,28 @@ def _dptr(a):
 
 
 def medfilt(x, w):
-    """In-place semantics of medfilt.medfilt (medfilt.pyx:26-33); returns the array."""
+    """In-place semantics of medfilt.medfilt (medfilt.pyx:26-33); returns the array.
+
+    NaN-free input with n >= w: the order-statistics restatement (oracle_medfilt).
+    Input holding NaN, or ceil(w/2) <= n < w: the two-heap restatement
+    (oracle_medfilt_twoheap), whose result for NaN follows Mediator.h's insertion
+    history as the reference's does."""
     x = np.ascontiguousarray(x, dtype=np.float64)
-    rc = lib().oracle_medfilt(_dptr(x), x.size, int(w))
-    if rc == -3:
-        raise ValueError('oracle_medfilt: NaN input (the two-heap order for NaN is not restated)')
+    if x.size >= w and not np.isnan(x).any():
+        rc = lib().oracle_medfilt(_dptr(x), x.size, int(w))
+    else:
+        rc = lib().oracle_medfilt_twoheap(_dptr(x), x.size, int(w))
     if rc != 0:
         raise ValueError(f'oracle_medfilt failed rc={rc} (n={x.size}, w={w})')
+    return x
+
+
+def medfilt_twoheap(x, w):
+    """The two-heap restatement on any input (in place; returns the array)."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    rc = lib().oracle_medfilt_twoheap(_dptr(x), x.size, int(w))
+    if rc != 0:
+        raise ValueError(f'oracle_medfilt_twoheap failed rc={rc} (n={x.size}, w={w})')
     return x
 
 

@@ -302,6 +302,12 @@ def gain_subtraction_fit(y, tsys):
     w, _, all_bad = gain_weights(tsys)
     if all_bad:
         return np.zeros(n)
+    if not np.isfinite(y).all():
+        # A non-finite y (a NaN / inf sample, or a channel whose normalisation rms is
+        # NaN) makes b = P^T Z d non-finite; cg's first matvec on it raises ValueError
+        # ('PtZPg is not finite', GainSubtraction.py:127-128), which
+        # solve_gain_solution catches and returns g = zeros (:154-158).
+        return np.zeros(n)
     return w @ y.reshape(B * C, n)
 
 

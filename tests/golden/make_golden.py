@@ -472,7 +472,20 @@ def main():
     ap.add_argument('--only-variants-new', action='store_true', help='tinyscan + f3 variants only')
     ap.add_argument('--only-timing', action='store_true', help='reference destriper C4 timing only')
     ap.add_argument('--c4-npz', default=None, help='time the reference on this dumped C4 problem')
+    ap.add_argument('--variants', nargs='+', default=None, help='only these Level-1 variants (variants.NAMES)')
     args = ap.parse_args()
+    if args.variants:
+        os.environ.setdefault('MPLBACKEND', 'agg')
+        build_reference_helpers()
+        install_stubs()
+        figdir = os.path.join(SCRATCH, 'figures')
+        os.makedirs(figdir, exist_ok=True)
+        mp = os.path.join(HERE, 'golden_meta.json')
+        meta = json.load(open(mp))
+        for name in args.variants:
+            meta[f'l1_{name}_sha256'] = run_l1_variant(name, figdir)
+        json.dump(meta, open(mp, 'w'), indent=1, default=str)
+        return
     if args.only_variants_new or args.only_timing:
         os.environ.setdefault('MPLBACKEND', 'agg')
         build_reference_helpers()

@@ -15,6 +15,17 @@ Each variant is the synthetic generator's output with a deterministic edit:
            (:834-838); the atmosphere fit has < 100 samples (NaN fit)
   f3       3 feeds numbered 1, 2, 20, T = 30,000 (two full scans): multi-feed unit
            tables, per-feed gain weights, and the feeds > 19 skip (:817-818)
+  inf      +-inf Level-1 samples, T = 30,000 (two scans), all in scan 0 at even
+           stride-4 positions, so normalise_data's rms of those channels is NaN
+           (Level1Averaging.py:667-679) and their filtered rows are NaN: the
+           fit_power_spectrum gate passes (nanmean skips them, :571), b = P^T Z d is
+           non-finite, cg's matvec raises and solve_gain_solution returns dG = 0
+           (GainSubtraction.py:127-128, 154-158); scan 1 keeps its gain fit
+  infodd   +inf / -inf samples at odd stride-4 positions (finite rms): the regression
+           of the median filter (np.linalg.solve, :701-705) turns the row into a mix
+           of +-inf and NaN, the band-0 channel nanmean holds +-inf so the gate raises
+           (dG = None, :834-838), and the band averages keep the +-inf entries
+           (only NaN becomes 0, :596-597)
 """
 import numpy as np
 
@@ -29,8 +40,9 @@ def make(name):
     if name == 'calib':
         cfg = synthetic.SyntheticConfig(n_feeds=1, n_samples=T_EDGE, obs_id=11, source='TauA')
     else:
-        cfg = synthetic.SyntheticConfig(n_feeds=1, n_samples=T_EDGE,
-                                        obs_id={'nan': 12, 'constel': 13, 'tinyscan': 14}[name])
+        cfg = synthetic.SyntheticConfig(n_feeds=1, n_samples=30_000 if name == 'inf' else T_EDGE,
+                                        obs_id={'nan': 12, 'constel': 13, 'tinyscan': 14, 'inf': 16,
+                                                'infodd': 15}[name])
     gen = synthetic.generate_level1(cfg)
     d = gen['data']
     if name == 'nan':
@@ -39,6 +51,17 @@ def make(name):
         tod[0, 3, 700, 8000:8050] = np.nan      # fitted channel, band 3
         tod[0, 1, 5, 1500:] = np.nan            # unfitted channel, NaN over the whole scan
         tod[0, 2, 300, 5000] = np.nan           # single sample
+        d['spectrometer/band_average'] = np.nanmean(tod, axis=2).astype(np.float32)
+    elif name in ('inf', 'infodd'):
+        tod = d['spectrometer/tod']
+        s0 = synthetic.SCAN_START                  # scan 0 = [1500, 15499)
+        if name == 'inf':
+            tod[0, 0, 100, s0 + 1500] = np.inf         # offset = 0 mod 4: in tod[..., 0::4]
+            tod[0, 2, 300, s0 + 3502] = -np.inf        # offset = 2 mod 4: in tod[..., 2::4]
+            tod[0, 1, 200, s0 + 2500:s0 + 2505] = np.inf
+        else:
+            tod[0, 0, 100, s0 + 1501] = np.inf         # offset = 1 mod 4
+            tod[0, 1, 300, s0 + 1503] = -np.inf        # offset = 3 mod 4
         d['spectrometer/band_average'] = np.nanmean(tod, axis=2).astype(np.float32)
     elif name == 'constel':
         f = d['spectrometer/features']
@@ -53,7 +76,7 @@ def make(name):
 
 F3_CONFIG = dict(n_feeds=3, n_samples=30_000, obs_id=5, feed_numbers=(1, 2, 20))
 F3_STRIDE = 7          # the f3 golden keeps averaged_tod/* at every 7th sample (fixture size)
-NAMES = ('nan', 'constel', 'calib', 'tinyscan', 'f3')
+NAMES = ('nan', 'constel', 'calib', 'tinyscan', 'f3', 'inf', 'infodd')
 
 
 def spikes_level2(golden_dir):

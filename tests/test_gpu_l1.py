@@ -101,6 +101,29 @@ def test_medfilt_dropin_infinities(path, monkeypatch):
         assert np.array_equal(g, oracle.medfilt(z, 400)[s.size:2 * s.size], equal_nan=True), s.size
 
 
+def test_medfilt_dropin_nan_fixtures(golden_dir):
+    """NaN input through the drop-in (comap_medfilt_f64) and the batched reflect-padded
+    form (comap_medfilt_batch_f64): the two-heap replay == the reference's compiled filter
+    on the committed known-answer fixtures, bit for bit, NaN positions included
+    (tests/golden/make_medfilt_nan.py)."""
+    from comapreduce_amd.tools.medfilt import medfilt, medfilt_batch
+    g = np.load(os.path.join(golden_dir, 'golden_medfilt_nan.npz'))
+    names = sorted(k[2:] for k in g.files if k.startswith('x_'))
+    assert len(names) == 12
+    for name in names:
+        x, y, w, r = g[f'x_{name}'], g[f'y_{name}'], int(g[f'w_{name}']), bool(g[f'r_{name}'])
+        if r:
+            got = medfilt_batch([x], w, reflect=True)[0]
+        else:
+            got = medfilt(x.copy(), w)
+        assert np.array_equal(got, y, equal_nan=True), name
+    # a batch mixing NaN-bearing series (replayed) with NaN-free ones (order statistics)
+    plain = [np.round(np.random.default_rng(s).standard_normal(n), 1) for s, n in ((1, 2000), (2, 4000))]
+    series = [plain[0], g['x_single_w400'], plain[1], g['x_head_tail_w100']]
+    for s, got in zip(series, medfilt_batch(series, 400)):
+        assert np.array_equal(got, oracle.medfilt(s.copy(), 400), equal_nan=True)
+
+
 @pytest.mark.parametrize('path', ['sort', 'devsort', 'bitmap'])
 def test_medfilt_long_series_split(path, monkeypatch):
     """Series longer than one median sub-job / segment are split internally."""
@@ -206,9 +229,9 @@ def test_l1_median_selection_bit_exact(c1_run):
             assert np.array_equal(mf[f, b, t0:t0 + n], ref), (f, s, b)
 
 
-@pytest.mark.parametrize('name', ['nan', 'constel', 'calib', 'tinyscan', 'f3'])
+@pytest.mark.parametrize('name', ['nan', 'constel', 'calib', 'tinyscan', 'f3', 'inf', 'infodd'])
 def test_l1_edge_variants_vs_reference(golden_dir, name):
-    """NaN fill/select_time, constant-elevation and calibrator paths on the device."""
+    """NaN fill/select_time, constant-elevation, calibrator and +-inf paths on the device."""
     import sys
     sys.path.insert(0, golden_dir)
     import variants
@@ -229,6 +252,8 @@ def test_l1_edge_variants_vs_reference(golden_dir, name):
         if name == 'f3' and k.startswith('averaged_tod'):
             v = v[..., ::variants.F3_STRIDE]
         assert relmax(v, g[k.replace('/', '__')]) < RTOL, (name, k)
+        bad = ~np.isfinite(g[k.replace('/', '__')])         # +inf / -inf / NaN as the reference has them
+        assert np.array_equal(v[bad], g[k.replace('/', '__')][bad], equal_nan=True), (name, k)
 
 
 def test_spikes_stage_bit_exact(golden_dir):
