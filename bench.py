@@ -463,24 +463,48 @@ def allreduce_probe(dev, sizes, reps=30):
             'alpha_us': float(alpha), 'beta_GBs': float(1e-3 / slope) if slope > 0 else None}
 
 
+FIELD_KAPPA = 6.5     # entries-equivalent CG work of one offset (rankplan.balanced_ranges weights)
+
+
+def field_split(n_obs, world, n_feeds=19, kappa=FIELD_KAPPA, device='cpu'):
+    """The field's (obs, feed) series dealt to ``world`` ranks as contiguous ranges balanced
+    on the CG work each rank takes on: its operator entries (the (offset, pixel run) pairs
+    of its pointing) + kappa x its offsets (rankplan.balanced_ranges).  Equal observation
+    counts (run_destriper.py:131-138's len // size split) left rank 0 with 1.32 / 1.63 /
+    1.86 x the mean entries at 2 / 4 / 8 ranks: the synthetic scan slows down with the
+    observation index.  COMAP_FIELD_SPLIT=obs restores the equal split.  Returns
+    ([(lo, hi)] series ranges, per-series entries, offsets per series)."""
+    from comapreduce_amd import synthetic
+    from comapreduce_amd.mapmaking import rankplan
+    ent, no = synthetic.field_series_work(n_obs, n_feeds=n_feeds, device=device)
+    if os.environ.get('COMAP_FIELD_SPLIT', 'work') == 'obs':
+        return [(n_feeds * (n_obs * r // world), n_feeds * (n_obs * (r + 1) // world)) for r in range(world)], ent, no
+    w = np.round(ent + kappa * no).astype(np.int64)
+    return rankplan.balanced_ranges(w, world), ent, no
+
+
 def destriper_c5_field_leg(n_obs, niter, device, world, rank, n_bands=4):
     """configs[4] as stated: n_obs (64) synthetic observations x 19 feeds x 180,000 samples
     co-added into ONE 480 x 480 1' CAR field map and solved as one system (run_destriper.py:
-    131-189 puts every rank's files into one map).  On N ranks the observations are split
-    N ways (rank r: observations [r n / N, (r + 1) n / N)), so total work is fixed
+    131-189 puts every rank's files into one map).  On N ranks the (obs, feed) series are
+    dealt in contiguous ranges balanced on CG work (field_split), so total work is fixed
     ("scaling": strong): the map numerator (compacted to the hit pixels) and the CG block
     partials are all-reduced over RCCL every iteration.  Reports the set-up, ms per CG
     iteration (fixed niter, no early exit; the max over ranks) and the converged solve
-    (threshold 1e-6); with N > 1 also the measured per-iteration all-reduce time and bytes
-    (TimedAllreduce) and the RCCL alpha / beta probe at the CG's message sizes."""
+    (threshold 1e-6); with N > 1 also, per rank, the entries, samples, set-up ms and the
+    rank's own compute ms per CG iteration (its local operator solved alone, no
+    collectives), the measured per-iteration all-reduce time and bytes (TimedAllreduce)
+    and the RCCL alpha / beta probe at the CG's message sizes."""
     import torch
     import torch.distributed as dist
     from comapreduce_amd import synthetic
     from comapreduce_amd.mapmaking import destriper as D
+    from comapreduce_amd.mapmaking import rankplan
     L, npix = 50, 480 * 480
-    lo, hi = n_obs * rank // world, n_obs * (rank + 1) // world
-    pix, tod, w = synthetic.destriper_inputs_device(hi - lo, offset_length=L, device=device, seed=5000,
-                                                    n_bands=n_bands, obs0=lo)
+    ranges, ent, no = field_split(n_obs, world, device=device)
+    lo, hi = ranges[rank]
+    pix, tod, w = synthetic.destriper_inputs_device(0, offset_length=L, device=device, seed=5000,
+                                                    n_bands=n_bands, series=(lo, hi))
     _timed_setup(pix, tod, w, L, npix, device=device, map_shape=(480, 480))          # warm (first use of these sizes)
     prob, setup = _timed_setup(pix, tod, w, L, npix, device=device, map_shape=(480, 480))
     N_local = int(pix.numel())
@@ -494,6 +518,7 @@ def destriper_c5_field_leg(n_obs, niter, device, world, rank, n_bands=4):
         dist.barrier()
     res, dt = _timed_solve(prob, 0.0, niter)
     it = max(max(res['iters']) if n_bands > 1 else res['iters'], 1)
+    local = {'nnz': int(prob.nnz()[0]), 'n_samples': N_local, 'setup_ms': setup * 1e3}
     times = [dt, setup, conv_s]
     if world > 1:
         e = torch.tensor(times, device='cuda', dtype=torch.float64)
@@ -505,15 +530,20 @@ def destriper_c5_field_leg(n_obs, niter, device, world, rank, n_bands=4):
         nt = torch.tensor([N_local], device='cuda', dtype=torch.int64)
         dist.all_reduce(nt)
         N = int(nt.item())
+    w_ranks = [float(ent[a:b].sum() + FIELD_KAPPA * no * (b - a)) for a, b in ranges]
     out = {'config': f'configs[4]: {n_obs} obs x 19 feeds x 180000 samples co-added into ONE 480x480 CAR field map, '
-                     f'{n_bands} bands batched, L={L}, split over {world} rank(s) by observation (strong scaling), '
+                     f'{n_bands} bands batched, L={L}, split over {world} rank(s) by CG work (strong scaling), '
                      f'{niter} CG iterations (no early exit)',
            'n_samples_per_band': N, 'n_offsets': N // L, 'n_samples_rank0': N_local,
            'setup_ms': setup * 1e3, 'ms_per_iter': dt / it * 1e3, 'cg_iters_per_s': it / dt,
            'band_iters_per_s': n_bands * it / dt, 'iters': res['iters'],
            'converged': {'threshold': 1e-6, 'iters': conv['iters'], 'solve_ms': conv_s * 1e3,
                          'setup_plus_solve_ms': (setup + conv_s) * 1e3},
-           'scaling': 'strong', 'nnz_rank0': prob.nnz(), 'entry_bytes': prob.entry_bytes()}
+           'scaling': 'strong', 'nnz_rank0': prob.nnz(), 'entry_bytes': prob.entry_bytes(),
+           'split': {'policy': os.environ.get('COMAP_FIELD_SPLIT', 'work'), 'kappa': FIELD_KAPPA,
+                     'series_ranges': [list(map(int, r)) for r in ranges],
+                     'modelled_work_max_over_mean': max(w_ranks) / (sum(w_ranks) / len(w_ranks)),
+                     'entries_max_over_mean': rankplan.imbalance(ent, ranges)}}
     if world == 1:
         op_bytes = operator_bytes(prob, N // L, n_bands)
         out['operator_bytes_per_iter'] = op_bytes
@@ -526,6 +556,24 @@ def destriper_c5_field_leg(n_obs, niter, device, world, rank, n_bands=4):
         nmap = int(prob.hit_index.numel()) if prob.hit_index is not None else npix
         out['allreduce_probe'] = allreduce_probe(torch.device('cuda', device),
                                                  [8 * nb, 8 * nb * 1024, 8 * nb * nmap, 1 << 20])
+        # each rank's own compute per CG iteration: its local operator solved alone (no
+        # collectives) -- the imbalance the sharded iteration waits on, and what remains
+        # once the all-reduce cost (comm_rank0) is known
+        prob.ops.solve_native(0.0, 3)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        prob.ops.solve_native(0.0, niter)
+        torch.cuda.synchronize()
+        local['local_ms_per_iter'] = (time.perf_counter() - t0) / niter * 1e3
+        vec = torch.tensor([local['nnz'], local['n_samples'], local['setup_ms'], local['local_ms_per_iter']],
+                           dtype=torch.float64, device='cuda')
+        parts = [torch.zeros_like(vec) for _ in range(world)]
+        dist.all_gather(parts, vec)
+        rows = [p.tolist() for p in parts]
+        out['per_rank'] = {'nnz': [int(r[0]) for r in rows], 'n_samples': [int(r[1]) for r in rows],
+                           'setup_ms': [r[2] for r in rows], 'local_ms_per_iter': [r[3] for r in rows]}
+        lm = [r[3] for r in rows]
+        out['per_rank']['local_iter_max_over_mean'] = max(lm) / (sum(lm) / len(lm))
     del prob, res, conv
     torch.cuda.empty_cache()
     return out

@@ -74,6 +74,10 @@ _SIGS = {
     'comap_destripe_dist_direction_fused': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     'comap_destripe_create_bands': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32,
                                             c_int64, c_int32, ctypes.POINTER(c_void_p)]),
+    'comap_destripe_create_keyed': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                                            c_int64, c_int32, c_int64, c_int32, ctypes.POINTER(c_void_p)]),
+    'comap_offset_centroid_keys': (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_int64, c_int64, c_void_p, c_int64,
+                                           c_void_p]),
     'comap_destripe_destroy': (c_int, [c_void_p]),
     'comap_destripe_n_offsets': (c_int64, [c_void_p]),
     'comap_destripe_n_bands': (c_int32, [c_void_p]),

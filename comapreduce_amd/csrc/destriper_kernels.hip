@@ -402,6 +402,10 @@ __global__ void __launch_bounds__(256) k_offset_keys(const int32_t *__restrict__
     const int lane = threadIdx.x & 63;
     for (int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); o < NO; o += (int64_t)gridDim.x * 4) {
         int32_t k = (int32_t)npix;
+        if (!pix) {                 // keys given by the caller: the sort's values only
+            if (lane == 0) val[o] = (int32_t)o;
+            continue;
+        }
         for (int j0 = 0; j0 < L; j0 += 64) {
             const int j = j0 + lane;
             const int32_t p = j < L ? pix[o * L + j] : -1;
@@ -2124,6 +2128,13 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
                                            const uint8_t *keep, int64_t N, int32_t L, int64_t npix, int32_t nb,
                                            comap_destriper **out)
 {
+    return comap_destripe_create_keyed(ctx, pix, tod, w, keep, nullptr, 0, N, L, npix, nb, out);
+}
+
+extern "C" int comap_destripe_create_keyed(comap_ctx *ctx, const int32_t *pix, const double *tod, const double *w,
+                                           const uint8_t *keep, const int32_t *okey, int64_t okey_max, int64_t N,
+                                           int32_t L, int64_t npix, int32_t nb, comap_destriper **out)
+{
     if (!ctx || !pix || !tod || !w || !out) return -1;
     COMAP_DEVICE_GUARD(ctx);
     *out = nullptr;
@@ -2158,12 +2169,15 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     if (rc) return -2;
     int end_bit = 1;
     while ((1ll << end_bit) <= npix) ++end_bit;
+    if (okey && (okey_max < 1 || okey_max >= (1ll << 31))) return comap_fail(ctx, -1, "okey_max must be in [1, 2^31)");
+    int key_bit = 1;          // radix bits of the offset order keys (the caller's bound, or npix)
+    while ((1ll << key_bit) <= (okey ? okey_max - 1 : npix)) ++key_bit;
     // ---- scratch: sizes first (hipcub temp storage for the largest sort / scan), one allocation
     size_t sort_tb = 0, scan_tb = 0, scan32_tb = 0;
     (void)sort_pairs_i32(false, nullptr, sort_tb, nullptr, nullptr, nullptr, nullptr, N, end_bit, st);
     {
         size_t tb9 = 0;       // the spatial offset sort (NO pairs)
-        (void)sort_pairs_i32(true, nullptr, tb9, nullptr, nullptr, nullptr, nullptr, NO, end_bit, st);
+        (void)sort_pairs_i32(true, nullptr, tb9, nullptr, nullptr, nullptr, nullptr, NO, key_bit, st);
         sort_tb = std::max(sort_tb, tb9);
     }
     size_t sort64_tb = 0;   // the count form's transpose: (pixel, u64 offset|counts) pairs
@@ -2221,10 +2235,15 @@ extern "C" int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pix, c
     }
     // ---- 1. spatial processing order of the offsets
     if (spatial) {
-        k_offset_keys<<<(unsigned)std::min<int64_t>((NO + 3) / 4, 65536), 256, 0, st>>>(pix, NO, L, npix, ekey, eval);
+        // the caller's keys (comap_offset_centroid_keys: the centroid's internal pixel), or
+        // the first on-map pixel of each offset
+        k_offset_keys<<<(unsigned)std::min<int64_t>((NO + 3) / 4, 65536), 256, 0, st>>>(okey ? nullptr : pix, NO, L,
+                                                                                         npix, ekey, eval);
         COMAP_LAUNCH_CHECK(ctx);
         size_t tb = cub_tb;
-        COMAP_CHECK(ctx, sort_pairs_i32(true, cub_tmp, tb, ekey, ekey2, eval, d->perm, NO, end_bit, st));
+        // (the caller's keys may exceed npix -- a compacted problem keeps its tiled-layout
+        // keys -- so they sort on the bits of the caller's bound)
+        COMAP_CHECK(ctx, sort_pairs_i32(true, cub_tmp, tb, okey ? okey : ekey, ekey2, eval, d->perm, NO, key_bit, st));
     }
     // ---- 2. count pass (+ the count-form test: non-zero weights uniform per offset and band)
     COMAP_CHECK(ctx, hipMemsetAsync(nonuni, 0, 4, st));
@@ -2445,6 +2464,56 @@ __global__ void k_relabel_pixels(const int32_t *__restrict__ pix, int64_t n, con
     for (int64_t i = 4 * n4 + t0; i < n; i += stride) out[i] = relabel_one(pix[i], lut, npix, nt);
 }
 }  // namespace
+
+// key[o] = lut[round(mean y) nx + round(mean x)] over offset o's on-map samples
+// (0 <= p < nx ny, row-major ids), n_internal when it has none.  One wave per offset.
+__global__ void __launch_bounds__(256) k_offset_centroid_keys(const int32_t *__restrict__ pix, int64_t NO, int L,
+                                                              int64_t nx, int64_t ny, const int32_t *__restrict__ lut,
+                                                              int64_t n_internal, int32_t *__restrict__ key)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t npix = nx * ny;
+    for (int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); o < NO; o += (int64_t)gridDim.x * 4) {
+        int64_t sy = 0, sx = 0, c = 0;
+        for (int j = lane; j < L; j += 64) {
+            const int32_t p = pix[o * L + j];
+            if (p >= 0 && p < npix) {
+                sy += p / nx;
+                sx += p % nx;
+                c += 1;
+            }
+        }
+#pragma unroll
+        for (int sh = 32; sh > 0; sh >>= 1) {
+            sy += __shfl_xor(sy, sh, 64);
+            sx += __shfl_xor(sx, sh, 64);
+            c += __shfl_xor(c, sh, 64);
+        }
+        if (lane == 0) {
+            int32_t k = (int32_t)n_internal;
+            if (c > 0) {
+                const int64_t yi = (2 * sy + c) / (2 * c), xi = (2 * sx + c) / (2 * c);   // round half up
+                k = lut[yi * nx + xi];
+            }
+            key[o] = k;
+        }
+    }
+}
+
+extern "C" int comap_offset_centroid_keys(comap_ctx *ctx, const int32_t *pix, int64_t n, int32_t L, int64_t nx,
+                                          int64_t ny, const int32_t *lut, int64_t n_internal, int32_t *key)
+{
+    if (!ctx || L < 1 || n < 0 || n % L || nx < 1 || ny < 1 || n_internal < nx * ny || n_internal >= (1ll << 31) ||
+        (n > 0 && (!pix || !lut || !key)))
+        return -1;
+    COMAP_DEVICE_GUARD(ctx);
+    const int64_t NO = n / L;
+    if (NO == 0) return 0;
+    k_offset_centroid_keys<<<(unsigned)std::min<int64_t>((NO + 3) / 4, 65536), 256, 0, ctx->stream>>>(
+        pix, NO, L, nx, ny, lut, n_internal, key);
+    COMAP_LAUNCH_CHECK(ctx);
+    return 0;
+}
 
 extern "C" int comap_relabel_pixels(comap_ctx *ctx, const int32_t *pix, int64_t n, const int32_t *lut, int64_t npix,
                                     int64_t n_internal, int32_t *out)

@@ -267,7 +267,10 @@ class DeviceOps:
     N/L]) marks the offsets each band's data prep kept.  Per-band vectors are
     interleaved band-fastest ([N/L][nb], [npix][nb])."""
 
-    def __init__(self, pixels, tod, weights, offset_length, npix, device=None, keep=None):
+    def __init__(self, pixels, tod, weights, offset_length, npix, device=None, keep=None, okey=None):
+        """okey (optional): (int32 CUDA [N/L] keys, exclusive bound) -- the offsets' internal
+        processing order (comap_destripe_create_keyed); default: each offset's first on-map
+        pixel."""
         import torch
         self.torch = torch
         device = N.current_device() if device is None else int(device)
@@ -302,9 +305,13 @@ class DeviceOps:
         self.tod, self.w, self.keep = tod2.contiguous(), w2.contiguous(), kp
         h = ctypes.c_void_p()
         N.bind_stream(self.ctx, self.dev)
-        rc = N.lib().comap_destripe_create_bands(self.ctx, N.dptr(self.pix), N.dptr(self.tod), N.dptr(self.w),
-                                                 None if kp is None else N.dptr(kp), n, self.L, self.npix,
-                                                 self.nb, ctypes.byref(h))
+        keys, kmax = okey if okey is not None else (None, 0)
+        if keys is not None and (keys.numel() != n // self.L or keys.dtype != torch.int32):
+            raise ValueError('okey must be int32 [n_samples // offset_length]')
+        rc = N.lib().comap_destripe_create_keyed(self.ctx, N.dptr(self.pix), N.dptr(self.tod), N.dptr(self.w),
+                                                 None if kp is None else N.dptr(kp),
+                                                 None if keys is None else N.dptr(keys), int(kmax), n, self.L,
+                                                 self.npix, self.nb, ctypes.byref(h))
         if rc == -3:
             raise IndexError(f'pixel index out of range for a map of {npix} pixels (valid: -{npix} .. {npix - 1})')
         N.check(rc, self.ctx, 'comap_destripe_create_bands')
@@ -549,6 +556,8 @@ def tiled_layout(ny, nx, T, device):
     obs: 1 band 0.139 -> 0.124, 4 bands 0.295 -> 0.275 ms per CG iteration with T = 8,
     scripts/ds_tiling_probe.py, profiles/r05/r05c_py2.log)."""
     import torch
+    if T < 1 or T & (T - 1):
+        raise ValueError(f'tile size must be a power of two, not {T}')
     key = (int(ny), int(nx), int(T), str(device))
     if key in _LAYOUTS:
         return _LAYOUTS[key]
@@ -585,13 +594,17 @@ class DeviceDestriper:
         """map_shape (ny, nx): the map's row-major layout (CAR / WCS maps), when known; the
         operator then runs on a 2-D tiled internal pixel order (tiled_layout) and the maps
         come back in the caller's order."""
-        self.layout = None
+        self.layout, self.okey = None, None
         T = int(os.environ.get('COMAP_DS_TILE', str(TILE)))
+        if T > 0 and T & (T - 1):
+            # the Morton code inside a tile interleaves log2(T) bits: for another T it would
+            # exceed T * T - 1 and merge distinct pixels of neighbouring tiles
+            raise ValueError(f'COMAP_DS_TILE must be 0 (row-major) or a power of two, not {T}')
         if map_shape is not None and T > 0:
             ny, nx = (int(v) for v in map_shape)
             if ny * nx != int(npix):
                 raise ValueError(f'map_shape {map_shape} does not hold {npix} pixels')
-            pixels, npix = self._tile(pixels, int(npix), ny, nx, T, device)
+            pixels, npix = self._tile(pixels, int(npix), ny, nx, T, device, int(offset_length))
         self.npix_full, self.hit_index = int(npix), None
         self.multi = np.ndim(tod) == 2 if not hasattr(tod, 'dim') else tod.dim() == 2
         self.gathered, self.plan = None, None
@@ -602,7 +615,7 @@ class DeviceDestriper:
                 return
             if os.environ.get('COMAP_DS_COMPACT', '1') != '0':
                 pixels, npix = self._compact(pixels, int(npix), device)
-        self.ops = N.retry_oom(DeviceOps, pixels, tod, weights, offset_length, npix, device, keep)
+        self.ops = N.retry_oom(DeviceOps, pixels, tod, weights, offset_length, npix, device, keep, self.okey)
 
     # ---- rank policy
     def _choose_gather(self, d, pixels, tod, offset_length):
@@ -707,9 +720,13 @@ class DeviceDestriper:
         maps = {k: mp[i].to(dev) for i, k in enumerate(keys)}
         return x, it, maps, nb, nbands
 
-    def _tile(self, pixels, npix, ny, nx, T, device):
+    def _tile(self, pixels, npix, ny, nx, T, device, L):
         """Relabel the pixel ids onto tiled_layout; a negative id p (an unbinned sample that
-        reads m[npix + p]) becomes the negative id that reads the same pixel there."""
+        reads m[npix + p]) becomes the negative id that reads the same pixel there.  With
+        COMAP_DS_OKEY=centroid (default) the offsets are also ordered by their centroid
+        pixel's internal id (comap_offset_centroid_keys) instead of their first pixel: the
+        offsets crossing one pixel then sit close together, which is what the CG bin's x
+        gathers touch."""
         import torch
         dev = torch.device('cuda', N.current_device() if device is None else int(device))
         pix = pixels.to(device=dev, dtype=torch.int32).reshape(-1) if isinstance(pixels, torch.Tensor) else \
@@ -723,6 +740,12 @@ class DeviceDestriper:
         N.bind_stream(c, dev)
         N.check(N.lib().comap_relabel_pixels(c, N.dptr(pix), pix.numel(), N.dptr(ids), int(npix), int(nt),
                                              N.dptr(out)), c, 'comap_relabel_pixels')
+        if os.environ.get('COMAP_DS_OKEY', 'centroid') == 'centroid' and pix.numel() % L == 0:
+            keys = torch.empty(pix.numel() // L, dtype=torch.int32, device=dev)
+            N.check(N.lib().comap_offset_centroid_keys(c, N.dptr(pix), pix.numel(), int(L), int(nx), int(ny),
+                                                       N.dptr(ids), int(nt), N.dptr(keys)), c,
+                    'comap_offset_centroid_keys')
+            self.okey = (keys, int(nt) + 1)
         self.layout = ids
         return out, nt
 

@@ -34,6 +34,8 @@ import json
 import os
 from dataclasses import dataclass, field
 
+import numpy as np
+
 MEASURED = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'rankplan_measured.json')
 
 
@@ -88,8 +90,8 @@ class CostModel:
         t = self.a_us + self.b_us_per_msample[nb] * n_samples / 1e6 / n
         if n > 1:
             # alpha + bytes / beta per all-reduce (the probe's fit already holds the ring's
-            # 2 (n - 1) / n factor in beta when measured)
-            ring = 1.0 if self.measured(n) else 2 * (n - 1) / n
+            # 2 (n - 1) / n factor in a MEASURED beta; the assumed bus bandwidth does not)
+            ring = 1.0 if n in self.beta_measured else 2 * (n - 1) / n
             t += 3 * self.alpha_us(n) + map_bytes * ring / (self.beta(n) * 1e3)
         return t
 
@@ -118,3 +120,41 @@ def plan(n_samples, nb, world, n_hit_pixels=31_000, iters=25, model=None):
     mode = 'gather' if world > 1 and t_gather < t_shard else 'shard'
     return {'mode': mode, 'shard_ms': t_shard, 'gather_ms': t_gather, 'iters': iters,
             'iter_us_by_ranks': per_iter}
+
+
+# ---------------------------------------------------------------- work-balanced splits
+# A sharded CG iteration waits for its slowest rank, and a rank's operator time follows its
+# sparse operator's entries -- the distinct (offset, pixel) pairs of its samples -- not its
+# sample count: a slow scan crosses fewer pixels per offset.  The reference splits the file
+# list into equal counts (run_destriper.py:131-138); the map it solves is the same whichever
+# rank holds a file, so the files can be dealt by work instead.
+
+
+def offset_pixel_runs(pix, offset_length, groups=1):
+    """Per group (``pix`` holds ``groups`` equal contiguous blocks of whole offsets, e.g. one
+    per observation): the number of (offset, pixel run) pairs -- 1 + the pixel changes
+    inside each offset.  That is the operator's entry count when no offset revisits a
+    pixel after leaving it (a scan track moves on), and an upper bound otherwise.  NumPy
+    or torch input (any device); returns int64 NumPy [groups]."""
+    L = int(offset_length)
+    if type(pix).__module__.startswith('torch'):                    # a torch tensor (any device)
+        p = pix.reshape(int(groups), -1, L)
+        runs = (p[:, :, 1:] != p[:, :, :-1]).sum(dim=(1, 2)) + p.shape[1]
+        return runs.cpu().numpy().astype(np.int64)
+    p = np.asarray(pix).reshape(int(groups), -1, L)
+    return ((p[:, :, 1:] != p[:, :, :-1]).sum(axis=(1, 2)) + p.shape[1]).astype(np.int64)
+
+
+def balanced_ranges(weights, world):
+    """Contiguous [(lo, hi)] index ranges, one per rank, minimising the largest rank's total
+    weight (the optimal contiguous partition of pipeline/sharding.partition_units); the
+    concatenation in rank order keeps the caller's order."""
+    from ..pipeline.sharding import partition_units
+    return partition_units(np.asarray(weights, dtype=np.int64), int(world))
+
+
+def imbalance(weights, ranges):
+    """max / mean of the ranks' total weights."""
+    w = np.asarray(weights, dtype=np.float64)
+    tot = np.array([w[a:b].sum() for a, b in ranges])
+    return float(tot.max() / max(tot.mean(), 1e-300))

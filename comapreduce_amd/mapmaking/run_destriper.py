@@ -81,6 +81,46 @@ def _healpix_edges(pointing):
     return np.arange(mx + 1, dtype=int)
 
 
+def _file_work(f, offset_length, feeds, map_info, healpix):
+    """The CG work one file brings a rank: its operator entries -- the (offset, pixel run)
+    pairs of its scan pointing (rankplan.offset_pixel_runs) -- plus FILE_KAPPA x its offsets
+    (per-offset CG vector work in entries-equivalent units, as bench.py's field split)."""
+    from . import rankplan
+    fi, _ = COMAPData.GetFeeds(f['spectrometer/feeds'], feeds)
+    datasize = int(COMAPData.countDataSize(f, len(fi), offset_length)['datasize'])
+    if datasize == 0 or len(fi) == 0:
+        return 0
+    read = COMAPData.read_pixels_healpix if healpix else COMAPData.read_pixels
+    pix = np.asarray(read(f, datasize, offset_length, feeds, map_info))[:len(fi), :datasize]
+    entries = int(rankplan.offset_pixel_runs(pix.astype(np.int64), offset_length, groups=pix.shape[0]).sum())
+    return entries + int(FILE_KAPPA * pix.size // offset_length)
+
+
+FILE_KAPPA = 6.5
+
+
+def _rank_files(filelist, rank, size, offset_length, feeds, map_info, healpix, open_file):
+    """This rank's files.  The mapped set is the reference's: the first (len // size) x size
+    files (run_destriper.py:131-138 drops the remainder); the reference then deals them in
+    equal counts.  Here (COMAP_DS_SPLIT=work, the default) they are dealt in contiguous
+    ranges balanced on each file's CG work (_file_work; every rank weighs its own
+    equal-count share, the weights are all-gathered): a sharded CG iteration waits for its
+    slowest rank, whose time follows its operator entries, not its file count.  The maps do
+    not depend on which rank holds a file.  COMAP_DS_SPLIT=count: the reference's split."""
+    step = filelist.size // size
+    lo, hi = step * rank, min(step * (rank + 1), filelist.size)
+    if size == 1 or step == 0 or os.environ.get('COMAP_DS_SPLIT', 'work') == 'count':
+        return filelist[lo:hi]
+    import torch.distributed as dist
+    from . import rankplan
+    mine = [_file_work(open_file(f), offset_length, feeds, map_info, healpix) for f in filelist[lo:hi]]
+    parts = [None] * size
+    dist.all_gather_object(parts, mine)
+    weights = [w for p in parts for w in p]
+    a, b = rankplan.balanced_ranges(weights, size)[rank]
+    return filelist[:step * size][a:b]
+
+
 def main(filelistname, offset_length=50, feed_weights=None, prefix='fg9', output_dir='maps/fg9/', obsid_cuts=[],
          feeds=[1, 2, 3, 5, 6, 9, 11, 12, 13, 14, 15, 16, 17, 18, 19], nxpix=480, nypix=480,
          crval=['05:32:00.3', '+12:30:28.0'], crpix=[240, 240], ctype=['RA---CAR', 'DEC--CAR'],
@@ -111,9 +151,7 @@ def main(filelistname, offset_length=50, feed_weights=None, prefix='fg9', output
     if isinstance(crval[0], str):
         crval = [sex2deg(c, hours=hr) for c, hr in zip(crval, [True, False])]
     map_info = COMAPData.map_info_from(crval, cdelt, crpix, ctype, nxpix, nypix)
-    step = filelist.size // size
-    lo, hi = step * rank, min(step * (rank + 1), filelist.size)
-    filelist = filelist[lo:hi]
+    filelist = _rank_files(filelist, rank, size, offset_length, feeds, map_info, healpix, open_file)
     if source in CALIBRATORS:
         offset_length = 250
         threshold = 1

@@ -326,9 +326,44 @@ def level2_mapmaking(obs_id: int, n_feeds: int = 19, n_samples: int = 45_000, sk
 C5_AMP_DEG = 3.8      # C5 Lissajous half-width: inside the 480 x 1' map's +-4.0 deg (every sample on-map)
 
 
+def _field_track(o, n_feeds, n, nx, ny, cdelt, dev, amp):
+    """Observation o's Lissajous track of destriper_inputs_device: ra / dec offsets (deg) and
+    the CAR pixel ids (int32, off-map -1) of its n_feeds x n samples, on device ``dev``."""
+    import math
+    import torch
+    t = torch.arange(n, device=dev, dtype=torch.float64)[None, :]
+    k = torch.arange(o * n_feeds, (o + 1) * n_feeds, device=dev, dtype=torch.float64)[:, None]
+    ra = amp * torch.sin(2 * math.pi * t / (1250.0 + 7.0 * k) + 0.37 * k)       # degrees from the field centre
+    dec = amp * torch.sin(2 * math.pi * t / (1700.0 + 5.0 * k) + 1.1 * k)
+    px = torch.floor(-ra / cdelt + (nx / 2 - 1) + 0.5)
+    py = torch.floor(dec / cdelt + (ny / 2 - 1) + 0.5)
+    ok = (px >= 0) & (px <= nx - 1) & (py >= 0) & (py <= ny - 1)
+    pix = torch.where(ok, py * nx + px, torch.full_like(px, -1)).to(torch.int32)
+    return ra, dec, pix
+
+
+def field_series_work(n_obs: int, n_feeds: int = 19, n_samples: int = 180_000, offset_length: int = 50,
+                      nx: int = 480, ny: int = 480, cdelt: float = 1.0 / 60.0, device='cpu', amp: float = C5_AMP_DEG):
+    """Per (obs, feed) series of destriper_inputs_device's field (series s = obs * n_feeds +
+    feed): the (offset, pixel run) pairs of its pointing (rankplan.offset_pixel_runs), i.e.
+    the sparse-operator entries a rank holding it takes on, and its offsets.  The track's
+    scan periods grow with the series index (1250 + 7 s samples), so later series cross
+    fewer pixels per offset.  Pointing only (no tod / noise); ``device``: 'cpu' or a CUDA
+    index.  Returns (entries int64 [n_obs * n_feeds], offsets per series)."""
+    import torch
+    from .mapmaking.rankplan import offset_pixel_runs
+    dev = torch.device(device) if isinstance(device, str) else torch.device('cuda', int(device))
+    n = n_samples // offset_length * offset_length
+    out = np.zeros(n_obs * n_feeds, dtype=np.int64)
+    for o in range(n_obs):
+        pix = _field_track(o, n_feeds, n, nx, ny, cdelt, dev, amp)[2]
+        out[o * n_feeds:(o + 1) * n_feeds] = offset_pixel_runs(pix, offset_length, groups=n_feeds)
+    return out, n // offset_length
+
+
 def destriper_inputs_device(n_obs: int, n_feeds: int = 19, n_samples: int = 180_000, offset_length: int = 50,
                             nx: int = 480, ny: int = 480, cdelt: float = 1.0 / 60.0, device: int = 0, seed: int = 0,
-                            n_bands: int = 1, amp: float = C5_AMP_DEG, obs0: int = 0):
+                            n_bands: int = 1, amp: float = C5_AMP_DEG, obs0: int = 0, series=None):
     """Destriper inputs at the SURVEY.md §8(d) C5 scale, generated on the device
     (bench only): observations obs0 .. obs0 + n_obs - 1 of a field, each n_feeds feeds x
     n_samples samples, every (obs, feed) series cut to a multiple of offset_length;
@@ -339,6 +374,9 @@ def destriper_inputs_device(n_obs: int, n_feeds: int = 19, n_samples: int = 180_
     and pointing, independent offsets and noise per band).  Every observation is drawn
     from its own generator, so a rank generating observations [obs0, obs0 + n) of a
     field gets exactly those observations' samples of the whole field.
+    ``series`` = (lo, hi): instead the (obs, feed) series lo .. hi - 1 of the field (series
+    s = obs * n_feeds + feed; n_obs / obs0 ignored) -- the same samples as in the whole
+    field, for a rank holding a work-balanced range of series (bench.py's field leg).
 
     The default half-width (3.8 deg on the +-4.0 deg map) keeps every sample on the
     map.  Rounds 2-4 drew 4.2 deg: ~37 % of the samples then fell off the map and, as
@@ -348,40 +386,35 @@ def destriper_inputs_device(n_obs: int, n_feeds: int = 19, n_samples: int = 180_
     import torch
     if n_bands > 1:
         pix, t0, w0 = destriper_inputs_device(n_obs, n_feeds, n_samples, offset_length, nx, ny, cdelt, device, seed,
-                                              amp=amp, obs0=obs0)
+                                              amp=amp, obs0=obs0, series=series)
         tods = torch.empty((n_bands,) + tuple(t0.shape), dtype=torch.float64, device=t0.device)
         ws = torch.empty_like(tods)
         tods[0], ws[0] = t0, w0
         del t0, w0
         for b in range(1, n_bands):
             _, tods[b], ws[b] = destriper_inputs_device(n_obs, n_feeds, n_samples, offset_length, nx, ny, cdelt,
-                                                        device, seed + 7919 * b, amp=amp, obs0=obs0)
+                                                        device, seed + 7919 * b, amp=amp, obs0=obs0, series=series)
         return pix, tods, ws
-    import math
     dev = torch.device('cuda', device)
     n = n_samples // offset_length * offset_length
     no = n // offset_length
-    S = n_obs * n_feeds
+    s_lo, s_hi = (obs0 * n_feeds, (obs0 + n_obs) * n_feeds) if series is None else (int(series[0]), int(series[1]))
+    S = s_hi - s_lo
     pix = torch.empty((S, n), dtype=torch.int32, device=dev)
     tod = torch.empty((S, n), dtype=torch.float64, device=dev)
     w = torch.empty((S, n), dtype=torch.float64, device=dev)
-    t = torch.arange(n, device=dev, dtype=torch.float64)[None, :]
     g = torch.Generator(device=dev)
-    for j, o in enumerate(range(obs0, obs0 + n_obs)):
+    for o in range(s_lo // n_feeds, (s_hi + n_feeds - 1) // n_feeds):
         g.manual_seed(int(seed) * 1_000_003 + o)
-        rows = slice(j * n_feeds, (j + 1) * n_feeds)
-        k = torch.arange(o * n_feeds, (o + 1) * n_feeds, device=dev, dtype=torch.float64)[:, None]
-        ra = amp * torch.sin(2 * math.pi * t / (1250.0 + 7.0 * k) + 0.37 * k)       # degrees from the field centre
-        dec = amp * torch.sin(2 * math.pi * t / (1700.0 + 5.0 * k) + 1.1 * k)
-        px = torch.floor(-ra / cdelt + (nx / 2 - 1) + 0.5)
-        py = torch.floor(dec / cdelt + (ny / 2 - 1) + 0.5)
-        ok = (px >= 0) & (px <= nx - 1) & (py >= 0) & (py <= ny - 1)
-        pix[rows] = torch.where(ok, py * nx + px, torch.full_like(px, -1)).to(torch.int32)
+        a, b = max(s_lo, o * n_feeds), min(s_hi, (o + 1) * n_feeds)      # this observation's rows in range
+        keep, rows = slice(a - o * n_feeds, b - o * n_feeds), slice(a - s_lo, b - s_lo)
+        ra, dec, p = _field_track(o, n_feeds, n, nx, ny, cdelt, dev, amp)
         sky = 0.05 * torch.sin(2.1 * ra) * torch.cos(1.7 * dec)
         steps = torch.randn((n_feeds, no), generator=g, device=dev, dtype=torch.float64) * 2e-3
         sky += torch.cumsum(steps, dim=1).repeat_interleave(offset_length, dim=1)
         sigma = 4e-3 + 2e-3 * torch.rand((n_feeds, 1), generator=g, device=dev, dtype=torch.float64)
         sky += sigma * torch.randn((n_feeds, n), generator=g, device=dev, dtype=torch.float64)
-        tod[rows] = sky
-        w[rows] = 1.0 / sigma ** 2
+        pix[rows] = p[keep]
+        tod[rows] = sky[keep]
+        w[rows] = (1.0 / sigma ** 2)[keep]
     return pix.reshape(-1), tod.reshape(-1), w.reshape(-1)

@@ -239,6 +239,13 @@ int comap_destripe_create(comap_ctx *ctx, const int32_t *pixels_dev, const doubl
 int comap_destripe_create_bands(comap_ctx *ctx, const int32_t *pixels_dev, const double *tod_dev,
                                 const double *weights_dev, const uint8_t *keep_dev, int64_t n_samples,
                                 int32_t offset_length, int64_t npix, int32_t n_bands, comap_destriper **out);
+/* comap_destripe_create_bands with the offsets' internal processing order given by the
+ * caller: okey_dev int32 [N/L] with keys in [0, okey_max), the offsets sorted by it
+ * (stable).  okey_dev NULL: the first on-map pixel of each offset (okey_max unused). */
+int comap_destripe_create_keyed(comap_ctx *ctx, const int32_t *pixels_dev, const double *tod_dev,
+                                const double *weights_dev, const uint8_t *keep_dev, const int32_t *okey_dev,
+                                int64_t okey_max, int64_t n_samples, int32_t offset_length, int64_t npix,
+                                int32_t n_bands, comap_destriper **out);
 int comap_destripe_destroy(comap_destriper *d);
 int64_t comap_destripe_n_offsets(const comap_destriper *d);
 int32_t comap_destripe_n_bands(const comap_destriper *d);
@@ -330,6 +337,12 @@ int comap_destripe_solve(comap_destriper *d, double threshold, int32_t niter, do
  * reads the same pixel of the internal map), n_internal for any other id (the set-up's
  * range check then rejects it, as it would the original).  Device pointers; one pass,
  * no host sync (replaces Destriper.py's row-major m[pointing] indexing order only). */
+/* Offset order keys for a row-major nx x ny map: key_dev[o] = lut[round(mean y) nx +
+ * round(mean x)] over offset o's samples with 0 <= p < nx ny (the internal id of the
+ * offset's centroid pixel), n_internal for an offset with none.  The offsets crossing a
+ * pixel then sit near each other in the internal order (the CG bin's x gathers). */
+int comap_offset_centroid_keys(comap_ctx *ctx, const int32_t *pix_dev, int64_t n, int32_t offset_length, int64_t nx,
+                               int64_t ny, const int32_t *lut_dev, int64_t n_internal, int32_t *key_dev);
 int comap_relabel_pixels(comap_ctx *ctx, const int32_t *pix_dev, int64_t n, const int32_t *lut_dev, int64_t npix,
                          int64_t n_internal, int32_t *out_dev);
 

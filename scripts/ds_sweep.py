@@ -13,12 +13,15 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 SETTINGS = [
     {},
-    {'COMAP_DS_TILES': '1'},
-    {'COMAP_DS_TILES': '1', 'COMAP_DS_PB': '1024'},
+    {'COMAP_DS_OKEY': 'first'},                  # offsets ordered by their first pixel (rounds 2-5)
+    {'COMAP_DS_TILE': '0'},                      # row-major internal pixel order
+    {'COMAP_DS_TILE': '16'},
+    {'COMAP_DS_PB': '1024'},
     {'COMAP_DS_SELL': '0'},
 ]
-KEYS = ('COMAP_DS_PG', 'COMAP_DS_PU', 'COMAP_DS_PB', 'COMAP_DS_BU', 'COMAP_DS_BL', 'COMAP_DS_SELL', 'COMAP_DS_SU',
-        'COMAP_DS_PXCD', 'COMAP_DS_BXCD', 'COMAP_DS_NT', 'COMAP_DS_SPRE', 'COMAP_DS_PPAIR', 'COMAP_DS_BPAIR', 'COMAP_DS_TILES')
+# knobs the current kernels read (the removed variants' knobs are gone with them)
+KEYS = ('COMAP_DS_PG', 'COMAP_DS_PU', 'COMAP_DS_PB', 'COMAP_DS_BU', 'COMAP_DS_BL', 'COMAP_DS_SELL', 'COMAP_DS_TILE',
+        'COMAP_DS_OKEY')
 
 
 def main():
@@ -35,7 +38,13 @@ def main():
             for k in KEYS:
                 os.environ.pop(k, None)
             os.environ.update(st)
-            prob = D.DeviceDestriper(pix, tod, w, 50, 480 * 480, device=0, map_shape=(480, 480))
+            setup = None
+            for _ in range(2):           # the second build is timed (the first warms the caches)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                prob = D.DeviceDestriper(pix, tod, w, 50, 480 * 480, device=0, map_shape=(480, 480))
+                torch.cuda.synchronize()
+                setup = (time.perf_counter() - t0) * 1e3
             prob.solve(threshold=0.0, niter=3)
             best = None
             for _ in range(2):
@@ -46,7 +55,7 @@ def main():
                 dt = (time.perf_counter() - t0) / iters * 1e3
                 best = dt if best is None else min(best, dt)
             x = res['x']
-            print(json.dumps({'bands': nb, 'setting': st, 'ms_per_iter': best,
+            print(json.dumps({'bands': nb, 'setting': st, 'ms_per_iter': best, 'setup_ms': setup,
                               'x_sum': float(x.double().sum()), 'x_abs': float(x.double().abs().sum())}), flush=True)
             del prob, res
         for k in KEYS:

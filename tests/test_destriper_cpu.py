@@ -161,3 +161,27 @@ def test_compacted_map_allreduce_two_ranks_gloo(problem, wrap):
         assert np.array_equal(idx, read) and np.all(np.diff(idx) > 0)
         assert idx.size < 0.3 * big * big
         assert itc == itu and np.array_equal(xc, xu) and np.array_equal(mc, mu), rank
+
+
+def test_tiled_layout_is_a_permutation():
+    """tiled_layout's internal ids (T x T tiles, Morton order inside) are distinct and
+    below the padded size for power-of-two tiles on ragged maps; any other T is refused
+    (its Morton code would exceed T*T - 1 and merge pixels of neighbouring tiles)."""
+    import torch
+    from comapreduce_amd.mapmaking.destriper import tiled_layout
+    for ny, nx in ((480, 480), (37, 53), (1, 9)):
+        for T in (1, 2, 8, 16):
+            ids, nt = tiled_layout(ny, nx, T, torch.device('cpu'))
+            assert ids.unique().numel() == ny * nx and int(ids.max()) < nt and int(ids.min()) >= 0, (ny, nx, T)
+    for T in (3, 12):
+        with pytest.raises(ValueError):
+            tiled_layout(48, 48, T, torch.device('cpu'))
+
+
+def test_device_destriper_rejects_non_power_of_two_tile(monkeypatch):
+    """COMAP_DS_TILE must be 0 or a power of two: checked before any device
+    work."""
+    from comapreduce_amd.mapmaking.destriper import DeviceDestriper
+    monkeypatch.setenv('COMAP_DS_TILE', '12')
+    with pytest.raises(ValueError, match='power of two'):
+        DeviceDestriper(np.zeros(100, np.int32), np.zeros(100), np.ones(100), 50, 16, map_shape=(4, 4))

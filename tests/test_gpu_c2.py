@@ -342,9 +342,13 @@ def _c5_shard_rank(rank, world, port, q):
     torch.cuda.set_device(0)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     L, npix = 50, 480 * 480
+    import bench
     pix, tod, w = synthetic.destriper_inputs_device(8, offset_length=L, device=0, seed=1000, n_bands=4)
-    n = pix.numel()
-    lo, hi = n * rank // world, n * (rank + 1) // world        # 4 observations x 19 feeds each
+    # bench.py's work-balanced split of the (obs, feed) series (uneven: the early
+    # observations scan faster and hold more entries per sample)
+    ranges, _, _ = bench.field_split(8, world, device=0)
+    ns = pix.numel() // (8 * 19)
+    lo, hi = ranges[rank][0] * ns, ranges[rank][1] * ns
     prob = DeviceDestriper(pix[lo:hi].contiguous(), tod[:, lo:hi].contiguous(), w[:, lo:hi].contiguous(), L, npix,
                            device=0)
     res = prob.solve(threshold=1e-6, niter=100)
@@ -356,8 +360,8 @@ def _c5_shard_rank(rank, world, port, q):
 
 def test_c5_two_ranks_sharded_field_scale():
     """The sharded multi-rank solve at field scale (C5 per-GPU size: 8 obs x 19 feeds x
-    180k samples, 4 bands, 547k offsets, 480x480 CAR), split 4 + 4 observations over 2
-    gloo ranks sharing cuda:0 (Destriper.py:61-82, 183-204: partial maps and CG sums
+    180k samples, 4 bands, 547k offsets, 480x480 CAR), its (obs, feed) series split over 2
+    gloo ranks sharing cuda:0 by bench.field_split's work balance (not 4 + 4 observations) (Destriper.py:61-82, 183-204: partial maps and CG sums
     over ranks), solved to the reference's stopping rule (threshold 1e-6, <= 100
     iterations).  Offsets and maps <= 1e-9 of the single-rank solve, hits bit-exact,
     equal iteration counts; the compacted union is exactly the hit pixels, which on the

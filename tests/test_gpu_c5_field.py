@@ -20,7 +20,8 @@ def rel(a, b):
 
 @pytest.fixture(scope='module')
 def field_band0():
-    """The field's band 0: device solve (3 CG iterations, threshold 0) and its inputs on
+    """The field's band 0: device solves (3 CG iterations at threshold 0, and converged at
+    the reference's stopping rule, threshold 1e-6 / <= 100 iterations) and its inputs on
     the host."""
     import torch
     from comapreduce_amd import synthetic
@@ -30,10 +31,13 @@ def field_band0():
     dd = DeviceDestriper(pix, tod, w, L, NPIX, device=0)
     nnz = dd.nnz()
     res = dd.solve(threshold=0.0, niter=3)
+    conv = dd.solve(threshold=1e-6, niter=100)
     out = {'x': res['x'].cpu().numpy(), 'iters': res['iters'], 'nnz': nnz,
            'maps': {k: v.cpu().numpy() for k, v in res['maps'].items()},
+           'conv_x': conv['x'].cpu().numpy(), 'conv_iters': conv['iters'],
+           'conv_maps': {k: v.cpu().numpy() for k, v in conv['maps'].items()},
            'p': pix.cpu().numpy(), 't': tod.cpu().numpy(), 'w': w.cpu().numpy()}
-    del dd, res, pix, tod, w
+    del dd, res, conv, pix, tod, w
     torch.cuda.empty_cache()
     return out
 
@@ -56,12 +60,31 @@ def test_c5_field_64obs_one_band_vs_oracle(field_band0):
     assert rel(f['x'], xr) < 1e-5
 
 
+def test_c5_field_64obs_converged_vs_oracle(field_band0):
+    """Band 0 of the 64-observation field (218.9 M samples, 4.38 M offsets) solved to the
+    reference's stopping rule -- threshold 1e-6, at most 100 iterations (Destriper.py:85-152,
+    402-453) -- on the device and by oracle/destriper.destriper_iteration on the host: equal
+    iteration counts, weight / hits / naive bit-exact, map and offsets <= 1e-5."""
+    import oracle.destriper as od
+    f = field_band0
+    ref, xr, itr = od.destriper_iteration(f['p'].astype(np.int64), f['t'], f['w'], L, NPIX, threshold=1e-6,
+                                          niter=100)
+    assert 1 < itr < 100, itr                       # stopped by the threshold
+    assert f['conv_iters'] == itr, (f['conv_iters'], itr)
+    for k in ('weight', 'hits', 'naive'):
+        assert np.array_equal(f['conv_maps'][k], ref[k]), k
+    assert rel(f['conv_maps']['map'], ref['map']) < 1e-5
+    assert rel(f['conv_x'], xr) < 1e-5
+
+
 def test_c5_field_64obs_four_bands_converged(field_band0):
     """All 4 sidebands of the field as one batched system, solved to the reference's
     stopping rule (threshold 1e-6, <= 100 iterations): every band converges by the
     threshold; band 0 (the same pointing, tod and weights as the 1-band problem) has
-    bit-identical weight / hits / naive maps and its first 3 iterations reproduce the
-    1-band solve; maps finite on the hit pixels."""
+    bit-identical weight / hits / naive maps, its first 3 iterations reproduce the 1-band
+    solve and its converged solve takes the 1-band solve's iterations (which the
+    converged oracle test pins) with the same map and offsets; maps finite on the hit
+    pixels."""
     import torch
     from comapreduce_amd import synthetic
     from comapreduce_amd.mapmaking.destriper import DeviceDestriper
@@ -75,6 +98,7 @@ def test_c5_field_64obs_four_bands_converged(field_band0):
     del r3
     res = dd.solve(threshold=1e-6, niter=100)
     its = res['iters']
+    x0 = res['x'][0].cpu().numpy()
     maps = {k: v.cpu().numpy() for k, v in res['maps'].items()}
     del dd, res
     torch.cuda.empty_cache()
@@ -83,6 +107,8 @@ def test_c5_field_64obs_four_bands_converged(field_band0):
     for k in ('weight', 'hits', 'naive'):
         assert np.array_equal(maps[k][0], f['maps'][k]), k
     assert rel(x3, f['x']) < 1e-9 and rel(m3, f['maps']['map']) < 1e-9
+    assert its[0] == f['conv_iters']
+    assert rel(x0, f['conv_x']) < 1e-9 and rel(maps['map'][0], f['conv_maps']['map']) < 1e-9
     for b in range(4):
         hit = maps['hits'][b] > 0
         assert maps['hits'][b].sum() == N_FIELD

@@ -150,3 +150,58 @@ def test_run_destriper_main_healpix(tmp_path, batch):
         assert np.array_equal(rec['PIXEL'], remap)
         assert np.array_equal(rec['TEMPERATURE'], got['map'], equal_nan=True)
         assert np.array_equal(rec['Q_POLARISATION'], got['naive'], equal_nan=True)
+
+
+def _rank_files_worker(rank, world, port, q):
+    import os
+    import sys
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden'))
+    import comapdata_case as cc
+    from comapreduce_amd.mapmaking import comapdata as C
+    from comapreduce_amd.mapmaking.run_destriper import _rank_files
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    store, names = cc.store()
+    m = cc.CASES['car']['map']
+    mi = C.map_info_from(m['crval'], m['cdelt'], m['crpix'], m['ctype'], m['nxpix'], m['nypix'])
+    files = _rank_files(np.array(names), rank, world, 50, cc.FEEDS, mi, False, C._opener(store))
+    q.put((rank, [str(f) for f in files]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_rank_files_balanced_on_work():
+    """run_destriper's file split on 2 gloo ranks: the mapped set stays the reference's
+    (the first len // size x size files, run_destriper.py:131-138), dealt in contiguous
+    ranges that minimise the largest rank's CG work (operator entries + offsets, weighed
+    from each file's pointing) instead of equal counts."""
+    import os
+    import sys
+    import torch.multiprocessing as mp
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden'))
+    import comapdata_case as cc
+    from comapreduce_amd.mapmaking import comapdata as C
+    from comapreduce_amd.mapmaking import rankplan
+    from comapreduce_amd.mapmaking.run_destriper import _file_work
+    store, names = cc.store()
+    m = cc.CASES['car']['map']
+    mi = C.map_info_from(m['crval'], m['cdelt'], m['crpix'], m['ctype'], m['nxpix'], m['nypix'])
+    opener = C._opener(store)
+    weights = [_file_work(opener(f), 50, cc.FEEDS, mi, False) for f in names[:2]]
+    assert all(w > 0 for w in weights)
+    want = rankplan.balanced_ranges(weights, 2)
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = 29400 + os.getpid() % 190
+    procs = [ctx.Process(target=_rank_files_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    assert res[0] + res[1] == list(names[:2])            # the reference's mapped set, in order
+    for r in range(2):
+        a, b = want[r]
+        assert res[r] == list(names[a:b]), r

@@ -57,3 +57,44 @@ def test_measured_alpha_beta_replace_the_assumptions(tmp_path):
             __import__('os').remove(out)
         else:
             open(out, 'w').write(saved)
+
+
+@pytest.fixture(scope='module')
+def field_work():
+    """Per-series work of bench.py's configs[4] field (64 obs x 19 feeds), from the
+    pointing alone (CPU)."""
+    import torch
+    from comapreduce_amd import synthetic
+    torch.set_num_threads(min(8, torch.get_num_threads()))
+    return synthetic.field_series_work(64, device='cpu')
+
+
+def test_field_work_counts_the_operator_entries(field_work):
+    """The (offset, pixel run) pairs of the field's pointing are its operator entries up to
+    the few offsets that revisit a pixel: 86,704,202 entries on one GPU (bench r05,
+    destriper_c5_field nnz)."""
+    ent, no = field_work
+    assert ent.size == 64 * 19 and no == 3600
+    assert 0 <= ent.sum() - 86_704_202 < 1000
+
+
+def test_field_split_balances_work(field_work, monkeypatch):
+    """bench.field_split deals the field's (obs, feed) series to 2 / 4 / 8 ranks in
+    contiguous ranges balanced on CG work (entries + FIELD_KAPPA x offsets): the slowest
+    rank's modelled work is within 2 % of the mean, and its entries within 15 %; equal
+    observation counts (run_destriper.py:131-138, rounds 2-5) gave rank 0 1.32 / 1.63 /
+    1.86 x the mean entries.  The ranges cover every series once, in order."""
+    import numpy as np
+    import bench
+    ent, no = field_work
+    w = ent + bench.FIELD_KAPPA * no
+    for world, obs_imb in ((2, 1.32), (4, 1.63), (8, 1.86)):
+        monkeypatch.setenv('COMAP_FIELD_SPLIT', 'obs')
+        eq, _, _ = bench.field_split(64, world)
+        assert rankplan.imbalance(ent, eq) == pytest.approx(obs_imb, abs=0.01)
+        monkeypatch.delenv('COMAP_FIELD_SPLIT')
+        r, _, _ = bench.field_split(64, world)
+        assert r[0][0] == 0 and r[-1][1] == ent.size and all(a[1] == b[0] for a, b in zip(r, r[1:]))
+        assert rankplan.imbalance(w, r) < 1.02, world
+        assert rankplan.imbalance(ent, r) < 1.15, world
+        assert np.all(np.diff([a for a, _ in r]) > 0)
