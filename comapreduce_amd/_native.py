@@ -94,6 +94,7 @@ _SIGS = {
     'comap_destripe_cg_direction': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     'comap_destripe_div_map': (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     'comap_relabel_pixels': (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_void_p]),
+    'comap_relabel_pixels_tiled': (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int32, c_void_p]),
     'comap_destripe_solve': (c_int, [c_void_p, c_double, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
                                      c_void_p, P_int32]),
     'comap_prep_auto_rms': (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int32, c_int64, c_void_p]),

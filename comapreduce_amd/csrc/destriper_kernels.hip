@@ -1167,10 +1167,14 @@ __device__ __forceinline__ int select_bit(uint64_t x, int r)
 // offset), and its (w, tod w) per band into LDS.  tod w comes from the count pass's
 // sample-major copy (ptw, one 8 NB-byte read); w is the offset's weight wb when all the
 // group's members have a non-zero weight in the band (count form: they all equal wb), 0
-// when none has, and only a mixed group reads w itself.  Then 3 NB lanes run the ordered
-// sums exactly as k_sample_walk does over the sorted samples.  Samples of groups without
+// when none has, and only a mixed group reads w itself.  Then 2 NB lanes run the ordered
+// sums of h and the naive numerator exactly as k_sample_walk does over the sorted samples.  Samples of groups without
 // an entry carry zero weights (they add nothing to h or to the naive numerator); their
 // hits come from the count pass's integer adds.
+//
+// The hits per band are integer counts (each kept member adds 1): they are summed as
+// integers per entry instead of a third LDS column -- the same bits (exact below 2^53), a
+// third less LDS per slot and 2 NB serial chains instead of 3 NB.
 template <int NB, int K, int M>
 __global__ void __launch_bounds__(256) k_sample_walk2(const int32_t *__restrict__ hrow,
                                                       const int64_t *__restrict__ hprow,
@@ -1188,21 +1192,27 @@ __global__ void __launch_bounds__(256) k_sample_walk2(const int32_t *__restrict_
 {
 #pragma clang fp contract(off)
     constexpr int CAP = 64 * M;
-    // per member slot, 3 NB doubles: w, tod w and 1 per band, each 0 where the band does not
+    // per member slot, 2 NB doubles: w and tod w per band, each 0 where the band does not
     // keep the member's offset -- adding +0 leaves a sum that never holds -0 unchanged, so
-    // lane l < 3 NB runs its ordered sum as one unconditional chain over column l
-    __shared__ double spl[4][CAP * 3 * NB];
+    // lane l < 2 NB runs its ordered sum as one unconditional chain over column l.  Slots are
+    // SW doubles apart, SW odd: the 16 lanes of a ds_write_b64 group then hit distinct bank
+    // pairs (an even stride would share bank pairs between lanes: multi-way conflicts)
+    constexpr int SW = (2 * NB) | 1;
+    __shared__ double spl[4][CAP * SW];
     __shared__ uint8_t sfl[4][CAP];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     double *pl = spl[wv];
     uint8_t *fl = sfl[wv];
-    const int kind = lane / NB, b = lane % NB;     // this lane's ordered sum (lanes < 3 NB)
+    const int kind = lane / NB, b = lane % NB;     // this lane's ordered sum (lanes < 2 NB)
     // the non-empty rows only (k_hit_flags wrote the empty ones): row i of nh = counts[1]
     const int64_t nh = counts[1];
     for (int64_t i = (int64_t)blockIdx.x * 4 + wv; i < nh; i += (int64_t)gridDim.x * 4) {
         const int64_t p = hrow[i];
         const int64_t lo = hprow[i], hi = hprow[i + 1];
         double acc = 0.0;
+        uint32_t hc[NB];               // this lane's entries' kept members per band (hits)
+#pragma unroll
+        for (int q = 0; q < NB; ++q) hc[q] = 0;
         // slot ids of a chunk's entries: each chunk loads the next chunk's as soon as its own
         // extent is known, so they are in flight during its member gathers (lanes past the
         // row's end re-read its last entry: an unconditional load, no select waiting on it)
@@ -1238,6 +1248,10 @@ __global__ void __launch_bounds__(256) k_sample_walk2(const int32_t *__restrict_
             const int ntake = __popcll(__ballot(take));     // >= 1: one entry holds <= L <= CAP members
             const int total = (int)__shfl(inc, ntake - 1, 64);
             const uint32_t excl = inc - cnt;
+            if (take) {
+#pragma unroll
+                for (int q = 0; q < NB; ++q) hc[q] += ((kb >> q) & 1u) ? cnt : 0u;
+            }
             // the chunk's entry start positions (taken entries hold >= 1 member each): each
             // taken entry flags its first slot in LDS, a ballot per 64 slots reads them back
             uint64_t sm[M];
@@ -1248,16 +1262,14 @@ __global__ void __launch_bounds__(256) k_sample_walk2(const int32_t *__restrict_
             wave_lds_sync();
 #pragma unroll
             for (int u = 0; u < M; ++u) sm[u] = __ballot(fl[lane + 64 * u] != 0);
+            int before = 0;                 // start positions in the slot words below u
+            const uint64_t upto_lane = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
 #pragma unroll
             for (int u = 0; u < M; ++u) {
                 const int t = lane + 64 * u;
                 // owning entry: start positions at or before t, minus one
-                int j = 0;
-#pragma unroll
-                for (int v = 0; v < M; ++v) {
-                    const uint64_t lm = v < u ? ~0ull : (v == u ? (lane == 63 ? ~0ull : ((2ull << lane) - 1ull)) : 0ull);
-                    j += __popcll(sm[v] & lm);
-                }
+                int j = before + __popcll(sm[u] & upto_lane);
+                before += __popcll(sm[u]);
                 j = t < total ? j - 1 : 0;
                 const uint32_t exj = (uint32_t)__shfl((int)excl, j, 64);
                 const uint32_t nmj = (uint32_t)__shfl((int)cnt, j, 64);
@@ -1311,24 +1323,27 @@ __global__ void __launch_bounds__(256) k_sample_walk2(const int32_t *__restrict_
 #pragma unroll
                     for (int bb = 0; bb < NB; ++bb) {
                         const bool kept = (kbj >> bb) & 1u;
-                        pl[t * 3 * NB + bb] = kept ? wvs[bb] : 0.0;
-                        pl[t * 3 * NB + NB + bb] = kept ? pv[bb] : 0.0;
-                        pl[t * 3 * NB + 2 * NB + bb] = kept ? 1.0 : 0.0;
+                        pl[t * SW + bb] = kept ? wvs[bb] : 0.0;
+                        pl[t * SW + NB + bb] = kept ? pv[bb] : 0.0;
                     }
                 }
             }
             wave_lds_sync();   // the chunk, before other lanes read it
-            if (lane < 3 * NB) {
+            if (lane < 2 * NB) {
 #pragma unroll 8
-                for (int t = 0; t < total; ++t) acc += pl[t * 3 * NB + lane];
+                for (int t = 0; t < total; ++t) acc += pl[t * SW + lane];
             }
             wave_lds_sync();   // read before the next chunk overwrites
             c += ntake;
         }
-        if (lane < 3 * NB) {
-            if (kind == 2) acc += (double)hextra[p * NB + b];
-            (kind == 0 ? h : kind == 1 ? nnum : hits)[p * NB + b] = acc;
+        uint32_t hv = 0;               // lane q < NB: band q's hits over the row
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            const uint32_t tq = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(hc[q]), 63);
+            hv = lane == q ? tq : hv;
         }
+        if (lane < 2 * NB) (kind == 0 ? h : nnum)[p * NB + b] = acc;
+        if (lane < NB) hits[p * NB + lane] = (double)(hv + hextra[p * NB + lane]);
     }
 }
 
@@ -2444,6 +2459,48 @@ __device__ __forceinline__ int32_t relabel_one(int32_t p32, const int32_t *__res
     return p >= 0 ? lut[p] : (int32_t)((int64_t)lut[npix + p] - nt);
 }
 
+// The tiled layout's id of row-major pixel p (destriper.tiled_layout): T x T tiles in
+// row-major tile order (ntx tiles a row), Morton order inside (bits of x at even, of y at
+// odd positions) -- computed, not looked up: the table gathers ran at 1.9 TB/s on the field.
+__device__ __forceinline__ int32_t tiled_id(int32_t p, int32_t nx, int32_t ntx, int tb, double inv)
+{
+    int32_t y = (int32_t)((double)p * inv);
+    int32_t x = p - y * nx;
+    if (x < 0) { --y; x += nx; }
+    else if (x >= nx) { ++y; x -= nx; }
+    const int32_t T = 1 << tb;
+    const uint32_t ix = (uint32_t)(x & (T - 1)), iy = (uint32_t)(y & (T - 1));
+    uint32_t z = 0;
+    for (int b = 0; b < tb; ++b) z |= (((ix >> b) & 1u) << (2 * b)) | (((iy >> b) & 1u) << (2 * b + 1));
+    return (((y >> tb) * ntx + (x >> tb)) << (2 * tb)) + (int32_t)z;
+}
+
+__device__ __forceinline__ int32_t relabel_tiled_one(int32_t p, int32_t npix, int32_t nx, int32_t ntx, int tb,
+                                                     double inv, int32_t nt)
+{
+    if (p >= npix || p < -npix) return nt;
+    return p >= 0 ? tiled_id(p, nx, ntx, tb, inv) : tiled_id(npix + p, nx, ntx, tb, inv) - nt;
+}
+
+__global__ void k_relabel_tiled(const int32_t *__restrict__ pix, int64_t n, int32_t npix, int32_t nx, int32_t ntx,
+                                int tb, int32_t nt, int32_t *__restrict__ out)
+{
+    const double inv = 1.0 / (double)nx;
+    const int64_t n4 = ((uintptr_t)pix % 16 == 0 && (uintptr_t)out % 16 == 0) ? n / 4 : 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    for (int64_t i = t0; i < n4; i += stride) {
+        const int4 v = reinterpret_cast<const int4 *>(pix)[i];
+        int4 r;
+        r.x = relabel_tiled_one(v.x, npix, nx, ntx, tb, inv, nt);
+        r.y = relabel_tiled_one(v.y, npix, nx, ntx, tb, inv, nt);
+        r.z = relabel_tiled_one(v.z, npix, nx, ntx, tb, inv, nt);
+        r.w = relabel_tiled_one(v.w, npix, nx, ntx, tb, inv, nt);
+        reinterpret_cast<int4 *>(out)[i] = r;
+    }
+    for (int64_t i = 4 * n4 + t0; i < n; i += stride) out[i] = relabel_tiled_one(pix[i], npix, nx, ntx, tb, inv, nt);
+}
+
 // four ids per thread (16-B loads and stores; torch's blocks are 256-B aligned), the tail
 // one by one
 __global__ void k_relabel_pixels(const int32_t *__restrict__ pix, int64_t n, const int32_t *__restrict__ lut,
@@ -2466,33 +2523,54 @@ __global__ void k_relabel_pixels(const int32_t *__restrict__ pix, int64_t n, con
 }  // namespace
 
 // key[o] = lut[round(mean y) nx + round(mean x)] over offset o's on-map samples
-// (0 <= p < nx ny, row-major ids), n_internal when it has none.  One wave per offset.
+// (0 <= p < nx ny, row-major ids), n_internal when it has none.  One wave per offset, a lane
+// per sample (coalesced), 32-bit sums reduced across the wave; p = y nx + x by a double
+// reciprocal and one integer fix-up (exact for p < 2^31).  (64-bit divisions and sums took
+// 1.7 ms on the field's 4.38 M offsets, a thread per offset with strided loads as long,
+// profiles/r06/r06c-d.)
 __global__ void __launch_bounds__(256) k_offset_centroid_keys(const int32_t *__restrict__ pix, int64_t NO, int L,
-                                                              int64_t nx, int64_t ny, const int32_t *__restrict__ lut,
-                                                              int64_t n_internal, int32_t *__restrict__ key)
+                                                              int32_t nx, int32_t ny, const int32_t *__restrict__ lut,
+                                                              int32_t n_internal, int32_t *__restrict__ key)
 {
     const int lane = threadIdx.x & 63;
-    const int64_t npix = nx * ny;
+    const double inv = 1.0 / (double)nx;
+    const int32_t npix = nx * ny;
+    // L <= 64 (one sample per lane) and per-offset coordinate sums below 2^16
+    const bool packed = L <= 64 && (int64_t)L * (nx - 1) < 65536 && (int64_t)L * (ny - 1) < 65536;
     for (int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); o < NO; o += (int64_t)gridDim.x * 4) {
-        int64_t sy = 0, sx = 0, c = 0;
+        int32_t sy = 0, sx = 0, c = 0;
         for (int j = lane; j < L; j += 64) {
             const int32_t p = pix[o * L + j];
             if (p >= 0 && p < npix) {
-                sy += p / nx;
-                sx += p % nx;
+                int32_t y = (int32_t)((double)p * inv);
+                int32_t x = p - y * nx;
+                if (x < 0) { --y; x += nx; }
+                else if (x >= nx) { ++y; x -= nx; }
+                sy += y;
+                sx += x;
                 c += 1;
             }
         }
+        if (packed) {
+            // y in the low, x in the high 16 bits (their offset sums fit): one DPP scan, the
+            // count by a ballot -- no LDS permutes
+            const uint32_t t = wave_incl_scan((uint32_t)sy | ((uint32_t)sx << 16));
+            const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)t, 63);
+            sy = (int32_t)(tot & 0xffffu);
+            sx = (int32_t)(tot >> 16);
+            c = __popcll(__ballot(c != 0));
+        } else {
 #pragma unroll
-        for (int sh = 32; sh > 0; sh >>= 1) {
-            sy += __shfl_xor(sy, sh, 64);
-            sx += __shfl_xor(sx, sh, 64);
-            c += __shfl_xor(c, sh, 64);
+            for (int sh = 32; sh > 0; sh >>= 1) {
+                sy += __shfl_xor(sy, sh, 64);
+                sx += __shfl_xor(sx, sh, 64);
+                c += __shfl_xor(c, sh, 64);
+            }
         }
         if (lane == 0) {
-            int32_t k = (int32_t)n_internal;
+            int32_t k = n_internal;
             if (c > 0) {
-                const int64_t yi = (2 * sy + c) / (2 * c), xi = (2 * sx + c) / (2 * c);   // round half up
+                const int32_t yi = (2 * sy + c) / (2 * c), xi = (2 * sx + c) / (2 * c);   // round half up
                 k = lut[yi * nx + xi];
             }
             key[o] = k;
@@ -2509,8 +2587,10 @@ extern "C" int comap_offset_centroid_keys(comap_ctx *ctx, const int32_t *pix, in
     COMAP_DEVICE_GUARD(ctx);
     const int64_t NO = n / L;
     if (NO == 0) return 0;
+    if ((int64_t)L * (nx - 1 + ny - 1) >= (1ll << 30) / 2)     // the per-offset int32 sums
+        return comap_fail(ctx, -1, "comap_offset_centroid_keys: map too large for the offset length");
     k_offset_centroid_keys<<<(unsigned)std::min<int64_t>((NO + 3) / 4, 65536), 256, 0, ctx->stream>>>(
-        pix, NO, L, nx, ny, lut, n_internal, key);
+        pix, NO, L, (int32_t)nx, (int32_t)ny, lut, (int32_t)n_internal, key);
     COMAP_LAUNCH_CHECK(ctx);
     return 0;
 }
@@ -2524,6 +2604,23 @@ extern "C" int comap_relabel_pixels(comap_ctx *ctx, const int32_t *pix, int64_t 
     COMAP_DEVICE_GUARD(ctx);
     if (n == 0) return 0;
     k_relabel_pixels<<<grid_for((n + 3) / 4, 16384), 256, 0, ctx->stream>>>(pix, n, lut, npix, n_internal, out);
+    COMAP_LAUNCH_CHECK(ctx);
+    return 0;
+}
+
+extern "C" int comap_relabel_pixels_tiled(comap_ctx *ctx, const int32_t *pix, int64_t n, int64_t nx, int64_t ny,
+                                          int32_t T, int32_t *out)
+{
+    if (!ctx || (n > 0 && (!pix || !out)) || n < 0 || nx < 1 || ny < 1 || T < 1 || (T & (T - 1)))
+        return -1;
+    int tb = 0;
+    while ((1 << tb) < T) ++tb;
+    const int64_t ntx = (nx + T - 1) / T, nty = (ny + T - 1) / T, nt = ntx * nty * T * T;
+    if (nt >= (1ll << 31)) return -1;
+    COMAP_DEVICE_GUARD(ctx);
+    if (n == 0) return 0;
+    k_relabel_tiled<<<grid_for((n + 3) / 4, 16384), 256, 0, ctx->stream>>>(pix, n, (int32_t)(nx * ny), (int32_t)nx,
+                                                                           (int32_t)ntx, tb, (int32_t)nt, out);
     COMAP_LAUNCH_CHECK(ctx);
     return 0;
 }

@@ -738,8 +738,8 @@ class DeviceDestriper:
         out = torch.empty_like(pix)
         c = N.ctx(dev.index)
         N.bind_stream(c, dev)
-        N.check(N.lib().comap_relabel_pixels(c, N.dptr(pix), pix.numel(), N.dptr(ids), int(npix), int(nt),
-                                             N.dptr(out)), c, 'comap_relabel_pixels')
+        N.check(N.lib().comap_relabel_pixels_tiled(c, N.dptr(pix), pix.numel(), int(nx), int(ny), int(T),
+                                                   N.dptr(out)), c, 'comap_relabel_pixels_tiled')
         if os.environ.get('COMAP_DS_OKEY', 'centroid') == 'centroid' and pix.numel() % L == 0:
             keys = torch.empty(pix.numel() // L, dtype=torch.int32, device=dev)
             N.check(N.lib().comap_offset_centroid_keys(c, N.dptr(pix), pix.numel(), int(L), int(nx), int(ny),

@@ -337,6 +337,11 @@ int comap_destripe_solve(comap_destriper *d, double threshold, int32_t niter, do
  * reads the same pixel of the internal map), n_internal for any other id (the set-up's
  * range check then rejects it, as it would the original).  Device pointers; one pass,
  * no host sync (replaces Destriper.py's row-major m[pointing] indexing order only). */
+/* comap_relabel_pixels for the tiled layout itself (T x T tiles, T a power of two, row-major
+ * tile order, Morton order inside: destriper.tiled_layout), the ids computed instead of
+ * looked up; n_internal = ceil(nx / T) ceil(ny / T) T^2. */
+int comap_relabel_pixels_tiled(comap_ctx *ctx, const int32_t *pix_dev, int64_t n, int64_t nx, int64_t ny, int32_t T,
+                               int32_t *out_dev);
 /* Offset order keys for a row-major nx x ny map: key_dev[o] = lut[round(mean y) nx +
  * round(mean x)] over offset o's samples with 0 <= p < nx ny (the internal id of the
  * offset's centroid pixel), n_internal for an offset with none.  The offsets crossing a

@@ -4,6 +4,8 @@ MI355X (218.9 M samples per band, 4.38 M offsets).  The reference puts every ran
 files into one map (run_destriper.py:131-189, Destriper.py:456-503); here the whole
 field's operator sits in one GPU's HBM, which proves the set-up's index widths at this
 size and anchors the 8-GPU strong-scaling curve (bench.py destriper_c5_field)."""
+import json
+
 import numpy as np
 import pytest
 
@@ -69,6 +71,9 @@ def test_c5_field_64obs_converged_vs_oracle(field_band0):
     f = field_band0
     ref, xr, itr = od.destriper_iteration(f['p'].astype(np.int64), f['t'], f['w'], L, NPIX, threshold=1e-6,
                                           niter=100)
+    print(json.dumps({'field_band0_converged': {'device_iters': f['conv_iters'], 'oracle_iters': itr,
+                                                'map_rel': rel(f['conv_maps']['map'], ref['map']),
+                                                'x_rel': rel(f['conv_x'], xr)}}))
     assert 1 < itr < 100, itr                       # stopped by the threshold
     assert f['conv_iters'] == itr, (f['conv_iters'], itr)
     for k in ('weight', 'hits', 'naive'):

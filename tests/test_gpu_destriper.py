@@ -552,6 +552,27 @@ def test_tiled_layout_equals_row_major(nb, wrap, monkeypatch):
         DeviceDestriper(*args, map_shape=(60, 61), **kw)
 
 
+@pytest.mark.parametrize('ny,nx,T', [(37, 53, 8), (480, 480, 8), (480, 480, 16), (64, 1, 4), (9, 130, 2)])
+def test_relabel_tiled_equals_table(ny, nx, T):
+    """comap_relabel_pixels_tiled (the layout's ids computed per id) == comap_relabel_pixels
+    through tiled_layout's table, for ids in range, negative ids and out-of-range ids."""
+    import torch
+    from comapreduce_amd import _native as N
+    from comapreduce_amd.mapmaking.destriper import tiled_layout
+    npix = ny * nx
+    ids, nt = tiled_layout(ny, nx, T, torch.device('cuda', 0))
+    rng = np.random.default_rng(4)
+    p = rng.integers(-npix - 40, npix + 40, 100_003).astype(np.int32)
+    p[:4] = [0, npix - 1, -1, -npix]
+    pd = torch.from_numpy(p).cuda()
+    a, b = torch.empty_like(pd), torch.empty_like(pd)
+    c = N.ctx(0)
+    N.bind_stream(c, torch.device('cuda', 0))
+    N.check(N.lib().comap_relabel_pixels(c, N.dptr(pd), pd.numel(), N.dptr(ids), npix, nt, N.dptr(a)), c, 'lut')
+    N.check(N.lib().comap_relabel_pixels_tiled(c, N.dptr(pd), pd.numel(), nx, ny, T, N.dptr(b)), c, 'tiled')
+    assert torch.equal(a, b)
+
+
 def test_relabel_pixels_kernel():
     """comap_relabel_pixels (the tiled layout's one-pass relabel) against its numpy
     statement: ids in [0, npix) through the table, ids in [-npix, 0) to the negative id
