@@ -1045,11 +1045,12 @@ __global__ void k_scale(const double *__restrict__ wbar, const double *__restric
 // sample-level maps here -- h = naive numerator = 0, hits = its zero-weight samples' count
 __global__ void k_hit_flags(const int64_t *__restrict__ prow, int64_t npix, int32_t *__restrict__ flag, int nb,
                             const uint32_t *__restrict__ hextra, double *__restrict__ h, double *__restrict__ hits,
-                            double *__restrict__ nnum)
+                            double *__restrict__ nnum, int64_t *__restrict__ counts)
 {
     for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x) {
         const bool hit = prow[p + 1] > prow[p];
         flag[p] = hit ? 1 : 0;
+        if (p == 0) counts[2] = 0;     // k_hit_rows' heavy-row count
         if (h && !hit)
             for (int b = 0; b < nb; ++b) {
                 h[p * nb + b] = 0.0;
@@ -1059,12 +1060,20 @@ __global__ void k_hit_flags(const int64_t *__restrict__ prow, int64_t npix, int3
     }
 }
 
+// heavy != NULL: also the list of the rows with more than heavy_min entries (any order,
+// count in counts[2], which k_hit_flags zeroed) -- the sample walk starts them first
 __global__ void k_hit_rows(const int64_t *__restrict__ prow, const int32_t *__restrict__ flag,
                            const int32_t *__restrict__ pos, int64_t npix, int32_t *__restrict__ hrow,
-                           int64_t *__restrict__ hprow, int64_t *__restrict__ counts)
+                           int64_t *__restrict__ hprow, int64_t *__restrict__ counts, int64_t heavy_min,
+                           int32_t *__restrict__ heavy)
 {
     for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x) {
-        if (flag[p]) { hrow[pos[p]] = (int32_t)p; hprow[pos[p]] = prow[p]; }
+        if (flag[p]) {
+            hrow[pos[p]] = (int32_t)p;
+            hprow[pos[p]] = prow[p];
+            if (heavy && prow[p + 1] - prow[p] > heavy_min)
+                heavy[atomicAdd(reinterpret_cast<unsigned long long *>(counts + 2), 1ull)] = pos[p];
+        }
         if (p == npix - 1) {
             const int64_t nh = (int64_t)pos[p] + flag[p];
             hprow[nh] = prow[npix];
@@ -1175,7 +1184,31 @@ __device__ __forceinline__ int select_bit(uint64_t x, int r)
 // The hits per band are integer counts (each kept member adds 1): they are summed as
 // integers per entry instead of a third LDS column -- the same bits (exact below 2^53), a
 // third less LDS per slot and 2 NB serial chains instead of 3 NB.
-template <int NB, int K, int M>
+// entries above which a row is walked first (COMAP_DS_HEAVY, 0 = row order only)
+int64_t heavy_env()
+{
+    const char *e = getenv("COMAP_DS_HEAVY");
+    return e ? (int64_t)atoll(e) : (int64_t)1024;
+}
+
+// the walk's rows dealt to the XCDs in contiguous ranges (COMAP_DS_WXCD=1; default 0:
+// field set-up walk 8.23 vs 7.86 ms, r06l)
+int walk_xcd_env()
+{
+    const char *e = getenv("COMAP_DS_WXCD");
+    return e ? atoi(e) : 0;
+}
+
+// the walk's record prefetch one chunk ahead (COMAP_DS_WPF, default 1; field walk 7.23 vs
+// 7.83 ms, C5 1.17 vs 1.20 ms, r06m.  Its 73 VGPRs give 6 waves per SIMD; capped for 7:
+// 7.28 ms, for 8: 9.05 ms with spills, r06n)
+int walk_pf_env()
+{
+    const char *e = getenv("COMAP_DS_WPF");
+    return e ? atoi(e) : 1;
+}
+
+template <int NB, int K, int M, bool PF>
 __global__ void __launch_bounds__(256) k_sample_walk2(const int32_t *__restrict__ hrow,
                                                       const int64_t *__restrict__ hprow,
                                                       const int64_t *__restrict__ counts,
@@ -1188,7 +1221,8 @@ __global__ void __launch_bounds__(256) k_sample_walk2(const int32_t *__restrict_
                                                       const uint8_t *__restrict__ kint,
                                                       const uint32_t *__restrict__ hextra, double *__restrict__ h,
                                                       double *__restrict__ hits, double *__restrict__ nnum,
-                                                      int32_t *__restrict__ poff, uint8_t *__restrict__ pcnt)
+                                                      int32_t *__restrict__ poff, uint8_t *__restrict__ pcnt,
+                                                      const int32_t *__restrict__ heavy, int64_t heavy_min, int xcd)
 {
 #pragma clang fp contract(off)
     constexpr int CAP = 64 * M;
@@ -1205,33 +1239,76 @@ __global__ void __launch_bounds__(256) k_sample_walk2(const int32_t *__restrict_
     uint8_t *fl = sfl[wv];
     const int kind = lane / NB, b = lane % NB;     // this lane's ordered sum (lanes < 2 NB)
     // the non-empty rows only (k_hit_flags wrote the empty ones): row i of nh = counts[1]
-    const int64_t nh = counts[1];
-    for (int64_t i = (int64_t)blockIdx.x * 4 + wv; i < nh; i += (int64_t)gridDim.x * 4) {
-        const int64_t p = hrow[i];
+    // Each wave walks its heavy rows first (the long walks start at once, dealt round-robin
+    // over the XCDs), then its rows of the row list.  xcd: the row list in 8 contiguous
+    // ranges, one per XCD (block b runs on XCD b % 8), so an XCD's concurrent waves walk
+    // neighbouring pixels, whose entries share offsets -- their sample lines -- in its L2.
+    const int64_t nh = counts[1], nhv = heavy ? counts[2] : 0;
+    const int64_t W = (int64_t)gridDim.x * 4, w0 = (int64_t)blockIdx.x * 4 + wv;
+    int64_t p0 = w0;
+    if (xcd) {
+        const int64_t x = blockIdx.x & 7, q = gridDim.x >> 3, r = gridDim.x & 7;
+        p0 = (x * q + (x < r ? x : r) + (blockIdx.x >> 3)) * 4 + wv;
+    }
+    // virtual rows: heavy v < nhv (this wave's w0, w0 + W, ...), then row v - nhv (p0, p0 + W, ...)
+    auto next = [&](int64_t v) {
+        if (v >= nhv) return v + W;
+        v += W;
+        return v < nhv ? v : nhv + p0;
+    };
+    for (int64_t ii = w0 < nhv ? w0 : nhv + p0; ii < nh + nhv; ii = next(ii)) {
+        const int64_t i = ii < nhv ? (int64_t)heavy[ii] : ii - nhv;
         const int64_t lo = hprow[i], hi = hprow[i + 1];
+        if (ii >= nhv && heavy && hi - lo > heavy_min) continue;     // walked from the heavy list
+        const int64_t p = hrow[i];
         double acc = 0.0;
         uint32_t hc[NB];               // this lane's entries' kept members per band (hits)
 #pragma unroll
         for (int q = 0; q < NB; ++q) hc[q] = 0;
         // slot ids of a chunk's entries: each chunk loads the next chunk's as soon as its own
-        // extent is known, so they are in flight during its member gathers (lanes past the
-        // row's end re-read its last entry: an unconditional load, no select waiting on it)
-        int64_t si_n = sval[lo + lane < hi ? lo + lane : hi - 1];
+        // extent is known (lanes past the row's end re-read its last entry: an unconditional
+        // load, no select waiting on it).  PF: the next chunk's records (member masks, counts,
+        // keep bits) are gathered too, once those ids are in, while this chunk's member
+        // gathers are in flight -- one dependent memory round trip per chunk instead of two
+        // (every gather below is unconditional -- lanes past the chunk re-read valid entries --
+        // so the compiler's wait for one load never has to drain the later ones: a load under
+        // a branch makes it wait for all of them at the join)
+        constexpr uint32_t kAll = (1u << NB) - 1u;
+        const uint8_t *kip = kint ? kint : reinterpret_cast<const uint8_t *>(sval);
+        int64_t si_c = sval[lo + lane < hi ? lo + lane : hi - 1];
+        // the prefetched record as raw 16-B words (decoded at use: a SlotRec copy made the
+        // compiler move the loaded registers at once, waiting for the load right there)
+        constexpr int NQ = (int)(sizeof(SlotRec<K>) / 16);
+        uint4 rq_n[NQ];
+        uint32_t kb_n = kAll;
+        if constexpr (PF) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) rq_n[q] = reinterpret_cast<const uint4 *>(srec + si_c)[q];
+            kb_n = kip[si_c / L];
+        }
         for (int64_t c = lo; c < hi;) {
             const int64_t e = c + lane;
             const bool live = e < hi;
-            // the entry's slot si = k L + r: its record (member mask, counts) from the count
-            // pass, the offset's weights and keep bits from k -- independent gathers
-            const int64_t si = si_n;
+            // the entry's slot si = k L + r: its record from the count pass, the offset's
+            // weights and keep bits from k
+            const int64_t si = si_c;
             const int64_t kk = si / L;
             SlotRec<K> rc;
             double wb[NB];
-            uint32_t kb = (1u << NB) - 1u;
-            if (live) {
+            uint32_t kb = kAll;
+            if constexpr (PF) {
+                const uint32_t *wd = reinterpret_cast<const uint32_t *>(rq_n);
+                rc.pix = (int32_t)wd[0];
+                rc.cnt = wd[1];
+#pragma unroll
+                for (int q = 0; q < K; ++q) rc.mask[q] = (uint64_t)wd[2 + 2 * q] | ((uint64_t)wd[3 + 2 * q] << 32);
+                kb = kint ? kb_n : kAll;
+            } else if (live) {
                 rc = srec[si];
-                ldb<NB>(wbar + kk * NB, wb);
                 if (kint) kb = kint[kk];
-            } else {
+            }
+            ldb<NB>(wbar + kk * NB, wb);          // used after the member gathers are issued
+            if (!live) {
                 rc.pix = 0;
                 rc.cnt = 0;
 #pragma unroll
@@ -1251,6 +1328,15 @@ __global__ void __launch_bounds__(256) k_sample_walk2(const int32_t *__restrict_
             if (take) {
 #pragma unroll
                 for (int q = 0; q < NB; ++q) hc[q] += ((kb >> q) & 1u) ? cnt : 0u;
+                // the taken entries' pixel-major offset / counts for the CG bin
+                poff[e] = (int32_t)kk;
+                if constexpr (NB == 4) *reinterpret_cast<uint32_t *>(pcnt + e * 4) = rc.cnt;
+                else if constexpr (NB == 2) *reinterpret_cast<uint16_t *>(pcnt + e * 2) = (uint16_t)rc.cnt;
+                else pcnt[e] = (uint8_t)rc.cnt;
+            }
+            {
+                const int64_t en = c + ntake + lane;
+                si_c = sval[en < hi ? en : hi - 1];            // the next chunk's slot ids
             }
             // the chunk's entry start positions (taken entries hold >= 1 member each): each
             // taken entry flags its first slot in LDS, a ballot per 64 slots reads them back
@@ -1262,8 +1348,12 @@ __global__ void __launch_bounds__(256) k_sample_walk2(const int32_t *__restrict_
             wave_lds_sync();
 #pragma unroll
             for (int u = 0; u < M; ++u) sm[u] = __ballot(fl[lane + 64 * u] != 0);
+            // member slots t = lane + 64 u, first the owning entries and the member gathers ...
             int before = 0;                 // start positions in the slot words below u
             const uint64_t upto_lane = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+            int ju[M], bit[M];
+            uint32_t nmu[M], ku[M], kbu[M], gcu[M];
+            double pv[M][NB];
 #pragma unroll
             for (int u = 0; u < M; ++u) {
                 const int t = lane + 64 * u;
@@ -1271,40 +1361,55 @@ __global__ void __launch_bounds__(256) k_sample_walk2(const int32_t *__restrict_
                 int j = before + __popcll(sm[u] & upto_lane);
                 before += __popcll(sm[u]);
                 j = t < total ? j - 1 : 0;
+                ju[u] = j;
                 const uint32_t exj = (uint32_t)__shfl((int)excl, j, 64);
-                const uint32_t nmj = (uint32_t)__shfl((int)cnt, j, 64);
-                const uint32_t kj = (uint32_t)__shfl((int)kk, j, 64);
-                const uint32_t kbj = (uint32_t)__shfl((int)kb, j, 64);
-                const uint32_t gcj = (uint32_t)__shfl((int)rc.cnt, j, 64);
+                nmu[u] = (uint32_t)__shfl((int)cnt, j, 64);
+                ku[u] = (uint32_t)__shfl((int)kk, j, 64);
+                kbu[u] = (uint32_t)__shfl((int)kb, j, 64);
+                gcu[u] = (uint32_t)__shfl((int)rc.cnt, j, 64);
                 uint64_t mj[K];
 #pragma unroll
                 for (int q = 0; q < K; ++q) mj[q] = (uint64_t)__shfl((long long)rc.mask[q], j, 64);
+                int r = t - (int)exj, bitpos = 0;
+#pragma unroll
+                for (int q = 0; q < K; ++q) {
+                    const int cq = __popcll(mj[q]);
+                    if (r >= 0 && r < cq) bitpos = 64 * q + select_bit(mj[q], r);
+                    r -= cq;
+                }
+                bit[u] = bitpos;
+                // (slots past the chunk: entry 0's first member, a valid address)
+                ldb<NB>(ptw + ((int64_t)ku[u] * L + bitpos) * NB, pv[u]);
+            }
+            // a mixed group (some members zero-weight in a band): the sample's own weights
+            double wmix[M][NB];
+#pragma unroll
+            for (int u = 0; u < M; ++u) {
+                const int t = lane + 64 * u;
+                if (t < total && !uniform_counts<NB>(gcu[u], nmu[u])) {
+                    const int64_t on = perm ? (int64_t)perm[ku[u]] : (int64_t)ku[u];
+#pragma unroll
+                    for (int bb = 0; bb < NB; ++bb) {
+                        const uint32_t gc = (gcu[u] >> (8 * bb)) & 255u;
+                        wmix[u][bb] = gc != 0 && gc != nmu[u] ? w[(int64_t)bb * N + on * L + bit[u]] : 0.0;
+                    }
+                }
+            }
+            if constexpr (PF) {
+                // ... then the next chunk's records (waits for its slot ids only) ...
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) rq_n[q] = reinterpret_cast<const uint4 *>(srec + si_c)[q];
+                kb_n = kip[si_c / L];
+            }
+            // ... then the slots' (w, tod w) per band into LDS
+#pragma unroll
+            for (int u = 0; u < M; ++u) {
+                const int t = lane + 64 * u;
                 double wbj[NB];
 #pragma unroll
-                for (int q = 0; q < NB; ++q) wbj[q] = __shfl(wb[q], j, 64);
-                if (u == 0) {
-                    // the taken entries' pixel-major offset / counts for the CG bin, then the
-                    // next chunk's slot ids: issued after the wait for this chunk's records
-                    // and before its member gathers, they retire during those (in-order vmcnt)
-                    if (take) {
-                        poff[e] = (int32_t)kk;
-                        if constexpr (NB == 4) *reinterpret_cast<uint32_t *>(pcnt + e * 4) = rc.cnt;
-                        else if constexpr (NB == 2) *reinterpret_cast<uint16_t *>(pcnt + e * 2) = (uint16_t)rc.cnt;
-                        else pcnt[e] = (uint8_t)rc.cnt;
-                    }
-                    const int64_t en = c + ntake + lane;
-                    si_n = sval[en < hi ? en : hi - 1];
-                }
+                for (int q = 0; q < NB; ++q) wbj[q] = __shfl(wb[q], ju[u], 64);
                 if (t < total) {
-                    int r = t - (int)exj, bitpos = 0;
-#pragma unroll
-                    for (int q = 0; q < K; ++q) {
-                        const int cq = __popcll(mj[q]);
-                        if (r >= 0 && r < cq) bitpos = 64 * q + select_bit(mj[q], r);
-                        r -= cq;
-                    }
-                    double pv[NB];
-                    ldb<NB>(ptw + ((int64_t)kj * L + bitpos) * NB, pv);
+                    const uint32_t gcj = gcu[u], nmj = nmu[u];
                     double wvs[NB];
 #pragma unroll
                     for (int bb = 0; bb < NB; ++bb) {
@@ -1312,19 +1417,17 @@ __global__ void __launch_bounds__(256) k_sample_walk2(const int32_t *__restrict_
                         wvs[bb] = gc == nmj ? wbj[bb] : 0.0;
                     }
                     if (!uniform_counts<NB>(gcj, nmj)) {
-                        // a mixed group (some members zero-weight in a band): the sample's own weight
-                        const int64_t on = perm ? (int64_t)perm[kj] : (int64_t)kj;
 #pragma unroll
                         for (int bb = 0; bb < NB; ++bb) {
                             const uint32_t gc = (gcj >> (8 * bb)) & 255u;
-                            if (gc != 0 && gc != nmj) wvs[bb] = w[(int64_t)bb * N + on * L + bitpos];
+                            if (gc != 0 && gc != nmj) wvs[bb] = wmix[u][bb];
                         }
                     }
 #pragma unroll
                     for (int bb = 0; bb < NB; ++bb) {
-                        const bool kept = (kbj >> bb) & 1u;
+                        const bool kept = (kbu[u] >> bb) & 1u;
                         pl[t * SW + bb] = kept ? wvs[bb] : 0.0;
-                        pl[t * SW + NB + bb] = kept ? pv[bb] : 0.0;
+                        pl[t * SW + NB + bb] = kept ? pv[u][bb] : 0.0;
                     }
                 }
             }
@@ -2206,7 +2309,7 @@ extern "C" int comap_destripe_create_keyed(comap_ctx *ctx, const int32_t *pix, c
     Arena ar;
     ar.cap = Arena::bytes<char>(cub_tb) + Arena::bytes<int64_t>(NO + 1) + 8 * Arena::bytes<int32_t>(N) +
              Arena::bytes<double>((size_t)N * 2 * NB) + Arena::bytes<int64_t>(npix + 1) +
-             2 * Arena::bytes<int32_t>(npix) + Arena::bytes<int64_t>(8) + Arena::bytes<int32_t>(N) +
+             3 * Arena::bytes<int32_t>(npix) + Arena::bytes<int64_t>(8) + Arena::bytes<int32_t>(N) +
              Arena::bytes<int32_t>(1) + 2 * Arena::bytes<uint64_t>(N) + Arena::bytes<int64_t>(NO / 32 + 2) +
              Arena::bytes<uint64_t>((size_t)N * rec_words) +
              Arena::bytes<uint32_t>((size_t)npix * NB) +
@@ -2231,6 +2334,7 @@ extern "C" int comap_destripe_create_keyed(comap_ctx *ctx, const int32_t *pix, c
     double *payload = ar.take<double>((size_t)N * 2 * NB);
     int64_t *srow = ar.take<int64_t>(npix + 1);
     int32_t *hflag = ar.take<int32_t>(npix), *hpos = ar.take<int32_t>(npix);
+    int32_t *hheavy = ar.take<int32_t>(npix);   // the walk's heavy rows (indices into hrow)
     int64_t *counts = ar.take<int64_t>(8);      // [nnzp, nh] (k_hit_rows); first the set-up sizes (k_setup_sizes)
     int32_t *nonuni = ar.take<int32_t>(1);
     uint64_t *epay = ar.take<uint64_t>(N), *epay2 = ar.take<uint64_t>(N);   // count form: offset << 32 | counts
@@ -2411,10 +2515,13 @@ extern "C" int comap_destripe_create_keyed(comap_ctx *ctx, const int32_t *pix, c
     }
     COMAP_LAUNCH_CHECK(ctx);
     k_hit_flags<<<grid_for(npix), 256, 0, st>>>(d->prow, npix, hflag, nb, hextra, walk ? d->h : nullptr, d->hits,
-                                                d->nnum);
+                                                d->nnum, counts);
     COMAP_LAUNCH_CHECK(ctx);
     COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(cub_tmp, scan32_tb, hflag, hpos, (int)npix, st));
-    k_hit_rows<<<grid_for(npix), 256, 0, st>>>(d->prow, hflag, hpos, npix, d->hrow, d->hprow, counts);
+    // the walk's heavy rows: more entries than kHeavyRow (the Lissajous turn-round pixels hold
+    // up to ~100x the mean; walked last they set the kernel's tail)
+    k_hit_rows<<<grid_for(npix), 256, 0, st>>>(d->prow, hflag, hpos, npix, d->hrow, d->hprow, counts,
+                                               heavy_env(), walk && heavy_env() > 0 ? hheavy : nullptr);
     COMAP_LAUNCH_CHECK(ctx);
     // ---- 5. sample-level maps (binValues order)
     const unsigned wgrid = (unsigned)std::min<int64_t>((npix + 3) / 4, 65536);
@@ -2425,9 +2532,11 @@ extern "C" int comap_destripe_create_keyed(comap_ctx *ctx, const int32_t *pix, c
         }
         // member slots per lane and chunk: 64 KW (one entry's members fit a chunk); one wave per
         // row (a fixed 2048-block grid: C5 0.80 -> 1.04 ms)
-#define COMAP_W2(KK, MM) k_sample_walk2<NB, KK, MM><<<wgrid, 256, 0, st>>>(                                   \
+#define COMAP_W2(KK, MM) (walk_pf_env() ? k_sample_walk2<NB, KK, MM, true> \
+                                         : k_sample_walk2<NB, KK, MM, false>)<<<wgrid, 256, 0, st>>>(                                   \
         d->hrow, d->hprow, counts, evn2, (const SlotRec<KK> *)srec, d->perm, d->wbar, w, payload, N, npix, L, NO, kint, \
-        hextra, d->h, d->hits, d->nnum, d->poff, d->pcnt)
+        hextra, d->h, d->hits, d->nnum, d->poff, d->pcnt, heavy_env() > 0 ? hheavy : nullptr, heavy_env(), \
+        walk_xcd_env())
         if (KW == 1) { COMAP_NB_SWITCH(nb, COMAP_W2(1, 1)); }
         else if (KW == 2) { COMAP_NB_SWITCH(nb, COMAP_W2(2, 2)); }
         else { COMAP_NB_SWITCH(nb, COMAP_W2(4, 4)); }

@@ -3,7 +3,7 @@ synthetic problem (bench.destriper_c5_leg's inputs) solved for a fixed number of
 iterations under each COMAP_DS_* setting (read when a problem is created); prints
 one JSON line per (bands, setting) with ms per iteration and the iterate's checksum
 (so a variant that changes the answer beyond rounding shows).
-    python scripts/ds_sweep.py [n_obs] [iters] [bands ...]"""
+    python scripts/ds_sweep.py [n_obs] [iters] [bands ...] [set=layout|heavy]"""
 import json
 import os
 import sys
@@ -11,7 +11,8 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-SETTINGS = [
+SETS = {}
+SETS['layout'] = [
     {},
     {'COMAP_DS_OKEY': 'first'},                  # offsets ordered by their first pixel (rounds 2-5)
     {'COMAP_DS_TILE': '0'},                      # row-major internal pixel order
@@ -19,9 +20,11 @@ SETTINGS = [
     {'COMAP_DS_PB': '1024'},
     {'COMAP_DS_SELL': '0'},
 ]
+SETS['heavy'] = [{'COMAP_DS_HEAVY': v} for v in ('0', '256', '1024', '4096')]   # walk: heavy rows first
+SETS['walk'] = [{}, {'COMAP_DS_WXCD': '0'}, {'COMAP_DS_HEAVY': '0'}, {'COMAP_DS_WXCD': '0', 'COMAP_DS_HEAVY': '0'}]
 # knobs the current kernels read (the removed variants' knobs are gone with them)
 KEYS = ('COMAP_DS_PG', 'COMAP_DS_PU', 'COMAP_DS_PB', 'COMAP_DS_BU', 'COMAP_DS_BL', 'COMAP_DS_SELL', 'COMAP_DS_TILE',
-        'COMAP_DS_OKEY')
+        'COMAP_DS_OKEY', 'COMAP_DS_HEAVY', 'COMAP_DS_WXCD')
 
 
 def main():
@@ -30,11 +33,12 @@ def main():
     from comapreduce_amd.mapmaking import destriper as D
     n_obs = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     iters = int(sys.argv[2]) if len(sys.argv) > 2 else 40
-    bands = [int(b) for b in sys.argv[3:]] or [1, 4]
+    bands = [int(b) for b in sys.argv[3:] if not b.startswith('set=')] or [1, 4]
+    which = ([a[4:] for a in sys.argv[3:] if a.startswith('set=')] or ['layout'])[0]
     torch.cuda.set_device(0)
     for nb in bands:
         pix, tod, w = synthetic.destriper_inputs_device(n_obs, offset_length=50, device=0, seed=1000, n_bands=nb)
-        for st in SETTINGS:
+        for st in SETS[which]:
             for k in KEYS:
                 os.environ.pop(k, None)
             os.environ.update(st)

@@ -622,12 +622,16 @@ def test_solve_to_host_equals_device_maps(nb):
 
 
 @pytest.mark.parametrize('case,Lc,nb', [('walk', 50, 4), ('payload', 50, 4), ('walk', 100, 1), ('walk', 250, 2),
+                                        ('heavy', 50, 4), ('heavy', 100, 2), ('noprefetch', 50, 4), ('xcd', 50, 4),
                                         ('zeros', 50, 4), ('nonfinite', 50, 1), ('nonfinite', 50, 4)])
 def test_sample_maps_set_up_paths(case, Lc, nb, monkeypatch):
     """The set-up's sample-level maps (weight, hits, naive: binValues' sample order, so
     bit-exact) on each of its paths against the oracle: the member-mask walk (default;
     member masks of 1, 2 and 4 words for L = 50, 100, 250), the sorted-sample payload walk
-    (COMAP_DS_WALK=0), kept offsets holding all-zero-weight pixel groups (their hits come
+    (COMAP_DS_WALK=0), the walk with most rows taken from its heavy-row list first
+    (COMAP_DS_HEAVY=2), without the record prefetch (COMAP_DS_WPF=0), with the rows dealt to
+    the XCDs in contiguous ranges (COMAP_DS_WXCD=1), kept offsets holding all-zero-weight pixel
+    groups (their hits come
     from the count pass's integer adds), and non-finite tod on zero-weight samples (the
     set-up falls back to the payload walk, whose NaN reaches the naive map as
     binValues' does; the solve itself is not compared there)."""
@@ -635,6 +639,12 @@ def test_sample_maps_set_up_paths(case, Lc, nb, monkeypatch):
     from comapreduce_amd.mapmaking.destriper import DeviceDestriper
     if case == 'payload':
         monkeypatch.setenv('COMAP_DS_WALK', '0')
+    if case == 'heavy':
+        monkeypatch.setenv('COMAP_DS_HEAVY', '2')
+    if case == 'noprefetch':
+        monkeypatch.setenv('COMAP_DS_WPF', '0')
+    if case == 'xcd':
+        monkeypatch.setenv('COMAP_DS_WXCD', '1')
     p, tods, ws, keep = _bands_problem(max(nb, 2))
     tods, ws, keep = tods[:nb].copy(), ws[:nb].copy(), keep[:nb]
     if Lc != L:                       # whole offsets of the new length, no band drops
