@@ -2687,6 +2687,49 @@ __global__ void __launch_bounds__(256) k_offset_centroid_keys(const int32_t *__r
     }
 }
 
+// The same keys for L <= 64, a block per 128 offsets: the block's 128 L pixel ids are one
+// contiguous run, staged in LDS by coalesced loads (every load of the block in flight at
+// once), then a thread per offset sums its samples from LDS -- one memory round trip per
+// 128 offsets instead of one per offset (the wave-per-offset kernel above: 765 us on the
+// field's 4.38 M offsets, latency-bound at 1.1 TB/s).
+constexpr int kCkOffsets = 128;
+__global__ void __launch_bounds__(256) k_offset_centroid_keys_lds(const int32_t *__restrict__ pix, int64_t NO, int L,
+                                                                  int32_t nx, int32_t ny,
+                                                                  const int32_t *__restrict__ lut, int32_t n_internal,
+                                                                  int32_t *__restrict__ key)
+{
+    __shared__ int32_t sp[kCkOffsets * 64];
+    const int64_t o0 = (int64_t)blockIdx.x * kCkOffsets;
+    const int no = (int)min<int64_t>(kCkOffsets, NO - o0);
+    const int cnt = no * L;
+    const int32_t *src = pix + o0 * L;
+    for (int i = threadIdx.x; i < cnt; i += 256) sp[i] = src[i];
+    __syncthreads();
+    const int t = threadIdx.x;
+    if (t >= no) return;
+    const double inv = 1.0 / (double)nx;
+    const int32_t npix = nx * ny;
+    int32_t sy = 0, sx = 0, c = 0;
+    for (int j = 0; j < L; ++j) {
+        const int32_t p = sp[t * L + j];
+        if (p >= 0 && p < npix) {
+            int32_t y = (int32_t)((double)p * inv);
+            int32_t x = p - y * nx;
+            if (x < 0) { --y; x += nx; }
+            else if (x >= nx) { ++y; x -= nx; }
+            sy += y;
+            sx += x;
+            c += 1;
+        }
+    }
+    int32_t k = n_internal;
+    if (c > 0) {
+        const int32_t yi = (2 * sy + c) / (2 * c), xi = (2 * sx + c) / (2 * c);   // round half up
+        k = lut[yi * nx + xi];
+    }
+    key[o0 + t] = k;
+}
+
 extern "C" int comap_offset_centroid_keys(comap_ctx *ctx, const int32_t *pix, int64_t n, int32_t L, int64_t nx,
                                           int64_t ny, const int32_t *lut, int64_t n_internal, int32_t *key)
 {
@@ -2698,8 +2741,12 @@ extern "C" int comap_offset_centroid_keys(comap_ctx *ctx, const int32_t *pix, in
     if (NO == 0) return 0;
     if ((int64_t)L * (nx - 1 + ny - 1) >= (1ll << 30) / 2)     // the per-offset int32 sums
         return comap_fail(ctx, -1, "comap_offset_centroid_keys: map too large for the offset length");
-    k_offset_centroid_keys<<<(unsigned)std::min<int64_t>((NO + 3) / 4, 65536), 256, 0, ctx->stream>>>(
-        pix, NO, L, (int32_t)nx, (int32_t)ny, lut, (int32_t)n_internal, key);
+    if (L <= 64 && (NO + kCkOffsets - 1) / kCkOffsets < (1ll << 31))
+        k_offset_centroid_keys_lds<<<(unsigned)((NO + kCkOffsets - 1) / kCkOffsets), 256, 0, ctx->stream>>>(
+            pix, NO, L, (int32_t)nx, (int32_t)ny, lut, (int32_t)n_internal, key);
+    else
+        k_offset_centroid_keys<<<(unsigned)std::min<int64_t>((NO + 3) / 4, 65536), 256, 0, ctx->stream>>>(
+            pix, NO, L, (int32_t)nx, (int32_t)ny, lut, (int32_t)n_internal, key);
     COMAP_LAUNCH_CHECK(ctx);
     return 0;
 }

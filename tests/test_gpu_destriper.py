@@ -685,3 +685,37 @@ def test_pixel_out_of_range_raises():
     p[1234] = NPIX
     with pytest.raises(IndexError):
         DeviceDestriper(p, t, w, L, NPIX)
+
+
+@pytest.mark.parametrize('L,nx,ny,n_off', [(50, 480, 480, 1000), (64, 37, 53, 300), (100, 60, 60, 257), (1, 9, 7, 130)])
+def test_offset_centroid_keys_vs_numpy(L, nx, ny, n_off):
+    """comap_offset_centroid_keys (the LDS-staged kernel for L <= 64, the wave-per-offset one
+    above) against NumPy: lut[round(mean y) nx + round(mean x)] over an offset's on-map
+    samples (0 <= p < nx ny; round half up), n_internal for an offset with none."""
+    import torch
+    from comapreduce_amd import _native as N
+    rng = np.random.default_rng(L + nx)
+    npix = nx * ny
+    pix = rng.integers(-3, npix + 3, size=n_off * L).astype(np.int32)
+    pix[:L] = -1                                            # an offset with no on-map sample
+    pix[L:2 * L] = npix - 1
+    lut = rng.permutation(npix).astype(np.int32)
+    n_internal = npix + 5
+    dev = torch.device('cuda', 0)
+    tp, tl = torch.from_numpy(pix).to(dev), torch.from_numpy(lut).to(dev)
+    keys = torch.empty(n_off, dtype=torch.int32, device=dev)
+    c = N.ctx(0)
+    N.bind_stream(c, dev)
+    N.check(N.lib().comap_offset_centroid_keys(c, N.dptr(tp), pix.size, L, nx, ny, N.dptr(tl), n_internal,
+                                               N.dptr(keys)), c, 'comap_offset_centroid_keys')
+    got = keys.cpu().numpy()
+    want = np.full(n_off, n_internal, dtype=np.int64)
+    for o in range(n_off):
+        p = pix[o * L:(o + 1) * L].astype(np.int64)
+        p = p[(p >= 0) & (p < npix)]
+        if p.size:
+            c_ = p.size
+            yi = (2 * (p // nx).sum() + c_) // (2 * c_)
+            xi = (2 * (p % nx).sum() + c_) // (2 * c_)
+            want[o] = lut[yi * nx + xi]
+    assert np.array_equal(got, want)
