@@ -1184,11 +1184,13 @@ __device__ __forceinline__ int select_bit(uint64_t x, int r)
 // The hits per band are integer counts (each kept member adds 1): they are summed as
 // integers per entry instead of a third LDS column -- the same bits (exact below 2^53), a
 // third less LDS per slot and 2 NB serial chains instead of 3 NB.
-// entries above which a row is walked first (COMAP_DS_HEAVY, 0 = row order only)
+// entries above which a row is walked first (COMAP_DS_HEAVY, 0 = row order only).  Field walk
+// (ms, r06w / r06x): 256: 9.00, 512: 8.20, 1024: 7.19, 1536: 6.89, 2048: 6.77-6.89, 3072: 7.00,
+// 4096: 8.85 (15 rows), none: 9.45; C5 (max row 1047 entries) unaffected
 int64_t heavy_env()
 {
     const char *e = getenv("COMAP_DS_HEAVY");
-    return e ? (int64_t)atoll(e) : (int64_t)1024;
+    return e ? (int64_t)atoll(e) : (int64_t)2048;
 }
 
 // the walk's rows dealt to the XCDs in contiguous ranges (COMAP_DS_WXCD=1; default 0:
