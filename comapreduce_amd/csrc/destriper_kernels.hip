@@ -2434,12 +2434,18 @@ extern "C" int comap_destripe_create_keyed(comap_ctx *ctx, const int32_t *pix, c
             return dflt;
         };
         d->bin_lanes = env_int("COMAP_DS_BL", 0, {4, 8, 16, 32, 64});
-        d->bin_u = env_int("COMAP_DS_BU", 4, {4, 8});
+        // long pixel rows (the field: 376 entries per pixel) keep 8 entry loads in flight per
+        // bin lane, and a problem of millions of offsets runs its SELL projection at 8192
+        // blocks (field 4 bands: 1.446 -> 1.380 ms per iteration; C5 1 / 4 bands unchanged,
+        // profiles/r06/r06cg).  Neither changes a result: a bin lane adds its entries in the
+        // same order, and single-rank p.q partials are re-summed in one fixed order.
+        const bool long_rows = d->nnz >= 256 * npix;
+        d->bin_u = env_int("COMAP_DS_BU", long_rows ? 8 : 4, {4, 8});
         d->proj_lanes = env_int("COMAP_DS_PG", 0, {4, 8, 16, 32, 64});
         d->proj_u = env_int("COMAP_DS_PU", 4, {4, 8});
         // the SELL projection runs one chunk per wave at 2048 blocks (1024: 0.254 vs 0.244 ms per
         // 4-band C5 iteration, r04h); its p.q partials fit kPartMax and the dist slots below
-        d->proj_blocks = env_int("COMAP_DS_PB", d->sell ? 2 * kProjBlocks : kProjBlocks,
+        d->proj_blocks = env_int("COMAP_DS_PB", d->sell ? (NO >= (2 << 20) ? 8192 : 2 * kProjBlocks) : kProjBlocks,
                                  {256, 512, 1024, 2048, 4096, 8192});
         d->cg_graph = env_int("COMAP_DS_CGGRAPH", -1, {0, 1});
     }
