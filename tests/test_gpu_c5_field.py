@@ -89,13 +89,15 @@ def test_c5_field_64obs_four_bands_converged(field_band0):
     bit-identical weight / hits / naive maps, its first 3 iterations reproduce the 1-band
     solve and its converged solve takes the 1-band solve's iterations (which the
     converged oracle test pins) with the same map and offsets; maps finite on the hit
-    pixels."""
+    pixels; band 3 equals the oracle's converged solve of its own tod and weights (iteration
+    count, weight / hits / naive bit-exact, map <= 1e-5)."""
     import torch
     from comapreduce_amd import synthetic
     from comapreduce_amd.mapmaking.destriper import DeviceDestriper
     pix, tod, w = synthetic.destriper_inputs_device(NOBS, offset_length=L, device=0, seed=5000, n_bands=4)
     assert tuple(tod.shape) == (4, N_FIELD)
     dd = DeviceDestriper(pix, tod, w, L, NPIX, device=0)
+    t3, w3 = tod[3].cpu().numpy(), w[3].cpu().numpy()      # band 3, for the oracle below
     del pix, tod, w
     r3 = dd.solve(threshold=0.0, niter=3)
     x3 = r3['x'][0].cpu().numpy()
@@ -118,3 +120,13 @@ def test_c5_field_64obs_four_bands_converged(field_band0):
         hit = maps['hits'][b] > 0
         assert maps['hits'][b].sum() == N_FIELD
         assert np.isfinite(maps['map'][b][hit]).all() and np.isfinite(maps['naive'][b][hit]).all()
+    # band 3 (its own offsets and noise) against the oracle's converged solve: the batched
+    # system's per-band stop test gives the reference's iteration count for that band too
+    import oracle.destriper as od
+    ref, xr, itr = od.destriper_iteration(f['p'].astype(np.int64), t3, w3, L, NPIX, threshold=1e-6, niter=100)
+    print(json.dumps({'field_band3_converged': {'device_iters': its[3], 'oracle_iters': itr,
+                                                'map_rel': rel(maps['map'][3], ref['map'])}}))
+    assert its[3] == itr, (its[3], itr)
+    for k in ('weight', 'hits', 'naive'):
+        assert np.array_equal(maps[k][3], ref[k]), k
+    assert rel(maps['map'][3], ref['map']) < 1e-5
