@@ -25,6 +25,7 @@ SETS['cg'] = [{}, {'COMAP_DS_BL': '32'}, {'COMAP_DS_BL': '64'}, {'COMAP_DS_BL': 
              {'COMAP_DS_PB': '4096'}, {'COMAP_DS_PB': '8192'}]
 SETS['cg2'] = [{}, {'COMAP_DS_BU': '8'}, {'COMAP_DS_PB': '8192'}, {'COMAP_DS_BU': '8', 'COMAP_DS_PB': '8192'},
               {'COMAP_DS_BL': '64', 'COMAP_DS_BU': '8', 'COMAP_DS_PB': '8192'}, {}]
+SETS['cg3'] = [{}, {'COMAP_DS_PU': '8'}, {'COMAP_DS_BL': '32'}, {'COMAP_DS_PB': '4096'}, {}]
 SETS['walk'] = [{}, {'COMAP_DS_WXCD': '0'}, {'COMAP_DS_HEAVY': '0'}, {'COMAP_DS_WXCD': '0', 'COMAP_DS_HEAVY': '0'}]
 # knobs the current kernels read (the removed variants' knobs are gone with them)
 KEYS = ('COMAP_DS_PG', 'COMAP_DS_PU', 'COMAP_DS_PB', 'COMAP_DS_BU', 'COMAP_DS_BL', 'COMAP_DS_SELL', 'COMAP_DS_TILE',
