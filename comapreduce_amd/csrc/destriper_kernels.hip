@@ -927,6 +927,15 @@ __global__ void k_setup_sizes(const int64_t *__restrict__ orow, int64_t NO, cons
     }
 }
 
+// nat0[k] = orow_nat[perm[k]]: each internal row's first slot in the caller's-order entry
+// array, gathered once so the compaction's rows need no dependent perm -> orow_nat load
+__global__ void k_nat_base(const int64_t *__restrict__ orow_nat, const int32_t *__restrict__ perm, int64_t NO,
+                           int64_t *__restrict__ nat0)
+{
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < NO; k += (int64_t)gridDim.x * blockDim.x)
+        nat0[k] = orow_nat[perm ? (int64_t)perm[k] : k];
+}
+
 // cnt_nat[perm[k]] = cnt[k]: the offsets' kept-entry counts in the caller's offset order
 __global__ void k_cnt_natural(const int64_t *__restrict__ cnt, const int32_t *__restrict__ perm, int64_t NO,
                               int64_t *__restrict__ cnt_nat)
@@ -950,7 +959,9 @@ __global__ void k_keep_bits(const uint8_t *__restrict__ keep, const int32_t *__r
 
 // Count-form fill for the member-mask walk: row k's kept entries from the count pass's slots
 // into the CSR rows (pixel, packed counts), and the transpose's sort pairs (pixel key, slot
-// k L + r: the entry's walk record) in the caller's offset order (orow_nat), so the stable
+// k L + r: the entry's walk record) in the caller's offset order (row k's first slot there:
+// orow_nat[perm[k]], or orow_nat[k] when perm is NULL -- the set-up passes k_nat_base's
+// gathered bases), so the stable
 // sort by pixel leaves each pixel's entries in sample order -- the order binValues adds
 // them in.  16 lanes per row (rows hold ~30 entries; a wave per row waited on its loads:
 // 0.6 ms at C5).
@@ -2393,6 +2404,8 @@ extern "C" int comap_destripe_create_keyed(comap_ctx *ctx, const int32_t *pix, c
         k_cnt_natural<<<grid_for(NO + 1, 8192), 256, 0, st>>>(cnt, d->perm, NO, cnt_nat);
         COMAP_LAUNCH_CHECK(ctx);
         COMAP_CHECK(ctx, hipcub::DeviceScan::ExclusiveSum(cub_tmp, scan_tb, cnt_nat, orow_nat, (int)(NO + 1), st));
+        k_nat_base<<<grid_for(NO, 8192), 256, 0, st>>>(orow_nat, d->perm, NO, cnt_nat);   // (cnt_nat is free)
+        COMAP_LAUNCH_CHECK(ctx);
     }
     {
         // sliced-ELLPACK projection: default for large problems (C5, 547k offsets: 1 band
@@ -2473,7 +2486,7 @@ extern "C" int comap_destripe_create_keyed(comap_ctx *ctx, const int32_t *pix, c
     int32_t *evn = skey2, *evn2 = sval2;   // walk: the sample-sort arrays are free
     if (walk) {
 #define COMAP_CW(KK) k_ds_compact_walk<NB, KK><<<(unsigned)((NO + 15) / 16), 256, 0, st>>>(                     \
-        d->orow, orow_nat, d->perm, NO, L, npix, (const SlotRec<KK> *)srec, d->opix, d->ocnt, ekey, evn)
+        d->orow, cnt_nat, nullptr, NO, L, npix, (const SlotRec<KK> *)srec, d->opix, d->ocnt, ekey, evn)
         if (KW == 1) { COMAP_NB_SWITCH(nb, COMAP_CW(1)); }
         else if (KW == 2) { COMAP_NB_SWITCH(nb, COMAP_CW(2)); }
         else { COMAP_NB_SWITCH(nb, COMAP_CW(4)); }
