@@ -1707,9 +1707,11 @@ __global__ void __launch_bounds__(256) k_sell_fill_lds(const int64_t *__restrict
                                                        const int64_t *__restrict__ sbase, int64_t NO,
                                                        int32_t *__restrict__ spix, void *__restrict__ sco)
 {
-    using CoefT = typename std::conditional<CF, uint8_t, double>::type;
+    // count form: an entry's NB uint8 counts moved as one NB-byte word (4 byte loads and
+    // stores per entry were most of this kernel's instructions)
+    using PackT = typename std::conditional<NB == 4, uint32_t, typename std::conditional<NB == 2, uint16_t, uint8_t>::type>::type;
     __shared__ int32_t lp[kSellStage];
-    __shared__ CoefT lc[CF ? kSellStage * NB : 1];
+    __shared__ PackT lc[CF ? kSellStage : 1];
     __shared__ int32_t rs[64], rn[64];
     constexpr int cw = 64;
     const int64_t c = blockIdx.x;
@@ -1726,8 +1728,7 @@ __global__ void __launch_bounds__(256) k_sell_fill_lds(const int64_t *__restrict
     if (staged) {
         for (int64_t i = threadIdx.x; i < ne; i += blockDim.x) {
             lp[i] = opix[e0 + i];
-#pragma unroll
-            for (int k = 0; k < NB; ++k) lc[i * NB + k] = reinterpret_cast<const CoefT *>(oco)[(e0 + i) * NB + k];
+            lc[i] = reinterpret_cast<const PackT *>(oco)[e0 + i];
         }
     }
     __syncthreads();
@@ -1738,23 +1739,27 @@ __global__ void __launch_bounds__(256) k_sell_fill_lds(const int64_t *__restrict
         const bool in = j < rn[r];
         const int64_t ei = (int64_t)rs[r] + j;
         int32_t q = kSellPad;
-        CoefT a[NB];
+        if constexpr (CF) {
+            PackT a = 0;
+            if (in) {
+                q = staged ? lp[ei] : opix[e0 + ei];
+                a = staged ? lc[ei] : reinterpret_cast<const PackT *>(oco)[e0 + ei];
+            }
+            spix[b0 + sl] = q;
+            reinterpret_cast<PackT *>(sco)[b0 + sl] = a;
+        } else {
+            double a[NB];
 #pragma unroll
-        for (int k = 0; k < NB; ++k) a[k] = 0;
-        if (in) {
-            if (staged) {
-                q = lp[ei];
-#pragma unroll
-                for (int k = 0; k < NB; ++k) a[k] = lc[ei * NB + k];
-            } else {
+            for (int k = 0; k < NB; ++k) a[k] = 0;
+            if (in) {
                 q = opix[e0 + ei];
 #pragma unroll
-                for (int k = 0; k < NB; ++k) a[k] = reinterpret_cast<const CoefT *>(oco)[(e0 + ei) * NB + k];
+                for (int k = 0; k < NB; ++k) a[k] = reinterpret_cast<const double *>(oco)[(e0 + ei) * NB + k];
             }
-        }
-        spix[b0 + sl] = q;
+            spix[b0 + sl] = q;
 #pragma unroll
-        for (int k = 0; k < NB; ++k) reinterpret_cast<CoefT *>(sco)[(b0 + sl) * NB + k] = a[k];
+            for (int k = 0; k < NB; ++k) reinterpret_cast<double *>(sco)[(b0 + sl) * NB + k] = a[k];
+        }
     }
 }
 
