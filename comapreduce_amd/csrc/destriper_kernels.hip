@@ -422,6 +422,12 @@ __global__ void __launch_bounds__(256) k_offset_keys(const int32_t *__restrict__
     }
 }
 
+__global__ void k_iota32(int32_t *__restrict__ v, int64_t n)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        v[i] = (int32_t)i;
+}
+
 // Member-mask walk: a kept entry's slot record, written by the count pass at slot
 // k L + r (offset k's r-th entry) -- pixel, packed per-band non-zero counts, member mask
 // (sample j of the offset = bit j) -- one 16-B-aligned gather for the sample walk
@@ -2377,8 +2383,11 @@ extern "C" int comap_destripe_create_keyed(comap_ctx *ctx, const int32_t *pix, c
     if (spatial) {
         // the caller's keys (comap_offset_centroid_keys: the centroid's internal pixel), or
         // the first on-map pixel of each offset
-        k_offset_keys<<<(unsigned)std::min<int64_t>((NO + 3) / 4, 65536), 256, 0, st>>>(okey ? nullptr : pix, NO, L,
-                                                                                         npix, ekey, eval);
+        if (okey)     // the sort's values only: a thread per offset
+            k_iota32<<<grid_for(NO, 8192), 256, 0, st>>>(eval, NO);
+        else
+            k_offset_keys<<<(unsigned)std::min<int64_t>((NO + 3) / 4, 65536), 256, 0, st>>>(pix, NO, L, npix, ekey,
+                                                                                             eval);
         COMAP_LAUNCH_CHECK(ctx);
         size_t tb = cub_tb;
         // (the caller's keys may exceed npix -- a compacted problem keeps its tiled-layout
